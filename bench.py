@@ -1,0 +1,180 @@
+#!/usr/bin/env python3
+"""bench.py - frames/s stacked (4096x4096 u16, sigma-clip) + achieved HBM GB/s on MI355X.
+
+BASELINE.json metric, measured on BASELINE.json configs[2] (the configuration the metric
+is quoted on that fits one GPU): sigma-clip rejection stack (SIGMA, sig = (4, 3),
+NO_NORM, registration shifts applied) of 512 synthetic 4096x4096 u16 mono frames,
+frames resident in HBM (generated on the device by include/sg_synth.h).
+
+One step = one sg_stack_u16_device() call over the whole 512-frame sequence.
+Multi-GPU (torchrun, one process per GPU): weak scaling by row bands -- rank r stacks its
+own 4096-row band of a (4096*G) x 4096 sequence of 512 frames; no data-path collective
+(each rank's band is written to its own output); the 6 rejection counters and the step
+times are all-reduced (max for time).
+
+Output: one JSON line on rank 0 (see README / DESIGN.md for the fields).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "siril-0.9_amd", "python"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--frames", type=int, default=512)
+    ap.add_argument("--width", type=int, default=4096)
+    ap.add_argument("--height", type=int, default=4096)
+    ap.add_argument("--rejection", default="sigma")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rows", type=int, default=8, help="rows of the CPU baseline sample")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, N, W):
+    """Oracle (C restatement of the reference stacker, -O2 -fopenmp, the reference's block
+    partition and OpenMP schedule) on a bounded sample of the same workload."""
+    import numpy as np
+    import oracle_lib as orc
+    rows = args.cpu_rows
+    threads = os.cpu_count() or 1
+    threads = min(threads, 256)
+    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    frames = orc.synth(N, 1, rows, W, seed=0x5151, maxshift=0)
+    sx = np.zeros(N, dtype=np.int32)
+    t0 = time.perf_counter()
+    rc, out, rej = orc.stack_rejection(frames, 2, sig=(4.0, 3.0), shiftx=sx, shifty=sx,
+                                       max_thread=threads, max_number_of_rows=rows)
+    dt = time.perf_counter() - t0
+    frac = rows / args.height
+    return {"value": round(N * frac / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{N} frames x {rows} rows x {W} cols (SIGMA 4/3), scaled by {rows}/{args.height}",
+            "seconds": round(dt, 3)}
+
+
+def main():
+    args = parse()
+    import torch
+    import sirilgpu as sg
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+
+    N, W, H = args.frames, args.width, args.height
+    rej_mode = {"sigma": sg.SIGMA, "winsorized": sg.WINSORIZED, "none": sg.NO_REJEC,
+                "percentile": sg.PERCENTILE}[args.rejection]
+    ctx = sg.Context([dev])
+    # this rank's band: rows [rank*H, (rank+1)*H) of a (H*world)-row sequence; the device
+    # buffer holds just the band, addressed through a biased base pointer
+    frames = torch.empty(N * H * W, dtype=torch.int16, device="cuda")
+    out = torch.empty(H * W, dtype=torch.int16, device="cuda")
+    ctx.synth_fill(frames.data_ptr(), N, 1, H, W, 0, H, 0x5151 + rank, 16)
+    import ctypes
+    sx = (ctypes.c_int * N)()
+    sy = (ctypes.c_int * N)()
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "liboracle.so")) if False else None
+    # the synthetic shifts are a pure function; recompute them with the same mixer
+    import numpy as np
+
+    def mix64(z):
+        z = (z + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+        return z ^ (z >> 31)
+
+    seed = 0x5151 + rank
+    shx = np.zeros(N, dtype=np.int32)
+    shy = np.zeros(N, dtype=np.int32)
+    for f in range(1, N):
+        h = mix64(seed ^ 0x51B1 ^ (f << 32))
+        shx[f] = -((h & 0xFFFFFFFF) % 33 - 16)
+        shy[f] = -(((h >> 32) & 0xFFFFFFFF) % 33 - 16)
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=rej_mode, sig=(4.0, 3.0),
+                              shiftx=shx, shifty=shy, max_thread=8, max_number_of_rows=H)
+
+    def step():
+        return ctx.stack_device(desc, frames.data_ptr(), H * W, H * W, out.data_ptr(), 0, H)
+
+    for _ in range(args.warmup):
+        step()
+    kms, slow = [], 0
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rej_tot = None
+    for _ in range(args.steps):
+        rej, _ = step()
+        st = ctx.stats()
+        kms.append(st.kernel_ms)
+        slow = st.slow_pixels
+        rej_tot = rej
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        r = torch.tensor(rej_tot.astype(np.int64).reshape(-1), device="cuda")
+        dist.all_reduce(r)
+    ms_step = elapsed / args.steps * 1e3
+    frames_per_s = N * world / (elapsed / args.steps)
+    kavg = sum(kms) / len(kms)
+    algo_bytes = N * H * W * 2 + H * W * 2
+    achieved = algo_bytes / (kavg * 1e-3) / 1e9
+    if rank == 0:
+        res = {
+            "metric": "frames/sec stacked (4096x4096 u16, sigma-clip) + achieved HBM GB/s",
+            "value": round(frames_per_s, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u16",
+            "data": "synthetic (include/sg_synth.h, generated in HBM)",
+            "config": {"workload": f"sigma-clip stack {N}x{H}x{W} u16 mono per GPU (BASELINE configs[2])",
+                       "frames": N, "height": H, "width": W, "rejection": args.rejection,
+                       "sig": [4.0, 3.0], "parallelism": f"row-band x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None},
+            "kernel_ms": round(kavg, 3),
+            "slow_pixels": int(slow),
+            "rejected": [int(x) for x in rej_tot.reshape(-1)[:2]],
+        }
+        if not args.no_cpu_baseline and world == 1:
+            res["cpu_baseline"] = cpu_baseline(args, N, W)
+        print(json.dumps(res), flush=True)
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

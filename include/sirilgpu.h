@@ -1,0 +1,143 @@
+/*
+ * sirilgpu.h - C ABI of libsirilgpu.so, the MI355X (gfx950) implementation of Siril 0.9's
+ * sequence registration + stacking hot path.
+ *
+ * Plain C types only (no torch, no HIP types in signatures).  Each entry point cites the
+ * reference interface whose body it replaces; the reference-side glue is shown in
+ * INTEGRATION.md.
+ *
+ * Conventions:
+ *   - WORD = uint16_t (src/core/siril.h:44).
+ *   - Images are planar per channel and bottom-up ("memory order", src/core/siril.h:391-442).
+ *   - A region read through sg_read_region_fn is a top-down band, exactly what
+ *     seq_opened_read_region() returns (src/io/sequence.c:690-700).
+ *   - Return codes mirror the reference: 0 ok, -1 generic/cancel/unsupported, -2 size or
+ *     allocation error, -3 read failure (src/stacking/stacking.c:244-246,1212-1220).
+ */
+#ifndef SIRILGPU_H
+#define SIRILGPU_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SG_OK 0
+#define SG_ERR_GENERIC -1
+#define SG_ERR_SIZE -2
+#define SG_ERR_READ -3
+#define SG_ERR_DEVICE -10
+
+/* stacking_methods[] order, src/stacking/stacking.c:54-56 */
+enum sg_stack_method {
+	SG_STACK_SUM = 0,	/* stack_summing            :196-355  */
+	SG_STACK_MEAN = 1,	/* stack_mean_with_rejection :1189-1858 */
+	SG_STACK_MEDIAN = 2,	/* stack_median             :362-816  */
+	SG_STACK_MAX = 3,	/* stack_addmax             :824-972  */
+	SG_STACK_MIN = 4	/* stack_addmin             :979-1128 */
+};
+
+/* src/stacking/stacking.h:14-21 */
+enum sg_rejection { SG_NO_REJEC, SG_PERCENTILE, SG_SIGMA, SG_SIGMEDIAN, SG_WINSORIZED, SG_LINEARFIT };
+/* src/stacking/stacking.h:24-30 */
+enum sg_normalization { SG_NO_NORM, SG_ADDITIVE, SG_MULTIPLICATIVE, SG_ADDITIVE_SCALING,
+	SG_MULTIPLICATIVE_SCALING };
+
+/* rectangle, src/core/siril.h:477-479 */
+typedef struct { int x, y, w, h; } sg_rect;
+
+/* shape of seq_opened_read_region (src/io/sequence.h:17): fill `buffer` with the top-down
+ * band `area` of channel `layer` of frame `index`; <0 on failure */
+typedef int (*sg_read_region_fn)(void *user, int layer, int index, uint16_t *buffer,
+		const sg_rect *area);
+/* get_thread_run() (src/core/processing.c:294-300): 0 = cancel requested */
+typedef int (*sg_should_continue_fn)(void *user);
+
+/* What a stack_method needs from struct stacking_args + sequence (src/stacking/stacking.h:38-56,
+ * src/core/siril.h:328-374), flattened to plain arrays.  Per-frame arrays are indexed by the
+ * stacked-frame position i (the reference's image_indices[i] order). */
+typedef struct {
+	int method;		/* enum sg_stack_method */
+	int rejection;		/* enum sg_rejection (SG_STACK_MEAN only) */
+	int normalize;		/* enum sg_normalization (MEAN and MEDIAN) */
+	double sig[2];		/* args->sig */
+	int nb_frames;		/* args->nb_images_to_stack */
+	int width, height, nb_layers;	/* seq->rx, seq->ry, naxes[2] */
+	const int *shiftx;	/* regparam[reglayer][image_indices[i]].shiftx, or NULL */
+	const int *shifty;	/* ... .shifty, or NULL (no registration data) */
+	const double *offset;	/* normalisation coefficients (compute_normalization), or NULL */
+	const double *mul;
+	const double *scale;
+	int max_thread;		/* com.max_thread: the reference's OpenMP team size */
+	int max_number_of_rows;	/* args->max_number_of_rows */
+	int reserved[6];
+} sg_stack_desc;
+
+typedef struct sg_ctx sg_ctx;
+
+/* Open the devices this context drives (ndev = 0: device 0).  One HIP stream per device. */
+int sg_init(sg_ctx **ctx, int ndev, const int *devs);
+void sg_shutdown(sg_ctx *ctx);
+const char *sg_last_error(const sg_ctx *ctx);
+
+/*
+ * Host-pull stack: replaces the bodies of stack_summing / stack_mean_with_rejection /
+ * stack_median / stack_addmax / stack_addmin (src/stacking/stacking.c:196,1189,362,824,979).
+ * Pixels are pulled through `pull` (seq_opened_read_region shape) into pinned staging and
+ * uploaded to HBM; the result is written bottom-up into `out` (nb_layers*H*W WORDs, the
+ * buffer the reference hands to gfit.data).  rej receives the per-channel low/high rejection
+ * counters of :1796-1817 (MEAN only), maxim the sum maximum of :311-313 (SUM only).
+ */
+int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *desc, sg_read_region_fn pull, void *user,
+		sg_should_continue_fn cont, void *cont_user, uint16_t *out, uint64_t rej[3][2],
+		uint64_t *maxim);
+
+/*
+ * Device-resident stack (frames already in HBM).  d_frames holds frame i, channel c, memory
+ * row r, column x at d_frames[i*frame_stride + c*plane_stride + r*width + x]; only rows
+ * [row_begin - 32768.., row_end + ..) reachable through the shifts are read, so a rank that
+ * owns a row band may pass a base pointer biased by -band_first_row*width.  Output rows
+ * [row_begin, row_end) (memory order) of every channel are written to d_out (same indexing
+ * as a [C][H][W] image).  `stream` is a hipStream_t (NULL = the context's stream of device
+ * `dev_index`).  Synchronous unless async != 0.
+ */
+int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_desc *desc,
+		const uint16_t *d_frames, int64_t frame_stride, int64_t plane_stride,
+		uint16_t *d_out, int row_begin, int row_end, uint64_t rej[3][2], uint64_t *maxim,
+		void *stream);
+
+/* Statistics of the last stack call on this context (for bench.py / rocprof cross-checks). */
+typedef struct {
+	double kernel_ms;	/* HIP-event time of the main stacking kernel(s) on their stream */
+	double total_ms;	/* HIP-event time of the whole device-side stack call */
+	uint64_t slow_pixels;	/* pixels re-done by the literal (fp80) path */
+	uint64_t chain_pixels;	/* pixels needing the cross-pixel stale-state replay */
+	uint64_t launches;	/* kernels launched by the main path */
+	int main_kernel_blocks;
+	int reserved;
+} sg_stack_stats;
+int sg_get_last_stats(const sg_ctx *ctx, sg_stack_stats *st);
+
+/*
+ * DFT registration: replaces register_shift_dft (src/registration/registration.c:182-400).
+ * d_sel / sel hold nframes bottom-up S x S selections (what seq_read_frame_part returns,
+ * src/io/sequence.c:567-609).  included may be NULL (process_all_frames).  Outputs the
+ * integer shifts and the normalised quality (normalizeQualityData :163-176) per frame.
+ */
+int sg_register_dft_u16(sg_ctx *ctx, const uint16_t *sel, int nframes, int S, int ref_image,
+		const int *included, int *shiftx, int *shifty, double *quality);
+int sg_register_dft_u16_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int nframes,
+		int S, int ref_image, const int *included, int *shiftx, int *shifty,
+		double *quality, void *stream);
+
+/* Synthetic sequence generator of include/sg_synth.h on the device (bench / tests). */
+int sg_synth_fill_device(sg_ctx *ctx, int dev_index, uint16_t *d_frames, int nframes,
+		int nb_layers, int height, int width, int row_begin, int row_end, uint64_t seed,
+		int maxshift, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SIRILGPU_H */

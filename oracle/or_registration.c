@@ -1,0 +1,315 @@
+/*
+ * or_registration.c - CPU restatement of Siril 0.9 DFT registration and the planetary
+ * quality estimate (TEST INFRASTRUCTURE ONLY; parity unpinned, see oracle.h).
+ *
+ *   register_shift_dft      src/registration/registration.c:182-400
+ *   normalizeQualityData    src/registration/registration.c:163-176
+ *   QualityEstimate         src/algos/quality.c:46-218
+ *   SubSample / Gradient / _smooth_image_16   src/algos/quality.c:223-349
+ *
+ * FFTW3 (third-party, version unpinned, configure.ac:65) is replaced by a plain
+ * double-precision DFT with FFTW's conventions: unnormalised, FFTW_FORWARD = e^{-i},
+ * FFTW_BACKWARD = e^{+i}, row-major 2-D.  Only the arg-max of the correlation survives
+ * into the result, so any accurate DFT gives the same shifts except at near ties.
+ */
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+#include <float.h>
+#include <stdint.h>
+#include "oracle.h"
+
+/* in-place 1-D complex DFT of length n with stride 1 (radix-2 if n is a power of two,
+ * otherwise direct O(n^2) summation in double) */
+static void dft1d(double *re, double *im, int n, int sign, double *wre, double *wim) {
+	if ((n & (n - 1)) == 0) {
+		/* bit reversal */
+		for (int i = 1, j = 0; i < n; i++) {
+			int bit = n >> 1;
+			for (; j & bit; bit >>= 1)
+				j ^= bit;
+			j ^= bit;
+			if (i < j) {
+				double t = re[i]; re[i] = re[j]; re[j] = t;
+				t = im[i]; im[i] = im[j]; im[j] = t;
+			}
+		}
+		for (int len = 2; len <= n; len <<= 1) {
+			double ang = sign * 2.0 * M_PI / len;
+			for (int k = 0; k < len / 2; k++) {
+				wre[k] = cos(ang * k);
+				wim[k] = sin(ang * k);
+			}
+			for (int i = 0; i < n; i += len) {
+				for (int k = 0; k < len / 2; k++) {
+					double ur = re[i + k], ui = im[i + k];
+					double xr = re[i + k + len / 2], xi = im[i + k + len / 2];
+					double vr = xr * wre[k] - xi * wim[k];
+					double vi = xr * wim[k] + xi * wre[k];
+					re[i + k] = ur + vr;
+					im[i + k] = ui + vi;
+					re[i + k + len / 2] = ur - vr;
+					im[i + k + len / 2] = ui - vi;
+				}
+			}
+		}
+	} else {
+		double *tr = malloc(n * sizeof(double)), *ti = malloc(n * sizeof(double));
+		for (int k = 0; k < n; k++) {
+			double sr = 0, si = 0;
+			for (int t = 0; t < n; t++) {
+				double a = sign * 2.0 * M_PI * (double)(((long)k * t) % n) / n;
+				sr += re[t] * cos(a) - im[t] * sin(a);
+				si += re[t] * sin(a) + im[t] * cos(a);
+			}
+			tr[k] = sr;
+			ti[k] = si;
+		}
+		memcpy(re, tr, n * sizeof(double));
+		memcpy(im, ti, n * sizeof(double));
+		free(tr);
+		free(ti);
+	}
+}
+
+void or_dft2d(double *re, double *im, int S, int sign) {
+	double *wre = malloc(S * sizeof(double)), *wim = malloc(S * sizeof(double));
+	double *cr = malloc(S * sizeof(double)), *ci = malloc(S * sizeof(double));
+	for (int y = 0; y < S; y++)
+		dft1d(re + (size_t)y * S, im + (size_t)y * S, S, sign, wre, wim);
+	for (int x = 0; x < S; x++) {
+		for (int y = 0; y < S; y++) {
+			cr[y] = re[(size_t)y * S + x];
+			ci[y] = im[(size_t)y * S + x];
+		}
+		dft1d(cr, ci, S, sign, wre, wim);
+		for (int y = 0; y < S; y++) {
+			re[(size_t)y * S + x] = cr[y];
+			im[(size_t)y * S + x] = ci[y];
+		}
+	}
+	free(wre); free(wim); free(cr); free(ci);
+}
+
+/* quality.h constants */
+#define MAXP 6
+#define QMARGIN 0.1
+#define QSUBSAMPLE_INC 1
+#define QSUBSAMPLE_MAX 5
+#define QSUBSAMPLE_MIN 3
+#define THRESHOLD 40
+
+static int32_t SubSample(const uint16_t *ptr, int img_wid, int x_size, int y_size) {
+	int x, y, val = 0;
+	for (y = 0; y < y_size; ++y) {
+		for (x = 0; x < x_size; x++)
+			val += ptr[x];
+		ptr += img_wid;
+	}
+	return val / (x_size * y_size);
+}
+
+static uint16_t *smooth_image_16(const uint16_t *buf, int width, int height) {
+	uint16_t *new_buff = calloc((size_t)width * height * 2, sizeof(uint16_t));
+	for (int y = 1; y < height - 1; ++y) {
+		int o = y * width + 1;
+		for (int x = 1; x < width - 1; ++x, ++o) {
+			unsigned int v = buf[o];
+			v += buf[o - width - 1];
+			v += buf[o - width];
+			v += buf[o - width + 1];
+			v += buf[o - 1];
+			v += buf[o + 1];
+			v += buf[o + width - 1];
+			v += buf[o + width];
+			v += buf[o + width + 1];
+			new_buff[o] = v / 9;
+		}
+	}
+	return new_buff;
+}
+
+static double Gradient(const uint16_t *buf, int width, int height) {
+	int pixels, x, y;
+	int yborder = (int)((double)height * QMARGIN) + 1;
+	int xborder = (int)((double)width * QMARGIN) + 1;
+	double d1, d2, val, avg = 0;
+	int threshhold = (THRESHOLD) << 8;
+	unsigned char *map = calloc((size_t)width * height, 1);
+	pixels = 0;
+	for (y = yborder; y < height - yborder; ++y) {
+		int o = y * width + xborder;
+		for (x = xborder; x < width - xborder; ++x, ++o) {
+			if (buf[o] >= threshhold) {
+				map[o - width - 1] = map[o - width] = map[o - width + 1] = 1;
+				map[o - 1] = map[o] = map[o + 1] = 1;
+				map[o + width - 1] = map[o + width] = map[o + width + 1] = 1;
+				++pixels;
+				avg += buf[o];
+			}
+		}
+	}
+	if (!pixels) {
+		val = -1.0;
+		goto end;
+	}
+	val = 0;
+	pixels = 0;
+	for (y = yborder; y < height - yborder; ++y) {
+		int o = y * width + xborder;
+		for (x = xborder; x < width - xborder; ++x, ++o)
+			if (map[o]) {
+				d1 = buf[o];
+				d2 = buf[o];
+				d1 = d1 - (int)(buf[o + 1]);
+				d2 = d2 - (int)(buf[o + width]);
+				val += (d1 * d1 + d2 * d2);
+				pixels++;
+			}
+	}
+	val = val / (double)pixels;
+	val = val / 10;
+end:
+	free(map);
+	return val;
+}
+
+double or_quality_estimate(const uint16_t *buffer, int width, int height) {
+	int region_w = width - 1, region_h = height - 1;
+	int x1 = 0, y1 = 0;
+	int subsample, i, j, n, x, y, max, maxp[MAXP], x_inc, x_samples, y_samples, y_last;
+	double mult, q, dval = 0.0;
+	uint16_t *buf = calloc((size_t)region_w * region_h + 1, sizeof(uint16_t));
+	subsample = QSUBSAMPLE_MIN;
+	while (subsample <= QSUBSAMPLE_MAX) {
+		const uint16_t *ptr;
+		x_samples = region_w / subsample;
+		y_samples = region_h / subsample;
+		if (x_samples < 2 || y_samples < 2)
+			break;
+		y_last = y1 + (y_samples - 1) * subsample;
+		x_inc = subsample;
+		for (i = 0; i < MAXP; ++i)
+			maxp[i] = 0;
+		y = y1;
+		n = 0;
+		ptr = buffer + (y * width + x1);
+		for (x = 0; x < x_samples; ++x, ptr += x_inc)
+			buf[n++] = SubSample(ptr, width, subsample, subsample);
+		for (y += subsample; y < y_last; y += subsample) {
+			ptr = buffer + (y * width + x1);
+			for (x = 0; x < x_samples; ++x, ptr += x_inc) {
+				int v = SubSample(ptr, width, subsample, subsample);
+				if (v > maxp[2] && v < 65530) {
+					int slot;
+					if (v > maxp[0])
+						slot = 0;
+					else if (v > maxp[1])
+						slot = 1;
+					else
+						slot = 2;
+					for (j = MAXP - 1; j > slot; --j) {
+						maxp[j] = maxp[j - 1];
+						maxp[j] = v;
+					}
+				}
+				buf[n++] = v;
+			}
+		}
+		ptr = buffer + (y * width + x1);
+		for (x = 0; x < x_samples; ++x, ptr += x_inc)
+			buf[n++] = SubSample(ptr, width, subsample, subsample);
+		j = MAXP / 2;
+		for (i = j, max = 0; i < MAXP; ++i)
+			max += maxp[i];
+		max /= (MAXP - j);
+		if (max > 0) {
+			mult = (double)60000 / (double)max;
+			for (i = 0; i < n; ++i) {
+				unsigned int v = buf[i];
+				v = (unsigned int)((double)v * mult);
+				if (v > 65535)
+					v = 65535;
+				buf[i] = v;
+			}
+		}
+		uint16_t *new_image = smooth_image_16(buf, x_samples, y_samples);
+		q = Gradient(new_image, x_samples, y_samples);
+		free(new_image);
+		dval += (q * ((QSUBSAMPLE_MIN * QSUBSAMPLE_MIN) / (subsample * subsample)));
+		do {
+			subsample += QSUBSAMPLE_INC;
+		} while (width / subsample == x_samples && height / subsample == y_samples);
+	}
+	dval = sqrt(dval);
+	free(buf);
+	return dval;
+}
+
+int or_register_shift_dft(const uint16_t *sel, int nframes, int S, int ref_image,
+		const int *included, int *shiftx, int *shifty, double *quality) {
+	size_t sq = (size_t)S * S;
+	double *inr = malloc(sq * sizeof(double)), *ini = malloc(sq * sizeof(double));
+	double *ar = malloc(sq * sizeof(double)), *ai = malloc(sq * sizeof(double));
+	double q_max, q_min;
+	if (ref_image < 0)
+		ref_image = 0;
+	const uint16_t *refsel = sel + (size_t)ref_image * sq;
+	for (size_t j = 0; j < sq; j++) {
+		inr[j] = (double)refsel[j];
+		ini[j] = 0.0;
+	}
+	quality[ref_image] = or_quality_estimate(refsel, S, S);
+	or_dft2d(inr, ini, S, -1);
+	shiftx[ref_image] = 0;
+	shifty[ref_image] = 0;
+	q_min = q_max = quality[ref_image];
+	for (int frame = 0; frame < nframes; ++frame) {
+		if (frame == ref_image)
+			continue;
+		if (included && !included[frame])
+			continue;
+		const uint16_t *img = sel + (size_t)frame * sq;
+		for (size_t x = 0; x < sq; x++) {
+			ar[x] = (double)img[x];
+			ai[x] = 0.0;
+		}
+		quality[frame] = or_quality_estimate(img, S, S);
+		{
+			double qual = quality[frame];
+			if (qual > q_max)
+				q_max = qual;
+			q_min = (q_min < qual) ? q_min : qual;	/* siril.h:30-33 min() */
+		}
+		or_dft2d(ar, ai, S, -1);
+		/* convol2 = in * conj(out2) */
+		for (size_t x = 0; x < sq; x++) {
+			double br = ar[x], bi = -ai[x];
+			double cr = inr[x] * br - ini[x] * bi;
+			double ci = inr[x] * bi + ini[x] * br;
+			ar[x] = cr;
+			ai[x] = ci;
+		}
+		or_dft2d(ar, ai, S, +1);
+		size_t shift = 0;
+		for (size_t x = 1; x < sq; ++x)
+			if (ar[x] > ar[shift])
+				shift = x;
+		int sy = (int)(shift / S), sx = (int)(shift % S);
+		if (sy > S / 2)
+			sy -= S;
+		if (sx > S / 2)
+			sx -= S;
+		shiftx[frame] = sx;
+		shifty[frame] = sy;
+	}
+	/* normalizeQualityData */
+	for (int frame = 0; frame < nframes; ++frame) {
+		if (included && !included[frame])
+			continue;
+		quality[frame] -= q_min;
+		quality[frame] /= (q_max - q_min);
+	}
+	free(inr); free(ini); free(ar); free(ai);
+	return 0;
+}

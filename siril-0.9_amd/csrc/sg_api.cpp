@@ -1,0 +1,495 @@
+/*
+ * sg_api.cpp - C ABI of libsirilgpu.so (include/sirilgpu.h): contexts, HBM workspaces,
+ * kernel selection and the host-pull stacking path.
+ *
+ * Everything here is plumbing around the gfx950 kernels of sg_stack.hip / sg_register.hip;
+ * no pixel is ever computed on the host.  If a launch fails the call fails loudly
+ * (SG_ERR_DEVICE + sg_last_error), there is no CPU fallback.
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+#include <vector>
+#include <string>
+#include <algorithm>
+#include "sg_common.hpp"
+#include "../../include/sirilgpu.h"
+
+struct SgChainTables {
+	const int *blk_of_row;
+	const int *blk_channel, *blk_start, *blk_end, *blk_first;
+	int nblocks;
+};
+
+template <int NREG> __global__ void k_stack_sorted(SgStackParams p);
+__global__ void k_stack_reduce(SgStackParams p);
+__global__ void k_sum_finalize(SgStackParams p);
+__global__ void k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *scratch, int phase);
+__global__ void k_synth_fill(uint16_t *frames, int nframes, int C, int H, int W, int row_begin,
+		int row_end, uint64_t seed, int maxshift);
+
+#define SG_LIT_THREADS 16384
+
+struct SgBuf {
+	void *p = nullptr;
+	size_t size = 0;
+};
+
+struct SgDevice {
+	int id = 0;
+	hipStream_t stream = nullptr;
+	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+	SgBuf flag_list, flag_map, flag_count, rej, sum_buf, maxim, shifts, norm, tables, scratch, frames, out;
+	uint16_t *pinned[2] = {nullptr, nullptr};
+	size_t pinned_size = 0;
+};
+
+struct sg_ctx {
+	std::vector<SgDevice> dev;
+	std::string err;
+	sg_stack_stats stats;
+};
+
+static int set_err(sg_ctx *ctx, int code, const char *fmt, const char *a = "", long b = 0) {
+	char buf[512];
+	snprintf(buf, sizeof buf, fmt, a, b);
+	if (ctx)
+		ctx->err = buf;
+	return code;
+}
+
+#define HIPCHK(call)                                                                       \
+	do {                                                                               \
+		hipError_t _e = (call);                                                    \
+		if (_e != hipSuccess)                                                      \
+			return set_err(ctx, SG_ERR_DEVICE, "HIP error %s at line %ld",     \
+					hipGetErrorString(_e), (long)__LINE__);            \
+	} while (0)
+
+static hipError_t ensure(SgBuf &b, size_t bytes) {
+	if (b.size >= bytes && b.p)
+		return hipSuccess;
+	if (b.p)
+		(void)hipFree(b.p);
+	b.p = nullptr;
+	b.size = 0;
+	size_t sz = bytes ? bytes : 16;
+	hipError_t e = hipMalloc(&b.p, sz);
+	if (e == hipSuccess)
+		b.size = sz;
+	return e;
+}
+
+extern "C" int sg_init(sg_ctx **out, int ndev, const int *devs) {
+	if (!out)
+		return SG_ERR_GENERIC;
+	*out = nullptr;
+	int count = 0;
+	if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+		return SG_ERR_DEVICE;
+	sg_ctx *ctx = new sg_ctx();
+	memset(&ctx->stats, 0, sizeof ctx->stats);
+	if (ndev <= 0)
+		ndev = 1;
+	for (int i = 0; i < ndev; i++) {
+		SgDevice d;
+		d.id = devs ? devs[i] : i;
+		if (d.id < 0 || d.id >= count) {
+			delete ctx;
+			return SG_ERR_DEVICE;
+		}
+		if (hipSetDevice(d.id) != hipSuccess || hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking) != hipSuccess) {
+			delete ctx;
+			return SG_ERR_DEVICE;
+		}
+		for (int k = 0; k < 4; k++)
+			(void)hipEventCreate(&d.ev[k]);
+		ctx->dev.push_back(d);
+	}
+	*out = ctx;
+	return SG_OK;
+}
+
+extern "C" void sg_shutdown(sg_ctx *ctx) {
+	if (!ctx)
+		return;
+	for (auto &d : ctx->dev) {
+		(void)hipSetDevice(d.id);
+		(void)hipStreamSynchronize(d.stream);
+		SgBuf *bufs[] = {&d.flag_list, &d.flag_map, &d.flag_count, &d.rej, &d.sum_buf, &d.maxim,
+			&d.shifts, &d.norm, &d.tables, &d.scratch, &d.frames, &d.out};
+		for (SgBuf *b : bufs)
+			if (b->p)
+				(void)hipFree(b->p);
+		for (int k = 0; k < 2; k++)
+			if (d.pinned[k])
+				(void)hipHostFree(d.pinned[k]);
+		for (int k = 0; k < 4; k++)
+			if (d.ev[k])
+				(void)hipEventDestroy(d.ev[k]);
+		(void)hipStreamDestroy(d.stream);
+	}
+	delete ctx;
+}
+
+extern "C" const char *sg_last_error(const sg_ctx *ctx) {
+	return ctx ? ctx->err.c_str() : "no context";
+}
+
+extern "C" int sg_get_last_stats(const sg_ctx *ctx, sg_stack_stats *st) {
+	if (!ctx || !st)
+		return SG_ERR_GENERIC;
+	*st = ctx->stats;
+	return SG_OK;
+}
+
+/* ---- reference block partition (src/stacking/stacking.c:1397-1476) and the libgomp
+ *      schedule(static) assignment of blocks to OpenMP threads (:1513-1516) ---- */
+struct Block {
+	long channel, start_row, end_row;
+};
+
+static int make_blocks(long H, int nb_channels, int max_number_of_rows, int nb_threads,
+		std::vector<Block> &blocks) {
+	int size_of_stacks = max_number_of_rows / nb_threads;
+	if (size_of_stacks == 0)
+		size_of_stacks = 1;
+	long nb_parallel_stacks;
+	int remainder;
+	if (H / size_of_stacks < 4) {
+		nb_parallel_stacks = 4 * nb_channels;
+		size_of_stacks = (int)(H / 4);
+		remainder = (int)(H % 4);
+	} else {
+		nb_parallel_stacks = H * nb_channels / size_of_stacks;
+		if (nb_parallel_stacks % nb_channels != 0 || (H * nb_channels) % size_of_stacks != 0) {
+			nb_parallel_stacks += nb_channels - (nb_parallel_stacks % nb_channels);
+			size_of_stacks = (int)(H * nb_channels / nb_parallel_stacks);
+		}
+		remainder = (int)(H - (nb_parallel_stacks / nb_channels * size_of_stacks));
+	}
+	if (size_of_stacks <= 0)
+		return -1;
+	blocks.clear();
+	long channel = 0, row = 0, end;
+	do {
+		if ((long)blocks.size() >= nb_parallel_stacks)
+			return -1;
+		Block b;
+		b.channel = channel;
+		b.start_row = row;
+		end = row + size_of_stacks - 1;
+		if (remainder > 0) {
+			end++;
+			remainder--;
+		}
+		if (end >= H - 1 || (H - end < size_of_stacks / 10)) {
+			end = H - 1;
+			row = 0;
+			channel++;
+			remainder = (int)(H - (nb_parallel_stacks / nb_channels * size_of_stacks));
+		} else {
+			row = end + 1;
+		}
+		b.end_row = end;
+		blocks.push_back(b);
+	} while (channel < nb_channels);
+	return (long)blocks.size() == nb_parallel_stacks ? 0 : -1;
+}
+
+static void omp_static_chunk(long n, int nthr, int t, long *begin, long *end) {
+	long q = n / nthr, r = n % nthr;
+	if (t < r) {
+		q++;
+		*begin = q * t;
+	} else {
+		*begin = q * t + r;
+	}
+	*end = *begin + q;
+}
+
+static int default_threads(void) {
+	long n = sysconf(_SC_NPROCESSORS_ONLN);
+	return n > 0 ? (int)n : 1;
+}
+
+static int pick_nreg(int N) {
+	if (N <= 64) return 1;
+	if (N <= 128) return 2;
+	if (N <= 256) return 4;
+	if (N <= 512) return 8;
+	if (N <= 1024) return 16;
+	return 0;
+}
+
+static hipError_t launch_sorted(int nreg, dim3 grid, size_t lds, hipStream_t s, const SgStackParams &p) {
+	switch (nreg) {
+#define SG_CASE(R)                                                                                  \
+	case R:                                                                                     \
+		(void)hipFuncSetAttribute((const void *)k_stack_sorted<R>,                          \
+				hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);              \
+		hipLaunchKernelGGL(k_stack_sorted<R>, grid, dim3(SG_SORT_THREADS), lds, s, p);      \
+		return hipGetLastError();
+		SG_CASE(1)
+		SG_CASE(2)
+		SG_CASE(4)
+		SG_CASE(8)
+		SG_CASE(16)
+#undef SG_CASE
+	}
+	return hipErrorInvalidValue;
+}
+
+extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
+		const uint16_t *d_frames, int64_t frame_stride, int64_t plane_stride, uint16_t *d_out,
+		int row_begin, int row_end, uint64_t rej[3][2], uint64_t *maxim_out, void *stream) {
+	if (!ctx || !d || dev_index < 0 || dev_index >= (int)ctx->dev.size())
+		return SG_ERR_GENERIC;
+	SgDevice &dv = ctx->dev[dev_index];
+	const int N = d->nb_frames, W = d->width, H = d->height, C = d->nb_layers;
+	if (N < 2)
+		return set_err(ctx, SG_ERR_GENERIC, "select at least two frames (%s%ld)", "", N);
+	if (W <= 0 || H <= 0 || C < 1 || C > 3 || row_begin < 0 || row_end > H || row_begin >= row_end)
+		return set_err(ctx, SG_ERR_SIZE, "bad geometry%s %ld", "", 0);
+	if (d->method < 0 || d->method > 4)
+		return set_err(ctx, SG_ERR_GENERIC, "unknown method%s %ld", "", d->method);
+	HIPCHK(hipSetDevice(dv.id));
+	hipStream_t s = stream ? (hipStream_t)stream : dv.stream;
+	const int nrows = row_end - row_begin;
+	const size_t npix_img = (size_t)C * H * W;
+	memset(&ctx->stats, 0, sizeof ctx->stats);
+
+	SgStackParams p;
+	memset(&p, 0, sizeof p);
+	p.frames = d_frames;
+	p.frame_stride = frame_stride;
+	p.plane_stride = plane_stride;
+	p.out = d_out;
+	p.N = N;
+	p.W = W;
+	p.H = H;
+	p.C = C;
+	p.method = d->method;
+	p.rejection = d->rejection;
+	p.normalize = (d->method == SG_STACK_MEAN || d->method == SG_STACK_MEDIAN) ? d->normalize : 0;
+	p.sig0 = d->sig[0];
+	p.sig1 = d->sig[1];
+	p.use_shift = (d->method != SG_STACK_MEDIAN) && d->shiftx && d->shifty;
+	p.row_begin = row_begin;
+	p.row_end = row_end;
+
+	/* per-frame constants: shifts + normalisation coefficients */
+	HIPCHK(ensure(dv.shifts, sizeof(int) * 2 * N));
+	HIPCHK(ensure(dv.norm, sizeof(double) * 3 * N));
+	if (p.use_shift) {
+		std::vector<int> sh(2 * N);
+		memcpy(sh.data(), d->shiftx, sizeof(int) * N);
+		memcpy(sh.data() + N, d->shifty, sizeof(int) * N);
+		HIPCHK(hipMemcpyAsync(dv.shifts.p, sh.data(), sizeof(int) * 2 * N, hipMemcpyHostToDevice, s));
+		p.shiftx = (const int *)dv.shifts.p;
+		p.shifty = p.shiftx + N;
+	}
+	if (p.normalize) {
+		std::vector<double> nm(3 * N);
+		for (int i = 0; i < N; i++) {
+			nm[i] = d->offset ? d->offset[i] : 0.0;
+			nm[N + i] = d->mul ? d->mul[i] : 1.0;
+			nm[2 * N + i] = d->scale ? d->scale[i] : 1.0;
+		}
+		HIPCHK(hipMemcpyAsync(dv.norm.p, nm.data(), sizeof(double) * 3 * N, hipMemcpyHostToDevice, s));
+		p.offset = (const double *)dv.norm.p;
+		p.mul = p.offset + N;
+		p.scale = p.offset + 2 * N;
+	}
+	HIPCHK(ensure(dv.rej, sizeof(unsigned long long) * SG_REJ_SHARDS * 6));
+	HIPCHK(ensure(dv.flag_count, 64));
+	HIPCHK(ensure(dv.maxim, 64));
+	HIPCHK(hipMemsetAsync(dv.rej.p, 0, sizeof(unsigned long long) * SG_REJ_SHARDS * 6, s));
+	HIPCHK(hipMemsetAsync(dv.flag_count.p, 0, 64, s));
+	HIPCHK(hipMemsetAsync(dv.maxim.p, 0, 64, s));
+	p.rej = (unsigned long long *)dv.rej.p;
+	p.flag_count = (unsigned int *)dv.flag_count.p;
+	p.maxim = (unsigned int *)dv.maxim.p;
+
+	const bool sorted = (d->method == SG_STACK_MEDIAN) ||
+		(d->method == SG_STACK_MEAN && d->rejection != SG_NO_REJEC);
+	std::vector<int> tables;
+	SgChainTables ct;
+	memset(&ct, 0, sizeof ct);
+	if (sorted) {
+		const int nreg = pick_nreg(N);
+		if (!nreg)
+			return set_err(ctx, SG_ERR_SIZE, "rejection/median stacking supports up to 1024 frames%s (%ld)", "", N);
+		const size_t npix_launch = (size_t)C * nrows * W;
+		HIPCHK(ensure(dv.flag_list, sizeof(unsigned int) * npix_launch));
+		HIPCHK(ensure(dv.flag_map, npix_img));
+		HIPCHK(hipMemsetAsync(dv.flag_map.p, 0, npix_img, s));
+		p.flag_list = (unsigned int *)dv.flag_list.p;
+		p.flag_cap = (unsigned int)npix_launch;
+		p.flag_map = (uint8_t *)dv.flag_map.p;
+
+		/* reference thread order tables for the stale-state chains */
+		int nthr = d->max_thread > 0 ? d->max_thread : default_threads();
+		int maxrows = d->max_number_of_rows > 0 ? d->max_number_of_rows : H;
+		std::vector<Block> blocks;
+		if (make_blocks(H, C, maxrows, nthr, blocks))
+			return set_err(ctx, SG_ERR_GENERIC, "block partition failed (the reference would read "
+					"uninitialised blocks)%s%ld", "", 0);
+		const int nb = (int)blocks.size();
+		tables.assign((size_t)C * H + 4 * nb, 0);
+		int *blk_of_row = tables.data(), *bch = blk_of_row + (size_t)C * H, *bst = bch + nb,
+		    *ben = bst + nb, *bfi = ben + nb;
+		for (int b = 0; b < nb; b++) {
+			bch[b] = (int)blocks[b].channel;
+			bst[b] = (int)blocks[b].start_row;
+			ben[b] = (int)blocks[b].end_row;
+			for (long r = blocks[b].start_row; r <= blocks[b].end_row; r++)
+				blk_of_row[(size_t)blocks[b].channel * H + r] = b;
+		}
+		for (int t = 0; t < nthr; t++) {
+			long b0, b1;
+			omp_static_chunk(nb, nthr, t, &b0, &b1);
+			for (long b = b0; b < b1; b++)
+				bfi[b] = (int)b0;
+		}
+		HIPCHK(ensure(dv.tables, sizeof(int) * tables.size()));
+		HIPCHK(hipMemcpyAsync(dv.tables.p, tables.data(), sizeof(int) * tables.size(), hipMemcpyHostToDevice, s));
+		const int *tb = (const int *)dv.tables.p;
+		ct.blk_of_row = tb;
+		ct.blk_channel = tb + (size_t)C * H;
+		ct.blk_start = ct.blk_channel + nb;
+		ct.blk_end = ct.blk_start + nb;
+		ct.blk_first = ct.blk_end + nb;
+		ct.nblocks = nb;
+
+		const int ntx = (W + SG_TILE_W - 1) / SG_TILE_W;
+		const size_t nblk = (size_t)ntx * nrows * C;
+		const size_t lds = (size_t)N * SG_STAGE_STRIDE * 2;
+		HIPCHK(hipEventRecord(dv.ev[0], s));
+		HIPCHK(launch_sorted(nreg, dim3((unsigned)nblk), lds, s, p));
+		HIPCHK(hipEventRecord(dv.ev[1], s));
+		ctx->stats.main_kernel_blocks = (int)nblk;
+		ctx->stats.launches = 1;
+		/* literal path for queued pixels: two phases, grid reads the count on device */
+		HIPCHK(ensure(dv.scratch, (size_t)SG_LIT_THREADS * (((size_t)N * 5 + 15) & ~(size_t)15)));
+		for (int phase = 1; phase <= 2; phase++) {
+			hipLaunchKernelGGL(k_stack_literal, dim3(SG_LIT_THREADS / 64), dim3(64), 0, s, p, ct,
+					0u, (uint8_t *)dv.scratch.p, phase);
+			HIPCHK(hipGetLastError());
+		}
+		ctx->stats.launches += 2;
+	} else {
+		if (d->method == SG_STACK_SUM) {
+			HIPCHK(ensure(dv.sum_buf, sizeof(uint32_t) * npix_img));
+			p.sum_buf = (uint32_t *)dv.sum_buf.p;
+		}
+		dim3 grid((W + 255) / 256, nrows, C);
+		HIPCHK(hipEventRecord(dv.ev[0], s));
+		hipLaunchKernelGGL(k_stack_reduce, grid, dim3(256), 0, s, p);
+		HIPCHK(hipGetLastError());
+		HIPCHK(hipEventRecord(dv.ev[1], s));
+		ctx->stats.main_kernel_blocks = (int)(grid.x * grid.y * grid.z);
+		ctx->stats.launches = 1;
+		if (d->method == SG_STACK_SUM) {
+			hipLaunchKernelGGL(k_sum_finalize, grid, dim3(256), 0, s, p);
+			HIPCHK(hipGetLastError());
+			ctx->stats.launches++;
+		}
+	}
+	HIPCHK(hipEventRecord(dv.ev[2], s));
+	/* counters back to the host */
+	std::vector<unsigned long long> shards(SG_REJ_SHARDS * 6);
+	unsigned int cnt[2] = {0, 0};
+	HIPCHK(hipMemcpyAsync(shards.data(), dv.rej.p, sizeof(unsigned long long) * shards.size(), hipMemcpyDeviceToHost, s));
+	HIPCHK(hipMemcpyAsync(cnt, dv.flag_count.p, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+	HIPCHK(hipMemcpyAsync(cnt + 1, dv.maxim.p, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+	HIPCHK(hipStreamSynchronize(s));
+	float ms = 0.f, ms2 = 0.f;
+	HIPCHK(hipEventElapsedTime(&ms, dv.ev[0], dv.ev[1]));
+	HIPCHK(hipEventElapsedTime(&ms2, dv.ev[0], dv.ev[2]));
+	ctx->stats.kernel_ms = ms;
+	ctx->stats.total_ms = ms2;
+	ctx->stats.slow_pixels = cnt[0];
+	if (rej) {
+		for (int c = 0; c < 3; c++)
+			rej[c][0] = rej[c][1] = 0;
+		for (int k = 0; k < SG_REJ_SHARDS; k++)
+			for (int c = 0; c < 3; c++) {
+				rej[c][0] += shards[(size_t)k * 6 + c * 2];
+				rej[c][1] += shards[(size_t)k * 6 + c * 2 + 1];
+			}
+	}
+	if (maxim_out)
+		*maxim_out = cnt[1];
+	return SG_OK;
+}
+
+/* host-pull path: frames come through seq_opened_read_region-shaped callbacks */
+extern "C" int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *d, sg_read_region_fn pull, void *user,
+		sg_should_continue_fn cont, void *cont_user, uint16_t *out, uint64_t rej[3][2],
+		uint64_t *maxim) {
+	if (!ctx || !d || !pull || !out || ctx->dev.empty())
+		return SG_ERR_GENERIC;
+	SgDevice &dv = ctx->dev[0];
+	const int N = d->nb_frames, W = d->width, H = d->height, C = d->nb_layers;
+	if (N < 2)
+		return set_err(ctx, SG_ERR_GENERIC, "select at least two frames%s (%ld)", "", N);
+	if (W <= 0 || H <= 0 || C < 1 || C > 3)
+		return SG_ERR_SIZE;
+	HIPCHK(hipSetDevice(dv.id));
+	const size_t plane = (size_t)W * H;
+	HIPCHK(ensure(dv.frames, plane * C * N * sizeof(uint16_t)));
+	HIPCHK(ensure(dv.out, plane * C * sizeof(uint16_t)));
+	if (dv.pinned_size < plane) {
+		for (int k = 0; k < 2; k++) {
+			if (dv.pinned[k])
+				(void)hipHostFree(dv.pinned[k]);
+			HIPCHK(hipHostMalloc((void **)&dv.pinned[k], plane * sizeof(uint16_t) * 2));
+		}
+		dv.pinned_size = plane;
+	}
+	uint16_t *band = dv.pinned[0] + plane;	/* top-down band as returned by the reader */
+	sg_rect area = {0, 0, W, H};
+	int k = 0;
+	for (int i = 0; i < N; i++) {
+		if (cont && !cont(cont_user))
+			return SG_ERR_GENERIC;	/* cancelled, like get_thread_run() */
+		for (int c = 0; c < C; c++) {
+			uint16_t *flip = dv.pinned[k];
+			HIPCHK(hipStreamSynchronize(dv.stream));	/* buffer k free again */
+			uint16_t *tb = flip + plane;
+			if (pull(user, c, i, tb, &area) < 0)
+				return set_err(ctx, SG_ERR_READ, "could not read frame%s %ld", "", i);
+			for (int t = 0; t < H; t++)
+				memcpy(flip + (size_t)(H - 1 - t) * W, tb + (size_t)t * W, W * sizeof(uint16_t));
+			HIPCHK(hipMemcpyAsync((uint16_t *)dv.frames.p + ((size_t)i * C + c) * plane, flip,
+					plane * sizeof(uint16_t), hipMemcpyHostToDevice, dv.stream));
+			k ^= 1;
+		}
+	}
+	(void)band;
+	int rc = sg_stack_u16_device(ctx, 0, d, (const uint16_t *)dv.frames.p, (int64_t)plane * C,
+			(int64_t)plane, (uint16_t *)dv.out.p, 0, H, rej, maxim, nullptr);
+	if (rc)
+		return rc;
+	HIPCHK(hipMemcpy(out, dv.out.p, plane * C * sizeof(uint16_t), hipMemcpyDeviceToHost));
+	return SG_OK;
+}
+
+extern "C" int sg_synth_fill_device(sg_ctx *ctx, int dev_index, uint16_t *d_frames, int nframes,
+		int nb_layers, int height, int width, int row_begin, int row_end, uint64_t seed,
+		int maxshift, void *stream) {
+	if (!ctx || dev_index < 0 || dev_index >= (int)ctx->dev.size())
+		return SG_ERR_GENERIC;
+	SgDevice &dv = ctx->dev[dev_index];
+	HIPCHK(hipSetDevice(dv.id));
+	hipStream_t s = stream ? (hipStream_t)stream : dv.stream;
+	hipLaunchKernelGGL(k_synth_fill, dim3(8192), dim3(256), 0, s, d_frames, nframes, nb_layers,
+			height, width, row_begin, row_end, seed, maxshift);
+	HIPCHK(hipGetLastError());
+	HIPCHK(hipStreamSynchronize(s));
+	return SG_OK;
+}

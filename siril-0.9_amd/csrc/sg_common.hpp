@@ -1,0 +1,82 @@
+/*
+ * sg_common.hpp - shared device-side definitions for the stacking kernels (gfx950).
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define SG_TILE_W 64		/* pixels per stacking tile (one 128-B row segment) */
+#define SG_STAGE_STRIDE 66	/* u16 per staged frame row: 64 px + 2 pad -> 33 dwords, bank-conflict free */
+#define SG_SORT_THREADS 256
+#define SG_REJ_SHARDS 1024
+
+enum { SG_CLS_OK = 0, SG_CLS_LITERAL = 1, SG_CLS_CHAIN = 2 };
+
+/* everything the stacking kernels need, passed by value */
+struct SgStackParams {
+	const uint16_t *frames;
+	int64_t frame_stride, plane_stride;	/* elements */
+	uint16_t *out;
+	int N, W, H, C;
+	int method, rejection, normalize;
+	int use_shift;
+	double sig0, sig1;
+	const int *shiftx, *shifty;		/* device [N] */
+	const double *offset, *mul, *scale;	/* device [N] or null */
+	int row_begin, row_end;			/* memory rows to compute */
+	unsigned long long *rej;		/* [SG_REJ_SHARDS][3][2] */
+	unsigned int *flag_count;
+	unsigned int *flag_list;		/* encoded (c*H + R)*W + x */
+	unsigned int flag_cap;
+	uint8_t *flag_map;			/* [C][H][W] class per pixel (chain walk) */
+	uint32_t *sum_buf;			/* SUM: raw sums [C][H][W] */
+	unsigned int *maxim;			/* SUM: global max of sums */
+};
+
+/* round_to_WORD, src/core/utils.c:68-74 */
+__device__ __forceinline__ uint16_t sg_round_to_WORD(double x) {
+	if (x <= 0.0)
+		return 0;
+	if (x > 65535.0)
+		return 65535;
+	return (uint16_t)(x + 0.5);
+}
+
+/* normalisation of one gathered sample, src/stacking/stacking.c:1635-1652 (and :750-764) */
+__device__ __forceinline__ uint16_t sg_normalize(const SgStackParams &p, int f, uint16_t v) {
+	switch (p.normalize) {
+	default:
+	case 0:
+		return v;
+	case 1:	/* ADDITIVE */
+	case 3: {	/* ADDITIVE_SCALING */
+		double tmp = (double)v * (p.scale ? p.scale[f] : 1.0);
+		return sg_round_to_WORD(tmp - (p.offset ? p.offset[f] : 0.0));
+	}
+	case 2:	/* MULTIPLICATIVE */
+	case 4: {
+		double tmp = (double)v * (p.scale ? p.scale[f] : 1.0);
+		return sg_round_to_WORD(tmp * (p.mul ? p.mul[f] : 1.0));
+	}
+	}
+}
+
+/* sample of frame f at output pixel (c, R, x) (memory coords): the rejection stacker's
+ * y-shifted band read (:1550-1577) leaves zero rows in the block buffer, and those zeros
+ * ARE normalised like read samples (:1644-1650); the x shift writes 0 directly into the
+ * stack, bypassing normalisation (:1628-1632).  The median stacker ignores shifts (:703-722). */
+__device__ __forceinline__ uint16_t sg_gather(const SgStackParams &p, int f, int c, int R, int x) {
+	int sx = 0, sy = 0;
+	if (p.use_shift) {
+		sx = p.shiftx[f];
+		sy = p.shifty[f];
+	}
+	int sr = R - sy, sc = x - sx;
+	if ((unsigned)sc >= (unsigned)p.W)
+		return 0;
+	uint16_t v = 0;
+	if ((unsigned)sr < (unsigned)p.H)
+		v = p.frames[(int64_t)f * p.frame_stride + (int64_t)c * p.plane_stride +
+			(int64_t)sr * p.W + sc];
+	return sg_normalize(p, f, v);
+}

@@ -1,0 +1,271 @@
+/*
+ * sg_f80.h - software x87 80-bit extended arithmetic (64-bit mantissa, round to nearest
+ * even), host + gfx950 device.
+ *
+ * Why: Siril's rejection stackers call gsl_stats_ushort_sd (src/stacking/stacking.c:1676,
+ * 1698,1713,1727), whose running mean/variance recurrences are long double, i.e. x87
+ * extended on x86-64.  The GPU fast path decides with exact integer moments and hands
+ * every pixel whose decision lies within a rounding band of a threshold to the literal
+ * slow path, which replays GSL's recurrences through this type so its sigma is
+ * bit-identical to the reference's.  Only normal numbers and zero are needed (inputs
+ * are u16 samples, counts and their squares).  Checked against native long double by
+ * tests/test_f80.py.
+ */
+#ifndef SG_F80_H
+#define SG_F80_H
+
+#include <stdint.h>
+#include <string.h>
+
+#if defined(__HIPCC__)
+#define F80_HD __host__ __device__ static inline
+#else
+#define F80_HD static inline
+#endif
+
+typedef struct {
+	uint64_t m;	/* normalised mantissa (bit 63 set) or 0 for zero */
+	int32_t e;	/* value = (-1)^s * m * 2^(e - 63) */
+	int32_t s;
+} sg_f80;
+
+F80_HD int f80_clz64(uint64_t x) {
+#if defined(__HIPCC__) || defined(__GNUC__)
+	return x ? __builtin_clzll(x) : 64;
+#else
+	int n = 0;
+	if (!x) return 64;
+	while (!(x & (1ull << 63))) { x <<= 1; n++; }
+	return n;
+#endif
+}
+
+F80_HD void f80_mul64(uint64_t a, uint64_t b, uint64_t *hi, uint64_t *lo) {
+	uint64_t a0 = a & 0xFFFFFFFFull, a1 = a >> 32, b0 = b & 0xFFFFFFFFull, b1 = b >> 32;
+	uint64_t p00 = a0 * b0, p01 = a0 * b1, p10 = a1 * b0, p11 = a1 * b1;
+	uint64_t mid = (p00 >> 32) + (p01 & 0xFFFFFFFFull) + (p10 & 0xFFFFFFFFull);
+	*lo = (p00 & 0xFFFFFFFFull) | (mid << 32);
+	*hi = p11 + (p01 >> 32) + (p10 >> 32) + (mid >> 32);
+}
+
+F80_HD sg_f80 f80_zero(void) {
+	sg_f80 r = {0, 0, 0};
+	return r;
+}
+
+/* (hi:lo) normalised (hi bit 63 set), value = (hi:lo) * 2^(E - 127); round to 64 bits */
+F80_HD sg_f80 f80_round128(uint64_t hi, uint64_t lo, int sticky, int32_t E, int32_t s) {
+	uint64_t m = hi;
+	int rb = (int)(lo >> 63);
+	int st = ((lo << 1) != 0) || sticky;
+	if (rb && (st || (m & 1))) {
+		m++;
+		if (m == 0) {
+			m = 1ull << 63;
+			E++;
+		}
+	}
+	sg_f80 r = {m, E, s};
+	return r;
+}
+
+F80_HD sg_f80 f80_from_u64(uint64_t x) {
+	if (!x) return f80_zero();
+	int sh = f80_clz64(x);
+	sg_f80 r = {x << sh, 63 - sh, 0};
+	return r;
+}
+
+F80_HD sg_f80 f80_from_double(double d) {
+	uint64_t bits;
+	memcpy(&bits, &d, 8);
+	int s = (int)(bits >> 63);
+	int ex = (int)((bits >> 52) & 0x7FF);
+	uint64_t fr = bits & 0xFFFFFFFFFFFFFull;
+	if (ex == 0 && fr == 0) {
+		sg_f80 z = {0, 0, s};
+		return z;
+	}
+	if (ex == 0) {	/* subnormal double: normalise */
+		int sh = f80_clz64(fr);
+		sg_f80 r = {fr << sh, -1074 + 63 - sh, s};
+		return r;
+	}
+	sg_f80 r = {(fr | (1ull << 52)) << 11, ex - 1023, s};
+	return r;
+}
+
+F80_HD double f80_to_double(sg_f80 a) {
+	if (!a.m) return a.s ? -0.0 : 0.0;
+	uint64_t keep = a.m >> 11, rem = a.m & 0x7FF;
+	int32_t e = a.e;
+	if (rem > 0x400 || (rem == 0x400 && (keep & 1))) {
+		keep++;
+		if (keep == (1ull << 53)) {
+			keep >>= 1;
+			e++;
+		}
+	}
+	/* normal range only (|e| < 1023 for every value this library sees) */
+	uint64_t bits = ((uint64_t)a.s << 63) | ((uint64_t)(e + 1023) << 52) | (keep & 0xFFFFFFFFFFFFFull);
+	double d;
+	memcpy(&d, &bits, 8);
+	return d;
+}
+
+F80_HD sg_f80 f80_neg(sg_f80 a) {
+	a.s ^= 1;
+	return a;
+}
+
+F80_HD sg_f80 f80_add(sg_f80 a, sg_f80 b) {
+	if (!a.m) return b.m ? b : (a.s && b.s ? a : f80_zero());
+	if (!b.m) return a;
+	if (b.e > a.e || (b.e == a.e && b.m > a.m)) {
+		sg_f80 t = a;
+		a = b;
+		b = t;
+	}
+	int32_t d = a.e - b.e;
+	uint64_t Ah = a.m, Al = 0, Bh, Bl;
+	int sticky = 0;
+	if (d == 0) {
+		Bh = b.m;
+		Bl = 0;
+	} else if (d < 64) {
+		Bh = b.m >> d;
+		Bl = b.m << (64 - d);
+	} else if (d < 128) {
+		Bh = 0;
+		Bl = (d == 64) ? b.m : (b.m >> (d - 64));
+		sticky = (d > 64) && ((b.m << (128 - d)) != 0);
+	} else {
+		Bh = 0;
+		Bl = 0;
+		sticky = 1;
+	}
+	if (a.s == b.s) {
+		uint64_t lo = Al + Bl;
+		uint64_t c = lo < Al;
+		uint64_t t = Ah + Bh;
+		uint64_t c1 = t < Ah;
+		uint64_t hi = t + c;
+		uint64_t c2 = hi < t;
+		int carry = (int)(c1 | c2);
+		if (carry) {
+			sticky |= (int)(lo & 1);
+			lo = (lo >> 1) | (hi << 63);
+			hi = (hi >> 1) | (1ull << 63);
+			return f80_round128(hi, lo, sticky, a.e + 1, a.s);
+		}
+		return f80_round128(hi, lo, sticky, a.e, a.s);
+	} else {
+		/* |A| >= |B|; a dropped sticky tail of B means the true B is a bit larger */
+		uint64_t lo = Al - Bl;
+		uint64_t bw = Al < Bl;
+		uint64_t hi = Ah - Bh - bw;
+		if (sticky) {
+			uint64_t b2 = (lo == 0);
+			lo -= 1;
+			hi -= b2;
+		}
+		if (!hi && !lo) return f80_zero();
+		int32_t E = a.e;
+		int sh = hi ? f80_clz64(hi) : 64 + f80_clz64(lo);
+		if (sh >= 64) {
+			hi = lo << (sh - 64);
+			lo = 0;
+		} else if (sh > 0) {
+			hi = (hi << sh) | (lo >> (64 - sh));
+			lo <<= sh;
+		}
+		return f80_round128(hi, lo, sticky, E - sh, a.s);
+	}
+}
+
+F80_HD sg_f80 f80_sub(sg_f80 a, sg_f80 b) {
+	return f80_add(a, f80_neg(b));
+}
+
+F80_HD sg_f80 f80_mul(sg_f80 a, sg_f80 b) {
+	if (!a.m || !b.m) return f80_zero();
+	uint64_t hi, lo;
+	f80_mul64(a.m, b.m, &hi, &lo);
+	int32_t E = a.e + b.e + 1;
+	if (!(hi >> 63)) {
+		hi = (hi << 1) | (lo >> 63);
+		lo <<= 1;
+		E--;
+	}
+	return f80_round128(hi, lo, 0, E, a.s ^ b.s);
+}
+
+F80_HD sg_f80 f80_div(sg_f80 a, sg_f80 b) {
+	if (!a.m) return f80_zero();
+	/* Q' = floor(a.m * 2^65 / b.m), 65 or 66 bits, by restoring division */
+	uint64_t rem = a.m, q_top = 0, q_lo = 0;
+	if (rem >= b.m) {
+		rem -= b.m;
+		q_lo = 1;
+	}
+	for (int i = 0; i < 65; i++) {
+		uint64_t carry = rem >> 63;
+		rem <<= 1;
+		uint64_t bit = 0;
+		if (carry || rem >= b.m) {
+			rem -= b.m;
+			bit = 1;
+		}
+		/* shift (q_top:q_lo) left by one and insert bit */
+		q_top = (q_top << 1) | (q_lo >> 63);
+		q_lo = (q_lo << 1) | bit;
+	}
+	int st = rem != 0;
+	uint64_t m;
+	int rb;
+	int32_t E;
+	if (q_top & 2) {	/* 66-bit quotient */
+		m = (q_top << 62) | (q_lo >> 2);
+		rb = (int)((q_lo >> 1) & 1);
+		st |= (int)(q_lo & 1);
+		E = a.e - b.e;
+	} else {		/* 65-bit quotient */
+		m = (q_top << 63) | (q_lo >> 1);
+		rb = (int)(q_lo & 1);
+		E = a.e - b.e - 1;
+	}
+	if (rb && (st || (m & 1))) {
+		m++;
+		if (m == 0) {
+			m = 1ull << 63;
+			E++;
+		}
+	}
+	sg_f80 r = {m, E, a.s ^ b.s};
+	return r;
+}
+
+/* gsl_stats_ushort_mean / sd restated on sg_f80 (see or_core.c for the algorithm) */
+F80_HD double f80_gsl_mean_u16(const uint16_t *data, int n) {
+	sg_f80 mean = f80_zero();
+	for (int i = 0; i < n; i++) {
+		sg_f80 t = f80_sub(f80_from_u64(data[i]), mean);
+		t = f80_div(t, f80_from_u64((uint64_t)i + 1));
+		mean = f80_add(mean, t);
+	}
+	return f80_to_double(mean);
+}
+
+F80_HD double f80_gsl_variance_m_u16(const uint16_t *data, int n, double mean) {
+	sg_f80 var = f80_zero();
+	for (int i = 0; i < n; i++) {
+		double dd = (double)data[i] - mean;	/* formed in double, as in GSL */
+		sg_f80 delta = f80_from_double(dd);
+		sg_f80 t = f80_sub(f80_mul(delta, delta), var);
+		t = f80_div(t, f80_from_u64((uint64_t)i + 1));
+		var = f80_add(var, t);
+	}
+	return f80_to_double(var);
+}
+
+#endif /* SG_F80_H */

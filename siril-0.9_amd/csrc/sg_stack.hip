@@ -1,0 +1,967 @@
+/*
+ * sg_stack.hip - gfx950 stacking kernels for the Siril 0.9 hot path.
+ *
+ * k_stack_sorted<NREG>  : median (stacking.c:362-816) and mean-with-rejection for
+ *                         PERCENTILE / SIGMA / WINSORIZED (stacking.c:1189-1858).
+ *   1. stage a 64-pixel x N-frame tile of one row into LDS (shift + zero fill +
+ *      normalisation fused into the gather, :1535-1654);
+ *   2. each wave sorts two pixel columns at once: the N samples (padded to 64*NREG
+ *      with 65535) live in NREG packed-u16 VGPRs per lane and go through a bitonic
+ *      network (v_pk_min_u16 / v_pk_max_u16 inside a lane, __shfl_xor across lanes);
+ *      the sorted columns are written back in place;
+ *   3. one lane per pixel runs the reference's iteration on the sorted column with
+ *      exact integer moments (S, SS) instead of GSL's long-double recurrences.  Every
+ *      threshold comparison is made against a rounding band; a pixel whose decision
+ *      falls inside the band, or whose loop hits the reference's early `break`
+ *      (N - r <= 4, :1684) before the last sample, is queued for the literal path.
+ * k_stack_literal       : the queued pixels, one thread each, replaying the reference
+ *                         loop literally (frame order, GSL sd via soft x87 fp80,
+ *                         stale rejected[] state carried between pixels in the
+ *                         reference's OpenMP thread order for first-pass breaks).
+ * k_stack_reduce        : SUM (:196-355), MAX (:824-972), MIN (:979-1128) and MEAN
+ *                         with NO_REJEC: streaming per-pixel reductions.
+ */
+#include "sg_common.hpp"
+#include "sg_f80.h"
+
+typedef unsigned short sg_u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b) {
+	sg_u16x2 x = __builtin_bit_cast(sg_u16x2, a), y = __builtin_bit_cast(sg_u16x2, b);
+	return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(x, y));
+}
+__device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) {
+	sg_u16x2 x = __builtin_bit_cast(sg_u16x2, a), y = __builtin_bit_cast(sg_u16x2, b);
+	return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(x, y));
+}
+
+/* ascending bitonic sort of 64*NREG packed pairs; element e = lane*NREG + r */
+template <int NREG>
+__device__ __forceinline__ void bitonic_sort_packed(uint32_t (&v)[NREG], int lane) {
+	constexpr int NPAD = 64 * NREG;
+#pragma unroll
+	for (int k = 2; k <= NPAD; k <<= 1) {
+		/* first stage of each merge: compare e with e ^ (k-1) (mirror), all ascending */
+		if (k <= NREG) {
+#pragma unroll
+			for (int r = 0; r < NREG; r++) {
+				const int q = r ^ (k - 1);
+				if (q > r) {
+					uint32_t a = v[r], b = v[q];
+					v[r] = pk_min(a, b);
+					v[q] = pk_max(a, b);
+				}
+			}
+		} else {
+			const int m = k / NREG - 1;
+			const bool lower = (lane & (k / (2 * NREG))) == 0;
+			uint32_t t[NREG];
+#pragma unroll
+			for (int r = 0; r < NREG; r++)
+				t[r] = (uint32_t)__shfl_xor((int)v[NREG - 1 - r], m, 64);
+#pragma unroll
+			for (int r = 0; r < NREG; r++)
+				v[r] = lower ? pk_min(v[r], t[r]) : pk_max(v[r], t[r]);
+		}
+		/* half cleaners */
+#pragma unroll
+		for (int j = k >> 2; j > 0; j >>= 1) {
+			if (j < NREG) {
+#pragma unroll
+				for (int r = 0; r < NREG; r++) {
+					const int q = r ^ j;
+					if (q > r) {
+						uint32_t a = v[r], b = v[q];
+						v[r] = pk_min(a, b);
+						v[q] = pk_max(a, b);
+					}
+				}
+			} else {
+				const int m = j / NREG;
+				const bool lower = (lane & m) == 0;
+#pragma unroll
+				for (int r = 0; r < NREG; r++) {
+					uint32_t t = (uint32_t)__shfl_xor((int)v[r], m, 64);
+					v[r] = lower ? pk_min(v[r], t) : pk_max(v[r], t);
+				}
+			}
+		}
+	}
+}
+
+/* ----------------------------------------------------------------------------------
+ * exact-moment rejection on a sorted column
+ * ---------------------------------------------------------------------------------- */
+struct SgCol {
+	const uint16_t *base;	/* LDS, element e at base[e * SG_STAGE_STRIDE] */
+	__device__ __forceinline__ uint32_t operator()(int e) const { return base[e * SG_STAGE_STRIDE]; }
+};
+
+/* # of elements in [lo,hi) with value < thr */
+__device__ __forceinline__ int col_count_lt(const SgCol &A, int lo, int hi, double thr) {
+	int a = lo, b = hi;
+	while (a < b) {
+		int m = (a + b) >> 1;
+		if ((double)A(m) < thr)
+			a = m + 1;
+		else
+			b = m;
+	}
+	return a - lo;
+}
+/* # of elements in [lo,hi) with value <= thr */
+__device__ __forceinline__ int col_count_le(const SgCol &A, int lo, int hi, double thr) {
+	int a = lo, b = hi;
+	while (a < b) {
+		int m = (a + b) >> 1;
+		if ((double)A(m) <= thr)
+			a = m + 1;
+		else
+			b = m;
+	}
+	return a - lo;
+}
+
+/* gsl_stats_ushort_median_from_sorted_data on [lo, lo+n) */
+__device__ __forceinline__ double col_median(const SgCol &A, int lo, int n) {
+	const int lhs = (n - 1) / 2, rhs = n / 2;
+	if (lhs == rhs)
+		return (double)A(lo + lhs);
+	return (double)(A(lo + lhs) + A(lo + rhs)) / 2.0;
+}
+
+/* sample sd from exact moments: sqrt(num / (n (n-1))), num = n*SS - S^2 */
+__device__ __forceinline__ double exact_sd(int n, uint64_t S, uint64_t SS, bool *exact0) {
+	int64_t num = (int64_t)n * (int64_t)SS - (int64_t)(S * S);
+	*exact0 = (num == 0);
+	if (num <= 0)
+		return 0.0;
+	return sqrt((double)num / ((double)n * (double)(n - 1)));
+}
+
+/* relative rounding band around every continuous threshold: GSL's long double sd
+ * differs from the exact one by ~(n+8)*2^-64 relative, the double ops add a few ulp */
+#define SG_BAND 1e-11
+
+struct SgRejState {
+	int lo, hi;
+	uint64_t S, SS;
+	int r, iter;
+	uint32_t rlo, rhi;
+};
+
+/* one clipping pass (:1679-1693 / :1731-1747) with given sigma / median on the sorted
+ * window.  Returns SG_CLS_*; *n = samples removed. */
+__device__ int clip_pass(const SgCol &A, SgRejState &st, double sigma, bool exact0,
+		double median, double sl, double sh, int N0, int *n_removed) {
+	const int N = st.hi - st.lo;
+	const double tl = sl * sigma, th = sh * sigma;
+	const double blo = median - tl, bhi = median + th;
+	int L, H;
+	if (exact0) {
+		L = col_count_lt(A, st.lo, st.hi, blo);
+		H = N - col_count_le(A, st.lo, st.hi, bhi);
+	} else {
+		const double tol = SG_BAND * (fabs(median) + fabs(tl) + fabs(th) + 1.0);
+		const int L1 = col_count_lt(A, st.lo, st.hi, blo - tol);
+		const int L2 = col_count_le(A, st.lo, st.hi, blo + tol);
+		if (L1 != L2)
+			return SG_CLS_LITERAL;
+		const int H1 = N - col_count_le(A, st.lo, st.hi, bhi + tol);
+		const int H2 = N - col_count_lt(A, st.lo, st.hi, bhi - tol);
+		if (H1 != H2)
+			return SG_CLS_LITERAL;
+		L = L1;
+		H = H1;
+	}
+	if (L + H > N)
+		return SG_CLS_LITERAL;	/* negative sigma factors: else-if order matters */
+	/* where does `if (N - r <= 4) break;` fire?  r counts rejections cumulatively */
+	const int need = N - 4 - st.r;
+	int fb = -1;
+	if (need <= 0)
+		fb = 0;
+	else if (L >= need)
+		fb = need - 1;
+	else if (L + H >= need)
+		fb = (N - H) + (need - L) - 1;
+	if (fb >= 0 && fb < N - 1) {
+		/* entries after fb keep stale values */
+		if (st.iter == 1) {
+			if (N0 > 4)
+				return SG_CLS_CHAIN;	/* stale values of the previous pixel */
+			/* N0 <= 4: only entry 0 is ever written, the rest stay calloc zero (:1497) */
+			const int low0 = (L >= 1);
+			const int high0 = (!low0) && (H == N);
+			if (low0)
+				st.rlo++;
+			if (high0)
+				st.rhi++;
+			const int n = low0 || high0;
+			if (n) {
+				const uint32_t v = A(st.lo);
+				st.S -= v;
+				st.SS -= (uint64_t)v * v;
+				st.lo++;
+			}
+			st.r += n;
+			*n_removed = n;
+			return SG_CLS_OK;
+		}
+		return SG_CLS_LITERAL;	/* stale values of this pixel's previous pass */
+	}
+	st.rlo += L;
+	st.rhi += H;
+	for (int i = 0; i < L; i++) {
+		const uint32_t v = A(st.lo + i);
+		st.S -= v;
+		st.SS -= (uint64_t)v * v;
+	}
+	for (int i = 0; i < H; i++) {
+		const uint32_t v = A(st.hi - 1 - i);
+		st.S -= v;
+		st.SS -= (uint64_t)v * v;
+	}
+	st.lo += L;
+	st.hi -= H;
+	st.r += L + H;
+	*n_removed = L + H;
+	return SG_CLS_OK;
+}
+
+__device__ int reject_sigma(const SgCol &A, SgRejState &st, double sl, double sh, int N0) {
+	int n;
+	do {
+		st.iter++;
+		const int N = st.hi - st.lo;
+		bool e0;
+		const double sigma = exact_sd(N, st.S, st.SS, &e0);
+		const double median = col_median(A, st.lo, N);
+		const int rc = clip_pass(A, st, sigma, e0, median, sl, sh, N0, &n);
+		if (rc != SG_CLS_OK)
+			return rc;
+	} while (n > 0 && (st.hi - st.lo) > 3);
+	return SG_CLS_OK;
+}
+
+/* element i of the Winsorized copy w = [vlo x Lw] ++ A[lo+Lw, hi-Hw) ++ [vhi x Hw] */
+struct SgWins {
+	int Lw, Hw;
+	uint32_t vlo, vhi;
+	uint64_t Sin, SSin;	/* moments of the inner (unclamped) part */
+};
+
+__device__ __forceinline__ uint32_t wins_at(const SgCol &A, const SgRejState &st, const SgWins &w, int i) {
+	const int N = st.hi - st.lo;
+	if (i < w.Lw)
+		return w.vlo;
+	if (i >= N - w.Hw)
+		return w.vhi;
+	return A(st.lo + i);
+}
+
+/* # of w elements < thr (w sorted) */
+__device__ __forceinline__ int wins_count_lt(const SgCol &A, const SgRejState &st, const SgWins &w, double thr) {
+	const int N = st.hi - st.lo;
+	int c = 0;
+	if (w.Lw && (double)w.vlo < thr)
+		c += w.Lw;
+	c += col_count_lt(A, st.lo + w.Lw, st.hi - w.Hw, thr);
+	if (w.Hw && (double)w.vhi < thr)
+		c += w.Hw;
+	(void)N;
+	return c;
+}
+__device__ __forceinline__ int wins_count_le(const SgCol &A, const SgRejState &st, const SgWins &w, double thr) {
+	int c = 0;
+	if (w.Lw && (double)w.vlo <= thr)
+		c += w.Lw;
+	c += col_count_le(A, st.lo + w.Lw, st.hi - w.Hw, thr);
+	if (w.Hw && (double)w.vhi <= thr)
+		c += w.Hw;
+	return c;
+}
+
+/* round_to_WORD(m) decision is ambiguous if m sits within tol of 0, 65535 or a .5 */
+__device__ __forceinline__ bool round_ambiguous(double m, double tol) {
+	if (fabs(m) <= tol || fabs(m - 65535.0) <= tol)
+		return true;
+	if (m <= 0.0 || m > 65535.0)
+		return false;
+	const double t = m + 0.5;
+	return fabs(t - rint(t)) <= tol;
+}
+
+__device__ int reject_winsorized(const SgCol &A, SgRejState &st, double sl, double sh, int N0) {
+	int n;
+	do {
+		st.iter++;
+		const int N = st.hi - st.lo;
+		bool e0;
+		double sigma = exact_sd(N, st.S, st.SS, &e0);
+		double median = col_median(A, st.lo, N);
+		SgWins w = {0, 0, 0, 0, st.S, st.SS};
+		bool sig_e0 = e0;
+		int guard = 0;
+		for (;;) {
+			if (++guard > 4096)
+				return SG_CLS_LITERAL;
+			const double m0 = median - 1.5 * sigma;
+			const double m1 = median + 1.5 * sigma;
+			const double tol = sig_e0 ? 0.0 : SG_BAND * (fabs(median) + 1.5 * sigma + 1.0);
+			/* clamp: w < m0 -> round(m0); else w > m1 -> round(m1) */
+			int clo = wins_count_lt(A, st, w, m0 - tol);
+			if (!sig_e0 && clo != wins_count_le(A, st, w, m0 + tol))
+				return SG_CLS_LITERAL;
+			int chi = N - wins_count_le(A, st, w, m1 + tol);
+			if (!sig_e0 && chi != N - wins_count_lt(A, st, w, m1 - tol))
+				return SG_CLS_LITERAL;
+			if (clo + chi > N)
+				return SG_CLS_LITERAL;
+			if (clo > 0) {
+				if (round_ambiguous(m0, tol + 1e-9 * tol))
+					return SG_CLS_LITERAL;
+				if (clo < w.Lw || clo > N - w.Hw)
+					return SG_CLS_LITERAL;
+				for (int i = w.Lw; i < clo; i++) {
+					const uint32_t v = A(st.lo + i);
+					w.Sin -= v;
+					w.SSin -= (uint64_t)v * v;
+				}
+				w.Lw = clo;
+				w.vlo = sg_round_to_WORD(m0);
+			}
+			if (chi > 0) {
+				if (round_ambiguous(m1, tol + 1e-9 * tol))
+					return SG_CLS_LITERAL;
+				if (chi < w.Hw || chi > N - w.Lw)
+					return SG_CLS_LITERAL;
+				for (int i = w.Hw; i < chi; i++) {
+					const uint32_t v = A(st.hi - 1 - i);
+					w.Sin -= v;
+					w.SSin -= (uint64_t)v * v;
+				}
+				w.Hw = chi;
+				w.vhi = sg_round_to_WORD(m1);
+			}
+			/* median and 1.134 * sd of w (w stays sorted: see DESIGN.md) */
+			{
+				const int lhs = (N - 1) / 2, rhs = N / 2;
+				if (lhs == rhs)
+					median = (double)wins_at(A, st, w, lhs);
+				else
+					median = (double)(wins_at(A, st, w, lhs) + wins_at(A, st, w, rhs)) / 2.0;
+			}
+			const uint64_t Sw = w.Sin + (uint64_t)w.vlo * w.Lw + (uint64_t)w.vhi * w.Hw;
+			const uint64_t SSw = w.SSin + (uint64_t)w.vlo * w.vlo * w.Lw + (uint64_t)w.vhi * w.vhi * w.Hw;
+			const double sigma0 = sigma;
+			const bool e00 = sig_e0;
+			bool we0;
+			sigma = 1.134 * exact_sd(N, Sw, SSw, &we0);
+			sig_e0 = we0;
+			/* while ((fabs(sigma - sigma0) / sigma0) > 0.0005) */
+			if (e00) {
+				if (we0)
+					break;	/* 0/0 = NaN: the loop exits */
+				continue;	/* x/0 = inf > 0.0005 */
+			}
+			const double q = fabs(sigma - sigma0) / sigma0;
+			if (fabs(q - 0.0005) <= 1e-9 * 0.0005 + SG_BAND * (1.0 + q))
+				return SG_CLS_LITERAL;
+			if (!(q > 0.0005))
+				break;
+		}
+		const int rc = clip_pass(A, st, sigma, sig_e0, median, sl, sh, N0, &n);
+		if (rc != SG_CLS_OK)
+			return rc;
+	} while (n > 0 && (st.hi - st.lo) > 3);
+	return SG_CLS_OK;
+}
+
+/* PERCENTILE (:1660-1673, percentile_clipping :1130-1143): pure double arithmetic, the
+ * same expressions are evaluated here, so no band is needed */
+__device__ int reject_percentile(const SgCol &A, SgRejState &st, double plow, double phigh) {
+	const int N = st.hi - st.lo;
+	const double median = col_median(A, st.lo, N);
+	/* low predicate is monotone decreasing in x for median >= 0 */
+	int a = 0, b = N;
+	while (a < b) {
+		int m = (a + b) >> 1;
+		if ((median - (double)A(st.lo + m)) / median > plow)
+			a = m + 1;
+		else
+			b = m;
+	}
+	const int L = a;
+	/* high predicate monotone increasing; evaluated only where low is false */
+	a = L;
+	b = N;
+	while (a < b) {
+		int m = (a + b) >> 1;
+		if (((double)A(st.lo + m) - median) / median > phigh)
+			b = m;
+		else
+			a = m + 1;
+	}
+	const int H = N - a;
+	st.rlo += L;
+	st.rhi += H;
+	int keep_lo, keep_hi;
+	if (L + H <= N - 1) {
+		keep_lo = L;
+		keep_hi = N - H;
+	} else {	/* removals stop at N == 1: the last sample survives */
+		keep_lo = N - 1;
+		keep_hi = N;
+	}
+	for (int i = 0; i < keep_lo; i++) {
+		const uint32_t v = A(st.lo + i);
+		st.S -= v;
+		st.SS -= (uint64_t)v * v;
+	}
+	for (int i = keep_hi; i < N; i++) {
+		const uint32_t v = A(st.lo + i);
+		st.S -= v;
+		st.SS -= (uint64_t)v * v;
+	}
+	st.hi = st.lo + keep_hi;
+	st.lo = st.lo + keep_lo;
+	return SG_CLS_OK;
+}
+
+/* ----------------------------------------------------------------------------------
+ * main sorted kernel
+ * ---------------------------------------------------------------------------------- */
+template <int NREG>
+__global__ void __launch_bounds__(SG_SORT_THREADS)
+k_stack_sorted(SgStackParams p) {
+	extern __shared__ __attribute__((aligned(16))) uint16_t stage[];
+	uint32_t *stage32 = (uint32_t *)stage;
+	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+	const int ntx = (p.W + SG_TILE_W - 1) / SG_TILE_W;
+	const int nrows = p.row_end - p.row_begin;
+	int b = blockIdx.x;
+	const int xt = b % ntx;
+	b /= ntx;
+	const int R = p.row_begin + (b % nrows);
+	const int c = b / nrows;
+	const int x0 = xt * SG_TILE_W;
+	const int N = p.N;
+
+	/* 1. stage the tile: frame f row -> stage[f][0..63] */
+	for (int idx = tid; idx < N * SG_TILE_W; idx += SG_SORT_THREADS) {
+		const int f = idx >> 6, px = idx & 63;
+		const int x = x0 + px;
+		uint16_t v = 0;
+		if (x < p.W)
+			v = sg_gather(p, f, c, R, x);
+		stage[f * SG_STAGE_STRIDE + px] = v;
+	}
+	__syncthreads();
+
+	/* 2. sort column pairs (2q, 2q+1) */
+	for (int q = wave; q < SG_TILE_W / 2; q += SG_SORT_THREADS / 64) {
+		uint32_t v[NREG];
+#pragma unroll
+		for (int r = 0; r < NREG; r++) {
+			const int f = r * 64 + lane;
+			v[r] = (f < N) ? stage32[f * (SG_STAGE_STRIDE / 2) + q] : 0xFFFFFFFFu;
+		}
+		bitonic_sort_packed<NREG>(v, lane);
+		/* write back sorted element e = lane*NREG + r into row e (only e < N) */
+#pragma unroll
+		for (int r = 0; r < NREG; r++) {
+			const int e = lane * NREG + r;
+			if (e < N)
+				stage32[e * (SG_STAGE_STRIDE / 2) + q] = v[r];
+		}
+	}
+	__syncthreads();
+
+	/* 3. per-pixel rejection, one lane per pixel */
+	uint32_t my_rlo = 0, my_rhi = 0;
+	if (tid < SG_TILE_W) {
+		const int x = x0 + tid;
+		if (x < p.W) {
+			SgCol A = {stage + tid};
+			uint16_t value = 0;
+			int cls = SG_CLS_OK;
+			if (p.method == 2) {	/* stack_median: implicit double -> WORD truncation */
+				value = (uint16_t)col_median(A, 0, N);
+			} else {
+				SgRejState st;
+				st.lo = 0;
+				st.hi = N;
+				st.r = 0;
+				st.iter = 0;
+				st.rlo = st.rhi = 0;
+				uint64_t S = 0, SS = 0;
+				for (int e = 0; e < N; e++) {
+					const uint32_t a = A(e);
+					S += a;
+					SS += (uint64_t)a * a;
+				}
+				st.S = S;
+				st.SS = SS;
+				switch (p.rejection) {
+				case 1:
+					cls = reject_percentile(A, st, p.sig0, p.sig1);
+					break;
+				case 2:
+					cls = reject_sigma(A, st, p.sig0, p.sig1, N);
+					break;
+				case 4:
+					cls = reject_winsorized(A, st, p.sig0, p.sig1, N);
+					break;
+				case 0:
+					break;
+				default:	/* SIGMEDIAN, LINEARFIT: literal path */
+					cls = SG_CLS_LITERAL;
+				}
+				if (cls == SG_CLS_OK) {
+					value = sg_round_to_WORD((double)st.S / (double)(st.hi - st.lo));
+					my_rlo = st.rlo;
+					my_rhi = st.rhi;
+				}
+			}
+			const int64_t pix = ((int64_t)c * p.H + R) * p.W + x;
+			if (cls == SG_CLS_OK) {
+				p.out[pix] = value;
+			} else {
+				p.flag_map[pix] = (uint8_t)cls;
+				const unsigned int slot = atomicAdd(p.flag_count, 1u);
+				if (slot < p.flag_cap)
+					p.flag_list[slot] = (unsigned int)pix;
+			}
+		}
+		/* rejection counters: wave reduce, one sharded atomic per tile */
+		if (p.method != 2) {
+			unsigned long long lo = my_rlo, hi = my_rhi;
+			for (int o = 32; o > 0; o >>= 1) {
+				lo += __shfl_down(lo, o, 64);
+				hi += __shfl_down(hi, o, 64);
+			}
+			if (tid == 0 && (lo | hi)) {
+				unsigned long long *sh = p.rej + ((size_t)(blockIdx.x % SG_REJ_SHARDS) * 6 + c * 2);
+				atomicAdd(sh, lo);
+				atomicAdd(sh + 1, hi);
+			}
+		}
+	}
+}
+
+template __global__ void k_stack_sorted<1>(SgStackParams);
+template __global__ void k_stack_sorted<2>(SgStackParams);
+template __global__ void k_stack_sorted<4>(SgStackParams);
+template __global__ void k_stack_sorted<8>(SgStackParams);
+template __global__ void k_stack_sorted<16>(SgStackParams);
+
+/* ----------------------------------------------------------------------------------
+ * streaming reductions: SUM / MAX / MIN / MEAN(NO_REJEC)
+ * ---------------------------------------------------------------------------------- */
+__global__ void __launch_bounds__(256)
+k_stack_reduce(SgStackParams p) {
+	const int x = blockIdx.x * 256 + threadIdx.x;
+	const int R = p.row_begin + blockIdx.y;
+	const int c = blockIdx.z;
+	unsigned int blockmax = 0;
+	if (x < p.W) {
+		const int64_t pix = ((int64_t)c * p.H + R) * p.W + x;
+		if (p.method == 1) {	/* mean, NO_REJEC: gathered (shift, zero fill, norm) */
+			uint32_t acc = 0;
+			for (int f = 0; f < p.N; f++)
+				acc += sg_gather(p, f, c, R, x);
+			p.out[pix] = sg_round_to_WORD((double)acc / (double)p.N);
+		} else {
+			uint32_t acc = (p.method == 4) ? 65535u : 0u;
+			for (int f = 0; f < p.N; f++) {
+				const int sx = p.use_shift ? p.shiftx[f] : 0;
+				const int sy = p.use_shift ? p.shifty[f] : 0;
+				const int nx = x - sx, ny = R - sy;
+				if ((unsigned)nx >= (unsigned)p.W || (unsigned)ny >= (unsigned)p.H)
+					continue;
+				if (nx == 0 && ny == 0)
+					continue;	/* `ii > 0`: source pixel 0 is never used (:307) */
+				const uint32_t v = p.frames[(int64_t)f * p.frame_stride +
+					(int64_t)c * p.plane_stride + (int64_t)ny * p.W + nx];
+				if (p.method == 0)
+					acc += v;
+				else if (p.method == 3)
+					acc = v > acc ? v : acc;
+				else
+					acc = v < acc ? v : acc;
+			}
+			if (p.method == 0) {
+				p.sum_buf[pix] = acc;
+				blockmax = acc;
+			} else {
+				p.out[pix] = (uint16_t)acc;
+			}
+		}
+	}
+	if (p.method == 0) {
+		for (int o = 32; o > 0; o >>= 1) {
+			unsigned int t = (unsigned int)__shfl_down((int)blockmax, o, 64);
+			blockmax = t > blockmax ? t : blockmax;
+		}
+		if ((threadIdx.x & 63) == 0 && blockmax)
+			atomicMax(p.maxim, blockmax);
+	}
+}
+
+/* SUM finalisation: out = round_to_WORD(sum) or round_to_WORD(sum * 65535/maxim) (:328-342) */
+__global__ void __launch_bounds__(256)
+k_sum_finalize(SgStackParams p) {
+	const int x = blockIdx.x * 256 + threadIdx.x;
+	const int R = p.row_begin + blockIdx.y;
+	const int c = blockIdx.z;
+	if (x >= p.W)
+		return;
+	const int64_t pix = ((int64_t)c * p.H + R) * p.W + x;
+	const unsigned int maxim = *p.maxim;
+	const double ratio = (maxim > 65535u) ? 65535.0 / (double)maxim : 1.0;
+	const uint32_t s = p.sum_buf[pix];
+	p.out[pix] = (ratio == 1.0) ? sg_round_to_WORD((double)s) : sg_round_to_WORD((double)s * ratio);
+}
+
+/* ----------------------------------------------------------------------------------
+ * literal path (one thread per queued pixel)
+ * ---------------------------------------------------------------------------------- */
+struct SgChainTables {
+	const int *blk_of_row;		/* [C][H] top-down row -> block index */
+	const int *blk_channel, *blk_start, *blk_end, *blk_first;	/* per block; first block of its thread chunk */
+	int nblocks;
+};
+
+__device__ void shellsort_u16(uint16_t *a, int n) {
+	const int gaps[8] = {701, 301, 132, 57, 23, 10, 4, 1};
+	for (int g = 0; g < 8; g++) {
+		const int gap = gaps[g];
+		for (int i = gap; i < n; i++) {
+			uint16_t t = a[i];
+			int j = i;
+			for (; j >= gap && a[j - gap] > t; j -= gap)
+				a[j] = a[j - gap];
+			a[j] = t;
+		}
+	}
+}
+
+__device__ __forceinline__ double lit_median(const uint16_t *s, int n) {
+	const int lhs = (n - 1) / 2, rhs = n / 2;
+	if (n == 0)
+		return 0.0;
+	if (lhs == rhs)
+		return (double)s[lhs];
+	return (s[lhs] + s[rhs]) / 2.0;
+}
+
+__device__ __forceinline__ double lit_sd(const uint16_t *s, int n) {
+	const double mean = f80_gsl_mean_u16(s, n);
+	const double var = f80_gsl_variance_m_u16(s, n, mean);
+	return sqrt(var * ((double)n / (double)(n - 1)));
+}
+
+__device__ __forceinline__ int lit_sigma_clip(uint16_t px, double sl, double sh, double sigma,
+		double median, uint32_t *rej) {
+	if (median - (double)px > sl * sigma) {
+		rej[0]++;
+		return -1;
+	} else if ((double)px - median > sh * sigma) {
+		rej[1]++;
+		return 1;
+	}
+	return 0;
+}
+
+__device__ __forceinline__ void lit_remove(uint16_t *a, int i, int n) {
+	for (int k = i; k < n - 1; k++)
+		a[k] = a[k + 1];
+}
+
+/* the reference loop of :1656-1794 on `stack` (frame order) with the carried `rejected` */
+__device__ uint16_t literal_pixel(uint16_t *stack, int8_t *rejected, uint16_t *wst, int nb_frames,
+		int type, double sl, double sh, uint32_t *crej, int *first_break) {
+	int N = nb_frames;
+	double median, sigma;
+	int n, j, r = 0, frame, pass = 0;
+	*first_break = 0;
+	switch (type) {
+	case 1:
+		shellsort_u16(stack, N);
+		median = lit_median(stack, N);
+		for (frame = 0; frame < N; frame++) {
+			int v = 0;
+			if ((median - (double)stack[frame]) / median > sl) {
+				crej[0]++;
+				v = -1;
+			} else if (((double)stack[frame] - median) / median > sh) {
+				crej[1]++;
+				v = 1;
+			}
+			rejected[frame] = (int8_t)v;
+		}
+		for (frame = 0, j = 0; frame < N; frame++, j++) {
+			if (rejected[j] != 0 && N > 1) {
+				lit_remove(stack, frame, N);
+				frame--;
+				N--;
+			}
+		}
+		break;
+	case 2:
+	case 4:
+		do {
+			sigma = lit_sd(stack, N);
+			shellsort_u16(stack, N);
+			median = lit_median(stack, N);
+			if (type == 4) {
+				double sigma0;
+				for (int jj = 0; jj < N; jj++)
+					wst[jj] = stack[jj];
+				int guard = 0;
+				do {
+					const double m0 = median - 1.5 * sigma;
+					const double m1 = median + 1.5 * sigma;
+					for (int jj = 0; jj < N; jj++) {
+						if (wst[jj] < m0)
+							wst[jj] = sg_round_to_WORD(m0);
+						else if (wst[jj] > m1)
+							wst[jj] = sg_round_to_WORD(m1);
+					}
+					shellsort_u16(wst, N);
+					median = lit_median(wst, N);
+					sigma0 = sigma;
+					sigma = 1.134 * lit_sd(wst, N);
+				} while ((fabs(sigma - sigma0) / sigma0) > 0.0005 && ++guard < 100000);
+			}
+			n = 0;
+			for (frame = 0; frame < N; frame++) {
+				rejected[frame] = (int8_t)lit_sigma_clip(stack[frame], sl, sh, sigma, median, crej);
+				if (rejected[frame])
+					r++;
+				if (N - r <= 4)
+					break;
+			}
+			if (pass++ == 0 && frame < N - 1)
+				*first_break = 1;
+			for (frame = 0, j = 0; frame < N - n; frame++, j++) {
+				if (rejected[j] != 0) {
+					lit_remove(stack, frame, N - n);
+					n++;
+					frame--;
+				}
+			}
+			N = N - n;
+		} while (n > 0 && N > 3);
+		break;
+	case 3: {
+		int guard = 0;
+		do {
+			sigma = lit_sd(stack, N);
+			shellsort_u16(stack, N);
+			median = lit_median(stack, N);
+			n = 0;
+			for (frame = 0; frame < N; frame++) {
+				if (lit_sigma_clip(stack[frame], sl, sh, sigma, median, crej)) {
+					stack[frame] = sg_round_to_WORD(median);
+					n++;
+				}
+			}
+		} while (n > 0 && N > 3 && ++guard < 100000);
+		break;
+	}
+	case 5:
+		do {
+			shellsort_u16(stack, N);
+			/* gsl_fit_linear(x = 0..N-1, y = stack): b = intercept, a = slope */
+			double m_x = 0, m_y = 0, m_dx2 = 0, m_dxdy = 0;
+			for (int i = 0; i < N; i++) {
+				m_x += ((double)i - m_x) / (i + 1.0);
+				m_y += ((double)stack[i] - m_y) / (i + 1.0);
+			}
+			for (int i = 0; i < N; i++) {
+				const double dx = (double)i - m_x;
+				const double dy = (double)stack[i] - m_y;
+				m_dx2 += (dx * dx - m_dx2) / (i + 1.0);
+				m_dxdy += (dx * dy - m_dxdy) / (i + 1.0);
+			}
+			const double a = m_dxdy / m_dx2;
+			const double b = m_y - m_x * a;
+			sigma = 0.0;
+			for (frame = 0; frame < N; frame++)
+				sigma += (fabs((double)stack[frame] - (a * (double)frame + b)));
+			sigma /= (double)N;
+			n = 0;
+			for (frame = 0; frame < N; frame++) {
+				int v = 0;
+				if (((a * (double)frame + b - (double)stack[frame]) / sigma) > sl) {
+					crej[0]++;
+					v = -1;
+				} else if ((((double)stack[frame] - a * (double)frame - b) / sigma) > sh) {
+					crej[1]++;
+					v = 1;
+				}
+				rejected[frame] = (int8_t)v;
+				if (v != 0)
+					r++;
+				if (N - r <= 4)
+					break;
+			}
+			if (pass++ == 0 && frame < N - 1)
+				*first_break = 1;
+			for (frame = 0, j = 0; frame < N - n; frame++, j++) {
+				if (rejected[j] != 0) {
+					lit_remove(stack, frame, N - n);
+					frame--;
+					n++;
+				}
+			}
+			N = N - n;
+		} while (n > 0 && N > 3);
+		break;
+	default:
+		break;
+	}
+	double sum = 0.0;
+	for (frame = 0; frame < N; ++frame)
+		sum += stack[frame];
+	return sg_round_to_WORD(sum / (double)N);
+}
+
+/* predecessor / successor in the reference's per-OpenMP-thread pixel order:
+ * blocks of the thread's static chunk in order, rows top-down, x ascending */
+__device__ int64_t chain_pred(const SgStackParams &p, const SgChainTables &t, int64_t pix) {
+	const int x = (int)(pix % p.W);
+	const int64_t cr = pix / p.W;
+	const int R = (int)(cr % p.H), c = (int)(cr / p.H);
+	if (x > 0)
+		return pix - 1;
+	const int trow = p.H - 1 - R;
+	const int b = t.blk_of_row[(int64_t)c * p.H + trow];
+	if (trow > t.blk_start[b])
+		return ((int64_t)c * p.H + (R + 1)) * p.W + (p.W - 1);
+	if (b > t.blk_first[b]) {
+		const int pb = b - 1;
+		const int pR = p.H - 1 - t.blk_end[pb];
+		return ((int64_t)t.blk_channel[pb] * p.H + pR) * p.W + (p.W - 1);
+	}
+	return -1;
+}
+
+__device__ int64_t chain_succ(const SgStackParams &p, const SgChainTables &t, int64_t pix) {
+	const int x = (int)(pix % p.W);
+	const int64_t cr = pix / p.W;
+	const int R = (int)(cr % p.H), c = (int)(cr / p.H);
+	if (x < p.W - 1)
+		return pix + 1;
+	const int trow = p.H - 1 - R;
+	const int b = t.blk_of_row[(int64_t)c * p.H + trow];
+	if (trow < t.blk_end[b])
+		return ((int64_t)c * p.H + (R - 1)) * p.W;
+	const int nb = b + 1;
+	if (nb < t.nblocks && t.blk_first[nb] == t.blk_first[b]) {
+		const int nR = p.H - 1 - t.blk_start[nb];
+		return ((int64_t)t.blk_channel[nb] * p.H + nR) * p.W;
+	}
+	return -1;
+}
+
+__device__ __forceinline__ void gather_stack(const SgStackParams &p, int64_t pix, uint16_t *stack) {
+	const int x = (int)(pix % p.W);
+	const int64_t cr = pix / p.W;
+	const int R = (int)(cr % p.H), c = (int)(cr / p.H);
+	for (int f = 0; f < p.N; f++)
+		stack[f] = sg_gather(p, f, c, R, x);
+}
+
+/* phase 1: queued pixels (class LITERAL) replayed with an all-zero incoming rejected[];
+ * a pixel whose first pass breaks early with N > 4 read its predecessor's stale entries
+ * and is promoted to class CHAIN (no output).  phase 2: class CHAIN pixels replay the
+ * chain from the last self-determined predecessor in reference thread order. */
+__global__ void __launch_bounds__(64)
+k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *scratch, int phase) {
+	const unsigned int nthreads = gridDim.x * blockDim.x;
+	const unsigned int gid = blockIdx.x * blockDim.x + threadIdx.x;
+	uint16_t *stack = (uint16_t *)(scratch + (size_t)gid * (((size_t)p.N * 5 + 15) & ~(size_t)15));
+	uint16_t *wst = stack + p.N;
+	int8_t *rejected = (int8_t *)(wst + p.N);
+	if (!count) {	/* 0: take the queue length from the device counter */
+		count = *p.flag_count;
+		if (count > p.flag_cap)
+			count = p.flag_cap;
+	}
+	for (unsigned int i = gid; i < count; i += nthreads) {
+		const int64_t pix = p.flag_list[i];
+		const int cls = p.flag_map[pix];
+		if ((phase == 1) != (cls == SG_CLS_LITERAL))
+			continue;
+		uint32_t crej[2] = {0, 0};
+		int fbrk;
+		for (int k = 0; k < p.N; k++)
+			rejected[k] = 0;
+		if (phase == 2) {
+			/* walk back to the last pixel whose final rejected[] is self-determined */
+			int64_t q = chain_pred(p, t, pix);
+			while (q >= 0 && p.flag_map[q] == SG_CLS_CHAIN)
+				q = chain_pred(p, t, q);
+			int64_t cur;
+			if (q >= 0) {
+				uint32_t dummy[2] = {0, 0};
+				gather_stack(p, q, stack);
+				literal_pixel(stack, rejected, wst, p.N, p.rejection, p.sig0, p.sig1, dummy, &fbrk);
+				cur = chain_succ(p, t, q);
+			} else {
+				/* start of the emulated thread's work: calloc'ed rejected[] */
+				cur = pix;
+				int64_t pr = chain_pred(p, t, cur);
+				while (pr >= 0) {
+					cur = pr;
+					pr = chain_pred(p, t, cur);
+				}
+			}
+			while (cur >= 0 && cur != pix) {
+				uint32_t dummy[2] = {0, 0};
+				gather_stack(p, cur, stack);
+				literal_pixel(stack, rejected, wst, p.N, p.rejection, p.sig0, p.sig1, dummy, &fbrk);
+				cur = chain_succ(p, t, cur);
+			}
+		}
+		gather_stack(p, pix, stack);
+		const uint16_t v = literal_pixel(stack, rejected, wst, p.N, p.rejection, p.sig0, p.sig1, crej, &fbrk);
+		if (phase == 1 && fbrk && p.N > 4) {
+			p.flag_map[pix] = SG_CLS_CHAIN;
+			continue;
+		}
+		p.out[pix] = v;
+		const int c = (int)(pix / ((int64_t)p.W * p.H));
+		unsigned long long *sh = p.rej + ((size_t)(i % SG_REJ_SHARDS) * 6 + c * 2);
+		if (crej[0])
+			atomicAdd(sh, (unsigned long long)crej[0]);
+		if (crej[1])
+			atomicAdd(sh + 1, (unsigned long long)crej[1]);
+	}
+}
+
+/* ----------------------------------------------------------------------------------
+ * synthetic generator (include/sg_synth.h) on the device
+ * ---------------------------------------------------------------------------------- */
+#include "../../include/sg_synth.h"
+
+__global__ void __launch_bounds__(256)
+k_synth_fill(uint16_t *frames, int nframes, int C, int H, int W, int row_begin, int row_end,
+		uint64_t seed, int maxshift) {
+	const int nrows = row_end - row_begin;
+	const int64_t total = (int64_t)nframes * C * nrows * W;
+	for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+			i += (int64_t)gridDim.x * blockDim.x) {
+		const int x = (int)(i % W);
+		int64_t t = i / W;
+		const int rr = (int)(t % nrows);
+		t /= nrows;
+		const int c = (int)(t % C);
+		const int f = (int)(t / C);
+		const int R = row_begin + rr;
+		frames[(((int64_t)f * C + c) * H + R) * W + x] = sg_synth_pixel(seed, f, c, R, x, maxshift);
+	}
+}

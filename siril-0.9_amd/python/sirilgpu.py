@@ -1,0 +1,223 @@
+"""ctypes binding of libsirilgpu.so (include/sirilgpu.h) for tests, bench.py and smoke().
+
+The product is the C ABI + gfx950 kernels; this module only marshals arguments.  It
+refuses to run if the shared library has not been built: there is no Python or CPU
+fallback for any pixel.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libsirilgpu.so")
+
+# enum values (src/stacking/stacking.c:54-56, src/stacking/stacking.h:14-30)
+SUM, MEAN, MEDIAN, MAX, MIN = range(5)
+NO_REJEC, PERCENTILE, SIGMA, SIGMEDIAN, WINSORIZED, LINEARFIT = range(6)
+NO_NORM, ADDITIVE, MULTIPLICATIVE, ADDITIVE_SCALING, MULTIPLICATIVE_SCALING = range(5)
+
+SG_OK = 0
+
+
+class StackDesc(ctypes.Structure):
+    _fields_ = [
+        ("method", ctypes.c_int),
+        ("rejection", ctypes.c_int),
+        ("normalize", ctypes.c_int),
+        ("sig", ctypes.c_double * 2),
+        ("nb_frames", ctypes.c_int),
+        ("width", ctypes.c_int),
+        ("height", ctypes.c_int),
+        ("nb_layers", ctypes.c_int),
+        ("shiftx", ctypes.POINTER(ctypes.c_int)),
+        ("shifty", ctypes.POINTER(ctypes.c_int)),
+        ("offset", ctypes.POINTER(ctypes.c_double)),
+        ("mul", ctypes.POINTER(ctypes.c_double)),
+        ("scale", ctypes.POINTER(ctypes.c_double)),
+        ("max_thread", ctypes.c_int),
+        ("max_number_of_rows", ctypes.c_int),
+        ("reserved", ctypes.c_int * 6),
+    ]
+
+
+class StackStats(ctypes.Structure):
+    _fields_ = [
+        ("kernel_ms", ctypes.c_double),
+        ("total_ms", ctypes.c_double),
+        ("slow_pixels", ctypes.c_uint64),
+        ("chain_pixels", ctypes.c_uint64),
+        ("launches", ctypes.c_uint64),
+        ("main_kernel_blocks", ctypes.c_int),
+        ("reserved", ctypes.c_int),
+    ]
+
+
+class Rect(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_int), ("y", ctypes.c_int), ("w", ctypes.c_int), ("h", ctypes.c_int)]
+
+
+READ_REGION_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                  ctypes.POINTER(ctypes.c_uint16), ctypes.POINTER(Rect))
+CONT_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
+
+# every symbol include/sirilgpu.h declares
+EXPORTS = ["sg_init", "sg_shutdown", "sg_last_error", "sg_stack_u16", "sg_stack_u16_device",
+           "sg_get_last_stats", "sg_register_dft_u16", "sg_register_dft_u16_device",
+           "sg_synth_fill_device"]
+
+_lib = None
+
+
+def load():
+    """Load libsirilgpu.so; raises if it is missing (fail loudly, no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} not built: run `make -C siril-0.9_amd` (no CPU fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    P = ctypes.c_void_p
+    lib.sg_init.argtypes = [ctypes.POINTER(P), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    lib.sg_init.restype = ctypes.c_int
+    lib.sg_shutdown.argtypes = [P]
+    lib.sg_shutdown.restype = None
+    lib.sg_last_error.argtypes = [P]
+    lib.sg_last_error.restype = ctypes.c_char_p
+    lib.sg_stack_u16.argtypes = [P, ctypes.POINTER(StackDesc), READ_REGION_FN, P, CONT_FN, P,
+                                 ctypes.POINTER(ctypes.c_uint16), ctypes.POINTER(ctypes.c_uint64),
+                                 ctypes.POINTER(ctypes.c_uint64)]
+    lib.sg_stack_u16.restype = ctypes.c_int
+    lib.sg_stack_u16_device.argtypes = [P, ctypes.c_int, ctypes.POINTER(StackDesc), P, ctypes.c_int64,
+                                        ctypes.c_int64, P, ctypes.c_int, ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64), P]
+    lib.sg_stack_u16_device.restype = ctypes.c_int
+    lib.sg_get_last_stats.argtypes = [P, ctypes.POINTER(StackStats)]
+    lib.sg_get_last_stats.restype = ctypes.c_int
+    lib.sg_synth_fill_device.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                         ctypes.c_int, P]
+    lib.sg_synth_fill_device.restype = ctypes.c_int
+    for name in ("sg_register_dft_u16",):
+        if hasattr(lib, name):
+            f = getattr(lib, name)
+            f.argtypes = [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, P]
+            f.restype = ctypes.c_int
+    if hasattr(lib, "sg_register_dft_u16_device"):
+        f = lib.sg_register_dft_u16_device
+        f.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, P, P]
+        f.restype = ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def _iptr(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int)) if a is not None else None
+
+
+def _dptr(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)) if a is not None else None
+
+
+def make_desc(method, N, W, H, C, rejection=NO_REJEC, normalize=NO_NORM, sig=(4.0, 3.0),
+              shiftx=None, shifty=None, offset=None, mul=None, scale=None, max_thread=8,
+              max_number_of_rows=0):
+    """Build a StackDesc; returns (desc, keepalive) -- keep the arrays alive during the call."""
+    keep = []
+
+    def arr(a, dt):
+        if a is None:
+            return None
+        a = np.ascontiguousarray(a, dtype=dt)
+        keep.append(a)
+        return a
+
+    sx, sy = arr(shiftx, np.int32), arr(shifty, np.int32)
+    of, mu, sc = arr(offset, np.float64), arr(mul, np.float64), arr(scale, np.float64)
+    d = StackDesc()
+    d.method, d.rejection, d.normalize = method, rejection, normalize
+    d.sig[0], d.sig[1] = float(sig[0]), float(sig[1])
+    d.nb_frames, d.width, d.height, d.nb_layers = N, W, H, C
+    d.shiftx, d.shifty = _iptr(sx), _iptr(sy)
+    d.offset, d.mul, d.scale = _dptr(of), _dptr(mu), _dptr(sc)
+    d.max_thread, d.max_number_of_rows = max_thread, max_number_of_rows
+    return d, keep
+
+
+class Context:
+    def __init__(self, devices=None):
+        self.lib = load()
+        self.ctx = ctypes.c_void_p()
+        if devices:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            rc = self.lib.sg_init(ctypes.byref(self.ctx), len(devices), arr)
+        else:
+            rc = self.lib.sg_init(ctypes.byref(self.ctx), 0, None)
+        if rc != SG_OK:
+            raise RuntimeError(f"sg_init failed ({rc})")
+
+    def close(self):
+        if self.ctx:
+            self.lib.sg_shutdown(self.ctx)
+            self.ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def error(self):
+        return self.lib.sg_last_error(self.ctx).decode()
+
+    def check(self, rc, what):
+        if rc != SG_OK:
+            raise RuntimeError(f"{what} failed ({rc}): {self.error()}")
+
+    def stats(self):
+        st = StackStats()
+        self.check(self.lib.sg_get_last_stats(self.ctx, ctypes.byref(st)), "sg_get_last_stats")
+        return st
+
+    def stack_device(self, desc, d_frames, frame_stride, plane_stride, d_out, row_begin, row_end,
+                     stream=None, dev_index=0):
+        rej = (ctypes.c_uint64 * 6)()
+        maxim = ctypes.c_uint64(0)
+        rc = self.lib.sg_stack_u16_device(self.ctx, dev_index, ctypes.byref(desc), ctypes.c_void_p(d_frames),
+                                          frame_stride, plane_stride, ctypes.c_void_p(d_out), row_begin,
+                                          row_end, rej, ctypes.byref(maxim),
+                                          ctypes.c_void_p(stream) if stream else None)
+        self.check(rc, "sg_stack_u16_device")
+        return np.array(list(rej), dtype=np.uint64).reshape(3, 2), int(maxim.value)
+
+    def stack_host(self, desc, frames, cancel_after=None):
+        """Host-pull path: frames[N][C][H][W] (memory order) served through a
+        seq_opened_read_region-shaped callback returning top-down bands."""
+        N, C, H, W = frames.shape
+        calls = [0]
+
+        def read_region(user, layer, index, buf, area):
+            a = area.contents
+            band = frames[index, layer, H - 1 - (a.y + np.arange(a.h)), a.x:a.x + a.w]
+            dst = np.ctypeslib.as_array(buf, shape=(a.h * a.w,))
+            dst[:] = np.ascontiguousarray(band).reshape(-1)
+            return 0
+
+        def cont(user):
+            calls[0] += 1
+            return 0 if (cancel_after is not None and calls[0] > cancel_after) else 1
+
+        rf, cf = READ_REGION_FN(read_region), CONT_FN(cont)
+        out = np.zeros((C, H, W), dtype=np.uint16)
+        rej = (ctypes.c_uint64 * 6)()
+        maxim = ctypes.c_uint64(0)
+        rc = self.lib.sg_stack_u16(self.ctx, ctypes.byref(desc), rf, None, cf, None,
+                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)), rej,
+                                   ctypes.byref(maxim))
+        return rc, out, np.array(list(rej), dtype=np.uint64).reshape(3, 2), int(maxim.value)
+
+    def synth_fill(self, d_frames, nframes, C, H, W, row_begin, row_end, seed, maxshift, dev_index=0):
+        rc = self.lib.sg_synth_fill_device(self.ctx, dev_index, ctypes.c_void_p(d_frames), nframes, C, H, W,
+                                           row_begin, row_end, seed, maxshift, None)
+        self.check(rc, "sg_synth_fill_device")

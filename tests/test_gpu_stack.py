@@ -1,0 +1,143 @@
+"""GPU parity of every stacker against the CPU oracle, through the C ABI.
+
+Bit-exact for every output pixel and the rejection counters (integer/median paths and the
+mean/sigma-clip paths alike: the kernels replay the reference's decisions exactly).
+"""
+import numpy as np
+import pytest
+
+import oracle_lib as orc
+import sirilgpu as sg
+
+pytestmark = pytest.mark.gpu
+
+REJ = {sg.PERCENTILE: (0.2, 0.1), sg.SIGMA: (4.0, 3.0), sg.SIGMEDIAN: (4.0, 3.0),
+       sg.WINSORIZED: (4.0, 3.0), sg.LINEARFIT: (5.0, 5.0), sg.NO_REJEC: (4.0, 3.0)}
+
+
+def gpu_stack(ctx, frames, method, rejection=sg.NO_REJEC, sig=(4.0, 3.0), shiftx=None, shifty=None,
+              normalize=sg.NO_NORM, offset=None, mul=None, scale=None, max_thread=8, max_rows=0):
+    N, C, H, W = frames.shape
+    desc, keep = sg.make_desc(method, N, W, H, C, rejection=rejection, normalize=normalize, sig=sig,
+                              shiftx=shiftx, shifty=shifty, offset=offset, mul=mul, scale=scale,
+                              max_thread=max_thread, max_number_of_rows=max_rows or H)
+    rc, out, rej, maxim = ctx.stack_host(desc, np.ascontiguousarray(frames))
+    assert rc == 0, ctx.error()
+    return out, rej, maxim
+
+
+def assert_same(a, b, what):
+    if not np.array_equal(a, b):
+        idx = np.argwhere(a != b)
+        raise AssertionError(f"{what}: {len(idx)} pixels differ, first {idx[:5].tolist()} "
+                             f"gpu={a[tuple(idx[0])]} ref={b[tuple(idx[0])]}")
+
+
+@pytest.mark.parametrize("C", [1, 3])
+@pytest.mark.parametrize("rejection", [sg.NO_REJEC, sg.PERCENTILE, sg.SIGMA, sg.WINSORIZED,
+                                       sg.SIGMEDIAN, sg.LINEARFIT])
+def test_rejection_parity(gpu_ctx, rejection, C):
+    N, H, W = 24, 40, 150
+    frames = orc.synth(N, C, H, W, seed=11 + C, maxshift=8)
+    sx, sy = orc.synth_shifts(N, seed=11 + C, maxshift=8)
+    sig = REJ[rejection]
+    rc, ref, rej_ref = orc.stack_rejection(frames, rejection, sig=sig, shiftx=sx, shifty=sy, max_thread=1)
+    assert rc == 0
+    out, rej, _ = gpu_stack(gpu_ctx, frames, sg.MEAN, rejection, sig, sx, sy, max_thread=1)
+    assert_same(out, ref, f"rejection {rejection}")
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+
+
+@pytest.mark.parametrize("N", [2, 3, 4, 5, 6, 7, 8, 9, 12])
+@pytest.mark.parametrize("rejection", [sg.SIGMA, sg.WINSORIZED, sg.LINEARFIT])
+def test_small_n_stale_state(gpu_ctx, N, rejection):
+    """early `break` (N - r <= 4) and stale rejected[] carried across pixels (SURVEY a3 iii)"""
+    H, W = 24, 70
+    rng = np.random.default_rng(100 + N)
+    frames = rng.integers(900, 1100, size=(N, 1, H, W)).astype(np.uint16)
+    # outliers on both sides so rejections (and early breaks) happen often
+    mask = rng.random(frames.shape)
+    frames[mask < 0.08] = 65535
+    frames[mask > 0.94] = 0
+    sig = (1.0, 1.0) if rejection != sg.LINEARFIT else (1.0, 1.0)
+    for max_thread in (1, 3):
+        rc, ref, rej_ref = orc.stack_rejection(frames, rejection, sig=sig, max_thread=max_thread)
+        assert rc == 0
+        out, rej, _ = gpu_stack(gpu_ctx, frames, sg.MEAN, rejection, sig, max_thread=max_thread)
+        assert_same(out, ref, f"N={N} rej={rejection} thr={max_thread}")
+        assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+
+
+@pytest.mark.parametrize("C", [1, 3])
+def test_median_parity(gpu_ctx, C):
+    N, H, W = 20, 33, 130   # even N: (a+b)/2 truncation
+    frames = orc.synth(N, C, H, W, seed=5, maxshift=8)
+    rc, ref = orc.stack_median(frames)
+    out, _, _ = gpu_stack(gpu_ctx, frames, sg.MEDIAN)
+    assert_same(out, ref, "median")
+
+
+@pytest.mark.parametrize("method", [sg.SUM, sg.MAX, sg.MIN])
+@pytest.mark.parametrize("C", [1, 3])
+def test_sum_max_min_parity(gpu_ctx, method, C):
+    N, H, W = 16, 48, 200
+    frames = orc.synth(N, C, H, W, seed=7, maxshift=16)
+    sx, sy = orc.synth_shifts(N, seed=7, maxshift=16)
+    if method == sg.SUM:
+        rc, ref, mref = orc.stack_sum(frames, sx, sy)
+    else:
+        rc, ref = orc.stack_maxmin(frames, method == sg.MAX, sx, sy)
+    out, _, maxim = gpu_stack(gpu_ctx, frames, method, shiftx=sx, shifty=sy)
+    assert_same(out, ref, f"method {method}")
+    assert out[:, 0, 0].tolist() == ref[:, 0, 0].tolist()
+    if method == sg.SUM:
+        assert maxim == mref
+
+
+def test_sum_no_scaling(gpu_ctx):
+    """maxim <= 65535: ratio == 1.0 branch (:328-330); pixel 0 stays 0 (:307)"""
+    frames = np.full((3, 1, 8, 9), 100, dtype=np.uint16)
+    rc, ref, mref = orc.stack_sum(frames)
+    out, _, maxim = gpu_stack(gpu_ctx, frames, sg.SUM)
+    assert_same(out, ref, "sum small")
+    assert out[0, 0, 0] == 0 and maxim == mref == 300
+
+
+@pytest.mark.parametrize("normalize", [sg.ADDITIVE, sg.MULTIPLICATIVE, sg.ADDITIVE_SCALING,
+                                       sg.MULTIPLICATIVE_SCALING])
+@pytest.mark.parametrize("method", [sg.MEDIAN, sg.MEAN])
+def test_normalization(gpu_ctx, normalize, method):
+    N, H, W = 12, 20, 90
+    frames = orc.synth(N, 1, H, W, seed=21, maxshift=4)
+    rng = np.random.default_rng(3)
+    loc = 1000 + rng.random(N) * 50
+    scl = 30 + rng.random(N) * 5
+    off, mul, scale = orc.compute_normalization(normalize, loc, scl, ref_image=0)
+    sx, sy = orc.synth_shifts(N, seed=21, maxshift=4)
+    if method == sg.MEDIAN:
+        rc, ref = orc.stack_median(frames, normalize, off, mul, scale)
+        out, _, _ = gpu_stack(gpu_ctx, frames, sg.MEDIAN, normalize=normalize, offset=off, mul=mul, scale=scale)
+    else:
+        rc, ref, rr = orc.stack_rejection(frames, sg.SIGMA, shiftx=sx, shifty=sy, normalize=normalize,
+                                          offset=off, mul=mul, scale=scale, max_thread=1)
+        out, rej, _ = gpu_stack(gpu_ctx, frames, sg.MEAN, sg.SIGMA, shiftx=sx, shifty=sy, normalize=normalize,
+                                offset=off, mul=mul, scale=scale, max_thread=1)
+        assert np.array_equal(rej, rr)
+    assert_same(out, ref, f"norm {normalize} method {method}")
+
+
+def test_constant_and_knife_edges(gpu_ctx):
+    """sigma == 0 stacks (Winsorized 0/0 exit) and integer patterns that put thresholds
+    exactly on sample values, forcing the literal (fp80) path"""
+    N, H, W = 16, 8, 64
+    frames = np.full((N, 1, H, W), 1234, dtype=np.uint16)
+    pats = [[1000] * 8 + [1010] * 8, [0] * 15 + [65535], list(range(1000, 1016)),
+            [5] * 4 + [9] * 4 + [13] * 8]
+    for i, p in enumerate(pats):
+        frames[:, 0, i, :] = np.array(p, dtype=np.uint16)[:, None]
+    for rej in (sg.SIGMA, sg.WINSORIZED, sg.PERCENTILE, sg.SIGMEDIAN, sg.LINEARFIT):
+        for sig in ((4.0, 3.0), (1.0, 1.0), (0.5, 0.5), (2.0, 1.5)):
+            rc, ref, rr = orc.stack_rejection(frames, rej, sig=sig, max_thread=2)
+            out, rj, _ = gpu_stack(gpu_ctx, frames, sg.MEAN, rej, sig, max_thread=2)
+            assert_same(out, ref, f"rej {rej} sig {sig}")
+            assert np.array_equal(rj, rr)
