@@ -37,7 +37,9 @@ def parse():
     ap.add_argument("--height", type=int, default=4096)
     ap.add_argument("--rejection", default="sigma")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rows", type=int, default=8, help="rows of the CPU baseline sample")
+    ap.add_argument("--cpu-rows", type=int, default=1024, help="rows of the CPU baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="OpenMP threads of the CPU baseline (the GPU box's CPU share is 16)")
     return ap.parse_args()
 
 
@@ -46,20 +48,27 @@ def cpu_baseline(args, N, W):
     partition and OpenMP schedule) on a bounded sample of the same workload."""
     import numpy as np
     import oracle_lib as orc
-    rows = args.cpu_rows
-    threads = os.cpu_count() or 1
-    threads = min(threads, 256)
-    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
-    frames = orc.synth(N, 1, rows, W, seed=0x5151, maxshift=0)
-    sx = np.zeros(N, dtype=np.int32)
+    rows = min(args.cpu_rows, args.height)
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    lib = orc.load()
+    try:
+        import ctypes
+        ctypes.CDLL("libgomp.so.1").omp_set_num_threads(threads)
+    except OSError:
+        pass
+    # the same synthetic scene and registration shifts as the GPU run, rows [0, rows)
+    frames = orc.synth(N, 1, rows, W, seed=0x5151, maxshift=16)
+    sx, sy = orc.synth_shifts(N, seed=0x5151, maxshift=16)
     t0 = time.perf_counter()
-    rc, out, rej = orc.stack_rejection(frames, 2, sig=(4.0, 3.0), shiftx=sx, shifty=sx,
+    rc, out, rej = orc.stack_rejection(frames, 2, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
                                        max_thread=threads, max_number_of_rows=rows)
     dt = time.perf_counter() - t0
+    del frames
     frac = rows / args.height
     return {"value": round(N * frac / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{N} frames x {rows} rows x {W} cols (SIGMA 4/3), scaled by {rows}/{args.height}",
-            "seconds": round(dt, 3)}
+            "sample": f"oracle stack_mean_with_rejection SIGMA(4,3), {N} frames x {rows} rows x {W} "
+                      f"cols ({threads} OpenMP threads); frames/s scaled by {rows}/{args.height} rows",
+            "seconds": round(dt, 3), "rc": rc}
 
 
 def main():
@@ -91,7 +100,6 @@ def main():
     import ctypes
     sx = (ctypes.c_int * N)()
     sy = (ctypes.c_int * N)()
-    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "liboracle.so")) if False else None
     # the synthetic shifts are a pure function; recompute them with the same mixer
     import numpy as np
 

@@ -31,57 +31,7 @@ __global__ void k_stack_literal(SgStackParams p, SgChainTables t, unsigned int c
 __global__ void k_synth_fill(uint16_t *frames, int nframes, int C, int H, int W, int row_begin,
 		int row_end, uint64_t seed, int maxshift);
 
-#define SG_LIT_THREADS 16384
-
-struct SgBuf {
-	void *p = nullptr;
-	size_t size = 0;
-};
-
-struct SgDevice {
-	int id = 0;
-	hipStream_t stream = nullptr;
-	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-	SgBuf flag_list, flag_map, flag_count, rej, sum_buf, maxim, shifts, norm, tables, scratch, frames, out;
-	uint16_t *pinned[2] = {nullptr, nullptr};
-	size_t pinned_size = 0;
-};
-
-struct sg_ctx {
-	std::vector<SgDevice> dev;
-	std::string err;
-	sg_stack_stats stats;
-};
-
-static int set_err(sg_ctx *ctx, int code, const char *fmt, const char *a = "", long b = 0) {
-	char buf[512];
-	snprintf(buf, sizeof buf, fmt, a, b);
-	if (ctx)
-		ctx->err = buf;
-	return code;
-}
-
-#define HIPCHK(call)                                                                       \
-	do {                                                                               \
-		hipError_t _e = (call);                                                    \
-		if (_e != hipSuccess)                                                      \
-			return set_err(ctx, SG_ERR_DEVICE, "HIP error %s at line %ld",     \
-					hipGetErrorString(_e), (long)__LINE__);            \
-	} while (0)
-
-static hipError_t ensure(SgBuf &b, size_t bytes) {
-	if (b.size >= bytes && b.p)
-		return hipSuccess;
-	if (b.p)
-		(void)hipFree(b.p);
-	b.p = nullptr;
-	b.size = 0;
-	size_t sz = bytes ? bytes : 16;
-	hipError_t e = hipMalloc(&b.p, sz);
-	if (e == hipSuccess)
-		b.size = sz;
-	return e;
-}
+#include "sg_ctx.hpp"
 
 extern "C" int sg_init(sg_ctx **out, int ndev, const int *devs) {
 	if (!out)
@@ -120,7 +70,8 @@ extern "C" void sg_shutdown(sg_ctx *ctx) {
 		(void)hipSetDevice(d.id);
 		(void)hipStreamSynchronize(d.stream);
 		SgBuf *bufs[] = {&d.flag_list, &d.flag_map, &d.flag_count, &d.rej, &d.sum_buf, &d.maxim,
-			&d.shifts, &d.norm, &d.tables, &d.scratch, &d.frames, &d.out};
+			&d.shifts, &d.norm, &d.tables, &d.scratch, &d.frames, &d.out, &d.reg_sel, &d.reg_spec,
+			&d.reg_work, &d.reg_tw, &d.reg_best, &d.reg_qbuf, &d.reg_qacc};
 		for (SgBuf *b : bufs)
 			if (b->p)
 				(void)hipFree(b->p);

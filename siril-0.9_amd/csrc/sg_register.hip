@@ -1,0 +1,572 @@
+/*
+ * sg_register.hip - gfx950 DFT registration (replaces register_shift_dft,
+ * src/registration/registration.c:182-400) and the planetary quality estimate it records
+ * (QualityEstimate, src/algos/quality.c:46-349; normalizeQualityData registration.c:163-176).
+ *
+ * Per frame the reference computes, with FFTW in complex double,
+ *     c = IFFT2( FFT2(ref) * conj(FFT2(img)) )      (unnormalised, FFTW_BACKWARD)
+ * and takes the first strict maximum of creal(c) in row-major order (:337-351).  Here:
+ *   - frames go through the 2-D FFT two at a time, packed as a + i b (both are real), and
+ *     their spectra are separated with F_a(k) = (Z(k) + conj Z(-k))/2,
+ *     F_b(k) = (Z(k) - conj Z(-k))/2i;
+ *   - the two cross-power spectra are packed back as P = R conj F_a + i R conj F_b, whose
+ *     inverse is c_a + i c_b (both correlations are real): one forward and one inverse
+ *     complex 2-D FFT per PAIR of frames;
+ *   - FFTs are radix-2 in LDS in double precision (rows: one workgroup per row; columns:
+ *     one workgroup per strip of CW columns), twiddles from a host table;
+ *   - the inverse row pass fuses the per-row arg-max (first index on ties), a tiny kernel
+ *     reduces the rows in order.
+ * Only the arg-max leaves the device, so results equal the reference wherever the top two
+ * correlation values are separated by more than the FFT rounding of either side (the exact
+ * correlations are integers; FFTW's own choice between exactly tied integers is not
+ * specified — "parity unpinned" there).  S must be a power of two.
+ */
+#include "sg_common.hpp"
+#include "sg_ctx.hpp"
+#include <math.h>
+#include <string.h>
+#include <vector>
+
+typedef double2 sg_c64;
+
+__device__ __forceinline__ int sg_bitrev(int x, int logn) {
+	return (int)(__brev((unsigned)x) >> (32 - logn));
+}
+
+/* nb independent length-n FFTs held in LDS (batch b at buf + b*bstride), input already in
+ * bit-reversed order, output natural order.  tw[k] = exp(-2 pi i k / n), k < n/2. */
+__device__ void sg_lds_fft(sg_c64 *buf, int n, int logn, int nb, int bstride, const sg_c64 *__restrict__ tw,
+		bool inverse) {
+	const int half = n >> 1;
+	for (int h = 1; h < n; h <<= 1) {
+		__syncthreads();
+		const int tstep = n / (2 * h);
+		for (int t = threadIdx.x; t < nb * half; t += blockDim.x) {
+			const int b = t >> (logn - 1);
+			const int bi = t & (half - 1);
+			const int k = bi & (h - 1);
+			const int i0 = ((bi - k) << 1) + k;
+			sg_c64 *x = buf + (size_t)b * bstride;
+			sg_c64 w = tw[k * tstep];
+			if (inverse)
+				w.y = -w.y;
+			const sg_c64 u = x[i0], v = x[i0 + h];
+			const double vr = v.x * w.x - v.y * w.y;
+			const double vi = v.x * w.y + v.y * w.x;
+			x[i0] = make_double2(u.x + vr, u.y + vi);
+			x[i0 + h] = make_double2(u.x - vr, u.y - vi);
+		}
+	}
+	__syncthreads();
+}
+
+/* row pass of the forward transform of a + i b (b = -1: zero imaginary part) */
+__global__ void __launch_bounds__(256)
+k_reg_rows_fwd(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const int *__restrict__ fb,
+		int S, int logS, const sg_c64 *__restrict__ tw, sg_c64 *__restrict__ work) {
+	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+	sg_c64 *buf = (sg_c64 *)smem;
+	const int row = blockIdx.x, pair = blockIdx.y;
+	const size_t plane = (size_t)S * S;
+	const uint16_t *pa = sel + (size_t)fa[pair] * plane + (size_t)row * S;
+	const int b = fb[pair];
+	const uint16_t *pb = b >= 0 ? sel + (size_t)b * plane + (size_t)row * S : nullptr;
+	for (int j = threadIdx.x; j < S; j += blockDim.x)
+		buf[sg_bitrev(j, logS)] = make_double2((double)pa[j], pb ? (double)pb[j] : 0.0);
+	sg_lds_fft(buf, S, logS, 1, S, tw, false);
+	sg_c64 *out = work + (size_t)pair * plane + (size_t)row * S;
+	for (int j = threadIdx.x; j < S; j += blockDim.x)
+		out[j] = buf[j];
+}
+
+/* column pass (forward or inverse) over strips of CW adjacent columns */
+__global__ void __launch_bounds__(512)
+k_reg_cols(sg_c64 *__restrict__ work, int S, int logS, int CW, const sg_c64 *__restrict__ tw, int inverse) {
+	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+	sg_c64 *buf = (sg_c64 *)smem;
+	const int x0 = blockIdx.x * CW, pair = blockIdx.y;
+	const int bstride = S + 1;
+	sg_c64 *base = work + (size_t)pair * S * S + x0;
+	for (int idx = threadIdx.x; idx < S * CW; idx += blockDim.x) {
+		const int r = idx / CW, c = idx - r * CW;
+		buf[c * bstride + sg_bitrev(r, logS)] = base[(size_t)r * S + c];
+	}
+	sg_lds_fft(buf, S, logS, CW, bstride, tw, inverse != 0);
+	for (int idx = threadIdx.x; idx < S * CW; idx += blockDim.x) {
+		const int r = idx / CW, c = idx - r * CW;
+		base[(size_t)r * S + c] = buf[c * bstride + r];
+	}
+}
+
+/* separate the packed spectra and form the packed cross-power spectrum, in place:
+ * each (k, -k) pair is handled by the thread of the smaller linear index */
+__global__ void __launch_bounds__(256)
+k_reg_xpower(sg_c64 *__restrict__ work, const sg_c64 *__restrict__ spec, int S) {
+	const size_t plane = (size_t)S * S;
+	sg_c64 *Z = work + (size_t)blockIdx.y * plane;
+	for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < plane; i += (size_t)gridDim.x * blockDim.x) {
+		const int ky = (int)(i / S), kx = (int)(i - (size_t)ky * S);
+		const int my = (S - ky) & (S - 1), mx = (S - kx) & (S - 1);
+		const size_t m = (size_t)my * S + mx;
+		if (m < i)
+			continue;
+		const sg_c64 zk = Z[i], zm = Z[m];
+		/* F_a(k) = (Z(k) + conj Z(-k))/2, F_b(k) = (Z(k) - conj Z(-k))/(2i) */
+		const double ar = 0.5 * (zk.x + zm.x), ai = 0.5 * (zk.y - zm.y);
+		const double br = 0.5 * (zk.y + zm.y), bi = -0.5 * (zk.x - zm.x);
+		const sg_c64 rk = spec[i], rm = spec[m];
+		/* P(k) = R(k) conj F_a(k) + i R(k) conj F_b(k) */
+		{
+			const double pr = rk.x * ar + rk.y * ai, pi = rk.y * ar - rk.x * ai;	/* R conj(Fa) */
+			const double qr = rk.x * br + rk.y * bi, qi = rk.y * br - rk.x * bi;	/* R conj(Fb) */
+			Z[i] = make_double2(pr - qi, pi + qr);
+		}
+		if (m != i) {
+			/* F_a(-k) = conj F_a(k), F_b(-k) = conj F_b(k): P(-k) = R(-k) F_a + i R(-k) F_b */
+			const double pr = rm.x * ar - rm.y * ai, pi = rm.x * ai + rm.y * ar;
+			const double qr = rm.x * br - rm.y * bi, qi = rm.x * bi + rm.y * br;
+			Z[m] = make_double2(pr - qi, pi + qr);
+		}
+	}
+}
+
+/* better (value, index): larger value, ties -> lower index (first strict max, :337-343) */
+__device__ __forceinline__ void sg_argmax_merge(double &v, int &i, double v2, int i2) {
+	if (v2 > v || (v2 == v && i2 < i)) {
+		v = v2;
+		i = i2;
+	}
+}
+
+struct SgBest {
+	double va, vb;
+	int ia, ib;
+};
+
+/* inverse row pass fused with the per-row arg-max of the real (frame a) and imaginary
+ * (frame b) parts */
+__global__ void __launch_bounds__(256)
+k_reg_rows_inv_argmax(const sg_c64 *__restrict__ work, int S, int logS, const sg_c64 *__restrict__ tw,
+		SgBest *__restrict__ best) {
+	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+	sg_c64 *buf = (sg_c64 *)smem;
+	__shared__ double rv[2][8];
+	__shared__ int ri[2][8];
+	const int row = blockIdx.x, pair = blockIdx.y;
+	const sg_c64 *in = work + (size_t)pair * S * S + (size_t)row * S;
+	for (int j = threadIdx.x; j < S; j += blockDim.x)
+		buf[sg_bitrev(j, logS)] = in[j];
+	sg_lds_fft(buf, S, logS, 1, S, tw, true);
+	double va = -INFINITY, vb = -INFINITY;
+	int ia = 0x7fffffff, ib = 0x7fffffff;
+	for (int j = threadIdx.x; j < S; j += blockDim.x) {
+		const sg_c64 c = buf[j];
+		const int idx = row * S + j;
+		sg_argmax_merge(va, ia, c.x, idx);
+		sg_argmax_merge(vb, ib, c.y, idx);
+	}
+	for (int o = 32; o > 0; o >>= 1) {
+		const double va2 = __shfl_down(va, o, 64), vb2 = __shfl_down(vb, o, 64);
+		const int ia2 = __shfl_down(ia, o, 64), ib2 = __shfl_down(ib, o, 64);
+		sg_argmax_merge(va, ia, va2, ia2);
+		sg_argmax_merge(vb, ib, vb2, ib2);
+	}
+	const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+	if ((threadIdx.x & 63) == 0) {
+		rv[0][wave] = va;
+		ri[0][wave] = ia;
+		rv[1][wave] = vb;
+		ri[1][wave] = ib;
+	}
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		for (int w = 1; w < nw; w++) {
+			sg_argmax_merge(va, ia, rv[0][w], ri[0][w]);
+			sg_argmax_merge(vb, ib, rv[1][w], ri[1][w]);
+		}
+		SgBest r;
+		r.va = va;
+		r.ia = ia;
+		r.vb = vb;
+		r.ib = ib;
+		best[(size_t)pair * S + row] = r;
+	}
+}
+
+/* per pair: reduce the row maxima and convert to (shiftx, shifty) (:344-351) */
+__global__ void __launch_bounds__(256)
+k_reg_final(const SgBest *__restrict__ best, int S, int *__restrict__ out /* [pair][4] */) {
+	__shared__ double rv[2][4];
+	__shared__ int ri[2][4];
+	const int pair = blockIdx.x;
+	double va = -INFINITY, vb = -INFINITY;
+	int ia = 0x7fffffff, ib = 0x7fffffff;
+	for (int r = threadIdx.x; r < S; r += blockDim.x) {
+		const SgBest b = best[(size_t)pair * S + r];
+		sg_argmax_merge(va, ia, b.va, b.ia);
+		sg_argmax_merge(vb, ib, b.vb, b.ib);
+	}
+	for (int o = 32; o > 0; o >>= 1) {
+		const double va2 = __shfl_down(va, o, 64), vb2 = __shfl_down(vb, o, 64);
+		const int ia2 = __shfl_down(ia, o, 64), ib2 = __shfl_down(ib, o, 64);
+		sg_argmax_merge(va, ia, va2, ia2);
+		sg_argmax_merge(vb, ib, vb2, ib2);
+	}
+	const int wave = threadIdx.x >> 6;
+	if ((threadIdx.x & 63) == 0) {
+		rv[0][wave] = va;
+		ri[0][wave] = ia;
+		rv[1][wave] = vb;
+		ri[1][wave] = ib;
+	}
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		for (int w = 1; w < (int)(blockDim.x >> 6); w++) {
+			sg_argmax_merge(va, ia, rv[0][w], ri[0][w]);
+			sg_argmax_merge(vb, ib, rv[1][w], ri[1][w]);
+		}
+		const int idx[2] = {ia, ib};
+		for (int k = 0; k < 2; k++) {
+			int sy = idx[k] / S, sx = idx[k] % S;
+			if (sy > S / 2)
+				sy -= S;
+			if (sx > S / 2)
+				sx -= S;
+			out[pair * 4 + 2 * k] = sx;
+			out[pair * 4 + 2 * k + 1] = sy;
+		}
+	}
+}
+
+/* ---------------------------------------------------------------------------------------
+ * QualityEstimate (src/algos/quality.c).  Only subsample 3 contributes to the result:
+ * dval += q * ((QSUBSAMPLE_MIN * QSUBSAMPLE_MIN) / (subsample * subsample)) uses integer
+ * division (:211), so the factor is 1 for subsample 3 and 0 for 4 and 5.
+ * ------------------------------------------------------------------------------------- */
+#define SG_Q_THRESHOLD (40 << 8)
+
+/* SubSample (:223-234) of one 3x3 sample row, plus the running max of the middle rows
+ * (the maxp[] loop :119-133 reduces to max over 0 < v < 65530) */
+__global__ void __launch_bounds__(256)
+k_quality_sub(const uint16_t *__restrict__ sel, const int *__restrict__ qframes, int S, int xs, int ys,
+		uint16_t *__restrict__ qbuf, unsigned int *__restrict__ qmax) {
+	const int j = blockIdx.x, q = blockIdx.y;
+	const uint16_t *img = sel + (size_t)qframes[q] * S * S + (size_t)(j * 3) * S;
+	uint16_t *dst = qbuf + (size_t)q * xs * ys + (size_t)j * xs;
+	unsigned int m = 0;
+	const bool middle = (j >= 1 && j <= ys - 2);
+	for (int i = threadIdx.x; i < xs; i += blockDim.x) {
+		const uint16_t *p = img + i * 3;
+		int v = 0;
+		for (int y = 0; y < 3; y++)
+			v += (int)p[y * S] + (int)p[y * S + 1] + (int)p[y * S + 2];
+		v /= 9;
+		dst[i] = (uint16_t)v;
+		if (middle && v > 0 && v < 65530 && (unsigned)v > m)
+			m = (unsigned)v;
+	}
+	for (int o = 32; o > 0; o >>= 1) {
+		const unsigned int t = (unsigned int)__shfl_down((int)m, o, 64);
+		m = t > m ? t : m;
+	}
+	if ((threadIdx.x & 63) == 0 && m)
+		atomicMax(qmax + q, m);
+}
+
+/* stretched sample (:139-148): v * (60000 / max), truncated, clamped at 65535 */
+__device__ __forceinline__ int sg_q_stretch(const uint16_t *b, int idx, double mult, bool stretch) {
+	unsigned int v = b[idx];
+	if (stretch) {
+		v = (unsigned int)((double)v * mult);
+		if (v > 65535u)
+			v = 65535u;
+	}
+	return (int)v;
+}
+
+/* _smooth_image_16 (:324-349) + Gradient (:236-321): threshold map dilated 3x3 inside the
+ * 10 % margins, gradient energy over mapped pixels; exact integer sums */
+__global__ void __launch_bounds__(256)
+k_quality_grad(const uint16_t *__restrict__ qbuf, int xs, int ys, const unsigned int *__restrict__ qmax,
+		unsigned long long *__restrict__ acc /* [q][3]: val, pixels, thresholded */) {
+	__shared__ unsigned long long sv[4], sp[4], sc[4];
+	const int q = blockIdx.z;
+	const uint16_t *b = qbuf + (size_t)q * xs * ys;
+	const unsigned int mx = qmax[q];
+	const bool stretch = mx > 0;
+	const double mult = stretch ? (double)60000 / (double)mx : 1.0;
+	const int yb = (int)((double)ys * 0.1) + 1;
+	const int xb = (int)((double)xs * 0.1) + 1;
+	const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+	const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+	unsigned long long val = 0, pix = 0, cnt = 0;
+	if (x >= xb && x < xs - xb && y >= yb && y < ys - yb) {
+		/* smoothed values on the 3x3 neighbourhood of (x, y) */
+		int sm[3][3];
+		for (int dy = -1; dy <= 1; dy++)
+			for (int dx = -1; dx <= 1; dx++) {
+				const int qx = x + dx, qy = y + dy;
+				int v = 0;
+				if (qx >= 1 && qx <= xs - 2 && qy >= 1 && qy <= ys - 2) {
+					unsigned int s = 0;
+					for (int ey = -1; ey <= 1; ey++)
+						for (int ex = -1; ex <= 1; ex++)
+							s += (unsigned int)sg_q_stretch(b, (qy + ey) * xs + qx + ex, mult, stretch);
+					v = (int)(s / 9);
+				}
+				sm[dy + 1][dx + 1] = v;
+			}
+		if (sm[1][1] >= SG_Q_THRESHOLD)
+			cnt = 1;
+		bool mapped = false;
+		for (int dy = -1; dy <= 1; dy++)
+			for (int dx = -1; dx <= 1; dx++) {
+				const int qx = x + dx, qy = y + dy;
+				if (qx >= xb && qx < xs - xb && qy >= yb && qy < ys - yb &&
+						sm[dy + 1][dx + 1] >= SG_Q_THRESHOLD)
+					mapped = true;
+			}
+		if (mapped) {
+			const long long d1 = sm[1][1] - sm[1][2];
+			const long long d2 = sm[1][1] - sm[2][1];
+			val = (unsigned long long)(d1 * d1 + d2 * d2);
+			pix = 1;
+		}
+	}
+	for (int o = 32; o > 0; o >>= 1) {
+		val += __shfl_down(val, o, 64);
+		pix += __shfl_down(pix, o, 64);
+		cnt += __shfl_down(cnt, o, 64);
+	}
+	const int wave = threadIdx.x >> 6;
+	if ((threadIdx.x & 63) == 0) {
+		sv[wave] = val;
+		sp[wave] = pix;
+		sc[wave] = cnt;
+	}
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		for (int w = 1; w < 4; w++) {
+			val += sv[w];
+			pix += sp[w];
+			cnt += sc[w];
+		}
+		if (val)
+			atomicAdd(acc + q * 3, val);
+		if (pix)
+			atomicAdd(acc + q * 3 + 1, pix);
+		if (cnt)
+			atomicAdd(acc + q * 3 + 2, cnt);
+	}
+}
+
+/* ---------------------------------------------------------------------------------------
+ * host side
+ * ------------------------------------------------------------------------------------- */
+static int reg_quality(sg_ctx *ctx, SgDevice &dv, hipStream_t s, const uint16_t *d_sel, int S,
+		const std::vector<int> &frames, std::vector<double> &qual) {
+	const int nq = (int)frames.size();
+	qual.assign(nq, 0.0);
+	if (!nq)
+		return SG_OK;
+	const int xs = (S - 1) / 3, ys = (S - 1) / 3;
+	if (xs < 2 || ys < 2)	/* the subsample loop never runs: dval = 0 (:95-98) */
+		return SG_OK;
+	HIPCHK(ensure(dv.reg_qbuf, (size_t)nq * xs * ys * sizeof(uint16_t) + sizeof(int) * nq + 64));
+	HIPCHK(ensure(dv.reg_qacc, (size_t)nq * (3 * sizeof(unsigned long long) + sizeof(unsigned int))));
+	uint16_t *qbuf = (uint16_t *)dv.reg_qbuf.p;
+	int *d_frames = (int *)((char *)dv.reg_qbuf.p + (((size_t)nq * xs * ys * sizeof(uint16_t) + 15) & ~(size_t)15));
+	unsigned long long *acc = (unsigned long long *)dv.reg_qacc.p;
+	unsigned int *qmax = (unsigned int *)(acc + 3 * nq);
+	HIPCHK(hipMemcpyAsync(d_frames, frames.data(), sizeof(int) * nq, hipMemcpyHostToDevice, s));
+	HIPCHK(hipMemsetAsync(dv.reg_qacc.p, 0, (size_t)nq * (3 * sizeof(unsigned long long) + sizeof(unsigned int)), s));
+	hipLaunchKernelGGL(k_quality_sub, dim3(ys, nq), dim3(256), 0, s, d_sel, d_frames, S, xs, ys, qbuf, qmax);
+	HIPCHK(hipGetLastError());
+	hipLaunchKernelGGL(k_quality_grad, dim3((xs + 63) / 64, (ys + 3) / 4, nq), dim3(256), 0, s, qbuf, xs, ys,
+			qmax, acc);
+	HIPCHK(hipGetLastError());
+	std::vector<unsigned long long> h(3 * (size_t)nq);
+	HIPCHK(hipMemcpyAsync(h.data(), acc, sizeof(unsigned long long) * 3 * nq, hipMemcpyDeviceToHost, s));
+	HIPCHK(hipStreamSynchronize(s));
+	for (int i = 0; i < nq; i++) {
+		double q;
+		if (!h[3 * i + 2]) {
+			q = -1.0;
+		} else {
+			q = (double)h[3 * i] / (double)h[3 * i + 1];
+			q = q / 10;
+		}
+		double dval = 0.0;
+		dval += q * 1;
+		qual[i] = sqrt(dval);
+	}
+	return SG_OK;
+}
+
+static int ilog2(int v) {
+	int l = 0;
+	while ((1 << l) < v)
+		l++;
+	return l;
+}
+
+extern "C" int sg_register_dft_u16_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int nframes,
+		int S, int ref_image, const int *included, int *shiftx, int *shifty, double *quality,
+		void *stream) {
+	if (!ctx || dev_index < 0 || dev_index >= (int)ctx->dev.size() || !d_sel || !shiftx || !shifty || !quality)
+		return SG_ERR_GENERIC;
+	if (nframes < 1)
+		return set_err(ctx, SG_ERR_GENERIC, "no frame to register%s%ld", "", nframes);
+	if (S < 8 || S > 4096 || (S & (S - 1)))
+		return set_err(ctx, SG_ERR_SIZE, "DFT registration needs a power-of-two selection side "
+				"between 8 and 4096%s (got %ld)", "", S);
+	if (ref_image < 0)
+		ref_image = 0;	/* seq->reference_image == -1 -> 0 (:212-215) */
+	if (ref_image >= nframes)
+		return set_err(ctx, SG_ERR_GENERIC, "reference image out of range%s %ld", "", ref_image);
+	SgDevice &dv = ctx->dev[dev_index];
+	HIPCHK(hipSetDevice(dv.id));
+	hipStream_t s = stream ? (hipStream_t)stream : dv.stream;
+	const int logS = ilog2(S);
+	const size_t plane = (size_t)S * S;
+
+	/* frames to register, in index order (the reference skips ref and excluded frames) */
+	std::vector<int> todo;
+	for (int f = 0; f < nframes; f++)
+		if (f != ref_image && (!included || included[f]))
+			todo.push_back(f);
+
+	/* twiddles exp(-2 pi i k / S) */
+	HIPCHK(ensure(dv.reg_tw, sizeof(sg_c64) * (S / 2)));
+	{
+		std::vector<double> tw(S);
+		for (int k = 0; k < S / 2; k++) {
+			const double a = -2.0 * M_PI * (double)k / (double)S;
+			tw[2 * k] = cos(a);
+			tw[2 * k + 1] = sin(a);
+		}
+		HIPCHK(hipMemcpyAsync(dv.reg_tw.p, tw.data(), sizeof(double) * S, hipMemcpyHostToDevice, s));
+		HIPCHK(hipStreamSynchronize(s));
+	}
+	const sg_c64 *tw = (const sg_c64 *)dv.reg_tw.p;
+
+	/* quality of the reference and of every registered frame */
+	std::vector<int> qframes;
+	qframes.push_back(ref_image);
+	qframes.insert(qframes.end(), todo.begin(), todo.end());
+	std::vector<double> qual;
+	int rc = reg_quality(ctx, dv, s, d_sel, S, qframes, qual);
+	if (rc)
+		return rc;
+
+	/* batch of pairs per launch */
+	int B = (int)((size_t)(512u << 20) / (plane * sizeof(sg_c64)));
+	if (B < 1)
+		B = 1;
+	if (B > 16)
+		B = 16;
+	const int npairs_total = (int)(todo.size() + 1) / 2;
+	if (B > npairs_total && npairs_total > 0)
+		B = npairs_total;
+	const size_t row_lds = plane / S * sizeof(sg_c64);
+	int CW = 8192 / S;
+	if (CW < 1)
+		CW = 1;
+	if (CW > 8)
+		CW = 8;
+	const size_t col_lds = (size_t)CW * (S + 1) * sizeof(sg_c64);
+	(void)hipFuncSetAttribute((const void *)k_reg_rows_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)row_lds);
+	(void)hipFuncSetAttribute((const void *)k_reg_rows_inv_argmax, hipFuncAttributeMaxDynamicSharedMemorySize, (int)row_lds);
+	(void)hipFuncSetAttribute((const void *)k_reg_cols, hipFuncAttributeMaxDynamicSharedMemorySize, (int)col_lds);
+
+	HIPCHK(ensure(dv.reg_spec, plane * sizeof(sg_c64)));
+	HIPCHK(ensure(dv.reg_work, (size_t)(B > 1 ? B : 1) * plane * sizeof(sg_c64)));
+	HIPCHK(ensure(dv.reg_best, (size_t)(B > 1 ? B : 1) * (S * sizeof(SgBest) + 4 * sizeof(int)) + 2 * B * sizeof(int) + 64));
+	sg_c64 *spec = (sg_c64 *)dv.reg_spec.p, *work = (sg_c64 *)dv.reg_work.p;
+	SgBest *best = (SgBest *)dv.reg_best.p;
+	int *d_out = (int *)(best + (size_t)(B > 1 ? B : 1) * S);
+	int *d_fa = d_out + 4 * (B > 1 ? B : 1);
+	int *d_fb = d_fa + (B > 1 ? B : 1);
+
+	std::vector<int> hfa(B), hfb(B), hout(4 * (size_t)B);
+	/* reference spectrum R = FFT2(ref) */
+	{
+		hfa[0] = ref_image;
+		hfb[0] = -1;
+		HIPCHK(hipMemcpyAsync(d_fa, hfa.data(), sizeof(int), hipMemcpyHostToDevice, s));
+		HIPCHK(hipMemcpyAsync(d_fb, hfb.data(), sizeof(int), hipMemcpyHostToDevice, s));
+		hipLaunchKernelGGL(k_reg_rows_fwd, dim3(S, 1), dim3(256), row_lds, s, d_sel, d_fa, d_fb, S, logS, tw, spec);
+		HIPCHK(hipGetLastError());
+		hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, 1), dim3(512), col_lds, s, spec, S, logS, CW, tw, 0);
+		HIPCHK(hipGetLastError());
+		HIPCHK(hipStreamSynchronize(s));
+	}
+	shiftx[ref_image] = 0;
+	shifty[ref_image] = 0;
+	for (size_t p0 = 0; p0 < todo.size(); p0 += 2 * (size_t)B) {
+		int np = 0;
+		for (size_t k = p0; k < todo.size() && np < B; k += 2, np++) {
+			hfa[np] = todo[k];
+			hfb[np] = (k + 1 < todo.size()) ? todo[k + 1] : -1;
+		}
+		HIPCHK(hipMemcpyAsync(d_fa, hfa.data(), sizeof(int) * np, hipMemcpyHostToDevice, s));
+		HIPCHK(hipMemcpyAsync(d_fb, hfb.data(), sizeof(int) * np, hipMemcpyHostToDevice, s));
+		hipLaunchKernelGGL(k_reg_rows_fwd, dim3(S, np), dim3(256), row_lds, s, d_sel, d_fa, d_fb, S, logS, tw, work);
+		HIPCHK(hipGetLastError());
+		hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, np), dim3(512), col_lds, s, work, S, logS, CW, tw, 0);
+		HIPCHK(hipGetLastError());
+		hipLaunchKernelGGL(k_reg_xpower, dim3(1024, np), dim3(256), 0, s, work, (const sg_c64 *)spec, S);
+		HIPCHK(hipGetLastError());
+		hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, np), dim3(512), col_lds, s, work, S, logS, CW, tw, 1);
+		HIPCHK(hipGetLastError());
+		hipLaunchKernelGGL(k_reg_rows_inv_argmax, dim3(S, np), dim3(256), row_lds, s, (const sg_c64 *)work, S, logS,
+				tw, best);
+		HIPCHK(hipGetLastError());
+		hipLaunchKernelGGL(k_reg_final, dim3(np), dim3(256), 0, s, (const SgBest *)best, S, d_out);
+		HIPCHK(hipGetLastError());
+		HIPCHK(hipMemcpyAsync(hout.data(), d_out, sizeof(int) * 4 * np, hipMemcpyDeviceToHost, s));
+		HIPCHK(hipStreamSynchronize(s));
+		for (int k = 0; k < np; k++) {
+			shiftx[hfa[k]] = hout[4 * k];
+			shifty[hfa[k]] = hout[4 * k + 1];
+			if (hfb[k] >= 0) {
+				shiftx[hfb[k]] = hout[4 * k + 2];
+				shifty[hfb[k]] = hout[4 * k + 3];
+			}
+		}
+	}
+
+	/* quality: q_min/q_max seeded by the reference frame, then frames in index order with
+	 * the reference's min() macro (src/core/siril.h), then normalizeQualityData */
+	double q_min = qual[0], q_max = qual[0];
+	quality[ref_image] = qual[0];
+	for (size_t k = 0; k < todo.size(); k++) {
+		const double qv = qual[k + 1];
+		quality[todo[k]] = qv;
+		if (qv > q_max)
+			q_max = qv;
+		q_min = (q_min < qv) ? q_min : qv;
+	}
+	for (int f = 0; f < nframes; f++) {
+		if (included && !included[f])
+			continue;
+		quality[f] -= q_min;
+		quality[f] /= (q_max - q_min);
+	}
+	return SG_OK;
+}
+
+extern "C" int sg_register_dft_u16(sg_ctx *ctx, const uint16_t *sel, int nframes, int S, int ref_image,
+		const int *included, int *shiftx, int *shifty, double *quality) {
+	if (!ctx || ctx->dev.empty() || !sel)
+		return SG_ERR_GENERIC;
+	if (nframes < 1 || S < 1)
+		return SG_ERR_GENERIC;
+	SgDevice &dv = ctx->dev[0];
+	HIPCHK(hipSetDevice(dv.id));
+	const size_t bytes = (size_t)nframes * S * S * sizeof(uint16_t);
+	HIPCHK(ensure(dv.reg_sel, bytes));
+	HIPCHK(hipMemcpyAsync(dv.reg_sel.p, sel, bytes, hipMemcpyHostToDevice, dv.stream));
+	return sg_register_dft_u16_device(ctx, 0, (const uint16_t *)dv.reg_sel.p, nframes, S, ref_image, included,
+			shiftx, shifty, quality, nullptr);
+}

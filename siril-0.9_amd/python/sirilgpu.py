@@ -99,15 +99,11 @@ def load():
                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                                          ctypes.c_int, P]
     lib.sg_synth_fill_device.restype = ctypes.c_int
-    for name in ("sg_register_dft_u16",):
-        if hasattr(lib, name):
-            f = getattr(lib, name)
-            f.argtypes = [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, P]
-            f.restype = ctypes.c_int
-    if hasattr(lib, "sg_register_dft_u16_device"):
-        f = lib.sg_register_dft_u16_device
-        f.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, P, P]
-        f.restype = ctypes.c_int
+    lib.sg_register_dft_u16.argtypes = [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, P]
+    lib.sg_register_dft_u16.restype = ctypes.c_int
+    lib.sg_register_dft_u16_device.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               P, P, P, P, P]
+    lib.sg_register_dft_u16_device.restype = ctypes.c_int
     _lib = lib
     return lib
 
@@ -216,6 +212,35 @@ class Context:
                                    out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)), rej,
                                    ctypes.byref(maxim))
         return rc, out, np.array(list(rej), dtype=np.uint64).reshape(3, 2), int(maxim.value)
+
+    def register_dft(self, sel, ref_image=0, included=None):
+        """register_shift_dft on host selections sel[nframes][S][S] (bottom-up, one layer)."""
+        sel = np.ascontiguousarray(sel, dtype=np.uint16)
+        n, S, S2 = sel.shape
+        assert S == S2
+        inc = None if included is None else np.ascontiguousarray(included, dtype=np.int32)
+        sx = np.zeros(n, dtype=np.int32)
+        sy = np.zeros(n, dtype=np.int32)
+        q = np.zeros(n, dtype=np.float64)
+        P = ctypes.c_void_p
+        rc = self.lib.sg_register_dft_u16(self.ctx, sel.ctypes.data_as(P), n, S, ref_image,
+                                          inc.ctypes.data_as(P) if inc is not None else None,
+                                          sx.ctypes.data_as(P), sy.ctypes.data_as(P), q.ctypes.data_as(P))
+        self.check(rc, "sg_register_dft_u16")
+        return sx, sy, q
+
+    def register_dft_device(self, d_sel, nframes, S, ref_image=0, included=None, stream=None, dev_index=0):
+        inc = None if included is None else np.ascontiguousarray(included, dtype=np.int32)
+        sx = np.zeros(nframes, dtype=np.int32)
+        sy = np.zeros(nframes, dtype=np.int32)
+        q = np.zeros(nframes, dtype=np.float64)
+        P = ctypes.c_void_p
+        rc = self.lib.sg_register_dft_u16_device(self.ctx, dev_index, P(d_sel), nframes, S, ref_image,
+                                                 inc.ctypes.data_as(P) if inc is not None else None,
+                                                 sx.ctypes.data_as(P), sy.ctypes.data_as(P),
+                                                 q.ctypes.data_as(P), P(stream) if stream else None)
+        self.check(rc, "sg_register_dft_u16_device")
+        return sx, sy, q
 
     def synth_fill(self, d_frames, nframes, C, H, W, row_begin, row_end, seed, maxshift, dev_index=0):
         rc = self.lib.sg_synth_fill_device(self.ctx, dev_index, ctypes.c_void_p(d_frames), nframes, C, H, W,
