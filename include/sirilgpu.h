@@ -45,6 +45,9 @@ enum sg_rejection { SG_NO_REJEC, SG_PERCENTILE, SG_SIGMA, SG_SIGMEDIAN, SG_WINSO
 enum sg_normalization { SG_NO_NORM, SG_ADDITIVE, SG_MULTIPLICATIVE, SG_ADDITIVE_SCALING,
 	SG_MULTIPLICATIVE_SCALING };
 
+/* kernel selection for sg_stack_desc.kernel_path (results are identical on every path) */
+enum sg_kernel_path { SG_PATH_AUTO = 0, SG_PATH_SORTED = 1 };
+
 /* rectangle, src/core/siril.h:477-479 */
 typedef struct { int x, y, w, h; } sg_rect;
 
@@ -72,7 +75,8 @@ typedef struct {
 	const double *scale;
 	int max_thread;		/* com.max_thread: the reference's OpenMP team size */
 	int max_number_of_rows;	/* args->max_number_of_rows */
-	int reserved[6];
+	int kernel_path;	/* SG_PATH_*: 0 = automatic (no reference equivalent; testing/A-B) */
+	int reserved[5];
 } sg_stack_desc;
 
 typedef struct sg_ctx sg_ctx;

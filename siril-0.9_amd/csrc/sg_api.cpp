@@ -24,7 +24,9 @@ struct SgChainTables {
 	int nblocks;
 };
 
-template <int NREG> __global__ void k_stack_sorted(SgStackParams p);
+template <int NREG, bool LISTED>
+__global__ void k_stack_sorted(SgStackParams p, const unsigned int *list, const unsigned int *list_count);
+__global__ void k_stack_hist(SgStackParams p, unsigned int *redo_count, unsigned int *redo_list);
 __global__ void k_stack_reduce(SgStackParams p);
 __global__ void k_sum_finalize(SgStackParams p);
 __global__ void k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *scratch, int phase);
@@ -71,7 +73,7 @@ extern "C" void sg_shutdown(sg_ctx *ctx) {
 		(void)hipStreamSynchronize(d.stream);
 		SgBuf *bufs[] = {&d.flag_list, &d.flag_map, &d.flag_count, &d.rej, &d.sum_buf, &d.maxim,
 			&d.shifts, &d.norm, &d.tables, &d.scratch, &d.frames, &d.out, &d.reg_sel, &d.reg_spec,
-			&d.reg_work, &d.reg_tw, &d.reg_best, &d.reg_qbuf, &d.reg_qacc};
+			&d.reg_work, &d.reg_tw, &d.reg_best, &d.reg_qbuf, &d.reg_qacc, &d.redo};
 		for (SgBuf *b : bufs)
 			if (b->p)
 				(void)hipFree(b->p);
@@ -176,19 +178,26 @@ static int pick_nreg(int N) {
 	return 0;
 }
 
-static hipError_t launch_sorted(int nreg, dim3 grid, size_t lds, hipStream_t s, const SgStackParams &p) {
-	switch (nreg) {
-#define SG_CASE(R)                                                                                  \
-	case R:                                                                                     \
-		(void)hipFuncSetAttribute((const void *)k_stack_sorted<R>,                          \
+static hipError_t launch_sorted(int nreg, bool listed, dim3 grid, size_t lds, hipStream_t s, const SgStackParams &p,
+		const unsigned int *list, const unsigned int *list_count) {
+	switch (nreg * 2 + (listed ? 1 : 0)) {
+#define SG_CASE(R, LI)                                                                              \
+	case R * 2 + LI:                                                                            \
+		(void)hipFuncSetAttribute((const void *)k_stack_sorted<R, LI>,                      \
 				hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);              \
-		hipLaunchKernelGGL(k_stack_sorted<R>, grid, dim3(SG_SORT_THREADS), lds, s, p);      \
+		hipLaunchKernelGGL((k_stack_sorted<R, LI>), grid, dim3(SG_SORT_THREADS), lds, s, p, list,  \
+				list_count);                                                        \
 		return hipGetLastError();
-		SG_CASE(1)
-		SG_CASE(2)
-		SG_CASE(4)
-		SG_CASE(8)
-		SG_CASE(16)
+		SG_CASE(1, 0)
+		SG_CASE(1, 1)
+		SG_CASE(2, 0)
+		SG_CASE(2, 1)
+		SG_CASE(4, 0)
+		SG_CASE(4, 1)
+		SG_CASE(8, 0)
+		SG_CASE(8, 1)
+		SG_CASE(16, 0)
+		SG_CASE(16, 1)
 #undef SG_CASE
 	}
 	return hipErrorInvalidValue;
@@ -319,11 +328,37 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 		const int ntx = (W + SG_TILE_W - 1) / SG_TILE_W;
 		const size_t nblk = (size_t)ntx * nrows * C;
 		const size_t lds = (size_t)N * SG_STAGE_STRIDE * 2;
-		HIPCHK(hipEventRecord(dv.ev[0], s));
-		HIPCHK(launch_sorted(nreg, dim3((unsigned)nblk), lds, s, p));
-		HIPCHK(hipEventRecord(dv.ev[1], s));
-		ctx->stats.main_kernel_blocks = (int)nblk;
-		ctx->stats.launches = 1;
+		/* histogram fast path (sg_stack_hist.hip): SIGMA, no normalisation, N >= 16 */
+		const int path = d->kernel_path;
+		const bool hist = path != SG_PATH_SORTED && d->method == SG_STACK_MEAN && d->rejection == SG_SIGMA &&
+			p.normalize == 0 && N >= 16;
+		if (hist) {
+			HIPCHK(ensure(dv.redo, sizeof(unsigned int) * (npix_launch + 16)));
+			unsigned int *redo_count = (unsigned int *)dv.redo.p;
+			unsigned int *redo_list = redo_count + 16;
+			HIPCHK(hipMemsetAsync(redo_count, 0, sizeof(unsigned int), s));
+			HIPCHK(hipEventRecord(dv.ev[0], s));
+			hipLaunchKernelGGL(k_stack_hist, dim3((unsigned)nblk), dim3(256), 0, s, p, redo_count, redo_list);
+			HIPCHK(hipGetLastError());
+			HIPCHK(hipEventRecord(dv.ev[1], s));
+			unsigned int nredo = 0;
+			HIPCHK(hipMemcpyAsync(&nredo, redo_count, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+			HIPCHK(hipStreamSynchronize(s));
+			ctx->stats.chain_pixels = nredo;
+			ctx->stats.main_kernel_blocks = (int)nblk;
+			ctx->stats.launches = 1;
+			if (nredo) {
+				HIPCHK(launch_sorted(nreg, true, dim3((nredo + SG_TILE_W - 1) / SG_TILE_W), lds, s, p,
+						redo_list, redo_count));
+				ctx->stats.launches++;
+			}
+		} else {
+			HIPCHK(hipEventRecord(dv.ev[0], s));
+			HIPCHK(launch_sorted(nreg, false, dim3((unsigned)nblk), lds, s, p, nullptr, nullptr));
+			HIPCHK(hipEventRecord(dv.ev[1], s));
+			ctx->stats.main_kernel_blocks = (int)nblk;
+			ctx->stats.launches = 1;
+		}
 		/* literal path for queued pixels: two phases, grid reads the count on device */
 		HIPCHK(ensure(dv.scratch, (size_t)SG_LIT_THREADS * (((size_t)N * 5 + 15) & ~(size_t)15)));
 		for (int phase = 1; phase <= 2; phase++) {

@@ -23,6 +23,7 @@ struct SgDevice {
 	SgBuf flag_list, flag_map, flag_count, rej, sum_buf, maxim, shifts, norm, tables, scratch, frames, out;
 	/* registration workspaces (sg_register.hip) */
 	SgBuf reg_sel, reg_spec, reg_work, reg_tw, reg_best, reg_qbuf, reg_qacc;
+	SgBuf redo;	/* redo list of the histogram stacking path */
 	uint16_t *pinned[2] = {nullptr, nullptr};
 	size_t pinned_size = 0;
 };

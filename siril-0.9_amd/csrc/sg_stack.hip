@@ -432,29 +432,57 @@ __device__ int reject_percentile(const SgCol &A, SgRejState &st, double plow, do
 /* ----------------------------------------------------------------------------------
  * main sorted kernel
  * ---------------------------------------------------------------------------------- */
-template <int NREG>
+template <int NREG, bool LISTED>
 __global__ void __launch_bounds__(SG_SORT_THREADS)
-k_stack_sorted(SgStackParams p) {
+k_stack_sorted(SgStackParams p, const unsigned int *__restrict__ list, const unsigned int *__restrict__ list_count) {
 	extern __shared__ __attribute__((aligned(16))) uint16_t stage[];
+	__shared__ int slot_c[SG_TILE_W], slot_R[SG_TILE_W], slot_x[SG_TILE_W];
 	uint32_t *stage32 = (uint32_t *)stage;
 	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-	const int ntx = (p.W + SG_TILE_W - 1) / SG_TILE_W;
-	const int nrows = p.row_end - p.row_begin;
-	int b = blockIdx.x;
-	const int xt = b % ntx;
-	b /= ntx;
-	const int R = p.row_begin + (b % nrows);
-	const int c = b / nrows;
-	const int x0 = xt * SG_TILE_W;
 	const int N = p.N;
+	int c0 = 0;
+	if (LISTED) {
+		/* redo list of the histogram path: slot i = pixel list[64 * block + i] */
+		const unsigned int count = *list_count;
+		if (tid < SG_TILE_W) {
+			const unsigned int k = blockIdx.x * SG_TILE_W + tid;
+			if (k < count) {
+				const unsigned int pix = list[k];
+				const int xx = (int)(pix % (unsigned)p.W);
+				const unsigned int cr = pix / (unsigned)p.W;
+				slot_x[tid] = xx;
+				slot_R[tid] = (int)(cr % (unsigned)p.H);
+				slot_c[tid] = (int)(cr / (unsigned)p.H);
+			} else {
+				slot_x[tid] = -1;
+				slot_R[tid] = 0;
+				slot_c[tid] = 0;
+			}
+		}
+	} else {
+		const int ntx = (p.W + SG_TILE_W - 1) / SG_TILE_W;
+		const int nrows = p.row_end - p.row_begin;
+		int b = blockIdx.x;
+		const int xt = b % ntx;
+		b /= ntx;
+		const int R = p.row_begin + (b % nrows);
+		c0 = b / nrows;
+		if (tid < SG_TILE_W) {
+			const int xx = xt * SG_TILE_W + tid;
+			slot_x[tid] = xx < p.W ? xx : -1;
+			slot_R[tid] = R;
+			slot_c[tid] = c0;
+		}
+	}
+	__syncthreads();
 
-	/* 1. stage the tile: frame f row -> stage[f][0..63] */
+	/* 1. stage the tile: frame f, slot -> stage[f][slot] */
 	for (int idx = tid; idx < N * SG_TILE_W; idx += SG_SORT_THREADS) {
 		const int f = idx >> 6, px = idx & 63;
-		const int x = x0 + px;
+		const int xx = slot_x[px];
 		uint16_t v = 0;
-		if (x < p.W)
-			v = sg_gather(p, f, c, R, x);
+		if (xx >= 0)
+			v = sg_gather(p, f, slot_c[px], slot_R[px], xx);
 		stage[f * SG_STAGE_STRIDE + px] = v;
 	}
 	__syncthreads();
@@ -481,8 +509,10 @@ k_stack_sorted(SgStackParams p) {
 	/* 3. per-pixel rejection, one lane per pixel */
 	uint32_t my_rlo = 0, my_rhi = 0;
 	if (tid < SG_TILE_W) {
-		const int x = x0 + tid;
-		if (x < p.W) {
+		const int x = slot_x[tid];
+		const int c = slot_c[tid];
+		const int R = slot_R[tid];
+		if (x >= 0) {
 			SgCol A = {stage + tid};
 			uint16_t value = 0;
 			int cls = SG_CLS_OK;
@@ -534,27 +564,42 @@ k_stack_sorted(SgStackParams p) {
 					p.flag_list[slot] = (unsigned int)pix;
 			}
 		}
-		/* rejection counters: wave reduce, one sharded atomic per tile */
+		/* rejection counters */
 		if (p.method != 2) {
-			unsigned long long lo = my_rlo, hi = my_rhi;
-			for (int o = 32; o > 0; o >>= 1) {
-				lo += __shfl_down(lo, o, 64);
-				hi += __shfl_down(hi, o, 64);
-			}
-			if (tid == 0 && (lo | hi)) {
-				unsigned long long *sh = p.rej + ((size_t)(blockIdx.x % SG_REJ_SHARDS) * 6 + c * 2);
-				atomicAdd(sh, lo);
-				atomicAdd(sh + 1, hi);
+			if (LISTED) {
+				if (my_rlo | my_rhi) {
+					unsigned long long *sh = p.rej + ((size_t)(tid % SG_REJ_SHARDS) * 6 + c * 2);
+					atomicAdd(sh, (unsigned long long)my_rlo);
+					atomicAdd(sh + 1, (unsigned long long)my_rhi);
+				}
+			} else {
+				/* wave reduce, one sharded atomic per tile */
+				unsigned long long lo = my_rlo, hi = my_rhi;
+				for (int o = 32; o > 0; o >>= 1) {
+					lo += __shfl_down(lo, o, 64);
+					hi += __shfl_down(hi, o, 64);
+				}
+				if (tid == 0 && (lo | hi)) {
+					unsigned long long *sh = p.rej + ((size_t)(blockIdx.x % SG_REJ_SHARDS) * 6 + c0 * 2);
+					atomicAdd(sh, lo);
+					atomicAdd(sh + 1, hi);
+				}
 			}
 		}
 	}
 }
 
-template __global__ void k_stack_sorted<1>(SgStackParams);
-template __global__ void k_stack_sorted<2>(SgStackParams);
-template __global__ void k_stack_sorted<4>(SgStackParams);
-template __global__ void k_stack_sorted<8>(SgStackParams);
-template __global__ void k_stack_sorted<16>(SgStackParams);
+template __global__ void k_stack_sorted<1, false>(SgStackParams, const unsigned int *, const unsigned int *);
+template __global__ void k_stack_sorted<1, true>(SgStackParams, const unsigned int *, const unsigned int *);
+template __global__ void k_stack_sorted<2, false>(SgStackParams, const unsigned int *, const unsigned int *);
+template __global__ void k_stack_sorted<2, true>(SgStackParams, const unsigned int *, const unsigned int *);
+template __global__ void k_stack_sorted<4, false>(SgStackParams, const unsigned int *, const unsigned int *);
+template __global__ void k_stack_sorted<4, true>(SgStackParams, const unsigned int *, const unsigned int *);
+template __global__ void k_stack_sorted<8, false>(SgStackParams, const unsigned int *, const unsigned int *);
+template __global__ void k_stack_sorted<8, true>(SgStackParams, const unsigned int *, const unsigned int *);
+template __global__ void k_stack_sorted<16, false>(SgStackParams, const unsigned int *, const unsigned int *);
+template __global__ void k_stack_sorted<16, true>(SgStackParams, const unsigned int *, const unsigned int *);
+
 
 /* ----------------------------------------------------------------------------------
  * streaming reductions: SUM / MAX / MIN / MEAN(NO_REJEC)

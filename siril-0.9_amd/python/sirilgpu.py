@@ -17,6 +17,7 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "libsirilgpu.so")
 SUM, MEAN, MEDIAN, MAX, MIN = range(5)
 NO_REJEC, PERCENTILE, SIGMA, SIGMEDIAN, WINSORIZED, LINEARFIT = range(6)
 NO_NORM, ADDITIVE, MULTIPLICATIVE, ADDITIVE_SCALING, MULTIPLICATIVE_SCALING = range(5)
+PATH_AUTO, PATH_SORTED = 0, 1
 
 SG_OK = 0
 
@@ -38,7 +39,8 @@ class StackDesc(ctypes.Structure):
         ("scale", ctypes.POINTER(ctypes.c_double)),
         ("max_thread", ctypes.c_int),
         ("max_number_of_rows", ctypes.c_int),
-        ("reserved", ctypes.c_int * 6),
+        ("kernel_path", ctypes.c_int),
+        ("reserved", ctypes.c_int * 5),
     ]
 
 
@@ -118,7 +120,7 @@ def _dptr(a):
 
 def make_desc(method, N, W, H, C, rejection=NO_REJEC, normalize=NO_NORM, sig=(4.0, 3.0),
               shiftx=None, shifty=None, offset=None, mul=None, scale=None, max_thread=8,
-              max_number_of_rows=0):
+              max_number_of_rows=0, kernel_path=PATH_AUTO):
     """Build a StackDesc; returns (desc, keepalive) -- keep the arrays alive during the call."""
     keep = []
 
@@ -138,6 +140,7 @@ def make_desc(method, N, W, H, C, rejection=NO_REJEC, normalize=NO_NORM, sig=(4.
     d.shiftx, d.shifty = _iptr(sx), _iptr(sy)
     d.offset, d.mul, d.scale = _dptr(of), _dptr(mu), _dptr(sc)
     d.max_thread, d.max_number_of_rows = max_thread, max_number_of_rows
+    d.kernel_path = kernel_path
     return d, keep
 
 

@@ -141,3 +141,57 @@ def test_constant_and_knife_edges(gpu_ctx):
             out, rj, _ = gpu_stack(gpu_ctx, frames, sg.MEAN, rej, sig, max_thread=2)
             assert_same(out, ref, f"rej {rej} sig {sig}")
             assert np.array_equal(rj, rr)
+
+
+def _stack_path(ctx, frames, rejection, sig, sx=None, sy=None, path=sg.PATH_AUTO, max_thread=8):
+    N, C, H, W = frames.shape
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, C, rejection=rejection, sig=sig, shiftx=sx, shifty=sy,
+                              max_thread=max_thread, max_number_of_rows=H, kernel_path=path)
+    rc, out, rej, _ = ctx.stack_host(desc, np.ascontiguousarray(frames))
+    assert rc == 0, ctx.error()
+    return out, rej, ctx.stats()
+
+
+@pytest.mark.parametrize("N", [16, 17, 40, 128, 512])
+def test_hist_path_matches_oracle_and_sorted(gpu_ctx, N):
+    """histogram SIGMA path (sg_stack_hist.hip) == sorted path == oracle, bit for bit"""
+    H, W = 24, 160
+    frames = orc.synth(N, 1, H, W, seed=300 + N, maxshift=10)
+    sx, sy = orc.synth_shifts(N, seed=300 + N, maxshift=10)
+    out_h, rej_h, st = _stack_path(gpu_ctx, frames, sg.SIGMA, (4.0, 3.0), sx, sy)
+    out_s, rej_s, _ = _stack_path(gpu_ctx, frames, sg.SIGMA, (4.0, 3.0), sx, sy, path=sg.PATH_SORTED)
+    rc, ref, rej_ref = orc.stack_rejection(frames, sg.SIGMA, sig=(4.0, 3.0), shiftx=sx, shifty=sy, max_thread=8)
+    assert_same(out_h, ref, f"hist N={N}")
+    assert_same(out_s, ref, f"sorted N={N}")
+    assert np.array_equal(rej_h, rej_ref) and np.array_equal(rej_s, rej_ref)
+    # the fast path must carry almost every pixel (redo list = pixels re-done by the sort)
+    assert st.chain_pixels <= 0.05 * H * W, st.chain_pixels
+
+
+@pytest.mark.parametrize("case", ["constant", "uniform", "bimodal", "saturated", "tight_sig", "dark"])
+def test_hist_path_adversarial(gpu_ctx, case):
+    """inputs that defeat the histogram's assumptions must fall back, not differ:
+    u8 bin overflow (>255 equal samples), tail overflow, medians outside the band,
+    decisions on knife edges"""
+    N, H, W = 300, 6, 128
+    rng = np.random.default_rng(7)
+    if case == "constant":
+        frames = np.full((N, 1, H, W), 4321, dtype=np.uint16)
+        frames[:5, :, ::2, :] = 4400
+    elif case == "uniform":
+        frames = rng.integers(0, 65536, size=(N, 1, H, W)).astype(np.uint16)
+    elif case == "bimodal":
+        frames = np.where(rng.random((N, 1, H, W)) < 0.5, 1000, 3000).astype(np.uint16)
+        frames += rng.integers(0, 20, size=frames.shape).astype(np.uint16)
+    elif case == "saturated":
+        frames = np.full((N, 1, H, W), 65535, dtype=np.uint16)
+        frames[: N // 3] = rng.integers(60000, 65536, size=(N // 3, 1, H, W)).astype(np.uint16)
+    elif case == "tight_sig":
+        frames = (1000 + rng.integers(0, 8, size=(N, 1, H, W))).astype(np.uint16)
+    else:
+        frames = rng.integers(0, 40, size=(N, 1, H, W)).astype(np.uint16)
+    sig = (1.0, 0.5) if case == "tight_sig" else (4.0, 3.0)
+    out_h, rej_h, _ = _stack_path(gpu_ctx, frames, sg.SIGMA, sig)
+    rc, ref, rej_ref = orc.stack_rejection(frames, sg.SIGMA, sig=sig, max_thread=8)
+    assert_same(out_h, ref, case)
+    assert np.array_equal(rej_h, rej_ref), (rej_h, rej_ref)
