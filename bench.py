@@ -124,7 +124,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    kms, slow = [], 0
+    kms, slow, redo = [], 0, 0
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -136,6 +136,7 @@ def main():
         st = ctx.stats()
         kms.append(st.kernel_ms)
         slow = st.slow_pixels
+        redo = st.chain_pixels
         rej_tot = rej
     torch.cuda.synchronize()
     if dist:
@@ -174,6 +175,7 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None},
             "kernel_ms": round(kavg, 3),
             "slow_pixels": int(slow),
+            "redo_pixels": int(redo),
             "rejected": [int(x) for x in rej_tot.reshape(-1)[:2]],
         }
         if not args.no_cpu_baseline and world == 1:

@@ -73,7 +73,7 @@ extern "C" void sg_shutdown(sg_ctx *ctx) {
 		(void)hipStreamSynchronize(d.stream);
 		SgBuf *bufs[] = {&d.flag_list, &d.flag_map, &d.flag_count, &d.rej, &d.sum_buf, &d.maxim,
 			&d.shifts, &d.norm, &d.tables, &d.scratch, &d.frames, &d.out, &d.reg_sel, &d.reg_spec,
-			&d.reg_work, &d.reg_tw, &d.reg_best, &d.reg_qbuf, &d.reg_qacc, &d.redo};
+			&d.reg_work, &d.reg_tw, &d.reg_best, &d.reg_qbuf, &d.reg_qacc, &d.redo, &d.zeros};
 		for (SgBuf *b : bufs)
 			if (b->p)
 				(void)hipFree(b->p);
@@ -242,14 +242,22 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 	p.row_end = row_end;
 
 	/* per-frame constants: shifts + normalisation coefficients */
-	HIPCHK(ensure(dv.shifts, sizeof(int) * 2 * N));
+	const int Npad = (N + 15) & ~15;	/* packed table: 64-byte aligned, padded to 16 entries */
+	HIPCHK(ensure(dv.shifts, sizeof(int) * (Npad + 2 * N)));
+	bool shifts16 = true;
 	HIPCHK(ensure(dv.norm, sizeof(double) * 3 * N));
 	if (p.use_shift) {
-		std::vector<int> sh(2 * N);
-		memcpy(sh.data(), d->shiftx, sizeof(int) * N);
-		memcpy(sh.data() + N, d->shifty, sizeof(int) * N);
-		HIPCHK(hipMemcpyAsync(dv.shifts.p, sh.data(), sizeof(int) * 2 * N, hipMemcpyHostToDevice, s));
-		p.shiftx = (const int *)dv.shifts.p;
+		std::vector<int> sh(Npad + 2 * N, 0);
+		for (int i = 0; i < N; i++) {
+			if (d->shiftx[i] < -32768 || d->shiftx[i] > 32767 || d->shifty[i] < -32768 || d->shifty[i] > 32767)
+				shifts16 = false;
+			sh[i] = (int)(((uint32_t)d->shiftx[i] & 0xFFFFu) | ((uint32_t)d->shifty[i] << 16));
+		}
+		memcpy(sh.data() + Npad, d->shiftx, sizeof(int) * N);
+		memcpy(sh.data() + Npad + N, d->shifty, sizeof(int) * N);
+		HIPCHK(hipMemcpyAsync(dv.shifts.p, sh.data(), sizeof(int) * sh.size(), hipMemcpyHostToDevice, s));
+		p.shiftxy = (const int *)dv.shifts.p;
+		p.shiftx = p.shiftxy + Npad;
 		p.shifty = p.shiftx + N;
 	}
 	if (p.normalize) {
@@ -331,8 +339,13 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 		/* histogram fast path (sg_stack_hist.hip): SIGMA, no normalisation, N >= 16 */
 		const int path = d->kernel_path;
 		const bool hist = path != SG_PATH_SORTED && d->method == SG_STACK_MEAN && d->rejection == SG_SIGMA &&
-			p.normalize == 0 && N >= 16;
+			p.normalize == 0 && N >= 16 && shifts16;
 		if (hist) {
+			if (!dv.zeros.p) {
+				HIPCHK(ensure(dv.zeros, 256));
+				HIPCHK(hipMemsetAsync(dv.zeros.p, 0, 256, s));
+			}
+			p.zeros = (const uint16_t *)dv.zeros.p;
 			HIPCHK(ensure(dv.redo, sizeof(unsigned int) * (npix_launch + 16)));
 			unsigned int *redo_count = (unsigned int *)dv.redo.p;
 			unsigned int *redo_list = redo_count + 16;

@@ -22,6 +22,8 @@ struct SgStackParams {
 	int use_shift;
 	double sig0, sig1;
 	const int *shiftx, *shifty;		/* device [N] */
+	const int *shiftxy;			/* device [N] packed (shiftx & 0xffff) | shifty << 16 */
+	const uint16_t *zeros;			/* >= 64 zero samples (out-of-frame loads) */
 	const double *offset, *mul, *scale;	/* device [N] or null */
 	int row_begin, row_end;			/* memory rows to compute */
 	unsigned long long *rej;		/* [SG_REJ_SHARDS][3][2] */

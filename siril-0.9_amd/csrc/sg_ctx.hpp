@@ -24,6 +24,7 @@ struct SgDevice {
 	/* registration workspaces (sg_register.hip) */
 	SgBuf reg_sel, reg_spec, reg_work, reg_tw, reg_best, reg_qbuf, reg_qacc;
 	SgBuf redo;	/* redo list of the histogram stacking path */
+	SgBuf zeros;	/* zero page for out-of-frame sample loads */
 	uint16_t *pinned[2] = {nullptr, nullptr};
 	size_t pinned_size = 0;
 };

@@ -40,12 +40,15 @@ struct SghLds {
 	uint16_t tails[2][SGH_T][64];		/* low / high out-of-band values */
 	uint32_t ntail[2][64];
 	uint32_t nband[64];
+	uint32_t nzero[64], nsat[64];		/* out-of-band samples equal to 0 / 65535 (not listed) */
 	unsigned long long tsum[64], tsq[64];	/* tail moments relative to lo (two's complement sum) */
 };
 
 struct SghPix {
 	int lo;			/* value of bin 0 */
-	int nlo, nhi, nb;	/* samples below / above / inside the band */
+	int nlo, nhi, nb;	/* samples below / above / inside the band (nlo, nhi include nz, ns) */
+	int nz, ns;		/* out-of-band zeros / 65535s (counted, not listed) */
+	int nll, nhl;		/* listed low / high tail values */
 	int lane;
 	const SghLds *L;
 };
@@ -69,21 +72,26 @@ __device__ int sgh_cnt_le(const SghPix &P, int v) {
 	if (v < 0)
 		return 0;
 	if (v < P.lo) {
-		int c = 0;
-		for (int k = 0; k < P.nlo; k++)
+		int c = P.nz;
+		for (int k = 0; k < P.nll; k++)
 			c += (int)P.L->tails[0][k][P.lane] <= v;
 		return c;
 	}
 	if (v < P.lo + SGH_BINS)
 		return P.nlo + sgh_band_le(P, v - P.lo);
-	int c = P.nlo + P.nb;
-	for (int k = 0; k < P.nhi; k++)
+	int c = P.nlo + P.nb + (v >= 65535 ? P.ns : 0);
+	for (int k = 0; k < P.nhl; k++)
 		c += (int)P.L->tails[1][k][P.lane] <= v;
 	return c;
 }
 
-/* value at global rank g (0-based) if it lies in the band, else -1 */
+/* value at global rank g (0-based) if it lies in the band or on a counted 0 / 65535
+ * tail, else -1 (listed tails are unsorted) */
 __device__ int sgh_value_at(const SghPix &P, int g) {
+	if (g < P.nz)
+		return 0;
+	if (g >= P.nlo + P.nb + P.nhl)
+		return 65535;
 	g -= P.nlo;
 	if (g < 0 || g >= P.nb)
 		return -1;
@@ -114,7 +122,19 @@ __device__ void sgh_range_moments(const SghPix &P, int v1, int v2, int &cnt, lon
 	ss = 0;
 	if (v1 > v2)
 		return;
-	for (int k = 0; k < P.nlo; k++) {
+	if (P.nz && v1 <= 0 && 0 <= v2) {
+		const long long d = -P.lo;
+		cnt += P.nz;
+		s += d * P.nz;
+		ss += (unsigned long long)(d * d) * (unsigned long long)P.nz;
+	}
+	if (P.ns && v1 <= 65535 && 65535 <= v2) {
+		const long long d = 65535 - P.lo;
+		cnt += P.ns;
+		s += d * P.ns;
+		ss += (unsigned long long)(d * d) * (unsigned long long)P.ns;
+	}
+	for (int k = 0; k < P.nll; k++) {
 		const int v = P.L->tails[0][k][P.lane];
 		if (v >= v1 && v <= v2) {
 			const long long d = v - P.lo;
@@ -123,7 +143,7 @@ __device__ void sgh_range_moments(const SghPix &P, int v1, int v2, int &cnt, lon
 			ss += (unsigned long long)(d * d);
 		}
 	}
-	for (int k = 0; k < P.nhi; k++) {
+	for (int k = 0; k < P.nhl; k++) {
 		const int v = P.L->tails[1][k][P.lane];
 		if (v >= v1 && v <= v2) {
 			const long long d = v - P.lo;
@@ -296,10 +316,16 @@ __device__ __forceinline__ void sgh_add(SghLds &L, int lane, int lo, uint32_t v,
 		atomicAdd(&L.hist[b >> 2][lane], 1u << ((b & 3) * 8));
 		nb++;
 	} else {
-		const int side = (int)v < lo ? 0 : 1;
-		const uint32_t slot = atomicAdd(&L.ntail[side][lane], 1u);
-		if (slot < SGH_T)
-			L.tails[side][slot][lane] = (uint16_t)v;
+		if (v == 0) {
+			atomicAdd(&L.nzero[lane], 1u);
+		} else if (v == 65535) {
+			atomicAdd(&L.nsat[lane], 1u);
+		} else {
+			const int side = (int)v < lo ? 0 : 1;
+			const uint32_t slot = atomicAdd(&L.ntail[side][lane], 1u);
+			if (slot < SGH_T)
+				L.tails[side][slot][lane] = (uint16_t)v;
+		}
 		const long long d = (long long)v - lo;
 		ts += d;
 		tq += (unsigned long long)(d * d);
@@ -307,14 +333,46 @@ __device__ __forceinline__ void sgh_add(SghLds &L, int lane, int lo, uint32_t v,
 }
 
 /* sample of frame f at (c, R, x) without normalisation (NO_NORM fast path): the y
- * shifted band read leaves zero rows, the x shift writes 0 (:1550-1577, :1628-1632) */
-__device__ __forceinline__ uint32_t sgh_load(const SgStackParams &p, const uint16_t *plane0, int f, int R, int x) {
-	const int sx = p.use_shift ? p.shiftx[f] : 0;
-	const int sy = p.use_shift ? p.shifty[f] : 0;
-	const int sr = R - sy, sc = x - sx;
-	if ((unsigned)sr >= (unsigned)p.H || (unsigned)sc >= (unsigned)p.W)
-		return 0;
-	return plane0[(int64_t)f * p.frame_stride + (int64_t)sr * p.W + sc];
+ * shifted band read leaves zero rows, the x shift writes 0 (:1550-1577, :1628-1632).
+ * f and sh (packed shift (shiftx & 0xffff) | shifty << 16) are wave-uniform: the row
+ * address is scalar, the column offset per lane; out-of-frame samples load a valid
+ * address and are masked to 0 (no divergent branch, so the loads stay in flight). */
+__device__ __forceinline__ uint32_t sgh_load(const SgStackParams &p, const uint16_t *plane0, int f, int sh,
+		int R, int x) {
+	const int sx = (int)(int16_t)(sh & 0xFFFF);
+	const int sy = sh >> 16;
+	const int sr = R - sy;
+	const bool rowok = (unsigned)sr < (unsigned)p.H;
+	const uint16_t *rowp = plane0 + (int64_t)f * p.frame_stride + (int64_t)sr * p.W;
+	const int sc = x - sx;
+	const bool ok = rowok && (unsigned)sc < (unsigned)p.W;
+	/* invalid samples read a zero page instead of being masked after the load */
+	const uint16_t *a = ok ? rowp + sc : p.zeros + (threadIdx.x & 63);
+	return *a;
+}
+
+__device__ __forceinline__ int sgh_shift(const SgStackParams &p, int f) {
+	return p.use_shift ? __builtin_amdgcn_readfirstlane(p.shiftxy[f]) : 0;
+}
+
+/* packed shifts of 16 consecutive frames f0..f0+15 (f0 % 16 == 0; the table is padded
+ * to a multiple of 16 entries and 64-byte aligned): 4 scalar dwordx4 loads */
+__device__ __forceinline__ void sgh_shift16(const SgStackParams &p, int f0, int (&sh)[16]) {
+	if (!p.use_shift) {
+#pragma unroll
+		for (int m = 0; m < 16; m++)
+			sh[m] = 0;
+		return;
+	}
+	const int4 *q = (const int4 *)(p.shiftxy + f0);
+#pragma unroll
+	for (int i = 0; i < 4; i++) {
+		const int4 t = q[i];
+		sh[4 * i] = __builtin_amdgcn_readfirstlane(t.x);
+		sh[4 * i + 1] = __builtin_amdgcn_readfirstlane(t.y);
+		sh[4 * i + 2] = __builtin_amdgcn_readfirstlane(t.z);
+		sh[4 * i + 3] = __builtin_amdgcn_readfirstlane(t.w);
+	}
 }
 
 __global__ void __launch_bounds__(64 * SGH_WAVES)
@@ -339,6 +397,8 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 		L.ntail[0][tid] = 0;
 		L.ntail[1][tid] = 0;
 		L.nband[tid] = 0;
+		L.nzero[tid] = 0;
+		L.nsat[tid] = 0;
 		L.tsum[tid] = 0;
 		L.tsq[tid] = 0;
 	}
@@ -346,7 +406,7 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 	uint32_t v16[SGH_CENTER];
 #pragma unroll
 	for (int k = 0; k < SGH_CENTER; k++)
-		v16[k] = sgh_load(p, plane0, k, R, x);
+		v16[k] = sgh_load(p, plane0, k, sgh_shift(p, k), R, x);
 	int lo = (int)sgh_median16(v16) - SGH_BINS / 2;
 	if (lo < 0)
 		lo = 0;
@@ -357,24 +417,48 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 	uint32_t nb = 0;
 	long long ts = 0;
 	unsigned long long tq = 0;
+	/* frames in chunks of 64: wave w bins frames [g0 + 16w, g0 + 16w + 16); the next
+	 * chunk's 16 loads are issued before the current 16 samples are binned.  Frames
+	 * 0..15 are wave 0's first block (already loaded for the centre). */
+	constexpr int M = 16;
+	const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+	auto load16 = [&](int f0, uint32_t(&dst)[M]) {
+		int sh[M];
+		sgh_shift16(p, f0, sh);
 #pragma unroll
-	for (int k = 0; k < SGH_CENTER; k++)
-		if ((k & (SGH_WAVES - 1)) == wave)
-			sgh_add(L, lane, lo, v16[k], nb, ts, tq);
-	/* frames 16.. N-1, interleaved over the waves, 8 loads in flight per batch */
-	constexpr int U = 8;
-	int f = SGH_CENTER + wave;
-	for (; f + (U - 1) * SGH_WAVES < N; f += U * SGH_WAVES) {
-		uint32_t v[U];
+		for (int m = 0; m < M; m++) {
+			const int f = f0 + m < N ? f0 + m : N - 1;
+			dst[m] = sgh_load(p, plane0, f, sh[m], R, x);
+		}
+	};
+	auto add16 = [&](int f0, const uint32_t(&src)[M]) {
 #pragma unroll
-		for (int u = 0; u < U; u++)
-			v[u] = sgh_load(p, plane0, f + u * SGH_WAVES, R, x);
+		for (int m = 0; m < M; m++)
+			if (f0 + m < N)
+				sgh_add(L, lane, lo, src[m], nb, ts, tq);
+	};
+	/* two named buffers: the loads of block k+1 are in flight while block k is binned */
+	uint32_t bufA[M], bufB[M];
+	int fb = M * wave_u;
+	if (fb == 0) {
 #pragma unroll
-		for (int u = 0; u < U; u++)
-			sgh_add(L, lane, lo, v[u], nb, ts, tq);
+		for (int m = 0; m < M; m++)
+			bufA[m] = v16[m];
+	} else if (fb < N) {
+		load16(fb, bufA);
 	}
-	for (; f < N; f += SGH_WAVES)
-		sgh_add(L, lane, lo, sgh_load(p, plane0, f, R, x), nb, ts, tq);
+	/* the prefetch is unconditional (the last block re-loads itself) so no register
+	 * merge forces the compiler to wait for it before binning */
+	while (fb < N) {
+		load16(fb + 64 < N ? fb + 64 : fb, bufB);
+		add16(fb, bufA);
+		fb += 64;
+		if (fb >= N)
+			break;
+		load16(fb + 64 < N ? fb + 64 : fb, bufA);
+		add16(fb, bufB);
+		fb += 64;
+	}
 	atomicAdd(&L.nband[lane], nb);
 	if (ts)
 		atomicAdd(&L.tsum[lane], (unsigned long long)ts);
@@ -399,8 +483,12 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 	}
 	SghPix P;
 	P.lo = lo;
-	P.nlo = (int)L.ntail[0][lane];
-	P.nhi = (int)L.ntail[1][lane];
+	P.nll = (int)L.ntail[0][lane];
+	P.nhl = (int)L.ntail[1][lane];
+	P.nz = (int)L.nzero[lane];
+	P.ns = (int)L.nsat[lane];
+	P.nlo = P.nll + P.nz;
+	P.nhi = P.nhl + P.ns;
 	P.nb = (int)L.nband[lane];
 	P.lane = lane;
 	P.L = &L;
@@ -408,7 +496,7 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 	uint16_t value = 0;
 	uint32_t rlo = 0, rhi = 0;
 	if (x < p.W) {
-		if ((int)cum != P.nb || P.nlo > SGH_T || P.nhi > SGH_T)
+		if ((int)cum != P.nb || P.nll > SGH_T || P.nhl > SGH_T)
 			cls = 1;	/* u8 bin overflow or tail overflow */
 		else
 			cls = sgh_sigma(P, N, p.sig0, p.sig1, (long long)s32 + (long long)L.tsum[lane],

@@ -155,12 +155,16 @@ def _stack_path(ctx, frames, rejection, sig, sx=None, sy=None, path=sg.PATH_AUTO
 @pytest.mark.parametrize("N", [16, 17, 40, 128, 512])
 def test_hist_path_matches_oracle_and_sorted(gpu_ctx, N):
     """histogram SIGMA path (sg_stack_hist.hip) == sorted path == oracle, bit for bit"""
-    H, W = 24, 160
+    # |shifty| < block height (4 blocks of 16 rows): the reference's heap overflow for
+    # larger shifts (SURVEY a2) is not reproduced
+    H, W = 64, 160
     frames = orc.synth(N, 1, H, W, seed=300 + N, maxshift=10)
     sx, sy = orc.synth_shifts(N, seed=300 + N, maxshift=10)
-    out_h, rej_h, st = _stack_path(gpu_ctx, frames, sg.SIGMA, (4.0, 3.0), sx, sy)
-    out_s, rej_s, _ = _stack_path(gpu_ctx, frames, sg.SIGMA, (4.0, 3.0), sx, sy, path=sg.PATH_SORTED)
-    rc, ref, rej_ref = orc.stack_rejection(frames, sg.SIGMA, sig=(4.0, 3.0), shiftx=sx, shifty=sy, max_thread=8)
+    out_h, rej_h, st = _stack_path(gpu_ctx, frames, sg.SIGMA, (4.0, 3.0), sx, sy, max_thread=2)
+    out_s, rej_s, _ = _stack_path(gpu_ctx, frames, sg.SIGMA, (4.0, 3.0), sx, sy, path=sg.PATH_SORTED,
+                                  max_thread=2)
+    rc, ref, rej_ref = orc.stack_rejection(frames, sg.SIGMA, sig=(4.0, 3.0), shiftx=sx, shifty=sy, max_thread=2)
+    assert rc == 0
     assert_same(out_h, ref, f"hist N={N}")
     assert_same(out_s, ref, f"sorted N={N}")
     assert np.array_equal(rej_h, rej_ref) and np.array_equal(rej_s, rej_ref)
