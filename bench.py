@@ -37,6 +37,8 @@ def parse():
     ap.add_argument("--height", type=int, default=4096)
     ap.add_argument("--rejection", default="sigma")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--frame-pad", type=int, default=0,
+                    help="extra elements between frames in HBM (breaks power-of-two frame strides)")
     ap.add_argument("--cpu-rows", type=int, default=1024, help="rows of the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="OpenMP threads of the CPU baseline (the GPU box's CPU share is 16)")
@@ -94,9 +96,10 @@ def main():
     ctx = sg.Context([dev])
     # this rank's band: rows [rank*H, (rank+1)*H) of a (H*world)-row sequence; the device
     # buffer holds just the band, addressed through a biased base pointer
-    frames = torch.empty(N * H * W, dtype=torch.int16, device="cuda")
+    fstride = H * W + args.frame_pad
+    frames = torch.empty(N * fstride, dtype=torch.int16, device="cuda")
     out = torch.empty(H * W, dtype=torch.int16, device="cuda")
-    ctx.synth_fill(frames.data_ptr(), N, 1, H, W, 0, H, 0x5151 + rank, 16)
+    ctx.synth_fill(frames.data_ptr(), N, 1, H, W, 0, H, 0x5151 + rank, 16, frame_stride=fstride)
     import ctypes
     sx = (ctypes.c_int * N)()
     sy = (ctypes.c_int * N)()
@@ -120,7 +123,7 @@ def main():
                               shiftx=shx, shifty=shy, max_thread=8, max_number_of_rows=H)
 
     def step():
-        return ctx.stack_device(desc, frames.data_ptr(), H * W, H * W, out.data_ptr(), 0, H)
+        return ctx.stack_device(desc, frames.data_ptr(), fstride, H * W, out.data_ptr(), 0, H)
 
     for _ in range(args.warmup):
         step()

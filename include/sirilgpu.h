@@ -136,10 +136,12 @@ int sg_register_dft_u16_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel
 		int S, int ref_image, const int *included, int *shiftx, int *shifty,
 		double *quality, void *stream);
 
-/* Synthetic sequence generator of include/sg_synth.h on the device (bench / tests). */
+/* Synthetic sequence generator of include/sg_synth.h on the device (bench / tests):
+ * frame f, channel c, row r at d_frames[f*frame_stride + (c*height + r)*width]
+ * (frame_stride 0 = nb_layers*height*width). */
 int sg_synth_fill_device(sg_ctx *ctx, int dev_index, uint16_t *d_frames, int nframes,
 		int nb_layers, int height, int width, int row_begin, int row_end, uint64_t seed,
-		int maxshift, void *stream);
+		int maxshift, int64_t frame_stride, void *stream);
 
 #ifdef __cplusplus
 }

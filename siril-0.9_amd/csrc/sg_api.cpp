@@ -31,7 +31,7 @@ __global__ void k_stack_reduce(SgStackParams p);
 __global__ void k_sum_finalize(SgStackParams p);
 __global__ void k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *scratch, int phase);
 __global__ void k_synth_fill(uint16_t *frames, int nframes, int C, int H, int W, int row_begin,
-		int row_end, uint64_t seed, int maxshift);
+		int row_end, uint64_t seed, int maxshift, int64_t frame_stride);
 
 #include "sg_ctx.hpp"
 
@@ -240,25 +240,39 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 	p.use_shift = (d->method != SG_STACK_MEDIAN) && d->shiftx && d->shifty;
 	p.row_begin = row_begin;
 	p.row_end = row_end;
+	{
+		const char *dbg = getenv("SG_HIST_DBG");
+		p.dbg = dbg ? atoi(dbg) : 0;
+	}
 
 	/* per-frame constants: shifts + normalisation coefficients */
-	const int Npad = (N + 15) & ~15;	/* packed table: 64-byte aligned, padded to 16 entries */
-	HIPCHK(ensure(dv.shifts, sizeof(int) * (Npad + 2 * N)));
-	bool shifts16 = true;
+	const int Npad = (N + 15) & ~15;	/* histogram-path table: 64-byte aligned, padded */
+	HIPCHK(ensure(dv.shifts, sizeof(int) * (2 * Npad + 2 * N)));
 	HIPCHK(ensure(dv.norm, sizeof(double) * 3 * N));
-	if (p.use_shift) {
-		std::vector<int> sh(Npad + 2 * N, 0);
-		for (int i = 0; i < N; i++) {
-			if (d->shiftx[i] < -32768 || d->shiftx[i] > 32767 || d->shifty[i] < -32768 || d->shifty[i] > 32767)
-				shifts16 = false;
-			sh[i] = (int)(((uint32_t)d->shiftx[i] & 0xFFFFu) | ((uint32_t)d->shifty[i] << 16));
+	/* the histogram path addresses a frame plane with 32-bit offsets: (R - sy) W 2 must fit */
+	bool hist_addr_ok = (int64_t)H * W * 2 <= (1ll << 30);
+	{
+		/* per frame {shifty*W*2 + 2*shiftx, 2*shiftx} for the histogram path (zeros when
+		 * there is no registration data), then the plain shift arrays */
+		std::vector<int> sh(2 * Npad + 2 * N, 0);
+		for (int i = 0; p.use_shift && i < N; i++) {
+			const int64_t sy = d->shifty[i], sx = d->shiftx[i];
+			const int64_t asy = sy < 0 ? -sy : sy, asx = sx < 0 ? -sx : sx;
+			if ((int64_t)(H + asy) * W * 2 + 2 * asx >= (1ll << 31))
+				hist_addr_ok = false;
+			sh[2 * i] = (int)(sy * W * 2 + 2 * sx);
+			sh[2 * i + 1] = (int)(2 * sx);
 		}
-		memcpy(sh.data() + Npad, d->shiftx, sizeof(int) * N);
-		memcpy(sh.data() + Npad + N, d->shifty, sizeof(int) * N);
+		if (p.use_shift) {
+			memcpy(sh.data() + 2 * Npad, d->shiftx, sizeof(int) * N);
+			memcpy(sh.data() + 2 * Npad + N, d->shifty, sizeof(int) * N);
+		}
 		HIPCHK(hipMemcpyAsync(dv.shifts.p, sh.data(), sizeof(int) * sh.size(), hipMemcpyHostToDevice, s));
-		p.shiftxy = (const int *)dv.shifts.p;
-		p.shiftx = p.shiftxy + Npad;
-		p.shifty = p.shiftx + N;
+		p.hist_tab = (const int *)dv.shifts.p;
+		if (p.use_shift) {
+			p.shiftx = p.hist_tab + 2 * Npad;
+			p.shifty = p.shiftx + N;
+		}
 	}
 	if (p.normalize) {
 		std::vector<double> nm(3 * N);
@@ -339,19 +353,15 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 		/* histogram fast path (sg_stack_hist.hip): SIGMA, no normalisation, N >= 16 */
 		const int path = d->kernel_path;
 		const bool hist = path != SG_PATH_SORTED && d->method == SG_STACK_MEAN && d->rejection == SG_SIGMA &&
-			p.normalize == 0 && N >= 16 && shifts16;
+			p.normalize == 0 && N >= 16 && hist_addr_ok;
 		if (hist) {
-			if (!dv.zeros.p) {
-				HIPCHK(ensure(dv.zeros, 256));
-				HIPCHK(hipMemsetAsync(dv.zeros.p, 0, 256, s));
-			}
-			p.zeros = (const uint16_t *)dv.zeros.p;
 			HIPCHK(ensure(dv.redo, sizeof(unsigned int) * (npix_launch + 16)));
 			unsigned int *redo_count = (unsigned int *)dv.redo.p;
 			unsigned int *redo_list = redo_count + 16;
 			HIPCHK(hipMemsetAsync(redo_count, 0, sizeof(unsigned int), s));
 			HIPCHK(hipEventRecord(dv.ev[0], s));
-			hipLaunchKernelGGL(k_stack_hist, dim3((unsigned)nblk), dim3(256), 0, s, p, redo_count, redo_list);
+			const size_t tab_lds = sizeof(int) * 2 * (size_t)Npad;
+			hipLaunchKernelGGL(k_stack_hist, dim3((unsigned)nblk), dim3(256), tab_lds, s, p, redo_count, redo_list);
 			HIPCHK(hipGetLastError());
 			HIPCHK(hipEventRecord(dv.ev[1], s));
 			unsigned int nredo = 0;
@@ -480,14 +490,15 @@ extern "C" int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *d, sg_read_region_
 
 extern "C" int sg_synth_fill_device(sg_ctx *ctx, int dev_index, uint16_t *d_frames, int nframes,
 		int nb_layers, int height, int width, int row_begin, int row_end, uint64_t seed,
-		int maxshift, void *stream) {
+		int maxshift, int64_t frame_stride, void *stream) {
 	if (!ctx || dev_index < 0 || dev_index >= (int)ctx->dev.size())
 		return SG_ERR_GENERIC;
 	SgDevice &dv = ctx->dev[dev_index];
 	HIPCHK(hipSetDevice(dv.id));
 	hipStream_t s = stream ? (hipStream_t)stream : dv.stream;
 	hipLaunchKernelGGL(k_synth_fill, dim3(8192), dim3(256), 0, s, d_frames, nframes, nb_layers,
-			height, width, row_begin, row_end, seed, maxshift);
+			height, width, row_begin, row_end, seed, maxshift,
+			frame_stride > 0 ? frame_stride : (int64_t)nb_layers * height * width);
 	HIPCHK(hipGetLastError());
 	HIPCHK(hipStreamSynchronize(s));
 	return SG_OK;

@@ -22,8 +22,8 @@ struct SgStackParams {
 	int use_shift;
 	double sig0, sig1;
 	const int *shiftx, *shifty;		/* device [N] */
-	const int *shiftxy;			/* device [N] packed (shiftx & 0xffff) | shifty << 16 */
-	const uint16_t *zeros;			/* >= 64 zero samples (out-of-frame loads) */
+	int dbg;				/* A/B timing knob (SG_HIST_DBG), 0 in production */
+	const int *hist_tab;			/* device int2[N]: {shifty * W * 2, 2 * shiftx} */
 	const double *offset, *mul, *scale;	/* device [N] or null */
 	int row_begin, row_end;			/* memory rows to compute */
 	unsigned long long *rej;		/* [SG_REJ_SHARDS][3][2] */

@@ -11,44 +11,46 @@
  *   - median of the kept set = value at a rank, counts below/above a threshold = ranks;
  *   - sigma comes from exact integer moments n, S, SS of the kept set.
  * So each 64-pixel tile builds, per pixel, an exact histogram of 256 unit-wide bins
- * around a centre c (median of the first 16 frames), u8 counts packed 4 per dword,
- * plus explicit lists of the (rare) values outside the band.  4 waves stream the N
- * frames into it with coalesced 128-byte row loads (shift + zero fill applied at load,
- * :1535-1654); wave 0 then prefix-sums the bins once and runs the reference's pass loop
- * as O(log) histogram queries.
+ * [lo, lo+255] around the median of the first 16 frames (u8 counts packed 4 per dword),
+ * plus counters of the samples below / above the band and of the zeros / 65535s among
+ * them (out-of-frame zero fill, dead pixels, saturation, cosmics).  4 waves stream the
+ * N frames into it: per-frame buffer descriptors give 128-byte coalesced row loads whose
+ * out-of-frame lanes read 0 from the hardware bounds check (shift + zero fill of
+ * :1535-1654 for free), two frames share a VGPR (16-bit halves) and are binned with
+ * packed u16 arithmetic and branch-free LDS atomics.  Wave 0 then prefix-sums the bins
+ * once and runs the reference's pass loop as O(log) histogram queries.
  *
  * Exactness: decisions use exact moments; a pixel whose decision falls within a rounding
  * band of a threshold (GSL's long-double sd vs exact), whose loop would hit the
  * reference's early `break` (N - r <= 4, :1684, stale rejected[]), whose median falls
- * outside the band, whose tail list overflows or whose u8 bins overflow (detected: the
- * byte sum must equal the band count) is appended to a redo list and recomputed by the
+ * outside the band, which has out-of-band samples other than 0 / 65535, or whose u8
+ * counters overflow (detected: the counts must add up to N) is appended to a redo list
+ * and recomputed by the
  * sorted kernel (k_stack_sorted<.., true>), which in turn hands knife-edge pixels to the
  * literal (fp80) path.  Output is therefore bit-identical to the sorted path.
  */
 #include "sg_common.hpp"
 
 #define SGH_BINS 256
-#define SGH_DW (SGH_BINS / 4)	/* dwords per pixel histogram */
-#define SGH_T 16		/* tail capacity per side per pixel */
+#define SGH_DW (SGH_BINS / 4)	/* band dwords per pixel */
 #define SGH_WAVES 4
 #define SGH_CENTER 16		/* frames used for the centre estimate */
 #define SGH_BAND 1e-11		/* same rounding band as the sorted path (SG_BAND) */
 
+typedef unsigned short sgh_u16x2 __attribute__((ext_vector_type(2)));
+
+/* hist[0]          : samples below the band (u32)
+ * hist[1 + j] byte b: count of value lo + 4j + b
+ * hist[1 + SGH_DW]  : samples above the band (u32) */
 struct SghLds {
-	uint32_t hist[SGH_DW][64];		/* byte b of hist[j][px] = count of bin 4j+b */
-	uint16_t cumdw[SGH_DW][64];		/* band samples in bins < 4(j+1) */
-	uint16_t tails[2][SGH_T][64];		/* low / high out-of-band values */
-	uint32_t ntail[2][64];
-	uint32_t nband[64];
-	uint32_t nzero[64], nsat[64];		/* out-of-band samples equal to 0 / 65535 (not listed) */
-	unsigned long long tsum[64], tsq[64];	/* tail moments relative to lo (two's complement sum) */
+	uint32_t hist[SGH_DW + 2][64];
+	uint16_t cum16[SGH_DW / 4][64];		/* band samples in bins < 16(j+1) */
+	uint32_t nz[64], ns[64];		/* zeros / 65535s (all of them lie outside the band) */
 };
 
 struct SghPix {
-	int lo;			/* value of bin 0 */
-	int nlo, nhi, nb;	/* samples below / above / inside the band (nlo, nhi include nz, ns) */
-	int nz, ns;		/* out-of-band zeros / 65535s (counted, not listed) */
-	int nll, nhl;		/* listed low / high tail values */
+	int lo;			/* value of bin 0, 1 <= lo <= 65279 */
+	int nz, ns, nb;		/* zeros, 65535s, band samples (nz + nb + ns == N) */
 	int lane;
 	const SghLds *L;
 };
@@ -59,98 +61,79 @@ __device__ __forceinline__ int sgh_band_le(const SghPix &P, int t) {
 		return 0;
 	if (t > SGH_BINS - 1)
 		t = SGH_BINS - 1;
-	const int j = t >> 2;
-	const int base = j ? (int)P.L->cumdw[j - 1][P.lane] : 0;
-	const uint32_t d = P.L->hist[j][P.lane];
+	const int j16 = t >> 4, jd = t >> 2;
+	int base = j16 ? (int)P.L->cum16[j16 - 1][P.lane] : 0;
+	for (int k = 4 * j16; k < jd; k++)
+		base += (int)__builtin_amdgcn_sad_u8(P.L->hist[1 + k][P.lane], 0u, 0u);
+	const uint32_t d = P.L->hist[1 + jd][P.lane];
 	const int sh = ((t & 3) + 1) * 8;
 	const uint32_t m = sh >= 32 ? 0xFFFFFFFFu : ((1u << sh) - 1u);
 	return base + (int)__builtin_amdgcn_sad_u8(d & m, 0u, 0u);
 }
 
-/* # samples (all frames) with value <= v, v in [-1, 65535] */
-__device__ int sgh_cnt_le(const SghPix &P, int v) {
+/* # samples with value <= v, v in [-1, 65535] */
+__device__ __forceinline__ int sgh_cnt_le(const SghPix &P, int v) {
 	if (v < 0)
 		return 0;
-	if (v < P.lo) {
-		int c = P.nz;
-		for (int k = 0; k < P.nll; k++)
-			c += (int)P.L->tails[0][k][P.lane] <= v;
-		return c;
-	}
+	if (v < P.lo)
+		return P.nz;
 	if (v < P.lo + SGH_BINS)
-		return P.nlo + sgh_band_le(P, v - P.lo);
-	int c = P.nlo + P.nb + (v >= 65535 ? P.ns : 0);
-	for (int k = 0; k < P.nhl; k++)
-		c += (int)P.L->tails[1][k][P.lane] <= v;
-	return c;
+		return P.nz + sgh_band_le(P, v - P.lo);
+	if (v < 65535)
+		return P.nz + P.nb;
+	return P.nz + P.nb + P.ns;
 }
 
-/* value at global rank g (0-based) if it lies in the band or on a counted 0 / 65535
- * tail, else -1 (listed tails are unsorted) */
+/* value at global rank g (0-based) */
 __device__ int sgh_value_at(const SghPix &P, int g) {
 	if (g < P.nz)
 		return 0;
-	if (g >= P.nlo + P.nb + P.nhl)
+	g -= P.nz;
+	if (g >= P.nb)
 		return 65535;
-	g -= P.nlo;
-	if (g < 0 || g >= P.nb)
-		return -1;
-	/* smallest j with cumdw[j] > g */
-	int a = 0, b = SGH_DW - 1;
+	/* smallest j with cum16[j] > g, then walk its 4 dwords */
+	int a = 0, b = SGH_DW / 4 - 1;
 	while (a < b) {
 		const int m = (a + b) >> 1;
-		if ((int)P.L->cumdw[m][P.lane] > g)
+		if ((int)P.L->cum16[m][P.lane] > g)
 			b = m;
 		else
 			a = m + 1;
 	}
-	int base = a ? (int)P.L->cumdw[a - 1][P.lane] : 0;
-	const uint32_t d = P.L->hist[a][P.lane];
+	int base = a ? (int)P.L->cum16[a - 1][P.lane] : 0;
+	int k = 4 * a;
+	uint32_t d = P.L->hist[1 + k][P.lane];
+	for (; k < 4 * a + 3; k++) {
+		const int bs = (int)__builtin_amdgcn_sad_u8(d, 0u, 0u);
+		if (base + bs > g)
+			break;
+		base += bs;
+		d = P.L->hist[2 + k][P.lane];
+	}
 	int i = 0;
 	for (; i < 3; i++) {
 		base += (int)((d >> (8 * i)) & 0xFF);
 		if (base > g)
 			break;
 	}
-	return P.lo + 4 * a + i;
+	return P.lo + 4 * k + i;
 }
 
 /* count, sum and sum of squares of (v - lo) over samples with v1 <= v <= v2 */
-__device__ void sgh_range_moments(const SghPix &P, int v1, int v2, int &cnt, long long &s, unsigned long long &ss) {
-	cnt = 0;
+__device__ void sgh_range_moments(const SghPix &P, int v1, int v2, long long &s, unsigned long long &ss) {
 	s = 0;
 	ss = 0;
 	if (v1 > v2)
 		return;
 	if (P.nz && v1 <= 0 && 0 <= v2) {
 		const long long d = -P.lo;
-		cnt += P.nz;
 		s += d * P.nz;
 		ss += (unsigned long long)(d * d) * (unsigned long long)P.nz;
 	}
 	if (P.ns && v1 <= 65535 && 65535 <= v2) {
 		const long long d = 65535 - P.lo;
-		cnt += P.ns;
 		s += d * P.ns;
 		ss += (unsigned long long)(d * d) * (unsigned long long)P.ns;
-	}
-	for (int k = 0; k < P.nll; k++) {
-		const int v = P.L->tails[0][k][P.lane];
-		if (v >= v1 && v <= v2) {
-			const long long d = v - P.lo;
-			cnt++;
-			s += d;
-			ss += (unsigned long long)(d * d);
-		}
-	}
-	for (int k = 0; k < P.nhl; k++) {
-		const int v = P.L->tails[1][k][P.lane];
-		if (v >= v1 && v <= v2) {
-			const long long d = v - P.lo;
-			cnt++;
-			s += d;
-			ss += (unsigned long long)(d * d);
-		}
 	}
 	int b1 = v1 - P.lo, b2 = v2 - P.lo;
 	if (b1 < 0)
@@ -159,9 +142,9 @@ __device__ void sgh_range_moments(const SghPix &P, int v1, int v2, int &cnt, lon
 		b2 = SGH_BINS - 1;
 	if (b1 > b2)
 		return;
-	uint32_t c32 = 0, s32 = 0, ss32 = 0;
+	uint32_t s32 = 0, ss32 = 0;
 	for (int j = b1 >> 2; j <= (b2 >> 2); j++) {
-		uint32_t d = P.L->hist[j][P.lane];
+		uint32_t d = P.L->hist[1 + j][P.lane];
 		const int first = 4 * j, last = 4 * j + 3;
 		if (first < b1)
 			d &= 0xFFFFFFFFu << (8 * (b1 - first));
@@ -171,11 +154,9 @@ __device__ void sgh_range_moments(const SghPix &P, int v1, int v2, int &cnt, lon
 		const uint32_t d1 = __builtin_amdgcn_udot4(d, 0x03020100u, 0u, false);
 		const uint32_t d2 = __builtin_amdgcn_udot4(d, 0x09040100u, 0u, false);
 		const uint32_t jj = (uint32_t)j;
-		c32 += bs;
 		s32 += 4u * jj * bs + d1;
 		ss32 += 16u * jj * jj * bs + 8u * jj * d1 + d2;
 	}
-	cnt += (int)c32;
 	s += (long long)s32;
 	ss += (unsigned long long)ss32;
 }
@@ -196,7 +177,7 @@ __device__ __forceinline__ int sgh_floor_clamp(double x) {
 }
 
 /* the reference's SIGMA loop on the histogram; returns SG_CLS_OK or 1 (redo in the
- * sorted kernel) */
+ * sorted kernel).  Decision logic mirrors clip_pass() of the sorted path. */
 __device__ int sgh_sigma(const SghPix &P, int N, double sl, double sh, long long S, unsigned long long SS,
 		uint16_t *value, uint32_t *rlo_out, uint32_t *rhi_out) {
 	int A = 0, B = 65535, n = N, r = 0, nrem;
@@ -209,8 +190,6 @@ __device__ int sgh_sigma(const SghPix &P, int N, double sl, double sh, long long
 		const int g1 = below + (n - 1) / 2, g2 = below + n / 2;
 		const int m1 = sgh_value_at(P, g1);
 		const int m2 = (g2 == g1) ? m1 : sgh_value_at(P, g2);
-		if (m1 < 0 || m2 < 0)
-			return 1;
 		const double median = (g1 == g2) ? (double)m1 : (double)(m1 + m2) / 2.0;
 		const double tl = sl * sigma, th = sh * sigma;
 		const double blo = median - tl, bhi = median + th;
@@ -253,19 +232,17 @@ __device__ int sgh_sigma(const SghPix &P, int N, double sl, double sh, long long
 		if (fb >= 0 && fb < n - 1)
 			return 1;
 		if (L) {
-			int c;
 			long long s;
 			unsigned long long ss;
-			sgh_range_moments(P, A, a - 1, c, s, ss);
+			sgh_range_moments(P, A, a - 1, s, ss);
 			S -= s;
 			SS -= ss;
 			A = a;
 		}
 		if (H) {
-			int c;
 			long long s;
 			unsigned long long ss;
-			sgh_range_moments(P, bt + 1, B, c, s, ss);
+			sgh_range_moments(P, bt + 1, B, s, ss);
 			S -= s;
 			SS -= ss;
 			B = bt;
@@ -283,7 +260,8 @@ __device__ int sgh_sigma(const SghPix &P, int N, double sl, double sh, long long
 	return SG_CLS_OK;
 }
 
-/* median of 16 values (the 9th smallest), bitonic network */
+/* centre estimate from 16 samples: median of those that are neither 0 nor 65535 (the
+ * out-of-frame zero fill of edge pixels must not drag the band away), bitonic network */
 __device__ __forceinline__ uint32_t sgh_median16(const uint32_t (&in)[SGH_CENTER]) {
 	uint32_t v[SGH_CENTER];
 #pragma unroll
@@ -306,79 +284,103 @@ __device__ __forceinline__ uint32_t sgh_median16(const uint32_t (&in)[SGH_CENTER
 			}
 		}
 	}
-	return v[SGH_CENTER / 2];
+	int z = 0, sat = 0;
+#pragma unroll
+	for (int i = 0; i < SGH_CENTER; i++) {
+		z += v[i] == 0;
+		sat += v[i] == 65535;
+	}
+	int idx = z + (SGH_CENTER - z - sat) / 2;
+	if (idx > SGH_CENTER - 1)
+		idx = SGH_CENTER - 1;
+	uint32_t r = v[0];
+#pragma unroll
+	for (int i = 1; i < SGH_CENTER; i++)
+		r = (i == idx) ? v[i] : r;
+	return r;
 }
 
-__device__ __forceinline__ void sgh_add(SghLds &L, int lane, int lo, uint32_t v, uint32_t &nb,
-		long long &ts, unsigned long long &tq) {
-	const uint32_t b = v - (uint32_t)lo;
-	if (b < SGH_BINS) {
-		atomicAdd(&L.hist[b >> 2][lane], 1u << ((b & 3) * 8));
-		nb++;
-	} else {
-		if (v == 0) {
-			atomicAdd(&L.nzero[lane], 1u);
-		} else if (v == 65535) {
-			atomicAdd(&L.nsat[lane], 1u);
-		} else {
-			const int side = (int)v < lo ? 0 : 1;
-			const uint32_t slot = atomicAdd(&L.ntail[side][lane], 1u);
-			if (slot < SGH_T)
-				L.tails[side][slot][lane] = (uint16_t)v;
-		}
-		const long long d = (long long)v - lo;
-		ts += d;
-		tq += (unsigned long long)(d * d);
+/* per-frame load context: each frame gets its own buffer descriptor (num_records = one
+ * plane) so that any offset outside the plane reads 0 through the hardware bounds check */
+struct SghFrame {
+	const char *plane0;		/* channel plane of frame 0 */
+	int64_t fstride2;		/* bytes between frames */
+	uint32_t plane_bytes;
+	int rw2;			/* R * W * 2 */
+	int w2;				/* W * 2 */
+	uint32_t x2;			/* 2 * x (per lane) */
+};
+
+/* one sample: c1 = shifty*W*2 + 2*shiftx, sx2 = 2*shiftx (per-frame table, read from LDS
+ * as wave-uniform VGPR values); byte offset (R - sy) W 2 + 2 (x - sx): a row outside the
+ * frame gives a negative (huge) or past-the-plane offset -> 0 (the zero rows of
+ * :1550-1577); the column check forces an out-of-range offset (the x shift writes 0,
+ * :1628-1632) */
+__device__ __forceinline__ uint32_t sgh_load(const SghFrame &F, const char *base, uint32_t nrec, int c1, int sx2) {
+	const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)nrec, 0x00020000);
+	const uint32_t sc2 = F.x2 - (uint32_t)sx2;
+	const uint32_t voff = sc2 < (uint32_t)F.w2 ? (uint32_t)(F.rw2 - c1) + F.x2 : 0x80000000u;
+	return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rsrc, (int)voff, 0, 0);
+}
+
+/* 16 frames f0..f0+15 (f0 % 16 == 0) into 8 packed pairs; tab = LDS copy of
+ * p.hist_tab (int2 {c1, sx2} per frame, zero padded to a multiple of 16 frames); frames
+ * >= N get num_records = 0 (every lane reads 0; never binned) */
+template <bool FULL>
+__device__ __forceinline__ void sgh_load16(const SghFrame &F, const int *tab, int N, int f0, uint32_t (&dst)[8]) {
+	const int4 *q = (const int4 *)(tab + 2 * f0);
+	int4 t[8];
+#pragma unroll
+	for (int i = 0; i < 8; i++)
+		t[i] = q[i];
+	const char *b = F.plane0 + (int64_t)f0 * F.fstride2;
+#pragma unroll
+	for (int m = 0; m < 8; m++) {
+		const uint32_t na = (FULL || f0 + 2 * m < N) ? F.plane_bytes : 0u;
+		const uint32_t nb = (FULL || f0 + 2 * m + 1 < N) ? F.plane_bytes : 0u;
+		const uint32_t va = sgh_load(F, b, na, t[m].x, t[m].y);
+		b += F.fstride2;
+		const uint32_t vb = sgh_load(F, b, nb, t[m].z, t[m].w);
+		b += F.fstride2;
+		dst[m] = va | (vb << 16);
 	}
 }
 
-/* sample of frame f at (c, R, x) without normalisation (NO_NORM fast path): the y
- * shifted band read leaves zero rows, the x shift writes 0 (:1550-1577, :1628-1632).
- * f and sh (packed shift (shiftx & 0xffff) | shifty << 16) are wave-uniform: the row
- * address is scalar, the column offset per lane; out-of-frame samples load a valid
- * address and are masked to 0 (no divergent branch, so the loads stay in flight). */
-__device__ __forceinline__ uint32_t sgh_load(const SgStackParams &p, const uint16_t *plane0, int f, int sh,
-		int R, int x) {
-	const int sx = (int)(int16_t)(sh & 0xFFFF);
-	const int sy = sh >> 16;
-	const int sr = R - sy;
-	const bool rowok = (unsigned)sr < (unsigned)p.H;
-	const uint16_t *rowp = plane0 + (int64_t)f * p.frame_stride + (int64_t)sr * p.W;
-	const int sc = x - sx;
-	const bool ok = rowok && (unsigned)sc < (unsigned)p.W;
-	/* invalid samples read a zero page instead of being masked after the load */
-	const uint16_t *a = ok ? rowp + sc : p.zeros + (threadIdx.x & 63);
-	return *a;
-}
-
-__device__ __forceinline__ int sgh_shift(const SgStackParams &p, int f) {
-	return p.use_shift ? __builtin_amdgcn_readfirstlane(p.shiftxy[f]) : 0;
-}
-
-/* packed shifts of 16 consecutive frames f0..f0+15 (f0 % 16 == 0; the table is padded
- * to a multiple of 16 entries and 64-byte aligned): 4 scalar dwordx4 loads */
-__device__ __forceinline__ void sgh_shift16(const SgStackParams &p, int f0, int (&sh)[16]) {
-	if (!p.use_shift) {
-#pragma unroll
-		for (int m = 0; m < 16; m++)
-			sh[m] = 0;
+/* bin a pair of samples (two frames of this lane's pixel, 16-bit halves of vv) */
+__device__ __forceinline__ void sgh_bin_pair(SghLds &L, uint32_t laneaddr, uint32_t lo1x2, uint32_t vv,
+		uint32_t &nonzero, uint32_t &nsat, int dbg) {
+	const sgh_u16x2 v = __builtin_bit_cast(sgh_u16x2, vv);
+	if (dbg == 3) {		/* A/B: loads only */
+		nonzero += vv;
 		return;
 	}
-	const int4 *q = (const int4 *)(p.shiftxy + f0);
-#pragma unroll
-	for (int i = 0; i < 4; i++) {
-		const int4 t = q[i];
-		sh[4 * i] = __builtin_amdgcn_readfirstlane(t.x);
-		sh[4 * i + 1] = __builtin_amdgcn_readfirstlane(t.y);
-		sh[4 * i + 2] = __builtin_amdgcn_readfirstlane(t.z);
-		sh[4 * i + 3] = __builtin_amdgcn_readfirstlane(t.w);
-	}
+	const sgh_u16x2 l1 = __builtin_bit_cast(sgh_u16x2, lo1x2);
+	sgh_u16x2 t = __builtin_elementwise_sub_sat(v, l1);	/* 0 below the band, 1..256 inside */
+	t = __builtin_elementwise_min(t, (sgh_u16x2){257, 257});
+	/* 0 below (dword 0, a u32 counter), 4..259 band, 260 above (dword 65, u32) */
+	t = t + __builtin_elementwise_min(t, (sgh_u16x2){1, 1}) * (sgh_u16x2){3, 3};
+	const uint32_t tt = __builtin_bit_cast(uint32_t, t);
+	const uint32_t t3 = tt << 3;
+	const uint32_t a0 = (__builtin_amdgcn_ubfe(tt, 2, 8) << 8) + laneaddr;
+	const uint32_t a1 = (__builtin_amdgcn_ubfe(tt, 18, 8) << 8) + laneaddr;
+	const uint32_t i0 = 1u << (t3 & 24u);
+	const uint32_t i1 = 1u << __builtin_amdgcn_ubfe(t3, 16, 5);
+	uint32_t *h = &L.hist[0][0];
+	atomicAdd(h + (a0 >> 2), i0);
+	atomicAdd(h + (a1 >> 2), i1);
+	/* nonzero samples and 65535 samples of the pair */
+	const sgh_u16x2 nzv = __builtin_elementwise_min(v, (sgh_u16x2){1, 1});
+	const sgh_u16x2 sv = __builtin_elementwise_sub_sat(v, (sgh_u16x2){65534, 65534});
+	nonzero = __builtin_amdgcn_udot2(nzv, (sgh_u16x2){1, 1}, nonzero, false);
+	nsat = __builtin_amdgcn_udot2(sv, (sgh_u16x2){1, 1}, nsat, false);
 }
 
 __global__ void __launch_bounds__(64 * SGH_WAVES)
 k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
 	__shared__ SghLds L;
-	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+	extern __shared__ __attribute__((aligned(16))) int tabL[];	/* int2 per frame, Npad frames */
+	const int tid = threadIdx.x, lane = tid & 63;
+	const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 	const int ntx = (p.W + SG_TILE_W - 1) / SG_TILE_W;
 	const int nrows = p.row_end - p.row_begin;
 	int bid = blockIdx.x;
@@ -388,90 +390,117 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 	const int c = bid / nrows;
 	const int x = xt * SG_TILE_W + lane;
 	const int N = p.N;
-	const uint16_t *plane0 = p.frames + (int64_t)c * p.plane_stride;
+	const int Npad = (N + 15) & ~15;
+	SghFrame F;
+	F.plane0 = (const char *)(p.frames + (int64_t)c * p.plane_stride);
+	F.fstride2 = p.frame_stride * 2;
+	F.plane_bytes = (uint32_t)p.H * (uint32_t)p.W * 2u;
+	F.w2 = p.W * 2;
+	F.rw2 = R * p.W * 2;
+	F.x2 = (uint32_t)x * 2u;
 
-	/* zero the histograms and counters */
-	for (int i = tid; i < SGH_DW * 64; i += 64 * SGH_WAVES)
+	for (int i = tid; i < (SGH_DW + 2) * 64; i += 64 * SGH_WAVES)
 		(&L.hist[0][0])[i] = 0;
 	if (tid < 64) {
-		L.ntail[0][tid] = 0;
-		L.ntail[1][tid] = 0;
-		L.nband[tid] = 0;
-		L.nzero[tid] = 0;
-		L.nsat[tid] = 0;
-		L.tsum[tid] = 0;
-		L.tsq[tid] = 0;
+		L.nz[tid] = 0;
+		L.ns[tid] = 0;
 	}
-	/* centre: median of the first 16 samples (every wave computes it identically) */
-	uint32_t v16[SGH_CENTER];
-#pragma unroll
-	for (int k = 0; k < SGH_CENTER; k++)
-		v16[k] = sgh_load(p, plane0, k, sgh_shift(p, k), R, x);
-	int lo = (int)sgh_median16(v16) - SGH_BINS / 2;
-	if (lo < 0)
-		lo = 0;
-	if (lo > 65536 - SGH_BINS)
-		lo = 65536 - SGH_BINS;
+	{
+		const int4 *src = (const int4 *)p.hist_tab;
+		int4 *dst = (int4 *)tabL;
+		for (int i = tid; i < Npad / 2; i += 64 * SGH_WAVES)
+			dst[i] = src[i];
+	}
 	__syncthreads();
 
-	uint32_t nb = 0;
-	long long ts = 0;
-	unsigned long long tq = 0;
-	/* frames in chunks of 64: wave w bins frames [g0 + 16w, g0 + 16w + 16); the next
-	 * chunk's 16 loads are issued before the current 16 samples are binned.  Frames
-	 * 0..15 are wave 0's first block (already loaded for the centre). */
-	constexpr int M = 16;
-	const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-	auto load16 = [&](int f0, uint32_t(&dst)[M]) {
-		int sh[M];
-		sgh_shift16(p, f0, sh);
-#pragma unroll
-		for (int m = 0; m < M; m++) {
-			const int f = f0 + m < N ? f0 + m : N - 1;
-			dst[m] = sgh_load(p, plane0, f, sh[m], R, x);
-		}
+	constexpr int M = 16, MP = M / 2;
+	auto load16 = [&](int f0, uint32_t (&dst)[MP]) {
+		if (f0 + M <= N)
+			sgh_load16<true>(F, tabL, N, f0, dst);
+		else
+			sgh_load16<false>(F, tabL, N, f0, dst);
 	};
-	auto add16 = [&](int f0, const uint32_t(&src)[M]) {
+	/* 16-frame blocks: wave w bins blocks w, w+4, ...; block 0 (frames 0..15) also gives
+	 * the centre (every wave loads it).  Two named buffers keep the next block's 16 loads
+	 * in flight while the current one is binned. */
+	uint32_t p16[MP], bufA[MP], bufB[MP];
+	sgh_load16<true>(F, tabL, N, 0, p16);
+	int fb = M * wave;
+	if (fb != 0 && fb < N)
+		load16(fb, bufA);
+	/* centre: median of the first 16 samples */
+	uint32_t v16[SGH_CENTER];
 #pragma unroll
-		for (int m = 0; m < M; m++)
-			if (f0 + m < N)
-				sgh_add(L, lane, lo, src[m], nb, ts, tq);
-	};
-	/* two named buffers: the loads of block k+1 are in flight while block k is binned */
-	uint32_t bufA[M], bufB[M];
-	int fb = M * wave_u;
+	for (int k = 0; k < SGH_CENTER / 2; k++) {
+		v16[2 * k] = p16[k] & 0xFFFFu;
+		v16[2 * k + 1] = p16[k] >> 16;
+	}
+	int lo = (int)sgh_median16(v16) - SGH_BINS / 2;
+	if (lo < 1)
+		lo = 1;
+	if (lo > 65535 - SGH_BINS)
+		lo = 65535 - SGH_BINS;
 	if (fb == 0) {
 #pragma unroll
-		for (int m = 0; m < M; m++)
-			bufA[m] = v16[m];
-	} else if (fb < N) {
-		load16(fb, bufA);
+		for (int m = 0; m < MP; m++)
+			bufA[m] = p16[m];
 	}
-	/* the prefetch is unconditional (the last block re-loads itself) so no register
-	 * merge forces the compiler to wait for it before binning */
+
+	const uint32_t laneaddr = (uint32_t)lane * 4u;
+	const uint32_t lo1x2 = (uint32_t)(lo - 1) * 0x10001u;
+	uint32_t nonzero = 0, nsat = 0, counted = 0;
+	auto bin16 = [&](int f0, const uint32_t (&src)[MP]) {
+		if (f0 + M <= N) {
+#pragma unroll
+			for (int m = 0; m < MP; m++)
+				sgh_bin_pair(L, laneaddr, lo1x2, src[m], nonzero, nsat, p.dbg);
+			counted += M;
+		} else {
+			/* partial last block: a lone frame is paired with a 65535 sample whose count
+			 * is taken back below */
+			for (int m = 0; m < MP; m++) {
+				const int fa = f0 + 2 * m;
+				if (fa >= N)
+					break;
+				const uint32_t vv = fa + 1 < N ? src[m] : ((src[m] & 0xFFFFu) | 0xFFFF0000u);
+				sgh_bin_pair(L, laneaddr, lo1x2, vv, nonzero, nsat, p.dbg);
+				counted += 2;
+				if (fa + 1 >= N) {
+					atomicSub(&L.hist[SGH_DW + 1][lane], 1u);	/* the padding 65535 */
+					nsat--;
+					nonzero--;
+					counted--;
+				}
+			}
+		}
+	};
 	while (fb < N) {
 		load16(fb + 64 < N ? fb + 64 : fb, bufB);
-		add16(fb, bufA);
+		bin16(fb, bufA);
 		fb += 64;
 		if (fb >= N)
 			break;
 		load16(fb + 64 < N ? fb + 64 : fb, bufA);
-		add16(fb, bufB);
+		bin16(fb, bufB);
 		fb += 64;
 	}
-	atomicAdd(&L.nband[lane], nb);
-	if (ts)
-		atomicAdd(&L.tsum[lane], (unsigned long long)ts);
-	if (tq)
-		atomicAdd(&L.tsq[lane], tq);
+	if (counted) {
+		atomicAdd(&L.nz[lane], counted - nonzero);
+		atomicAdd(&L.ns[lane], nsat);
+	}
 	__syncthreads();
 	if (wave != 0)
 		return;
 
+	if (p.dbg >= 2) {
+		if (x < p.W)
+			p.out[((int64_t)c * p.H + R) * p.W + x] = (uint16_t)(L.hist[1][lane] + nonzero);
+		return;
+	}
 	/* wave 0: prefix counts + band moments (relative to lo) */
 	uint32_t cum = 0, s32 = 0, ss32 = 0;
 	for (int j = 0; j < SGH_DW; j++) {
-		const uint32_t d = L.hist[j][lane];
+		const uint32_t d = L.hist[1 + j][lane];
 		const uint32_t bs = __builtin_amdgcn_sad_u8(d, 0u, 0u);
 		const uint32_t d1 = __builtin_amdgcn_udot4(d, 0x03020100u, 0u, false);
 		const uint32_t d2 = __builtin_amdgcn_udot4(d, 0x09040100u, 0u, false);
@@ -479,28 +508,35 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 		s32 += 4u * jj * bs + d1;
 		ss32 += 16u * jj * jj * bs + 8u * jj * d1 + d2;
 		cum += bs;
-		L.cumdw[j][lane] = (uint16_t)cum;
+		if ((j & 3) == 3)
+			L.cum16[j >> 2][lane] = (uint16_t)cum;
 	}
+	const int below = (int)L.hist[0][lane];
+	const int above = (int)L.hist[SGH_DW + 1][lane];
 	SghPix P;
 	P.lo = lo;
-	P.nll = (int)L.ntail[0][lane];
-	P.nhl = (int)L.ntail[1][lane];
-	P.nz = (int)L.nzero[lane];
-	P.ns = (int)L.nsat[lane];
-	P.nlo = P.nll + P.nz;
-	P.nhi = P.nhl + P.ns;
-	P.nb = (int)L.nband[lane];
+	P.nz = (int)L.nz[lane];
+	P.ns = (int)L.ns[lane];
+	P.nb = (int)cum;
 	P.lane = lane;
 	P.L = &L;
 	int cls = SG_CLS_OK;
 	uint16_t value = 0;
 	uint32_t rlo = 0, rhi = 0;
 	if (x < p.W) {
-		if ((int)cum != P.nb || P.nll > SGH_T || P.nhl > SGH_T)
-			cls = 1;	/* u8 bin overflow or tail overflow */
-		else
-			cls = sgh_sigma(P, N, p.sig0, p.sig1, (long long)s32 + (long long)L.tsum[lane],
-					(unsigned long long)ss32 + L.tsq[lane], &value, &rlo, &rhi);
+		/* every out-of-band sample must be a 0 or a 65535, and no counter may have wrapped */
+		if (p.dbg == 1) {
+			value = (uint16_t)(s32 + ss32);
+		} else if (below + P.nb + above != N || below != P.nz || above != P.ns) {
+			cls = 1;
+		} else {
+			const long long dz = -(long long)lo, ds = 65535 - (long long)lo;
+			const long long S = (long long)s32 + dz * P.nz + ds * P.ns;
+			const unsigned long long SS = (unsigned long long)ss32 +
+				(unsigned long long)(dz * dz) * (unsigned long long)P.nz +
+				(unsigned long long)(ds * ds) * (unsigned long long)P.ns;
+			cls = sgh_sigma(P, N, p.sig0, p.sig1, S, SS, &value, &rlo, &rhi);
+		}
 		const int64_t pix = ((int64_t)c * p.H + R) * p.W + x;
 		if (cls == SG_CLS_OK) {
 			p.out[pix] = value;

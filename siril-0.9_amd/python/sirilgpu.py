@@ -99,7 +99,7 @@ def load():
     lib.sg_get_last_stats.restype = ctypes.c_int
     lib.sg_synth_fill_device.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
-                                         ctypes.c_int, P]
+                                         ctypes.c_int, ctypes.c_int64, P]
     lib.sg_synth_fill_device.restype = ctypes.c_int
     lib.sg_register_dft_u16.argtypes = [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, P]
     lib.sg_register_dft_u16.restype = ctypes.c_int
@@ -245,7 +245,8 @@ class Context:
         self.check(rc, "sg_register_dft_u16_device")
         return sx, sy, q
 
-    def synth_fill(self, d_frames, nframes, C, H, W, row_begin, row_end, seed, maxshift, dev_index=0):
+    def synth_fill(self, d_frames, nframes, C, H, W, row_begin, row_end, seed, maxshift, dev_index=0,
+                   frame_stride=0):
         rc = self.lib.sg_synth_fill_device(self.ctx, dev_index, ctypes.c_void_p(d_frames), nframes, C, H, W,
-                                           row_begin, row_end, seed, maxshift, None)
+                                           row_begin, row_end, seed, maxshift, frame_stride, None)
         self.check(rc, "sg_synth_fill_device")
