@@ -147,11 +147,9 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        r = torch.tensor(rej_tot.astype(np.int64).reshape(-1), device="cuda")
-        dist.all_reduce(r)
+        import sirilgpu_dist as sd
+        elapsed = sd.max_time(elapsed, dist, device="cuda")
+        rej_tot = sd.sum_counters(rej_tot, dist, device="cuda")
     ms_step = elapsed / args.steps * 1e3
     frames_per_s = N * world / (elapsed / args.steps)
     kavg = sum(kms) / len(kms)

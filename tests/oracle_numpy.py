@@ -198,9 +198,10 @@ def reject_pixel(stack, rejected, rejection, sig, crej):
     return round_to_word(fdiv(s, float(N)))
 
 
-def stack_rejection_1thread(frames, rejection, sig, shiftx=None, shifty=None):
+def stack_rejection_1thread(frames, rejection, sig, shiftx=None, shifty=None, rows=None):
     """stack_mean_with_rejection with one OpenMP thread and one block per channel-quarter
-    order (blocks top-down, channel-major); frames [N][C][H][W] memory order (bottom-up)."""
+    order (blocks top-down, channel-major); frames [N][C][H][W] memory order (bottom-up).
+    rows = (begin, end): only memory rows [begin, end) (a row band), others stay 0."""
     N, C, H, W = frames.shape
     out = np.zeros((C, H, W), dtype=np.uint16)
     rej = np.zeros((3, 2), dtype=np.uint64)
@@ -208,6 +209,8 @@ def stack_rejection_1thread(frames, rejection, sig, shiftx=None, shifty=None):
     for c in range(C):
         for t in range(H):              # top-down rows, as the block loop visits them
             R = H - 1 - t
+            if rows is not None and not (rows[0] <= R < rows[1]):
+                continue
             crej = [0, 0]
             for x in range(W):
                 col = []

@@ -1,0 +1,54 @@
+"""Multi-rank path on CPU (gloo, world size 2): row-band sharding of the stack
+(siril-0.9_amd/python/sirilgpu_dist.py) must reassemble exactly the single-process image
+and rejection counters.  The per-band stacker here is the numpy restatement (test
+infrastructure); on the GPU node it is sg_stack_u16_device with row_begin/row_end."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_lib as orc
+import oracle_numpy as onp
+import sirilgpu_dist as sd
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_row_band_sharding_gloo(world, tmp_path):
+    N, C, H, W = 10, 1, 13, 9
+    frames = orc.synth(N, C, H, W, seed=17, maxshift=2)
+    sx, sy = orc.synth_shifts(N, seed=17, maxshift=2)
+    full, full_rej = onp.stack_rejection_1thread(frames, 2, (3.0, 3.0), sx, sy)
+    inp = tmp_path / "in.npz"
+    np.savez(inp, frames=frames, sx=sx, sy=sy)
+    port = _free_port()
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_worker.py")
+    procs = [subprocess.Popen([sys.executable, worker, str(r), str(world), str(port), str(inp),
+                               str(tmp_path / f"out{r}.npz")]) for r in range(world)]
+    for p in procs:
+        assert p.wait(timeout=180) == 0
+    for r in range(world):
+        d = np.load(tmp_path / f"out{r}.npz", allow_pickle=False)
+        assert np.array_equal(d["img"], full), r
+        assert np.array_equal(d["rej"], full_rej), (d["rej"], full_rej)
+        assert float(d["t"]) == 0.5 + (world - 1)
+
+
+def test_row_band_partition():
+    for H in (1, 7, 4096, 4097):
+        for world in (1, 2, 3, 8):
+            bands = [sd.row_band(r, world, H) for r in range(world)]
+            assert bands[0][0] == 0 and bands[-1][1] == H
+            assert all(bands[i][1] == bands[i + 1][0] for i in range(world - 1))
+            sizes = [e - b for b, e in bands]
+            assert max(sizes) - min(sizes) <= 1
