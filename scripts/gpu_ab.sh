@@ -5,7 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-for cfg in "0 0" "1 0" "2 0" "3 0"; do
+for cfg in "0 0" "2 0" "3 0"; do
   set -- $cfg
   SG_HIST_DBG=$1 timeout -k 10 200 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --frame-pad $2 > gpurun_out/ab_$1_$2.log 2>&1 || { echo "ab $cfg failed"; tail -5 gpurun_out/ab_$1_$2.log; exit 3; }
   python3 -c "import json;d=json.loads(open('gpurun_out/ab_$1_$2.log').read().splitlines()[-1]);print('dbg=$1 pad=$2', d['kernel_ms'], d['ms_per_step'], d['roofline']['achieved'], d['redo_pixels'])"

@@ -180,14 +180,14 @@ __device__ __forceinline__ int sgh_floor_clamp(double x) {
  * sorted kernel).  Decision logic mirrors clip_pass() of the sorted path. */
 __device__ int sgh_sigma(const SghPix &P, int N, double sl, double sh, long long S, unsigned long long SS,
 		uint16_t *value, uint32_t *rlo_out, uint32_t *rhi_out) {
-	int A = 0, B = 65535, n = N, r = 0, nrem;
+	/* kept set = samples with A <= v <= B; cntA = # samples < A, cntB = # samples <= B */
+	int A = 0, B = 65535, n = N, r = 0, nrem, cntA = 0, cntB = N;
 	uint32_t rlo = 0, rhi = 0;
 	do {
 		const long long num = (long long)n * (long long)SS - S * S;
 		const bool exact0 = (num == 0);
 		const double sigma = num <= 0 ? 0.0 : sqrt((double)num / ((double)n * (double)(n - 1)));
-		const int below = sgh_cnt_le(P, A - 1);
-		const int g1 = below + (n - 1) / 2, g2 = below + n / 2;
+		const int g1 = cntA + (n - 1) / 2, g2 = cntA + n / 2;
 		const int m1 = sgh_value_at(P, g1);
 		const int m2 = (g2 == g1) ? m1 : sgh_value_at(P, g2);
 		const double median = (g1 == g2) ? (double)m1 : (double)(m1 + m2) / 2.0;
@@ -201,23 +201,21 @@ __device__ int sgh_sigma(const SghPix &P, int N, double sl, double sh, long long
 		int bt = sgh_floor_clamp(bhi + tol);
 		if (bt > B)
 			bt = B;
+		const int cnt_a = a > A ? sgh_cnt_le(P, a - 1) : cntA;	/* # < a */
+		const int cnt_bt = bt < B ? sgh_cnt_le(P, bt) : cntB;	/* # <= bt */
 		if (!exact0) {
 			int amb1 = sgh_floor_clamp(blo + tol);
 			if (amb1 > B)
 				amb1 = B;
-			if (a <= amb1 && sgh_cnt_le(P, amb1) - sgh_cnt_le(P, a - 1) > 0)
+			if (a <= amb1 && sgh_cnt_le(P, amb1) - cnt_a > 0)
 				return 1;
 			int amb0 = sgh_ceil_clamp(bhi - tol);
 			if (amb0 < A)
 				amb0 = A;
-			if (amb0 <= bt && sgh_cnt_le(P, bt) - sgh_cnt_le(P, amb0 - 1) > 0)
+			if (amb0 <= bt && cnt_bt - sgh_cnt_le(P, amb0 - 1) > 0)
 				return 1;
 		}
-		int L = 0, H = 0;
-		if (a > A)
-			L = sgh_cnt_le(P, a - 1) - below;
-		if (bt < B)
-			H = sgh_cnt_le(P, B) - sgh_cnt_le(P, bt);
+		const int L = cnt_a - cntA, H = cntB - cnt_bt;
 		if (L + H > n)
 			return 1;
 		/* `if (N - r <= 4) break;` inside the clipping loop (:1684) */
@@ -238,6 +236,7 @@ __device__ int sgh_sigma(const SghPix &P, int N, double sl, double sh, long long
 			S -= s;
 			SS -= ss;
 			A = a;
+			cntA = cnt_a;
 		}
 		if (H) {
 			long long s;
@@ -246,6 +245,7 @@ __device__ int sgh_sigma(const SghPix &P, int N, double sl, double sh, long long
 			S -= s;
 			SS -= ss;
 			B = bt;
+			cntB = cnt_bt;
 		}
 		rlo += L;
 		rhi += H;
@@ -323,19 +323,19 @@ __device__ __forceinline__ uint32_t sgh_load(const SghFrame &F, const char *base
 	return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rsrc, (int)voff, 0, 0);
 }
 
-/* 16 frames f0..f0+15 (f0 % 16 == 0) into 8 packed pairs; tab = LDS copy of
- * p.hist_tab (int2 {c1, sx2} per frame, zero padded to a multiple of 16 frames); frames
- * >= N get num_records = 0 (every lane reads 0; never binned) */
-template <bool FULL>
-__device__ __forceinline__ void sgh_load16(const SghFrame &F, const int *tab, int N, int f0, uint32_t (&dst)[8]) {
+/* NP*2 frames f0.. (f0 % 8 == 0) into NP packed pairs; tab = LDS copy of p.hist_tab
+ * (int2 {c1, sx2} per frame, zero padded to a multiple of 16 frames); frames >= N get
+ * num_records = 0 (every lane reads 0; never binned) */
+template <int NP, bool FULL>
+__device__ __forceinline__ void sgh_loadblk(const SghFrame &F, const int *tab, int N, int f0, uint32_t (&dst)[NP]) {
 	const int4 *q = (const int4 *)(tab + 2 * f0);
-	int4 t[8];
+	int4 t[NP];
 #pragma unroll
-	for (int i = 0; i < 8; i++)
+	for (int i = 0; i < NP; i++)
 		t[i] = q[i];
 	const char *b = F.plane0 + (int64_t)f0 * F.fstride2;
 #pragma unroll
-	for (int m = 0; m < 8; m++) {
+	for (int m = 0; m < NP; m++) {
 		const uint32_t na = (FULL || f0 + 2 * m < N) ? F.plane_bytes : 0u;
 		const uint32_t nb = (FULL || f0 + 2 * m + 1 < N) ? F.plane_bytes : 0u;
 		const uint32_t va = sgh_load(F, b, na, t[m].x, t[m].y);
@@ -413,21 +413,21 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 	}
 	__syncthreads();
 
-	constexpr int M = 16, MP = M / 2;
-	auto load16 = [&](int f0, uint32_t (&dst)[MP]) {
+	constexpr int M = 16, MP = M / 2;	/* frames per block, packed pairs per block */
+	auto loadblk = [&](int f0, uint32_t (&dst)[MP]) {
 		if (f0 + M <= N)
-			sgh_load16<true>(F, tabL, N, f0, dst);
+			sgh_loadblk<MP, true>(F, tabL, N, f0, dst);
 		else
-			sgh_load16<false>(F, tabL, N, f0, dst);
+			sgh_loadblk<MP, false>(F, tabL, N, f0, dst);
 	};
-	/* 16-frame blocks: wave w bins blocks w, w+4, ...; block 0 (frames 0..15) also gives
-	 * the centre (every wave loads it).  Two named buffers keep the next block's 16 loads
+	/* 16-frame blocks: wave w bins blocks w, w+4, ...; frames 0..15 (block 0) are the
+	 * centre sample every wave loads.  Two named buffers keep the next block's loads
 	 * in flight while the current one is binned. */
-	uint32_t p16[MP], bufA[MP], bufB[MP];
-	sgh_load16<true>(F, tabL, N, 0, p16);
+	uint32_t p16[SGH_CENTER / 2], bufA[MP], bufB[MP];
+	sgh_loadblk<SGH_CENTER / 2, true>(F, tabL, N, 0, p16);
 	int fb = M * wave;
-	if (fb != 0 && fb < N)
-		load16(fb, bufA);
+	if (fb >= SGH_CENTER && fb < N)
+		loadblk(fb, bufA);
 	/* centre: median of the first 16 samples */
 	uint32_t v16[SGH_CENTER];
 #pragma unroll
@@ -440,16 +440,16 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 		lo = 1;
 	if (lo > 65535 - SGH_BINS)
 		lo = 65535 - SGH_BINS;
-	if (fb == 0) {
+	if (fb < SGH_CENTER) {
 #pragma unroll
 		for (int m = 0; m < MP; m++)
-			bufA[m] = p16[m];
+			bufA[m] = p16[(fb / 2) + m];
 	}
 
 	const uint32_t laneaddr = (uint32_t)lane * 4u;
 	const uint32_t lo1x2 = (uint32_t)(lo - 1) * 0x10001u;
 	uint32_t nonzero = 0, nsat = 0, counted = 0;
-	auto bin16 = [&](int f0, const uint32_t (&src)[MP]) {
+	auto binblk = [&](int f0, const uint32_t (&src)[MP]) {
 		if (f0 + M <= N) {
 #pragma unroll
 			for (int m = 0; m < MP; m++)
@@ -474,15 +474,16 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 			}
 		}
 	};
+	constexpr int STEP = M * SGH_WAVES;
 	while (fb < N) {
-		load16(fb + 64 < N ? fb + 64 : fb, bufB);
-		bin16(fb, bufA);
-		fb += 64;
+		loadblk(fb + STEP < N ? fb + STEP : fb, bufB);
+		binblk(fb, bufA);
+		fb += STEP;
 		if (fb >= N)
 			break;
-		load16(fb + 64 < N ? fb + 64 : fb, bufA);
-		bin16(fb, bufB);
-		fb += 64;
+		loadblk(fb + STEP < N ? fb + STEP : fb, bufA);
+		binblk(fb, bufB);
+		fb += STEP;
 	}
 	if (counted) {
 		atomicAdd(&L.nz[lane], counted - nonzero);
@@ -499,6 +500,7 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 	}
 	/* wave 0: prefix counts + band moments (relative to lo) */
 	uint32_t cum = 0, s32 = 0, ss32 = 0;
+#pragma unroll 16
 	for (int j = 0; j < SGH_DW; j++) {
 		const uint32_t d = L.hist[1 + j][lane];
 		const uint32_t bs = __builtin_amdgcn_sad_u8(d, 0u, 0u);
