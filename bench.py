@@ -37,6 +37,7 @@ def parse():
     ap.add_argument("--height", type=int, default=4096)
     ap.add_argument("--rejection", default="sigma")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--maxshift", type=int, default=16, help="synthetic registration shift range")
     ap.add_argument("--frame-pad", type=int, default=0,
                     help="extra elements between frames in HBM (breaks power-of-two frame strides)")
     ap.add_argument("--cpu-rows", type=int, default=1024, help="rows of the CPU baseline sample")
@@ -99,7 +100,7 @@ def main():
     fstride = H * W + args.frame_pad
     frames = torch.empty(N * fstride, dtype=torch.int16, device="cuda")
     out = torch.empty(H * W, dtype=torch.int16, device="cuda")
-    ctx.synth_fill(frames.data_ptr(), N, 1, H, W, 0, H, 0x5151 + rank, 16, frame_stride=fstride)
+    ctx.synth_fill(frames.data_ptr(), N, 1, H, W, 0, H, 0x5151 + rank, args.maxshift, frame_stride=fstride)
     import ctypes
     sx = (ctypes.c_int * N)()
     sy = (ctypes.c_int * N)()
@@ -117,8 +118,10 @@ def main():
     shy = np.zeros(N, dtype=np.int32)
     for f in range(1, N):
         h = mix64(seed ^ 0x51B1 ^ (f << 32))
-        shx[f] = -((h & 0xFFFFFFFF) % 33 - 16)
-        shy[f] = -(((h >> 32) & 0xFFFFFFFF) % 33 - 16)
+        if args.maxshift > 0:
+            span = 2 * args.maxshift + 1
+            shx[f] = -((h & 0xFFFFFFFF) % span - args.maxshift)
+            shy[f] = -(((h >> 32) & 0xFFFFFFFF) % span - args.maxshift)
     desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=rej_mode, sig=(4.0, 3.0),
                               shiftx=shx, shifty=shy, max_thread=8, max_number_of_rows=H)
 

@@ -247,30 +247,33 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 
 	/* per-frame constants: shifts + normalisation coefficients */
 	const int Npad = (N + 15) & ~15;	/* histogram-path table: 64-byte aligned, padded */
-	HIPCHK(ensure(dv.shifts, sizeof(int) * (2 * Npad + 2 * N)));
+	/* layout: c1[Npad] int, sx2[Npad] int16, shiftx[N], shifty[N] */
+	HIPCHK(ensure(dv.shifts, sizeof(int) * (Npad + Npad / 2 + 2 * N)));
 	HIPCHK(ensure(dv.norm, sizeof(double) * 3 * N));
 	/* the histogram path addresses a frame plane with 32-bit offsets: (R - sy) W 2 must fit */
 	bool hist_addr_ok = (int64_t)H * W * 2 <= (1ll << 30);
 	{
-		/* per frame {shifty*W*2 + 2*shiftx, 2*shiftx} for the histogram path (zeros when
-		 * there is no registration data), then the plain shift arrays */
-		std::vector<int> sh(2 * Npad + 2 * N, 0);
+		/* per frame c1 = shifty*W*2 + 2*shiftx and sx2 = 2*shiftx for the histogram path
+		 * (zeros when there is no registration data), then the plain shift arrays */
+		std::vector<int> sh(Npad + Npad / 2 + 2 * N, 0);
+		int16_t *sx2 = (int16_t *)(sh.data() + Npad);
 		for (int i = 0; p.use_shift && i < N; i++) {
 			const int64_t sy = d->shifty[i], sx = d->shiftx[i];
 			const int64_t asy = sy < 0 ? -sy : sy, asx = sx < 0 ? -sx : sx;
-			if ((int64_t)(H + asy) * W * 2 + 2 * asx >= (1ll << 31))
+			if ((int64_t)(H + asy) * W * 2 + 2 * asx >= (1ll << 31) || asx > 16383)
 				hist_addr_ok = false;
-			sh[2 * i] = (int)(sy * W * 2 + 2 * sx);
-			sh[2 * i + 1] = (int)(2 * sx);
+			sh[i] = (int)(sy * W * 2 + 2 * sx);
+			sx2[i] = (int16_t)(2 * sx);
 		}
 		if (p.use_shift) {
-			memcpy(sh.data() + 2 * Npad, d->shiftx, sizeof(int) * N);
-			memcpy(sh.data() + 2 * Npad + N, d->shifty, sizeof(int) * N);
+			memcpy(sh.data() + Npad + Npad / 2, d->shiftx, sizeof(int) * N);
+			memcpy(sh.data() + Npad + Npad / 2 + N, d->shifty, sizeof(int) * N);
 		}
 		HIPCHK(hipMemcpyAsync(dv.shifts.p, sh.data(), sizeof(int) * sh.size(), hipMemcpyHostToDevice, s));
 		p.hist_tab = (const int *)dv.shifts.p;
+		p.hist_npad = Npad;
 		if (p.use_shift) {
-			p.shiftx = p.hist_tab + 2 * Npad;
+			p.shiftx = p.hist_tab + Npad + Npad / 2;
 			p.shifty = p.shiftx + N;
 		}
 	}
@@ -360,8 +363,7 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 			unsigned int *redo_list = redo_count + 16;
 			HIPCHK(hipMemsetAsync(redo_count, 0, sizeof(unsigned int), s));
 			HIPCHK(hipEventRecord(dv.ev[0], s));
-			const size_t tab_lds = sizeof(int) * 2 * (size_t)Npad;
-			hipLaunchKernelGGL(k_stack_hist, dim3((unsigned)nblk), dim3(256), tab_lds, s, p, redo_count, redo_list);
+			hipLaunchKernelGGL(k_stack_hist, dim3((unsigned)nblk), dim3(256), 0, s, p, redo_count, redo_list);
 			HIPCHK(hipGetLastError());
 			HIPCHK(hipEventRecord(dv.ev[1], s));
 			unsigned int nredo = 0;

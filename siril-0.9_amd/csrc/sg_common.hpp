@@ -23,7 +23,8 @@ struct SgStackParams {
 	double sig0, sig1;
 	const int *shiftx, *shifty;		/* device [N] */
 	int dbg;				/* A/B timing knob (SG_HIST_DBG), 0 in production */
-	const int *hist_tab;			/* device int2[N]: {shifty * W * 2, 2 * shiftx} */
+	const int *hist_tab;			/* device: c1[hist_npad] = shifty*W*2 + 2*shiftx, then int16 sx2[hist_npad] = 2*shiftx */
+	int hist_npad;				/* N rounded up to a multiple of 16 */
 	const double *offset, *mul, *scale;	/* device [N] or null */
 	int row_begin, row_end;			/* memory rows to compute */
 	unsigned long long *rej;		/* [SG_REJ_SHARDS][3][2] */

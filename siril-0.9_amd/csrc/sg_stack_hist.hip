@@ -316,33 +316,56 @@ struct SghFrame {
  * frame gives a negative (huge) or past-the-plane offset -> 0 (the zero rows of
  * :1550-1577); the column check forces an out-of-range offset (the x shift writes 0,
  * :1628-1632) */
-__device__ __forceinline__ uint32_t sgh_load(const SghFrame &F, const char *base, uint32_t nrec, int c1, int sx2) {
+__device__ __forceinline__ unsigned short sgh_load(const SghFrame &F, const char *base, uint32_t nrec, int c1, int sx2) {
 	const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)nrec, 0x00020000);
 	const uint32_t sc2 = F.x2 - (uint32_t)sx2;
 	const uint32_t voff = sc2 < (uint32_t)F.w2 ? (uint32_t)(F.rw2 - c1) + F.x2 : 0x80000000u;
-	return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rsrc, (int)voff, 0, 0);
+	return __builtin_amdgcn_raw_buffer_load_b16(rsrc, (int)voff, 0, 0);
 }
 
-/* NP*2 frames f0.. (f0 % 8 == 0) into NP packed pairs; tab = LDS copy of p.hist_tab
- * (int2 {c1, sx2} per frame, zero padded to a multiple of 16 frames); frames >= N get
- * num_records = 0 (every lane reads 0; never binned) */
-template <int NP, bool FULL>
-__device__ __forceinline__ void sgh_loadblk(const SghFrame &F, const int *tab, int N, int f0, uint32_t (&dst)[NP]) {
-	const int4 *q = (const int4 *)(tab + 2 * f0);
-	int4 t[NP];
+/* shift table of the 16 frames f0..f0+15 (f0 % 16 == 0): c1 (one s_load_dwordx16) and the
+ * int16 sx2 (one s_load_dwordx8), wave-uniform values in SGPRs; the table is padded to a
+ * multiple of 16 frames with zeros */
+struct SghTab16 {
+	int c1[16];
+	uint32_t sx2p[8];
+};
+__device__ __forceinline__ void sgh_tab16(const SgStackParams &p, int f0, SghTab16 &T) {
+	const int4 *q = (const int4 *)(p.hist_tab + f0);
+	const int4 *r = (const int4 *)(p.hist_tab + p.hist_npad + f0 / 2);
 #pragma unroll
-	for (int i = 0; i < NP; i++)
-		t[i] = q[i];
+	for (int i = 0; i < 4; i++) {
+		const int4 v = q[i];
+		T.c1[4 * i] = __builtin_amdgcn_readfirstlane(v.x);
+		T.c1[4 * i + 1] = __builtin_amdgcn_readfirstlane(v.y);
+		T.c1[4 * i + 2] = __builtin_amdgcn_readfirstlane(v.z);
+		T.c1[4 * i + 3] = __builtin_amdgcn_readfirstlane(v.w);
+	}
+#pragma unroll
+	for (int i = 0; i < 2; i++) {
+		const int4 v = r[i];
+		T.sx2p[4 * i] = (uint32_t)__builtin_amdgcn_readfirstlane(v.x);
+		T.sx2p[4 * i + 1] = (uint32_t)__builtin_amdgcn_readfirstlane(v.y);
+		T.sx2p[4 * i + 2] = (uint32_t)__builtin_amdgcn_readfirstlane(v.z);
+		T.sx2p[4 * i + 3] = (uint32_t)__builtin_amdgcn_readfirstlane(v.w);
+	}
+}
+
+/* 16 frames f0..f0+15, one sample per register (packing at load time would make the
+ * compiler wait for each load right after issuing it); frames >= N get num_records = 0
+ * (every lane reads 0; never binned) */
+template <bool FULL>
+__device__ __forceinline__ void sgh_loadblk(const SghFrame &F, const SghTab16 &T, int N, int f0, uint32_t (&dst)[16]) {
 	const char *b = F.plane0 + (int64_t)f0 * F.fstride2;
 #pragma unroll
-	for (int m = 0; m < NP; m++) {
+	for (int m = 0; m < 8; m++) {
 		const uint32_t na = (FULL || f0 + 2 * m < N) ? F.plane_bytes : 0u;
 		const uint32_t nb = (FULL || f0 + 2 * m + 1 < N) ? F.plane_bytes : 0u;
-		const uint32_t va = sgh_load(F, b, na, t[m].x, t[m].y);
+		const int sxa = (int)(int16_t)(T.sx2p[m] & 0xFFFFu), sxb = (int)T.sx2p[m] >> 16;
+		dst[2 * m] = sgh_load(F, b, na, T.c1[2 * m], sxa);
 		b += F.fstride2;
-		const uint32_t vb = sgh_load(F, b, nb, t[m].z, t[m].w);
+		dst[2 * m + 1] = sgh_load(F, b, nb, T.c1[2 * m + 1], sxb);
 		b += F.fstride2;
-		dst[m] = va | (vb << 16);
 	}
 }
 
@@ -378,7 +401,6 @@ __device__ __forceinline__ void sgh_bin_pair(SghLds &L, uint32_t laneaddr, uint3
 __global__ void __launch_bounds__(64 * SGH_WAVES)
 k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
 	__shared__ SghLds L;
-	extern __shared__ __attribute__((aligned(16))) int tabL[];	/* int2 per frame, Npad frames */
 	const int tid = threadIdx.x, lane = tid & 63;
 	const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 	const int ntx = (p.W + SG_TILE_W - 1) / SG_TILE_W;
@@ -405,36 +427,35 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 		L.nz[tid] = 0;
 		L.ns[tid] = 0;
 	}
-	{
-		const int4 *src = (const int4 *)p.hist_tab;
-		int4 *dst = (int4 *)tabL;
-		for (int i = tid; i < Npad / 2; i += 64 * SGH_WAVES)
-			dst[i] = src[i];
-	}
 	__syncthreads();
 
 	constexpr int M = 16, MP = M / 2;	/* frames per block, packed pairs per block */
-	auto loadblk = [&](int f0, uint32_t (&dst)[MP]) {
+	auto loadblk = [&](int f0, const SghTab16 &T, uint32_t (&dst)[M]) {
 		if (f0 + M <= N)
-			sgh_loadblk<MP, true>(F, tabL, N, f0, dst);
+			sgh_loadblk<true>(F, T, N, f0, dst);
 		else
-			sgh_loadblk<MP, false>(F, tabL, N, f0, dst);
+			sgh_loadblk<false>(F, T, N, f0, dst);
 	};
 	/* 16-frame blocks: wave w bins blocks w, w+4, ...; frames 0..15 (block 0) are the
-	 * centre sample every wave loads.  Two named buffers keep the next block's loads
-	 * in flight while the current one is binned. */
-	uint32_t p16[SGH_CENTER / 2], bufA[MP], bufB[MP];
-	sgh_loadblk<SGH_CENTER / 2, true>(F, tabL, N, 0, p16);
+	 * centre sample every wave loads.  Two named buffers keep the next block's loads in
+	 * flight while the current one is binned; the shift table of the block after that is
+	 * fetched (scalar loads) before binning. */
+	uint32_t p16[SGH_CENTER], bufA[M], bufB[M];
+	SghTab16 T;
+	sgh_tab16(p, 0, T);
+	sgh_loadblk<true>(F, T, N, 0, p16);
 	int fb = M * wave;
-	if (fb >= SGH_CENTER && fb < N)
-		loadblk(fb, bufA);
+	if (fb >= SGH_CENTER && fb < N) {
+		sgh_tab16(p, fb, T);
+		loadblk(fb, T, bufA);
+	}
+	constexpr int STEP = M * SGH_WAVES;
+	sgh_tab16(p, fb + STEP < N ? fb + STEP : (fb < Npad ? fb : 0), T);
 	/* centre: median of the first 16 samples */
 	uint32_t v16[SGH_CENTER];
 #pragma unroll
-	for (int k = 0; k < SGH_CENTER / 2; k++) {
-		v16[2 * k] = p16[k] & 0xFFFFu;
-		v16[2 * k + 1] = p16[k] >> 16;
-	}
+	for (int k = 0; k < SGH_CENTER; k++)
+		v16[k] = p16[k];
 	int lo = (int)sgh_median16(v16) - SGH_BINS / 2;
 	if (lo < 1)
 		lo = 1;
@@ -442,14 +463,18 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 		lo = 65535 - SGH_BINS;
 	if (fb < SGH_CENTER) {
 #pragma unroll
-		for (int m = 0; m < MP; m++)
-			bufA[m] = p16[(fb / 2) + m];
+		for (int m = 0; m < M; m++)
+			bufA[m] = p16[m];
 	}
 
 	const uint32_t laneaddr = (uint32_t)lane * 4u;
 	const uint32_t lo1x2 = (uint32_t)(lo - 1) * 0x10001u;
 	uint32_t nonzero = 0, nsat = 0, counted = 0;
-	auto binblk = [&](int f0, const uint32_t (&src)[MP]) {
+	auto binblk = [&](int f0, const uint32_t (&raw)[M]) {
+		uint32_t src[MP];
+#pragma unroll
+		for (int m = 0; m < MP; m++)
+			src[m] = raw[2 * m] | (raw[2 * m + 1] << 16);
 		if (f0 + M <= N) {
 #pragma unroll
 			for (int m = 0; m < MP; m++)
@@ -474,14 +499,17 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 			}
 		}
 	};
-	constexpr int STEP = M * SGH_WAVES;
+	/* invariant: T = table of block nx(fb) = the block loaded next */
+	auto nx = [&](int f) { return f + STEP < N ? f + STEP : f; };
 	while (fb < N) {
-		loadblk(fb + STEP < N ? fb + STEP : fb, bufB);
+		loadblk(nx(fb), T, bufB);
+		sgh_tab16(p, nx(nx(fb)), T);
 		binblk(fb, bufA);
 		fb += STEP;
 		if (fb >= N)
 			break;
-		loadblk(fb + STEP < N ? fb + STEP : fb, bufA);
+		loadblk(nx(fb), T, bufA);
+		sgh_tab16(p, nx(nx(fb)), T);
 		binblk(fb, bufB);
 		fb += STEP;
 	}
