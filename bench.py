@@ -38,6 +38,10 @@ def parse():
     ap.add_argument("--rejection", default="sigma")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--maxshift", type=int, default=16, help="synthetic registration shift range")
+    ap.add_argument("--even-shifts", action="store_true",
+                    help="A/B only: round x shifts down to even (4-byte aligned pixel-pair loads)")
+    ap.add_argument("--zero-shift", choices=["x", "y"], default=None,
+                    help="A/B only: drop the x or y registration shifts")
     ap.add_argument("--frame-pad", type=int, default=0,
                     help="extra elements between frames in HBM (breaks power-of-two frame strides)")
     ap.add_argument("--cpu-rows", type=int, default=1024, help="rows of the CPU baseline sample")
@@ -122,6 +126,10 @@ def main():
             span = 2 * args.maxshift + 1
             shx[f] = -((h & 0xFFFFFFFF) % span - args.maxshift)
             shy[f] = -(((h >> 32) & 0xFFFFFFFF) % span - args.maxshift)
+    if args.even_shifts:
+        shx &= ~1
+    if args.zero_shift:
+        (shx if args.zero_shift == "x" else shy)[:] = 0
     desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=rej_mode, sig=(4.0, 3.0),
                               shiftx=shx, shifty=shy, max_thread=8, max_number_of_rows=H)
 

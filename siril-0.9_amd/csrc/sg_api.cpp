@@ -257,6 +257,7 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 		 * (zeros when there is no registration data), then the plain shift arrays */
 		std::vector<int> sh(Npad + Npad / 2 + 2 * N, 0);
 		int16_t *sx2 = (int16_t *)(sh.data() + Npad);
+		p.hist_maxsx = 0;
 		for (int i = 0; p.use_shift && i < N; i++) {
 			const int64_t sy = d->shifty[i], sx = d->shiftx[i];
 			const int64_t asy = sy < 0 ? -sy : sy, asx = sx < 0 ? -sx : sx;
@@ -264,6 +265,8 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 				hist_addr_ok = false;
 			sh[i] = (int)(sy * W * 2 + 2 * sx);
 			sx2[i] = (int16_t)(2 * sx);
+			if (asx > p.hist_maxsx)
+				p.hist_maxsx = (int)asx;
 		}
 		if (p.use_shift) {
 			memcpy(sh.data() + Npad + Npad / 2, d->shiftx, sizeof(int) * N);
@@ -363,7 +366,8 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 			unsigned int *redo_list = redo_count + 16;
 			HIPCHK(hipMemsetAsync(redo_count, 0, sizeof(unsigned int), s));
 			HIPCHK(hipEventRecord(dv.ev[0], s));
-			hipLaunchKernelGGL(k_stack_hist, dim3((unsigned)nblk), dim3(256), 0, s, p, redo_count, redo_list);
+			const size_t nblk_h = (size_t)((W + 127) / 128) * nrows * C;	/* 128-pixel tiles */
+			hipLaunchKernelGGL(k_stack_hist, dim3((unsigned)nblk_h), dim3(256), 0, s, p, redo_count, redo_list);
 			HIPCHK(hipGetLastError());
 			HIPCHK(hipEventRecord(dv.ev[1], s));
 			unsigned int nredo = 0;

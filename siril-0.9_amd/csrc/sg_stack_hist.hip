@@ -10,15 +10,19 @@
  *     lowest values, high clips the highest; the set stays a value interval);
  *   - median of the kept set = value at a rank, counts below/above a threshold = ranks;
  *   - sigma comes from exact integer moments n, S, SS of the kept set.
- * So each 64-pixel tile builds, per pixel, an exact histogram of 256 unit-wide bins
+ * So each 128-pixel tile builds, per pixel, an exact histogram of 256 unit-wide bins
  * [lo, lo+255] around the median of the first 16 frames (u8 counts packed 4 per dword),
- * plus counters of the samples below / above the band and of the zeros / 65535s among
- * them (out-of-frame zero fill, dead pixels, saturation, cosmics).  4 waves stream the
- * N frames into it: per-frame buffer descriptors give 128-byte coalesced row loads whose
- * out-of-frame lanes read 0 from the hardware bounds check (shift + zero fill of
- * :1535-1654 for free), two frames share a VGPR (16-bit halves) and are binned with
- * packed u16 arithmetic and branch-free LDS atomics.  Wave 0 then prefix-sums the bins
- * once and runs the reference's pass loop as O(log) histogram queries.
+ * plus a counter of the samples above the band and of the zeros / 65535s (the number
+ * below the band follows from N) (out-of-frame zero fill, dead pixels, saturation, cosmics).  4 waves stream the
+ * N frames into it, one lane per PAIR of adjacent pixels: each frame row is one 256-byte
+ * coalesced dword load per wave (2-byte aligned dword loads are legal on gfx950), the
+ * per-frame buffer descriptor makes out-of-frame rows read 0 through the hardware bounds
+ * check (the zero fill of :1550-1577 for free), and the pixel pair is binned with packed
+ * u16 arithmetic and branch-free LDS atomics.  Tiles whose shifted columns can leave the
+ * image (the two image-edge tile columns) load pixel by pixel with the column check of
+ * :1628-1632 (one latency per 16-frame block; they are 2 of every W/128 tiles).  Waves 0
+ * and 1 then prefix-sum the bins once and run the reference's pass
+ * loop as O(log) histogram queries, 64 pixels each.
  *
  * Exactness: decisions use exact moments; a pixel whose decision falls within a rounding
  * band of a threshold (GSL's long-double sd vs exact), whose loop would hit the
@@ -34,24 +38,25 @@
 #define SGH_BINS 256
 #define SGH_DW (SGH_BINS / 4)	/* band dwords per pixel */
 #define SGH_WAVES 4
+#define SGH_COLS 128		/* pixels per tile: lane l owns pixels 2l (col l) and 2l+1 (col 64+l) */
 #define SGH_CENTER 16		/* frames used for the centre estimate */
 #define SGH_BAND 1e-11		/* same rounding band as the sorted path (SG_BAND) */
 
 typedef unsigned short sgh_u16x2 __attribute__((ext_vector_type(2)));
 
-/* hist[0]          : samples below the band (u32)
- * hist[1 + j] byte b: count of value lo + 4j + b
- * hist[1 + SGH_DW]  : samples above the band (u32) */
+/* hist[0][col]          : samples below the band land in byte 3 (garbage, unused)
+ * hist[1 + j][col] byte b: count of value lo + 4j + b
+ * hist[1 + SGH_DW][col]  : samples above the band (u32) */
 struct SghLds {
-	uint32_t hist[SGH_DW + 2][64];
-	uint16_t cum16[SGH_DW / 4][64];		/* band samples in bins < 16(j+1) */
-	uint32_t nz[64], ns[64];		/* zeros / 65535s (all of them lie outside the band) */
+	uint32_t hist[SGH_DW + 2][SGH_COLS];
+	uint16_t cum16[SGH_DW / 4][SGH_COLS];	/* band samples in bins < 16(j+1) */
+	uint32_t nz[SGH_COLS], ns[SGH_COLS];	/* zeros / 65535s (all of them lie outside the band) */
 };
 
 struct SghPix {
 	int lo;			/* value of bin 0, 1 <= lo <= 65279 */
 	int nz, ns, nb;		/* zeros, 65535s, band samples (nz + nb + ns == N) */
-	int lane;
+	int col;
 	const SghLds *L;
 };
 
@@ -62,10 +67,10 @@ __device__ __forceinline__ int sgh_band_le(const SghPix &P, int t) {
 	if (t > SGH_BINS - 1)
 		t = SGH_BINS - 1;
 	const int j16 = t >> 4, jd = t >> 2;
-	int base = j16 ? (int)P.L->cum16[j16 - 1][P.lane] : 0;
+	int base = j16 ? (int)P.L->cum16[j16 - 1][P.col] : 0;
 	for (int k = 4 * j16; k < jd; k++)
-		base += (int)__builtin_amdgcn_sad_u8(P.L->hist[1 + k][P.lane], 0u, 0u);
-	const uint32_t d = P.L->hist[1 + jd][P.lane];
+		base += (int)__builtin_amdgcn_sad_u8(P.L->hist[1 + k][P.col], 0u, 0u);
+	const uint32_t d = P.L->hist[1 + jd][P.col];
 	const int sh = ((t & 3) + 1) * 8;
 	const uint32_t m = sh >= 32 ? 0xFFFFFFFFu : ((1u << sh) - 1u);
 	return base + (int)__builtin_amdgcn_sad_u8(d & m, 0u, 0u);
@@ -95,20 +100,20 @@ __device__ int sgh_value_at(const SghPix &P, int g) {
 	int a = 0, b = SGH_DW / 4 - 1;
 	while (a < b) {
 		const int m = (a + b) >> 1;
-		if ((int)P.L->cum16[m][P.lane] > g)
+		if ((int)P.L->cum16[m][P.col] > g)
 			b = m;
 		else
 			a = m + 1;
 	}
-	int base = a ? (int)P.L->cum16[a - 1][P.lane] : 0;
+	int base = a ? (int)P.L->cum16[a - 1][P.col] : 0;
 	int k = 4 * a;
-	uint32_t d = P.L->hist[1 + k][P.lane];
+	uint32_t d = P.L->hist[1 + k][P.col];
 	for (; k < 4 * a + 3; k++) {
 		const int bs = (int)__builtin_amdgcn_sad_u8(d, 0u, 0u);
 		if (base + bs > g)
 			break;
 		base += bs;
-		d = P.L->hist[2 + k][P.lane];
+		d = P.L->hist[2 + k][P.col];
 	}
 	int i = 0;
 	for (; i < 3; i++) {
@@ -119,7 +124,7 @@ __device__ int sgh_value_at(const SghPix &P, int g) {
 	return P.lo + 4 * k + i;
 }
 
-/* count, sum and sum of squares of (v - lo) over samples with v1 <= v <= v2 */
+/* sum and sum of squares of (v - lo) over samples with v1 <= v <= v2 */
 __device__ void sgh_range_moments(const SghPix &P, int v1, int v2, long long &s, unsigned long long &ss) {
 	s = 0;
 	ss = 0;
@@ -144,7 +149,7 @@ __device__ void sgh_range_moments(const SghPix &P, int v1, int v2, long long &s,
 		return;
 	uint32_t s32 = 0, ss32 = 0;
 	for (int j = b1 >> 2; j <= (b2 >> 2); j++) {
-		uint32_t d = P.L->hist[1 + j][P.lane];
+		uint32_t d = P.L->hist[1 + j][P.col];
 		const int first = 4 * j, last = 4 * j + 3;
 		if (first < b1)
 			d &= 0xFFFFFFFFu << (8 * (b1 - first));
@@ -260,13 +265,18 @@ __device__ int sgh_sigma(const SghPix &P, int N, double sl, double sh, long long
 	return SG_CLS_OK;
 }
 
-/* centre estimate from 16 samples: median of those that are neither 0 nor 65535 (the
- * out-of-frame zero fill of edge pixels must not drag the band away), bitonic network */
-__device__ __forceinline__ uint32_t sgh_median16(const uint32_t (&in)[SGH_CENTER]) {
-	uint32_t v[SGH_CENTER];
+/* centre estimate of the two pixels of a lane from 16 samples each (16-bit halves of
+ * p[]): median of the samples that are neither 0 nor 65535 (the out-of-frame zero fill of
+ * edge pixels must not drag the band away); packed bitonic network */
+__device__ __forceinline__ void sgh_centre2(const uint32_t (&p)[SGH_CENTER], int &lo_a, int &lo_b) {
+	sgh_u16x2 v[SGH_CENTER];
+	sgh_u16x2 nzc = {0, 0}, sc = {0, 0};
 #pragma unroll
-	for (int i = 0; i < SGH_CENTER; i++)
-		v[i] = in[i];
+	for (int i = 0; i < SGH_CENTER; i++) {
+		v[i] = __builtin_bit_cast(sgh_u16x2, p[i]);
+		nzc += __builtin_elementwise_min(v[i], (sgh_u16x2){1, 1});
+		sc += __builtin_elementwise_sub_sat(v[i], (sgh_u16x2){65534, 65534});
+	}
 #pragma unroll
 	for (int k = 2; k <= SGH_CENTER; k <<= 1) {
 #pragma unroll
@@ -276,56 +286,49 @@ __device__ __forceinline__ uint32_t sgh_median16(const uint32_t (&in)[SGH_CENTER
 				const int l = i ^ j;
 				if (l > i) {
 					const bool up = (i & k) == 0;
-					const uint32_t a = v[i], b = v[l];
-					const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
-					v[i] = up ? lo : hi;
-					v[l] = up ? hi : lo;
+					const sgh_u16x2 a = v[i], b = v[l];
+					const sgh_u16x2 mn = __builtin_elementwise_min(a, b), mx = __builtin_elementwise_max(a, b);
+					v[i] = up ? mn : mx;
+					v[l] = up ? mx : mn;
 				}
 			}
 		}
 	}
-	int z = 0, sat = 0;
+	int lo2[2];
 #pragma unroll
-	for (int i = 0; i < SGH_CENTER; i++) {
-		z += v[i] == 0;
-		sat += v[i] == 65535;
+	for (int h = 0; h < 2; h++) {
+		const int z = SGH_CENTER - (int)nzc[h], s = (int)sc[h];
+		int idx = z + (SGH_CENTER - z - s) / 2;
+		if (idx > SGH_CENTER - 1)
+			idx = SGH_CENTER - 1;
+		int r = v[0][h];
+#pragma unroll
+		for (int i = 1; i < SGH_CENTER; i++)
+			r = (i == idx) ? (int)v[i][h] : r;
+		r -= SGH_BINS / 2;
+		if (r < 1)
+			r = 1;
+		if (r > 65535 - SGH_BINS)
+			r = 65535 - SGH_BINS;
+		lo2[h] = r;
 	}
-	int idx = z + (SGH_CENTER - z - sat) / 2;
-	if (idx > SGH_CENTER - 1)
-		idx = SGH_CENTER - 1;
-	uint32_t r = v[0];
-#pragma unroll
-	for (int i = 1; i < SGH_CENTER; i++)
-		r = (i == idx) ? v[i] : r;
-	return r;
+	lo_a = lo2[0];
+	lo_b = lo2[1];
 }
 
-/* per-frame load context: each frame gets its own buffer descriptor (num_records = one
- * plane) so that any offset outside the plane reads 0 through the hardware bounds check */
+/* per-tile load context */
 struct SghFrame {
 	const char *plane0;		/* channel plane of frame 0 */
 	int64_t fstride2;		/* bytes between frames */
 	uint32_t plane_bytes;
 	int rw2;			/* R * W * 2 */
 	int w2;				/* W * 2 */
-	uint32_t x2;			/* 2 * x (per lane) */
+	uint32_t xa2;			/* 2 * x of the lane's first pixel */
 };
 
-/* one sample: c1 = shifty*W*2 + 2*shiftx, sx2 = 2*shiftx (per-frame table, read from LDS
- * as wave-uniform VGPR values); byte offset (R - sy) W 2 + 2 (x - sx): a row outside the
- * frame gives a negative (huge) or past-the-plane offset -> 0 (the zero rows of
- * :1550-1577); the column check forces an out-of-range offset (the x shift writes 0,
- * :1628-1632) */
-__device__ __forceinline__ unsigned short sgh_load(const SghFrame &F, const char *base, uint32_t nrec, int c1, int sx2) {
-	const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)nrec, 0x00020000);
-	const uint32_t sc2 = F.x2 - (uint32_t)sx2;
-	const uint32_t voff = sc2 < (uint32_t)F.w2 ? (uint32_t)(F.rw2 - c1) + F.x2 : 0x80000000u;
-	return __builtin_amdgcn_raw_buffer_load_b16(rsrc, (int)voff, 0, 0);
-}
-
-/* shift table of the 16 frames f0..f0+15 (f0 % 16 == 0): c1 (one s_load_dwordx16) and the
- * int16 sx2 (one s_load_dwordx8), wave-uniform values in SGPRs; the table is padded to a
- * multiple of 16 frames with zeros */
+/* shift table of the 16 frames f0..f0+15 (f0 % 16 == 0): c1 = shifty*W*2 + 2*shiftx (one
+ * s_load_dwordx16) and int16 sx2 = 2*shiftx (one s_load_dwordx8); zero padded to a
+ * multiple of 16 frames */
 struct SghTab16 {
 	int c1[16];
 	uint32_t sx2p[8];
@@ -351,186 +354,102 @@ __device__ __forceinline__ void sgh_tab16(const SgStackParams &p, int f0, SghTab
 	}
 }
 
-/* 16 frames f0..f0+15, one sample per register (packing at load time would make the
- * compiler wait for each load right after issuing it); frames >= N get num_records = 0
- * (every lane reads 0; never binned) */
-template <bool FULL>
-__device__ __forceinline__ void sgh_loadblk(const SghFrame &F, const SghTab16 &T, int N, int f0, uint32_t (&dst)[16]) {
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sgh_rsrc(const char *base, uint32_t nrec) {
+	return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)nrec, 0x00020000);
+}
+
+/* 16 frames f0..f0+15, one 2-byte aligned dword load per frame and lane at
+ * (R - sy) W 2 + 2 (x - sx) (the lane's pixel pair); a row outside the frame reads 0
+ * through the bounds check, frames >= N get num_records = 0 (read 0; never binned).
+ * EDGE (image-edge tiles, where a shifted column can leave the image; the x shift writes 0
+ * there, :1628-1632): a pair with both columns outside loads out of bounds (0); a pair
+ * straddling the left edge loads one pixel to the right and the binning moves the valid
+ * pixel to the high half (<< 16), one straddling the right edge loads one pixel to the
+ * left (>> 16); two fix bits per frame in `fix` */
+template <bool FULL, bool EDGE>
+__device__ __forceinline__ void sgh_loadblk(const SghFrame &F, const SghTab16 &T, int N, int f0, uint32_t (&dst)[16],
+		uint32_t &fix) {
 	const char *b = F.plane0 + (int64_t)f0 * F.fstride2;
+	if (EDGE)
+		fix = 0;
 #pragma unroll
-	for (int m = 0; m < 8; m++) {
-		const uint32_t na = (FULL || f0 + 2 * m < N) ? F.plane_bytes : 0u;
-		const uint32_t nb = (FULL || f0 + 2 * m + 1 < N) ? F.plane_bytes : 0u;
-		const int sxa = (int)(int16_t)(T.sx2p[m] & 0xFFFFu), sxb = (int)T.sx2p[m] >> 16;
-		dst[2 * m] = sgh_load(F, b, na, T.c1[2 * m], sxa);
-		b += F.fstride2;
-		dst[2 * m + 1] = sgh_load(F, b, nb, T.c1[2 * m + 1], sxb);
+	for (int m = 0; m < 16; m++) {
+		const uint32_t nrec = (FULL || f0 + m < N) ? F.plane_bytes : 0u;
+		const uint32_t k = (uint32_t)(F.rw2 - T.c1[m]);
+		uint32_t off = k + F.xa2;
+		if (EDGE) {
+			const int sx2 = (m & 1) ? ((int)T.sx2p[m >> 1] >> 16) : (int)(int16_t)(T.sx2p[m >> 1] & 0xFFFFu);
+			const uint32_t sca = F.xa2 - (uint32_t)sx2;
+			const bool bada = sca >= (uint32_t)F.w2, badb = sca + 2u >= (uint32_t)F.w2;
+			off = bada ? (badb ? 0x80000000u : off + 2u) : (badb ? off - 2u : off);
+			fix |= ((bada && !badb) ? 1u : ((!bada && badb) ? 2u : 0u)) << (2 * m);
+		}
+		dst[m] = __builtin_amdgcn_raw_buffer_load_b32(sgh_rsrc(b, nrec), (int)off, 0, 0);
 		b += F.fstride2;
 	}
 }
 
-/* bin a pair of samples (two frames of this lane's pixel, 16-bit halves of vv) */
-__device__ __forceinline__ void sgh_bin_pair(SghLds &L, uint32_t laneaddr, uint32_t lo1x2, uint32_t vv,
-		uint32_t &nonzero, uint32_t &nsat, int dbg) {
+template <bool EDGE>
+__device__ __forceinline__ uint32_t sgh_fixup(uint32_t v, uint32_t fix, int m) {
+	if (!EDGE)
+		return v;
+	const uint32_t f = (fix >> (2 * m)) & 3u;
+	return f == 1u ? v << 16 : (f == 2u ? v >> 16 : v);
+}
+
+/* packed u16 min / saturating sub kept as single instructions (LLVM otherwise rewrites
+ * min(v, 1) and sat(v - 65534) into per-half compares and selects) */
+__device__ __forceinline__ uint32_t sgh_pk_min(uint32_t a, uint32_t b) {
+	uint32_t r;
+	asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "s"(b));
+	return r;
+}
+__device__ __forceinline__ uint32_t sgh_pk_sub_sat(uint32_t a, uint32_t b) {
+	uint32_t r;
+	asm("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(r) : "v"(a), "s"(b));
+	return r;
+}
+__device__ __forceinline__ uint32_t sgh_pk_add(uint32_t a, uint32_t b) {
+	uint32_t r;
+	asm("v_pk_add_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+	return r;
+}
+
+/* bin the pixel pair of one frame (low half -> column of addrA, high half -> addrB):
+ * s = min(max(v - lo + 1, 0), 257) + 3 is 3 below the band (dword 0 byte 3, ignored),
+ * v - lo + 4 inside (dword 1 + (v-lo)/4, byte (v-lo)%4), 260 above (dword 65, a u32
+ * counter); zeros and 65535s are counted per half */
+__device__ __forceinline__ void sgh_bin_pair(uint32_t *h, uint32_t addrA, uint32_t addrB, uint32_t lo1x2, uint32_t vv,
+		uint32_t &nonzero, uint32_t &nsat) {
 	const sgh_u16x2 v = __builtin_bit_cast(sgh_u16x2, vv);
-	if (dbg == 3) {		/* A/B: loads only */
-		nonzero += vv;
-		return;
-	}
-	const sgh_u16x2 l1 = __builtin_bit_cast(sgh_u16x2, lo1x2);
-	sgh_u16x2 t = __builtin_elementwise_sub_sat(v, l1);	/* 0 below the band, 1..256 inside */
-	t = __builtin_elementwise_min(t, (sgh_u16x2){257, 257});
-	/* 0 below (dword 0, a u32 counter), 4..259 band, 260 above (dword 65, u32) */
-	t = t + __builtin_elementwise_min(t, (sgh_u16x2){1, 1}) * (sgh_u16x2){3, 3};
+	sgh_u16x2 t = __builtin_elementwise_sub_sat(v, __builtin_bit_cast(sgh_u16x2, lo1x2));
+	t = __builtin_elementwise_min(t, (sgh_u16x2){257, 257}) + (sgh_u16x2){3, 3};
 	const uint32_t tt = __builtin_bit_cast(uint32_t, t);
-	const uint32_t t3 = tt << 3;
-	const uint32_t a0 = (__builtin_amdgcn_ubfe(tt, 2, 8) << 8) + laneaddr;
-	const uint32_t a1 = (__builtin_amdgcn_ubfe(tt, 18, 8) << 8) + laneaddr;
-	const uint32_t i0 = 1u << (t3 & 24u);
-	const uint32_t i1 = 1u << __builtin_amdgcn_ubfe(t3, 16, 5);
-	uint32_t *h = &L.hist[0][0];
+	const uint32_t a0 = ((tt << 7) & (0x7Fu << 9)) | addrA;	/* row stride 128 cols x 4 B */
+	const uint32_t a1 = ((tt >> 9) & (0x7Fu << 9)) | addrB;
+	const uint32_t i0 = 1u << ((tt << 3) & 24u);
+	const uint32_t i1 = 1u << ((tt >> 13) & 24u);
 	atomicAdd(h + (a0 >> 2), i0);
 	atomicAdd(h + (a1 >> 2), i1);
-	/* nonzero samples and 65535 samples of the pair */
-	const sgh_u16x2 nzv = __builtin_elementwise_min(v, (sgh_u16x2){1, 1});
-	const sgh_u16x2 sv = __builtin_elementwise_sub_sat(v, (sgh_u16x2){65534, 65534});
-	nonzero = __builtin_amdgcn_udot2(nzv, (sgh_u16x2){1, 1}, nonzero, false);
-	nsat = __builtin_amdgcn_udot2(sv, (sgh_u16x2){1, 1}, nsat, false);
+	nonzero = sgh_pk_add(nonzero, sgh_pk_min(vv, 0x00010001u));
+	nsat = sgh_pk_add(nsat, sgh_pk_sub_sat(vv, 0xFFFEFFFEu));
 }
 
-__global__ void __launch_bounds__(64 * SGH_WAVES)
-k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
-	__shared__ SghLds L;
-	const int tid = threadIdx.x, lane = tid & 63;
-	const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-	const int ntx = (p.W + SG_TILE_W - 1) / SG_TILE_W;
-	const int nrows = p.row_end - p.row_begin;
-	int bid = blockIdx.x;
-	const int xt = bid % ntx;
-	bid /= ntx;
-	const int R = p.row_begin + (bid % nrows);
-	const int c = bid / nrows;
-	const int x = xt * SG_TILE_W + lane;
+/* after the build, 64 pixels (one column half) per wave: prefix counts, band moments and
+ * the SIGMA loop; writes the outputs, the redo list and the counters */
+__device__ void sgh_finish(const SgStackParams &p, SghLds &L, int col, int lo, int R, int c, int x,
+		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
+	const int lane = threadIdx.x & 63;
 	const int N = p.N;
-	const int Npad = (N + 15) & ~15;
-	SghFrame F;
-	F.plane0 = (const char *)(p.frames + (int64_t)c * p.plane_stride);
-	F.fstride2 = p.frame_stride * 2;
-	F.plane_bytes = (uint32_t)p.H * (uint32_t)p.W * 2u;
-	F.w2 = p.W * 2;
-	F.rw2 = R * p.W * 2;
-	F.x2 = (uint32_t)x * 2u;
-
-	for (int i = tid; i < (SGH_DW + 2) * 64; i += 64 * SGH_WAVES)
-		(&L.hist[0][0])[i] = 0;
-	if (tid < 64) {
-		L.nz[tid] = 0;
-		L.ns[tid] = 0;
-	}
-	__syncthreads();
-
-	constexpr int M = 16, MP = M / 2;	/* frames per block, packed pairs per block */
-	auto loadblk = [&](int f0, const SghTab16 &T, uint32_t (&dst)[M]) {
-		if (f0 + M <= N)
-			sgh_loadblk<true>(F, T, N, f0, dst);
-		else
-			sgh_loadblk<false>(F, T, N, f0, dst);
-	};
-	/* 16-frame blocks: wave w bins blocks w, w+4, ...; frames 0..15 (block 0) are the
-	 * centre sample every wave loads.  Two named buffers keep the next block's loads in
-	 * flight while the current one is binned; the shift table of the block after that is
-	 * fetched (scalar loads) before binning. */
-	uint32_t p16[SGH_CENTER], bufA[M], bufB[M];
-	SghTab16 T;
-	sgh_tab16(p, 0, T);
-	sgh_loadblk<true>(F, T, N, 0, p16);
-	int fb = M * wave;
-	if (fb >= SGH_CENTER && fb < N) {
-		sgh_tab16(p, fb, T);
-		loadblk(fb, T, bufA);
-	}
-	constexpr int STEP = M * SGH_WAVES;
-	sgh_tab16(p, fb + STEP < N ? fb + STEP : (fb < Npad ? fb : 0), T);
-	/* centre: median of the first 16 samples */
-	uint32_t v16[SGH_CENTER];
-#pragma unroll
-	for (int k = 0; k < SGH_CENTER; k++)
-		v16[k] = p16[k];
-	int lo = (int)sgh_median16(v16) - SGH_BINS / 2;
-	if (lo < 1)
-		lo = 1;
-	if (lo > 65535 - SGH_BINS)
-		lo = 65535 - SGH_BINS;
-	if (fb < SGH_CENTER) {
-#pragma unroll
-		for (int m = 0; m < M; m++)
-			bufA[m] = p16[m];
-	}
-
-	const uint32_t laneaddr = (uint32_t)lane * 4u;
-	const uint32_t lo1x2 = (uint32_t)(lo - 1) * 0x10001u;
-	uint32_t nonzero = 0, nsat = 0, counted = 0;
-	auto binblk = [&](int f0, const uint32_t (&raw)[M]) {
-		uint32_t src[MP];
-#pragma unroll
-		for (int m = 0; m < MP; m++)
-			src[m] = raw[2 * m] | (raw[2 * m + 1] << 16);
-		if (f0 + M <= N) {
-#pragma unroll
-			for (int m = 0; m < MP; m++)
-				sgh_bin_pair(L, laneaddr, lo1x2, src[m], nonzero, nsat, p.dbg);
-			counted += M;
-		} else {
-			/* partial last block: a lone frame is paired with a 65535 sample whose count
-			 * is taken back below */
-			for (int m = 0; m < MP; m++) {
-				const int fa = f0 + 2 * m;
-				if (fa >= N)
-					break;
-				const uint32_t vv = fa + 1 < N ? src[m] : ((src[m] & 0xFFFFu) | 0xFFFF0000u);
-				sgh_bin_pair(L, laneaddr, lo1x2, vv, nonzero, nsat, p.dbg);
-				counted += 2;
-				if (fa + 1 >= N) {
-					atomicSub(&L.hist[SGH_DW + 1][lane], 1u);	/* the padding 65535 */
-					nsat--;
-					nonzero--;
-					counted--;
-				}
-			}
-		}
-	};
-	/* invariant: T = table of block nx(fb) = the block loaded next */
-	auto nx = [&](int f) { return f + STEP < N ? f + STEP : f; };
-	while (fb < N) {
-		loadblk(nx(fb), T, bufB);
-		sgh_tab16(p, nx(nx(fb)), T);
-		binblk(fb, bufA);
-		fb += STEP;
-		if (fb >= N)
-			break;
-		loadblk(nx(fb), T, bufA);
-		sgh_tab16(p, nx(nx(fb)), T);
-		binblk(fb, bufB);
-		fb += STEP;
-	}
-	if (counted) {
-		atomicAdd(&L.nz[lane], counted - nonzero);
-		atomicAdd(&L.ns[lane], nsat);
-	}
-	__syncthreads();
-	if (wave != 0)
-		return;
-
-	if (p.dbg >= 2) {
+	if (p.dbg == 2 || p.dbg == 3) {
 		if (x < p.W)
-			p.out[((int64_t)c * p.H + R) * p.W + x] = (uint16_t)(L.hist[1][lane] + nonzero);
+			p.out[((int64_t)c * p.H + R) * p.W + x] = (uint16_t)(L.hist[1][col] + L.nz[col]);
 		return;
 	}
-	/* wave 0: prefix counts + band moments (relative to lo) */
 	uint32_t cum = 0, s32 = 0, ss32 = 0;
 #pragma unroll 16
 	for (int j = 0; j < SGH_DW; j++) {
-		const uint32_t d = L.hist[1 + j][lane];
+		const uint32_t d = L.hist[1 + j][col];
 		const uint32_t bs = __builtin_amdgcn_sad_u8(d, 0u, 0u);
 		const uint32_t d1 = __builtin_amdgcn_udot4(d, 0x03020100u, 0u, false);
 		const uint32_t d2 = __builtin_amdgcn_udot4(d, 0x09040100u, 0u, false);
@@ -539,25 +458,25 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 		ss32 += 16u * jj * jj * bs + 8u * jj * d1 + d2;
 		cum += bs;
 		if ((j & 3) == 3)
-			L.cum16[j >> 2][lane] = (uint16_t)cum;
+			L.cum16[j >> 2][col] = (uint16_t)cum;
 	}
-	const int below = (int)L.hist[0][lane];
-	const int above = (int)L.hist[SGH_DW + 1][lane];
+	const int above = (int)L.hist[SGH_DW + 1][col];
 	SghPix P;
 	P.lo = lo;
-	P.nz = (int)L.nz[lane];
-	P.ns = (int)L.ns[lane];
+	P.nz = (int)L.nz[col];
+	P.ns = (int)L.ns[col];
 	P.nb = (int)cum;
-	P.lane = lane;
+	P.col = col;
 	P.L = &L;
 	int cls = SG_CLS_OK;
 	uint16_t value = 0;
 	uint32_t rlo = 0, rhi = 0;
 	if (x < p.W) {
-		/* every out-of-band sample must be a 0 or a 65535, and no counter may have wrapped */
 		if (p.dbg == 1) {
 			value = (uint16_t)(s32 + ss32);
-		} else if (below + P.nb + above != N || below != P.nz || above != P.ns) {
+		} else if (N - P.nb - above != P.nz || above != P.ns) {
+			/* an out-of-band sample that is not 0 / 65535, or a wrapped u8 counter (a
+			 * carry loses 255 or 256 band counts, so N - nb - above exceeds the zeros) */
 			cls = 1;
 		} else {
 			const long long dz = -(long long)lo, ds = 65535 - (long long)lo;
@@ -582,8 +501,139 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 		b += __shfl_down(b, o, 64);
 	}
 	if (lane == 0 && (a | b)) {
-		unsigned long long *sh = p.rej + ((size_t)(blockIdx.x % SG_REJ_SHARDS) * 6 + c * 2);
+		unsigned long long *sh = p.rej + ((size_t)((blockIdx.x * 2 + (col >> 6)) % SG_REJ_SHARDS) * 6 + c * 2);
 		atomicAdd(sh, a);
 		atomicAdd(sh + 1, b);
 	}
+}
+
+/* one wave's share of the tile's histogram build: 16-frame blocks, wave w bins blocks w,
+ * w+4, ...; frames 0..15 (block 0) are the centre sample every wave loads.  Two named
+ * buffers keep the next block's loads in flight while the current one is binned; the
+ * shift table of the block after that is fetched (scalar loads) before binning. */
+template <bool EDGE>
+__device__ __forceinline__ void sgh_build(const SgStackParams &p, SghLds &L, const SghFrame &F, int wave, int lane,
+		int &lo_a, int &lo_b, uint32_t &nonzero, uint32_t &nsat, int &counted) {
+	constexpr int M = 16;		/* frames per block */
+	constexpr int STEP = M * SGH_WAVES;
+	const int N = p.N;
+	uint32_t *const h = &L.hist[0][0];
+	const uint32_t addrA = (uint32_t)lane * 4u, addrB = (uint32_t)(64 + lane) * 4u;
+	uint32_t bufA[M], bufB[M], p16[SGH_CENTER], fixA = 0, fixB = 0, fix0 = 0;
+	SghTab16 T;
+	auto loadblk = [&](int f0, uint32_t (&dst)[M], uint32_t &fix) {
+		if (f0 + M <= N)
+			sgh_loadblk<true, EDGE>(F, T, N, f0, dst, fix);
+		else
+			sgh_loadblk<false, EDGE>(F, T, N, f0, dst, fix);
+	};
+	int fb = M * wave;
+	sgh_tab16(p, 0, T);
+	loadblk(0, p16, fix0);
+	if (fb >= SGH_CENTER && fb < N) {
+		sgh_tab16(p, fb, T);
+		loadblk(fb, bufA, fixA);
+	}
+	sgh_tab16(p, fb + STEP < N ? fb + STEP : (fb < p.hist_npad ? fb : 0), T);
+#pragma unroll
+	for (int m = 0; m < M; m++)
+		p16[m] = sgh_fixup<EDGE>(p16[m], fix0, m);
+	sgh_centre2(p16, lo_a, lo_b);
+	if (fb < SGH_CENTER) {
+#pragma unroll
+		for (int m = 0; m < M; m++)
+			bufA[m] = p16[m];
+		fixA = 0;
+	}
+	const uint32_t lo1x2 = (uint32_t)(lo_a - 1) | ((uint32_t)(lo_b - 1) << 16);
+	const bool loads_only = p.dbg == 3;
+	auto binblk = [&](int f0, const uint32_t (&raw)[M], uint32_t fix) {
+		if (loads_only) {
+#pragma unroll
+			for (int m = 0; m < M; m++)
+				nonzero ^= raw[m];
+		} else if (f0 + M <= N) {
+#pragma unroll
+			for (int m = 0; m < M; m++)
+				sgh_bin_pair(h, addrA, addrB, lo1x2, sgh_fixup<EDGE>(raw[m], fix, m), nonzero, nsat);
+		} else {
+#pragma unroll
+			for (int m = 0; m < M; m++)
+				if (f0 + m < N)
+					sgh_bin_pair(h, addrA, addrB, lo1x2, sgh_fixup<EDGE>(raw[m], fix, m), nonzero, nsat);
+		}
+		counted += (N - f0 < M ? N - f0 : M);
+	};
+	/* invariant: T = table of block nx(fb) = the block loaded next */
+	auto nx = [&](int f) { return f + STEP < N ? f + STEP : f; };
+	while (fb < N) {
+		loadblk(nx(fb), bufB, fixB);
+		sgh_tab16(p, nx(nx(fb)), T);
+		binblk(fb, bufA, fixA);
+		fb += STEP;
+		if (fb >= N)
+			break;
+		loadblk(nx(fb), bufA, fixA);
+		sgh_tab16(p, nx(nx(fb)), T);
+		binblk(fb, bufB, fixB);
+		fb += STEP;
+	}
+}
+
+__global__ void __launch_bounds__(64 * SGH_WAVES)
+k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
+	__shared__ SghLds L;
+	const int tid = threadIdx.x, lane = tid & 63;
+	const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+	const int ntx = (p.W + SGH_COLS - 1) / SGH_COLS;
+	const int nrows = p.row_end - p.row_begin;
+	/* XCD-aware tile order: the dispatcher deals workgroups round-robin to the 8 XCDs, so
+	 * XCD k gets a contiguous run of tiles (whole rows: neighbouring tiles share the 128-B
+	 * lines their shifted rows straddle in that XCD's L2, and the slower image-edge tiles
+	 * spread evenly instead of all landing on XCDs 0 and 7) */
+	const int nblk = (int)gridDim.x, xcd = (int)blockIdx.x & 7, q = nblk >> 3, rem = nblk & 7;
+	int bid = xcd * q + (xcd < rem ? xcd : rem) + ((int)blockIdx.x >> 3);
+	const int xt = bid % ntx;
+	bid /= ntx;
+	const int R = p.row_begin + (bid % nrows);
+	const int c = bid / nrows;
+	const int x0 = xt * SGH_COLS;
+	bool interior = x0 >= p.hist_maxsx && x0 + SGH_COLS + p.hist_maxsx <= p.W;
+	if (p.dbg == 4)		/* A/B: every full tile on the dword path (wrong edges) */
+		interior = x0 + SGH_COLS <= p.W;
+	if (p.dbg == 5 && !interior)	/* A/B: skip the edge tiles */
+		return;
+	SghFrame F;
+	F.plane0 = (const char *)(p.frames + (int64_t)c * p.plane_stride);
+	F.fstride2 = p.frame_stride * 2;
+	F.plane_bytes = (uint32_t)p.H * (uint32_t)p.W * 2u;
+	F.w2 = p.W * 2;
+	F.rw2 = R * p.W * 2;
+	F.xa2 = (uint32_t)(x0 + 2 * lane) * 2u;
+
+	for (int i = tid; i < (SGH_DW + 2) * SGH_COLS; i += 64 * SGH_WAVES)
+		(&L.hist[0][0])[i] = 0;
+	if (tid < SGH_COLS) {
+		L.nz[tid] = 0;
+		L.ns[tid] = 0;
+	}
+	__syncthreads();
+
+	uint32_t nonzero = 0, nsat = 0;
+	int counted = 0, lo_a, lo_b;
+	if (interior)
+		sgh_build<false>(p, L, F, wave, lane, lo_a, lo_b, nonzero, nsat, counted);
+	else
+		sgh_build<true>(p, L, F, wave, lane, lo_a, lo_b, nonzero, nsat, counted);
+	if (counted) {
+		atomicAdd(&L.nz[lane], (uint32_t)counted - (nonzero & 0xFFFFu));
+		atomicAdd(&L.nz[64 + lane], (uint32_t)counted - (nonzero >> 16));
+		atomicAdd(&L.ns[lane], nsat & 0xFFFFu);
+		atomicAdd(&L.ns[64 + lane], nsat >> 16);
+	}
+	__syncthreads();
+	if (wave >= 2)
+		return;
+	/* waves 0 / 1 finish the even / odd pixels of the tile */
+	sgh_finish(p, L, lane + 64 * wave, wave ? lo_b : lo_a, R, c, x0 + 2 * lane + wave, redo_count, redo_list);
 }

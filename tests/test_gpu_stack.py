@@ -172,6 +172,22 @@ def test_hist_path_matches_oracle_and_sorted(gpu_ctx, N):
     assert st.chain_pixels <= 0.05 * H * W, st.chain_pixels
 
 
+@pytest.mark.parametrize("shifts", [True, False])
+@pytest.mark.parametrize("W", [700, 1024])
+def test_hist_path_interior_tiles(gpu_ctx, W, shifts):
+    """wide frames: interior 128-pixel tiles take the dword-load path (no column checks),
+    the two image-edge tile columns the per-pixel path; both must agree with the oracle"""
+    N, H = 40, 48
+    frames = orc.synth(N, 1, H, W, seed=900 + W, maxshift=12)
+    sx, sy = orc.synth_shifts(N, seed=900 + W, maxshift=12) if shifts else (None, None)
+    out_h, rej_h, st = _stack_path(gpu_ctx, frames, sg.SIGMA, (3.0, 3.0), sx, sy, max_thread=2)
+    rc, ref, rej_ref = orc.stack_rejection(frames, sg.SIGMA, sig=(3.0, 3.0), shiftx=sx, shifty=sy, max_thread=2)
+    assert rc == 0
+    assert_same(out_h, ref, f"hist W={W} shifts={shifts}")
+    assert np.array_equal(rej_h, rej_ref)
+    assert st.chain_pixels <= 0.05 * H * W, st.chain_pixels
+
+
 @pytest.mark.parametrize("case", ["constant", "uniform", "bimodal", "saturated", "tight_sig", "dark"])
 def test_hist_path_adversarial(gpu_ctx, case):
     """inputs that defeat the histogram's assumptions must fall back, not differ:
