@@ -50,6 +50,28 @@ def parse():
     return ap.parse_args()
 
 
+def _mix64(z):
+    z = (z + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return z ^ (z >> 31)
+
+
+def synth_shifts_np(N, seed, maxshift):
+    """registration shifts of the synthetic sequence (include/sg_synth.h sg_synth_shift):
+    (shiftx, shifty) = (-dx_f, -dy_f), frame 0 = 0"""
+    import numpy as np
+    shx = np.zeros(N, dtype=np.int32)
+    shy = np.zeros(N, dtype=np.int32)
+    for f in range(1, N):
+        h = _mix64(seed ^ 0x51B1 ^ (f << 32))
+        if maxshift > 0:
+            span = 2 * maxshift + 1
+            shx[f] = -((h & 0xFFFFFFFF) % span - maxshift)
+            shy[f] = -(((h >> 32) & 0xFFFFFFFF) % span - maxshift)
+    return shx, shy
+
+
 def cpu_baseline(args, N, W):
     """Oracle (C restatement of the reference stacker, -O2 -fopenmp, the reference's block
     partition and OpenMP schedule) on a bounded sample of the same workload."""
@@ -105,27 +127,7 @@ def main():
     frames = torch.empty(N * fstride, dtype=torch.int16, device="cuda")
     out = torch.empty(H * W, dtype=torch.int16, device="cuda")
     ctx.synth_fill(frames.data_ptr(), N, 1, H, W, 0, H, 0x5151 + rank, args.maxshift, frame_stride=fstride)
-    import ctypes
-    sx = (ctypes.c_int * N)()
-    sy = (ctypes.c_int * N)()
-    # the synthetic shifts are a pure function; recompute them with the same mixer
-    import numpy as np
-
-    def mix64(z):
-        z = (z + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
-        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
-        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
-        return z ^ (z >> 31)
-
-    seed = 0x5151 + rank
-    shx = np.zeros(N, dtype=np.int32)
-    shy = np.zeros(N, dtype=np.int32)
-    for f in range(1, N):
-        h = mix64(seed ^ 0x51B1 ^ (f << 32))
-        if args.maxshift > 0:
-            span = 2 * args.maxshift + 1
-            shx[f] = -((h & 0xFFFFFFFF) % span - args.maxshift)
-            shy[f] = -(((h >> 32) & 0xFFFFFFFF) % span - args.maxshift)
+    shx, shy = synth_shifts_np(N, 0x5151 + rank, args.maxshift)
     if args.even_shifts:
         shx &= ~1
     if args.zero_shift:

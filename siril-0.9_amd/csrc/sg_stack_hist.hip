@@ -49,8 +49,21 @@ typedef unsigned short sgh_u16x2 __attribute__((ext_vector_type(2)));
  * hist[1 + SGH_DW][col]  : samples above the band (u32) */
 struct SghLds {
 	uint32_t hist[SGH_DW + 2][SGH_COLS];
-	uint16_t cum16[SGH_DW / 4][SGH_COLS];	/* band samples in bins < 16(j+1) */
 	uint32_t nz[SGH_COLS], ns[SGH_COLS];	/* zeros / 65535s (all of them lie outside the band) */
+};
+
+/* Finish-phase queries.  The band is cut into SGH_NGRP groups of SGH_GRP dwords (32 bins);
+ * the exclusive prefix count / moments at each group start are kept in registers, so a
+ * rank or prefix query is one lane-local table select plus SGH_GRP independent LDS reads
+ * (one LDS round trip) instead of a dependent walk. */
+#define SGH_GRP 8
+#define SGH_NGRP (SGH_DW / SGH_GRP)
+
+/* count / sum / sum of squares of (v - lo) over a set of samples */
+struct SghM {
+	int c;
+	long long s;
+	unsigned long long ss;
 };
 
 struct SghPix {
@@ -58,112 +71,158 @@ struct SghPix {
 	int nz, ns, nb;		/* zeros, 65535s, band samples (nz + nb + ns == N) */
 	int col;
 	const SghLds *L;
+	uint32_t pc[SGH_NGRP], ps[SGH_NGRP], pss[SGH_NGRP];	/* band prefix before group g */
+	SghM Z;			/* moments of the zeros */
+	SghM T;			/* moments of all samples */
 };
 
-/* # band samples with bin index <= t (t in [-1, 255]) */
-__device__ __forceinline__ int sgh_band_le(const SghPix &P, int t) {
-	if (t < 0)
-		return 0;
-	if (t > SGH_BINS - 1)
-		t = SGH_BINS - 1;
-	const int j16 = t >> 4, jd = t >> 2;
-	int base = j16 ? (int)P.L->cum16[j16 - 1][P.col] : 0;
-	for (int k = 4 * j16; k < jd; k++)
-		base += (int)__builtin_amdgcn_sad_u8(P.L->hist[1 + k][P.col], 0u, 0u);
-	const uint32_t d = P.L->hist[1 + jd][P.col];
+/* t[k] for a lane-varying k in [0, 8): a 3-level select tree on the bits of k */
+__device__ __forceinline__ uint32_t sgh_sel(const uint32_t (&t)[SGH_NGRP], int k) {
+	static_assert(SGH_NGRP == 8, "3-level tree");
+	const bool b0 = (k & 1) != 0, b1 = (k & 2) != 0, b2 = (k & 4) != 0;
+	const uint32_t a0 = b0 ? t[1] : t[0], a1 = b0 ? t[3] : t[2], a2 = b0 ? t[5] : t[4], a3 = b0 ? t[7] : t[6];
+	const uint32_t c0 = b1 ? a1 : a0, c1 = b1 ? a3 : a2;
+	return b2 ? c1 : c0;
+}
+
+__device__ __forceinline__ void sgh_grp(const SghPix &P, int g, uint32_t (&d)[SGH_GRP]) {
+	const uint32_t *b = &P.L->hist[1 + g * SGH_GRP][P.col];
+#pragma unroll
+	for (int k = 0; k < SGH_GRP; k++)
+		d[k] = b[k * SGH_COLS];
+}
+
+typedef unsigned short sgh_u16x2v __attribute__((ext_vector_type(2)));
+
+/* moments of the bins of one group, relative to the group's first bin: the dword k of the
+ * group holds bins 4k..4k+3, so sum (4k+b) c_b is a u8 dot product and sum (4k+b)^2 c_b
+ * two u16 dot products on the unpacked byte pairs (all weights compile-time constants) */
+template <int K>
+__device__ __forceinline__ void sgh_dw_moments(uint32_t dd, uint32_t &c, uint32_t &s, uint32_t &ss) {
+	constexpr uint32_t w1 = (uint32_t)(4 * K) | ((uint32_t)(4 * K + 1) << 8) | ((uint32_t)(4 * K + 2) << 16) |
+		((uint32_t)(4 * K + 3) << 24);
+	constexpr unsigned short q0 = (unsigned short)((4 * K) * (4 * K)), q1 = (unsigned short)((4 * K + 1) * (4 * K + 1));
+	constexpr unsigned short q2 = (unsigned short)((4 * K + 2) * (4 * K + 2)), q3 = (unsigned short)((4 * K + 3) * (4 * K + 3));
+	c = __builtin_amdgcn_sad_u8(dd, 0u, c);
+	s = __builtin_amdgcn_udot4(dd, w1, s, false);
+	const uint32_t lo = __builtin_amdgcn_perm(dd, dd, 0x0c010c00u), hi = __builtin_amdgcn_perm(dd, dd, 0x0c030c02u);
+	ss = __builtin_amdgcn_udot2(__builtin_bit_cast(sgh_u16x2v, lo), (sgh_u16x2v){q0, q1}, ss, false);
+	ss = __builtin_amdgcn_udot2(__builtin_bit_cast(sgh_u16x2v, hi), (sgh_u16x2v){q2, q3}, ss, false);
+}
+
+__device__ __forceinline__ void sgh_grp_moments(const uint32_t (&d)[SGH_GRP], uint32_t &c, uint32_t &s, uint32_t &ss) {
+	static_assert(SGH_GRP == 8, "unrolled for 8 dwords");
+	sgh_dw_moments<0>(d[0], c, s, ss);
+	sgh_dw_moments<1>(d[1], c, s, ss);
+	sgh_dw_moments<2>(d[2], c, s, ss);
+	sgh_dw_moments<3>(d[3], c, s, ss);
+	sgh_dw_moments<4>(d[4], c, s, ss);
+	sgh_dw_moments<5>(d[5], c, s, ss);
+	sgh_dw_moments<6>(d[6], c, s, ss);
+	sgh_dw_moments<7>(d[7], c, s, ss);
+}
+
+/* a prefix query "samples with value <= v" (v in [-1, 65535]): the group of the band bin is
+ * read once; the count is cheap and the moments are only formed for the passes that
+ * actually remove samples */
+struct SghQ {
+	int v, t, g;
+	uint32_t d[SGH_GRP];	/* the group's dwords, masked to bins <= t */
+};
+
+__device__ __forceinline__ void sgh_q_load(const SghPix &P, int v, SghQ &q) {
+	int t = v - P.lo;
+	t = t < -1 ? -1 : (t > SGH_BINS - 1 ? SGH_BINS - 1 : t);
+	q.v = v;
+	q.t = t;
+	q.g = (t < 0 ? 0 : t) >> 5;
+	sgh_grp(P, q.g, q.d);
+	const int jt = t >> 2;	/* -1 for t = -1: nothing counted */
 	const int sh = ((t & 3) + 1) * 8;
-	const uint32_t m = sh >= 32 ? 0xFFFFFFFFu : ((1u << sh) - 1u);
-	return base + (int)__builtin_amdgcn_sad_u8(d & m, 0u, 0u);
+	const uint32_t mt = sh >= 32 ? 0xFFFFFFFFu : ((1u << sh) - 1u);
+#pragma unroll
+	for (int k = 0; k < SGH_GRP; k++) {
+		const int j = q.g * SGH_GRP + k;
+		q.d[k] &= (j < jt ? 0xFFFFFFFFu : (j == jt ? mt : 0u));
+	}
 }
 
-/* # samples with value <= v, v in [-1, 65535] */
+__device__ __forceinline__ int sgh_q_count(const SghPix &P, const SghQ &q) {
+	uint32_t c = sgh_sel(P.pc, q.g);
+#pragma unroll
+	for (int k = 0; k < SGH_GRP; k++)
+		c = __builtin_amdgcn_sad_u8(q.d[k], 0u, c);
+	if (q.v < 0)
+		return 0;
+	if (q.v >= 65535)
+		return P.T.c;
+	return P.nz + (int)c;
+}
+
+__device__ __forceinline__ SghM sgh_q_moments(const SghPix &P, const SghQ &q) {
+	uint32_t c = 0, s = 0, ss = 0;
+	sgh_grp_moments(q.d, c, s, ss);
+	const uint32_t b0 = (uint32_t)q.g * (4u * SGH_GRP);	/* first bin of the group */
+	SghM m;
+	m.c = P.nz + (int)(sgh_sel(P.pc, q.g) + c);
+	m.s = P.Z.s + (long long)(sgh_sel(P.ps, q.g) + s + b0 * c);
+	m.ss = P.Z.ss + (unsigned long long)(sgh_sel(P.pss, q.g) + ss + 2u * b0 * s + b0 * b0 * c);
+	if (q.v < 0) {
+		m.c = 0;
+		m.s = 0;
+		m.ss = 0;
+	}
+	if (q.v >= 65535)
+		m = P.T;
+	return m;
+}
+
+/* moments of the samples with value <= v (rare paths) */
 __device__ __forceinline__ int sgh_cnt_le(const SghPix &P, int v) {
-	if (v < 0)
-		return 0;
-	if (v < P.lo)
-		return P.nz;
-	if (v < P.lo + SGH_BINS)
-		return P.nz + sgh_band_le(P, v - P.lo);
-	if (v < 65535)
-		return P.nz + P.nb;
-	return P.nz + P.nb + P.ns;
+	SghQ q;
+	sgh_q_load(P, v, q);
+	return sgh_q_count(P, q);
 }
 
-/* value at global rank g (0-based) */
-__device__ int sgh_value_at(const SghPix &P, int g) {
-	if (g < P.nz)
-		return 0;
-	g -= P.nz;
-	if (g >= P.nb)
-		return 65535;
-	/* smallest j with cum16[j] > g, then walk its 4 dwords */
-	int a = 0, b = SGH_DW / 4 - 1;
-	while (a < b) {
-		const int m = (a + b) >> 1;
-		if ((int)P.L->cum16[m][P.col] > g)
-			b = m;
-		else
-			a = m + 1;
+/* value of band rank r inside group g (d = the group's dwords, base = samples before it) */
+__device__ __forceinline__ int sgh_locate(const SghPix &P, int g, const uint32_t (&d)[SGH_GRP], uint32_t base, uint32_t r) {
+	uint32_t cum = base, before = base, kk = 0, dsel = d[0];
+#pragma unroll
+	for (int k = 0; k < SGH_GRP - 1; k++) {
+		cum += __builtin_amdgcn_sad_u8(d[k], 0u, 0u);
+		const bool past = cum <= r;	/* rank r lies after dword k */
+		kk += past ? 1u : 0u;
+		before = past ? cum : before;
+		dsel = past ? d[k + 1] : dsel;
 	}
-	int base = a ? (int)P.L->cum16[a - 1][P.col] : 0;
-	int k = 4 * a;
-	uint32_t d = P.L->hist[1 + k][P.col];
-	for (; k < 4 * a + 3; k++) {
-		const int bs = (int)__builtin_amdgcn_sad_u8(d, 0u, 0u);
-		if (base + bs > g)
-			break;
-		base += bs;
-		d = P.L->hist[2 + k][P.col];
-	}
-	int i = 0;
-	for (; i < 3; i++) {
-		base += (int)((d >> (8 * i)) & 0xFF);
-		if (base > g)
-			break;
-	}
-	return P.lo + 4 * k + i;
+	const uint32_t b0 = before + (dsel & 0xFFu), b1 = b0 + ((dsel >> 8) & 0xFFu), b2 = b1 + ((dsel >> 16) & 0xFFu);
+	const int i = (b0 <= r ? 1 : 0) + (b1 <= r ? 1 : 0) + (b2 <= r ? 1 : 0);
+	return P.lo + 4 * (g * SGH_GRP + (int)kk) + i;
 }
 
-/* sum and sum of squares of (v - lo) over samples with v1 <= v <= v2 */
-__device__ void sgh_range_moments(const SghPix &P, int v1, int v2, long long &s, unsigned long long &ss) {
-	s = 0;
-	ss = 0;
-	if (v1 > v2)
-		return;
-	if (P.nz && v1 <= 0 && 0 <= v2) {
-		const long long d = -P.lo;
-		s += d * P.nz;
-		ss += (unsigned long long)(d * d) * (unsigned long long)P.nz;
+/* values at global ranks g1 and g2 (g2 == g1 or g1 + 1), one group read when both lie
+ * in the same band group */
+__device__ __forceinline__ void sgh_value_at2(const SghPix &P, int g1, int g2, int &m1, int &m2) {
+	const int r1 = g1 - P.nz, r2 = g2 - P.nz;
+	const bool in1 = r1 >= 0 && r1 < P.nb, in2 = r2 >= 0 && r2 < P.nb;
+	int grp1 = 0, grp2 = 0;
+#pragma unroll
+	for (int k = 1; k < SGH_NGRP; k++) {
+		grp1 += (int)P.pc[k] <= r1 ? 1 : 0;
+		grp2 += (int)P.pc[k] <= r2 ? 1 : 0;
 	}
-	if (P.ns && v1 <= 65535 && 65535 <= v2) {
-		const long long d = 65535 - P.lo;
-		s += d * P.ns;
-		ss += (unsigned long long)(d * d) * (unsigned long long)P.ns;
+	uint32_t d[SGH_GRP];
+	sgh_grp(P, grp1, d);
+	const uint32_t base1 = sgh_sel(P.pc, grp1);
+	m1 = in1 ? sgh_locate(P, grp1, d, base1, (uint32_t)r1) : (r1 < 0 ? 0 : 65535);
+	if (in2 && grp2 == grp1) {
+		m2 = sgh_locate(P, grp1, d, base1, (uint32_t)r2);
+	} else if (in2) {
+		sgh_grp(P, grp2, d);
+		m2 = sgh_locate(P, grp2, d, sgh_sel(P.pc, grp2), (uint32_t)r2);
+	} else {
+		m2 = r2 < 0 ? 0 : 65535;
 	}
-	int b1 = v1 - P.lo, b2 = v2 - P.lo;
-	if (b1 < 0)
-		b1 = 0;
-	if (b2 > SGH_BINS - 1)
-		b2 = SGH_BINS - 1;
-	if (b1 > b2)
-		return;
-	uint32_t s32 = 0, ss32 = 0;
-	for (int j = b1 >> 2; j <= (b2 >> 2); j++) {
-		uint32_t d = P.L->hist[1 + j][P.col];
-		const int first = 4 * j, last = 4 * j + 3;
-		if (first < b1)
-			d &= 0xFFFFFFFFu << (8 * (b1 - first));
-		if (last > b2)
-			d &= 0xFFFFFFFFu >> (8 * (last - b2));
-		const uint32_t bs = __builtin_amdgcn_sad_u8(d, 0u, 0u);
-		const uint32_t d1 = __builtin_amdgcn_udot4(d, 0x03020100u, 0u, false);
-		const uint32_t d2 = __builtin_amdgcn_udot4(d, 0x09040100u, 0u, false);
-		const uint32_t jj = (uint32_t)j;
-		s32 += 4u * jj * bs + d1;
-		ss32 += 16u * jj * jj * bs + 8u * jj * d1 + d2;
-	}
-	s += (long long)s32;
-	ss += (unsigned long long)ss32;
 }
 
 __device__ __forceinline__ int sgh_ceil_clamp(double x) {
@@ -182,19 +241,23 @@ __device__ __forceinline__ int sgh_floor_clamp(double x) {
 }
 
 /* the reference's SIGMA loop on the histogram; returns SG_CLS_OK or 1 (redo in the
- * sorted kernel).  Decision logic mirrors clip_pass() of the sorted path. */
-__device__ int sgh_sigma(const SghPix &P, int N, double sl, double sh, long long S, unsigned long long SS,
-		uint16_t *value, uint32_t *rlo_out, uint32_t *rhi_out) {
-	/* kept set = samples with A <= v <= B; cntA = # samples < A, cntB = # samples <= B */
-	int A = 0, B = 65535, n = N, r = 0, nrem, cntA = 0, cntB = N;
+ * sorted kernel).  Decision logic mirrors clip_pass() of the sorted path.  The kept set
+ * is the value interval [A, B]; MA / MB = moments of the samples < A / <= B. */
+__device__ __forceinline__ int sgh_sigma(const SghPix &P, int N, double sl, double sh, uint16_t *value, uint32_t *rlo_out,
+		uint32_t *rhi_out, int &passes) {
+	int A = 0, B = 65535, n = N, r = 0, nrem;
+	passes = 0;
+	SghM MA = {0, 0, 0}, MB = P.T;
 	uint32_t rlo = 0, rhi = 0;
 	do {
+		const long long S = MB.s - MA.s;
+		const unsigned long long SS = MB.ss - MA.ss;
 		const long long num = (long long)n * (long long)SS - S * S;
 		const bool exact0 = (num == 0);
 		const double sigma = num <= 0 ? 0.0 : sqrt((double)num / ((double)n * (double)(n - 1)));
-		const int g1 = cntA + (n - 1) / 2, g2 = cntA + n / 2;
-		const int m1 = sgh_value_at(P, g1);
-		const int m2 = (g2 == g1) ? m1 : sgh_value_at(P, g2);
+		const int g1 = MA.c + (n - 1) / 2, g2 = MA.c + n / 2;
+		int m1, m2;
+		sgh_value_at2(P, g1, g2, m1, m2);
 		const double median = (g1 == g2) ? (double)m1 : (double)(m1 + m2) / 2.0;
 		const double tl = sl * sigma, th = sh * sigma;
 		const double blo = median - tl, bhi = median + th;
@@ -206,8 +269,11 @@ __device__ int sgh_sigma(const SghPix &P, int N, double sl, double sh, long long
 		int bt = sgh_floor_clamp(bhi + tol);
 		if (bt > B)
 			bt = B;
-		const int cnt_a = a > A ? sgh_cnt_le(P, a - 1) : cntA;	/* # < a */
-		const int cnt_bt = bt < B ? sgh_cnt_le(P, bt) : cntB;	/* # <= bt */
+		/* a == A gives M(A - 1) == MA and bt == B gives MB: both queries unconditional */
+		SghQ qa, qb;
+		sgh_q_load(P, a - 1, qa);
+		sgh_q_load(P, bt, qb);
+		const int cnt_a = sgh_q_count(P, qa), cnt_bt = sgh_q_count(P, qb);
 		if (!exact0) {
 			int amb1 = sgh_floor_clamp(blo + tol);
 			if (amb1 > B)
@@ -220,7 +286,7 @@ __device__ int sgh_sigma(const SghPix &P, int N, double sl, double sh, long long
 			if (amb0 <= bt && cnt_bt - sgh_cnt_le(P, amb0 - 1) > 0)
 				return 1;
 		}
-		const int L = cnt_a - cntA, H = cntB - cnt_bt;
+		const int L = cnt_a - MA.c, H = MB.c - cnt_bt;
 		if (L + H > n)
 			return 1;
 		/* `if (N - r <= 4) break;` inside the clipping loop (:1684) */
@@ -235,30 +301,21 @@ __device__ int sgh_sigma(const SghPix &P, int N, double sl, double sh, long long
 		if (fb >= 0 && fb < n - 1)
 			return 1;
 		if (L) {
-			long long s;
-			unsigned long long ss;
-			sgh_range_moments(P, A, a - 1, s, ss);
-			S -= s;
-			SS -= ss;
 			A = a;
-			cntA = cnt_a;
+			MA = sgh_q_moments(P, qa);
 		}
 		if (H) {
-			long long s;
-			unsigned long long ss;
-			sgh_range_moments(P, bt + 1, B, s, ss);
-			S -= s;
-			SS -= ss;
 			B = bt;
-			cntB = cnt_bt;
+			MB = sgh_q_moments(P, qb);
 		}
 		rlo += L;
 		rhi += H;
 		r += L + H;
 		nrem = L + H;
 		n -= nrem;
+		passes++;
 	} while (nrem > 0 && n > 3);
-	const long long tot = S + (long long)n * P.lo;
+	const long long tot = (MB.s - MA.s) + (long long)n * P.lo;
 	*value = sg_round_to_WORD((double)tot / (double)n);
 	*rlo_out = rlo;
 	*rhi_out = rhi;
@@ -446,22 +503,24 @@ __device__ void sgh_finish(const SgStackParams &p, SghLds &L, int col, int lo, i
 			p.out[((int64_t)c * p.H + R) * p.W + x] = (uint16_t)(L.hist[1][col] + L.nz[col]);
 		return;
 	}
+	SghPix P;
 	uint32_t cum = 0, s32 = 0, ss32 = 0;
-#pragma unroll 16
-	for (int j = 0; j < SGH_DW; j++) {
-		const uint32_t d = L.hist[1 + j][col];
-		const uint32_t bs = __builtin_amdgcn_sad_u8(d, 0u, 0u);
-		const uint32_t d1 = __builtin_amdgcn_udot4(d, 0x03020100u, 0u, false);
-		const uint32_t d2 = __builtin_amdgcn_udot4(d, 0x09040100u, 0u, false);
-		const uint32_t jj = (uint32_t)j;
-		s32 += 4u * jj * bs + d1;
-		ss32 += 16u * jj * jj * bs + 8u * jj * d1 + d2;
-		cum += bs;
-		if ((j & 3) == 3)
-			L.cum16[j >> 2][col] = (uint16_t)cum;
+#pragma unroll
+	for (int g = 0; g < SGH_NGRP; g++) {
+		P.pc[g] = cum;
+		P.ps[g] = s32;
+		P.pss[g] = ss32;
+		uint32_t d[SGH_GRP], c = 0, s = 0, ss = 0;
+#pragma unroll
+		for (int k = 0; k < SGH_GRP; k++)
+			d[k] = L.hist[1 + g * SGH_GRP + k][col];
+		sgh_grp_moments(d, c, s, ss);
+		const uint32_t b0 = (uint32_t)g * (4u * SGH_GRP);
+		cum += c;
+		s32 += s + b0 * c;
+		ss32 += ss + 2u * b0 * s + b0 * b0 * c;
 	}
 	const int above = (int)L.hist[SGH_DW + 1][col];
-	SghPix P;
 	P.lo = lo;
 	P.nz = (int)L.nz[col];
 	P.ns = (int)L.ns[col];
@@ -480,11 +539,16 @@ __device__ void sgh_finish(const SgStackParams &p, SghLds &L, int col, int lo, i
 			cls = 1;
 		} else {
 			const long long dz = -(long long)lo, ds = 65535 - (long long)lo;
-			const long long S = (long long)s32 + dz * P.nz + ds * P.ns;
-			const unsigned long long SS = (unsigned long long)ss32 +
-				(unsigned long long)(dz * dz) * (unsigned long long)P.nz +
-				(unsigned long long)(ds * ds) * (unsigned long long)P.ns;
-			cls = sgh_sigma(P, N, p.sig0, p.sig1, S, SS, &value, &rlo, &rhi);
+			P.Z.c = P.nz;
+			P.Z.s = dz * P.nz;
+			P.Z.ss = (unsigned long long)(dz * dz) * (unsigned long long)P.nz;
+			P.T.c = N;
+			P.T.s = (long long)s32 + P.Z.s + ds * P.ns;
+			P.T.ss = (unsigned long long)ss32 + P.Z.ss + (unsigned long long)(ds * ds) * (unsigned long long)P.ns;
+			int passes;
+			cls = sgh_sigma(P, N, p.sig0, p.sig1, &value, &rlo, &rhi, passes);
+			if (p.dbg == 7)	/* A/B: pass count per pixel */
+				value = (uint16_t)passes;
 		}
 		const int64_t pix = ((int64_t)c * p.H + R) * p.W + x;
 		if (cls == SG_CLS_OK) {
@@ -637,3 +701,4 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 	/* waves 0 / 1 finish the even / odd pixels of the tile */
 	sgh_finish(p, L, lane + 64 * wave, wave ? lo_b : lo_a, R, c, x0 + 2 * lane + wave, redo_count, redo_list);
 }
+
