@@ -15,3 +15,4 @@ run() { # name dbg extra-args
 run full 0
 run prefix_only 1
 run no_finish 2
+run loads_only 3

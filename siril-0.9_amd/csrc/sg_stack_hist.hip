@@ -44,11 +44,15 @@
 
 typedef unsigned short sgh_u16x2 __attribute__((ext_vector_type(2)));
 
-/* hist[0][col]          : samples below the band land in byte 3 (garbage, unused)
- * hist[1 + j][col] byte b: count of value lo + 4j + b
- * hist[1 + SGH_DW][col]  : samples above the band (u32) */
+/* Histogram layout: pixel column c = 64 half + l (half 0 = the low u16 of a lane's pixel
+ * pair, half 1 the high one, l = lane) keeps its band in h[half][j][l]: a wave's 64 lanes
+ * always address 64 different banks, whatever bins they hit.
+ *   h[half][j][l] byte b (j < 64): count of value lo + 4 j + b   (u8 counters)
+ *   h[half][64][l]               : samples outside the band (u32: zeros, 65535s; anything
+ *                                  else sends the pixel to the redo list) */
+#define SGH_HROWS (SGH_DW + 1)
 struct SghLds {
-	uint32_t hist[SGH_DW + 2][SGH_COLS];
+	uint32_t h[2][SGH_HROWS][64];
 	uint32_t nz[SGH_COLS], ns[SGH_COLS];	/* zeros / 65535s (all of them lie outside the band) */
 };
 
@@ -86,10 +90,10 @@ __device__ __forceinline__ uint32_t sgh_sel(const uint32_t (&t)[SGH_NGRP], int k
 }
 
 __device__ __forceinline__ void sgh_grp(const SghPix &P, int g, uint32_t (&d)[SGH_GRP]) {
-	const uint32_t *b = &P.L->hist[1 + g * SGH_GRP][P.col];
+	const uint32_t *b = &P.L->h[P.col >> 6][g * SGH_GRP][P.col & 63];
 #pragma unroll
 	for (int k = 0; k < SGH_GRP; k++)
-		d[k] = b[k * SGH_COLS];
+		d[k] = b[k * 64];
 }
 
 typedef unsigned short sgh_u16x2v __attribute__((ext_vector_type(2)));
@@ -472,22 +476,30 @@ __device__ __forceinline__ uint32_t sgh_pk_add(uint32_t a, uint32_t b) {
 	return r;
 }
 
-/* bin the pixel pair of one frame (low half -> column of addrA, high half -> addrB):
- * s = min(max(v - lo + 1, 0), 257) + 3 is 3 below the band (dword 0 byte 3, ignored),
- * v - lo + 4 inside (dword 1 + (v-lo)/4, byte (v-lo)%4), 260 above (dword 65, a u32
- * counter); zeros and 65535s are counted per half */
-__device__ __forceinline__ void sgh_bin_pair(uint32_t *h, uint32_t addrA, uint32_t addrB, uint32_t lo1x2, uint32_t vv,
+__device__ __forceinline__ uint32_t sgh_pk_sub_wrap(uint32_t a, uint32_t b) {
+	uint32_t r;
+	asm("v_pk_sub_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+	return r;
+}
+__device__ __forceinline__ uint32_t sgh_pk_shl(uint32_t a, int n) {
+	uint32_t r;
+	asm("v_pk_lshlrev_b16 %0, %2, %1 op_sel_hi:[0,1]" : "=v"(r) : "v"(a), "i"(n));
+	return r;
+}
+
+/* bin the pixel pair of one frame (low half -> h[0], high half -> h[1], lane l4 = 4 l):
+ * t = min(v - lo (mod 2^16), 256) is the band bin, or 256 = the out-of-band counter (row
+ * 64) for anything below or above the band; row t >> 2 is at byte 256 (t >> 2), i.e. byte 1
+ * of t << 6 (one byte permute each), the counter byte is t & 3, so the increment is
+ * 1 << 8 (t & 3) = 1 << (8 t mod 32).  Zeros and 65535s are counted per half. */
+__device__ __forceinline__ void sgh_bin_pair(uint32_t *h, uint32_t l4, uint32_t lo2, uint32_t vv,
 		uint32_t &nonzero, uint32_t &nsat) {
-	const sgh_u16x2 v = __builtin_bit_cast(sgh_u16x2, vv);
-	sgh_u16x2 t = __builtin_elementwise_sub_sat(v, __builtin_bit_cast(sgh_u16x2, lo1x2));
-	t = __builtin_elementwise_min(t, (sgh_u16x2){257, 257}) + (sgh_u16x2){3, 3};
-	const uint32_t tt = __builtin_bit_cast(uint32_t, t);
-	const uint32_t a0 = ((tt << 7) & (0x7Fu << 9)) | addrA;	/* row stride 128 cols x 4 B */
-	const uint32_t a1 = ((tt >> 9) & (0x7Fu << 9)) | addrB;
-	const uint32_t i0 = 1u << ((tt << 3) & 24u);
-	const uint32_t i1 = 1u << ((tt >> 13) & 24u);
-	atomicAdd(h + (a0 >> 2), i0);
-	atomicAdd(h + (a1 >> 2), i1);
+	const uint32_t t = sgh_pk_min(sgh_pk_sub_wrap(vv, lo2), 0x01000100u);
+	const uint32_t t64 = sgh_pk_shl(t, 6), t8 = sgh_pk_shl(t, 3);
+	const uint32_t a0 = __builtin_amdgcn_perm(t64, l4, 0x0c0c0500u), a1 = __builtin_amdgcn_perm(t64, l4, 0x0c0c0700u);
+	const uint32_t i0 = 1u << (t8 & 31u), i1 = 1u << ((t8 >> 16) & 31u);
+	atomicAdd((uint32_t *)((char *)h + a0), i0);
+	atomicAdd((uint32_t *)((char *)h + sizeof(uint32_t) * SGH_HROWS * 64 + a1), i1);
 	nonzero = sgh_pk_add(nonzero, sgh_pk_min(vv, 0x00010001u));
 	nsat = sgh_pk_add(nsat, sgh_pk_sub_sat(vv, 0xFFFEFFFEu));
 }
@@ -498,9 +510,10 @@ __device__ void sgh_finish(const SgStackParams &p, SghLds &L, int col, int lo, i
 		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
 	const int lane = threadIdx.x & 63;
 	const int N = p.N;
+	const uint32_t *hc = &L.h[col >> 6][0][col & 63];	/* dword j at hc[64 j] */
 	if (p.dbg == 2 || p.dbg == 3) {
 		if (x < p.W)
-			p.out[((int64_t)c * p.H + R) * p.W + x] = (uint16_t)(L.hist[1][col] + L.nz[col]);
+			p.out[((int64_t)c * p.H + R) * p.W + x] = (uint16_t)(hc[0] + L.nz[col]);
 		return;
 	}
 	SghPix P;
@@ -513,14 +526,14 @@ __device__ void sgh_finish(const SgStackParams &p, SghLds &L, int col, int lo, i
 		uint32_t d[SGH_GRP], c = 0, s = 0, ss = 0;
 #pragma unroll
 		for (int k = 0; k < SGH_GRP; k++)
-			d[k] = L.hist[1 + g * SGH_GRP + k][col];
+			d[k] = hc[64 * (g * SGH_GRP + k)];
 		sgh_grp_moments(d, c, s, ss);
 		const uint32_t b0 = (uint32_t)g * (4u * SGH_GRP);
 		cum += c;
 		s32 += s + b0 * c;
 		ss32 += ss + 2u * b0 * s + b0 * b0 * c;
 	}
-	const int above = (int)L.hist[SGH_DW + 1][col];
+	const int oob = (int)hc[64 * SGH_DW];
 	P.lo = lo;
 	P.nz = (int)L.nz[col];
 	P.ns = (int)L.ns[col];
@@ -533,9 +546,9 @@ __device__ void sgh_finish(const SgStackParams &p, SghLds &L, int col, int lo, i
 	if (x < p.W) {
 		if (p.dbg == 1) {
 			value = (uint16_t)(s32 + ss32);
-		} else if (N - P.nb - above != P.nz || above != P.ns) {
+		} else if (P.nb + oob != N || oob != P.nz + P.ns) {
 			/* an out-of-band sample that is not 0 / 65535, or a wrapped u8 counter (a
-			 * carry loses 255 or 256 band counts, so N - nb - above exceeds the zeros) */
+			 * carry loses 256 band counts) */
 			cls = 1;
 		} else {
 			const long long dz = -(long long)lo, ds = 65535 - (long long)lo;
@@ -581,8 +594,8 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, SghLds &L, con
 	constexpr int M = 16;		/* frames per block */
 	constexpr int STEP = M * SGH_WAVES;
 	const int N = p.N;
-	uint32_t *const h = &L.hist[0][0];
-	const uint32_t addrA = (uint32_t)lane * 4u, addrB = (uint32_t)(64 + lane) * 4u;
+	uint32_t *const h = &L.h[0][0][0];
+	const uint32_t l4 = (uint32_t)lane * 4u;
 	uint32_t bufA[M], bufB[M], p16[SGH_CENTER], fixA = 0, fixB = 0, fix0 = 0;
 	SghTab16 T;
 	auto loadblk = [&](int f0, uint32_t (&dst)[M], uint32_t &fix) {
@@ -609,7 +622,7 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, SghLds &L, con
 			bufA[m] = p16[m];
 		fixA = 0;
 	}
-	const uint32_t lo1x2 = (uint32_t)(lo_a - 1) | ((uint32_t)(lo_b - 1) << 16);
+	const uint32_t lo2 = (uint32_t)lo_a | ((uint32_t)lo_b << 16);
 	const bool loads_only = p.dbg == 3;
 	auto binblk = [&](int f0, const uint32_t (&raw)[M], uint32_t fix) {
 		if (loads_only) {
@@ -619,12 +632,12 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, SghLds &L, con
 		} else if (f0 + M <= N) {
 #pragma unroll
 			for (int m = 0; m < M; m++)
-				sgh_bin_pair(h, addrA, addrB, lo1x2, sgh_fixup<EDGE>(raw[m], fix, m), nonzero, nsat);
+				sgh_bin_pair(h, l4, lo2, sgh_fixup<EDGE>(raw[m], fix, m), nonzero, nsat);
 		} else {
 #pragma unroll
 			for (int m = 0; m < M; m++)
 				if (f0 + m < N)
-					sgh_bin_pair(h, addrA, addrB, lo1x2, sgh_fixup<EDGE>(raw[m], fix, m), nonzero, nsat);
+					sgh_bin_pair(h, l4, lo2, sgh_fixup<EDGE>(raw[m], fix, m), nonzero, nsat);
 		}
 		counted += (N - f0 < M ? N - f0 : M);
 	};
@@ -675,8 +688,8 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 	F.rw2 = R * p.W * 2;
 	F.xa2 = (uint32_t)(x0 + 2 * lane) * 2u;
 
-	for (int i = tid; i < (SGH_DW + 2) * SGH_COLS; i += 64 * SGH_WAVES)
-		(&L.hist[0][0])[i] = 0;
+	for (int i = tid; i < 2 * SGH_HROWS * 64; i += 64 * SGH_WAVES)
+		(&L.h[0][0][0])[i] = 0;
 	if (tid < SGH_COLS) {
 		L.nz[tid] = 0;
 		L.ns[tid] = 0;
