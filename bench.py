@@ -100,6 +100,24 @@ def cpu_baseline(args, N, W):
             "seconds": round(dt, 3), "rc": rc}
 
 
+def roofline(achieved, algo_bytes, N, H, W, rejection):
+    """roofline object of the dominant kernel (k_stack_hist for sigma): achieved = algorithmic
+    bytes per launch / HIP-event kernel time; traffic = HBM bytes per launch from the
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of the same workload (scripts/gpu_pmc_traffic.sh
+    -> profiles/traffic_<workload>.json, corrected per MI355X_MICROARCH.md), when present"""
+    r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None}
+    path = os.path.join(ROOT, "profiles", f"traffic_{rejection}_{N}x{H}x{W}.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            t = json.load(f)
+        r["traffic"] = int(t["traffic_bytes"])
+        r["traffic_unit"] = "B/launch"
+        r["traffic_over_algorithmic"] = round(t["traffic_bytes"] / algo_bytes, 4)
+        r["traffic_src"] = os.path.relpath(path, ROOT)
+    return r
+
+
 def main():
     args = parse()
     import torch
@@ -185,8 +203,7 @@ def main():
             "config": {"workload": f"sigma-clip stack {N}x{H}x{W} u16 mono per GPU (BASELINE configs[2])",
                        "frames": N, "height": H, "width": W, "rejection": args.rejection,
                        "sig": [4.0, 3.0], "parallelism": f"row-band x{world}"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None},
+            "roofline": roofline(achieved, algo_bytes, N, H, W, args.rejection),
             "kernel_ms": round(kavg, 3),
             "slow_pixels": int(slow),
             "redo_pixels": int(redo),
