@@ -30,6 +30,9 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--workload", choices=["sigma", "register-mean", "winsorized-rgb"], default="sigma",
+                    help="sigma = BASELINE configs[2] (the metric's configuration, default); "
+                         "register-mean = configs[1]; winsorized-rgb = configs[4] at one GPU")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--frames", type=int, default=512)
@@ -118,8 +121,91 @@ def roofline(achieved, algo_bytes, N, H, W, rejection):
     return r
 
 
+def main_config(args):
+    """BASELINE configs[1] (register-mean: DFT registration of 128 full 2048x2048 SER-like
+    frames + NO_REJEC mean stack with the found shifts) and configs[4] (winsorized-rgb: 256
+    3-plane 6000x4000 frames, DFT registration of a centred 2048x2048 selection of layer 1,
+    WINSORIZED (4, 3) stack), one GPU, frames resident in HBM.  One step = registration +
+    stack; the stage times are reported beside the step time."""
+    import numpy as np
+    import torch
+    import sirilgpu as sg
+    torch.cuda.set_device(0)
+    ctx = sg.Context([0])
+    if args.workload == "register-mean":
+        N, C, H, W, S, layer, rej, cfg = 128, 1, 2048, 2048, 2048, 0, sg.NO_REJEC, "BASELINE configs[1]"
+    else:
+        N, C, H, W, S, layer, rej, cfg = 256, 3, 4000, 6000, 2048, 1, sg.WINSORIZED, "BASELINE configs[4], 1 GPU"
+    fstride = C * H * W
+    frames = torch.empty(N * fstride, dtype=torch.int16, device="cuda")
+    out = torch.empty(C * H * W, dtype=torch.int16, device="cuda")
+    ctx.synth_fill(frames.data_ptr(), N, C, H, W, 0, H, 0x5EED, 16)
+    fv = frames.view(N, C, H, W)
+    y0, x0 = (H - S) // 2, (W - S) // 2
+
+    def step():
+        t0 = time.perf_counter()
+        if S == H and S == W and C == 1:
+            sel = frames                      # full-frame selection: the frames themselves
+        else:                                 # seq_read_frame_part of layer `layer`
+            sel = fv[:, layer, y0:y0 + S, x0:x0 + S].contiguous()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        sx, sy, q = ctx.register_dft_device(sel.data_ptr(), N, S)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        desc, keep = sg.make_desc(sg.MEAN, N, W, H, C, rejection=rej, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                                  max_thread=8, max_number_of_rows=H)
+        rejc, _ = ctx.stack_device(desc, frames.data_ptr(), fstride, H * W, out.data_ptr(), 0, H)
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        return (t1 - t0, t2 - t1, t3 - t2), ctx.stats(), sx, sy
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    stages = np.zeros(3)
+    kms = []
+    for _ in range(args.steps):
+        st, stats, sx, sy = step()
+        stages += np.array(st)
+        kms.append(stats.kernel_ms)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    stages /= args.steps
+    # registration shifts must recover the synthetic translations (frame 0 = reference)
+    ex, ey = synth_shifts_np(N, 0x5EED, 16)
+    reg_ok = bool(np.array_equal(sx, ex) and np.array_equal(sy, ey))
+    kavg = sum(kms) / len(kms)
+    stack_bytes = N * C * H * W * 2 + C * H * W * 2
+    achieved = stack_bytes / (kavg * 1e-3) / 1e9
+    reg_bytes = N * S * S * 58          # stated 2-pass c64 FFT model, SURVEY.md section 8(d)
+    res = {
+        "metric": "frames/sec stacked (registration + stack) + achieved HBM GB/s",
+        "value": round(N / (elapsed / args.steps), 2), "unit": "frames/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u16",
+        "data": "synthetic (include/sg_synth.h, generated in HBM)",
+        "config": {"workload": f"{args.workload} {N}x{C}x{H}x{W} ({cfg})", "frames": N, "layers": C,
+                   "height": H, "width": W, "selection": S, "register_layer": layer,
+                   "rejection": "none" if rej == sg.NO_REJEC else "winsorized"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "stack"},
+        "stage_ms": {"selection": round(stages[0] * 1e3, 3), "register": round(stages[1] * 1e3, 3),
+                     "stack": round(stages[2] * 1e3, 3), "stack_kernel": round(kavg, 3)},
+        "register_GBps_model": round(reg_bytes / stages[1] / 1e9, 1),
+        "slow_pixels": int(stats.slow_pixels), "redo_pixels": int(stats.chain_pixels),
+        "register_shifts_exact": reg_ok,
+    }
+    print(json.dumps(res), flush=True)
+    ctx.close()
+
+
 def main():
     args = parse()
+    if args.workload != "sigma":
+        return main_config(args)
     import torch
     import sirilgpu as sg
 

@@ -27,6 +27,7 @@ struct SgChainTables {
 template <int NREG, bool LISTED>
 __global__ void k_stack_sorted(SgStackParams p, const unsigned int *list, const unsigned int *list_count);
 __global__ void k_stack_hist(SgStackParams p, unsigned int *redo_count, unsigned int *redo_list);
+void sg_dbg_why_dump(hipStream_t s);
 __global__ void k_stack_reduce(SgStackParams p);
 __global__ void k_sum_finalize(SgStackParams p);
 __global__ void k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *scratch, int phase);
@@ -422,6 +423,8 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 	HIPCHK(hipMemcpyAsync(cnt, dv.flag_count.p, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
 	HIPCHK(hipMemcpyAsync(cnt + 1, dv.maxim.p, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
 	HIPCHK(hipStreamSynchronize(s));
+	if (p.dbg == 12)
+		sg_dbg_why_dump(s);
 	float ms = 0.f, ms2 = 0.f;
 	HIPCHK(hipEventElapsedTime(&ms, dv.ev[0], dv.ev[1]));
 	HIPCHK(hipEventElapsedTime(&ms2, dv.ev[0], dv.ev[2]));

@@ -9,7 +9,7 @@
 #include <vector>
 #include "../../include/sirilgpu.h"
 
-#define SG_LIT_THREADS 16384
+#define SG_LIT_THREADS 65536
 
 struct SgBuf {
 	void *p = nullptr;

@@ -143,6 +143,10 @@ __device__ __forceinline__ double exact_sd(int n, uint64_t S, uint64_t SS, bool 
  * differs from the exact one by ~(n+8)*2^-64 relative, the double ops add a few ulp */
 #define SG_BAND 1e-11
 
+/* A/B diagnostics (SG_HIST_DBG=12): why pixels leave the sorted path */
+__device__ unsigned int g_sg_why[32];
+#define SG_WHY(k) (atomicAdd(&g_sg_why[k], 1u), SG_CLS_LITERAL)
+
 struct SgRejState {
 	int lo, hi;
 	uint64_t S, SS;
@@ -166,16 +170,16 @@ __device__ int clip_pass(const SgCol &A, SgRejState &st, double sigma, bool exac
 		const int L1 = col_count_lt(A, st.lo, st.hi, blo - tol);
 		const int L2 = col_count_le(A, st.lo, st.hi, blo + tol);
 		if (L1 != L2)
-			return SG_CLS_LITERAL;
+			return SG_WHY(1);
 		const int H1 = N - col_count_le(A, st.lo, st.hi, bhi + tol);
 		const int H2 = N - col_count_lt(A, st.lo, st.hi, bhi - tol);
 		if (H1 != H2)
-			return SG_CLS_LITERAL;
+			return SG_WHY(2);
 		L = L1;
 		H = H1;
 	}
 	if (L + H > N)
-		return SG_CLS_LITERAL;	/* negative sigma factors: else-if order matters */
+		return SG_WHY(3);	/* negative sigma factors: else-if order matters */
 	/* where does `if (N - r <= 4) break;` fire?  r counts rejections cumulatively */
 	const int need = N - 4 - st.r;
 	int fb = -1;
@@ -189,7 +193,7 @@ __device__ int clip_pass(const SgCol &A, SgRejState &st, double sigma, bool exac
 		/* entries after fb keep stale values */
 		if (st.iter == 1) {
 			if (N0 > 4)
-				return SG_CLS_CHAIN;	/* stale values of the previous pixel */
+				return (atomicAdd(&g_sg_why[20], 1u), SG_CLS_CHAIN);	/* stale values of the previous pixel */
 			/* N0 <= 4: only entry 0 is ever written, the rest stay calloc zero (:1497) */
 			const int low0 = (L >= 1);
 			const int high0 = (!low0) && (H == N);
@@ -208,7 +212,7 @@ __device__ int clip_pass(const SgCol &A, SgRejState &st, double sigma, bool exac
 			*n_removed = n;
 			return SG_CLS_OK;
 		}
-		return SG_CLS_LITERAL;	/* stale values of this pixel's previous pass */
+		return SG_WHY(4);	/* stale values of this pixel's previous pass */
 	}
 	st.rlo += L;
 	st.rhi += H;
@@ -305,24 +309,24 @@ __device__ int reject_winsorized(const SgCol &A, SgRejState &st, double sl, doub
 		int guard = 0;
 		for (;;) {
 			if (++guard > 4096)
-				return SG_CLS_LITERAL;
+				return SG_WHY(5);
 			const double m0 = median - 1.5 * sigma;
 			const double m1 = median + 1.5 * sigma;
 			const double tol = sig_e0 ? 0.0 : SG_BAND * (fabs(median) + 1.5 * sigma + 1.0);
 			/* clamp: w < m0 -> round(m0); else w > m1 -> round(m1) */
 			int clo = wins_count_lt(A, st, w, m0 - tol);
 			if (!sig_e0 && clo != wins_count_le(A, st, w, m0 + tol))
-				return SG_CLS_LITERAL;
+				return SG_WHY(6);
 			int chi = N - wins_count_le(A, st, w, m1 + tol);
 			if (!sig_e0 && chi != N - wins_count_lt(A, st, w, m1 - tol))
-				return SG_CLS_LITERAL;
+				return SG_WHY(7);
 			if (clo + chi > N)
-				return SG_CLS_LITERAL;
+				return SG_WHY(8);
 			if (clo > 0) {
 				if (round_ambiguous(m0, tol + 1e-9 * tol))
-					return SG_CLS_LITERAL;
+					return SG_WHY(9);
 				if (clo < w.Lw || clo > N - w.Hw)
-					return SG_CLS_LITERAL;
+					return SG_WHY(10);
 				for (int i = w.Lw; i < clo; i++) {
 					const uint32_t v = A(st.lo + i);
 					w.Sin -= v;
@@ -333,9 +337,9 @@ __device__ int reject_winsorized(const SgCol &A, SgRejState &st, double sl, doub
 			}
 			if (chi > 0) {
 				if (round_ambiguous(m1, tol + 1e-9 * tol))
-					return SG_CLS_LITERAL;
+					return SG_WHY(11);
 				if (chi < w.Hw || chi > N - w.Lw)
-					return SG_CLS_LITERAL;
+					return SG_WHY(12);
 				for (int i = w.Hw; i < chi; i++) {
 					const uint32_t v = A(st.hi - 1 - i);
 					w.Sin -= v;
@@ -367,7 +371,7 @@ __device__ int reject_winsorized(const SgCol &A, SgRejState &st, double sl, doub
 			}
 			const double q = fabs(sigma - sigma0) / sigma0;
 			if (fabs(q - 0.0005) <= 1e-9 * 0.0005 + SG_BAND * (1.0 + q))
-				return SG_CLS_LITERAL;
+				return SG_WHY(13);
 			if (!(q > 0.0005))
 				break;
 		}
@@ -609,39 +613,56 @@ k_stack_reduce(SgStackParams p) {
 	const int x = blockIdx.x * 256 + threadIdx.x;
 	const int R = p.row_begin + blockIdx.y;
 	const int c = blockIdx.z;
-	unsigned int blockmax = 0;
-	if (x < p.W) {
-		const int64_t pix = ((int64_t)c * p.H + R) * p.W + x;
-		if (p.method == 1) {	/* mean, NO_REJEC: gathered (shift, zero fill, norm) */
-			uint32_t acc = 0;
-			for (int f = 0; f < p.N; f++)
-				acc += sg_gather(p, f, c, R, x);
-			p.out[pix] = sg_round_to_WORD((double)acc / (double)p.N);
-		} else {
-			uint32_t acc = (p.method == 4) ? 65535u : 0u;
-			for (int f = 0; f < p.N; f++) {
-				const int sx = p.use_shift ? p.shiftx[f] : 0;
-				const int sy = p.use_shift ? p.shifty[f] : 0;
-				const int nx = x - sx, ny = R - sy;
-				if ((unsigned)nx >= (unsigned)p.W || (unsigned)ny >= (unsigned)p.H)
-					continue;
-				if (nx == 0 && ny == 0)
-					continue;	/* `ii > 0`: source pixel 0 is never used (:307) */
-				const uint32_t v = p.frames[(int64_t)f * p.frame_stride +
-					(int64_t)c * p.plane_stride + (int64_t)ny * p.W + nx];
+	const bool live = x < p.W;
+	const int64_t pix = ((int64_t)c * p.H + R) * p.W + x;
+	const uint16_t *plane = p.frames + (int64_t)c * p.plane_stride;
+	const int N = p.N;
+	/* frames in batches of 16: every load of a batch is issued before any is used (an
+	 * out-of-frame sample loads a valid dummy address and is masked), so each wave keeps 16
+	 * row reads in flight */
+	uint32_t acc = (p.method == 4) ? 65535u : 0u;
+	for (int f0 = 0; f0 < N; f0 += 16) {
+		uint32_t v[16], xin = 0, ok = 0;
+#pragma unroll
+		for (int m = 0; m < 16; m++) {
+			const int f = f0 + m < N ? f0 + m : N - 1;
+			const int sx = p.use_shift ? p.shiftx[f] : 0;
+			const int sy = p.use_shift ? p.shifty[f] : 0;
+			const int nx = x - sx, ny = R - sy;
+			const bool xi = (unsigned)nx < (unsigned)p.W, yi = (unsigned)ny < (unsigned)p.H;
+			bool ld = live && f0 + m < N && xi && yi;
+			if (p.method != 1 && nx == 0 && ny == 0)
+				ld = false;	/* `ii > 0`: source pixel 0 is never used (:307) */
+			const int64_t off = ld ? (int64_t)f * p.frame_stride + (int64_t)ny * p.W + nx : 0;
+			v[m] = plane[off];
+			v[m] = ld ? v[m] : 0u;
+			xin |= (uint32_t)(xi && f0 + m < N) << m;
+			ok |= (uint32_t)ld << m;
+		}
+#pragma unroll
+		for (int m = 0; m < 16; m++) {
+			if (p.method == 1) {	/* mean, NO_REJEC: the gather of sg_gather (shift, zero fill, norm) */
+				if ((xin >> m) & 1u)
+					acc += p.normalize ? sg_normalize(p, f0 + m, (uint16_t)v[m]) : v[m];
+			} else if ((ok >> m) & 1u) {
 				if (p.method == 0)
-					acc += v;
+					acc += v[m];
 				else if (p.method == 3)
-					acc = v > acc ? v : acc;
+					acc = v[m] > acc ? v[m] : acc;
 				else
-					acc = v < acc ? v : acc;
+					acc = v[m] < acc ? v[m] : acc;
 			}
-			if (p.method == 0) {
-				p.sum_buf[pix] = acc;
-				blockmax = acc;
-			} else {
-				p.out[pix] = (uint16_t)acc;
-			}
+		}
+	}
+	unsigned int blockmax = 0;
+	if (live) {
+		if (p.method == 1) {
+			p.out[pix] = sg_round_to_WORD((double)acc / (double)N);
+		} else if (p.method == 0) {
+			p.sum_buf[pix] = acc;
+			blockmax = acc;
+		} else {
+			p.out[pix] = (uint16_t)acc;
 		}
 	}
 	if (p.method == 0) {
@@ -1009,4 +1030,20 @@ k_synth_fill(uint16_t *frames, int nframes, int C, int H, int W, int row_begin, 
 		const int R = row_begin + rr;
 		frames[(int64_t)f * frame_stride + ((int64_t)c * H + R) * W + x] = sg_synth_pixel(seed, f, c, R, x, maxshift);
 	}
+}
+
+/* A/B diagnostics: print and clear the reason counters (SG_HIST_DBG=12) */
+void sg_dbg_why_dump(hipStream_t s) {
+	unsigned int h[32];
+	if (hipMemcpyFromSymbolAsync(h, HIP_SYMBOL(g_sg_why), sizeof h, 0, hipMemcpyDeviceToHost, s) != hipSuccess)
+		return;
+	if (hipStreamSynchronize(s) != hipSuccess)
+		return;
+	fprintf(stderr, "sg why:");
+	for (int k = 0; k < 32; k++)
+		if (h[k])
+			fprintf(stderr, " %d:%u", k, h[k]);
+	fprintf(stderr, "\n");
+	memset(h, 0, sizeof h);
+	(void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_sg_why), h, sizeof h, 0, hipMemcpyHostToDevice, s);
 }
