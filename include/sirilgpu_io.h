@@ -1,0 +1,51 @@
+/*
+ * sirilgpu_io.h - frame sources for libsirilgpu.so: SER files and FITS sequences
+ * (SURVEY.md §8 rows a13, a15, a16).  Plain C ABI.
+ *
+ * sg_seq_read_region has exactly the sg_read_region_fn shape (sirilgpu.h), so an opened
+ * sequence can be handed to sg_stack_u16 as its pull callback (user = the sg_seq*).
+ */
+#ifndef SIRILGPU_IO_H
+#define SIRILGPU_IO_H
+
+#include "sirilgpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct sg_seq sg_seq;
+
+typedef struct {
+	int width, height, nb_layers, nb_frames;
+	int bytes_per_sample;	/* 1 or 2 on disk */
+	int source;		/* 0 = SER, 1 = FITS */
+	int ser_color_id;	/* SER ColorID (src/io/ser.h:17-29), -1 for FITS */
+	int64_t frame_bytes;	/* raw bytes of one frame on disk */
+} sg_seq_info;
+
+/* ser_open_file (src/io/ser.c:555-600) + ser_read_header (:290-350): 0 / SG_ERR_* */
+int sg_seq_open_ser(const char *path, sg_seq **out);
+/* a FITS sequence, one file per frame (seq->type SEQ_REGULAR, src/io/sequence.c):
+ * BITPIX 8 or 16 (BZERO 0 or 32768), NAXIS 2 or 3 */
+int sg_seq_open_fits(const char *const *paths, int nframes, sg_seq **out);
+void sg_seq_close(sg_seq *seq);
+int sg_seq_get_info(const sg_seq *seq, sg_seq_info *info);
+
+/* seq_opened_read_region (src/io/sequence.c:690-700): top-down band `area` of channel
+ * `layer` of frame `index` (ser_read_opened_partial src/io/ser.c:772-971,
+ * read_opened_fits_partial src/io/image_format_fits.c:581-635); 0 ok, -1 failure */
+int sg_seq_read_region(void *seq, int layer, int index, uint16_t *buffer, const sg_rect *area);
+/* seq_read_frame (src/io/sequence.c): whole frame, planar, bottom-up (Siril memory order) */
+int sg_seq_read_frame(const sg_seq *seq, int index, uint16_t *out);
+/* frames [first, first+count) decoded on the device into d_frames[f*frame_stride + ...]
+ * (Siril memory order; frame_stride 0 = nb_layers*height*width): raw bytes go through
+ * pinned staging to HBM and are decoded there (byte order, BZERO, 8-bit widening, RGB/BGR
+ * de-interleaving, SER row flip) */
+int sg_seq_load_device(sg_ctx *ctx, int dev_index, const sg_seq *seq, int first, int count,
+		uint16_t *d_frames, int64_t frame_stride, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SIRILGPU_IO_H */

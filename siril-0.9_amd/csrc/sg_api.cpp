@@ -60,6 +60,8 @@ extern "C" int sg_init(sg_ctx **out, int ndev, const int *devs) {
 		}
 		for (int k = 0; k < 4; k++)
 			(void)hipEventCreate(&d.ev[k]);
+		for (int k = 0; k < 2; k++)
+			(void)hipEventCreateWithFlags(&d.io_ev[k], hipEventDisableTiming);
 		ctx->dev.push_back(d);
 	}
 	*out = ctx;
@@ -74,13 +76,20 @@ extern "C" void sg_shutdown(sg_ctx *ctx) {
 		(void)hipStreamSynchronize(d.stream);
 		SgBuf *bufs[] = {&d.flag_list, &d.flag_map, &d.flag_count, &d.rej, &d.sum_buf, &d.maxim,
 			&d.shifts, &d.norm, &d.tables, &d.scratch, &d.frames, &d.out, &d.reg_sel, &d.reg_spec,
-			&d.reg_work, &d.reg_tw, &d.reg_best, &d.reg_qbuf, &d.reg_qacc, &d.redo, &d.zeros};
+			&d.reg_work, &d.reg_tw, &d.reg_best, &d.reg_qbuf, &d.reg_qacc, &d.redo, &d.zeros,
+			&d.io_raw, &d.io_bad};
 		for (SgBuf *b : bufs)
 			if (b->p)
 				(void)hipFree(b->p);
 		for (int k = 0; k < 2; k++)
 			if (d.pinned[k])
 				(void)hipHostFree(d.pinned[k]);
+		for (int k = 0; k < 2; k++) {
+			if (d.io_stage[k])
+				(void)hipHostFree(d.io_stage[k]);
+			if (d.io_ev[k])
+				(void)hipEventDestroy(d.io_ev[k]);
+		}
 		for (int k = 0; k < 4; k++)
 			if (d.ev[k])
 				(void)hipEventDestroy(d.ev[k]);

@@ -27,6 +27,12 @@ struct SgDevice {
 	SgBuf zeros;	/* zero page for out-of-frame sample loads */
 	uint16_t *pinned[2] = {nullptr, nullptr};
 	size_t pinned_size = 0;
+	/* file decode path (sg_io.hip): pinned staging of raw frames, device raw buffers */
+	void *io_stage[2] = {nullptr, nullptr};
+	size_t io_stage_size = 0;
+	SgBuf io_raw, io_bad;
+	hipEvent_t io_ev[2] = {nullptr, nullptr};
+	int io_ev_used[2] = {0, 0};
 };
 
 struct sg_ctx {

@@ -1,0 +1,443 @@
+/*
+ * sg_io.hip - frame sources of the stacking / registration path: SER files and FITS
+ * sequences (one file per frame), SURVEY.md §8 rows a13, a15, a16.
+ *
+ * Host side (no GPU needed):
+ *   - header parsing: SER (src/io/ser.c:290-336, ser.h:15-76; the endianness flag is used
+ *     with the inverted meaning Siril adopted, ser.h:33-41: 1 = big-endian samples), FITS
+ *     primary HDU with BITPIX 8 / 16 (BZERO 32768 = USHORT_IMG, image_format_fits.c:88,488),
+ *     NAXIS 2 or 3 (planes);
+ *   - sg_seq_read_region: seq_opened_read_region (src/io/sequence.c:690-700) -> a top-down
+ *     band of one layer, i.e. ser_read_opened_partial (src/io/ser.c:772-971, mono / RGB /
+ *     BGR; CFA data is read as mono, as with open_debayer off) and read_opened_fits_partial
+ *     (src/io/image_format_fits.c:581-635: FITS rows are bottom-up, the band is reversed);
+ *   - sg_seq_read_frame: seq_read_frame (ser_read_frame :648-760 + fits_flip_top_to_bottom,
+ *     readfits) -> a whole frame in Siril memory order (planar, bottom-up).
+ * Device side:
+ *   - sg_seq_load_device: raw file bytes of a run of frames -> pinned staging -> HBM ->
+ *     k_decode_frames, which does byte order, BZERO, 8-bit widening, RGB/BGR
+ *     de-interleaving and the SER top-down -> bottom-up flip in one pass (one thread per
+ *     output sample, coalesced writes), writing frames at a caller-chosen stride so they
+ *     land directly in the stacking layout.
+ */
+#include "sg_common.hpp"
+#include "sg_ctx.hpp"
+#include <errno.h>
+#include <fcntl.h>
+#include <string.h>
+#include <unistd.h>
+#include <stdlib.h>
+#include <string>
+#include <vector>
+
+enum { SG_SRC_SER = 1, SG_SRC_FITS = 2 };
+enum { SG_ENC_U16LE = 0, SG_ENC_U16BE = 1, SG_ENC_U8 = 2, SG_ENC_FITS16_BZ = 3, SG_ENC_FITS16 = 4 };
+
+struct sg_seq {
+	int kind;		/* SG_SRC_* */
+	int width, height, layers, frames;
+	int bytes_per_sample;	/* 1 or 2 */
+	int enc;		/* SG_ENC_* */
+	int interleaved;	/* SER RGB / BGR */
+	int bgr;
+	int color_id, bitpix, bzero;
+	std::vector<int> fd;	/* SER: one; FITS: one per frame */
+	std::vector<int64_t> data_off;	/* byte offset of the pixel data (per file) */
+	int64_t frame_bytes;	/* raw bytes of one frame */
+};
+
+#include "../../include/sirilgpu_io.h"
+
+static int rd_exact(int fd, void *buf, size_t n, int64_t off) {
+	char *p = (char *)buf;
+	while (n) {
+		ssize_t r = pread(fd, p, n, (off_t)off);
+		if (r < 0 && errno == EINTR)
+			continue;
+		if (r <= 0)
+			return -1;
+		p += r;
+		n -= (size_t)r;
+		off += r;
+	}
+	return 0;
+}
+
+static inline uint32_t le32(const unsigned char *p) {
+	return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+extern "C" int sg_seq_open_ser(const char *path, sg_seq **out) {
+	if (!path || !out)
+		return SG_ERR_GENERIC;
+	*out = nullptr;
+	int fd = open(path, O_RDONLY);
+	if (fd < 0)
+		return SG_ERR_READ;
+	unsigned char h[178];	/* SER_HEADER_LEN, ser.h:15 */
+	if (rd_exact(fd, h, sizeof h, 0)) {
+		close(fd);
+		return SG_ERR_READ;
+	}
+	sg_seq *s = new sg_seq();
+	s->kind = SG_SRC_SER;
+	/* the 7 little-endian ints at byte 14 (ser.c:312) */
+	s->color_id = (int)le32(h + 18);
+	const int big = (int)le32(h + 22) == 1;	/* SER_BIG_ENDIAN = 1 (ser.h:41) */
+	s->width = (int)le32(h + 26);
+	s->height = (int)le32(h + 30);
+	const int depth = (int)le32(h + 34);
+	s->frames = (int)le32(h + 38);
+	s->bytes_per_sample = depth <= 8 ? 1 : 2;	/* ser.c:327-330 */
+	s->interleaved = (s->color_id == 100 || s->color_id == 101);	/* SER_RGB / SER_BGR */
+	s->bgr = s->color_id == 101;
+	s->layers = s->interleaved ? 3 : 1;	/* ser.c:332-335; CFA opened as mono */
+	s->enc = s->bytes_per_sample == 1 ? SG_ENC_U8 : (big ? SG_ENC_U16BE : SG_ENC_U16LE);
+	s->frame_bytes = (int64_t)s->width * s->height * s->layers * s->bytes_per_sample;
+	s->fd.push_back(fd);
+	s->data_off.push_back(178);
+	if (s->width <= 0 || s->height <= 0 || s->frames <= 0) {
+		sg_seq_close(s);
+		return SG_ERR_SIZE;
+	}
+	/* frame_count == 0 repair of ser.c:341-347 is not done (the file is read-only here) */
+	const off_t size = lseek(fd, 0, SEEK_END);
+	if (size < 178 + s->frame_bytes * (int64_t)s->frames) {
+		sg_seq_close(s);
+		return SG_ERR_READ;
+	}
+	*out = s;
+	return SG_OK;
+}
+
+/* FITS primary header: 80-byte cards in 2880-byte blocks */
+static int fits_header(int fd, int *bitpix, int *naxis, long naxes[3], double *bzero, double *bscale,
+		int64_t *data_off) {
+	char card[81];
+	card[80] = 0;
+	*bitpix = 0;
+	*naxis = 0;
+	naxes[0] = naxes[1] = naxes[2] = 1;
+	*bzero = 0.0;
+	*bscale = 1.0;
+	for (int64_t off = 0;; off += 80) {
+		if (rd_exact(fd, card, 80, off))
+			return -1;
+		if (!strncmp(card, "END", 3) && (card[3] == ' ' || card[3] == 0)) {
+			*data_off = ((off + 80 + 2879) / 2880) * 2880;
+			return 0;
+		}
+		if (card[8] != '=')
+			continue;
+		char key[9];
+		memcpy(key, card, 8);
+		key[8] = 0;
+		for (int i = 7; i >= 0 && key[i] == ' '; i--)
+			key[i] = 0;
+		const char *val = card + 10;
+		if (!strcmp(key, "BITPIX"))
+			*bitpix = atoi(val);
+		else if (!strcmp(key, "NAXIS"))
+			*naxis = atoi(val);
+		else if (!strcmp(key, "NAXIS1"))
+			naxes[0] = atol(val);
+		else if (!strcmp(key, "NAXIS2"))
+			naxes[1] = atol(val);
+		else if (!strcmp(key, "NAXIS3"))
+			naxes[2] = atol(val);
+		else if (!strcmp(key, "BZERO"))
+			*bzero = atof(val);
+		else if (!strcmp(key, "BSCALE"))
+			*bscale = atof(val);
+		if (off > (int64_t)2880 * 1000)
+			return -1;
+	}
+}
+
+extern "C" int sg_seq_open_fits(const char *const *paths, int nframes, sg_seq **out) {
+	if (!paths || nframes <= 0 || !out)
+		return SG_ERR_GENERIC;
+	*out = nullptr;
+	sg_seq *s = new sg_seq();
+	s->kind = SG_SRC_FITS;
+	for (int i = 0; i < nframes; i++) {
+		int fd = open(paths[i], O_RDONLY);
+		if (fd < 0) {
+			sg_seq_close(s);
+			return SG_ERR_READ;
+		}
+		s->fd.push_back(fd);
+		int bitpix, naxis;
+		long naxes[3];
+		double bzero, bscale;
+		int64_t doff;
+		if (fits_header(fd, &bitpix, &naxis, naxes, &bzero, &bscale, &doff)) {
+			sg_seq_close(s);
+			return SG_ERR_READ;
+		}
+		if ((bitpix != 8 && bitpix != 16) || (naxis != 2 && naxis != 3) || bscale != 1.0 ||
+				(bitpix == 16 && bzero != 0.0 && bzero != 32768.0) || (bitpix == 8 && bzero != 0.0) ||
+				(naxis == 3 && naxes[2] != 3 && naxes[2] != 1)) {
+			sg_seq_close(s);
+			return SG_ERR_GENERIC;	/* unsupported image type for this path */
+		}
+		const int layers = naxis == 3 ? (int)naxes[2] : 1;
+		if (i == 0) {
+			s->width = (int)naxes[0];
+			s->height = (int)naxes[1];
+			s->layers = layers;
+			s->bitpix = bitpix;
+			s->bzero = (int)bzero;
+		} else if (naxes[0] != s->width || naxes[1] != s->height || layers != s->layers ||
+				bitpix != s->bitpix || (int)bzero != s->bzero) {
+			sg_seq_close(s);
+			return SG_ERR_SIZE;	/* sequences hold images of one size and type */
+		}
+		s->data_off.push_back(doff);
+	}
+	s->frames = nframes;
+	s->bytes_per_sample = s->bitpix == 8 ? 1 : 2;
+	s->enc = s->bitpix == 8 ? SG_ENC_U8 : (s->bzero == 32768 ? SG_ENC_FITS16_BZ : SG_ENC_FITS16);
+	s->frame_bytes = (int64_t)s->width * s->height * s->layers * s->bytes_per_sample;
+	*out = s;
+	return SG_OK;
+}
+
+extern "C" void sg_seq_close(sg_seq *s) {
+	if (!s)
+		return;
+	for (int fd : s->fd)
+		if (fd >= 0)
+			close(fd);
+	delete s;
+}
+
+extern "C" int sg_seq_get_info(const sg_seq *s, sg_seq_info *info) {
+	if (!s || !info)
+		return SG_ERR_GENERIC;
+	info->width = s->width;
+	info->height = s->height;
+	info->nb_layers = s->layers;
+	info->nb_frames = s->frames;
+	info->bytes_per_sample = s->bytes_per_sample;
+	info->source = s->kind == SG_SRC_SER ? 0 : 1;
+	info->ser_color_id = s->kind == SG_SRC_SER ? s->color_id : -1;
+	info->frame_bytes = s->frame_bytes;
+	return SG_OK;
+}
+
+/* one raw sample -> WORD (ser_manage_endianess_and_depth ser.c:476-491; FITS TUSHORT) */
+static inline uint16_t conv_host(const unsigned char *p, int enc, int *bad) {
+	switch (enc) {
+	case SG_ENC_U8:
+		return p[0];
+	case SG_ENC_U16LE:
+		return (uint16_t)(p[0] | (p[1] << 8));
+	case SG_ENC_U16BE:
+		return (uint16_t)((p[0] << 8) | p[1]);
+	case SG_ENC_FITS16_BZ:
+		return (uint16_t)(((p[0] << 8) | p[1]) ^ 0x8000);
+	default: {	/* signed 16-bit, BZERO 0: negative values cannot be a WORD */
+		const uint16_t v = (uint16_t)((p[0] << 8) | p[1]);
+		if (v & 0x8000)
+			*bad = 1;
+		return v;
+	}
+	}
+}
+
+extern "C" int sg_seq_read_region(void *user, int layer, int index, uint16_t *buffer, const sg_rect *area) {
+	const sg_seq *s = (const sg_seq *)user;
+	if (!s || !buffer || !area || index < 0 || index >= s->frames || layer < 0 || layer >= s->layers)
+		return -1;
+	if (area->x < 0 || area->y < 0 || area->w <= 0 || area->h <= 0 || area->x + area->w > s->width ||
+			area->y + area->h > s->height)
+		return -1;
+	const int bps = s->bytes_per_sample;
+	const int fd = s->kind == SG_SRC_SER ? s->fd[0] : s->fd[index];
+	const int64_t base = s->kind == SG_SRC_SER ? s->data_off[0] + s->frame_bytes * (int64_t)index : s->data_off[index];
+	int bad = 0;
+	if (s->kind == SG_SRC_SER) {
+		/* SER rows are top-down: band rows y .. y+h-1 from the top */
+		const int ns = s->interleaved ? 3 : 1;
+		const int coff = s->bgr ? 2 - layer : layer;
+		std::vector<unsigned char> raw((size_t)area->w * ns * bps);
+		for (int r = 0; r < area->h; r++) {
+			const int64_t off = base + ((int64_t)(area->y + r) * s->width + area->x) * ns * bps;
+			if (rd_exact(fd, raw.data(), raw.size(), off))
+				return -1;
+			for (int x = 0; x < area->w; x++)
+				buffer[(size_t)r * area->w + x] = conv_host(&raw[((size_t)x * ns + coff) * bps], s->enc, &bad);
+		}
+	} else {
+		/* FITS rows are bottom-up (file row 1 = bottom): the band's top row is file row
+		 * ry - y (1-based), the band is returned top-down (image_format_fits.c:597-632) */
+		const int64_t plane = (int64_t)s->width * s->height * bps;
+		std::vector<unsigned char> raw((size_t)area->w * bps);
+		for (int r = 0; r < area->h; r++) {
+			const int frow = s->height - area->y - 1 - r;	/* 0-based file row */
+			const int64_t off = base + plane * layer + ((int64_t)frow * s->width + area->x) * bps;
+			if (rd_exact(fd, raw.data(), raw.size(), off))
+				return -1;
+			for (int x = 0; x < area->w; x++)
+				buffer[(size_t)r * area->w + x] = conv_host(&raw[(size_t)x * bps], s->enc, &bad);
+		}
+	}
+	return bad ? -1 : 0;
+}
+
+extern "C" int sg_seq_read_frame(const sg_seq *s, int index, uint16_t *out) {
+	if (!s || !out || index < 0 || index >= s->frames)
+		return SG_ERR_GENERIC;
+	const int fd = s->kind == SG_SRC_SER ? s->fd[0] : s->fd[index];
+	const int64_t base = s->kind == SG_SRC_SER ? s->data_off[0] + s->frame_bytes * (int64_t)index : s->data_off[index];
+	std::vector<unsigned char> raw((size_t)s->frame_bytes);
+	if (rd_exact(fd, raw.data(), raw.size(), base))
+		return SG_ERR_READ;
+	const int W = s->width, H = s->height, C = s->layers, bps = s->bytes_per_sample;
+	int bad = 0;
+	for (int c = 0; c < C; c++)
+		for (int r = 0; r < H; r++)
+			for (int x = 0; x < W; x++) {
+				size_t src;
+				if (s->kind == SG_SRC_SER) {
+					/* top-down file -> bottom-up memory (fits_flip_top_to_bottom), RGB/BGR
+					 * de-interleaved (ser.c:735-749) */
+					const int coff = s->interleaved ? (s->bgr ? 2 - c : c) : 0;
+					src = (((size_t)(H - 1 - r) * W + x) * (s->interleaved ? 3 : 1) + coff) * bps;
+				} else {
+					src = (((size_t)c * H + r) * W + x) * bps;	/* file order = memory order */
+				}
+				out[((size_t)c * H + r) * W + x] = conv_host(&raw[src], s->enc, &bad);
+			}
+	return bad ? SG_ERR_GENERIC : SG_OK;
+}
+
+/* ------------------------------------------------------------------------------------
+ * device decode
+ * ------------------------------------------------------------------------------------ */
+struct SgDecode {
+	const unsigned char *raw;	/* nframes raw frames, back to back */
+	int64_t raw_frame_bytes;
+	uint16_t *out;
+	int64_t out_frame_stride;	/* elements */
+	int W, H, C, enc, interleaved, bgr, ser, nframes;
+	unsigned int *bad;
+};
+
+__device__ __forceinline__ uint16_t sg_conv(const unsigned char *p, int enc, bool &bad) {
+	if (enc == SG_ENC_U8)
+		return p[0];
+	const uint16_t lo = p[0], hi = p[1];
+	switch (enc) {
+	case SG_ENC_U16LE:
+		return (uint16_t)(lo | (hi << 8));
+	case SG_ENC_U16BE:
+		return (uint16_t)((lo << 8) | hi);
+	case SG_ENC_FITS16_BZ:
+		return (uint16_t)(((lo << 8) | hi) ^ 0x8000);
+	default: {
+		const uint16_t v = (uint16_t)((lo << 8) | hi);
+		bad |= (v & 0x8000) != 0;
+		return v;
+	}
+	}
+}
+
+/* one thread per output sample of frame blockIdx.y; rows flipped for SER */
+__global__ void __launch_bounds__(256) k_decode_frames(SgDecode d) {
+	const int64_t plane = (int64_t)d.W * d.H;
+	const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+	const int f = blockIdx.y;
+	if (i >= plane * d.C)
+		return;
+	const int c = (int)(i / plane);
+	const int64_t rest = i - (int64_t)c * plane;
+	const int r = (int)(rest / d.W), x = (int)(rest - (int64_t)r * d.W);
+	const int bps = d.enc == SG_ENC_U8 ? 1 : 2;
+	int64_t src;
+	if (d.ser) {
+		const int coff = d.interleaved ? (d.bgr ? 2 - c : c) : 0;
+		src = (((int64_t)(d.H - 1 - r) * d.W + x) * (d.interleaved ? 3 : 1) + coff) * bps;
+	} else {
+		src = i * bps;
+	}
+	bool bad = false;
+	const uint16_t v = sg_conv(d.raw + (int64_t)f * d.raw_frame_bytes + src, d.enc, bad);
+	d.out[(int64_t)f * d.out_frame_stride + i] = v;
+	if (bad)
+		atomicOr(d.bad, 1u);
+}
+
+extern "C" int sg_seq_load_device(sg_ctx *ctx, int dev_index, const sg_seq *s, int first, int count,
+		uint16_t *d_frames, int64_t frame_stride, void *stream) {
+	if (!ctx || !s || !d_frames || dev_index < 0 || dev_index >= (int)ctx->dev.size() || first < 0 || count <= 0 ||
+			first + count > s->frames)
+		return SG_ERR_GENERIC;
+	SgDevice &dv = ctx->dev[dev_index];
+	HIPCHK(hipSetDevice(dv.id));
+	hipStream_t st = stream ? (hipStream_t)stream : dv.stream;
+	const int64_t plane_elems = (int64_t)s->width * s->height * s->layers;
+	if (frame_stride == 0)
+		frame_stride = plane_elems;
+	/* double-buffered pinned staging of up to 64 MiB (at least one frame) */
+	const int64_t fb = s->frame_bytes;
+	int per = (int)((64ll << 20) / fb);
+	if (per < 1)
+		per = 1;
+	const size_t stage = (size_t)per * (size_t)fb;
+	if (dv.io_stage_size < stage) {
+		for (int k = 0; k < 2; k++) {
+			if (dv.io_stage[k])
+				(void)hipHostFree(dv.io_stage[k]);
+			dv.io_stage[k] = nullptr;
+			HIPCHK(hipHostMalloc((void **)&dv.io_stage[k], stage));
+		}
+		dv.io_stage_size = stage;
+	}
+	HIPCHK(ensure(dv.io_raw, 2 * stage));
+	HIPCHK(ensure(dv.io_bad, 16));
+	HIPCHK(hipMemsetAsync(dv.io_bad.p, 0, 4, st));
+	int k = 0;
+	for (int f0 = first; f0 < first + count; f0 += per, k ^= 1) {
+		const int n = (first + count - f0) < per ? (first + count - f0) : per;
+		/* the buffer about to be refilled was last used two batches ago: wait for its copy */
+		if (dv.io_ev_used[k])
+			HIPCHK(hipEventSynchronize(dv.io_ev[k]));
+		unsigned char *hs = (unsigned char *)dv.io_stage[k];
+		for (int j = 0; j < n; j++) {
+			const int idx = f0 + j;
+			const int fd = s->kind == SG_SRC_SER ? s->fd[0] : s->fd[idx];
+			const int64_t off = s->kind == SG_SRC_SER ? s->data_off[0] + fb * (int64_t)idx : s->data_off[idx];
+			if (rd_exact(fd, hs + (size_t)j * fb, (size_t)fb, off))
+				return set_err(ctx, SG_ERR_READ, "read failure in frame %s%ld", "", idx);
+		}
+		unsigned char *draw = (unsigned char *)dv.io_raw.p + (size_t)k * stage;
+		HIPCHK(hipMemcpyAsync(draw, hs, (size_t)n * fb, hipMemcpyHostToDevice, st));
+		HIPCHK(hipEventRecord(dv.io_ev[k], st));
+		dv.io_ev_used[k] = 1;
+		SgDecode d;
+		d.raw = draw;
+		d.raw_frame_bytes = fb;
+		d.out = d_frames + (int64_t)(f0 - first) * frame_stride;
+		d.out_frame_stride = frame_stride;
+		d.W = s->width;
+		d.H = s->height;
+		d.C = s->layers;
+		d.enc = s->enc;
+		d.interleaved = s->interleaved;
+		d.bgr = s->bgr;
+		d.ser = s->kind == SG_SRC_SER;
+		d.nframes = n;
+		d.bad = (unsigned int *)dv.io_bad.p;
+		hipLaunchKernelGGL(k_decode_frames, dim3((unsigned)((plane_elems + 255) / 256), (unsigned)n), dim3(256), 0, st, d);
+		HIPCHK(hipGetLastError());
+	}
+	unsigned int bad = 0;
+	HIPCHK(hipMemcpyAsync(&bad, dv.io_bad.p, 4, hipMemcpyDeviceToHost, st));
+	HIPCHK(hipStreamSynchronize(st));
+	dv.io_ev_used[0] = dv.io_ev_used[1] = 0;
+	if (bad)
+		return set_err(ctx, SG_ERR_GENERIC, "negative samples in a signed 16-bit FITS%s (%ld)", "", 0);
+	return SG_OK;
+}

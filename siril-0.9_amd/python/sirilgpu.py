@@ -64,10 +64,18 @@ READ_REGION_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, c
                                   ctypes.POINTER(ctypes.c_uint16), ctypes.POINTER(Rect))
 CONT_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
 
-# every symbol include/sirilgpu.h declares
+class SeqInfo(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int), ("height", ctypes.c_int), ("nb_layers", ctypes.c_int),
+                ("nb_frames", ctypes.c_int), ("bytes_per_sample", ctypes.c_int), ("source", ctypes.c_int),
+                ("ser_color_id", ctypes.c_int), ("frame_bytes", ctypes.c_int64)]
+
+
+# every symbol include/sirilgpu.h and include/sirilgpu_io.h declare
 EXPORTS = ["sg_init", "sg_shutdown", "sg_last_error", "sg_stack_u16", "sg_stack_u16_device",
            "sg_get_last_stats", "sg_register_dft_u16", "sg_register_dft_u16_device",
-           "sg_synth_fill_device"]
+           "sg_synth_fill_device",
+           "sg_seq_open_ser", "sg_seq_open_fits", "sg_seq_close", "sg_seq_get_info", "sg_seq_read_region",
+           "sg_seq_read_frame", "sg_seq_load_device"]
 
 _lib = None
 
@@ -106,8 +114,81 @@ def load():
     lib.sg_register_dft_u16_device.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                P, P, P, P, P]
     lib.sg_register_dft_u16_device.restype = ctypes.c_int
+    lib.sg_seq_open_ser.argtypes = [ctypes.c_char_p, ctypes.POINTER(P)]
+    lib.sg_seq_open_ser.restype = ctypes.c_int
+    lib.sg_seq_open_fits.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.POINTER(P)]
+    lib.sg_seq_open_fits.restype = ctypes.c_int
+    lib.sg_seq_close.argtypes = [P]
+    lib.sg_seq_close.restype = None
+    lib.sg_seq_get_info.argtypes = [P, ctypes.POINTER(SeqInfo)]
+    lib.sg_seq_get_info.restype = ctypes.c_int
+    lib.sg_seq_read_region.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint16),
+                                       ctypes.POINTER(Rect)]
+    lib.sg_seq_read_region.restype = ctypes.c_int
+    lib.sg_seq_read_frame.argtypes = [P, ctypes.c_int, ctypes.POINTER(ctypes.c_uint16)]
+    lib.sg_seq_read_frame.restype = ctypes.c_int
+    lib.sg_seq_load_device.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int64, P]
+    lib.sg_seq_load_device.restype = ctypes.c_int
     _lib = lib
     return lib
+
+
+class Seq:
+    """An opened SER file or FITS sequence (include/sirilgpu_io.h); host-side reads need no GPU."""
+
+    def __init__(self, handle):
+        self.lib = load()
+        self.h = handle
+        info = SeqInfo()
+        rc = self.lib.sg_seq_get_info(self.h, ctypes.byref(info))
+        if rc != SG_OK:
+            raise RuntimeError(f"sg_seq_get_info failed ({rc})")
+        self.info = info
+        self.shape = (info.nb_frames, info.nb_layers, info.height, info.width)
+
+    @classmethod
+    def open_ser(cls, path):
+        lib = load()
+        h = ctypes.c_void_p()
+        rc = lib.sg_seq_open_ser(os.fsencode(path), ctypes.byref(h))
+        if rc != SG_OK:
+            raise OSError(f"sg_seq_open_ser({path}) failed ({rc})")
+        return cls(h)
+
+    @classmethod
+    def open_fits(cls, paths):
+        lib = load()
+        arr = (ctypes.c_char_p * len(paths))(*[os.fsencode(p) for p in paths])
+        h = ctypes.c_void_p()
+        rc = lib.sg_seq_open_fits(arr, len(paths), ctypes.byref(h))
+        if rc != SG_OK:
+            raise OSError(f"sg_seq_open_fits failed ({rc})")
+        return cls(h)
+
+    def close(self):
+        if self.h:
+            self.lib.sg_seq_close(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def read_region(self, layer, index, x, y, w, h):
+        """top-down band (seq_opened_read_region); returns (rc, array[h][w])"""
+        buf = np.zeros((h, w), dtype=np.uint16)
+        rc = self.lib.sg_seq_read_region(self.h, layer, index, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)),
+                                         ctypes.byref(Rect(x, y, w, h)))
+        return rc, buf
+
+    def read_frame(self, index):
+        out = np.zeros(self.shape[1:], dtype=np.uint16)
+        rc = self.lib.sg_seq_read_frame(self.h, index, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)))
+        if rc != SG_OK:
+            raise RuntimeError(f"sg_seq_read_frame({index}) failed ({rc})")
+        return out
 
 
 def _iptr(a):
@@ -189,6 +270,28 @@ class Context:
                                           ctypes.c_void_p(stream) if stream else None)
         self.check(rc, "sg_stack_u16_device")
         return np.array(list(rej), dtype=np.uint64).reshape(3, 2), int(maxim.value)
+
+    def load_seq_device(self, seq, d_frames, first=0, count=None, frame_stride=0, dev_index=0, stream=None):
+        """frames of an opened Seq decoded on the device (sg_seq_load_device)"""
+        if count is None:
+            count = seq.shape[0] - first
+        rc = self.lib.sg_seq_load_device(self.ctx, dev_index, seq.h, first, count, ctypes.c_void_p(d_frames),
+                                         frame_stride, ctypes.c_void_p(stream) if stream else None)
+        self.check(rc, "sg_seq_load_device")
+
+    def stack_seq(self, desc, seq):
+        """Host-pull stack whose pull callback is the library's own sg_seq_read_region (C),
+        i.e. stack_mean_with_rejection & co. reading the sequence's files directly."""
+        N, C, H, W = seq.shape
+        rf = ctypes.cast(self.lib.sg_seq_read_region, READ_REGION_FN)
+        cf = CONT_FN(lambda user: 1)
+        out = np.zeros((C, H, W), dtype=np.uint16)
+        rej = (ctypes.c_uint64 * 6)()
+        maxim = ctypes.c_uint64(0)
+        rc = self.lib.sg_stack_u16(self.ctx, ctypes.byref(desc), rf, seq.h, cf, None,
+                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)), rej,
+                                   ctypes.byref(maxim))
+        return rc, out, np.array(list(rej), dtype=np.uint64).reshape(3, 2), int(maxim.value)
 
     def stack_host(self, desc, frames, cancel_after=None):
         """Host-pull path: frames[N][C][H][W] (memory order) served through a

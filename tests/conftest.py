@@ -15,6 +15,11 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def gpu_ctx():
+    # torch (device buffers for the device-resident tests) brings its own HIP runtime; it
+    # must initialise the GPU before libsirilgpu's runtime does, as bench.py does
+    import torch
+    torch.cuda.init()
+    torch.zeros(1, device="cuda")
     import sirilgpu
     ctx = sirilgpu.Context()
     yield ctx
