@@ -136,6 +136,22 @@ int sg_register_dft_u16_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel
 		int S, int ref_image, const int *included, int *shiftx, int *shifty,
 		double *quality, void *stream);
 
+/*
+ * Perspective warp: replaces cvTransformImage (src/opencv/opencv.cpp:242-309) as the
+ * star-alignment registration uses it (src/registration/registration.c:719-723, flip /
+ * warp / flip): memory-order (bottom-up) planes in, memory-order planes out of size
+ * out_width x out_height (ref.x, ref.y); hom = Homography h00..h22 row-major (the
+ * forward map, inverted as warpPerspective does without WARP_INVERSE_MAP);
+ * interpolation = opencv_interpolation (src/core/siril.h:257-264: 0 nearest, 1 linear,
+ * 2 area (= linear), 3 cubic, 4 lanczos4), border constant 0.  OpenCV's algorithm is
+ * restated (sg_warp.hip); OpenCV is unpinned, so parity is unpinned.
+ */
+int sg_warp_u16(sg_ctx *ctx, const uint16_t *in, int width, int height, int nb_layers,
+		uint16_t *out, int out_width, int out_height, const double *hom, int interpolation);
+int sg_warp_u16_device(sg_ctx *ctx, int dev_index, const uint16_t *d_in, int width, int height,
+		int nb_layers, uint16_t *d_out, int out_width, int out_height, const double *hom,
+		int interpolation, void *stream);
+
 /* Synthetic sequence generator of include/sg_synth.h on the device (bench / tests):
  * frame f, channel c, row r at d_frames[f*frame_stride + (c*height + r)*width]
  * (frame_stride 0 = nb_layers*height*width). */

@@ -31,6 +31,8 @@ struct SgDevice {
 	void *io_stage[2] = {nullptr, nullptr};
 	size_t io_stage_size = 0;
 	SgBuf io_raw, io_bad;
+	SgBuf warp_tab;		/* sg_warp.hip interpolation table */
+	int warp_tab_interp = -1;
 	hipEvent_t io_ev[2] = {nullptr, nullptr};
 	int io_ev_used[2] = {0, 0};
 };

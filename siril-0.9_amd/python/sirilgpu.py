@@ -75,7 +75,9 @@ EXPORTS = ["sg_init", "sg_shutdown", "sg_last_error", "sg_stack_u16", "sg_stack_
            "sg_get_last_stats", "sg_register_dft_u16", "sg_register_dft_u16_device",
            "sg_synth_fill_device",
            "sg_seq_open_ser", "sg_seq_open_fits", "sg_seq_close", "sg_seq_get_info", "sg_seq_read_region",
-           "sg_seq_read_frame", "sg_seq_load_device"]
+           "sg_seq_read_frame", "sg_seq_load_device", "sg_warp_u16", "sg_warp_u16_device"]
+# opencv_interpolation (src/core/siril.h:257-264)
+OPENCV_NEAREST, OPENCV_LINEAR, OPENCV_AREA, OPENCV_CUBIC, OPENCV_LANCZOS4 = range(5)
 
 _lib = None
 
@@ -129,6 +131,12 @@ def load():
     lib.sg_seq_read_frame.restype = ctypes.c_int
     lib.sg_seq_load_device.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int64, P]
     lib.sg_seq_load_device.restype = ctypes.c_int
+    lib.sg_warp_u16.argtypes = [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.c_int,
+                                ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+    lib.sg_warp_u16.restype = ctypes.c_int
+    lib.sg_warp_u16_device.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, ctypes.c_int,
+                                       ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_int, P]
+    lib.sg_warp_u16_device.restype = ctypes.c_int
     _lib = lib
     return lib
 
@@ -278,6 +286,19 @@ class Context:
         rc = self.lib.sg_seq_load_device(self.ctx, dev_index, seq.h, first, count, ctypes.c_void_p(d_frames),
                                          frame_stride, ctypes.c_void_p(stream) if stream else None)
         self.check(rc, "sg_seq_load_device")
+
+    def warp(self, image, hom, out_size=None, interpolation=OPENCV_LINEAR):
+        """cvTransformImage on a memory-order image [C][H][W]; hom = the 3x3 homography
+        (Homography h00..h22), out_size = (ref.x, ref.y)"""
+        image = np.ascontiguousarray(image, dtype=np.uint16)
+        C, H, W = image.shape
+        oW, oH = out_size if out_size else (W, H)
+        out = np.zeros((C, oH, oW), dtype=np.uint16)
+        h = (ctypes.c_double * 9)(*[float(v) for v in np.asarray(hom, dtype=np.float64).reshape(9)])
+        rc = self.lib.sg_warp_u16(self.ctx, image.ctypes.data_as(ctypes.c_void_p), W, H, C,
+                                  out.ctypes.data_as(ctypes.c_void_p), oW, oH, h, interpolation)
+        self.check(rc, "sg_warp_u16")
+        return out
 
     def stack_seq(self, desc, seq):
         """Host-pull stack whose pull callback is the library's own sg_seq_read_region (C),
