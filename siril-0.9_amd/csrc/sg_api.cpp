@@ -28,6 +28,7 @@ template <int NREG, bool LISTED>
 __global__ void k_stack_sorted(SgStackParams p, const unsigned int *list, const unsigned int *list_count);
 __global__ void k_stack_hist(SgStackParams p, unsigned int *redo_count, unsigned int *redo_list);
 void sg_dbg_why_dump(hipStream_t s);
+__global__ void k_stack_replay(SgStackParams p);
 __global__ void k_stack_reduce(SgStackParams p);
 __global__ void k_sum_finalize(SgStackParams p);
 __global__ void k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *scratch, int phase);
@@ -398,7 +399,14 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 			ctx->stats.main_kernel_blocks = (int)nblk;
 			ctx->stats.launches = 1;
 		}
-		/* literal path for queued pixels: two phases, grid reads the count on device */
+		/* exact wave-per-pixel replay of queued SIGMA / WINSORIZED pixels (early breaks with
+		 * this pixel's own stale rejected[]), then the literal path for what remains: two
+		 * phases, grids read the count on the device */
+		if ((p.rejection == SG_SIGMA || p.rejection == SG_WINSORIZED) && N <= 2048) {
+			hipLaunchKernelGGL(k_stack_replay, dim3(1024), dim3(256), 0, s, p);
+			HIPCHK(hipGetLastError());
+			ctx->stats.launches++;
+		}
 		HIPCHK(ensure(dv.scratch, (size_t)SG_LIT_THREADS * (((size_t)N * 5 + 15) & ~(size_t)15)));
 		for (int phase = 1; phase <= 2; phase++) {
 			hipLaunchKernelGGL(k_stack_literal, dim3(SG_LIT_THREADS / 64), dim3(64), 0, s, p, ct,

@@ -10,7 +10,7 @@
 #define SG_SORT_THREADS 256
 #define SG_REJ_SHARDS 1024
 
-enum { SG_CLS_OK = 0, SG_CLS_LITERAL = 1, SG_CLS_CHAIN = 2 };
+enum { SG_CLS_OK = 0, SG_CLS_LITERAL = 1, SG_CLS_CHAIN = 2, SG_CLS_DONE = 3 };
 
 /* everything the stacking kernels need, passed by value */
 struct SgStackParams {

@@ -139,9 +139,11 @@ __device__ __forceinline__ double exact_sd(int n, uint64_t S, uint64_t SS, bool 
 	return sqrt((double)num / ((double)n * (double)(n - 1)));
 }
 
-/* relative rounding band around every continuous threshold: GSL's long double sd
- * differs from the exact one by ~(n+8)*2^-64 relative, the double ops add a few ulp */
-#define SG_BAND 1e-11
+/* relative rounding band around every continuous threshold (relative to the median's
+ * magnitude): GSL's long double mean recurrence is off by <= n 2^-64 |mean| ~ 3e-17 |mean|
+ * for n = 512, which moves sd by about the same absolute amount; the double operations
+ * after it add a few ulp (~1e-16).  1e-13 leaves a margin of ~1000 */
+#define SG_BAND 1e-13
 
 /* A/B diagnostics (SG_HIST_DBG=12): why pixels leave the sorted path */
 __device__ unsigned int g_sg_why[32];
@@ -941,6 +943,296 @@ __device__ __forceinline__ void gather_stack(const SgStackParams &p, int64_t pix
 		stack[f] = sg_gather(p, f, c, R, x);
 }
 
+/* ----------------------------------------------------------------------------------
+ * exact wave-per-pixel replay (SIGMA / WINSORIZED queued pixels)
+ * ---------------------------------------------------------------------------------- */
+/*
+ * k_stack_replay: one wave per queued pixel replays the reference loop (:1674-1749)
+ * literally in structure - the stack array in frame order, quicksort, the rejected[]
+ * array by POSITION, the `if (N - r <= 4) break;` with the entries after the break keeping
+ * this pixel's previous-pass values, the order-preserving removal - but with exact
+ * integer moments instead of GSL's long double sums.  Every continuous decision gets the
+ * same rounding band as the sorted path; a pixel that meets an ambiguous decision, or whose
+ * FIRST pass breaks early (its stale entries belong to the previous pixel of the OpenMP
+ * thread), stays queued for k_stack_literal.  This takes the early-break pixels (e.g.
+ * image-edge columns half filled by the shift zero fill under WINSORIZED) off the
+ * one-thread fp80 path.  The stack is sorted once: after the first pass the removal keeps
+ * it sorted, and quicksort_s of a sorted array is the identity; the Winsorized copy stays
+ * sorted under clamping.
+ */
+#define SG_REPLAY_MAXN 2048
+#define SG_REPLAY_WAVES 4
+
+struct SgReplayLds {
+	uint16_t stack[SG_REPLAY_MAXN];
+	uint16_t w[SG_REPLAY_MAXN];
+	int8_t rej[SG_REPLAY_MAXN];
+};
+
+__device__ __forceinline__ int wave_excl_scan(int v, int lane) {
+	int x = v;
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		const int t = __shfl_up(x, o, 64);
+		if (lane >= o)
+			x += t;
+	}
+	return x - v;
+}
+
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1)
+		v += __shfl_xor(v, o, 64);
+	return v;
+}
+
+__device__ __forceinline__ int wave_or(int v) {
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1)
+		v |= __shfl_xor(v, o, 64);
+	return v;
+}
+
+__device__ __forceinline__ void replay_moments(const uint16_t *a, int n, int lane, uint64_t &S, uint64_t &SS) {
+	uint64_t s = 0, ss = 0;
+	for (int j = lane; j < n; j += 64) {
+		const uint64_t v = a[j];
+		s += v;
+		ss += v * v;
+	}
+	S = wave_sum_u64(s);
+	SS = wave_sum_u64(ss);
+}
+
+/* ascending bitonic sort of a[0..n) (padded with 65535 up to a power of two; the pad lies
+ * inside the array's capacity and is never read as data) */
+__device__ void replay_sort(uint16_t *a, int n, int lane) {
+	int P = 1;
+	while (P < n)
+		P <<= 1;
+	for (int j = n + lane; j < P; j += 64)
+		a[j] = 0xFFFF;
+	__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+	for (int k = 2; k <= P; k <<= 1)
+		for (int j = k >> 1; j > 0; j >>= 1) {
+			for (int i = lane; i < P; i += 64) {
+				const int l = i ^ j;
+				if (l > i) {
+					const uint16_t x = a[i], y = a[l];
+					const bool up = (i & k) == 0;
+					if ((x > y) == up) {
+						a[i] = y;
+						a[l] = x;
+					}
+				}
+			}
+			__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+		}
+}
+
+__device__ __forceinline__ double replay_median(const uint16_t *a, int n) {
+	const int lhs = (n - 1) / 2, rhs = n / 2;
+	if (lhs == rhs)
+		return (double)a[lhs];
+	return (double)(a[lhs] + a[rhs]) / 2.0;
+}
+
+/* returns 1 on success (value / counters set), 0 = leave the pixel to the literal path */
+__device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double sh, int lane, uint16_t *value,
+		uint32_t *rlo, uint32_t *rhi) {
+	int N = N0, r = 0, n, iter = 0;
+	uint32_t clo = 0, chi = 0;
+	for (int j = lane; j < N0; j += 64)
+		L.rej[j] = 0;
+	do {
+		iter++;
+		uint64_t S, SS;
+		replay_moments(L.stack, N, lane, S, SS);
+		bool e0;
+		double sigma = exact_sd(N, S, SS, &e0);
+		if (iter == 1)
+			replay_sort(L.stack, N, lane);
+		double median = replay_median(L.stack, N);
+		if (type == 4) {
+			for (int j = lane; j < N; j += 64)
+				L.w[j] = L.stack[j];
+			__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+			bool sig_e0 = e0;
+			for (int guard = 0;; guard++) {
+				if (guard > 100000)
+					return 0;
+				const double m0 = median - 1.5 * sigma, m1 = median + 1.5 * sigma;
+				const double tol = sig_e0 ? 0.0 : SG_BAND * (fabs(median) + 1.5 * sigma + 1.0);
+				int amb = 0, clamped_lo = 0, clamped_hi = 0;
+				const uint16_t vlo = sg_round_to_WORD(m0), vhi = sg_round_to_WORD(m1);
+				for (int j = lane; j < N; j += 64) {
+					const double x = (double)L.w[j];
+					if (!sig_e0 && ((x >= m0 - tol && x <= m0 + tol) || (x >= m1 - tol && x <= m1 + tol)))
+						amb = 1;
+					if (x < m0) {
+						L.w[j] = vlo;
+						clamped_lo = 1;
+					} else if (x > m1) {
+						L.w[j] = vhi;
+						clamped_hi = 1;
+					}
+				}
+				amb = wave_or(amb);
+				clamped_lo = wave_or(clamped_lo);
+				clamped_hi = wave_or(clamped_hi);
+				if (amb)
+					return 0;
+				if ((clamped_lo && round_ambiguous(m0, tol + 1e-9 * tol)) ||
+						(clamped_hi && round_ambiguous(m1, tol + 1e-9 * tol)))
+					return 0;
+				__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+				median = replay_median(L.w, N);
+				uint64_t Sw, SSw;
+				replay_moments(L.w, N, lane, Sw, SSw);
+				const double sigma0 = sigma;
+				const bool e00 = sig_e0;
+				bool we0;
+				sigma = 1.134 * exact_sd(N, Sw, SSw, &we0);
+				sig_e0 = we0;
+				if (e00) {
+					if (we0)
+						break;	/* 0/0 = NaN: the loop exits */
+					continue;	/* x/0 = inf > 0.0005 */
+				}
+				const double q = fabs(sigma - sigma0) / sigma0;
+				if (fabs(q - 0.0005) <= 1e-9 * 0.0005 + SG_BAND * (1.0 + q))
+					return 0;
+				if (!(q > 0.0005))
+					break;
+			}
+			e0 = sig_e0;
+		}
+		/* decisions, frame order, with the early break */
+		const double tl = sl * sigma, th = sh * sigma;
+		const double blo = median - tl, bhi = median + th;
+		const double tol = e0 ? 0.0 : SG_BAND * (fabs(median) + fabs(tl) + fabs(th) + 1.0);
+		const int per = (N + 63) / 64, j0 = lane * per;
+		int amb = 0, cnt = 0;
+		int8_t d[SG_REPLAY_MAXN / 64];
+#pragma unroll 4
+		for (int k = 0; k < per; k++) {
+			const int j = j0 + k;
+			int8_t v = 0;
+			if (j < N) {
+				const double x = (double)L.stack[j];
+				if (!e0 && ((x >= blo - tol && x <= blo + tol) || (x >= bhi - tol && x <= bhi + tol)))
+					amb = 1;
+				v = (median - x > tl) ? -1 : ((x - median > th) ? 1 : 0);
+			}
+			d[k] = v;
+			cnt += v != 0;
+		}
+		if (wave_or(amb))
+			return 0;
+		/* first frame fb with N - (r + #rejections in [0, fb]) <= 4 */
+		const int before = wave_excl_scan(cnt, lane);
+		int fb_lane = N;
+		{
+			int c = r + before;
+			for (int k = 0; k < per; k++) {
+				const int j = j0 + k;
+				if (j >= N)
+					break;
+				c += d[k] != 0;
+				if (N - c <= 4) {
+					fb_lane = j;
+					break;
+				}
+			}
+		}
+		int fb = fb_lane;
+#pragma unroll
+		for (int o = 32; o > 0; o >>= 1) {
+			const int t = __shfl_xor(fb, o, 64);
+			fb = t < fb ? t : fb;
+		}
+		if (fb > N - 1)
+			fb = N - 1;
+		if (iter == 1 && fb < N - 1)
+			return 0;	/* stale entries of the previous pixel */
+		int nrej = 0;
+		for (int k = 0; k < per; k++) {
+			const int j = j0 + k;
+			if (j <= fb) {
+				L.rej[j] = d[k];
+				nrej += d[k] != 0;
+				clo += d[k] < 0;
+				chi += d[k] > 0;
+			}
+		}
+		r += (int)wave_sum_u64((uint64_t)nrej);
+		__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+		/* order-preserving removal of every position j < N with rejected[j] != 0 */
+		int keep = 0;
+		uint16_t kv[SG_REPLAY_MAXN / 64];
+		for (int k = 0; k < per; k++) {
+			const int j = j0 + k;
+			kv[k] = j < N ? L.stack[j] : 0;
+			keep += (j < N && L.rej[j] == 0);
+		}
+		int pos = wave_excl_scan(keep, lane);
+		const int kept = (int)wave_sum_u64((uint64_t)keep);
+		__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+		for (int k = 0; k < per; k++) {
+			const int j = j0 + k;
+			if (j < N && L.rej[j] == 0)
+				L.stack[pos++] = kv[k];
+		}
+		__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+		n = N - kept;
+		N = kept;
+	} while (n > 0 && N > 3);
+	uint64_t S, SS;
+	replay_moments(L.stack, N, lane, S, SS);
+	*value = sg_round_to_WORD((double)S / (double)N);
+	*rlo = (uint32_t)wave_sum_u64((uint64_t)clo);
+	*rhi = (uint32_t)wave_sum_u64((uint64_t)chi);
+	return 1;
+}
+
+__global__ void __launch_bounds__(64 * SG_REPLAY_WAVES)
+k_stack_replay(SgStackParams p) {
+	__shared__ SgReplayLds Ls[SG_REPLAY_WAVES];
+	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+	SgReplayLds &L = Ls[wv];
+	unsigned int count = *p.flag_count;
+	if (count > p.flag_cap)
+		count = p.flag_cap;
+	if ((p.rejection != 2 && p.rejection != 4) || p.N > SG_REPLAY_MAXN)
+		return;
+	const unsigned int nw = gridDim.x * SG_REPLAY_WAVES;
+	for (unsigned int i = blockIdx.x * SG_REPLAY_WAVES + wv; i < count; i += nw) {
+		const int64_t pix = p.flag_list[i];
+		if (p.flag_map[pix] != SG_CLS_LITERAL)
+			continue;
+		const int x = (int)(pix % p.W);
+		const int64_t cr = pix / p.W;
+		const int R = (int)(cr % p.H), c = (int)(cr / p.H);
+		for (int f = lane; f < p.N; f += 64)
+			L.stack[f] = sg_gather(p, f, c, R, x);
+		__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+		uint16_t v;
+		uint32_t rl, rh;
+		if (!replay_pixel(L, p.N, p.rejection, p.sig0, p.sig1, lane, &v, &rl, &rh))
+			continue;
+		if (lane == 0) {
+			p.out[pix] = v;
+			p.flag_map[pix] = SG_CLS_DONE;
+			unsigned long long *sh = p.rej + ((size_t)(i % SG_REJ_SHARDS) * 6 + c * 2);
+			if (rl)
+				atomicAdd(sh, (unsigned long long)rl);
+			if (rh)
+				atomicAdd(sh + 1, (unsigned long long)rh);
+		}
+	}
+}
+
 /* phase 1: queued pixels (class LITERAL) replayed with an all-zero incoming rejected[];
  * a pixel whose first pass breaks early with N > 4 read its predecessor's stale entries
  * and is promoted to class CHAIN (no output).  phase 2: class CHAIN pixels replay the
@@ -960,8 +1252,8 @@ k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *s
 	for (unsigned int i = gid; i < count; i += nthreads) {
 		const int64_t pix = p.flag_list[i];
 		const int cls = p.flag_map[pix];
-		if ((phase == 1) != (cls == SG_CLS_LITERAL))
-			continue;
+		if (cls != (phase == 1 ? SG_CLS_LITERAL : SG_CLS_CHAIN))
+			continue;	/* SG_CLS_DONE: finished by k_stack_replay */
 		uint32_t crej[2] = {0, 0};
 		int fbrk;
 		for (int k = 0; k < p.N; k++)

@@ -40,7 +40,7 @@
 #define SGH_WAVES 4
 #define SGH_COLS 128		/* pixels per tile: lane l owns pixels 2l (col l) and 2l+1 (col 64+l) */
 #define SGH_CENTER 16		/* frames used for the centre estimate */
-#define SGH_BAND 1e-11		/* same rounding band as the sorted path (SG_BAND) */
+#define SGH_BAND 1e-13		/* same rounding band as the sorted path (SG_BAND) */
 
 typedef unsigned short sgh_u16x2 __attribute__((ext_vector_type(2)));
 

@@ -215,3 +215,20 @@ def test_hist_path_adversarial(gpu_ctx, case):
     rc, ref, rej_ref = orc.stack_rejection(frames, sg.SIGMA, sig=sig, max_thread=8)
     assert_same(out_h, ref, case)
     assert np.array_equal(rej_h, rej_ref), (rej_h, rej_ref)
+
+
+@pytest.mark.parametrize("rejection,sig", [(sg.WINSORIZED, (4.0, 3.0)), (sg.WINSORIZED, (2.0, 1.5)),
+                                           (sg.SIGMA, (1.0, 1.0)), (sg.SIGMA, (2.0, 0.8))])
+def test_early_break_replay(gpu_ctx, rejection, sig):
+    """columns half filled by the shift zero fill (image edges, large shifts) and tight
+    sigmas make the reference's `if (N - r <= 4) break;` fire in later passes, leaving this
+    pixel's stale rejected[] entries in play: the exact wave replay (k_stack_replay) must
+    reproduce the oracle bit for bit, rejection counters included"""
+    N, C, H, W = 48, 1, 72, 64     # |shifty| < block height (H/4): the reference's :1560 overflow
+    frames = orc.synth(N, C, H, W, seed=4242 + rejection, maxshift=12)
+    sx, sy = orc.synth_shifts(N, seed=4242 + rejection, maxshift=12)
+    rc, ref, rej_ref = orc.stack_rejection(frames, rejection, sig=sig, shiftx=sx, shifty=sy, max_thread=2)
+    assert rc == 0
+    out, rej, st = _stack_path(gpu_ctx, frames, rejection, sig, sx, sy, path=sg.PATH_SORTED, max_thread=2)
+    assert_same(out, ref, f"rej {rejection} sig {sig}")
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
