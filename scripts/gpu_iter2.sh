@@ -16,3 +16,4 @@ run full 0
 run prefix_only 1
 run no_finish 2
 run loads_only 3
+

@@ -378,7 +378,18 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 			HIPCHK(hipMemsetAsync(redo_count, 0, sizeof(unsigned int), s));
 			HIPCHK(hipEventRecord(dv.ev[0], s));
 			const size_t nblk_h = (size_t)((W + 127) / 128) * nrows * C;	/* 128-pixel tiles */
-			hipLaunchKernelGGL(k_stack_hist, dim3((unsigned)nblk_h), dim3(256), 0, s, p, redo_count, redo_list);
+			const char *pad = getenv("SG_HIST_LDSPAD");	/* A/B: extra LDS per workgroup (occupancy) */
+			if (p.dbg == 14) {	/* A/B: report the resident workgroups per CU */
+				int per_cu = -1;
+				(void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_stack_hist, 256,
+						pad ? (size_t)atoi(pad) : 0);
+				hipDeviceProp_t prop;
+				(void)hipGetDeviceProperties(&prop, dv.id);
+				fprintf(stderr, "k_stack_hist: %d workgroups/CU (lds/CU %zu, lds/block max %zu, pad %s)\n", per_cu,
+						(size_t)prop.maxSharedMemoryPerMultiProcessor, (size_t)prop.sharedMemPerBlock, pad ? pad : "0");
+			}
+			hipLaunchKernelGGL(k_stack_hist, dim3((unsigned)nblk_h), dim3(256), pad ? (size_t)atoi(pad) : 0, s, p,
+					redo_count, redo_list);
 			HIPCHK(hipGetLastError());
 			HIPCHK(hipEventRecord(dv.ev[1], s));
 			unsigned int nredo = 0;

@@ -244,88 +244,6 @@ __device__ __forceinline__ int sgh_floor_clamp(double x) {
 	return (int)floor(x);
 }
 
-/* the reference's SIGMA loop on the histogram; returns SG_CLS_OK or 1 (redo in the
- * sorted kernel).  Decision logic mirrors clip_pass() of the sorted path.  The kept set
- * is the value interval [A, B]; MA / MB = moments of the samples < A / <= B. */
-__device__ __forceinline__ int sgh_sigma(const SghPix &P, int N, double sl, double sh, uint16_t *value, uint32_t *rlo_out,
-		uint32_t *rhi_out, int &passes) {
-	int A = 0, B = 65535, n = N, r = 0, nrem;
-	passes = 0;
-	SghM MA = {0, 0, 0}, MB = P.T;
-	uint32_t rlo = 0, rhi = 0;
-	do {
-		const long long S = MB.s - MA.s;
-		const unsigned long long SS = MB.ss - MA.ss;
-		const long long num = (long long)n * (long long)SS - S * S;
-		const bool exact0 = (num == 0);
-		const double sigma = num <= 0 ? 0.0 : sqrt((double)num / ((double)n * (double)(n - 1)));
-		const int g1 = MA.c + (n - 1) / 2, g2 = MA.c + n / 2;
-		int m1, m2;
-		sgh_value_at2(P, g1, g2, m1, m2);
-		const double median = (g1 == g2) ? (double)m1 : (double)(m1 + m2) / 2.0;
-		const double tl = sl * sigma, th = sh * sigma;
-		const double blo = median - tl, bhi = median + th;
-		const double tol = exact0 ? 0.0 : SGH_BAND * (fabs(median) + fabs(tl) + fabs(th) + 1.0);
-		/* low: v < blo - tol rejected; v in [blo - tol, blo + tol] ambiguous */
-		int a = sgh_ceil_clamp(blo - tol);
-		if (a < A)
-			a = A;
-		int bt = sgh_floor_clamp(bhi + tol);
-		if (bt > B)
-			bt = B;
-		/* a == A gives M(A - 1) == MA and bt == B gives MB: both queries unconditional */
-		SghQ qa, qb;
-		sgh_q_load(P, a - 1, qa);
-		sgh_q_load(P, bt, qb);
-		const int cnt_a = sgh_q_count(P, qa), cnt_bt = sgh_q_count(P, qb);
-		if (!exact0) {
-			int amb1 = sgh_floor_clamp(blo + tol);
-			if (amb1 > B)
-				amb1 = B;
-			if (a <= amb1 && sgh_cnt_le(P, amb1) - cnt_a > 0)
-				return 1;
-			int amb0 = sgh_ceil_clamp(bhi - tol);
-			if (amb0 < A)
-				amb0 = A;
-			if (amb0 <= bt && cnt_bt - sgh_cnt_le(P, amb0 - 1) > 0)
-				return 1;
-		}
-		const int L = cnt_a - MA.c, H = MB.c - cnt_bt;
-		if (L + H > n)
-			return 1;
-		/* `if (N - r <= 4) break;` inside the clipping loop (:1684) */
-		const int need = n - 4 - r;
-		int fb = -1;
-		if (need <= 0)
-			fb = 0;
-		else if (L >= need)
-			fb = need - 1;
-		else if (L + H >= need)
-			fb = (n - H) + (need - L) - 1;
-		if (fb >= 0 && fb < n - 1)
-			return 1;
-		if (L) {
-			A = a;
-			MA = sgh_q_moments(P, qa);
-		}
-		if (H) {
-			B = bt;
-			MB = sgh_q_moments(P, qb);
-		}
-		rlo += L;
-		rhi += H;
-		r += L + H;
-		nrem = L + H;
-		n -= nrem;
-		passes++;
-	} while (nrem > 0 && n > 3);
-	const long long tot = (MB.s - MA.s) + (long long)n * P.lo;
-	*value = sg_round_to_WORD((double)tot / (double)n);
-	*rlo_out = rlo;
-	*rhi_out = rhi;
-	return SG_CLS_OK;
-}
-
 /* centre estimate of the two pixels of a lane from 16 samples each (16-bit halves of
  * p[]): median of the samples that are neither 0 nor 65535 (the out-of-frame zero fill of
  * edge pixels must not drag the band away); packed bitonic network */
@@ -504,34 +422,171 @@ __device__ __forceinline__ void sgh_bin_pair(uint32_t *h, uint32_t l4, uint32_t 
 	nsat = sgh_pk_add(nsat, sgh_pk_sub_sat(vv, 0xFFFEFFFEu));
 }
 
-/* after the build, 64 pixels (one column half) per wave: prefix counts, band moments and
- * the SIGMA loop; writes the outputs, the redo list and the counters */
-__device__ void sgh_finish(const SgStackParams &p, SghLds &L, int col, int lo, int R, int c, int x,
+/* ------------------------------------------------------------------------------------
+ * paired-lane finish: all 4 waves, 32 pixels per wave, the two lanes of a pair share one
+ * pixel and split its work (prefix groups, the two medians, the two threshold queries and
+ * their moments), exchanging results through DPP; both lanes carry identical loop state,
+ * so a pair never diverges and the per-pixel instruction chain is about halved.
+ * ------------------------------------------------------------------------------------ */
+__device__ __forceinline__ uint32_t sgh_x(uint32_t v) {	/* value of the partner lane (quad_perm 1,0,3,2) */
+	return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint64_t sgh_x64(uint64_t v) {
+	return (uint64_t)sgh_x((uint32_t)v) | ((uint64_t)sgh_x((uint32_t)(v >> 32)) << 32);
+}
+
+/* value at global rank g (single rank) */
+__device__ __forceinline__ int sgh_value_at1(const SghPix &P, int g) {
+	const int r = g - P.nz;
+	const bool in = r >= 0 && r < P.nb;
+	int grp = 0;
+#pragma unroll
+	for (int k = 1; k < SGH_NGRP; k++)
+		grp += (int)P.pc[k] <= r ? 1 : 0;
+	uint32_t d[SGH_GRP];
+	sgh_grp(P, grp, d);
+	return in ? sgh_locate(P, grp, d, sgh_sel(P.pc, grp), (uint32_t)r) : (r < 0 ? 0 : 65535);
+}
+
+/* the SIGMA loop of sgh_sigma, split over a lane pair: half 0 owns the low side (median
+ * rank g1, threshold a - 1, M(A - 1)), half 1 the high side (rank g2, threshold bt, M(B)) */
+__device__ __forceinline__ int sgh_sigma2(const SghPix &P, int N, double sl, double sh, int half, uint16_t *value,
+		uint32_t *rlo_out, uint32_t *rhi_out) {
+	int A = 0, B = 65535, n = N, r = 0, nrem;
+	SghM MA = {0, 0, 0}, MB = P.T;
+	uint32_t rlo = 0, rhi = 0;
+	do {
+		const long long S = MB.s - MA.s;
+		const unsigned long long SS = MB.ss - MA.ss;
+		const long long num = (long long)n * (long long)SS - S * S;
+		const bool exact0 = (num == 0);
+		const double sigma = num <= 0 ? 0.0 : sqrt((double)num / ((double)n * (double)(n - 1)));
+		const int g1 = MA.c + (n - 1) / 2, g2 = MA.c + n / 2;
+		const int mv = sgh_value_at1(P, half ? g2 : g1);
+		const int mo = (int)sgh_x((uint32_t)mv);
+		const int m1 = half ? mo : mv, m2 = half ? mv : mo;
+		const double median = (g1 == g2) ? (double)m1 : (double)(m1 + m2) / 2.0;
+		const double tl = sl * sigma, th = sh * sigma;
+		const double blo = median - tl, bhi = median + th;
+		const double tol = exact0 ? 0.0 : SGH_BAND * (fabs(median) + fabs(tl) + fabs(th) + 1.0);
+		int a = sgh_ceil_clamp(blo - tol);
+		if (a < A)
+			a = A;
+		int bt = sgh_floor_clamp(bhi + tol);
+		if (bt > B)
+			bt = B;
+		SghQ q;
+		sgh_q_load(P, half ? bt : a - 1, q);
+		const int cm = sgh_q_count(P, q), co = (int)sgh_x((uint32_t)cm);
+		const int cnt_a = half ? co : cm, cnt_bt = half ? cm : co;
+		uint32_t amb = 0;
+		if (!exact0) {
+			if (!half) {
+				int amb1 = sgh_floor_clamp(blo + tol);
+				if (amb1 > B)
+					amb1 = B;
+				amb = (a <= amb1 && sgh_cnt_le(P, amb1) - cnt_a > 0) ? 1u : 0u;
+			} else {
+				int amb0 = sgh_ceil_clamp(bhi - tol);
+				if (amb0 < A)
+					amb0 = A;
+				amb = (amb0 <= bt && cnt_bt - sgh_cnt_le(P, amb0 - 1) > 0) ? 1u : 0u;
+			}
+		}
+		if (amb | sgh_x(amb))
+			return 1;
+		const int L = cnt_a - MA.c, H = MB.c - cnt_bt;
+		if (L + H > n)
+			return 1;
+		/* `if (N - r <= 4) break;` inside the clipping loop (:1684) */
+		const int need = n - 4 - r;
+		int fb = -1;
+		if (need <= 0)
+			fb = 0;
+		else if (L >= need)
+			fb = need - 1;
+		else if (L + H >= need)
+			fb = (n - H) + (need - L) - 1;
+		if (fb >= 0 && fb < n - 1)
+			return 1;
+		if (L | H) {
+			/* field-wise selects: a select of whole structs becomes a scratch access */
+			SghM Mm;
+			if (half ? H : L) {
+				Mm = sgh_q_moments(P, q);
+			} else {
+				Mm.c = half ? MB.c : MA.c;
+				Mm.s = half ? MB.s : MA.s;
+				Mm.ss = half ? MB.ss : MA.ss;
+			}
+			const int oc = (int)sgh_x((uint32_t)Mm.c);
+			const long long os = (long long)sgh_x64((uint64_t)Mm.s);
+			const unsigned long long oss = sgh_x64(Mm.ss);
+			if (L) {
+				A = a;
+				MA.c = half ? oc : Mm.c;
+				MA.s = half ? os : Mm.s;
+				MA.ss = half ? oss : Mm.ss;
+			}
+			if (H) {
+				B = bt;
+				MB.c = half ? Mm.c : oc;
+				MB.s = half ? Mm.s : os;
+				MB.ss = half ? Mm.ss : oss;
+			}
+		}
+		rlo += L;
+		rhi += H;
+		r += L + H;
+		nrem = L + H;
+		n -= nrem;
+	} while (nrem > 0 && n > 3);
+	const long long tot = (MB.s - MA.s) + (long long)n * P.lo;
+	*value = sg_round_to_WORD((double)tot / (double)n);
+	*rlo_out = rlo;
+	*rhi_out = rhi;
+	return SG_CLS_OK;
+}
+
+/* pixel column `col` of the tile (x its image column), lane pair half `half` */
+__device__ void sgh_finish2(const SgStackParams &p, SghLds &L, int col, int half, int lo, int R, int c, int x,
 		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
 	const int lane = threadIdx.x & 63;
 	const int N = p.N;
 	const uint32_t *hc = &L.h[col >> 6][0][col & 63];	/* dword j at hc[64 j] */
 	if (p.dbg == 2 || p.dbg == 3) {
-		if (x < p.W)
+		if (x < p.W && !half)
 			p.out[((int64_t)c * p.H + R) * p.W + x] = (uint16_t)(hc[0] + L.nz[col]);
 		return;
+	}
+	/* prefix: this lane's 4 groups, then the partner's 4 */
+	uint32_t gc[SGH_NGRP / 2], gs[SGH_NGRP / 2], gss[SGH_NGRP / 2];
+#pragma unroll
+	for (int k = 0; k < SGH_NGRP / 2; k++) {
+		const int g = (SGH_NGRP / 2) * half + k;
+		uint32_t d[SGH_GRP], cc = 0, s = 0, ss = 0;
+#pragma unroll
+		for (int j = 0; j < SGH_GRP; j++)
+			d[j] = hc[64 * (g * SGH_GRP + j)];
+		sgh_grp_moments(d, cc, s, ss);
+		const uint32_t b0 = (uint32_t)g * (4u * SGH_GRP);
+		gc[k] = cc;
+		gs[k] = s + b0 * cc;
+		gss[k] = ss + 2u * b0 * s + b0 * b0 * cc;
 	}
 	SghPix P;
 	uint32_t cum = 0, s32 = 0, ss32 = 0;
 #pragma unroll
 	for (int g = 0; g < SGH_NGRP; g++) {
+		const int k = g % (SGH_NGRP / 2);
+		const bool mine = (g >= SGH_NGRP / 2) == (half != 0);
+		const uint32_t oc = sgh_x(gc[k]), os = sgh_x(gs[k]), oss = sgh_x(gss[k]);
 		P.pc[g] = cum;
 		P.ps[g] = s32;
 		P.pss[g] = ss32;
-		uint32_t d[SGH_GRP], c = 0, s = 0, ss = 0;
-#pragma unroll
-		for (int k = 0; k < SGH_GRP; k++)
-			d[k] = hc[64 * (g * SGH_GRP + k)];
-		sgh_grp_moments(d, c, s, ss);
-		const uint32_t b0 = (uint32_t)g * (4u * SGH_GRP);
-		cum += c;
-		s32 += s + b0 * c;
-		ss32 += ss + 2u * b0 * s + b0 * b0 * c;
+		cum += mine ? gc[k] : oc;
+		s32 += mine ? gs[k] : os;
+		ss32 += mine ? gss[k] : oss;
 	}
 	const int oob = (int)hc[64 * SGH_DW];
 	P.lo = lo;
@@ -547,9 +602,7 @@ __device__ void sgh_finish(const SgStackParams &p, SghLds &L, int col, int lo, i
 		if (p.dbg == 1) {
 			value = (uint16_t)(s32 + ss32);
 		} else if (P.nb + oob != N || oob != P.nz + P.ns) {
-			/* an out-of-band sample that is not 0 / 65535, or a wrapped u8 counter (a
-			 * carry loses 256 band counts) */
-			cls = 1;
+			cls = 1;	/* out-of-band sample other than 0 / 65535, or a wrapped u8 counter */
 		} else {
 			const long long dz = -(long long)lo, ds = 65535 - (long long)lo;
 			P.Z.c = P.nz;
@@ -558,19 +611,19 @@ __device__ void sgh_finish(const SgStackParams &p, SghLds &L, int col, int lo, i
 			P.T.c = N;
 			P.T.s = (long long)s32 + P.Z.s + ds * P.ns;
 			P.T.ss = (unsigned long long)ss32 + P.Z.ss + (unsigned long long)(ds * ds) * (unsigned long long)P.ns;
-			int passes;
-			cls = sgh_sigma(P, N, p.sig0, p.sig1, &value, &rlo, &rhi, passes);
-			if (p.dbg == 7)	/* A/B: pass count per pixel */
-				value = (uint16_t)passes;
+			cls = sgh_sigma2(P, N, p.sig0, p.sig1, half, &value, &rlo, &rhi);
 		}
 		const int64_t pix = ((int64_t)c * p.H + R) * p.W + x;
-		if (cls == SG_CLS_OK) {
-			p.out[pix] = value;
-		} else {
-			const unsigned int slot = atomicAdd(redo_count, 1u);
-			redo_list[slot] = (unsigned int)pix;
-			rlo = rhi = 0;
+		if (!half) {
+			if (cls == SG_CLS_OK) {
+				p.out[pix] = value;
+			} else {
+				const unsigned int slot = atomicAdd(redo_count, 1u);
+				redo_list[slot] = (unsigned int)pix;
+			}
 		}
+		if (cls != SG_CLS_OK || half)
+			rlo = rhi = 0;
 	}
 	unsigned long long a = rlo, b = rhi;
 	for (int o = 32; o > 0; o >>= 1) {
@@ -578,7 +631,7 @@ __device__ void sgh_finish(const SgStackParams &p, SghLds &L, int col, int lo, i
 		b += __shfl_down(b, o, 64);
 	}
 	if (lane == 0 && (a | b)) {
-		unsigned long long *sh = p.rej + ((size_t)((blockIdx.x * 2 + (col >> 6)) % SG_REJ_SHARDS) * 6 + c * 2);
+		unsigned long long *sh = p.rej + ((size_t)((blockIdx.x * 4 + (col >> 5)) % SG_REJ_SHARDS) * 6 + c * 2);
 		atomicAdd(sh, a);
 		atomicAdd(sh + 1, b);
 	}
@@ -709,9 +762,10 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 		atomicAdd(&L.ns[64 + lane], nsat >> 16);
 	}
 	__syncthreads();
-	if (wave >= 2)
-		return;
-	/* waves 0 / 1 finish the even / odd pixels of the tile */
-	sgh_finish(p, L, lane + 64 * wave, wave ? lo_b : lo_a, R, c, x0 + 2 * lane + wave, redo_count, redo_list);
+	/* every wave finishes 32 pixel columns, a lane pair per column; the band start of column
+	 * col is held by lane col & 63 of every wave (each wave computed the centres) */
+	const int col = 32 * wave + (lane >> 1), half = lane & 1;
+	const int lo = __shfl(wave < 2 ? lo_a : lo_b, col & 63, 64);
+	sgh_finish2(p, L, col, half, lo, R, c, x0 + 2 * (col & 63) + (col >> 6), redo_count, redo_list);
 }
 
