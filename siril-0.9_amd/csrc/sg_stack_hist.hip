@@ -40,6 +40,9 @@
 #define SGH_WAVES 4
 #define SGH_COLS 128		/* pixels per tile: lane l owns pixels 2l (col l) and 2l+1 (col 64+l) */
 #define SGH_CENTER 16		/* frames used for the centre estimate */
+#ifndef SGH_NBUF
+#define SGH_NBUF 2		/* register buffers of 16 frames per wave (NBUF-1 blocks in flight while binning) */
+#endif
 #define SGH_BAND 1e-13		/* same rounding band as the sorted path (SG_BAND) */
 
 typedef unsigned short sgh_u16x2 __attribute__((ext_vector_type(2)));
@@ -54,6 +57,7 @@ typedef unsigned short sgh_u16x2 __attribute__((ext_vector_type(2)));
 struct SghLds {
 	uint32_t h[2][SGH_HROWS][64];
 	uint32_t nz[SGH_COLS], ns[SGH_COLS];	/* zeros / 65535s (all of them lie outside the band) */
+	uint32_t lo2[64];			/* band starts of the lane pixel pairs (u16 halves) */
 };
 
 /* Finish-phase queries.  The band is cut into SGH_NGRP groups of SGH_GRP dwords (32 bins);
@@ -638,46 +642,57 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds &L, int col, int half
 }
 
 /* one wave's share of the tile's histogram build: 16-frame blocks, wave w bins blocks w,
- * w+4, ...; frames 0..15 (block 0) are the centre sample every wave loads.  Two named
- * buffers keep the next block's loads in flight while the current one is binned; the
- * shift table of the block after that is fetched (scalar loads) before binning. */
-template <bool EDGE>
+ * w+4, w+8, ... in order, with NBUF named register buffers: a buffer is refilled with the
+ * wave's block NBUF steps ahead right after it has been binned, so NBUF-1 blocks stay in
+ * flight during the binning; the shift table of that block is fetched (scalar loads)
+ * before the binning.  No block is loaded twice.  Frames 0..15 (wave 0's first block) are
+ * the centre sample: wave 0 sorts them and publishes the band starts through LDS while the
+ * other waves' first blocks are in flight (one barrier, which also covers the clear). */
+template <bool EDGE, int NBUF>
 __device__ __forceinline__ void sgh_build(const SgStackParams &p, SghLds &L, const SghFrame &F, int wave, int lane,
 		int &lo_a, int &lo_b, uint32_t &nonzero, uint32_t &nsat, int &counted) {
 	constexpr int M = 16;		/* frames per block */
 	constexpr int STEP = M * SGH_WAVES;
+	constexpr int AHEAD = NBUF * STEP;
 	const int N = p.N;
 	uint32_t *const h = &L.h[0][0][0];
 	const uint32_t l4 = (uint32_t)lane * 4u;
-	uint32_t bufA[M], bufB[M], p16[SGH_CENTER], fixA = 0, fixB = 0, fix0 = 0;
+	uint32_t buf[NBUF][M], fix[NBUF];
 	SghTab16 T;
-	auto loadblk = [&](int f0, uint32_t (&dst)[M], uint32_t &fix) {
+	auto loadblk = [&](int f0, uint32_t (&dst)[M], uint32_t &fx) {
 		if (f0 + M <= N)
-			sgh_loadblk<true, EDGE>(F, T, N, f0, dst, fix);
+			sgh_loadblk<true, EDGE>(F, T, N, f0, dst, fx);
 		else
-			sgh_loadblk<false, EDGE>(F, T, N, f0, dst, fix);
+			sgh_loadblk<false, EDGE>(F, T, N, f0, dst, fx);
 	};
-	int fb = M * wave;
-	sgh_tab16(p, 0, T);
-	loadblk(0, p16, fix0);
-	if (fb >= SGH_CENTER && fb < N) {
-		sgh_tab16(p, fb, T);
-		loadblk(fb, bufA, fixA);
+	int f[NBUF];
+#pragma unroll
+	for (int k = 0; k < NBUF; k++) {
+		f[k] = M * wave + k * STEP;
+		fix[k] = 0;
+		if (f[k] < N) {
+			sgh_tab16(p, f[k], T);
+			loadblk(f[k], buf[k], fix[k]);
+		}
 	}
-	sgh_tab16(p, fb + STEP < N ? fb + STEP : (fb < p.hist_npad ? fb : 0), T);
+	if (wave == 0) {
+		uint32_t p16[SGH_CENTER];
 #pragma unroll
-	for (int m = 0; m < M; m++)
-		p16[m] = sgh_fixup<EDGE>(p16[m], fix0, m);
-	sgh_centre2(p16, lo_a, lo_b);
-	if (fb < SGH_CENTER) {
-#pragma unroll
-		for (int m = 0; m < M; m++)
-			bufA[m] = p16[m];
-		fixA = 0;
+		for (int m = 0; m < SGH_CENTER; m++)
+			p16[m] = sgh_fixup<EDGE>(buf[0][m], fix[0], m);
+		int la, lb;
+		sgh_centre2(p16, la, lb);
+		L.lo2[lane] = (uint32_t)la | ((uint32_t)lb << 16);
+	}
+	__syncthreads();	/* histogram cleared, band starts published */
+	{
+		const uint32_t l2 = L.lo2[lane];
+		lo_a = (int)(l2 & 0xFFFFu);
+		lo_b = (int)(l2 >> 16);
 	}
 	const uint32_t lo2 = (uint32_t)lo_a | ((uint32_t)lo_b << 16);
 	const bool loads_only = p.dbg == 3;
-	auto binblk = [&](int f0, const uint32_t (&raw)[M], uint32_t fix) {
+	auto binblk = [&](int f0, const uint32_t (&raw)[M], uint32_t fx) {
 		if (loads_only) {
 #pragma unroll
 			for (int m = 0; m < M; m++)
@@ -685,28 +700,32 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, SghLds &L, con
 		} else if (f0 + M <= N) {
 #pragma unroll
 			for (int m = 0; m < M; m++)
-				sgh_bin_pair(h, l4, lo2, sgh_fixup<EDGE>(raw[m], fix, m), nonzero, nsat);
+				sgh_bin_pair(h, l4, lo2, sgh_fixup<EDGE>(raw[m], fx, m), nonzero, nsat);
 		} else {
 #pragma unroll
 			for (int m = 0; m < M; m++)
 				if (f0 + m < N)
-					sgh_bin_pair(h, l4, lo2, sgh_fixup<EDGE>(raw[m], fix, m), nonzero, nsat);
+					sgh_bin_pair(h, l4, lo2, sgh_fixup<EDGE>(raw[m], fx, m), nonzero, nsat);
 		}
 		counted += (N - f0 < M ? N - f0 : M);
 	};
-	/* invariant: T = table of block nx(fb) = the block loaded next */
-	auto nx = [&](int f) { return f + STEP < N ? f + STEP : f; };
-	while (fb < N) {
-		loadblk(nx(fb), bufB, fixB);
-		sgh_tab16(p, nx(nx(fb)), T);
-		binblk(fb, bufA, fixA);
-		fb += STEP;
-		if (fb >= N)
-			break;
-		loadblk(nx(fb), bufA, fixA);
-		sgh_tab16(p, nx(nx(fb)), T);
-		binblk(fb, bufB, fixB);
-		fb += STEP;
+	if (f[0] + AHEAD < N)
+		sgh_tab16(p, f[0] + AHEAD, T);
+	while (f[0] < N) {
+#pragma unroll
+		for (int k = 0; k < NBUF; k++) {
+			if (f[k] >= N)
+				break;
+			binblk(f[k], buf[k], fix[k]);
+			const int nf = f[k] + AHEAD;
+			if (nf < N)
+				loadblk(nf, buf[k], fix[k]);	/* T = table of nf */
+			f[k] = nf;
+			const int kn = (k + 1) % NBUF;
+			const int tn = f[kn] + AHEAD;	/* the next buffer's refill */
+			if (f[kn] < N && tn < N)
+				sgh_tab16(p, tn, T);
+		}
 	}
 }
 
@@ -747,14 +766,14 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 		L.nz[tid] = 0;
 		L.ns[tid] = 0;
 	}
-	__syncthreads();
+	/* no barrier here: sgh_build issues its first loads, then its barrier covers the clear */
 
 	uint32_t nonzero = 0, nsat = 0;
 	int counted = 0, lo_a, lo_b;
 	if (interior)
-		sgh_build<false>(p, L, F, wave, lane, lo_a, lo_b, nonzero, nsat, counted);
+		sgh_build<false, SGH_NBUF>(p, L, F, wave, lane, lo_a, lo_b, nonzero, nsat, counted);
 	else
-		sgh_build<true>(p, L, F, wave, lane, lo_a, lo_b, nonzero, nsat, counted);
+		sgh_build<true, SGH_NBUF>(p, L, F, wave, lane, lo_a, lo_b, nonzero, nsat, counted);
 	if (counted) {
 		atomicAdd(&L.nz[lane], (uint32_t)counted - (nonzero & 0xFFFFu));
 		atomicAdd(&L.nz[64 + lane], (uint32_t)counted - (nonzero >> 16));

@@ -11,7 +11,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libsirilgpu.so")
+LIB_PATH = os.environ.get("SG_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libsirilgpu.so")  # A/B builds
 
 # enum values (src/stacking/stacking.c:54-56, src/stacking/stacking.h:14-30)
 SUM, MEAN, MEDIAN, MAX, MIN = range(5)
