@@ -33,31 +33,137 @@ __device__ __forceinline__ int sg_bitrev(int x, int logn) {
 	return (int)(__brev((unsigned)x) >> (32 - logn));
 }
 
-/* nb independent length-n FFTs held in LDS (batch b at buf + b*bstride), input already in
- * bit-reversed order, output natural order.  tw[k] = exp(-2 pi i k / n), k < n/2. */
-__device__ void sg_lds_fft(sg_c64 *buf, int n, int logn, int nb, int bstride, const sg_c64 *__restrict__ tw,
-		bool inverse) {
-	const int half = n >> 1;
-	for (int h = 1; h < n; h <<= 1) {
-		__syncthreads();
-		const int tstep = n / (2 * h);
-		for (int t = threadIdx.x; t < nb * half; t += blockDim.x) {
-			const int b = t >> (logn - 1);
-			const int bi = t & (half - 1);
-			const int k = bi & (h - 1);
-			const int i0 = ((bi - k) << 1) + k;
-			sg_c64 *x = buf + (size_t)b * bstride;
-			sg_c64 w = tw[k * tstep];
-			if (inverse)
-				w.y = -w.y;
-			const sg_c64 u = x[i0], v = x[i0 + h];
-			const double vr = v.x * w.x - v.y * w.y;
-			const double vi = v.x * w.y + v.y * w.x;
-			x[i0] = make_double2(u.x + vr, u.y + vi);
-			x[i0 + h] = make_double2(u.x - vr, u.y - vi);
+/* ------------------------------------------------------------------------------------
+ * nb independent length-n FFTs held in LDS (transform b at buf + b*bstride), natural order
+ * in and out: Stockham auto-sort passes of radix 8 (then 4 / 2 for the remaining factor),
+ * each thread taking whole radix-R butterflies in registers (a 2048-point transform is 4
+ * LDS round trips instead of 11).  tw[k] = exp(-2 pi i k / n), k < n/2; the inverse uses
+ * conjugate twiddles (unnormalised, FFTW_BACKWARD).
+ * ------------------------------------------------------------------------------------ */
+__device__ __forceinline__ sg_c64 sg_cmul(sg_c64 a, sg_c64 b) {
+	return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ sg_c64 sg_cadd(sg_c64 a, sg_c64 b) {
+	return make_double2(a.x + b.x, a.y + b.y);
+}
+__device__ __forceinline__ sg_c64 sg_csub(sg_c64 a, sg_c64 b) {
+	return make_double2(a.x - b.x, a.y - b.y);
+}
+/* multiply by -i (forward) or +i (inverse) */
+__device__ __forceinline__ sg_c64 sg_mul_mi(sg_c64 a, bool inv) {
+	return inv ? make_double2(-a.y, a.x) : make_double2(a.y, -a.x);
+}
+
+/* in-register DFT of R = 2, 4, 8 points (natural order in and out) */
+template <int R, int RV>
+__device__ __forceinline__ void sg_dft_small(sg_c64 (&v)[RV], bool inv) {
+	if constexpr (R == 2) {
+		const sg_c64 a = v[0], b = v[1];
+		v[0] = sg_cadd(a, b);
+		v[1] = sg_csub(a, b);
+		return;
+	}
+	else if constexpr (R == 4) {
+		const sg_c64 a0 = sg_cadd(v[0], v[2]), a1 = sg_csub(v[0], v[2]);
+		const sg_c64 b0 = sg_cadd(v[1], v[3]), b1 = sg_mul_mi(sg_csub(v[1], v[3]), inv);
+		v[0] = sg_cadd(a0, b0);
+		v[2] = sg_csub(a0, b0);
+		v[1] = sg_cadd(a1, b1);
+		v[3] = sg_csub(a1, b1);
+		return;
+	} else {
+	/* R = 8: radix-2 DIF into two 4-point DFTs */
+	const double h = 0.70710678118654752440;
+	sg_c64 e[4], o[4];
+#pragma unroll
+	for (int k = 0; k < 4; k++) {
+		e[k] = sg_cadd(v[k], v[k + 4]);
+		o[k] = sg_csub(v[k], v[k + 4]);
+	}
+	/* o[k] *= W8^k */
+	o[1] = inv ? make_double2(h * (o[1].x - o[1].y), h * (o[1].x + o[1].y))
+		   : make_double2(h * (o[1].x + o[1].y), h * (o[1].y - o[1].x));
+	o[2] = sg_mul_mi(o[2], inv);
+	o[3] = inv ? make_double2(-h * (o[3].x + o[3].y), h * (o[3].x - o[3].y))
+		   : make_double2(h * (o[3].y - o[3].x), -h * (o[3].x + o[3].y));
+	sg_dft_small<4>(e, inv);
+	sg_dft_small<4>(o, inv);
+	const sg_c64 *E = e, *O = o;
+#pragma unroll
+	for (int k = 0; k < 4; k++) {
+		v[2 * k] = E[k];
+		v[2 * k + 1] = O[k];
+	}
+	}
+}
+
+__device__ __forceinline__ sg_c64 sg_twiddle(const sg_c64 *__restrict__ tw, int n, int k, bool inv) {
+	sg_c64 w = (k < (n >> 1)) ? tw[k] : tw[k - (n >> 1)];
+	if (k >= (n >> 1))
+		w = make_double2(-w.x, -w.y);
+	if (inv)
+		w.y = -w.y;
+	return w;
+}
+
+template <int R>
+__device__ __forceinline__ void sg_stockham_pass(sg_c64 *buf, int n, int nb, int bstride, int Ns,
+		const sg_c64 *__restrict__ tw, bool inv) {
+	constexpr int MAXI = 16 / R;	/* work items per thread: nb * n / R <= MAXI * blockDim (host-checked) */
+	const int per = n / R, items = nb * per;
+	sg_c64 v[MAXI][R];
+	/* load every item's R inputs before anyone stores (in-place pass) */
+#pragma unroll
+	for (int it = 0; it < MAXI; it++) {
+		const int t = threadIdx.x + it * blockDim.x;
+		if (t < items) {
+			const int b = t / per, j = t - b * per;
+			const sg_c64 *x = buf + (size_t)b * bstride;
+#pragma unroll
+			for (int r = 0; r < R; r++)
+				v[it][r] = x[j + r * per];
 		}
 	}
 	__syncthreads();
+#pragma unroll
+	for (int it = 0; it < MAXI; it++) {
+		const int t = threadIdx.x + it * blockDim.x;
+		if (t < items) {
+			const int b = t / per, j = t - b * per;
+			const int jm = j & (Ns - 1);
+			const int kstep = jm * (n / (Ns * R));
+#pragma unroll
+			for (int r = 1; r < R; r++)
+				v[it][r] = sg_cmul(v[it][r], sg_twiddle(tw, n, r * kstep, inv));
+			sg_dft_small<R, R>(v[it], inv);
+			sg_c64 *y = buf + (size_t)b * bstride;
+			const int base = (j - jm) * R + jm;
+#pragma unroll
+			for (int r = 0; r < R; r++)
+				y[base + r * Ns] = v[it][r];
+		}
+	}
+	__syncthreads();
+}
+
+__device__ void sg_lds_fft(sg_c64 *buf, int n, int logn, int nb, int bstride, const sg_c64 *__restrict__ tw,
+		bool inverse) {
+	(void)logn;
+	__syncthreads();
+	int Ns = 1;
+	while (Ns < n) {
+		const int rem = n / Ns;
+		if (rem >= 8) {
+			sg_stockham_pass<8>(buf, n, nb, bstride, Ns, tw, inverse);
+			Ns *= 8;
+		} else if (rem == 4) {
+			sg_stockham_pass<4>(buf, n, nb, bstride, Ns, tw, inverse);
+			Ns *= 4;
+		} else {
+			sg_stockham_pass<2>(buf, n, nb, bstride, Ns, tw, inverse);
+			Ns *= 2;
+		}
+	}
 }
 
 /* row pass of the forward transform of a + i b (b = -1: zero imaginary part) */
@@ -72,7 +178,7 @@ k_reg_rows_fwd(const uint16_t *__restrict__ sel, const int *__restrict__ fa, con
 	const int b = fb[pair];
 	const uint16_t *pb = b >= 0 ? sel + (size_t)b * plane + (size_t)row * S : nullptr;
 	for (int j = threadIdx.x; j < S; j += blockDim.x)
-		buf[sg_bitrev(j, logS)] = make_double2((double)pa[j], pb ? (double)pb[j] : 0.0);
+		buf[j] = make_double2((double)pa[j], pb ? (double)pb[j] : 0.0);
 	sg_lds_fft(buf, S, logS, 1, S, tw, false);
 	sg_c64 *out = work + (size_t)pair * plane + (size_t)row * S;
 	for (int j = threadIdx.x; j < S; j += blockDim.x)
@@ -89,7 +195,7 @@ k_reg_cols(sg_c64 *__restrict__ work, int S, int logS, int CW, const sg_c64 *__r
 	sg_c64 *base = work + (size_t)pair * S * S + x0;
 	for (int idx = threadIdx.x; idx < S * CW; idx += blockDim.x) {
 		const int r = idx / CW, c = idx - r * CW;
-		buf[c * bstride + sg_bitrev(r, logS)] = base[(size_t)r * S + c];
+		buf[c * bstride + r] = base[(size_t)r * S + c];
 	}
 	sg_lds_fft(buf, S, logS, CW, bstride, tw, inverse != 0);
 	for (int idx = threadIdx.x; idx < S * CW; idx += blockDim.x) {
@@ -155,7 +261,7 @@ k_reg_rows_inv_argmax(const sg_c64 *__restrict__ work, int S, int logS, const sg
 	const int row = blockIdx.x, pair = blockIdx.y;
 	const sg_c64 *in = work + (size_t)pair * S * S + (size_t)row * S;
 	for (int j = threadIdx.x; j < S; j += blockDim.x)
-		buf[sg_bitrev(j, logS)] = in[j];
+		buf[j] = in[j];
 	sg_lds_fft(buf, S, logS, 1, S, tw, true);
 	double va = -INFINITY, vb = -INFINITY;
 	int ia = 0x7fffffff, ib = 0x7fffffff;
