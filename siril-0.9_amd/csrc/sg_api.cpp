@@ -26,6 +26,7 @@ struct SgChainTables {
 
 template <int NREG, bool LISTED>
 __global__ void k_stack_sorted(SgStackParams p, const unsigned int *list, const unsigned int *list_count);
+template <int REJ>
 __global__ void k_stack_hist(SgStackParams p, unsigned int *redo_count, unsigned int *redo_list);
 void sg_dbg_why_dump(hipStream_t s);
 __global__ void k_stack_replay(SgStackParams p);
@@ -369,7 +370,8 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 		const size_t lds = (size_t)N * SG_STAGE_STRIDE * 2;
 		/* histogram fast path (sg_stack_hist.hip): SIGMA, no normalisation, N >= 16 */
 		const int path = d->kernel_path;
-		const bool hist = path != SG_PATH_SORTED && d->method == SG_STACK_MEAN && d->rejection == SG_SIGMA &&
+		const bool hist = path != SG_PATH_SORTED && d->method == SG_STACK_MEAN &&
+			(d->rejection == SG_SIGMA || d->rejection == SG_WINSORIZED) &&
 			p.normalize == 0 && N >= 16 && hist_addr_ok;
 		if (hist) {
 			HIPCHK(ensure(dv.redo, sizeof(unsigned int) * (npix_launch + 16)));
@@ -381,15 +383,19 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 			const char *pad = getenv("SG_HIST_LDSPAD");	/* A/B: extra LDS per workgroup (occupancy) */
 			if (p.dbg == 14) {	/* A/B: report the resident workgroups per CU */
 				int per_cu = -1;
-				(void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_stack_hist, 256,
+				(void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_stack_hist<2>, 256,
 						pad ? (size_t)atoi(pad) : 0);
 				hipDeviceProp_t prop;
 				(void)hipGetDeviceProperties(&prop, dv.id);
 				fprintf(stderr, "k_stack_hist: %d workgroups/CU (lds/CU %zu, lds/block max %zu, pad %s)\n", per_cu,
 						(size_t)prop.maxSharedMemoryPerMultiProcessor, (size_t)prop.sharedMemPerBlock, pad ? pad : "0");
 			}
-			hipLaunchKernelGGL(k_stack_hist, dim3((unsigned)nblk_h), dim3(256), pad ? (size_t)atoi(pad) : 0, s, p,
-					redo_count, redo_list);
+			if (p.rejection == SG_WINSORIZED)
+				hipLaunchKernelGGL(k_stack_hist<4>, dim3((unsigned)nblk_h), dim3(256), pad ? (size_t)atoi(pad) : 0, s,
+						p, redo_count, redo_list);
+			else
+				hipLaunchKernelGGL(k_stack_hist<2>, dim3((unsigned)nblk_h), dim3(256), pad ? (size_t)atoi(pad) : 0, s,
+						p, redo_count, redo_list);
 			HIPCHK(hipGetLastError());
 			HIPCHK(hipEventRecord(dv.ev[1], s));
 			unsigned int nredo = 0;

@@ -552,7 +552,230 @@ __device__ __forceinline__ int sgh_sigma2(const SghPix &P, int N, double sl, dou
 	return SG_CLS_OK;
 }
 
+/* ------------------------------------------------------------------------------------
+ * WINSORIZED (:1710-1749 + Winsorized :1163-1168) on the histogram, mirroring
+ * reject_winsorized() of the sorted path decision for decision.  The kept set is the value
+ * interval [A, B] (moments MA = M(A-1), MB = M(B), as in SIGMA); the Winsorized copy w of
+ * the sorted kept samples is Lw copies of vlo, the kept samples with values in [IA, IB]
+ * (the inner part, moments MI_A = M(IA-1), MI_B = M(IB)), Hw copies of vhi; clamping keeps
+ * w sorted, so its median is a rank query and its moments are the inner moments plus the
+ * clamped copies.  Both lanes of a pair run the same loop (no split); moments are relative
+ * to lo, and sd is shift invariant.
+ * ------------------------------------------------------------------------------------ */
+__device__ __forceinline__ double sgh_sd_rel(int n, long long S, long long SS, bool *e0) {
+	const long long num = (long long)n * SS - S * S;
+	*e0 = (num == 0);
+	return num <= 0 ? 0.0 : sqrt((double)num / ((double)n * (double)(n - 1)));
+}
+
+/* round_to_WORD(m) decision ambiguous (m within tol of 0, 65535 or a .5) */
+__device__ __forceinline__ bool sgh_round_ambiguous(double m, double tol) {
+	if (fabs(m) <= tol || fabs(m - 65535.0) <= tol)
+		return true;
+	if (m <= 0.0 || m > 65535.0)
+		return false;
+	const double t = m + 0.5;
+	return fabs(t - rint(t)) <= tol;
+}
+
+/* # samples with value < thr (thr real) */
+__device__ __forceinline__ int sgh_cnt_lt(const SghPix &P, double thr) {
+	/* v < thr <=> v <= ceil(thr) - 1 */
+	double c = ceil(thr) - 1.0;
+	if (c < -1.0)
+		c = -1.0;
+	if (c > 65535.0)
+		c = 65535.0;
+	return sgh_cnt_le(P, (int)c);
+}
+/* # samples with value <= thr */
+__device__ __forceinline__ int sgh_cnt_le_d(const SghPix &P, double thr) {
+	double c = floor(thr);
+	if (c < -1.0)
+		c = -1.0;
+	if (c > 65535.0)
+		c = 65535.0;
+	return sgh_cnt_le(P, (int)c);
+}
+
+__device__ __forceinline__ SghM sgh_M_le(const SghPix &P, int v) {
+	SghQ q;
+	sgh_q_load(P, v, q);
+	return sgh_q_moments(P, q);
+}
+
+__device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint16_t *value, uint32_t *rlo_out,
+		uint32_t *rhi_out) {
+	int A = 0, B = 65535, n = N, r = 0, nrem;
+	SghM MA = {0, 0, 0}, MB = P.T;
+	uint32_t rlo = 0, rhi = 0;
+	do {
+		const long long S = MB.s - MA.s;
+		const long long SS = (long long)(MB.ss - MA.ss);
+		bool e0;
+		double sigma = sgh_sd_rel(n, S, SS, &e0);
+		const int g1 = MA.c + (n - 1) / 2, g2 = MA.c + n / 2;
+		int m1, m2;
+		sgh_value_at2(P, g1, g2, m1, m2);
+		double median = (g1 == g2) ? (double)m1 : (double)(m1 + m2) / 2.0;
+		/* inner loop */
+		int Lw = 0, Hw = 0, vlo = 0, vhi = 0, IA = A, IB = B;
+		SghM MIA = MA, MIB = MB;
+		bool sig_e0 = e0;
+		for (int guard = 0;; guard++) {
+			if (guard > 4096)
+				return 1;
+			const double m0 = median - 1.5 * sigma, m1d = median + 1.5 * sigma;
+			const double tol = sig_e0 ? 0.0 : SGH_BAND * (fabs(median) + 1.5 * sigma + 1.0);
+			/* w elements < thr / <= thr */
+			auto w_lt = [&](double thr) {
+				int c = (Lw && (double)vlo < thr) ? Lw : 0;
+				int k = sgh_cnt_lt(P, thr);
+				k = k < MIA.c ? MIA.c : (k > MIB.c ? MIB.c : k);
+				c += k - MIA.c;
+				if (Hw && (double)vhi < thr)
+					c += Hw;
+				return c;
+			};
+			auto w_le = [&](double thr) {
+				int c = (Lw && (double)vlo <= thr) ? Lw : 0;
+				int k = sgh_cnt_le_d(P, thr);
+				k = k < MIA.c ? MIA.c : (k > MIB.c ? MIB.c : k);
+				c += k - MIA.c;
+				if (Hw && (double)vhi <= thr)
+					c += Hw;
+				return c;
+			};
+			const int clo = w_lt(m0 - tol);
+			if (!sig_e0 && clo != w_le(m0 + tol))
+				return 1;
+			const int chi = n - w_le(m1d + tol);
+			if (!sig_e0 && chi != n - w_lt(m1d - tol))
+				return 1;
+			if (clo + chi > n)
+				return 1;
+			if (clo > 0) {
+				if (sgh_round_ambiguous(m0, tol + 1e-9 * tol))
+					return 1;
+				if (clo < Lw || clo > n - Hw)
+					return 1;
+				if (clo > Lw) {
+					/* the inner samples below m0 join the clamped copies */
+					double c = ceil(m0 - tol);
+					IA = c < 0.0 ? 0 : (c > 65536.0 ? 65536 : (int)c);
+					MIA = sgh_M_le(P, IA - 1);
+				}
+				Lw = clo;
+				vlo = sg_round_to_WORD(m0);
+			}
+			if (chi > 0) {
+				if (sgh_round_ambiguous(m1d, tol + 1e-9 * tol))
+					return 1;
+				if (chi < Hw || chi > n - Lw)
+					return 1;
+				if (chi > Hw) {
+					double c = floor(m1d + tol);
+					IB = c < -1.0 ? -1 : (c > 65535.0 ? 65535 : (int)c);
+					MIB = sgh_M_le(P, IB);
+				}
+				Hw = chi;
+				vhi = sg_round_to_WORD(m1d);
+			}
+			if (MIB.c - MIA.c != n - Lw - Hw)
+				return 1;	/* inner part and clamp counts disagree: leave it to the sorted path */
+			/* median of w */
+			{
+				const int lhs = (n - 1) / 2, rhs = n / 2;
+				auto wat = [&](int i) {
+					if (i < Lw)
+						return vlo;
+					if (i >= n - Hw)
+						return vhi;
+					return sgh_value_at1(P, MA.c + i);
+				};
+				median = (lhs == rhs) ? (double)wat(lhs) : (double)(wat(lhs) + wat(rhs)) / 2.0;
+			}
+			const long long dl = (long long)vlo - P.lo, dh = (long long)vhi - P.lo;
+			const long long Sw = (MIB.s - MIA.s) + dl * Lw + dh * Hw;
+			const long long SSw = (long long)(MIB.ss - MIA.ss) + dl * dl * Lw + dh * dh * Hw;
+			const double sigma0 = sigma;
+			const bool e00 = sig_e0;
+			bool we0;
+			sigma = 1.134 * sgh_sd_rel(n, Sw, SSw, &we0);
+			sig_e0 = we0;
+			if (e00) {
+				if (we0)
+					break;	/* 0/0 = NaN: the loop exits */
+				continue;	/* x/0 = inf > 0.0005 */
+			}
+			const double q = fabs(sigma - sigma0) / sigma0;
+			if (fabs(q - 0.0005) <= 1e-9 * 0.0005 + SGH_BAND * (1.0 + q))
+				return 1;
+			if (!(q > 0.0005))
+				break;
+		}
+		/* clip pass on the kept set with the Winsorized sigma / median (:1731-1747) */
+		const double tl = sl * sigma, th = sh * sigma;
+		const double blo = median - tl, bhi = median + th;
+		const double tol = sig_e0 ? 0.0 : SGH_BAND * (fabs(median) + fabs(tl) + fabs(th) + 1.0);
+		int a = sgh_ceil_clamp(blo - tol);
+		if (a < A)
+			a = A;
+		int bt = sgh_floor_clamp(bhi + tol);
+		if (bt > B)
+			bt = B;
+		SghQ qa, qb;
+		sgh_q_load(P, a - 1, qa);
+		sgh_q_load(P, bt, qb);
+		const int cnt_a = sgh_q_count(P, qa), cnt_bt = sgh_q_count(P, qb);
+		if (!sig_e0) {
+			int amb1 = sgh_floor_clamp(blo + tol);
+			if (amb1 > B)
+				amb1 = B;
+			if (a <= amb1 && sgh_cnt_le(P, amb1) - cnt_a > 0)
+				return 1;
+			int amb0 = sgh_ceil_clamp(bhi - tol);
+			if (amb0 < A)
+				amb0 = A;
+			if (amb0 <= bt && cnt_bt - sgh_cnt_le(P, amb0 - 1) > 0)
+				return 1;
+		}
+		const int L = cnt_a - MA.c, H = MB.c - cnt_bt;
+		if (L + H > n)
+			return 1;
+		const int need = n - 4 - r;
+		int fb = -1;
+		if (need <= 0)
+			fb = 0;
+		else if (L >= need)
+			fb = need - 1;
+		else if (L + H >= need)
+			fb = (n - H) + (need - L) - 1;
+		if (fb >= 0 && fb < n - 1)
+			return 1;
+		if (L) {
+			A = a;
+			MA = sgh_q_moments(P, qa);
+		}
+		if (H) {
+			B = bt;
+			MB = sgh_q_moments(P, qb);
+		}
+		rlo += L;
+		rhi += H;
+		r += L + H;
+		nrem = L + H;
+		n -= nrem;
+	} while (nrem > 0 && n > 3);
+	const long long tot = (MB.s - MA.s) + (long long)n * P.lo;
+	*value = sg_round_to_WORD((double)tot / (double)n);
+	*rlo_out = rlo;
+	*rhi_out = rhi;
+	return SG_CLS_OK;
+}
+
 /* pixel column `col` of the tile (x its image column), lane pair half `half` */
+template <int REJ>
 __device__ void sgh_finish2(const SgStackParams &p, SghLds &L, int col, int half, int lo, int R, int c, int x,
 		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
 	const int lane = threadIdx.x & 63;
@@ -615,7 +838,10 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds &L, int col, int half
 			P.T.c = N;
 			P.T.s = (long long)s32 + P.Z.s + ds * P.ns;
 			P.T.ss = (unsigned long long)ss32 + P.Z.ss + (unsigned long long)(ds * ds) * (unsigned long long)P.ns;
-			cls = sgh_sigma2(P, N, p.sig0, p.sig1, half, &value, &rlo, &rhi);
+			if (REJ == 4)
+				cls = sgh_winsorized(P, N, p.sig0, p.sig1, &value, &rlo, &rhi);
+			else
+				cls = sgh_sigma2(P, N, p.sig0, p.sig1, half, &value, &rlo, &rhi);
 		}
 		const int64_t pix = ((int64_t)c * p.H + R) * p.W + x;
 		if (!half) {
@@ -729,6 +955,7 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, SghLds &L, con
 	}
 }
 
+template <int REJ>	/* 2 = SIGMA, 4 = WINSORIZED */
 __global__ void __launch_bounds__(64 * SGH_WAVES)
 k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
 	__shared__ SghLds L;
@@ -785,6 +1012,9 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 	 * col is held by lane col & 63 of every wave (each wave computed the centres) */
 	const int col = 32 * wave + (lane >> 1), half = lane & 1;
 	const int lo = __shfl(wave < 2 ? lo_a : lo_b, col & 63, 64);
-	sgh_finish2(p, L, col, half, lo, R, c, x0 + 2 * (col & 63) + (col >> 6), redo_count, redo_list);
+	sgh_finish2<REJ>(p, L, col, half, lo, R, c, x0 + 2 * (col & 63) + (col >> 6), redo_count, redo_list);
 }
 
+
+template __global__ void k_stack_hist<2>(SgStackParams, unsigned int *, unsigned int *);
+template __global__ void k_stack_hist<4>(SgStackParams, unsigned int *, unsigned int *);

@@ -152,24 +152,29 @@ def _stack_path(ctx, frames, rejection, sig, sx=None, sy=None, path=sg.PATH_AUTO
     return out, rej, ctx.stats()
 
 
+@pytest.mark.parametrize("rejection", [sg.SIGMA, sg.WINSORIZED])
 @pytest.mark.parametrize("N", [16, 17, 40, 128, 512])
-def test_hist_path_matches_oracle_and_sorted(gpu_ctx, N):
-    """histogram SIGMA path (sg_stack_hist.hip) == sorted path == oracle, bit for bit"""
+def test_hist_path_matches_oracle_and_sorted(gpu_ctx, N, rejection):
+    """histogram SIGMA / WINSORIZED path (sg_stack_hist.hip) == sorted path == oracle, bit
+    for bit"""
     # |shifty| < block height (4 blocks of 16 rows): the reference's heap overflow for
     # larger shifts (SURVEY a2) is not reproduced
     H, W = 64, 160
     frames = orc.synth(N, 1, H, W, seed=300 + N, maxshift=10)
     sx, sy = orc.synth_shifts(N, seed=300 + N, maxshift=10)
-    out_h, rej_h, st = _stack_path(gpu_ctx, frames, sg.SIGMA, (4.0, 3.0), sx, sy, max_thread=2)
-    out_s, rej_s, _ = _stack_path(gpu_ctx, frames, sg.SIGMA, (4.0, 3.0), sx, sy, path=sg.PATH_SORTED,
+    out_h, rej_h, st = _stack_path(gpu_ctx, frames, rejection, (4.0, 3.0), sx, sy, max_thread=2)
+    out_s, rej_s, _ = _stack_path(gpu_ctx, frames, rejection, (4.0, 3.0), sx, sy, path=sg.PATH_SORTED,
                                   max_thread=2)
-    rc, ref, rej_ref = orc.stack_rejection(frames, sg.SIGMA, sig=(4.0, 3.0), shiftx=sx, shifty=sy, max_thread=2)
+    rc, ref, rej_ref = orc.stack_rejection(frames, rejection, sig=(4.0, 3.0), shiftx=sx, shifty=sy, max_thread=2)
     assert rc == 0
     assert_same(out_h, ref, f"hist N={N}")
     assert_same(out_s, ref, f"sorted N={N}")
     assert np.array_equal(rej_h, rej_ref) and np.array_equal(rej_s, rej_ref)
-    # the fast path must carry almost every pixel (redo list = pixels re-done by the sort)
-    assert st.chain_pixels <= 0.05 * H * W, st.chain_pixels
+    # the fast path must carry almost every pixel (redo list = pixels re-done by the sort);
+    # WINSORIZED's small sigma makes the reference's early break (N - r <= 4) common at
+    # small N, and those pixels are redone by design
+    limit = 0.05 if (rejection == sg.SIGMA or N >= 40) else 0.2
+    assert st.chain_pixels <= limit * H * W, st.chain_pixels
 
 
 @pytest.mark.parametrize("shifts", [True, False])
@@ -188,8 +193,9 @@ def test_hist_path_interior_tiles(gpu_ctx, W, shifts):
     assert st.chain_pixels <= 0.05 * H * W, st.chain_pixels
 
 
+@pytest.mark.parametrize("rejection", [sg.SIGMA, sg.WINSORIZED])
 @pytest.mark.parametrize("case", ["constant", "uniform", "bimodal", "saturated", "tight_sig", "dark"])
-def test_hist_path_adversarial(gpu_ctx, case):
+def test_hist_path_adversarial(gpu_ctx, case, rejection):
     """inputs that defeat the histogram's assumptions must fall back, not differ:
     u8 bin overflow (>255 equal samples), tail overflow, medians outside the band,
     decisions on knife edges"""
@@ -211,8 +217,8 @@ def test_hist_path_adversarial(gpu_ctx, case):
     else:
         frames = rng.integers(0, 40, size=(N, 1, H, W)).astype(np.uint16)
     sig = (1.0, 0.5) if case == "tight_sig" else (4.0, 3.0)
-    out_h, rej_h, _ = _stack_path(gpu_ctx, frames, sg.SIGMA, sig)
-    rc, ref, rej_ref = orc.stack_rejection(frames, sg.SIGMA, sig=sig, max_thread=8)
+    out_h, rej_h, _ = _stack_path(gpu_ctx, frames, rejection, sig)
+    rc, ref, rej_ref = orc.stack_rejection(frames, rejection, sig=sig, max_thread=8)
     assert_same(out_h, ref, case)
     assert np.array_equal(rej_h, rej_ref), (rej_h, rej_ref)
 
