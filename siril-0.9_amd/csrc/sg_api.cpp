@@ -419,8 +419,8 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 		/* exact wave-per-pixel replay of queued SIGMA / WINSORIZED pixels (early breaks with
 		 * this pixel's own stale rejected[]), then the literal path for what remains: two
 		 * phases, grids read the count on the device */
-		if ((p.rejection == SG_SIGMA || p.rejection == SG_WINSORIZED) && N <= 2048) {
-			hipLaunchKernelGGL(k_stack_replay, dim3(1024), dim3(256), 0, s, p);
+		if ((p.rejection == SG_SIGMA || p.rejection == SG_WINSORIZED) && N <= SG_REPLAY_MAXN) {
+			hipLaunchKernelGGL(k_stack_replay, dim3(2048), dim3(64 * SG_REPLAY_WAVES), 0, s, p);
 			HIPCHK(hipGetLastError());
 			ctx->stats.launches++;
 		}

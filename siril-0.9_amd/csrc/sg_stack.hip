@@ -952,20 +952,20 @@ __device__ __forceinline__ void gather_stack(const SgStackParams &p, int64_t pix
  * array by POSITION, the `if (N - r <= 4) break;` with the entries after the break keeping
  * this pixel's previous-pass values, the order-preserving removal - but with exact
  * integer moments instead of GSL's long double sums.  Every continuous decision gets the
- * same rounding band as the sorted path; a pixel that meets an ambiguous decision, or whose
+ * same rounding band as the sorted path; a decision inside the band switches the pixel to
+ * exact mode (GSL's sd in soft fp80 on lane 0 from then on, no band).  Only a pixel whose
  * FIRST pass breaks early (its stale entries belong to the previous pixel of the OpenMP
- * thread), stays queued for k_stack_literal.  This takes the early-break pixels (e.g.
- * image-edge columns half filled by the shift zero fill under WINSORIZED) off the
- * one-thread fp80 path.  The stack is sorted once: after the first pass the removal keeps
+ * thread) stays queued for k_stack_literal.  This takes the early-break and near-tie
+ * pixels (e.g. image-edge columns half filled by the shift zero fill under WINSORIZED) off
+ * the one-thread fp80 path.  The stack is sorted once: after the first pass the removal keeps
  * it sorted, and quicksort_s of a sorted array is the identity; the Winsorized copy stays
  * sorted under clamping.
  */
-#define SG_REPLAY_MAXN 2048
-#define SG_REPLAY_WAVES 4
-
 struct SgReplayLds {
 	uint16_t stack[SG_REPLAY_MAXN];
 	uint16_t w[SG_REPLAY_MAXN];
+	uint16_t wprev[SG_REPLAY_MAXN];	/* w before the current clamp (exact-mode recomputation) */
+	uint16_t orig[SG_REPLAY_MAXN];	/* the first pass's stack in frame order */
 	int8_t rej[SG_REPLAY_MAXN];
 };
 
@@ -1038,10 +1038,25 @@ __device__ __forceinline__ double replay_median(const uint16_t *a, int n) {
 	return (double)(a[lhs] + a[rhs]) / 2.0;
 }
 
-/* returns 1 on success (value / counters set), 0 = leave the pixel to the literal path */
+/* GSL's sd (long double recurrences in soft fp80) of a[0..n), computed on lane 0 and
+ * broadcast: the reference's gsl_stats_sd, as lit_sd */
+__device__ __forceinline__ double replay_gsl_sd(const uint16_t *a, int n, int lane) {
+	double v = 0.0;
+	if (lane == 0)
+		v = lit_sd(a, n);
+	return __shfl(v, 0, 64);
+}
+
+/* returns 1 on success (value / counters set), 0 = leave the pixel to the literal path
+ * (first pass broken early, or the Winsorize guard).  Sigmas come from exact integer
+ * moments until a decision falls inside the rounding band; the pixel then switches to
+ * exact mode: that sigma and every later one is recomputed the reference's way
+ * (replay_gsl_sd, on the same array in the same order) and decisions are evaluated in the
+ * reference's double arithmetic with no band. */
 __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double sh, int lane, uint16_t *value,
 		uint32_t *rlo, uint32_t *rhi) {
 	int N = N0, r = 0, n, iter = 0;
+	bool ex = false;
 	uint32_t clo = 0, chi = 0;
 	for (int j = lane; j < N0; j += 64)
 		L.rej[j] = 0;
@@ -1051,6 +1066,14 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 		replay_moments(L.stack, N, lane, S, SS);
 		bool e0;
 		double sigma = exact_sd(N, S, SS, &e0);
+		if (iter == 1) {
+			for (int j = lane; j < N; j += 64)
+				L.orig[j] = L.stack[j];	/* frame order: the first pass's sd input */
+			__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+		}
+		const uint16_t *src = iter == 1 ? L.orig : L.stack;	/* this pass's sd input */
+		if (ex)
+			sigma = replay_gsl_sd(src, N, lane);
 		if (iter == 1)
 			replay_sort(L.stack, N, lane);
 		double median = replay_median(L.stack, N);
@@ -1059,77 +1082,111 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 				L.w[j] = L.stack[j];
 			__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 			bool sig_e0 = e0;
+			bool from_w = false;	/* sigma's input: the pass-level array, or w */
 			for (int guard = 0;; guard++) {
 				if (guard > 100000)
 					return 0;
-				const double m0 = median - 1.5 * sigma, m1 = median + 1.5 * sigma;
-				const double tol = sig_e0 ? 0.0 : SG_BAND * (fabs(median) + 1.5 * sigma + 1.0);
-				int amb = 0, clamped_lo = 0, clamped_hi = 0;
+				double m0 = median - 1.5 * sigma, m1 = median + 1.5 * sigma;
+				if (!ex) {
+					const double tol = sig_e0 ? 0.0 : SG_BAND * (fabs(median) + 1.5 * sigma + 1.0);
+					int amb = 0, clamped_lo = 0, clamped_hi = 0;
+					for (int j = lane; j < N; j += 64) {
+						const double x = (double)L.w[j];
+						if (!sig_e0 && ((x >= m0 - tol && x <= m0 + tol) || (x >= m1 - tol && x <= m1 + tol)))
+							amb = 1;
+						if (x < m0)
+							clamped_lo = 1;
+						else if (x > m1)
+							clamped_hi = 1;
+					}
+					amb = wave_or(amb);
+					clamped_lo = wave_or(clamped_lo);
+					clamped_hi = wave_or(clamped_hi);
+					if (amb || (clamped_lo && round_ambiguous(m0, tol + 1e-9 * tol)) ||
+							(clamped_hi && round_ambiguous(m1, tol + 1e-9 * tol))) {
+						ex = true;
+						sigma = from_w ? 1.134 * replay_gsl_sd(L.w, N, lane) : replay_gsl_sd(src, N, lane);
+						m0 = median - 1.5 * sigma;
+						m1 = median + 1.5 * sigma;
+					} else {
+						for (int j = lane; j < N; j += 64)
+							L.wprev[j] = L.w[j];
+					}
+				}
 				const uint16_t vlo = sg_round_to_WORD(m0), vhi = sg_round_to_WORD(m1);
 				for (int j = lane; j < N; j += 64) {
 					const double x = (double)L.w[j];
-					if (!sig_e0 && ((x >= m0 - tol && x <= m0 + tol) || (x >= m1 - tol && x <= m1 + tol)))
-						amb = 1;
-					if (x < m0) {
+					if (x < m0)
 						L.w[j] = vlo;
-						clamped_lo = 1;
-					} else if (x > m1) {
+					else if (x > m1)
 						L.w[j] = vhi;
-						clamped_hi = 1;
-					}
 				}
-				amb = wave_or(amb);
-				clamped_lo = wave_or(clamped_lo);
-				clamped_hi = wave_or(clamped_hi);
-				if (amb)
-					return 0;
-				if ((clamped_lo && round_ambiguous(m0, tol + 1e-9 * tol)) ||
-						(clamped_hi && round_ambiguous(m1, tol + 1e-9 * tol)))
-					return 0;
 				__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 				median = replay_median(L.w, N);
 				uint64_t Sw, SSw;
 				replay_moments(L.w, N, lane, Sw, SSw);
 				const double sigma0 = sigma;
 				const bool e00 = sig_e0;
+				const bool prev_from_w = from_w;
 				bool we0;
-				sigma = 1.134 * exact_sd(N, Sw, SSw, &we0);
+				const double sw = exact_sd(N, Sw, SSw, &we0);
 				sig_e0 = we0;
+				from_w = true;
+				if (ex) {
+					sigma = 1.134 * replay_gsl_sd(L.w, N, lane);
+					if (!((fabs(sigma - sigma0) / sigma0) > 0.0005))
+						break;
+					continue;
+				}
+				sigma = 1.134 * sw;
 				if (e00) {
 					if (we0)
 						break;	/* 0/0 = NaN: the loop exits */
 					continue;	/* x/0 = inf > 0.0005 */
 				}
 				const double q = fabs(sigma - sigma0) / sigma0;
-				if (fabs(q - 0.0005) <= 1e-9 * 0.0005 + SG_BAND * (1.0 + q))
-					return 0;
+				if (fabs(q - 0.0005) <= 1e-9 * 0.0005 + SG_BAND * (1.0 + q)) {
+					ex = true;
+					const double s0 = prev_from_w ? 1.134 * replay_gsl_sd(L.wprev, N, lane)
+								      : replay_gsl_sd(src, N, lane);
+					sigma = 1.134 * replay_gsl_sd(L.w, N, lane);
+					if (!((fabs(sigma - s0) / s0) > 0.0005))
+						break;
+					continue;
+				}
 				if (!(q > 0.0005))
 					break;
 			}
 			e0 = sig_e0;
 		}
 		/* decisions, frame order, with the early break */
-		const double tl = sl * sigma, th = sh * sigma;
-		const double blo = median - tl, bhi = median + th;
-		const double tol = e0 ? 0.0 : SG_BAND * (fabs(median) + fabs(tl) + fabs(th) + 1.0);
 		const int per = (N + 63) / 64, j0 = lane * per;
-		int amb = 0, cnt = 0;
+		int cnt = 0;
 		int8_t d[SG_REPLAY_MAXN / 64];
-#pragma unroll 4
-		for (int k = 0; k < per; k++) {
-			const int j = j0 + k;
-			int8_t v = 0;
-			if (j < N) {
-				const double x = (double)L.stack[j];
-				if (!e0 && ((x >= blo - tol && x <= blo + tol) || (x >= bhi - tol && x <= bhi + tol)))
-					amb = 1;
-				v = (median - x > tl) ? -1 : ((x - median > th) ? 1 : 0);
+		for (int attempt = 0; attempt < 2; attempt++) {
+			const double tl = sl * sigma, th = sh * sigma;
+			const double blo = median - tl, bhi = median + th;
+			const double tol = (e0 || ex) ? 0.0 : SG_BAND * (fabs(median) + fabs(tl) + fabs(th) + 1.0);
+			int amb = 0;
+			cnt = 0;
+			for (int k = 0; k < per; k++) {
+				const int j = j0 + k;
+				int8_t v = 0;
+				if (j < N) {
+					const double x = (double)L.stack[j];
+					if (tol > 0.0 && ((x >= blo - tol && x <= blo + tol) || (x >= bhi - tol && x <= bhi + tol)))
+						amb = 1;
+					v = (median - x > tl) ? -1 : ((x - median > th) ? 1 : 0);
+				}
+				d[k] = v;
+				cnt += v != 0;
 			}
-			d[k] = v;
-			cnt += v != 0;
+			if (!wave_or(amb))
+				break;
+			/* recompute this pass's sigma the reference's way and decide again, exactly */
+			ex = true;
+			sigma = type == 4 ? 1.134 * replay_gsl_sd(L.w, N, lane) : replay_gsl_sd(src, N, lane);
 		}
-		if (wave_or(amb))
-			return 0;
 		/* first frame fb with N - (r + #rejections in [0, fb]) <= 4 */
 		const int before = wave_excl_scan(cnt, lane);
 		int fb_lane = N;
