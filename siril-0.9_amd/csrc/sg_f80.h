@@ -245,12 +245,48 @@ F80_HD sg_f80 f80_div(sg_f80 a, sg_f80 b) {
 	return r;
 }
 
+/* a / d for an integer 1 <= d < 2^20, rounded exactly as f80_div(a, f80_from_u64(d)).
+ * Long division of the 128-bit a.m * 2^64 by d in 32-bit digits: the remainder stays
+ * below d, so every partial dividend rem * 2^32 + digit is below 2^52 and exact in a
+ * double; the double quotient digit is off by at most one and is corrected from the
+ * integer remainder.  Four steps instead of f80_div's 65-step restoring loop. */
+F80_HD sg_f80 f80_div_u32(sg_f80 a, uint32_t d) {
+	if (!a.m) return f80_zero();
+	const uint64_t dg[4] = {a.m >> 32, a.m & 0xFFFFFFFFull, 0, 0};
+	uint64_t q[4], rem = 0;
+	for (int k = 0; k < 4; k++) {
+		const uint64_t x = (rem << 32) | dg[k];
+		int64_t qk = (int64_t)((double)x / (double)d);
+		int64_t r = (int64_t)x - qk * (int64_t)d;
+		if (r < 0) {
+			qk--;
+			r += d;
+		} else if (r >= (int64_t)d) {
+			qk++;
+			r -= d;
+		}
+		q[k] = (uint64_t)qk;
+		rem = (uint64_t)r;
+	}
+	uint64_t hi = (q[0] << 32) | q[1], lo = (q[2] << 32) | q[3];
+	const int sh = f80_clz64(hi);	/* hi = floor(a.m / d) >= 2^43 */
+	if (sh > 0) {
+		hi = (hi << sh) | (lo >> (64 - sh));
+		lo <<= sh;
+	}
+	return f80_round128(hi, lo, rem != 0, a.e - sh, a.s);
+}
+
+F80_HD sg_f80 f80_div_count(sg_f80 a, uint64_t d) {
+	return d < (1u << 20) ? f80_div_u32(a, (uint32_t)d) : f80_div(a, f80_from_u64(d));
+}
+
 /* gsl_stats_ushort_mean / sd restated on sg_f80 (see or_core.c for the algorithm) */
 F80_HD double f80_gsl_mean_u16(const uint16_t *data, int n) {
 	sg_f80 mean = f80_zero();
 	for (int i = 0; i < n; i++) {
 		sg_f80 t = f80_sub(f80_from_u64(data[i]), mean);
-		t = f80_div(t, f80_from_u64((uint64_t)i + 1));
+		t = f80_div_count(t, (uint64_t)i + 1);
 		mean = f80_add(mean, t);
 	}
 	return f80_to_double(mean);
@@ -262,7 +298,7 @@ F80_HD double f80_gsl_variance_m_u16(const uint16_t *data, int n, double mean) {
 		double dd = (double)data[i] - mean;	/* formed in double, as in GSL */
 		sg_f80 delta = f80_from_double(dd);
 		sg_f80 t = f80_sub(f80_mul(delta, delta), var);
-		t = f80_div(t, f80_from_u64((uint64_t)i + 1));
+		t = f80_div_count(t, (uint64_t)i + 1);
 		var = f80_add(var, t);
 	}
 	return f80_to_double(var);

@@ -1048,15 +1048,16 @@ __device__ __forceinline__ double replay_gsl_sd(const uint16_t *a, int n, int la
 }
 
 /* returns 1 on success (value / counters set), 0 = leave the pixel to the literal path
- * (first pass broken early, or the Winsorize guard).  Sigmas come from exact integer
- * moments until a decision falls inside the rounding band; the pixel then switches to
- * exact mode: that sigma and every later one is recomputed the reference's way
- * (replay_gsl_sd, on the same array in the same order) and decisions are evaluated in the
- * reference's double arithmetic with no band. */
+ * (first pass broken early, or the Winsorize guard).  Each sigma comes from exact integer
+ * moments; when a decision that uses it falls inside the rounding band, that sigma is
+ * recomputed the reference's way (replay_gsl_sd, on the same array in the same order) and
+ * the decision is evaluated in the reference's double arithmetic with no band (`sx`: the
+ * current sigma is the reference's own value).  Every sigma is a function of an integer
+ * array, and the arrays depend on earlier sigmas only through discrete decisions, so the
+ * next sigma starts from exact moments again. */
 __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double sh, int lane, uint16_t *value,
 		uint32_t *rlo, uint32_t *rhi) {
 	int N = N0, r = 0, n, iter = 0;
-	bool ex = false;
 	uint32_t clo = 0, chi = 0;
 	for (int j = lane; j < N0; j += 64)
 		L.rej[j] = 0;
@@ -1066,14 +1067,13 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 		replay_moments(L.stack, N, lane, S, SS);
 		bool e0;
 		double sigma = exact_sd(N, S, SS, &e0);
+		bool sx = false;
 		if (iter == 1) {
 			for (int j = lane; j < N; j += 64)
 				L.orig[j] = L.stack[j];	/* frame order: the first pass's sd input */
 			__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 		}
 		const uint16_t *src = iter == 1 ? L.orig : L.stack;	/* this pass's sd input */
-		if (ex)
-			sigma = replay_gsl_sd(src, N, lane);
 		if (iter == 1)
 			replay_sort(L.stack, N, lane);
 		double median = replay_median(L.stack, N);
@@ -1087,7 +1087,7 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 				if (guard > 100000)
 					return 0;
 				double m0 = median - 1.5 * sigma, m1 = median + 1.5 * sigma;
-				if (!ex) {
+				if (!sx) {
 					const double tol = sig_e0 ? 0.0 : SG_BAND * (fabs(median) + 1.5 * sigma + 1.0);
 					int amb = 0, clamped_lo = 0, clamped_hi = 0;
 					for (int j = lane; j < N; j += 64) {
@@ -1104,14 +1104,15 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 					clamped_hi = wave_or(clamped_hi);
 					if (amb || (clamped_lo && round_ambiguous(m0, tol + 1e-9 * tol)) ||
 							(clamped_hi && round_ambiguous(m1, tol + 1e-9 * tol))) {
-						ex = true;
+						sx = true;
 						sigma = from_w ? 1.134 * replay_gsl_sd(L.w, N, lane) : replay_gsl_sd(src, N, lane);
 						m0 = median - 1.5 * sigma;
 						m1 = median + 1.5 * sigma;
-					} else {
-						for (int j = lane; j < N; j += 64)
-							L.wprev[j] = L.w[j];
 					}
+				}
+				if (!sx && from_w) {
+					for (int j = lane; j < N; j += 64)
+						L.wprev[j] = L.w[j];	/* sigma's input, for a later recomputation */
 				}
 				const uint16_t vlo = sg_round_to_WORD(m0), vhi = sg_round_to_WORD(m1);
 				for (int j = lane; j < N; j += 64) {
@@ -1126,19 +1127,12 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 				uint64_t Sw, SSw;
 				replay_moments(L.w, N, lane, Sw, SSw);
 				const double sigma0 = sigma;
-				const bool e00 = sig_e0;
-				const bool prev_from_w = from_w;
+				const bool e00 = sig_e0, s0x = sx, prev_from_w = from_w;
 				bool we0;
-				const double sw = exact_sd(N, Sw, SSw, &we0);
+				sigma = 1.134 * exact_sd(N, Sw, SSw, &we0);
 				sig_e0 = we0;
+				sx = false;
 				from_w = true;
-				if (ex) {
-					sigma = 1.134 * replay_gsl_sd(L.w, N, lane);
-					if (!((fabs(sigma - sigma0) / sigma0) > 0.0005))
-						break;
-					continue;
-				}
-				sigma = 1.134 * sw;
 				if (e00) {
 					if (we0)
 						break;	/* 0/0 = NaN: the loop exits */
@@ -1146,10 +1140,11 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 				}
 				const double q = fabs(sigma - sigma0) / sigma0;
 				if (fabs(q - 0.0005) <= 1e-9 * 0.0005 + SG_BAND * (1.0 + q)) {
-					ex = true;
-					const double s0 = prev_from_w ? 1.134 * replay_gsl_sd(L.wprev, N, lane)
-								      : replay_gsl_sd(src, N, lane);
+					const double s0 = s0x ? sigma0
+							      : prev_from_w ? 1.134 * replay_gsl_sd(L.wprev, N, lane)
+									    : replay_gsl_sd(src, N, lane);
 					sigma = 1.134 * replay_gsl_sd(L.w, N, lane);
+					sx = true;
 					if (!((fabs(sigma - s0) / s0) > 0.0005))
 						break;
 					continue;
@@ -1166,7 +1161,7 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 		for (int attempt = 0; attempt < 2; attempt++) {
 			const double tl = sl * sigma, th = sh * sigma;
 			const double blo = median - tl, bhi = median + th;
-			const double tol = (e0 || ex) ? 0.0 : SG_BAND * (fabs(median) + fabs(tl) + fabs(th) + 1.0);
+			const double tol = (e0 || sx) ? 0.0 : SG_BAND * (fabs(median) + fabs(tl) + fabs(th) + 1.0);
 			int amb = 0;
 			cnt = 0;
 			for (int k = 0; k < per; k++) {
@@ -1184,7 +1179,7 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 			if (!wave_or(amb))
 				break;
 			/* recompute this pass's sigma the reference's way and decide again, exactly */
-			ex = true;
+			sx = true;
 			sigma = type == 4 ? 1.134 * replay_gsl_sd(L.w, N, lane) : replay_gsl_sd(src, N, lane);
 		}
 		/* first frame fb with N - (r + #rejections in [0, fb]) <= 4 */

@@ -211,6 +211,19 @@ int main(void) {
         if (gm != m || gv != v) { bad++; if (bad < 5) printf("n=%d mean %.17g %.17g var %.17g %.17g\n", n, m, gm, v, gv); }
         free(d);
     }
+    /* the small-integer divider against the general one and native long double */
+    for (int t = 0; t < 200000; t++) {
+        sg_f80 a = {rnd() | (1ull << 63), (int32_t)(rnd() % 64) - 32, (int32_t)(rnd() & 1)};
+        uint32_t d = t % 4 == 0 ? (uint32_t)(rnd() % ((1u << 20) - 1)) + 1 : (uint32_t)(rnd() % 4096) + 1;
+        sg_f80 x = f80_div_u32(a, d), y = f80_div(a, f80_from_u64(d));
+        long double la = ldexpl((long double)a.m, a.e - 63) * (a.s ? -1 : 1);
+        long double lq = la / (long double)d;
+        long double lx = ldexpl((long double)x.m, x.e - 63) * (x.s ? -1 : 1);
+        if (x.m != y.m || x.e != y.e || x.s != y.s || lx != lq) {
+            bad++;
+            if (bad < 5) printf("div %llx e%d / %u\n", (unsigned long long)a.m, a.e, d);
+        }
+    }
     printf("bad=%d\n", bad);
     return bad != 0;
 }
