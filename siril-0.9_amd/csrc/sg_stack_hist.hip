@@ -615,45 +615,60 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint
 		bool e0;
 		double sigma = sgh_sd_rel(n, S, SS, &e0);
 		const int g1 = MA.c + (n - 1) / 2, g2 = MA.c + n / 2;
-		int m1, m2;
-		sgh_value_at2(P, g1, g2, m1, m2);
-		double median = (g1 == g2) ? (double)m1 : (double)(m1 + m2) / 2.0;
-		/* inner loop */
+		int km1, km2;	/* kept values at the median ranks: fixed for the whole pass */
+		sgh_value_at2(P, g1, g2, km1, km2);
+		double median = (g1 == g2) ? (double)km1 : (double)(km1 + km2) / 2.0;
+		/* inner loop.  The inner part of w is the kept ranks [Lw, n - Hw); its smallest and
+		 * largest values (ulo, uhi) change only when a clamp grows, so a threshold outside
+		 * [ulo, uhi] - the common case once the clamps have settled - is counted without a
+		 * histogram query, and the median of w is vlo, vhi or km1 / km2 */
 		int Lw = 0, Hw = 0, vlo = 0, vhi = 0, IA = A, IB = B;
 		SghM MIA = MA, MIB = MB;
+		int ulo = sgh_value_at1(P, MA.c), uhi = sgh_value_at1(P, MA.c + n - 1);
 		bool sig_e0 = e0;
 		for (int guard = 0;; guard++) {
 			if (guard > 4096)
 				return 1;
 			const double m0 = median - 1.5 * sigma, m1d = median + 1.5 * sigma;
 			const double tol = sig_e0 ? 0.0 : SGH_BAND * (fabs(median) + 1.5 * sigma + 1.0);
-			/* w elements < thr / <= thr */
-			auto w_lt = [&](double thr) {
-				int c = (Lw && (double)vlo < thr) ? Lw : 0;
-				int k = sgh_cnt_lt(P, thr);
-				k = k < MIA.c ? MIA.c : (k > MIB.c ? MIB.c : k);
-				c += k - MIA.c;
-				if (Hw && (double)vhi < thr)
+			const int nin = n - Lw - Hw;
+			/* # w elements <= v (integer v in [-1, 65535]); "< thr" is "<= ceil(thr) - 1" and
+			 * "<= thr" is "<= floor(thr)", so both sides of a rounding band usually name the
+			 * same v and one count serves both */
+			auto w_le = [&](int v) {
+				int c = (Lw && vlo <= v) ? Lw : 0;
+				if (nin > 0 && v >= ulo) {
+					if (v >= uhi) {
+						c += nin;
+					} else {
+						int k = sgh_cnt_le(P, v);
+						k = k < MIA.c ? MIA.c : (k > MIB.c ? MIB.c : k);
+						c += k - MIA.c;
+					}
+				}
+				if (Hw && vhi <= v)
 					c += Hw;
 				return c;
 			};
-			auto w_le = [&](double thr) {
-				int c = (Lw && (double)vlo <= thr) ? Lw : 0;
-				int k = sgh_cnt_le_d(P, thr);
-				k = k < MIA.c ? MIA.c : (k > MIB.c ? MIB.c : k);
-				c += k - MIA.c;
-				if (Hw && (double)vhi <= thr)
-					c += Hw;
-				return c;
+			auto v_lt = [](double thr) {
+				const double c = ceil(thr) - 1.0;
+				return c < -1.0 ? -1 : (c > 65535.0 ? 65535 : (int)c);
 			};
-			const int clo = w_lt(m0 - tol);
-			if (!sig_e0 && clo != w_le(m0 + tol))
+			auto v_le = [](double thr) {
+				const double c = floor(thr);
+				return c < -1.0 ? -1 : (c > 65535.0 ? 65535 : (int)c);
+			};
+			const int a1 = v_lt(m0 - tol), a2 = v_le(m0 + tol);
+			const int b1 = v_le(m1d + tol), b2 = v_lt(m1d - tol);
+			const int clo = w_le(a1);
+			if (!sig_e0 && a2 != a1 && clo != w_le(a2))
 				return 1;
-			const int chi = n - w_le(m1d + tol);
-			if (!sig_e0 && chi != n - w_lt(m1d - tol))
+			const int chi = n - w_le(b1);
+			if (!sig_e0 && b2 != b1 && chi != n - w_le(b2))
 				return 1;
 			if (clo + chi > n)
 				return 1;
+			bool grew_lo = false, grew_hi = false;
 			if (clo > 0) {
 				if (sgh_round_ambiguous(m0, tol + 1e-9 * tol))
 					return 1;
@@ -664,6 +679,7 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint
 					double c = ceil(m0 - tol);
 					IA = c < 0.0 ? 0 : (c > 65536.0 ? 65536 : (int)c);
 					MIA = sgh_M_le(P, IA - 1);
+					grew_lo = true;
 				}
 				Lw = clo;
 				vlo = sg_round_to_WORD(m0);
@@ -677,23 +693,25 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint
 					double c = floor(m1d + tol);
 					IB = c < -1.0 ? -1 : (c > 65535.0 ? 65535 : (int)c);
 					MIB = sgh_M_le(P, IB);
+					grew_hi = true;
 				}
 				Hw = chi;
 				vhi = sg_round_to_WORD(m1d);
 			}
 			if (MIB.c - MIA.c != n - Lw - Hw)
 				return 1;	/* inner part and clamp counts disagree: leave it to the sorted path */
-			/* median of w */
+			if (n - Lw - Hw > 0) {
+				if (grew_lo)
+					ulo = sgh_value_at1(P, MA.c + Lw);
+				if (grew_hi)
+					uhi = sgh_value_at1(P, MA.c + n - Hw - 1);
+			}
+			/* median of w: the kept values at the median ranks unless clamped */
 			{
 				const int lhs = (n - 1) / 2, rhs = n / 2;
-				auto wat = [&](int i) {
-					if (i < Lw)
-						return vlo;
-					if (i >= n - Hw)
-						return vhi;
-					return sgh_value_at1(P, MA.c + i);
-				};
-				median = (lhs == rhs) ? (double)wat(lhs) : (double)(wat(lhs) + wat(rhs)) / 2.0;
+				const int wl = lhs < Lw ? vlo : (lhs >= n - Hw ? vhi : km1);
+				const int wr = rhs < Lw ? vlo : (rhs >= n - Hw ? vhi : km2);
+				median = (lhs == rhs) ? (double)wl : (double)(wl + wr) / 2.0;
 			}
 			const long long dl = (long long)vlo - P.lo, dh = (long long)vhi - P.lo;
 			const long long Sw = (MIB.s - MIA.s) + dl * Lw + dh * Hw;
@@ -774,8 +792,9 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint
 	return SG_CLS_OK;
 }
 
-/* pixel column `col` of the tile (x its image column), lane pair half `half` */
-template <int REJ>
+/* pixel column `col` of the tile (x its image column); PAIR: lane pair half `half`, else one
+ * lane per column (half = 0) */
+template <int REJ, bool PAIR>
 __device__ void sgh_finish2(const SgStackParams &p, SghLds &L, int col, int half, int lo, int R, int c, int x,
 		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
 	const int lane = threadIdx.x & 63;
@@ -786,11 +805,12 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds &L, int col, int half
 			p.out[((int64_t)c * p.H + R) * p.W + x] = (uint16_t)(hc[0] + L.nz[col]);
 		return;
 	}
-	/* prefix: this lane's 4 groups, then the partner's 4 */
-	uint32_t gc[SGH_NGRP / 2], gs[SGH_NGRP / 2], gss[SGH_NGRP / 2];
+	/* prefix: this lane's 4 groups, then the partner's 4 (PAIR), or all 8 */
+	constexpr int NG = PAIR ? SGH_NGRP / 2 : SGH_NGRP;
+	uint32_t gc[NG], gs[NG], gss[NG];
 #pragma unroll
-	for (int k = 0; k < SGH_NGRP / 2; k++) {
-		const int g = (SGH_NGRP / 2) * half + k;
+	for (int k = 0; k < NG; k++) {
+		const int g = PAIR ? (SGH_NGRP / 2) * half + k : k;
 		uint32_t d[SGH_GRP], cc = 0, s = 0, ss = 0;
 #pragma unroll
 		for (int j = 0; j < SGH_GRP; j++)
@@ -805,15 +825,21 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds &L, int col, int half
 	uint32_t cum = 0, s32 = 0, ss32 = 0;
 #pragma unroll
 	for (int g = 0; g < SGH_NGRP; g++) {
-		const int k = g % (SGH_NGRP / 2);
-		const bool mine = (g >= SGH_NGRP / 2) == (half != 0);
-		const uint32_t oc = sgh_x(gc[k]), os = sgh_x(gs[k]), oss = sgh_x(gss[k]);
 		P.pc[g] = cum;
 		P.ps[g] = s32;
 		P.pss[g] = ss32;
-		cum += mine ? gc[k] : oc;
-		s32 += mine ? gs[k] : os;
-		ss32 += mine ? gss[k] : oss;
+		if constexpr (PAIR) {
+			const int k = g % (SGH_NGRP / 2);
+			const bool mine = (g >= SGH_NGRP / 2) == (half != 0);
+			const uint32_t oc = sgh_x(gc[k]), os = sgh_x(gs[k]), oss = sgh_x(gss[k]);
+			cum += mine ? gc[k] : oc;
+			s32 += mine ? gs[k] : os;
+			ss32 += mine ? gss[k] : oss;
+		} else {
+			cum += gc[g];
+			s32 += gs[g];
+			ss32 += gss[g];
+		}
 	}
 	const int oob = (int)hc[64 * SGH_DW];
 	P.lo = lo;
@@ -1008,11 +1034,21 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 		atomicAdd(&L.ns[64 + lane], nsat >> 16);
 	}
 	__syncthreads();
+	if (REJ == 4) {
+		/* WINSORIZED: the finish is VALU-bound and both lanes of a pair would run the same
+		 * loop, so waves 0 / 1 take one pixel column per lane (the even / odd image columns)
+		 * and waves 2 / 3 leave their SIMD slots to other tiles */
+		if (wave >= 2)
+			return;
+		sgh_finish2<REJ, false>(p, L, 64 * wave + lane, 0, wave ? lo_b : lo_a, R, c, x0 + 2 * lane + wave,
+				redo_count, redo_list);
+		return;
+	}
 	/* every wave finishes 32 pixel columns, a lane pair per column; the band start of column
 	 * col is held by lane col & 63 of every wave (each wave computed the centres) */
 	const int col = 32 * wave + (lane >> 1), half = lane & 1;
 	const int lo = __shfl(wave < 2 ? lo_a : lo_b, col & 63, 64);
-	sgh_finish2<REJ>(p, L, col, half, lo, R, c, x0 + 2 * (col & 63) + (col >> 6), redo_count, redo_list);
+	sgh_finish2<REJ, true>(p, L, col, half, lo, R, c, x0 + 2 * (col & 63) + (col >> 6), redo_count, redo_list);
 }
 
 
