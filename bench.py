@@ -40,6 +40,9 @@ def parse():
     ap.add_argument("--height", type=int, default=4096)
     ap.add_argument("--rejection", default="sigma")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--normalize", choices=["none", "additive-scaling", "multiplicative-scaling"], default="none",
+                    help="sigma workload: per-frame normalisation (synthetic location / scale, as "
+                         "compute_normalization derives them)")
     ap.add_argument("--maxshift", type=int, default=16, help="synthetic registration shift range")
     ap.add_argument("--even-shifts", action="store_true",
                     help="A/B only: round x shifts down to even (4-byte aligned pixel-pair loads)")
@@ -206,6 +209,7 @@ def main():
     args = parse()
     if args.workload != "sigma":
         return main_config(args)
+    import numpy as np
     import torch
     import sirilgpu as sg
 
@@ -236,8 +240,25 @@ def main():
         shx &= ~1
     if args.zero_shift:
         (shx if args.zero_shift == "x" else shy)[:] = 0
+    norm_mode, off, mul, scale = sg.NO_NORM, None, None, None
+    if args.normalize != "none":
+        # synthetic per-frame location / scale (the cached IKSS statistics), coefficients as
+        # compute_normalization (src/stacking/stacking.c:79-190) forms them, reference frame 0
+        # (the synthetic frames share one background, so their statistics differ only by noise)
+        i = np.arange(N, dtype=np.float64)
+        loc = 1000.0 + 0.6 * np.sin(0.37 * i)
+        scl = 30.0 + 0.3 * np.cos(0.23 * i)
+        if args.normalize == "additive-scaling":
+            norm_mode = sg.ADDITIVE_SCALING
+            scale = scl[0] / scl
+            off = scale * loc - loc[0]
+        else:
+            norm_mode = sg.MULTIPLICATIVE_SCALING
+            scale = scl[0] / scl
+            mul = loc[0] / loc
     desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=rej_mode, sig=(4.0, 3.0),
-                              shiftx=shx, shifty=shy, max_thread=8, max_number_of_rows=H)
+                              shiftx=shx, shifty=shy, normalize=norm_mode, offset=off, mul=mul, scale=scale,
+                              max_thread=8, max_number_of_rows=H)
 
     def step():
         return ctx.stack_device(desc, frames.data_ptr(), fstride, H * W, out.data_ptr(), 0, H)
@@ -288,8 +309,9 @@ def main():
             "data": "synthetic (include/sg_synth.h, generated in HBM)",
             "config": {"workload": f"sigma-clip stack {N}x{H}x{W} u16 mono per GPU (BASELINE configs[2])",
                        "frames": N, "height": H, "width": W, "rejection": args.rejection,
-                       "sig": [4.0, 3.0], "parallelism": f"row-band x{world}"},
-            "roofline": roofline(achieved, algo_bytes, N, H, W, args.rejection),
+                       "sig": [4.0, 3.0], "normalize": args.normalize, "parallelism": f"row-band x{world}"},
+            "roofline": roofline(achieved, algo_bytes, N, H, W, args.rejection
+                                 if args.normalize == "none" else f"{args.rejection}_{args.normalize}"),
             "kernel_ms": round(kavg, 3),
             "slow_pixels": int(slow),
             "redo_pixels": int(redo),

@@ -120,7 +120,7 @@ typedef struct {
 	uint64_t chain_pixels;	/* pixels needing the cross-pixel stale-state replay */
 	uint64_t launches;	/* kernels launched by the main path */
 	int main_kernel_blocks;
-	int reserved;
+	int path;		/* main path of a MEAN stack: 1 = histogram (k_stack_hist), 0 = other */
 } sg_stack_stats;
 int sg_get_last_stats(const sg_ctx *ctx, sg_stack_stats *st);
 

@@ -26,7 +26,7 @@ struct SgChainTables {
 
 template <int NREG, bool LISTED>
 __global__ void k_stack_sorted(SgStackParams p, const unsigned int *list, const unsigned int *list_count);
-template <int REJ>
+template <int REJ, int NORM>
 __global__ void k_stack_hist(SgStackParams p, unsigned int *redo_count, unsigned int *redo_list);
 void sg_dbg_why_dump(hipStream_t s);
 __global__ void k_stack_replay(SgStackParams p);
@@ -261,7 +261,7 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 	const int Npad = (N + 15) & ~15;	/* histogram-path table: 64-byte aligned, padded */
 	/* layout: c1[Npad] int, sx2[Npad] int16, shiftx[N], shifty[N] */
 	HIPCHK(ensure(dv.shifts, sizeof(int) * (Npad + Npad / 2 + 2 * N)));
-	HIPCHK(ensure(dv.norm, sizeof(double) * 3 * N));
+	HIPCHK(ensure(dv.norm, sizeof(double) * (3 * N + 2 * Npad)));
 	/* the histogram path addresses a frame plane with 32-bit offsets: (R - sy) W 2 must fit */
 	bool hist_addr_ok = (int64_t)H * W * 2 <= (1ll << 30);
 	{
@@ -299,7 +299,16 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 			nm[N + i] = d->mul ? d->mul[i] : 1.0;
 			nm[2 * N + i] = d->scale ? d->scale[i] : 1.0;
 		}
-		HIPCHK(hipMemcpyAsync(dv.norm.p, nm.data(), sizeof(double) * 3 * N, hipMemcpyHostToDevice, s));
+		/* the histogram path's per-frame pair {scale, offset} (additive) or {scale, mul}
+		 * (multiplicative), read with one scalar load per frame */
+		const bool additive = p.normalize == SG_ADDITIVE || p.normalize == SG_ADDITIVE_SCALING;
+		nm.resize(3 * N + 2 * Npad, 0.0);
+		for (int i = 0; i < N; i++) {
+			nm[3 * N + 2 * i] = nm[2 * N + i];
+			nm[3 * N + 2 * i + 1] = additive ? nm[i] : nm[N + i];
+		}
+		HIPCHK(hipMemcpyAsync(dv.norm.p, nm.data(), sizeof(double) * nm.size(), hipMemcpyHostToDevice, s));
+		p.hist_norm = (const double *)dv.norm.p + 3 * N;
 		p.offset = (const double *)dv.norm.p;
 		p.mul = p.offset + N;
 		p.scale = p.offset + 2 * N;
@@ -368,11 +377,11 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 		const int ntx = (W + SG_TILE_W - 1) / SG_TILE_W;
 		const size_t nblk = (size_t)ntx * nrows * C;
 		const size_t lds = (size_t)N * SG_STAGE_STRIDE * 2;
-		/* histogram fast path (sg_stack_hist.hip): SIGMA, no normalisation, N >= 16 */
+		/* histogram fast path (sg_stack_hist.hip): SIGMA / WINSORIZED, any normalisation, N >= 16 */
 		const int path = d->kernel_path;
 		const bool hist = path != SG_PATH_SORTED && d->method == SG_STACK_MEAN &&
 			(d->rejection == SG_SIGMA || d->rejection == SG_WINSORIZED) &&
-			p.normalize == 0 && N >= 16 && hist_addr_ok;
+			N >= 16 && hist_addr_ok;
 		if (hist) {
 			HIPCHK(ensure(dv.redo, sizeof(unsigned int) * (npix_launch + 16)));
 			unsigned int *redo_count = (unsigned int *)dv.redo.p;
@@ -383,25 +392,33 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 			const char *pad = getenv("SG_HIST_LDSPAD");	/* A/B: extra LDS per workgroup (occupancy) */
 			if (p.dbg == 14) {	/* A/B: report the resident workgroups per CU */
 				int per_cu = -1;
-				(void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_stack_hist<2>, 256,
+				(void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_stack_hist<2, 0>, 256,
 						pad ? (size_t)atoi(pad) : 0);
 				hipDeviceProp_t prop;
 				(void)hipGetDeviceProperties(&prop, dv.id);
 				fprintf(stderr, "k_stack_hist: %d workgroups/CU (lds/CU %zu, lds/block max %zu, pad %s)\n", per_cu,
 						(size_t)prop.maxSharedMemoryPerMultiProcessor, (size_t)prop.sharedMemPerBlock, pad ? pad : "0");
 			}
-			if (p.rejection == SG_WINSORIZED)
-				hipLaunchKernelGGL(k_stack_hist<4>, dim3((unsigned)nblk_h), dim3(256), pad ? (size_t)atoi(pad) : 0, s,
-						p, redo_count, redo_list);
-			else
-				hipLaunchKernelGGL(k_stack_hist<2>, dim3((unsigned)nblk_h), dim3(256), pad ? (size_t)atoi(pad) : 0, s,
-						p, redo_count, redo_list);
+			/* NORM: 0 none, 1 additive (round(v scale - offset)), 2 multiplicative (round(v scale mul)) */
+			const int norm = p.normalize == SG_NO_NORM ? 0 :
+				(p.normalize == SG_ADDITIVE || p.normalize == SG_ADDITIVE_SCALING) ? 1 : 2;
+			const size_t lds_pad = pad ? (size_t)atoi(pad) : 0;
+			const dim3 hg((unsigned)nblk_h), hb(256);
+			switch ((p.rejection == SG_WINSORIZED ? 10 : 0) + norm) {
+			case 0: hipLaunchKernelGGL((k_stack_hist<2, 0>), hg, hb, lds_pad, s, p, redo_count, redo_list); break;
+			case 1: hipLaunchKernelGGL((k_stack_hist<2, 1>), hg, hb, lds_pad, s, p, redo_count, redo_list); break;
+			case 2: hipLaunchKernelGGL((k_stack_hist<2, 2>), hg, hb, lds_pad, s, p, redo_count, redo_list); break;
+			case 10: hipLaunchKernelGGL((k_stack_hist<4, 0>), hg, hb, lds_pad, s, p, redo_count, redo_list); break;
+			case 11: hipLaunchKernelGGL((k_stack_hist<4, 1>), hg, hb, lds_pad, s, p, redo_count, redo_list); break;
+			default: hipLaunchKernelGGL((k_stack_hist<4, 2>), hg, hb, lds_pad, s, p, redo_count, redo_list); break;
+			}
 			HIPCHK(hipGetLastError());
 			HIPCHK(hipEventRecord(dv.ev[1], s));
 			unsigned int nredo = 0;
 			HIPCHK(hipMemcpyAsync(&nredo, redo_count, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
 			HIPCHK(hipStreamSynchronize(s));
 			ctx->stats.chain_pixels = nredo;
+			ctx->stats.path = 1;
 			ctx->stats.main_kernel_blocks = (int)nblk;
 			ctx->stats.launches = 1;
 			if (nredo) {

@@ -29,6 +29,7 @@ struct SgStackParams {
 	const int *hist_tab;			/* device: c1[hist_npad] = shifty*W*2 + 2*shiftx, then int16 sx2[hist_npad] = 2*shiftx */
 	int hist_npad;				/* N rounded up to a multiple of 16 */
 	int hist_maxsx;				/* max |shiftx| (interior-tile test of the histogram path) */
+	const double *hist_norm;		/* device: {scale, offset | mul} per frame (hist_npad pairs), normalised stacks */
 	const double *offset, *mul, *scale;	/* device [N] or null */
 	int row_begin, row_end;			/* memory rows to compute */
 	unsigned long long *rej;		/* [SG_REJ_SHARDS][3][2] */

@@ -365,7 +365,7 @@ __device__ __forceinline__ void sgh_loadblk(const SghFrame &F, const SghTab16 &T
 			const uint32_t sca = F.xa2 - (uint32_t)sx2;
 			const bool bada = sca >= (uint32_t)F.w2, badb = sca + 2u >= (uint32_t)F.w2;
 			off = bada ? (badb ? 0x80000000u : off + 2u) : (badb ? off - 2u : off);
-			fix |= ((bada && !badb) ? 1u : ((!bada && badb) ? 2u : 0u)) << (2 * m);
+			fix |= ((bada && !badb) ? 1u : ((!bada && badb) ? 2u : ((bada && badb) ? 3u : 0u))) << (2 * m);
 		}
 		dst[m] = __builtin_amdgcn_raw_buffer_load_b32(sgh_rsrc(b, nrec), (int)off, 0, 0);
 		b += F.fstride2;
@@ -378,6 +378,40 @@ __device__ __forceinline__ uint32_t sgh_fixup(uint32_t v, uint32_t fix, int m) {
 		return v;
 	const uint32_t f = (fix >> (2 * m)) & 3u;
 	return f == 1u ? v << 16 : (f == 2u ? v >> 16 : v);
+}
+
+/* normalisation of a loaded pixel pair (:1635-1652): NORM 1 = round_to_WORD(v scale - offset),
+ * 2 = round_to_WORD(v scale mul), in the reference's double operations; rows outside the
+ * frame (read as 0) are normalised like read samples, but columns outside the image (EDGE
+ * fix codes 1..3) stay 0, as the x shift writes 0 straight into the stack (:1628-1632) */
+template <int NORM, bool EDGE>
+__device__ __forceinline__ uint32_t sgh_norm_pair(uint32_t v, double a, double b, uint32_t fix, int m) {
+	if (NORM == 0)
+		return v;
+	/* round_to_WORD(y) = min(trunc(y + 0.5), 65535) with the conversion's clamp of
+	 * negative values to 0 (y <= 0 gives y + 0.5 <= 0.5, truncated to 0 either way) */
+	auto g = [&](uint32_t x) -> uint32_t {
+		const double t = (double)x * a;
+		const double y = NORM == 1 ? t - b : t * b;
+		uint32_t r;
+		asm("v_cvt_u32_f64 %0, %1" : "=v"(r) : "v"(y + 0.5));
+		return r < 65535u ? r : 65535u;
+	};
+	uint32_t r = g(v & 0xFFFFu) | (g(v >> 16) << 16);
+	if (EDGE) {
+		const uint32_t f = (fix >> (2 * m)) & 3u;
+		r &= f == 0u ? 0xFFFFFFFFu : (f == 1u ? 0xFFFF0000u : (f == 2u ? 0x0000FFFFu : 0u));
+	}
+	return r;
+}
+
+/* per-frame normalisation pair {scale, offset | mul} (one scalar load) */
+__device__ __forceinline__ void sgh_coef(const SgStackParams &p, int f, double &a, double &b) {
+	const int4 v = ((const int4 *)p.hist_norm)[f];
+	const int x = __builtin_amdgcn_readfirstlane(v.x), y = __builtin_amdgcn_readfirstlane(v.y);
+	const int z = __builtin_amdgcn_readfirstlane(v.z), w = __builtin_amdgcn_readfirstlane(v.w);
+	a = __hiloint2double(y, x);
+	b = __hiloint2double(w, z);
 }
 
 /* packed u16 min / saturating sub kept as single instructions (LLVM otherwise rewrites
@@ -900,7 +934,7 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds &L, int col, int half
  * before the binning.  No block is loaded twice.  Frames 0..15 (wave 0's first block) are
  * the centre sample: wave 0 sorts them and publishes the band starts through LDS while the
  * other waves' first blocks are in flight (one barrier, which also covers the clear). */
-template <bool EDGE, int NBUF>
+template <bool EDGE, int NBUF, int NORM>
 __device__ __forceinline__ void sgh_build(const SgStackParams &p, SghLds &L, const SghFrame &F, int wave, int lane,
 		int &lo_a, int &lo_b, uint32_t &nonzero, uint32_t &nsat, int &counted) {
 	constexpr int M = 16;		/* frames per block */
@@ -930,8 +964,14 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, SghLds &L, con
 	if (wave == 0) {
 		uint32_t p16[SGH_CENTER];
 #pragma unroll
-		for (int m = 0; m < SGH_CENTER; m++)
+		for (int m = 0; m < SGH_CENTER; m++) {
 			p16[m] = sgh_fixup<EDGE>(buf[0][m], fix[0], m);
+			if (NORM) {
+				double a, b;
+				sgh_coef(p, m, a, b);
+				p16[m] = sgh_norm_pair<NORM, EDGE>(p16[m], a, b, fix[0], m);
+			}
+		}
 		int la, lb;
 		sgh_centre2(p16, la, lb);
 		L.lo2[lane] = (uint32_t)la | ((uint32_t)lb << 16);
@@ -949,15 +989,19 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, SghLds &L, con
 #pragma unroll
 			for (int m = 0; m < M; m++)
 				nonzero ^= raw[m];
-		} else if (f0 + M <= N) {
-#pragma unroll
-			for (int m = 0; m < M; m++)
-				sgh_bin_pair(h, l4, lo2, sgh_fixup<EDGE>(raw[m], fx, m), nonzero, nsat);
 		} else {
 #pragma unroll
-			for (int m = 0; m < M; m++)
-				if (f0 + m < N)
-					sgh_bin_pair(h, l4, lo2, sgh_fixup<EDGE>(raw[m], fx, m), nonzero, nsat);
+			for (int m = 0; m < M; m++) {
+				if (f0 + M <= N || f0 + m < N) {
+					uint32_t v = sgh_fixup<EDGE>(raw[m], fx, m);
+					if (NORM) {
+						double a, b;
+						sgh_coef(p, f0 + m, a, b);
+						v = sgh_norm_pair<NORM, EDGE>(v, a, b, fx, m);
+					}
+					sgh_bin_pair(h, l4, lo2, v, nonzero, nsat);
+				}
+			}
 		}
 		counted += (N - f0 < M ? N - f0 : M);
 	};
@@ -981,7 +1025,7 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, SghLds &L, con
 	}
 }
 
-template <int REJ>	/* 2 = SIGMA, 4 = WINSORIZED */
+template <int REJ, int NORM>	/* REJ 2 = SIGMA, 4 = WINSORIZED; NORM 0 none, 1 additive, 2 multiplicative */
 __global__ void __launch_bounds__(64 * SGH_WAVES)
 k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
 	__shared__ SghLds L;
@@ -1024,9 +1068,9 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 	uint32_t nonzero = 0, nsat = 0;
 	int counted = 0, lo_a, lo_b;
 	if (interior)
-		sgh_build<false, SGH_NBUF>(p, L, F, wave, lane, lo_a, lo_b, nonzero, nsat, counted);
+		sgh_build<false, SGH_NBUF, NORM>(p, L, F, wave, lane, lo_a, lo_b, nonzero, nsat, counted);
 	else
-		sgh_build<true, SGH_NBUF>(p, L, F, wave, lane, lo_a, lo_b, nonzero, nsat, counted);
+		sgh_build<true, SGH_NBUF, NORM>(p, L, F, wave, lane, lo_a, lo_b, nonzero, nsat, counted);
 	if (counted) {
 		atomicAdd(&L.nz[lane], (uint32_t)counted - (nonzero & 0xFFFFu));
 		atomicAdd(&L.nz[64 + lane], (uint32_t)counted - (nonzero >> 16));
@@ -1052,5 +1096,9 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 }
 
 
-template __global__ void k_stack_hist<2>(SgStackParams, unsigned int *, unsigned int *);
-template __global__ void k_stack_hist<4>(SgStackParams, unsigned int *, unsigned int *);
+template __global__ void k_stack_hist<2, 0>(SgStackParams, unsigned int *, unsigned int *);
+template __global__ void k_stack_hist<2, 1>(SgStackParams, unsigned int *, unsigned int *);
+template __global__ void k_stack_hist<2, 2>(SgStackParams, unsigned int *, unsigned int *);
+template __global__ void k_stack_hist<4, 0>(SgStackParams, unsigned int *, unsigned int *);
+template __global__ void k_stack_hist<4, 1>(SgStackParams, unsigned int *, unsigned int *);
+template __global__ void k_stack_hist<4, 2>(SgStackParams, unsigned int *, unsigned int *);

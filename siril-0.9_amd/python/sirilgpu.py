@@ -52,7 +52,7 @@ class StackStats(ctypes.Structure):
         ("chain_pixels", ctypes.c_uint64),
         ("launches", ctypes.c_uint64),
         ("main_kernel_blocks", ctypes.c_int),
-        ("reserved", ctypes.c_int),
+        ("path", ctypes.c_int),
     ]
 
 

@@ -177,6 +177,40 @@ def test_hist_path_matches_oracle_and_sorted(gpu_ctx, N, rejection):
     assert st.chain_pixels <= limit * H * W, st.chain_pixels
 
 
+@pytest.mark.parametrize("rejection", [sg.SIGMA, sg.WINSORIZED])
+@pytest.mark.parametrize("normalize", [sg.ADDITIVE, sg.MULTIPLICATIVE, sg.ADDITIVE_SCALING,
+                                       sg.MULTIPLICATIVE_SCALING])
+def test_hist_path_normalization(gpu_ctx, normalize, rejection):
+    """normalised stacks on the histogram path (samples normalised at load, :1635-1652):
+    rows shifted out of the frame are normalised zeros, columns shifted out of the image
+    stay 0; both interior and image-edge tiles"""
+    N, H, W = 40, 64, 300
+    frames = orc.synth(N, 1, H, W, seed=410 + normalize, maxshift=10)
+    sx, sy = orc.synth_shifts(N, seed=410 + normalize, maxshift=10)
+    rng = np.random.default_rng(normalize)
+    loc = 1000 + rng.random(N) * 80
+    # scale spread of a few %: MULTIPLICATIVE_SCALING puts frame i's background at
+    # loc0 * s0 / s_i (:108-119), so a wide spread scatters the frames outside the 256-bin band
+    scl = 30 + rng.random(N) * 0.9
+    off, mul, scale = orc.compute_normalization(normalize, loc, scl, ref_image=0)
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=rejection, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                              normalize=normalize, offset=off, mul=mul, scale=scale, max_thread=2,
+                              max_number_of_rows=H)
+    rc, out, rej, _ = gpu_ctx.stack_host(desc, np.ascontiguousarray(frames))
+    assert rc == 0, gpu_ctx.error()
+    st = gpu_ctx.stats()
+    assert st.path == 1, "normalised SIGMA / WINSORIZED must take the histogram path"
+    rc, ref, rej_ref = orc.stack_rejection(frames, rejection, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                                           normalize=normalize, offset=off, mul=mul, scale=scale, max_thread=2)
+    assert rc == 0
+    assert_same(out, ref, f"hist norm={normalize} rej={rejection}")
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+    # rows within max|shifty| of the frame border hold normalised zeros of the rows shifted
+    # out (round(-offset) etc.): out-of-band values other than 0 / 65535, redone by design
+    border = int(np.max(np.abs(sy)))
+    assert st.chain_pixels <= (2 * border + 0.05 * H) * W, st.chain_pixels
+
+
 @pytest.mark.parametrize("shifts", [True, False])
 @pytest.mark.parametrize("W", [700, 1024])
 def test_hist_path_interior_tiles(gpu_ctx, W, shifts):
