@@ -41,6 +41,14 @@ __device__ __forceinline__ int sg_bitrev(int x, int logn) {
  * LDS round trips instead of 11).  tw[k] = exp(-2 pi i k / n), k < n/2; the inverse uses
  * conjugate twiddles (unnormalised, FFTW_BACKWARD).
  * ------------------------------------------------------------------------------------ */
+/* LDS element index with one pad slot per 8 elements: the Stockham stores of the first
+ * passes (stride 8 and 64 elements between neighbouring threads) would otherwise hit the
+ * same banks 8- to 32-fold */
+__device__ __forceinline__ int sg_pad(int i) {
+	return i + (i >> 3);
+}
+#define SG_PADN(n) ((n) + ((n) >> 3))
+
 __device__ __forceinline__ sg_c64 sg_cmul(sg_c64 a, sg_c64 b) {
 	return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
@@ -110,10 +118,12 @@ __device__ __forceinline__ sg_c64 sg_twiddle(const sg_c64 *__restrict__ tw, int 
 template <int R>
 __device__ __forceinline__ void sg_stockham_pass(sg_c64 *buf, int n, int nb, int bstride, int Ns,
 		const sg_c64 *__restrict__ tw, bool inv) {
-	constexpr int MAXI = 16 / R;	/* work items per thread: nb * n / R <= MAXI * blockDim (host-checked) */
+	constexpr int MAXI = 8 / R;	/* work items per thread: nb * n <= 8 * blockDim (host-sized launches) */
 	const int per = n / R, items = nb * per;
-	sg_c64 v[MAXI][R];
-	/* load every item's R inputs before anyone stores (in-place pass) */
+	sg_c64 v[MAXI][R], w[MAXI][R];
+	const bool twiddled = Ns > 1;	/* the first pass (Ns = 1) multiplies by w^0 = 1 only */
+	/* load every item's R inputs before anyone stores (in-place pass); the twiddles are
+	 * fetched here too, so their latency overlaps the barrier wait */
 #pragma unroll
 	for (int it = 0; it < MAXI; it++) {
 		const int t = threadIdx.x + it * blockDim.x;
@@ -122,7 +132,14 @@ __device__ __forceinline__ void sg_stockham_pass(sg_c64 *buf, int n, int nb, int
 			const sg_c64 *x = buf + (size_t)b * bstride;
 #pragma unroll
 			for (int r = 0; r < R; r++)
-				v[it][r] = x[j + r * per];
+				v[it][r] = x[sg_pad(j + r * per)];
+			if (twiddled) {
+				const int jm = j & (Ns - 1);
+				const int kstep = jm * (n / (Ns * R));
+#pragma unroll
+				for (int r = 1; r < R; r++)
+					w[it][r] = sg_twiddle(tw, n, r * kstep, inv);
+			}
 		}
 	}
 	__syncthreads();
@@ -132,22 +149,23 @@ __device__ __forceinline__ void sg_stockham_pass(sg_c64 *buf, int n, int nb, int
 		if (t < items) {
 			const int b = t / per, j = t - b * per;
 			const int jm = j & (Ns - 1);
-			const int kstep = jm * (n / (Ns * R));
+			if (twiddled) {
 #pragma unroll
-			for (int r = 1; r < R; r++)
-				v[it][r] = sg_cmul(v[it][r], sg_twiddle(tw, n, r * kstep, inv));
+				for (int r = 1; r < R; r++)
+					v[it][r] = sg_cmul(v[it][r], w[it][r]);
+			}
 			sg_dft_small<R, R>(v[it], inv);
 			sg_c64 *y = buf + (size_t)b * bstride;
 			const int base = (j - jm) * R + jm;
 #pragma unroll
 			for (int r = 0; r < R; r++)
-				y[base + r * Ns] = v[it][r];
+				y[sg_pad(base + r * Ns)] = v[it][r];
 		}
 	}
 	__syncthreads();
 }
 
-__device__ void sg_lds_fft(sg_c64 *buf, int n, int logn, int nb, int bstride, const sg_c64 *__restrict__ tw,
+__device__ __forceinline__ void sg_lds_fft(sg_c64 *buf, int n, int logn, int nb, int bstride, const sg_c64 *__restrict__ tw,
 		bool inverse) {
 	(void)logn;
 	__syncthreads();
@@ -168,7 +186,7 @@ __device__ void sg_lds_fft(sg_c64 *buf, int n, int logn, int nb, int bstride, co
 }
 
 /* row pass of the forward transform of a + i b (b = -1: zero imaginary part) */
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(512)
 k_reg_rows_fwd(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const int *__restrict__ fb,
 		int S, int logS, const sg_c64 *__restrict__ tw, sg_c64 *__restrict__ work) {
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -179,29 +197,29 @@ k_reg_rows_fwd(const uint16_t *__restrict__ sel, const int *__restrict__ fa, con
 	const int b = fb[pair];
 	const uint16_t *pb = b >= 0 ? sel + (size_t)b * plane + (size_t)row * S : nullptr;
 	for (int j = threadIdx.x; j < S; j += blockDim.x)
-		buf[j] = make_double2((double)pa[j], pb ? (double)pb[j] : 0.0);
+		buf[sg_pad(j)] = make_double2((double)pa[j], pb ? (double)pb[j] : 0.0);
 	sg_lds_fft(buf, S, logS, 1, S, tw, false);
 	sg_c64 *out = work + (size_t)pair * plane + (size_t)row * S;
 	for (int j = threadIdx.x; j < S; j += blockDim.x)
-		out[j] = buf[j];
+		out[j] = buf[sg_pad(j)];
 }
 
 /* column pass (forward or inverse) over strips of CW adjacent columns */
-__global__ void __launch_bounds__(512)
+__global__ void __launch_bounds__(1024)
 k_reg_cols(sg_c64 *__restrict__ work, int S, int logS, int CW, const sg_c64 *__restrict__ tw, int inverse) {
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 	sg_c64 *buf = (sg_c64 *)smem;
 	const int x0 = blockIdx.x * CW, pair = blockIdx.y;
-	const int bstride = S + 1;
+	const int bstride = SG_PADN(S) + 1;
 	sg_c64 *base = work + (size_t)pair * S * S + x0;
 	for (int idx = threadIdx.x; idx < S * CW; idx += blockDim.x) {
 		const int r = idx / CW, c = idx - r * CW;
-		buf[c * bstride + r] = base[(size_t)r * S + c];
+		buf[c * bstride + sg_pad(r)] = base[(size_t)r * S + c];
 	}
 	sg_lds_fft(buf, S, logS, CW, bstride, tw, inverse != 0);
 	for (int idx = threadIdx.x; idx < S * CW; idx += blockDim.x) {
 		const int r = idx / CW, c = idx - r * CW;
-		base[(size_t)r * S + c] = buf[c * bstride + r];
+		base[(size_t)r * S + c] = buf[c * bstride + sg_pad(r)];
 	}
 }
 
@@ -237,6 +255,53 @@ k_reg_xpower(sg_c64 *__restrict__ work, const sg_c64 *__restrict__ spec, int S) 
 	}
 }
 
+/* cross-power fused into the inverse ROW pass: workgroup (ky, pair) holds rows ky and
+ * -ky (mod S) of the forward spectrum in LDS, forms the packed cross-power spectrum of
+ * both (each (k, -k) pair once, as k_reg_xpower), runs the inverse row FFT of both and
+ * writes them back.  The inverse column pass then only reads (k_reg_cols_inv_argmax). */
+__global__ void __launch_bounds__(1024)
+k_reg_xpower_rows_inv(sg_c64 *__restrict__ work, const sg_c64 *__restrict__ spec, int S, int logS,
+		const sg_c64 *__restrict__ tw) {
+	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+	sg_c64 *buf = (sg_c64 *)smem;
+	const int ky = blockIdx.x, pair = blockIdx.y;
+	const int my = (S - ky) & (S - 1);
+	const bool self = my == ky;
+	sg_c64 *Z = work + (size_t)pair * S * S;
+	sg_c64 *A = buf, *Bv = self ? buf : buf + SG_PADN(S);
+	for (int j = threadIdx.x; j < S; j += blockDim.x) {
+		A[sg_pad(j)] = Z[(size_t)ky * S + j];
+		if (!self)
+			Bv[sg_pad(j)] = Z[(size_t)my * S + j];
+	}
+	__syncthreads();
+	for (int kx = threadIdx.x; kx < S; kx += blockDim.x) {
+		const int mx = (S - kx) & (S - 1);
+		if (self && mx < kx)
+			continue;
+		const sg_c64 zk = A[sg_pad(kx)], zm = Bv[sg_pad(mx)];
+		const double ar = 0.5 * (zk.x + zm.x), ai = 0.5 * (zk.y - zm.y);
+		const double br = 0.5 * (zk.y + zm.y), bi = -0.5 * (zk.x - zm.x);
+		const sg_c64 rk = spec[(size_t)ky * S + kx], rm = spec[(size_t)my * S + mx];
+		{
+			const double pr = rk.x * ar + rk.y * ai, pi = rk.y * ar - rk.x * ai;
+			const double qr = rk.x * br + rk.y * bi, qi = rk.y * br - rk.x * bi;
+			A[sg_pad(kx)] = make_double2(pr - qi, pi + qr);
+		}
+		if (!(self && mx == kx)) {
+			const double pr = rm.x * ar - rm.y * ai, pi = rm.x * ai + rm.y * ar;
+			const double qr = rm.x * br - rm.y * bi, qi = rm.x * bi + rm.y * br;
+			Bv[sg_pad(mx)] = make_double2(pr - qi, pi + qr);
+		}
+	}
+	sg_lds_fft(buf, S, logS, self ? 1 : 2, SG_PADN(S), tw, true);
+	for (int j = threadIdx.x; j < S; j += blockDim.x) {
+		Z[(size_t)ky * S + j] = A[sg_pad(j)];
+		if (!self)
+			Z[(size_t)my * S + j] = Bv[sg_pad(j)];
+	}
+}
+
 /* better (value, index): larger value, ties -> lower index (first strict max, :337-343) */
 __device__ __forceinline__ void sg_argmax_merge(double &v, int &i, double v2, int i2) {
 	if (v2 > v || (v2 == v && i2 < i)) {
@@ -252,7 +317,7 @@ struct SgBest {
 
 /* inverse row pass fused with the per-row arg-max of the real (frame a) and imaginary
  * (frame b) parts */
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(512)
 k_reg_rows_inv_argmax(const sg_c64 *__restrict__ work, int S, int logS, const sg_c64 *__restrict__ tw,
 		SgBest *__restrict__ best) {
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -262,12 +327,12 @@ k_reg_rows_inv_argmax(const sg_c64 *__restrict__ work, int S, int logS, const sg
 	const int row = blockIdx.x, pair = blockIdx.y;
 	const sg_c64 *in = work + (size_t)pair * S * S + (size_t)row * S;
 	for (int j = threadIdx.x; j < S; j += blockDim.x)
-		buf[j] = in[j];
+		buf[sg_pad(j)] = in[j];
 	sg_lds_fft(buf, S, logS, 1, S, tw, true);
 	double va = -INFINITY, vb = -INFINITY;
 	int ia = 0x7fffffff, ib = 0x7fffffff;
 	for (int j = threadIdx.x; j < S; j += blockDim.x) {
-		const sg_c64 c = buf[j];
+		const sg_c64 c = buf[sg_pad(j)];
 		const int idx = row * S + j;
 		sg_argmax_merge(va, ia, c.x, idx);
 		sg_argmax_merge(vb, ib, c.y, idx);
@@ -300,16 +365,70 @@ k_reg_rows_inv_argmax(const sg_c64 *__restrict__ work, int S, int logS, const sg
 	}
 }
 
+/* inverse column pass fused with the arg-max of the real (frame a) and imaginary (frame b)
+ * parts over the strip: nothing is written back */
+__global__ void __launch_bounds__(1024)
+k_reg_cols_inv_argmax(const sg_c64 *__restrict__ work, int S, int logS, int CW, const sg_c64 *__restrict__ tw,
+		SgBest *__restrict__ best) {
+	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+	sg_c64 *buf = (sg_c64 *)smem;
+	__shared__ double rv[2][16];
+	__shared__ int ri[2][16];
+	const int x0 = blockIdx.x * CW, pair = blockIdx.y;
+	const int bstride = SG_PADN(S) + 1;
+	const sg_c64 *base = work + (size_t)pair * S * S + x0;
+	for (int idx = threadIdx.x; idx < S * CW; idx += blockDim.x) {
+		const int r = idx / CW, c = idx - r * CW;
+		buf[c * bstride + sg_pad(r)] = base[(size_t)r * S + c];
+	}
+	sg_lds_fft(buf, S, logS, CW, bstride, tw, true);
+	double va = -INFINITY, vb = -INFINITY;
+	int ia = 0x7fffffff, ib = 0x7fffffff;
+	for (int idx = threadIdx.x; idx < S * CW; idx += blockDim.x) {
+		const int r = idx / CW, c = idx - r * CW;
+		const sg_c64 v = buf[c * bstride + sg_pad(r)];
+		const int lin = r * S + x0 + c;
+		sg_argmax_merge(va, ia, v.x, lin);
+		sg_argmax_merge(vb, ib, v.y, lin);
+	}
+	for (int o = 32; o > 0; o >>= 1) {
+		const double va2 = __shfl_down(va, o, 64), vb2 = __shfl_down(vb, o, 64);
+		const int ia2 = __shfl_down(ia, o, 64), ib2 = __shfl_down(ib, o, 64);
+		sg_argmax_merge(va, ia, va2, ia2);
+		sg_argmax_merge(vb, ib, vb2, ib2);
+	}
+	const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+	if ((threadIdx.x & 63) == 0) {
+		rv[0][wave] = va;
+		ri[0][wave] = ia;
+		rv[1][wave] = vb;
+		ri[1][wave] = ib;
+	}
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		for (int w = 1; w < nw; w++) {
+			sg_argmax_merge(va, ia, rv[0][w], ri[0][w]);
+			sg_argmax_merge(vb, ib, rv[1][w], ri[1][w]);
+		}
+		SgBest r;
+		r.va = va;
+		r.ia = ia;
+		r.vb = vb;
+		r.ib = ib;
+		best[(size_t)pair * gridDim.x + blockIdx.x] = r;
+	}
+}
+
 /* per pair: reduce the row maxima and convert to (shiftx, shifty) (:344-351) */
 __global__ void __launch_bounds__(256)
-k_reg_final(const SgBest *__restrict__ best, int S, int *__restrict__ out /* [pair][4] */) {
+k_reg_final(const SgBest *__restrict__ best, int S, int count, int *__restrict__ out /* [pair][4] */) {
 	__shared__ double rv[2][4];
 	__shared__ int ri[2][4];
 	const int pair = blockIdx.x;
 	double va = -INFINITY, vb = -INFINITY;
 	int ia = 0x7fffffff, ib = 0x7fffffff;
-	for (int r = threadIdx.x; r < S; r += blockDim.x) {
-		const SgBest b = best[(size_t)pair * S + r];
+	for (int r = threadIdx.x; r < count; r += blockDim.x) {
+		const SgBest b = best[(size_t)pair * count + r];
 		sg_argmax_merge(va, ia, b.va, b.ia);
 		sg_argmax_merge(vb, ib, b.vb, b.ib);
 	}
@@ -577,16 +696,29 @@ extern "C" int sg_register_dft_u16_device(sg_ctx *ctx, int dev_index, const uint
 	const int npairs_total = (int)(todo.size() + 1) / 2;
 	if (B > npairs_total && npairs_total > 0)
 		B = npairs_total;
-	const size_t row_lds = plane / S * sizeof(sg_c64);
+	const size_t row_lds = (size_t)SG_PADN(S) * sizeof(sg_c64);
 	int CW = 8192 / S;
 	if (CW < 1)
 		CW = 1;
 	if (CW > 8)
 		CW = 8;
-	const size_t col_lds = (size_t)CW * (S + 1) * sizeof(sg_c64);
+	if (const char *e = getenv("SG_REG_CW"))	/* A/B knob: columns per column-pass workgroup */
+		CW = atoi(e) > 0 ? atoi(e) : CW;
+	const size_t col_lds = (size_t)CW * (SG_PADN(S) + 1) * sizeof(sg_c64);
 	(void)hipFuncSetAttribute((const void *)k_reg_rows_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)row_lds);
 	(void)hipFuncSetAttribute((const void *)k_reg_rows_inv_argmax, hipFuncAttributeMaxDynamicSharedMemorySize, (int)row_lds);
 	(void)hipFuncSetAttribute((const void *)k_reg_cols, hipFuncAttributeMaxDynamicSharedMemorySize, (int)col_lds);
+	(void)hipFuncSetAttribute((const void *)k_reg_cols_inv_argmax, hipFuncAttributeMaxDynamicSharedMemorySize,
+			(int)col_lds);
+	(void)hipFuncSetAttribute((const void *)k_reg_xpower_rows_inv, hipFuncAttributeMaxDynamicSharedMemorySize,
+			(int)(2 * row_lds));
+	/* threads: 8 elements per thread in every LDS FFT (sg_stockham_pass's register budget),
+	 * at least one wave */
+	auto thr_for = [](int elems) { return elems / 8 < 64 ? 64 : elems / 8; };
+	const int row_thr = thr_for(S), col_thr = thr_for(CW * S), xri_thr = thr_for(2 * S);
+	bool fused = true;
+	if (const char *e = getenv("SG_REG_FUSED"))	/* A/B knob: 0 = the unfused pass order */
+		fused = atoi(e) != 0;
 
 	HIPCHK(ensure(dv.reg_spec, plane * sizeof(sg_c64)));
 	HIPCHK(ensure(dv.reg_work, (size_t)(B > 1 ? B : 1) * plane * sizeof(sg_c64)));
@@ -612,28 +744,41 @@ extern "C" int sg_register_dft_u16_device(sg_ctx *ctx, int dev_index, const uint
 	HIPCHK(hipMemcpyAsync(d_fa, hfa.data(), sizeof(int) * (NP + 1), hipMemcpyHostToDevice, s));
 	HIPCHK(hipMemcpyAsync(d_fb, hfb.data(), sizeof(int) * (NP + 1), hipMemcpyHostToDevice, s));
 	/* reference spectrum R = FFT2(ref) */
-	hipLaunchKernelGGL(k_reg_rows_fwd, dim3(S, 1), dim3(256), row_lds, s, d_sel, d_fa + NP, d_fb + NP, S, logS, tw,
-			spec);
+	hipLaunchKernelGGL(k_reg_rows_fwd, dim3(S, 1), dim3(row_thr), row_lds, s, d_sel, d_fa + NP, d_fb + NP, S, logS,
+			tw, spec);
 	HIPCHK(hipGetLastError());
-	hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, 1), dim3(512), col_lds, s, spec, S, logS, CW, tw, 0);
+	hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, 1), dim3(col_thr), col_lds, s, spec, S, logS, CW, tw, 0);
 	HIPCHK(hipGetLastError());
 	shiftx[ref_image] = 0;
 	shifty[ref_image] = 0;
 	for (int p0 = 0; p0 < npairs_total; p0 += B) {
 		const int np = npairs_total - p0 < B ? npairs_total - p0 : B;
-		hipLaunchKernelGGL(k_reg_rows_fwd, dim3(S, np), dim3(256), row_lds, s, d_sel, d_fa + p0, d_fb + p0, S, logS,
-				tw, work);
+		hipLaunchKernelGGL(k_reg_rows_fwd, dim3(S, np), dim3(row_thr), row_lds, s, d_sel, d_fa + p0, d_fb + p0, S,
+				logS, tw, work);
 		HIPCHK(hipGetLastError());
-		hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, np), dim3(512), col_lds, s, work, S, logS, CW, tw, 0);
+		hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, np), dim3(col_thr), col_lds, s, work, S, logS, CW, tw, 0);
 		HIPCHK(hipGetLastError());
-		hipLaunchKernelGGL(k_reg_xpower, dim3(1024, np), dim3(256), 0, s, work, (const sg_c64 *)spec, S);
-		HIPCHK(hipGetLastError());
-		hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, np), dim3(512), col_lds, s, work, S, logS, CW, tw, 1);
-		HIPCHK(hipGetLastError());
-		hipLaunchKernelGGL(k_reg_rows_inv_argmax, dim3(S, np), dim3(256), row_lds, s, (const sg_c64 *)work, S, logS,
-				tw, best);
-		HIPCHK(hipGetLastError());
-		hipLaunchKernelGGL(k_reg_final, dim3(np), dim3(256), 0, s, (const SgBest *)best, S, d_out + 4 * p0);
+		if (fused) {
+			/* cross-power + inverse rows (row pairs ky, -ky), then inverse columns with the
+			 * arg-max: two plane round trips fewer than the unfused order */
+			hipLaunchKernelGGL(k_reg_xpower_rows_inv, dim3(S / 2 + 1, np), dim3(xri_thr), 2 * row_lds, s, work,
+					(const sg_c64 *)spec, S, logS, tw);
+			HIPCHK(hipGetLastError());
+			hipLaunchKernelGGL(k_reg_cols_inv_argmax, dim3(S / CW, np), dim3(col_thr), col_lds, s,
+					(const sg_c64 *)work, S, logS, CW, tw, best);
+			HIPCHK(hipGetLastError());
+			hipLaunchKernelGGL(k_reg_final, dim3(np), dim3(256), 0, s, (const SgBest *)best, S, S / CW,
+					d_out + 4 * p0);
+		} else {
+			hipLaunchKernelGGL(k_reg_xpower, dim3(1024, np), dim3(256), 0, s, work, (const sg_c64 *)spec, S);
+			HIPCHK(hipGetLastError());
+			hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, np), dim3(col_thr), col_lds, s, work, S, logS, CW, tw, 1);
+			HIPCHK(hipGetLastError());
+			hipLaunchKernelGGL(k_reg_rows_inv_argmax, dim3(S, np), dim3(row_thr), row_lds, s, (const sg_c64 *)work,
+					S, logS, tw, best);
+			HIPCHK(hipGetLastError());
+			hipLaunchKernelGGL(k_reg_final, dim3(np), dim3(256), 0, s, (const SgBest *)best, S, S, d_out + 4 * p0);
+		}
 		HIPCHK(hipGetLastError());
 	}
 	if (npairs_total > 0)
