@@ -470,26 +470,40 @@ k_reg_final(const SgBest *__restrict__ best, int S, int count, int *__restrict__
  * division (:211), so the factor is 1 for subsample 3 and 0 for 4 and 5.
  * ------------------------------------------------------------------------------------- */
 #define SG_Q_THRESHOLD (40 << 8)
+#define SG_QROWS 4	/* subsampled rows per k_quality_sub workgroup */
 
 /* SubSample (:223-234) of one 3x3 sample row, plus the running max of the middle rows
  * (the maxp[] loop :119-133 reduces to max over 0 < v < 65530) */
 __global__ void __launch_bounds__(256)
 k_quality_sub(const uint16_t *__restrict__ sel, const int *__restrict__ qframes, int S, int xs, int ys,
 		uint16_t *__restrict__ qbuf, unsigned int *__restrict__ qmax) {
-	const int j = blockIdx.x, q = blockIdx.y;
-	const uint16_t *img = sel + (size_t)qframes[q] * S * S + (size_t)(j * 3) * S;
-	uint16_t *dst = qbuf + (size_t)q * xs * ys + (size_t)j * xs;
+	/* SG_QROWS output rows per workgroup; a thread forms two adjacent outputs from three
+	 * 12-byte (6-pixel, dword-aligned) loads, one per input row */
+	const int q = blockIdx.y;
+	const uint16_t *frame = sel + (size_t)qframes[q] * S * S;
 	unsigned int m = 0;
-	const bool middle = (j >= 1 && j <= ys - 2);
-	for (int i = threadIdx.x; i < xs; i += blockDim.x) {
-		const uint16_t *p = img + i * 3;
-		int v = 0;
-		for (int y = 0; y < 3; y++)
-			v += (int)p[y * S] + (int)p[y * S + 1] + (int)p[y * S + 2];
-		v /= 9;
-		dst[i] = (uint16_t)v;
-		if (middle && v > 0 && v < 65530 && (unsigned)v > m)
-			m = (unsigned)v;
+	for (int j = blockIdx.x * SG_QROWS; j < ys && j < (blockIdx.x + 1) * SG_QROWS; j++) {
+		const bool middle = (j >= 1 && j <= ys - 2);
+		uint16_t *dst = qbuf + (size_t)q * xs * ys + (size_t)j * xs;
+		for (int k = threadIdx.x; 2 * k < xs; k += blockDim.x) {
+			int va = 0, vb = 0;
+			for (int y = 0; y < 3; y++) {
+				const uint32_t *p = (const uint32_t *)(frame + (size_t)(3 * j + y) * S + 6 * k);
+				const uint32_t d0 = p[0], d1 = p[1], d2 = p[2];
+				va += (int)(d0 & 0xFFFFu) + (int)(d0 >> 16) + (int)(d1 & 0xFFFFu);
+				vb += (int)(d1 >> 16) + (int)(d2 & 0xFFFFu) + (int)(d2 >> 16);
+			}
+			va /= 9;
+			vb /= 9;
+			dst[2 * k] = (uint16_t)va;
+			if (middle && va > 0 && va < 65530 && (unsigned)va > m)
+				m = (unsigned)va;
+			if (2 * k + 1 < xs) {
+				dst[2 * k + 1] = (uint16_t)vb;
+				if (middle && vb > 0 && vb < 65530 && (unsigned)vb > m)
+					m = (unsigned)vb;
+			}
+		}
 	}
 	for (int o = 32; o > 0; o >>= 1) {
 		const unsigned int t = (unsigned int)__shfl_down((int)m, o, 64);
@@ -516,6 +530,10 @@ __global__ void __launch_bounds__(256)
 k_quality_grad(const uint16_t *__restrict__ qbuf, int xs, int ys, const unsigned int *__restrict__ qmax,
 		unsigned long long *__restrict__ acc /* [q][3]: val, pixels, thresholded */) {
 	__shared__ unsigned long long sv[4], sp[4], sc[4];
+	/* a 64 x 4 tile of outputs: stretched samples of the 68 x 8 neighbourhood, then the
+	 * smoothed values of the 66 x 6 one, each formed once in LDS */
+	__shared__ unsigned int st[8][68];
+	__shared__ int sms[6][66];
 	const int q = blockIdx.z;
 	const uint16_t *b = qbuf + (size_t)q * xs * ys;
 	const unsigned int mx = qmax[q];
@@ -523,25 +541,37 @@ k_quality_grad(const uint16_t *__restrict__ qbuf, int xs, int ys, const unsigned
 	const double mult = stretch ? (double)60000 / (double)mx : 1.0;
 	const int yb = (int)((double)ys * 0.1) + 1;
 	const int xb = (int)((double)xs * 0.1) + 1;
-	const int x = blockIdx.x * 64 + (threadIdx.x & 63);
-	const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+	const int x0 = blockIdx.x * 64, y0 = blockIdx.y * 4;
+	for (int i = threadIdx.x; i < 8 * 68; i += blockDim.x) {
+		const int ly = i / 68, lx = i - ly * 68;
+		const int gx = x0 - 2 + lx, gy = y0 - 2 + ly;
+		st[ly][lx] = (gx >= 0 && gx < xs && gy >= 0 && gy < ys) ? (unsigned int)sg_q_stretch(b, gy * xs + gx, mult, stretch)
+									     : 0u;
+	}
+	__syncthreads();
+	for (int i = threadIdx.x; i < 6 * 66; i += blockDim.x) {
+		const int ly = i / 66, lx = i - ly * 66;
+		const int qx = x0 - 1 + lx, qy = y0 - 1 + ly;
+		int v = 0;
+		if (qx >= 1 && qx <= xs - 2 && qy >= 1 && qy <= ys - 2) {
+			unsigned int sum = 0;
+			for (int ey = 0; ey < 3; ey++)
+				for (int ex = 0; ex < 3; ex++)
+					sum += st[ly + ey][lx + ex];
+			v = (int)(sum / 9);
+		}
+		sms[ly][lx] = v;
+	}
+	__syncthreads();
+	const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+	const int x = x0 + tx, y = y0 + ty;
 	unsigned long long val = 0, pix = 0, cnt = 0;
 	if (x >= xb && x < xs - xb && y >= yb && y < ys - yb) {
 		/* smoothed values on the 3x3 neighbourhood of (x, y) */
 		int sm[3][3];
-		for (int dy = -1; dy <= 1; dy++)
-			for (int dx = -1; dx <= 1; dx++) {
-				const int qx = x + dx, qy = y + dy;
-				int v = 0;
-				if (qx >= 1 && qx <= xs - 2 && qy >= 1 && qy <= ys - 2) {
-					unsigned int s = 0;
-					for (int ey = -1; ey <= 1; ey++)
-						for (int ex = -1; ex <= 1; ex++)
-							s += (unsigned int)sg_q_stretch(b, (qy + ey) * xs + qx + ex, mult, stretch);
-					v = (int)(s / 9);
-				}
-				sm[dy + 1][dx + 1] = v;
-			}
+		for (int dy = 0; dy < 3; dy++)
+			for (int dx = 0; dx < 3; dx++)
+				sm[dy][dx] = sms[ty + dy][tx + dx];
 		if (sm[1][1] >= SG_Q_THRESHOLD)
 			cnt = 1;
 		bool mapped = false;
@@ -586,9 +616,6 @@ k_quality_grad(const uint16_t *__restrict__ qbuf, int xs, int ys, const unsigned
 	}
 }
 
-/* ---------------------------------------------------------------------------------------
- * host side
- * ------------------------------------------------------------------------------------- */
 static int reg_quality(sg_ctx *ctx, SgDevice &dv, hipStream_t s, const uint16_t *d_sel, int S,
 		const std::vector<int> &frames, std::vector<double> &qual) {
 	const int nq = (int)frames.size();
@@ -606,7 +633,8 @@ static int reg_quality(sg_ctx *ctx, SgDevice &dv, hipStream_t s, const uint16_t 
 	unsigned int *qmax = (unsigned int *)(acc + 3 * nq);
 	HIPCHK(hipMemcpyAsync(d_frames, frames.data(), sizeof(int) * nq, hipMemcpyHostToDevice, s));
 	HIPCHK(hipMemsetAsync(dv.reg_qacc.p, 0, (size_t)nq * (3 * sizeof(unsigned long long) + sizeof(unsigned int)), s));
-	hipLaunchKernelGGL(k_quality_sub, dim3(ys, nq), dim3(256), 0, s, d_sel, d_frames, S, xs, ys, qbuf, qmax);
+	hipLaunchKernelGGL(k_quality_sub, dim3((ys + SG_QROWS - 1) / SG_QROWS, nq), dim3(256), 0, s, d_sel, d_frames, S,
+			xs, ys, qbuf, qmax);
 	HIPCHK(hipGetLastError());
 	hipLaunchKernelGGL(k_quality_grad, dim3((xs + 63) / 64, (ys + 3) / 4, nq), dim3(256), 0, s, qbuf, xs, ys,
 			qmax, acc);
