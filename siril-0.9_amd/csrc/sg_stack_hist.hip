@@ -1,6 +1,7 @@
 /*
  * sg_stack_hist.hip - gfx950 fast path of stack_mean_with_rejection, SIGMA rejection
- * (src/stacking/stacking.c:1674-1695 + sigma_clipping :1148-1161), without sorting.
+ * (src/stacking/stacking.c:1674-1695 + sigma_clipping :1148-1161) and WINSORIZED
+ * (:1710-1749), any normalisation (:1635-1652, applied at load), without sorting.
  *
  * Why: the reference sorts every pixel column (quicksort_s) on every clipping pass.  A
  * sort of N = 512 u16 per pixel costs ~O(N log^2 N) compare-exchanges on a GPU, far more
@@ -20,9 +21,10 @@
  * check (the zero fill of :1550-1577 for free), and the pixel pair is binned with packed
  * u16 arithmetic and branch-free LDS atomics.  Tiles whose shifted columns can leave the
  * image (the two image-edge tile columns) load pixel by pixel with the column check of
- * :1628-1632 (one latency per 16-frame block; they are 2 of every W/128 tiles).  Waves 0
- * and 1 then prefix-sum the bins once and run the reference's pass
- * loop as O(log) histogram queries, 64 pixels each.
+ * :1628-1632 (one latency per 16-frame block; they are 2 of every W/128 tiles).  The
+ * finish then prefix-sums the bins once and runs the reference's pass loop as O(log)
+ * histogram queries: SIGMA with a lane pair per pixel on all 4 waves, WINSORIZED with one
+ * lane per pixel on waves 0 / 1.
  *
  * Exactness: decisions use exact moments; a pixel whose decision falls within a rounding
  * band of a threshold (GSL's long-double sd vs exact), whose loop would hit the
