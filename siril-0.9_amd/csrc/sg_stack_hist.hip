@@ -603,6 +603,13 @@ __device__ __forceinline__ double sgh_sd_rel(int n, long long S, long long SS, b
 	*e0 = (num == 0);
 	return num <= 0 ? 0.0 : sqrt((double)num / ((double)n * (double)(n - 1)));
 }
+/* the same with 1 / (n (n - 1)) precomputed: within 2 ulp of sgh_sd_rel, far inside the
+ * rounding band every decision keeps */
+__device__ __forceinline__ double sgh_sd_rel_inv(int n, long long S, long long SS, double inn, bool *e0) {
+	const long long num = (long long)n * SS - S * S;
+	*e0 = (num == 0);
+	return num <= 0 ? 0.0 : sqrt((double)num * inn);
+}
 
 /* round_to_WORD(m) decision ambiguous (m within tol of 0, 65535 or a .5) */
 __device__ __forceinline__ bool sgh_round_ambiguous(double m, double tol) {
@@ -661,6 +668,7 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint
 		int Lw = 0, Hw = 0, vlo = 0, vhi = 0, IA = A, IB = B;
 		SghM MIA = MA, MIB = MB;
 		int ulo = sgh_value_at1(P, MA.c), uhi = sgh_value_at1(P, MA.c + n - 1);
+		const double inn = 1.0 / ((double)n * (double)(n - 1));
 		bool sig_e0 = e0;
 		for (int guard = 0;; guard++) {
 			if (guard > 4096)
@@ -755,17 +763,20 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint
 			const double sigma0 = sigma;
 			const bool e00 = sig_e0;
 			bool we0;
-			sigma = 1.134 * sgh_sd_rel(n, Sw, SSw, &we0);
+			sigma = 1.134 * sgh_sd_rel_inv(n, Sw, SSw, inn, &we0);
 			sig_e0 = we0;
 			if (e00) {
 				if (we0)
 					break;	/* 0/0 = NaN: the loop exits */
 				continue;	/* x/0 = inf > 0.0005 */
 			}
-			const double q = fabs(sigma - sigma0) / sigma0;
-			if (fabs(q - 0.0005) <= 1e-9 * 0.0005 + SGH_BAND * (1.0 + q))
+			/* |sigma - sigma0| / sigma0 > 0.0005 as the sign of d = |sigma - sigma0| -
+			 * 0.0005 sigma0 (sigma0 > 0 here): no division; |d| <= 7e-13 sigma0 covers the
+			 * band |q - 0.0005| <= 5e-13 + 1e-13 (1 + q) of the divided form near q = 0.0005 */
+			const double d = fabs(sigma - sigma0) - 0.0005 * sigma0;
+			if (fabs(d) <= 7e-13 * sigma0)
 				return 1;
-			if (!(q > 0.0005))
+			if (!(d > 0.0))
 				break;
 		}
 		/* clip pass on the kept set with the Winsorized sigma / median (:1731-1747) */
