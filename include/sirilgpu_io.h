@@ -45,6 +45,17 @@ int sg_seq_read_frame(const sg_seq *seq, int index, uint16_t *out);
 int sg_seq_load_device(sg_ctx *ctx, int dev_index, const sg_seq *seq, int first, int count,
 		uint16_t *d_frames, int64_t frame_stride, void *stream);
 
+/* CFA (Bayer) SER sequences opened with demosaicing (com.debayer.open_debayer,
+ * ser_read_frame src/io/ser.c:708-731 -> debayer() src/algos/demosaicing.c:727-760 with
+ * BAYER_BILINEAR, bayer_Bilinear :89-176): after this call the sequence has 3 layers and
+ * sg_seq_load_device demosaics on the device (borders 0, as the reference leaves them).
+ * pattern: SG_BAYER_* (the sensor_pattern order of src/core/siril.h:266-271), or -1 = the
+ * one the SER ColorID names (use_bayer_header, retrieveSERBayerPattern ser.c:453-471).
+ * Host reads (sg_seq_read_region / sg_seq_read_frame) of a demosaiced sequence are not
+ * provided and fail with SG_ERR_GENERIC. 0, or SG_ERR_GENERIC for a non-CFA sequence. */
+enum { SG_BAYER_RGGB = 0, SG_BAYER_BGGR = 1, SG_BAYER_GBRG = 2, SG_BAYER_GRBG = 3 };
+int sg_seq_set_debayer(sg_seq *seq, int pattern);
+
 #ifdef __cplusplus
 }
 #endif

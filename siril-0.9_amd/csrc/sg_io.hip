@@ -41,6 +41,7 @@ struct sg_seq {
 	int interleaved;	/* SER RGB / BGR */
 	int bgr;
 	int color_id, bitpix, bzero;
+	int debayer;		/* -1, or the SG_BAYER_* pattern of a demosaiced CFA SER */
 	std::vector<int> fd;	/* SER: one; FITS: one per frame */
 	std::vector<int64_t> data_off;	/* byte offset of the pixel data (per file) */
 	int64_t frame_bytes;	/* raw bytes of one frame */
@@ -81,6 +82,7 @@ extern "C" int sg_seq_open_ser(const char *path, sg_seq **out) {
 	}
 	sg_seq *s = new sg_seq();
 	s->kind = SG_SRC_SER;
+	s->debayer = -1;
 	/* the 7 little-endian ints at byte 14 (ser.c:312) */
 	s->color_id = (int)le32(h + 18);
 	const int big = (int)le32(h + 22) == 1;	/* SER_BIG_ENDIAN = 1 (ser.h:41) */
@@ -160,6 +162,7 @@ extern "C" int sg_seq_open_fits(const char *const *paths, int nframes, sg_seq **
 	*out = nullptr;
 	sg_seq *s = new sg_seq();
 	s->kind = SG_SRC_FITS;
+	s->debayer = -1;
 	for (int i = 0; i < nframes; i++) {
 		int fd = open(paths[i], O_RDONLY);
 		if (fd < 0) {
@@ -246,10 +249,25 @@ static inline uint16_t conv_host(const unsigned char *p, int enc, int *bad) {
 	}
 }
 
+extern "C" int sg_seq_set_debayer(sg_seq *s, int pattern) {
+	if (!s || s->kind != SG_SRC_SER || s->color_id < 8 || s->color_id > 11 || pattern < -1 || pattern > 3)
+		return SG_ERR_GENERIC;
+	if (pattern < 0) {
+		/* SER ColorID 8..11 = RGGB, GRBG, GBRG, BGGR (ser.h:19-22) */
+		static const int from_id[4] = {SG_BAYER_RGGB, SG_BAYER_GRBG, SG_BAYER_GBRG, SG_BAYER_BGGR};
+		pattern = from_id[s->color_id - 8];
+	}
+	s->debayer = pattern;
+	s->layers = 3;	/* frame_bytes stays the raw CFA frame */
+	return SG_OK;
+}
+
 extern "C" int sg_seq_read_region(void *user, int layer, int index, uint16_t *buffer, const sg_rect *area) {
 	const sg_seq *s = (const sg_seq *)user;
 	if (!s || !buffer || !area || index < 0 || index >= s->frames || layer < 0 || layer >= s->layers)
 		return -1;
+	if (s->debayer >= 0)
+		return -1;	/* demosaicing runs on the device only (sg_seq_load_device) */
 	if (area->x < 0 || area->y < 0 || area->w <= 0 || area->h <= 0 || area->x + area->w > s->width ||
 			area->y + area->h > s->height)
 		return -1;
@@ -287,7 +305,7 @@ extern "C" int sg_seq_read_region(void *user, int layer, int index, uint16_t *bu
 }
 
 extern "C" int sg_seq_read_frame(const sg_seq *s, int index, uint16_t *out) {
-	if (!s || !out || index < 0 || index >= s->frames)
+	if (!s || !out || index < 0 || index >= s->frames || s->debayer >= 0)
 		return SG_ERR_GENERIC;
 	const int fd = s->kind == SG_SRC_SER ? s->fd[0] : s->fd[index];
 	const int64_t base = s->kind == SG_SRC_SER ? s->data_off[0] + s->frame_bytes * (int64_t)index : s->data_off[index];
@@ -369,6 +387,50 @@ __global__ void __launch_bounds__(256) k_decode_frames(SgDecode d) {
 		atomicOr(d.bad, 1u);
 }
 
+/* bayer_Bilinear (src/algos/demosaicing.c:89-176) per output pixel, on the top-down CFA
+ * frame: interior pixels only (the reference's calloc'd border stays 0).  A red / blue
+ * centre takes the 4 greens ((sum + 2) >> 2) and the 4 diagonal opposites ((sum + 2) >> 2);
+ * a green centre takes the horizontal pair ((a + b + 1) >> 1) for its row's red / blue and
+ * the vertical pair for the other.  Planes R, G, B, rows flipped to bottom-up
+ * (fits_flip_top_to_bottom after debayer(), ser.c:730,758). */
+__global__ void __launch_bounds__(256) k_debayer_frames(SgDecode d, int pattern) {
+	const int64_t plane = (int64_t)d.W * d.H;
+	const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+	const int f = blockIdx.y;
+	if (i >= plane)
+		return;
+	const int ty = (int)(i / d.W), x = (int)(i - (int64_t)ty * d.W);	/* top-down */
+	const int bps = d.enc == SG_ENC_U8 ? 1 : 2;
+	const unsigned char *raw = d.raw + (int64_t)f * d.raw_frame_bytes;
+	bool bad = false;
+	auto at = [&](int yy, int xx) -> int { return sg_conv(raw + ((int64_t)yy * d.W + xx) * bps, d.enc, bad); };
+	int rgb[3] = {0, 0, 0};
+	if (ty >= 1 && ty <= d.H - 2 && x >= 1 && x <= d.W - 2) {
+		/* colour of (y, x): 0 R, 1 G, 2 B = cell[pattern][y & 1][x & 1] */
+		const int cell[4][2][2] = {{{0, 1}, {1, 2}}, {{2, 1}, {1, 0}}, {{1, 2}, {0, 1}}, {{1, 0}, {2, 1}}};
+		const int col = cell[pattern][ty & 1][x & 1];
+		const int c = at(ty, x);
+		if (col != 1) {
+			const int cross = (at(ty - 1, x) + at(ty, x - 1) + at(ty, x + 1) + at(ty + 1, x) + 2) >> 2;
+			const int diag = (at(ty - 1, x - 1) + at(ty - 1, x + 1) + at(ty + 1, x - 1) + at(ty + 1, x + 1) + 2) >> 2;
+			rgb[col] = c;
+			rgb[1] = cross;
+			rgb[2 - col] = diag;
+		} else {
+			const int rowc = cell[pattern][ty & 1][(x + 1) & 1];	/* this row's red / blue */
+			rgb[1] = c;
+			rgb[rowc] = (at(ty, x - 1) + at(ty, x + 1) + 1) >> 1;
+			rgb[2 - rowc] = (at(ty - 1, x) + at(ty + 1, x) + 1) >> 1;
+		}
+	}
+	const int64_t o = (int64_t)(d.H - 1 - ty) * d.W + x;
+	uint16_t *out = d.out + (int64_t)f * d.out_frame_stride;
+	for (int k = 0; k < 3; k++)
+		out[(int64_t)k * plane + o] = (uint16_t)rgb[k];
+	if (bad)
+		atomicOr(d.bad, 1u);
+}
+
 extern "C" int sg_seq_load_device(sg_ctx *ctx, int dev_index, const sg_seq *s, int first, int count,
 		uint16_t *d_frames, int64_t frame_stride, void *stream) {
 	if (!ctx || !s || !d_frames || dev_index < 0 || dev_index >= (int)ctx->dev.size() || first < 0 || count <= 0 ||
@@ -430,7 +492,12 @@ extern "C" int sg_seq_load_device(sg_ctx *ctx, int dev_index, const sg_seq *s, i
 		d.ser = s->kind == SG_SRC_SER;
 		d.nframes = n;
 		d.bad = (unsigned int *)dv.io_bad.p;
-		hipLaunchKernelGGL(k_decode_frames, dim3((unsigned)((plane_elems + 255) / 256), (unsigned)n), dim3(256), 0, st, d);
+		if (s->debayer >= 0)
+			hipLaunchKernelGGL(k_debayer_frames, dim3((unsigned)(((int64_t)s->width * s->height + 255) / 256), (unsigned)n),
+					dim3(256), 0, st, d, s->debayer);
+		else
+			hipLaunchKernelGGL(k_decode_frames, dim3((unsigned)((plane_elems + 255) / 256), (unsigned)n), dim3(256), 0,
+					st, d);
 		HIPCHK(hipGetLastError());
 	}
 	unsigned int bad = 0;

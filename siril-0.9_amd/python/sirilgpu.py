@@ -75,7 +75,7 @@ EXPORTS = ["sg_init", "sg_shutdown", "sg_last_error", "sg_stack_u16", "sg_stack_
            "sg_get_last_stats", "sg_register_dft_u16", "sg_register_dft_u16_device",
            "sg_synth_fill_device",
            "sg_seq_open_ser", "sg_seq_open_fits", "sg_seq_close", "sg_seq_get_info", "sg_seq_read_region",
-           "sg_seq_read_frame", "sg_seq_load_device", "sg_warp_u16", "sg_warp_u16_device"]
+           "sg_seq_read_frame", "sg_seq_load_device", "sg_seq_set_debayer", "sg_warp_u16", "sg_warp_u16_device"]
 # opencv_interpolation (src/core/siril.h:257-264)
 OPENCV_NEAREST, OPENCV_LINEAR, OPENCV_AREA, OPENCV_CUBIC, OPENCV_LANCZOS4 = range(5)
 
@@ -131,6 +131,8 @@ def load():
     lib.sg_seq_read_frame.restype = ctypes.c_int
     lib.sg_seq_load_device.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int64, P]
     lib.sg_seq_load_device.restype = ctypes.c_int
+    lib.sg_seq_set_debayer.argtypes = [P, ctypes.c_int]
+    lib.sg_seq_set_debayer.restype = ctypes.c_int
     lib.sg_warp_u16.argtypes = [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.c_int,
                                 ctypes.POINTER(ctypes.c_double), ctypes.c_int]
     lib.sg_warp_u16.restype = ctypes.c_int
@@ -139,6 +141,10 @@ def load():
     lib.sg_warp_u16_device.restype = ctypes.c_int
     _lib = lib
     return lib
+
+
+# sensor_pattern (src/core/siril.h:266-271)
+BAYER_RGGB, BAYER_BGGR, BAYER_GBRG, BAYER_GRBG = 0, 1, 2, 3
 
 
 class Seq:
@@ -183,6 +189,16 @@ class Seq:
 
     def __exit__(self, *a):
         self.close()
+
+    def set_debayer(self, pattern=-1):
+        """demosaic a CFA SER on device loads (bilinear); pattern BAYER_* or -1 = from the header"""
+        rc = self.lib.sg_seq_set_debayer(self.h, pattern)
+        if rc != SG_OK:
+            raise RuntimeError(f"sg_seq_set_debayer failed ({rc})")
+        info = SeqInfo()
+        self.lib.sg_seq_get_info(self.h, ctypes.byref(info))
+        self.info = info
+        self.shape = (info.nb_frames, info.nb_layers, info.height, info.width)
 
     def read_region(self, layer, index, x, y, w, h):
         """top-down band (seq_opened_read_region); returns (rc, array[h][w])"""

@@ -144,3 +144,64 @@ def test_stack_from_files(tmp_path, gpu_ctx, fmt):
         rej2, _ = gpu_ctx.stack_device(desc, d.data_ptr(), C * H * W, H * W, o.data_ptr(), 0, H)
         assert np.array_equal(o.cpu().numpy().view(np.uint16).reshape(C, H, W), ref)
         assert np.array_equal(rej2, rej_ref)
+
+
+# ---- CFA (Bayer) SER demosaiced on device loads (sg_seq_set_debayer, bilinear) ----
+
+def _bilinear_rule(bayer, tile):
+    """the per-pixel form k_debayer_frames uses (colour table + neighbour averages)"""
+    import debayer_ref as dr  # noqa: F401
+    H, W = bayer.shape
+    cell = [[[0, 1], [1, 2]], [[2, 1], [1, 0]], [[1, 2], [0, 1]], [[1, 0], [2, 1]]]
+    b = bayer.astype(np.int64)
+    out = np.zeros((H, W, 3), dtype=np.int64)
+    for y in range(1, H - 1):
+        for x in range(1, W - 1):
+            col = cell[tile][y & 1][x & 1]
+            if col != 1:
+                out[y, x, col] = b[y, x]
+                out[y, x, 1] = (b[y - 1, x] + b[y, x - 1] + b[y, x + 1] + b[y + 1, x] + 2) >> 2
+                out[y, x, 2 - col] = (b[y - 1, x - 1] + b[y - 1, x + 1] + b[y + 1, x - 1] + b[y + 1, x + 1] + 2) >> 2
+            else:
+                rowc = cell[tile][y & 1][(x + 1) & 1]
+                out[y, x, 1] = b[y, x]
+                out[y, x, rowc] = (b[y, x - 1] + b[y, x + 1] + 1) >> 1
+                out[y, x, 2 - rowc] = (b[y - 1, x] + b[y + 1, x] + 1) >> 1
+    return out.astype(np.uint16)
+
+
+@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+@pytest.mark.parametrize("shape", [(9, 12), (10, 13), (7, 7)])
+def test_bilinear_rule_matches_reference_loop(tile, shape):
+    """the kernel's per-pixel rule == the reference's row loop (restated literally)"""
+    import debayer_ref as dr
+    rng = np.random.default_rng(tile * 100 + shape[1])
+    bayer = rng.integers(0, 65536, size=shape).astype(np.uint16)
+    assert np.array_equal(_bilinear_rule(bayer, tile), dr.bayer_bilinear(bayer, tile))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", [8, 16])
+@pytest.mark.parametrize("color_id,forced", [(8, -1), (9, -1), (10, -1), (11, -1), (8, 3), (11, 2)])
+def test_debayer_load_device(tmp_path, gpu_ctx, color_id, forced, depth):
+    """CFA SER opened with demosaicing: the device decode == debayer() + flip of every frame"""
+    import torch
+    import debayer_ref as dr
+    N, H, W = 3, 21, 30
+    rng = np.random.default_rng(color_id * 10 + depth)
+    hi = 256 if depth == 8 else 65536
+    frames = rng.integers(0, hi, size=(N, 1, H, W)).astype(np.uint16)   # memory order (bottom-up)
+    path = str(tmp_path / f"cfa{color_id}.ser")
+    write_ser(path, frames, depth=depth, color_id=color_id)
+    tile = forced if forced >= 0 else {8: dr.BAYER_RGGB, 9: dr.BAYER_GRBG, 10: dr.BAYER_GBRG, 11: dr.BAYER_BGGR}[color_id]
+    with sg.Seq.open_ser(path) as seq:
+        seq.set_debayer(forced)
+        assert seq.shape == (N, 3, H, W)
+        rc, _ = seq.read_region(0, 0, 0, 0, W, 4)
+        assert rc != 0                                   # host reads are not provided
+        d = torch.zeros(N * 3 * H * W, dtype=torch.int16, device="cuda")
+        gpu_ctx.load_seq_device(seq, d.data_ptr())
+        got = d.cpu().numpy().view(np.uint16).reshape(N, 3, H, W)
+    for i in range(N):
+        topdown = frames[i, 0, ::-1, :]                  # the SER file's row order
+        assert np.array_equal(got[i], dr.debayer_frame_memory_order(topdown, tile)), i
