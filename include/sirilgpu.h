@@ -125,6 +125,21 @@ typedef struct {
 int sg_get_last_stats(const sg_ctx *ctx, sg_stack_stats *st);
 
 /*
+ * Per-frame normalisation statistics: location / scale of layer 0 as
+ * statistics(fit, 0, NULL, STATS_IKSS, STATS_ZERO_NULLCHECK) computes them
+ * (src/algos/statistics.c:152-326; the imstats _compute_normalization_for_image reads,
+ * src/stacking/stacking.c:79-123).  d_frames: nframes frames [C][H][W] in Siril memory order
+ * at frame_stride elements (0 = C*H*W); location / scale: host arrays [nframes].
+ * 0, or SG_ERR_GENERIC when a frame has no non-zero pixel (statistics() returns NULL).
+ */
+int sg_frame_stats_ikss_device(sg_ctx *ctx, int dev_index, const uint16_t *d_frames, int nframes, int C,
+		int H, int W, int64_t frame_stride, double *location, double *scale, void *stream);
+/* compute_normalization (src/stacking/stacking.c:125-190): offset / mul / scale [nframes]
+ * from per-frame location / scale (host arithmetic; ref_image -1 = 0) */
+int sg_compute_normalization(int mode, int nframes, int ref_image, const double *location,
+		const double *scale_in, double *offset, double *mul, double *scale);
+
+/*
  * DFT registration: replaces register_shift_dft (src/registration/registration.c:182-400).
  * d_sel / sel hold nframes bottom-up S x S selections (what seq_read_frame_part returns,
  * src/io/sequence.c:567-609).  included may be NULL (process_all_frames).  Outputs the

@@ -73,6 +73,9 @@ int or_stack_addmax(const or_seq *seq, const int *shiftx, const int *shifty, uin
 int or_stack_addmin(const or_seq *seq, const int *shiftx, const int *shifty, uint16_t *out);
 
 /* normalisation coefficients from per-frame (location, scale), stacking.c:79-190 */
+/* statistics(fit, 0, NULL, STATS_IKSS, STATS_ZERO_NULLCHECK) -> location / scale
+ * (src/algos/statistics.c:152-326), or_statistics.c */
+int or_statistics_ikss(const uint16_t *frame, int C, int H, int W, double *location, double *scale);
 int or_compute_normalization(int nb, int ref_image, int mode, const double *location,
 		const double *scalev, double *offset, double *mul, double *scale);
 

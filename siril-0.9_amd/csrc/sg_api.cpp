@@ -79,7 +79,7 @@ extern "C" void sg_shutdown(sg_ctx *ctx) {
 		SgBuf *bufs[] = {&d.flag_list, &d.flag_map, &d.flag_count, &d.rej, &d.sum_buf, &d.maxim,
 			&d.shifts, &d.norm, &d.tables, &d.scratch, &d.frames, &d.out, &d.reg_sel, &d.reg_spec,
 			&d.reg_work, &d.reg_tw, &d.reg_best, &d.reg_qbuf, &d.reg_qacc, &d.redo, &d.zeros,
-			&d.io_raw, &d.io_bad, &d.warp_tab};
+			&d.io_raw, &d.io_bad, &d.warp_tab, &d.stats_buf};
 		for (SgBuf *b : bufs)
 			if (b->p)
 				(void)hipFree(b->p);

@@ -20,7 +20,7 @@ struct SgDevice {
 	int id = 0;
 	hipStream_t stream = nullptr;
 	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-	SgBuf flag_list, flag_map, flag_count, rej, sum_buf, maxim, shifts, norm, tables, scratch, frames, out;
+	SgBuf flag_list, flag_map, flag_count, rej, sum_buf, maxim, shifts, norm, tables, scratch, frames, out, stats_buf;
 	/* registration workspaces (sg_register.hip) */
 	SgBuf reg_sel, reg_spec, reg_work, reg_tw, reg_best, reg_qbuf, reg_qacc;
 	SgBuf redo;	/* redo list of the histogram stacking path */

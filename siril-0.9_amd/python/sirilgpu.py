@@ -75,7 +75,8 @@ EXPORTS = ["sg_init", "sg_shutdown", "sg_last_error", "sg_stack_u16", "sg_stack_
            "sg_get_last_stats", "sg_register_dft_u16", "sg_register_dft_u16_device",
            "sg_synth_fill_device",
            "sg_seq_open_ser", "sg_seq_open_fits", "sg_seq_close", "sg_seq_get_info", "sg_seq_read_region",
-           "sg_seq_read_frame", "sg_seq_load_device", "sg_seq_set_debayer", "sg_warp_u16", "sg_warp_u16_device"]
+           "sg_seq_read_frame", "sg_seq_load_device", "sg_seq_set_debayer", "sg_warp_u16", "sg_warp_u16_device",
+           "sg_frame_stats_ikss_device", "sg_compute_normalization"]
 # opencv_interpolation (src/core/siril.h:257-264)
 OPENCV_NEAREST, OPENCV_LINEAR, OPENCV_AREA, OPENCV_CUBIC, OPENCV_LANCZOS4 = range(5)
 
@@ -131,6 +132,11 @@ def load():
     lib.sg_seq_read_frame.restype = ctypes.c_int
     lib.sg_seq_load_device.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int64, P]
     lib.sg_seq_load_device.restype = ctypes.c_int
+    lib.sg_frame_stats_ikss_device.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_int, ctypes.c_int64, P, P, P]
+    lib.sg_frame_stats_ikss_device.restype = ctypes.c_int
+    lib.sg_compute_normalization.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, P, P]
+    lib.sg_compute_normalization.restype = ctypes.c_int
     lib.sg_seq_set_debayer.argtypes = [P, ctypes.c_int]
     lib.sg_seq_set_debayer.restype = ctypes.c_int
     lib.sg_warp_u16.argtypes = [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.c_int,
@@ -303,6 +309,17 @@ class Context:
                                          frame_stride, ctypes.c_void_p(stream) if stream else None)
         self.check(rc, "sg_seq_load_device")
 
+    def frame_stats_ikss(self, d_frames, nframes, C, H, W, frame_stride=0, dev_index=0, stream=None):
+        """per-frame IKSS location / scale of layer 0 (sg_frame_stats_ikss_device);
+        returns (rc, location[nframes], scale[nframes])"""
+        loc = np.zeros(nframes, dtype=np.float64)
+        scl = np.zeros(nframes, dtype=np.float64)
+        rc = self.lib.sg_frame_stats_ikss_device(self.ctx, dev_index, ctypes.c_void_p(d_frames), nframes, C, H, W,
+                                                 frame_stride, loc.ctypes.data_as(ctypes.c_void_p),
+                                                 scl.ctypes.data_as(ctypes.c_void_p),
+                                                 ctypes.c_void_p(stream) if stream else None)
+        return rc, loc, scl
+
     def warp(self, image, hom, out_size=None, interpolation=OPENCV_LINEAR):
         """cvTransformImage on a memory-order image [C][H][W]; hom = the 3x3 homography
         (Homography h00..h22), out_size = (ref.x, ref.y)"""
@@ -390,3 +407,18 @@ class Context:
         rc = self.lib.sg_synth_fill_device(self.ctx, dev_index, ctypes.c_void_p(d_frames), nframes, C, H, W,
                                            row_begin, row_end, seed, maxshift, frame_stride, None)
         self.check(rc, "sg_synth_fill_device")
+
+
+def compute_normalization(mode, location, scale, ref_image=0):
+    """compute_normalization (stacking.c:125-190) through the C ABI: (offset, mul, scale)"""
+    lib = load()
+    n = len(location)
+    loc = np.ascontiguousarray(location, dtype=np.float64)
+    sc = np.ascontiguousarray(scale, dtype=np.float64)
+    off, mul, so = (np.zeros(n), np.zeros(n), np.zeros(n))
+    rc = lib.sg_compute_normalization(mode, n, ref_image, loc.ctypes.data_as(ctypes.c_void_p),
+                                      sc.ctypes.data_as(ctypes.c_void_p), off.ctypes.data_as(ctypes.c_void_p),
+                                      mul.ctypes.data_as(ctypes.c_void_p), so.ctypes.data_as(ctypes.c_void_p))
+    if rc != SG_OK:
+        raise RuntimeError(f"sg_compute_normalization failed ({rc})")
+    return off, mul, so

@@ -54,6 +54,8 @@ def load():
     lib.or_quality_estimate.argtypes = [P, ctypes.c_int, ctypes.c_int]
     lib.or_quality_estimate.restype = ctypes.c_double
     lib.or_compute_normalization.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, P, P]
+    lib.or_statistics_ikss.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P]
+    lib.or_statistics_ikss.restype = ctypes.c_int
     _lib = lib
     return lib
 
@@ -189,3 +191,14 @@ def compute_normalization(mode, location, scalev, ref_image=0):
     off, mul, scale = np.zeros(n), np.ones(n), np.ones(n)
     lib.or_compute_normalization(n, ref_image, mode, _p(loc), _p(sc), _p(off), _p(mul), _p(scale))
     return off, mul, scale
+
+
+def statistics_ikss(frame):
+    """frame [C][H][W] u16 -> (rc, location, scale) of layer 0 (statistics.c IKSS)"""
+    lib = load()
+    f = np.ascontiguousarray(frame, dtype=np.uint16)
+    C, H, W = f.shape
+    loc = ctypes.c_double(0.0)
+    sc = ctypes.c_double(0.0)
+    rc = lib.or_statistics_ikss(_p(f), C, H, W, ctypes.byref(loc), ctypes.byref(sc))
+    return rc, loc.value, sc.value

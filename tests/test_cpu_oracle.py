@@ -233,3 +233,41 @@ int main(void) {
     subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-I", inc, str(src), "-o", str(exe), "-lm"], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
+
+
+def test_add_repeat_matches_sequential_loop(tmp_path):
+    """sg_repadd.h (the device BWMV's run-length summation) == the literal sequential loop,
+    including half-ulp ties, signed zeros and binade crossings"""
+    src = tmp_path / "ra.c"
+    src.write_text(r'''
+#include <stdio.h>
+#include <string.h>
+#include "sg_repadd.h"
+static uint64_t s = 88172645463325252ull;
+static uint64_t rnd(void) { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; }
+static double rdouble(void) { double m = (double)(rnd() >> 11) / 9007199254740992.0; int e = (int)(rnd() % 60) - 30;
+	return ldexp(m + 0.5, e) * ((rnd() & 1) ? -1 : 1); }
+int main(void) {
+	int bad = 0;
+	for (int it = 0; it < 60000; it++) {
+		double acc = (it % 5 == 0) ? 0.0 : rdouble(), t = rdouble();
+		if (it % 7 == 0) { int e = sg_ra_exp(acc == 0 ? 1.0 : acc);
+			t = ldexp((double)(rnd() % 64) + 0.5, e - 52) * ((rnd() & 1) ? -1 : 1); }
+		if (it % 11 == 0) t = acc * 1e-3;
+		if (it % 13 == 0) t = (rnd() & 1) ? 0.0 : -0.0;
+		if (it % 17 == 0) acc = (rnd() & 1) ? 0.0 : -0.0;
+		uint64_t k = rnd() % (it % 3 == 0 ? 100000 : 2000);
+		double lit = acc;
+		for (uint64_t i = 0; i < k; i++) lit = lit + t;
+		double fast = sg_add_repeat(acc, t, k);
+		if (memcmp(&lit, &fast, 8) != 0) bad++;
+	}
+	printf("bad=%d\n", bad);
+	return bad != 0;
+}
+''')
+    exe = tmp_path / "ra"
+    inc = os.path.join(ROOT, "siril-0.9_amd", "csrc")
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-I", inc, str(src), "-o", str(exe), "-lm"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout
