@@ -10,7 +10,7 @@
  * multiple of u and every later step adds the even neighbour of t/u.  So two equal
  * consecutive increments are followed by the same increment until a sum would leave the
  * binade (kept one ulp away from the boundary, where the unit changes); there one step is
- * done literally.  Checked against the literal loop by tests/test_cpu_oracle.py.
+ * done literally.  Checked against the literal loop by the CPU test suite (tests/).
  */
 #ifndef SG_REPADD_H
 #define SG_REPADD_H

@@ -17,7 +17,7 @@
  *     sg_add_repeat (sg_repadd.h), which reproduces the sequential double sum exactly.
  * All double expressions are written as the reference writes them (no contraction), so
  * location / scale equal the reference's bit for bit (tests/test_gpu_stats.py against the
- * oracle's restatement).
+ * CPU restatement in tests/).
  */
 #include "sg_common.hpp"
 #include "sg_ctx.hpp"
