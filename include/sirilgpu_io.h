@@ -56,6 +56,38 @@ int sg_seq_load_device(sg_ctx *ctx, int dev_index, const sg_seq *seq, int first,
 enum { SG_BAYER_RGGB = 0, SG_BAYER_BGGR = 1, SG_BAYER_GBRG = 2, SG_BAYER_GRBG = 3 };
 int sg_seq_set_debayer(sg_seq *seq, int pattern);
 
+/*
+ * Siril .seq files (readseqfile / writeseqfile, src/io/seqfile.c:43-357): the sequence
+ * description with the cached per-image statistics (I lines: mean median sigma avgDev mad
+ * sqrtbwmv location scale min max, written with %g) and the registration data (R lines).
+ * Host-only.  The selection count is recomputed from the inclusion flags on read, as the
+ * reference does.
+ */
+typedef struct sg_seqfile sg_seqfile;
+enum { SG_SEQFILE_REGULAR = 0, SG_SEQFILE_SER = 1, SG_SEQFILE_FILM = 2 };
+typedef struct {
+	char name[512];
+	int beg, number, selnum, fixed, reference_image;
+	int type;		/* SG_SEQFILE_* (T line) */
+	int nb_layers;		/* L line, -1 when absent */
+} sg_seqfile_info;
+/* path with or without ".seq"; 0, SG_ERR_READ (missing / malformed file) */
+int sg_seqfile_read(const char *path, sg_seqfile **out);
+int sg_seqfile_create(const char *name, int beg, int number, int fixed, int reference_image, int type,
+		int nb_layers, sg_seqfile **out);
+void sg_seqfile_free(sg_seqfile *sf);
+int sg_seqfile_get_info(const sg_seqfile *sf, sg_seqfile_info *info);
+/* arrays [number] (stats: [number][10]); any pointer may be NULL */
+int sg_seqfile_get_images(const sg_seqfile *sf, int *filenum, int *incl, int *has_stats, double *stats);
+/* stats: 10 values, or NULL for an image without cached statistics */
+int sg_seqfile_set_image(sg_seqfile *sf, int index, int filenum, int incl, const double *stats);
+/* 0, 1 when the layer has no R lines, SG_ERR_GENERIC; arrays [number], any may be NULL */
+int sg_seqfile_get_registration(const sg_seqfile *sf, int layer, int *shiftx, int *shifty,
+		float *rot_centre_x, float *rot_centre_y, float *angle, float *fwhm, double *quality);
+int sg_seqfile_set_registration(sg_seqfile *sf, int layer, const int *shiftx, const int *shifty,
+		const double *quality);
+int sg_seqfile_write(const sg_seqfile *sf, const char *path);
+
 #ifdef __cplusplus
 }
 #endif

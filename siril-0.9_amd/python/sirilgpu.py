@@ -76,7 +76,9 @@ EXPORTS = ["sg_init", "sg_shutdown", "sg_last_error", "sg_stack_u16", "sg_stack_
            "sg_synth_fill_device",
            "sg_seq_open_ser", "sg_seq_open_fits", "sg_seq_close", "sg_seq_get_info", "sg_seq_read_region",
            "sg_seq_read_frame", "sg_seq_load_device", "sg_seq_set_debayer", "sg_warp_u16", "sg_warp_u16_device",
-           "sg_frame_stats_ikss_device", "sg_compute_normalization"]
+           "sg_frame_stats_ikss_device", "sg_compute_normalization", "sg_seqfile_read", "sg_seqfile_create",
+           "sg_seqfile_free", "sg_seqfile_get_info", "sg_seqfile_get_images", "sg_seqfile_set_image",
+           "sg_seqfile_get_registration", "sg_seqfile_set_registration", "sg_seqfile_write"]
 # opencv_interpolation (src/core/siril.h:257-264)
 OPENCV_NEAREST, OPENCV_LINEAR, OPENCV_AREA, OPENCV_CUBIC, OPENCV_LANCZOS4 = range(5)
 
@@ -137,6 +139,17 @@ def load():
     lib.sg_frame_stats_ikss_device.restype = ctypes.c_int
     lib.sg_compute_normalization.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, P, P]
     lib.sg_compute_normalization.restype = ctypes.c_int
+    lib.sg_seqfile_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(P)]
+    lib.sg_seqfile_create.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_int, ctypes.c_int, ctypes.POINTER(P)]
+    lib.sg_seqfile_free.argtypes = [P]
+    lib.sg_seqfile_free.restype = None
+    lib.sg_seqfile_get_info.argtypes = [P, ctypes.POINTER(SeqFileInfo)]
+    lib.sg_seqfile_get_images.argtypes = [P, P, P, P, P]
+    lib.sg_seqfile_set_image.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
+    lib.sg_seqfile_get_registration.argtypes = [P, ctypes.c_int, P, P, P, P, P, P, P]
+    lib.sg_seqfile_set_registration.argtypes = [P, ctypes.c_int, P, P, P]
+    lib.sg_seqfile_write.argtypes = [P, ctypes.c_char_p]
     lib.sg_seq_set_debayer.argtypes = [P, ctypes.c_int]
     lib.sg_seq_set_debayer.restype = ctypes.c_int
     lib.sg_warp_u16.argtypes = [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, ctypes.c_int, ctypes.c_int,
@@ -147,6 +160,99 @@ def load():
     lib.sg_warp_u16_device.restype = ctypes.c_int
     _lib = lib
     return lib
+
+
+class SeqFileInfo(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 512), ("beg", ctypes.c_int), ("number", ctypes.c_int),
+                ("selnum", ctypes.c_int), ("fixed", ctypes.c_int), ("reference_image", ctypes.c_int),
+                ("type", ctypes.c_int), ("nb_layers", ctypes.c_int)]
+
+
+SEQFILE_REGULAR, SEQFILE_SER, SEQFILE_FILM = 0, 1, 2
+
+
+class SeqFile:
+    """A Siril .seq file (include/sirilgpu_io.h sg_seqfile_*): host-only."""
+
+    def __init__(self, handle):
+        self.lib = load()
+        self.h = handle
+
+    @classmethod
+    def read(cls, path):
+        lib = load()
+        h = ctypes.c_void_p()
+        rc = lib.sg_seqfile_read(os.fsencode(path), ctypes.byref(h))
+        if rc != SG_OK:
+            raise OSError(f"sg_seqfile_read({path}) failed ({rc})")
+        return cls(h)
+
+    @classmethod
+    def create(cls, name, number, beg=1, fixed=5, reference_image=-1, type=SEQFILE_REGULAR, nb_layers=1):
+        lib = load()
+        h = ctypes.c_void_p()
+        rc = lib.sg_seqfile_create(name.encode(), beg, number, fixed, reference_image, type, nb_layers, ctypes.byref(h))
+        if rc != SG_OK:
+            raise RuntimeError(f"sg_seqfile_create failed ({rc})")
+        return cls(h)
+
+    def close(self):
+        if self.h:
+            self.lib.sg_seqfile_free(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def info(self):
+        i = SeqFileInfo()
+        self.lib.sg_seqfile_get_info(self.h, ctypes.byref(i))
+        return i
+
+    def images(self):
+        n = self.info().number
+        fn, inc, hs = (np.zeros(n, np.int32) for _ in range(3))
+        st = np.zeros((n, 10), np.float64)
+        self.lib.sg_seqfile_get_images(self.h, fn.ctypes.data_as(ctypes.c_void_p), inc.ctypes.data_as(ctypes.c_void_p),
+                                       hs.ctypes.data_as(ctypes.c_void_p), st.ctypes.data_as(ctypes.c_void_p))
+        return fn, inc, hs, st
+
+    def set_image(self, index, filenum, incl, stats=None):
+        st = None if stats is None else np.ascontiguousarray(stats, dtype=np.float64)
+        rc = self.lib.sg_seqfile_set_image(self.h, index, filenum, incl,
+                                           None if st is None else st.ctypes.data_as(ctypes.c_void_p))
+        if rc != SG_OK:
+            raise RuntimeError("sg_seqfile_set_image failed")
+
+    def registration(self, layer):
+        """(rc, shiftx, shifty, rot_centre_x, rot_centre_y, angle, fwhm, quality); rc 1 = no data"""
+        n = self.info().number
+        sx, sy = np.zeros(n, np.int32), np.zeros(n, np.int32)
+        fl = [np.zeros(n, np.float32) for _ in range(4)]
+        q = np.zeros(n, np.float64)
+        rc = self.lib.sg_seqfile_get_registration(self.h, layer, sx.ctypes.data_as(ctypes.c_void_p),
+                                                  sy.ctypes.data_as(ctypes.c_void_p),
+                                                  *[a.ctypes.data_as(ctypes.c_void_p) for a in fl],
+                                                  q.ctypes.data_as(ctypes.c_void_p))
+        return (rc, sx, sy, *fl, q)
+
+    def set_registration(self, layer, shiftx, shifty, quality=None):
+        sx = np.ascontiguousarray(shiftx, dtype=np.int32)
+        sy = np.ascontiguousarray(shifty, dtype=np.int32)
+        q = None if quality is None else np.ascontiguousarray(quality, dtype=np.float64)
+        rc = self.lib.sg_seqfile_set_registration(self.h, layer, sx.ctypes.data_as(ctypes.c_void_p),
+                                                  sy.ctypes.data_as(ctypes.c_void_p),
+                                                  None if q is None else q.ctypes.data_as(ctypes.c_void_p))
+        if rc != SG_OK:
+            raise RuntimeError("sg_seqfile_set_registration failed")
+
+    def write(self, path):
+        rc = self.lib.sg_seqfile_write(self.h, os.fsencode(path))
+        if rc != SG_OK:
+            raise OSError(f"sg_seqfile_write({path}) failed ({rc})")
 
 
 # sensor_pattern (src/core/siril.h:266-271)
