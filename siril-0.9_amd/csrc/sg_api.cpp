@@ -30,6 +30,7 @@ template <int REJ, int NORM>
 __global__ void k_stack_hist(SgStackParams p, unsigned int *redo_count, unsigned int *redo_list);
 void sg_dbg_why_dump(hipStream_t s);
 __global__ void k_stack_replay(SgStackParams p);
+__global__ void k_redo_to_literal(SgStackParams p, const unsigned int *list, const unsigned int *count);
 __global__ void k_stack_reduce(SgStackParams p);
 __global__ void k_sum_finalize(SgStackParams p);
 __global__ void k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *scratch, int phase);
@@ -421,7 +422,18 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 			ctx->stats.path = 1;
 			ctx->stats.main_kernel_blocks = (int)nblk;
 			ctx->stats.launches = 1;
-			if (nredo) {
+			/* the histogram path's redo pixels: a few go straight to the wave-per-pixel replay
+			 * (k_stack_replay below: every sample of a pixel gathered by one wave at once);
+			 * many go through the sorted kernel, 64 pixels per workgroup */
+			bool to_replay = N <= SG_REPLAY_MAXN && nredo <= SG_REDO_REPLAY_MAX;
+			if (const char *e = getenv("SG_REDO_REPLAY"))	/* A/B knob: 0 sorted kernel, 2 replay always */
+				to_replay = atoi(e) == 2 ? N <= SG_REPLAY_MAXN : (to_replay && atoi(e) != 0);
+			if (nredo && to_replay) {
+				hipLaunchKernelGGL(k_redo_to_literal, dim3((nredo + 255) / 256), dim3(256), 0, s, p,
+						(const unsigned int *)redo_list, (const unsigned int *)redo_count);
+				HIPCHK(hipGetLastError());
+				ctx->stats.launches++;
+			} else if (nredo) {
 				HIPCHK(launch_sorted(nreg, true, dim3((nredo + SG_TILE_W - 1) / SG_TILE_W), lds, s, p,
 						redo_list, redo_count));
 				ctx->stats.launches++;

@@ -14,6 +14,7 @@ enum { SG_CLS_OK = 0, SG_CLS_LITERAL = 1, SG_CLS_CHAIN = 2, SG_CLS_DONE = 3 };
 /* k_stack_replay: waves per block (one pixel per wave, ~18 KB of LDS each), max frames */
 #define SG_REPLAY_WAVES 2
 #define SG_REPLAY_MAXN 2048
+#define SG_REDO_REPLAY_MAX 32768	/* histogram redo pixels sent straight to k_stack_replay (measured: 22 k faster there, 113 k slower) */
 
 /* everything the stacking kernels need, passed by value */
 struct SgStackParams {
