@@ -1249,17 +1249,21 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 }
 
 /* the histogram path's redo list queued for k_stack_replay / k_stack_literal: class
- * LITERAL, appended to the flag list the sorted kernel would have appended them to */
+ * LITERAL, appended to the flag list the sorted kernel would have appended them to.  The
+ * count is read on the device; a list longer than maxn is left to the sorted kernel. */
 __global__ void __launch_bounds__(256)
-k_redo_to_literal(SgStackParams p, const unsigned int *__restrict__ list, const unsigned int *__restrict__ count) {
-	const unsigned int i = blockIdx.x * 256 + threadIdx.x;
-	if (i >= *count)
+k_redo_to_literal(SgStackParams p, const unsigned int *__restrict__ list, const unsigned int *__restrict__ count,
+		unsigned int maxn) {
+	const unsigned int n = *count;
+	if (n > maxn)
 		return;
-	const unsigned int pix = list[i];
-	p.flag_map[pix] = SG_CLS_LITERAL;
-	const unsigned int slot = atomicAdd(p.flag_count, 1u);
-	if (slot < p.flag_cap)
-		p.flag_list[slot] = pix;
+	for (unsigned int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+		const unsigned int pix = list[i];
+		p.flag_map[pix] = SG_CLS_LITERAL;
+		const unsigned int slot = atomicAdd(p.flag_count, 1u);
+		if (slot < p.flag_cap)
+			p.flag_list[slot] = pix;
+	}
 }
 
 __global__ void __launch_bounds__(64 * SG_REPLAY_WAVES)
