@@ -26,6 +26,7 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#include <type_traits>
 #include <vector>
 
 typedef double2 sg_c64;
@@ -185,6 +186,82 @@ __device__ __forceinline__ void sg_lds_fft(sg_c64 *buf, int n, int logn, int nb,
 	}
 }
 
+/* The same transform with its first pass reading the input straight from memory and its
+ * last pass writing the output straight to memory (ld(b, i) / st(b, i, v): element i of
+ * transform b): two LDS round trips and four barriers fewer than staging through LDS.
+ * Work items of these two passes are batch-minor (item t -> b = t % nb), so neighbouring
+ * lanes of a column strip touch neighbouring columns of one row (64-B row segments).
+ * The arithmetic is that of sg_lds_fft, operation for operation (n < 16, a single pass:
+ * staged through LDS). */
+template <class LD, class ST>
+__device__ __forceinline__ void sg_fft_io(sg_c64 *buf, int n, int nb, int bstride, const sg_c64 *__restrict__ tw,
+		bool inv, LD ld, ST st) {
+	if (n < 16) {
+		for (int t = threadIdx.x; t < nb * n; t += blockDim.x)
+			buf[(size_t)(t % nb) * bstride + sg_pad(t / nb)] = ld(t % nb, t / nb);
+		sg_lds_fft(buf, n, 0, nb, bstride, tw, inv);
+		for (int t = threadIdx.x; t < nb * n; t += blockDim.x)
+			st(t % nb, t / nb, buf[(size_t)(t % nb) * bstride + sg_pad(t / nb)]);
+		return;
+	}
+	/* first pass: radix 8, Ns = 1 (no twiddles) */
+	{
+		const int per = n >> 3, items = nb * per;
+		const int t = threadIdx.x;
+		if (t < items) {
+			const int b = t % nb, j = t / nb;
+			sg_c64 v[8];
+#pragma unroll
+			for (int r = 0; r < 8; r++)
+				v[r] = ld(b, j + r * per);
+			sg_dft_small<8, 8>(v, inv);
+			sg_c64 *y = buf + (size_t)b * bstride;
+#pragma unroll
+			for (int r = 0; r < 8; r++)
+				y[sg_pad(j * 8 + r)] = v[r];
+		}
+	}
+	__syncthreads();
+	int Ns = 8;
+	/* middle passes in LDS (sg_lds_fft's radix sequence: 8 while n / Ns >= 8, then 4 or 2),
+	 * leaving the last one */
+	while (n / Ns > 8) {
+		sg_stockham_pass<8>(buf, n, nb, bstride, Ns, tw, inv);
+		Ns *= 8;
+	}
+	const int rl = n / Ns;
+	auto last = [&](auto RC) {
+		constexpr int R = decltype(RC)::value;
+		constexpr int MAXI = 8 / R;
+		const int per = n / R, items = nb * per;
+#pragma unroll
+		for (int it = 0; it < MAXI; it++) {
+			const int t = threadIdx.x + it * blockDim.x;
+			if (t < items) {
+				const int b = t % nb, j = t / nb;
+				const sg_c64 *x = buf + (size_t)b * bstride;
+				sg_c64 v[R];
+#pragma unroll
+				for (int r = 0; r < R; r++)
+					v[r] = x[sg_pad(j + r * per)];
+#pragma unroll
+				for (int r = 1; r < R; r++)
+					v[r] = sg_cmul(v[r], sg_twiddle(tw, n, r * j, inv));
+				sg_dft_small<R, R>(v, inv);
+#pragma unroll
+				for (int r = 0; r < R; r++)
+					st(b, j + r * per, v[r]);
+			}
+		}
+	};
+	if (rl == 8)
+		last(std::integral_constant<int, 8>());
+	else if (rl == 4)
+		last(std::integral_constant<int, 4>());
+	else
+		last(std::integral_constant<int, 2>());
+}
+
 /* row pass of the forward transform of a + i b (b = -1: zero imaginary part) */
 __global__ void __launch_bounds__(512)
 k_reg_rows_fwd(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const int *__restrict__ fb,
@@ -196,12 +273,11 @@ k_reg_rows_fwd(const uint16_t *__restrict__ sel, const int *__restrict__ fa, con
 	const uint16_t *pa = sel + (size_t)fa[pair] * plane + (size_t)row * S;
 	const int b = fb[pair];
 	const uint16_t *pb = b >= 0 ? sel + (size_t)b * plane + (size_t)row * S : nullptr;
-	for (int j = threadIdx.x; j < S; j += blockDim.x)
-		buf[sg_pad(j)] = make_double2((double)pa[j], pb ? (double)pb[j] : 0.0);
-	sg_lds_fft(buf, S, logS, 1, S, tw, false);
 	sg_c64 *out = work + (size_t)pair * plane + (size_t)row * S;
-	for (int j = threadIdx.x; j < S; j += blockDim.x)
-		out[j] = buf[sg_pad(j)];
+	(void)logS;
+	sg_fft_io(buf, S, 1, S, tw, false,
+			[&](int, int i) { return make_double2((double)pa[i], pb ? (double)pb[i] : 0.0); },
+			[&](int, int i, sg_c64 v) { out[i] = v; });
 }
 
 /* column pass (forward or inverse) over strips of CW adjacent columns */
@@ -212,15 +288,22 @@ k_reg_cols(sg_c64 *__restrict__ work, int S, int logS, int CW, const sg_c64 *__r
 	const int x0 = blockIdx.x * CW, pair = blockIdx.y;
 	const int bstride = SG_PADN(S) + 1;
 	sg_c64 *base = work + (size_t)pair * S * S + x0;
-	for (int idx = threadIdx.x; idx < S * CW; idx += blockDim.x) {
-		const int r = idx / CW, c = idx - r * CW;
-		buf[c * bstride + sg_pad(r)] = base[(size_t)r * S + c];
-	}
-	sg_lds_fft(buf, S, logS, CW, bstride, tw, inverse != 0);
-	for (int idx = threadIdx.x; idx < S * CW; idx += blockDim.x) {
-		const int r = idx / CW, c = idx - r * CW;
-		base[(size_t)r * S + c] = buf[c * bstride + sg_pad(r)];
-	}
+	(void)logS;
+	sg_fft_io(buf, S, CW, bstride, tw, inverse != 0, [&](int c, int r) { return base[(size_t)r * S + c]; },
+			[&](int c, int r, sg_c64 v) { base[(size_t)r * S + c] = v; });
+}
+
+/* one term of the packed cross-power spectrum at (ky, kx): zk = Z(ky, kx),
+ * zm = Z(-ky, -kx), rk = R(ky, kx).  F_a = (zk + conj zm) / 2, F_b = (zk - conj zm) / 2i;
+ * result R conj F_a + i R conj F_b.  The term at (-ky, -kx) is this function with zk and
+ * zm swapped (the negated differences are exact, products and sums commute), so every
+ * element is formed by the same expression. */
+__device__ __forceinline__ sg_c64 sg_xpower_at(sg_c64 zk, sg_c64 zm, sg_c64 rk) {
+	const double ar = 0.5 * (zk.x + zm.x), ai = 0.5 * (zk.y - zm.y);
+	const double br = 0.5 * (zk.y + zm.y), bi = -0.5 * (zk.x - zm.x);
+	const double pr = rk.x * ar + rk.y * ai, pi = rk.y * ar - rk.x * ai;
+	const double qr = rk.x * br + rk.y * bi, qi = rk.y * br - rk.x * bi;
+	return make_double2(pr - qi, pi + qr);
 }
 
 /* separate the packed spectra and form the packed cross-power spectrum, in place:
@@ -255,10 +338,11 @@ k_reg_xpower(sg_c64 *__restrict__ work, const sg_c64 *__restrict__ spec, int S) 
 	}
 }
 
-/* cross-power fused into the inverse ROW pass: workgroup (ky, pair) holds rows ky and
- * -ky (mod S) of the forward spectrum in LDS, forms the packed cross-power spectrum of
- * both (each (k, -k) pair once, as k_reg_xpower), runs the inverse row FFT of both and
- * writes them back.  The inverse column pass then only reads (k_reg_cols_inv_argmax). */
+/* cross-power fused into the inverse ROW pass: workgroup (ky, pair) transforms rows ky
+ * and -ky (mod S) together (the rows whose cross-power terms need each other): the first
+ * FFT pass forms each term from the forward spectrum and the reference spectrum as it
+ * reads them (sg_xpower_at), the last writes the inverse rows back in place.  The
+ * inverse column pass then only reads (k_reg_cols_inv_argmax). */
 __global__ void __launch_bounds__(1024)
 k_reg_xpower_rows_inv(sg_c64 *__restrict__ work, const sg_c64 *__restrict__ spec, int S, int logS,
 		const sg_c64 *__restrict__ tw) {
@@ -268,38 +352,17 @@ k_reg_xpower_rows_inv(sg_c64 *__restrict__ work, const sg_c64 *__restrict__ spec
 	const int my = (S - ky) & (S - 1);
 	const bool self = my == ky;
 	sg_c64 *Z = work + (size_t)pair * S * S;
-	sg_c64 *A = buf, *Bv = self ? buf : buf + SG_PADN(S);
-	for (int j = threadIdx.x; j < S; j += blockDim.x) {
-		A[sg_pad(j)] = Z[(size_t)ky * S + j];
-		if (!self)
-			Bv[sg_pad(j)] = Z[(size_t)my * S + j];
-	}
-	__syncthreads();
-	for (int kx = threadIdx.x; kx < S; kx += blockDim.x) {
-		const int mx = (S - kx) & (S - 1);
-		if (self && mx < kx)
-			continue;
-		const sg_c64 zk = A[sg_pad(kx)], zm = Bv[sg_pad(mx)];
-		const double ar = 0.5 * (zk.x + zm.x), ai = 0.5 * (zk.y - zm.y);
-		const double br = 0.5 * (zk.y + zm.y), bi = -0.5 * (zk.x - zm.x);
-		const sg_c64 rk = spec[(size_t)ky * S + kx], rm = spec[(size_t)my * S + mx];
-		{
-			const double pr = rk.x * ar + rk.y * ai, pi = rk.y * ar - rk.x * ai;
-			const double qr = rk.x * br + rk.y * bi, qi = rk.y * br - rk.x * bi;
-			A[sg_pad(kx)] = make_double2(pr - qi, pi + qr);
-		}
-		if (!(self && mx == kx)) {
-			const double pr = rm.x * ar - rm.y * ai, pi = rm.x * ai + rm.y * ar;
-			const double qr = rm.x * br - rm.y * bi, qi = rm.x * bi + rm.y * br;
-			Bv[sg_pad(mx)] = make_double2(pr - qi, pi + qr);
-		}
-	}
-	sg_lds_fft(buf, S, logS, self ? 1 : 2, SG_PADN(S), tw, true);
-	for (int j = threadIdx.x; j < S; j += blockDim.x) {
-		Z[(size_t)ky * S + j] = A[sg_pad(j)];
-		if (!self)
-			Z[(size_t)my * S + j] = Bv[sg_pad(j)];
-	}
+	const sg_c64 *Rs = spec;
+	(void)logS;
+	/* element i of row `row` (its mirror row `mrow`): the cross-power term as
+	 * sg_xpower_at forms it, read straight from memory by the first FFT pass */
+	sg_fft_io(buf, S, self ? 1 : 2, SG_PADN(S), tw, true,
+			[&](int b, int i) {
+				const int rw = b ? my : ky, mr = b ? ky : my;
+				return sg_xpower_at(Z[(size_t)rw * S + i], Z[(size_t)mr * S + ((S - i) & (S - 1))],
+						Rs[(size_t)rw * S + i]);
+			},
+			[&](int b, int i, sg_c64 v) { Z[(size_t)(b ? my : ky) * S + i] = v; });
 }
 
 /* better (value, index): larger value, ties -> lower index (first strict max, :337-343) */
@@ -326,17 +389,15 @@ k_reg_rows_inv_argmax(const sg_c64 *__restrict__ work, int S, int logS, const sg
 	__shared__ int ri[2][8];
 	const int row = blockIdx.x, pair = blockIdx.y;
 	const sg_c64 *in = work + (size_t)pair * S * S + (size_t)row * S;
-	for (int j = threadIdx.x; j < S; j += blockDim.x)
-		buf[sg_pad(j)] = in[j];
-	sg_lds_fft(buf, S, logS, 1, S, tw, true);
 	double va = -INFINITY, vb = -INFINITY;
 	int ia = 0x7fffffff, ib = 0x7fffffff;
-	for (int j = threadIdx.x; j < S; j += blockDim.x) {
-		const sg_c64 c = buf[sg_pad(j)];
-		const int idx = row * S + j;
-		sg_argmax_merge(va, ia, c.x, idx);
-		sg_argmax_merge(vb, ib, c.y, idx);
-	}
+	(void)logS;
+	sg_fft_io(buf, S, 1, S, tw, true, [&](int, int j) { return in[j]; },
+			[&](int, int j, sg_c64 c) {
+				const int idx = row * S + j;
+				sg_argmax_merge(va, ia, c.x, idx);
+				sg_argmax_merge(vb, ib, c.y, idx);
+			});
 	for (int o = 32; o > 0; o >>= 1) {
 		const double va2 = __shfl_down(va, o, 64), vb2 = __shfl_down(vb, o, 64);
 		const int ia2 = __shfl_down(ia, o, 64), ib2 = __shfl_down(ib, o, 64);
@@ -377,20 +438,15 @@ k_reg_cols_inv_argmax(const sg_c64 *__restrict__ work, int S, int logS, int CW, 
 	const int x0 = blockIdx.x * CW, pair = blockIdx.y;
 	const int bstride = SG_PADN(S) + 1;
 	const sg_c64 *base = work + (size_t)pair * S * S + x0;
-	for (int idx = threadIdx.x; idx < S * CW; idx += blockDim.x) {
-		const int r = idx / CW, c = idx - r * CW;
-		buf[c * bstride + sg_pad(r)] = base[(size_t)r * S + c];
-	}
-	sg_lds_fft(buf, S, logS, CW, bstride, tw, true);
 	double va = -INFINITY, vb = -INFINITY;
 	int ia = 0x7fffffff, ib = 0x7fffffff;
-	for (int idx = threadIdx.x; idx < S * CW; idx += blockDim.x) {
-		const int r = idx / CW, c = idx - r * CW;
-		const sg_c64 v = buf[c * bstride + sg_pad(r)];
-		const int lin = r * S + x0 + c;
-		sg_argmax_merge(va, ia, v.x, lin);
-		sg_argmax_merge(vb, ib, v.y, lin);
-	}
+	(void)logS;
+	sg_fft_io(buf, S, CW, bstride, tw, true, [&](int c, int r) { return base[(size_t)r * S + c]; },
+			[&](int c, int r, sg_c64 v) {
+				const int lin = r * S + x0 + c;
+				sg_argmax_merge(va, ia, v.x, lin);
+				sg_argmax_merge(vb, ib, v.y, lin);
+			});
 	for (int o = 32; o > 0; o >>= 1) {
 		const double va2 = __shfl_down(va, o, 64), vb2 = __shfl_down(vb, o, 64);
 		const int ia2 = __shfl_down(ia, o, 64), ib2 = __shfl_down(ib, o, 64);
