@@ -280,12 +280,23 @@ k_reg_rows_fwd(const uint16_t *__restrict__ sel, const int *__restrict__ fa, con
 			[&](int, int i, sg_c64 v) { out[i] = v; });
 }
 
+/* strip of workgroup `id` out of n: the dispatcher deals workgroups round-robin over the 8
+ * XCDs, so neighbouring strips (which share 128-B lines: a strip row is 64 B) would be
+ * fetched by two L2s; give each XCD a contiguous range of strips instead (PMC FETCH_SIZE
+ * of the column passes halves) */
+__device__ __forceinline__ int sg_xcd_strip(int id, int n, int xcdmap) {
+	if (!xcdmap || (n & 7))
+		return id;
+	return (id & 7) * (n >> 3) + (id >> 3);
+}
+
 /* column pass (forward or inverse) over strips of CW adjacent columns */
 __global__ void __launch_bounds__(1024)
-k_reg_cols(sg_c64 *__restrict__ work, int S, int logS, int CW, const sg_c64 *__restrict__ tw, int inverse) {
+k_reg_cols(sg_c64 *__restrict__ work, int S, int logS, int CW, const sg_c64 *__restrict__ tw, int inverse,
+		int xcdmap) {
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 	sg_c64 *buf = (sg_c64 *)smem;
-	const int x0 = blockIdx.x * CW, pair = blockIdx.y;
+	const int x0 = sg_xcd_strip(blockIdx.x, gridDim.x, xcdmap) * CW, pair = blockIdx.y;
 	const int bstride = SG_PADN(S) + 1;
 	sg_c64 *base = work + (size_t)pair * S * S + x0;
 	(void)logS;
@@ -430,12 +441,13 @@ k_reg_rows_inv_argmax(const sg_c64 *__restrict__ work, int S, int logS, const sg
  * parts over the strip: nothing is written back */
 __global__ void __launch_bounds__(1024)
 k_reg_cols_inv_argmax(const sg_c64 *__restrict__ work, int S, int logS, int CW, const sg_c64 *__restrict__ tw,
-		SgBest *__restrict__ best) {
+		SgBest *__restrict__ best, int xcdmap) {
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 	sg_c64 *buf = (sg_c64 *)smem;
 	__shared__ double rv[2][16];
 	__shared__ int ri[2][16];
-	const int x0 = blockIdx.x * CW, pair = blockIdx.y;
+	const int strip = sg_xcd_strip(blockIdx.x, gridDim.x, xcdmap);
+	const int x0 = strip * CW, pair = blockIdx.y;
 	const int bstride = SG_PADN(S) + 1;
 	const sg_c64 *base = work + (size_t)pair * S * S + x0;
 	double va = -INFINITY, vb = -INFINITY;
@@ -471,7 +483,7 @@ k_reg_cols_inv_argmax(const sg_c64 *__restrict__ work, int S, int logS, int CW, 
 		r.ia = ia;
 		r.vb = vb;
 		r.ib = ib;
-		best[(size_t)pair * gridDim.x + blockIdx.x] = r;
+		best[(size_t)pair * gridDim.x + strip] = r;
 	}
 }
 
@@ -803,6 +815,9 @@ extern "C" int sg_register_dft_u16_device(sg_ctx *ctx, int dev_index, const uint
 	bool fused = true;
 	if (const char *e = getenv("SG_REG_FUSED"))	/* A/B knob: 0 = the unfused pass order */
 		fused = atoi(e) != 0;
+	int xcdmap = 1;
+	if (const char *e = getenv("SG_REG_XCD"))	/* A/B knob: 0 = strips in dispatch order */
+		xcdmap = atoi(e) != 0;
 
 	HIPCHK(ensure(dv.reg_spec, plane * sizeof(sg_c64)));
 	HIPCHK(ensure(dv.reg_work, (size_t)(B > 1 ? B : 1) * plane * sizeof(sg_c64)));
@@ -831,7 +846,7 @@ extern "C" int sg_register_dft_u16_device(sg_ctx *ctx, int dev_index, const uint
 	hipLaunchKernelGGL(k_reg_rows_fwd, dim3(S, 1), dim3(row_thr), row_lds, s, d_sel, d_fa + NP, d_fb + NP, S, logS,
 			tw, spec);
 	HIPCHK(hipGetLastError());
-	hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, 1), dim3(col_thr), col_lds, s, spec, S, logS, CW, tw, 0);
+	hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, 1), dim3(col_thr), col_lds, s, spec, S, logS, CW, tw, 0, xcdmap);
 	HIPCHK(hipGetLastError());
 	shiftx[ref_image] = 0;
 	shifty[ref_image] = 0;
@@ -840,7 +855,8 @@ extern "C" int sg_register_dft_u16_device(sg_ctx *ctx, int dev_index, const uint
 		hipLaunchKernelGGL(k_reg_rows_fwd, dim3(S, np), dim3(row_thr), row_lds, s, d_sel, d_fa + p0, d_fb + p0, S,
 				logS, tw, work);
 		HIPCHK(hipGetLastError());
-		hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, np), dim3(col_thr), col_lds, s, work, S, logS, CW, tw, 0);
+		hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, np), dim3(col_thr), col_lds, s, work, S, logS, CW, tw, 0,
+				xcdmap);
 		HIPCHK(hipGetLastError());
 		if (fused) {
 			/* cross-power + inverse rows (row pairs ky, -ky), then inverse columns with the
@@ -849,14 +865,15 @@ extern "C" int sg_register_dft_u16_device(sg_ctx *ctx, int dev_index, const uint
 					(const sg_c64 *)spec, S, logS, tw);
 			HIPCHK(hipGetLastError());
 			hipLaunchKernelGGL(k_reg_cols_inv_argmax, dim3(S / CW, np), dim3(col_thr), col_lds, s,
-					(const sg_c64 *)work, S, logS, CW, tw, best);
+					(const sg_c64 *)work, S, logS, CW, tw, best, xcdmap);
 			HIPCHK(hipGetLastError());
 			hipLaunchKernelGGL(k_reg_final, dim3(np), dim3(256), 0, s, (const SgBest *)best, S, S / CW,
 					d_out + 4 * p0);
 		} else {
 			hipLaunchKernelGGL(k_reg_xpower, dim3(1024, np), dim3(256), 0, s, work, (const sg_c64 *)spec, S);
 			HIPCHK(hipGetLastError());
-			hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, np), dim3(col_thr), col_lds, s, work, S, logS, CW, tw, 1);
+			hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, np), dim3(col_thr), col_lds, s, work, S, logS, CW, tw, 1,
+					xcdmap);
 			HIPCHK(hipGetLastError());
 			hipLaunchKernelGGL(k_reg_rows_inv_argmax, dim3(S, np), dim3(row_thr), row_lds, s, (const sg_c64 *)work,
 					S, logS, tw, best);
