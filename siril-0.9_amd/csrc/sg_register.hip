@@ -193,7 +193,11 @@ __device__ __forceinline__ void sg_lds_fft(sg_c64 *buf, int n, int logn, int nb,
  * lanes of a column strip touch neighbouring columns of one row (64-B row segments).
  * The arithmetic is that of sg_lds_fft, operation for operation (n < 16, a single pass:
  * staged through LDS). */
-template <class LD, class ST>
+/* LDS_IN: ld reads this same LDS buffer (element i of transform b at its padded slot), so
+ * the first pass loads everything before anyone stores.  A st that writes element i back
+ * to its own slot is race-free as is: the last pass's thread reads exactly the slots it
+ * writes. */
+template <bool LDS_IN = false, class LD, class ST>
 __device__ __forceinline__ void sg_fft_io(sg_c64 *buf, int n, int nb, int bstride, const sg_c64 *__restrict__ tw,
 		bool inv, LD ld, ST st) {
 	if (n < 16) {
@@ -208,12 +212,17 @@ __device__ __forceinline__ void sg_fft_io(sg_c64 *buf, int n, int nb, int bstrid
 	{
 		const int per = n >> 3, items = nb * per;
 		const int t = threadIdx.x;
-		if (t < items) {
-			const int b = t % nb, j = t / nb;
-			sg_c64 v[8];
+		const bool act = t < items;
+		const int b = act ? t % nb : 0, j = act ? t / nb : 0;
+		sg_c64 v[8];
+		if (act) {
 #pragma unroll
 			for (int r = 0; r < 8; r++)
 				v[r] = ld(b, j + r * per);
+		}
+		if (LDS_IN)
+			__syncthreads();
+		if (act) {
 			sg_dft_small<8, 8>(v, inv);
 			sg_c64 *y = buf + (size_t)b * bstride;
 #pragma unroll
@@ -484,6 +493,158 @@ k_reg_cols_inv_argmax(const sg_c64 *__restrict__ work, int S, int logS, int CW, 
 		r.vb = vb;
 		r.ib = ib;
 		best[(size_t)pair * gridDim.x + strip] = r;
+	}
+}
+
+/* ---------------------------------------------------------------------------------------
+ * Half-spectrum pass order (default): three plane passes per pair instead of four.
+ *   1. k_reg_rows_fwd_half: row FFT of a + i b, separated per row into the row spectra of
+ *      the two real frames, A(kx) = (z(kx) + conj z(-kx))/2, B(kx) = (z(kx) - conj z(-kx))/2i,
+ *      of which kx in [0, S/2] is kept (Hermitian rows).  A(0) and A(S/2) are real, so
+ *      column 0 packs A(0) + i A(S/2).  Layout of a pair plane row: [A' | B'], S/2 + S/2.
+ *   2. k_reg_cols_xpower: per column (of A' or B'), forward column FFT, cross-power with
+ *      the reference's column (R conj F), inverse column FFT: the cross-power needs no
+ *      mirrored column any more, so the forward and inverse column passes fuse.  Column 0
+ *      of each half holds two real sequences and is separated / re-packed over (ky, -ky),
+ *      which lie in the same column.
+ *   3. k_reg_rows_inv_half_argmax: the inverse column output is Hermitian in kx (the
+ *      correlation is real), so each row's full spectrum is rebuilt from kx <= S/2, the
+ *      two frames packed as Qa + i Qb, inverse row FFT -> c_a + i c_b, arg-max fused.
+ * Same unnormalised FFTW_BACKWARD result as the full complex transforms; plane traffic per
+ * pair 84 B per pixel instead of 116.
+ * ------------------------------------------------------------------------------------- */
+__global__ void __launch_bounds__(512)
+k_reg_rows_fwd_half(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const int *__restrict__ fb,
+		int S, const sg_c64 *__restrict__ tw, sg_c64 *__restrict__ work) {
+	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+	sg_c64 *buf = (sg_c64 *)smem;
+	const int row = blockIdx.x, pair = blockIdx.y, H = S >> 1;
+	const size_t plane = (size_t)S * S;
+	const uint16_t *pa = sel + (size_t)fa[pair] * plane + (size_t)row * S;
+	const int b = fb[pair];
+	const uint16_t *pb = b >= 0 ? sel + (size_t)b * plane + (size_t)row * S : nullptr;
+	sg_c64 *out = work + (size_t)pair * plane + (size_t)row * S;
+	sg_fft_io(buf, S, 1, S, tw, false,
+			[&](int, int i) { return make_double2((double)pa[i], pb ? (double)pb[i] : 0.0); },
+			[&](int, int i, sg_c64 v) { buf[sg_pad(i)] = v; });
+	__syncthreads();
+	for (int k = threadIdx.x; k < H; k += blockDim.x) {
+		const sg_c64 zk = buf[sg_pad(k)], zm = buf[sg_pad(k ? S - k : H)];
+		sg_c64 A, B;
+		if (k == 0) {
+			A = make_double2(zk.x, zm.x);	/* A(0) + i A(S/2) */
+			B = make_double2(zk.y, zm.y);
+		} else {
+			A = make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
+			B = make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x));
+		}
+		out[k] = A;
+		out[H + k] = B;
+	}
+}
+
+/* R conj F */
+__device__ __forceinline__ sg_c64 sg_rconj(sg_c64 r, sg_c64 f) {
+	return make_double2(r.x * f.x + r.y * f.y, r.y * f.x - r.x * f.y);
+}
+
+__global__ void __launch_bounds__(1024)
+k_reg_cols_xpower(sg_c64 *__restrict__ work, const sg_c64 *__restrict__ spec, int S, int CW,
+		const sg_c64 *__restrict__ tw, int xcdmap) {
+	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+	sg_c64 *buf = (sg_c64 *)smem;
+	const int x0 = sg_xcd_strip(blockIdx.x, gridDim.x, xcdmap) * CW, pair = blockIdx.y;
+	const int bstride = SG_PADN(S) + 1, H = S >> 1;
+	sg_c64 *base = work + (size_t)pair * S * S + x0;
+	auto slot = [&](int c, int r) -> sg_c64 & { return buf[(size_t)c * bstride + sg_pad(r)]; };
+	sg_fft_io(buf, S, CW, bstride, tw, false, [&](int c, int r) { return base[(size_t)r * S + c]; },
+			[&](int c, int r, sg_c64 v) { slot(c, r) = v; });
+	__syncthreads();
+	for (int t = threadIdx.x; t < CW * S; t += blockDim.x) {
+		const int c = t % CW, ky = t / CW, kx = (x0 + c) & (H - 1);
+		if (kx) {
+			slot(c, ky) = sg_rconj(spec[(size_t)ky * S + kx], slot(c, ky));
+			continue;
+		}
+		/* packed column: Z = F0 + i FN (F0, FN spectra of real columns), same for the
+		 * reference; P = R0 conj F0 + i RN conj FN, written at ky and -ky */
+		const int m = (S - ky) & (S - 1);
+		if (m < ky)
+			continue;
+		const sg_c64 zk = slot(c, ky), zm = slot(c, m);
+		const sg_c64 rk = spec[(size_t)ky * S], rm = spec[(size_t)m * S];
+		const sg_c64 f0 = make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
+		const sg_c64 fn = make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x));
+		const sg_c64 r0 = make_double2(0.5 * (rk.x + rm.x), 0.5 * (rk.y - rm.y));
+		const sg_c64 rn = make_double2(0.5 * (rk.y + rm.y), -0.5 * (rk.x - rm.x));
+		const sg_c64 p0 = sg_rconj(r0, f0), pn = sg_rconj(rn, fn);
+		slot(c, ky) = make_double2(p0.x - pn.y, p0.y + pn.x);
+		if (m != ky)	/* P0(-k) = conj P0(k), PN(-k) = conj PN(k) */
+			slot(c, m) = make_double2(p0.x + pn.y, pn.x - p0.y);
+	}
+	__syncthreads();
+	sg_fft_io<true>(buf, S, CW, bstride, tw, true, [&](int c, int r) { return slot(c, r); },
+			[&](int c, int r, sg_c64 v) { base[(size_t)r * S + c] = v; });
+}
+
+__global__ void __launch_bounds__(512)
+k_reg_rows_inv_half_argmax(const sg_c64 *__restrict__ work, int S, const sg_c64 *__restrict__ tw,
+		SgBest *__restrict__ best) {
+	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+	sg_c64 *buf = (sg_c64 *)smem;
+	__shared__ double rv[2][8];
+	__shared__ int ri[2][8];
+	const int row = blockIdx.x, pair = blockIdx.y, H = S >> 1;
+	const sg_c64 *in = work + (size_t)pair * S * S + (size_t)row * S;
+	double va = -INFINITY, vb = -INFINITY;
+	int ia = 0x7fffffff, ib = 0x7fffffff;
+	sg_fft_io(buf, S, 1, S, tw, true,
+			[&](int, int i) {
+				sg_c64 qa, qb;
+				if ((i & (H - 1)) == 0) {	/* kx = 0 or S/2: the packed real pair */
+					const sg_c64 a = in[0], b = in[H];
+					qa = make_double2(i ? a.y : a.x, 0.0);
+					qb = make_double2(i ? b.y : b.x, 0.0);
+				} else if (i < H) {
+					qa = in[i];
+					qb = in[H + i];
+				} else {
+					const sg_c64 a = in[S - i], b = in[H + S - i];
+					qa = make_double2(a.x, -a.y);
+					qb = make_double2(b.x, -b.y);
+				}
+				return make_double2(qa.x - qb.y, qa.y + qb.x);
+			},
+			[&](int, int j, sg_c64 c) {
+				const int idx = row * S + j;
+				sg_argmax_merge(va, ia, c.x, idx);
+				sg_argmax_merge(vb, ib, c.y, idx);
+			});
+	for (int o = 32; o > 0; o >>= 1) {
+		const double va2 = __shfl_down(va, o, 64), vb2 = __shfl_down(vb, o, 64);
+		const int ia2 = __shfl_down(ia, o, 64), ib2 = __shfl_down(ib, o, 64);
+		sg_argmax_merge(va, ia, va2, ia2);
+		sg_argmax_merge(vb, ib, vb2, ib2);
+	}
+	const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+	if ((threadIdx.x & 63) == 0) {
+		rv[0][wave] = va;
+		ri[0][wave] = ia;
+		rv[1][wave] = vb;
+		ri[1][wave] = ib;
+	}
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		for (int w = 1; w < nw; w++) {
+			sg_argmax_merge(va, ia, rv[0][w], ri[0][w]);
+			sg_argmax_merge(vb, ib, rv[1][w], ri[1][w]);
+		}
+		SgBest r;
+		r.va = va;
+		r.ia = ia;
+		r.vb = vb;
+		r.ib = ib;
+		best[(size_t)pair * S + row] = r;
 	}
 }
 
@@ -812,9 +973,25 @@ extern "C" int sg_register_dft_u16_device(sg_ctx *ctx, int dev_index, const uint
 	 * at least one wave */
 	auto thr_for = [](int elems) { return elems / 8 < 64 ? 64 : elems / 8; };
 	const int row_thr = thr_for(S), col_thr = thr_for(CW * S), xri_thr = thr_for(2 * S);
-	bool fused = true;
-	if (const char *e = getenv("SG_REG_FUSED"))	/* A/B knob: 0 = the unfused pass order */
-		fused = atoi(e) != 0;
+	/* pass order: 2 = half spectra (3 plane passes), 1 = full spectra with the cross-power
+	 * fused into the inverse row pass (4), 0 = unfused (5) */
+	int path = 2;
+	if (const char *e = getenv("SG_REG_FUSED"))	/* A/B knob (older name): 0 = unfused */
+		path = atoi(e) != 0 ? 1 : 0;
+	if (const char *e = getenv("SG_REG_PATH"))	/* A/B knob: pass order */
+		path = atoi(e);
+	const bool fused = path == 1;
+	const bool half = path == 2;
+	/* half-spectrum columns: a strip stays inside one half (CW divides S/2) */
+	const int CWh = CW < S / 2 ? CW : S / 2;
+	const size_t colh_lds = (size_t)CWh * (SG_PADN(S) + 1) * sizeof(sg_c64);
+	const int colh_thr = thr_for(CWh * S);
+	(void)hipFuncSetAttribute((const void *)k_reg_rows_fwd_half, hipFuncAttributeMaxDynamicSharedMemorySize,
+			(int)row_lds);
+	(void)hipFuncSetAttribute((const void *)k_reg_rows_inv_half_argmax, hipFuncAttributeMaxDynamicSharedMemorySize,
+			(int)row_lds);
+	(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower, hipFuncAttributeMaxDynamicSharedMemorySize,
+			(int)colh_lds);
 	int xcdmap = 1;
 	if (const char *e = getenv("SG_REG_XCD"))	/* A/B knob: 0 = strips in dispatch order */
 		xcdmap = atoi(e) != 0;
@@ -842,16 +1019,38 @@ extern "C" int sg_register_dft_u16_device(sg_ctx *ctx, int dev_index, const uint
 	hfb[NP] = -1;
 	HIPCHK(hipMemcpyAsync(d_fa, hfa.data(), sizeof(int) * (NP + 1), hipMemcpyHostToDevice, s));
 	HIPCHK(hipMemcpyAsync(d_fb, hfb.data(), sizeof(int) * (NP + 1), hipMemcpyHostToDevice, s));
-	/* reference spectrum R = FFT2(ref) */
-	hipLaunchKernelGGL(k_reg_rows_fwd, dim3(S, 1), dim3(row_thr), row_lds, s, d_sel, d_fa + NP, d_fb + NP, S, logS,
-			tw, spec);
-	HIPCHK(hipGetLastError());
-	hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, 1), dim3(col_thr), col_lds, s, spec, S, logS, CW, tw, 0, xcdmap);
+	/* reference spectrum R = FFT2(ref) (half layout: the A' half only) */
+	if (half) {
+		hipLaunchKernelGGL(k_reg_rows_fwd_half, dim3(S, 1), dim3(row_thr), row_lds, s, d_sel, d_fa + NP, d_fb + NP,
+				S, tw, spec);
+		HIPCHK(hipGetLastError());
+		hipLaunchKernelGGL(k_reg_cols, dim3(S / 2 / CWh, 1), dim3(colh_thr), colh_lds, s, spec, S, logS, CWh, tw, 0,
+				xcdmap);
+	} else {
+		hipLaunchKernelGGL(k_reg_rows_fwd, dim3(S, 1), dim3(row_thr), row_lds, s, d_sel, d_fa + NP, d_fb + NP, S,
+				logS, tw, spec);
+		HIPCHK(hipGetLastError());
+		hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, 1), dim3(col_thr), col_lds, s, spec, S, logS, CW, tw, 0, xcdmap);
+	}
 	HIPCHK(hipGetLastError());
 	shiftx[ref_image] = 0;
 	shifty[ref_image] = 0;
 	for (int p0 = 0; p0 < npairs_total; p0 += B) {
 		const int np = npairs_total - p0 < B ? npairs_total - p0 : B;
+		if (half) {
+			hipLaunchKernelGGL(k_reg_rows_fwd_half, dim3(S, np), dim3(row_thr), row_lds, s, d_sel, d_fa + p0,
+					d_fb + p0, S, tw, work);
+			HIPCHK(hipGetLastError());
+			hipLaunchKernelGGL(k_reg_cols_xpower, dim3(S / CWh, np), dim3(colh_thr), colh_lds, s, work,
+					(const sg_c64 *)spec, S, CWh, tw, xcdmap);
+			HIPCHK(hipGetLastError());
+			hipLaunchKernelGGL(k_reg_rows_inv_half_argmax, dim3(S, np), dim3(row_thr), row_lds, s,
+					(const sg_c64 *)work, S, tw, best);
+			HIPCHK(hipGetLastError());
+			hipLaunchKernelGGL(k_reg_final, dim3(np), dim3(256), 0, s, (const SgBest *)best, S, S, d_out + 4 * p0);
+			HIPCHK(hipGetLastError());
+			continue;
+		}
 		hipLaunchKernelGGL(k_reg_rows_fwd, dim3(S, np), dim3(row_thr), row_lds, s, d_sel, d_fa + p0, d_fb + p0, S,
 				logS, tw, work);
 		HIPCHK(hipGetLastError());
