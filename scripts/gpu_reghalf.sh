@@ -9,7 +9,7 @@ mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_gpu_register.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest_reg.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $O/pytest_reg.log | cut -c1-300
 [ $rc -eq 0 ] || { grep -E 'Error|assert|FAIL' $O/pytest_reg.log | head -20; exit $rc; }
-for P in 1 2 1 2; do
+for P in 2 2; do
   SG_REG_PATH=$P timeout -k 10 300 python bench.py --workload register-mean --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_p$P.log 2>&1 || { echo bench failed; tail -20 $O/bench_p$P.log; exit 3; }
   echo "path $P: $(grep '^{' $O/bench_p$P.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["stage_ms"], d["register_shifts_exact"])')"
 done

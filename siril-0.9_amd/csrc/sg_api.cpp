@@ -33,6 +33,7 @@ __global__ void k_stack_replay(SgStackParams p);
 __global__ void k_redo_to_literal(SgStackParams p, const unsigned int *list, const unsigned int *count,
 		unsigned int maxn);
 __global__ void k_stack_reduce(SgStackParams p);
+__global__ void k_stack_reduce2(SgStackParams p);
 __global__ void k_sum_finalize(SgStackParams p);
 __global__ void k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *scratch, int phase);
 __global__ void k_synth_fill(uint16_t *frames, int nframes, int C, int H, int W, int row_begin,
@@ -494,11 +495,19 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 			p.sum_buf = (uint32_t *)dv.sum_buf.p;
 		}
 		dim3 grid((W + 255) / 256, nrows, C);
+		/* pixel pairs per lane (dword loads) unless a plane is too large for a 31-bit offset */
+		bool pairs = W >= 2 && (uint64_t)W * (uint64_t)H * 2u < (1ull << 31);
+		if (const char *e = getenv("SG_REDUCE1"))	/* A/B knob: 1 = one pixel per lane */
+			pairs = pairs && atoi(e) == 0;
+		const dim3 grid2(((W + 1) / 2 + 255) / 256, nrows, C);
 		HIPCHK(hipEventRecord(dv.ev[0], s));
-		hipLaunchKernelGGL(k_stack_reduce, grid, dim3(256), 0, s, p);
+		if (pairs)
+			hipLaunchKernelGGL(k_stack_reduce2, grid2, dim3(256), 0, s, p);
+		else
+			hipLaunchKernelGGL(k_stack_reduce, grid, dim3(256), 0, s, p);
 		HIPCHK(hipGetLastError());
 		HIPCHK(hipEventRecord(dv.ev[1], s));
-		ctx->stats.main_kernel_blocks = (int)(grid.x * grid.y * grid.z);
+		ctx->stats.main_kernel_blocks = pairs ? (int)(grid2.x * grid2.y * grid2.z) : (int)(grid.x * grid.y * grid.z);
 		ctx->stats.launches = 1;
 		if (d->method == SG_STACK_SUM) {
 			hipLaunchKernelGGL(k_sum_finalize, grid, dim3(256), 0, s, p);

@@ -548,6 +548,9 @@ __device__ __forceinline__ sg_c64 sg_rconj(sg_c64 r, sg_c64 f) {
 	return make_double2(r.x * f.x + r.y * f.y, r.y * f.x - r.x * f.y);
 }
 
+/* The reference-spectrum loads of all 8 cross-power items of a thread are issued together
+ * (launches are sized so that CW * S = 8 * blockDim, thr_for).  Issuing them before the
+ * forward FFT instead spills (128 VGPRs at 4 waves per SIMD). */
 __global__ void __launch_bounds__(1024)
 k_reg_cols_xpower(sg_c64 *__restrict__ work, const sg_c64 *__restrict__ spec, int S, int CW,
 		const sg_c64 *__restrict__ tw, int xcdmap) {
@@ -557,13 +560,35 @@ k_reg_cols_xpower(sg_c64 *__restrict__ work, const sg_c64 *__restrict__ spec, in
 	const int bstride = SG_PADN(S) + 1, H = S >> 1;
 	sg_c64 *base = work + (size_t)pair * S * S + x0;
 	auto slot = [&](int c, int r) -> sg_c64 & { return buf[(size_t)c * bstride + sg_pad(r)]; };
+	constexpr int NI = 8;
+	const int items = CW * S;
+	sg_c64 rk[NI], rm[NI];
+	auto fetch = [&]() {
+#pragma unroll
+		for (int it = 0; it < NI; it++) {
+			const int t = threadIdx.x + it * blockDim.x;
+			rk[it] = make_double2(0.0, 0.0);
+			rm[it] = make_double2(0.0, 0.0);
+			if (t < items) {
+				const int c = t % CW, ky = t / CW, kx = (x0 + c) & (H - 1);
+				rk[it] = spec[(size_t)ky * S + kx];
+				if (!kx)
+					rm[it] = spec[(size_t)((S - ky) & (S - 1)) * S];
+			}
+		}
+	};
 	sg_fft_io(buf, S, CW, bstride, tw, false, [&](int c, int r) { return base[(size_t)r * S + c]; },
 			[&](int c, int r, sg_c64 v) { slot(c, r) = v; });
+	fetch();
 	__syncthreads();
-	for (int t = threadIdx.x; t < CW * S; t += blockDim.x) {
+#pragma unroll
+	for (int it = 0; it < NI; it++) {
+		const int t = threadIdx.x + it * blockDim.x;
+		if (t >= items)
+			continue;
 		const int c = t % CW, ky = t / CW, kx = (x0 + c) & (H - 1);
 		if (kx) {
-			slot(c, ky) = sg_rconj(spec[(size_t)ky * S + kx], slot(c, ky));
+			slot(c, ky) = sg_rconj(rk[it], slot(c, ky));
 			continue;
 		}
 		/* packed column: Z = F0 + i FN (F0, FN spectra of real columns), same for the
@@ -571,12 +596,11 @@ k_reg_cols_xpower(sg_c64 *__restrict__ work, const sg_c64 *__restrict__ spec, in
 		const int m = (S - ky) & (S - 1);
 		if (m < ky)
 			continue;
-		const sg_c64 zk = slot(c, ky), zm = slot(c, m);
-		const sg_c64 rk = spec[(size_t)ky * S], rm = spec[(size_t)m * S];
+		const sg_c64 zk = slot(c, ky), zm = slot(c, m), r1 = rk[it], r2 = rm[it];
 		const sg_c64 f0 = make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
 		const sg_c64 fn = make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x));
-		const sg_c64 r0 = make_double2(0.5 * (rk.x + rm.x), 0.5 * (rk.y - rm.y));
-		const sg_c64 rn = make_double2(0.5 * (rk.y + rm.y), -0.5 * (rk.x - rm.x));
+		const sg_c64 r0 = make_double2(0.5 * (r1.x + r2.x), 0.5 * (r1.y - r2.y));
+		const sg_c64 rn = make_double2(0.5 * (r1.y + r2.y), -0.5 * (r1.x - r2.x));
 		const sg_c64 p0 = sg_rconj(r0, f0), pn = sg_rconj(rn, fn);
 		slot(c, ky) = make_double2(p0.x - pn.y, p0.y + pn.x);
 		if (m != ky)	/* P0(-k) = conj P0(k), PN(-k) = conj PN(k) */

@@ -677,6 +677,112 @@ k_stack_reduce(SgStackParams p) {
 	}
 }
 
+/* The same reductions with a pixel PAIR per lane: one 4-byte buffer load per frame at the
+ * shifted (2-byte aligned) address, 256 B per wave instruction instead of 128 B of u16
+ * loads.  Each frame gets a buffer resource spanning its plane, so a row shifted out of the
+ * frame reads 0 from the bounds check; at the left / right image edge, where one pixel of
+ * the pair leaves the image, the load moves by one sample and the pair is fixed up.  Rows
+ * and pixels are then masked exactly as k_stack_reduce does (xin / ok).  Host: plane bytes
+ * < 2^31. */
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sg_plane_rsrc(const uint16_t *base, uint32_t nrec) {
+	return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)nrec, 0x00020000);
+}
+
+__global__ void __launch_bounds__(256)
+k_stack_reduce2(SgStackParams p) {
+	const int x = 2 * (blockIdx.x * 256 + threadIdx.x);
+	const int R = p.row_begin + blockIdx.y;
+	const int c = blockIdx.z;
+	const bool live_a = x < p.W, live_b = x + 1 < p.W;
+	const uint16_t *plane = p.frames + (int64_t)c * p.plane_stride;
+	const uint32_t nrec = (uint32_t)p.H * (uint32_t)p.W * 2u;
+	const int N = p.N;
+	uint32_t acc_a = (p.method == 4) ? 65535u : 0u, acc_b = acc_a;
+	for (int f0 = 0; f0 < N; f0 += 16) {
+		uint32_t v[16];
+		int nxs[16];
+		bool yis[16], y0s[16];
+#pragma unroll
+		for (int m = 0; m < 16; m++) {
+			const int f = f0 + m < N ? f0 + m : N - 1;
+			const int sx = p.use_shift ? p.shiftx[f] : 0;
+			const int sy = p.use_shift ? p.shifty[f] : 0;
+			const int nx = x - sx, ny = R - sy;
+			nxs[m] = nx;
+			yis[m] = (unsigned)ny < (unsigned)p.H && f0 + m < N;
+			y0s[m] = ny == 0;
+			/* the dword holding (nx, nx + 1), moved inside the row at the image edges */
+			const int lx = nx < 0 ? nx + 1 : (nx + 1 >= p.W ? nx - 1 : nx);
+			const uint32_t off = yis[m] ? (uint32_t)(ny * p.W + lx) * 2u : 0x80000000u;
+			v[m] = __builtin_amdgcn_raw_buffer_load_b32(sg_plane_rsrc(plane + (int64_t)f * p.frame_stride, nrec),
+					(int)off, 0, 0);
+		}
+#pragma unroll
+		for (int m = 0; m < 16; m++) {
+			const int nx = nxs[m];
+			const bool yi = yis[m];
+			/* samples of pixel a (source column nx) and b (nx + 1) */
+			uint32_t a, b;
+			if (nx < 0) {
+				a = 0u;
+				b = v[m] & 0xFFFFu;
+			} else if (nx + 1 >= p.W) {
+				a = v[m] >> 16;
+				b = 0u;
+			} else {
+				a = v[m] & 0xFFFFu;
+				b = v[m] >> 16;
+			}
+			const bool in = f0 + m < N;
+			const bool xa = live_a && in && (unsigned)nx < (unsigned)p.W;
+			const bool xb = live_b && in && (unsigned)(nx + 1) < (unsigned)p.W;
+			if (p.method == 1) {	/* mean, NO_REJEC: y-shifted rows are zeros (normalised), x-shifted are skipped */
+				if (xa)
+					acc_a += p.normalize ? sg_normalize(p, f0 + m, (uint16_t)(yi ? a : 0u)) : (yi ? a : 0u);
+				if (xb)
+					acc_b += p.normalize ? sg_normalize(p, f0 + m, (uint16_t)(yi ? b : 0u)) : (yi ? b : 0u);
+			} else {
+				/* `ii > 0`: source pixel 0 is never used (:307) */
+				const bool oka = xa && yi && !(nx == 0 && y0s[m]);
+				const bool okb = xb && yi && !(nx + 1 == 0 && y0s[m]);
+				if (p.method == 0) {
+					acc_a += oka ? a : 0u;
+					acc_b += okb ? b : 0u;
+				} else if (p.method == 3) {
+					acc_a = (oka && a > acc_a) ? a : acc_a;
+					acc_b = (okb && b > acc_b) ? b : acc_b;
+				} else {
+					acc_a = (oka && a < acc_a) ? a : acc_a;
+					acc_b = (okb && b < acc_b) ? b : acc_b;
+				}
+			}
+		}
+	}
+	unsigned int blockmax = 0;
+	const int64_t pix = ((int64_t)c * p.H + R) * p.W + x;
+	for (int k = 0; k < 2; k++) {
+		if (!(k ? live_b : live_a))
+			continue;
+		const uint32_t acc = k ? acc_b : acc_a;
+		if (p.method == 1) {
+			p.out[pix + k] = sg_round_to_WORD((double)acc / (double)N);
+		} else if (p.method == 0) {
+			p.sum_buf[pix + k] = acc;
+			blockmax = acc > blockmax ? acc : blockmax;
+		} else {
+			p.out[pix + k] = (uint16_t)acc;
+		}
+	}
+	if (p.method == 0) {
+		for (int o = 32; o > 0; o >>= 1) {
+			unsigned int t = (unsigned int)__shfl_down((int)blockmax, o, 64);
+			blockmax = t > blockmax ? t : blockmax;
+		}
+		if ((threadIdx.x & 63) == 0 && blockmax)
+			atomicMax(p.maxim, blockmax);
+	}
+}
+
 /* SUM finalisation: out = round_to_WORD(sum) or round_to_WORD(sum * 65535/maxim) (:328-342) */
 __global__ void __launch_bounds__(256)
 k_sum_finalize(SgStackParams p) {
