@@ -39,7 +39,7 @@ __device__ __forceinline__ int sg_bitrev(int x, int logn) {
  * nb independent length-n FFTs held in LDS (transform b at buf + b*bstride), natural order
  * in and out: Stockham auto-sort passes of radix 8 (then 4 / 2 for the remaining factor),
  * each thread taking whole radix-R butterflies in registers (a 2048-point transform is 4
- * LDS round trips instead of 11).  tw[k] = exp(-2 pi i k / n), k < n/2; the inverse uses
+ * LDS round trips instead of 11).  tw: see sg_twiddle; the inverse uses
  * conjugate twiddles (unnormalised, FFTW_BACKWARD).
  * ------------------------------------------------------------------------------------ */
 /* LDS element index with one pad slot per 8 elements: the Stockham stores of the first
@@ -107,13 +107,11 @@ __device__ __forceinline__ void sg_dft_small(sg_c64 (&v)[RV], bool inv) {
 	}
 }
 
+/* tw holds the full circle twice: tw[k] = exp(-2 pi i k / n) and tw[n + k] = its conjugate
+ * (the inverse), k < n, built on the host from the half-circle values by exact negation /
+ * conjugation, so a twiddle is one load with no select (the direction is uniform) */
 __device__ __forceinline__ sg_c64 sg_twiddle(const sg_c64 *__restrict__ tw, int n, int k, bool inv) {
-	sg_c64 w = (k < (n >> 1)) ? tw[k] : tw[k - (n >> 1)];
-	if (k >= (n >> 1))
-		w = make_double2(-w.x, -w.y);
-	if (inv)
-		w.y = -w.y;
-	return w;
+	return (inv ? tw + n : tw)[k];
 }
 
 template <int R>
@@ -944,15 +942,23 @@ extern "C" int sg_register_dft_u16_device(sg_ctx *ctx, int dev_index, const uint
 			todo.push_back(f);
 
 	/* twiddles exp(-2 pi i k / S) */
-	HIPCHK(ensure(dv.reg_tw, sizeof(sg_c64) * (S / 2)));
+	HIPCHK(ensure(dv.reg_tw, sizeof(sg_c64) * 2 * S));
 	{
-		std::vector<double> tw(S);
+		/* forward full circle (k >= S/2: the negated half-circle value), then its conjugate */
+		std::vector<double> tw(4 * (size_t)S);
 		for (int k = 0; k < S / 2; k++) {
 			const double a = -2.0 * M_PI * (double)k / (double)S;
-			tw[2 * k] = cos(a);
-			tw[2 * k + 1] = sin(a);
+			const double c = cos(a), sn = sin(a);
+			const int kk[2] = {k, k + S / 2};
+			const double sg[2] = {1.0, -1.0};
+			for (int h = 0; h < 2; h++) {
+				tw[2 * kk[h]] = sg[h] * c;
+				tw[2 * kk[h] + 1] = sg[h] * sn;
+				tw[2 * (S + kk[h])] = sg[h] * c;
+				tw[2 * (S + kk[h]) + 1] = -(sg[h] * sn);
+			}
 		}
-		HIPCHK(hipMemcpyAsync(dv.reg_tw.p, tw.data(), sizeof(double) * S, hipMemcpyHostToDevice, s));
+		HIPCHK(hipMemcpyAsync(dv.reg_tw.p, tw.data(), sizeof(double) * 4 * S, hipMemcpyHostToDevice, s));
 		HIPCHK(hipStreamSynchronize(s));
 	}
 	const sg_c64 *tw = (const sg_c64 *)dv.reg_tw.p;
