@@ -722,6 +722,7 @@ k_reg_final(const SgBest *__restrict__ best, int S, int count, int *__restrict__
  * ------------------------------------------------------------------------------------- */
 #define SG_Q_THRESHOLD (40 << 8)
 #define SG_QROWS 4	/* subsampled rows per k_quality_sub workgroup */
+#define SG_QGT 16	/* output rows per k_quality_grad tile (64 columns) */
 
 /* SubSample (:223-234) of one 3x3 sample row, plus the running max of the middle rows
  * (the maxp[] loop :119-133 reduces to max over 0 < v < 65530) */
@@ -733,14 +734,32 @@ k_quality_sub(const uint16_t *__restrict__ sel, const int *__restrict__ qframes,
 	const int q = blockIdx.y;
 	const uint16_t *frame = sel + (size_t)qframes[q] * S * S;
 	unsigned int m = 0;
-	for (int j = blockIdx.x * SG_QROWS; j < ys && j < (blockIdx.x + 1) * SG_QROWS; j++) {
-		const bool middle = (j >= 1 && j <= ys - 2);
-		uint16_t *dst = qbuf + (size_t)q * xs * ys + (size_t)j * xs;
-		for (int k = threadIdx.x; 2 * k < xs; k += blockDim.x) {
-			int va = 0, vb = 0;
+	const int j0 = blockIdx.x * SG_QROWS;
+	for (int k = threadIdx.x; 2 * k < xs; k += blockDim.x) {
+		/* the 3 x SG_QROWS input rows of this pair: every load issued before any is used */
+		uint32_t d[SG_QROWS][3][3];
+#pragma unroll
+		for (int jj = 0; jj < SG_QROWS; jj++) {
+			const int j = j0 + jj < ys ? j0 + jj : ys - 1;
+#pragma unroll
 			for (int y = 0; y < 3; y++) {
 				const uint32_t *p = (const uint32_t *)(frame + (size_t)(3 * j + y) * S + 6 * k);
-				const uint32_t d0 = p[0], d1 = p[1], d2 = p[2];
+				d[jj][y][0] = p[0];
+				d[jj][y][1] = p[1];
+				d[jj][y][2] = p[2];
+			}
+		}
+#pragma unroll
+		for (int jj = 0; jj < SG_QROWS; jj++) {
+			const int j = j0 + jj;
+			if (j >= ys)
+				break;
+			const bool middle = (j >= 1 && j <= ys - 2);
+			uint16_t *dst = qbuf + (size_t)q * xs * ys + (size_t)j * xs;
+			int va = 0, vb = 0;
+#pragma unroll
+			for (int y = 0; y < 3; y++) {
+				const uint32_t d0 = d[jj][y][0], d1 = d[jj][y][1], d2 = d[jj][y][2];
 				va += (int)(d0 & 0xFFFFu) + (int)(d0 >> 16) + (int)(d1 & 0xFFFFu);
 				vb += (int)(d1 >> 16) + (int)(d2 & 0xFFFFu) + (int)(d2 >> 16);
 			}
@@ -781,10 +800,11 @@ __global__ void __launch_bounds__(256)
 k_quality_grad(const uint16_t *__restrict__ qbuf, int xs, int ys, const unsigned int *__restrict__ qmax,
 		unsigned long long *__restrict__ acc /* [q][3]: val, pixels, thresholded */) {
 	__shared__ unsigned long long sv[4], sp[4], sc[4];
-	/* a 64 x 4 tile of outputs: stretched samples of the 68 x 8 neighbourhood, then the
-	 * smoothed values of the 66 x 6 one, each formed once in LDS */
-	__shared__ unsigned int st[8][68];
-	__shared__ int sms[6][66];
+	/* a 64 x SG_QGT tile of outputs: stretched samples of the 68 x (SG_QGT + 4)
+	 * neighbourhood, then the smoothed values of the 66 x (SG_QGT + 2) one, each formed once
+	 * in LDS; each wave takes SG_QGT / 4 output rows */
+	__shared__ unsigned int st[SG_QGT + 4][68];
+	__shared__ int sms[SG_QGT + 2][66];
 	const int q = blockIdx.z;
 	const uint16_t *b = qbuf + (size_t)q * xs * ys;
 	const unsigned int mx = qmax[q];
@@ -792,15 +812,15 @@ k_quality_grad(const uint16_t *__restrict__ qbuf, int xs, int ys, const unsigned
 	const double mult = stretch ? (double)60000 / (double)mx : 1.0;
 	const int yb = (int)((double)ys * 0.1) + 1;
 	const int xb = (int)((double)xs * 0.1) + 1;
-	const int x0 = blockIdx.x * 64, y0 = blockIdx.y * 4;
-	for (int i = threadIdx.x; i < 8 * 68; i += blockDim.x) {
+	const int x0 = blockIdx.x * 64, y0 = blockIdx.y * SG_QGT;
+	for (int i = threadIdx.x; i < (SG_QGT + 4) * 68; i += blockDim.x) {
 		const int ly = i / 68, lx = i - ly * 68;
 		const int gx = x0 - 2 + lx, gy = y0 - 2 + ly;
 		st[ly][lx] = (gx >= 0 && gx < xs && gy >= 0 && gy < ys) ? (unsigned int)sg_q_stretch(b, gy * xs + gx, mult, stretch)
 									     : 0u;
 	}
 	__syncthreads();
-	for (int i = threadIdx.x; i < 6 * 66; i += blockDim.x) {
+	for (int i = threadIdx.x; i < (SG_QGT + 2) * 66; i += blockDim.x) {
 		const int ly = i / 66, lx = i - ly * 66;
 		const int qx = x0 - 1 + lx, qy = y0 - 1 + ly;
 		int v = 0;
@@ -814,9 +834,11 @@ k_quality_grad(const uint16_t *__restrict__ qbuf, int xs, int ys, const unsigned
 		sms[ly][lx] = v;
 	}
 	__syncthreads();
-	const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-	const int x = x0 + tx, y = y0 + ty;
+	const int tx = threadIdx.x & 63;
+	const int x = x0 + tx;
 	unsigned long long val = 0, pix = 0, cnt = 0;
+	for (int ty = threadIdx.x >> 6; ty < SG_QGT; ty += 4) {
+	const int y = y0 + ty;
 	if (x >= xb && x < xs - xb && y >= yb && y < ys - yb) {
 		/* smoothed values on the 3x3 neighbourhood of (x, y) */
 		int sm[3][3];
@@ -824,7 +846,7 @@ k_quality_grad(const uint16_t *__restrict__ qbuf, int xs, int ys, const unsigned
 			for (int dx = 0; dx < 3; dx++)
 				sm[dy][dx] = sms[ty + dy][tx + dx];
 		if (sm[1][1] >= SG_Q_THRESHOLD)
-			cnt = 1;
+			cnt += 1;
 		bool mapped = false;
 		for (int dy = -1; dy <= 1; dy++)
 			for (int dx = -1; dx <= 1; dx++) {
@@ -836,9 +858,10 @@ k_quality_grad(const uint16_t *__restrict__ qbuf, int xs, int ys, const unsigned
 		if (mapped) {
 			const long long d1 = sm[1][1] - sm[1][2];
 			const long long d2 = sm[1][1] - sm[2][1];
-			val = (unsigned long long)(d1 * d1 + d2 * d2);
-			pix = 1;
+			val += (unsigned long long)(d1 * d1 + d2 * d2);
+			pix += 1;
 		}
+	}
 	}
 	for (int o = 32; o > 0; o >>= 1) {
 		val += __shfl_down(val, o, 64);
@@ -887,7 +910,7 @@ static int reg_quality(sg_ctx *ctx, SgDevice &dv, hipStream_t s, const uint16_t 
 	hipLaunchKernelGGL(k_quality_sub, dim3((ys + SG_QROWS - 1) / SG_QROWS, nq), dim3(256), 0, s, d_sel, d_frames, S,
 			xs, ys, qbuf, qmax);
 	HIPCHK(hipGetLastError());
-	hipLaunchKernelGGL(k_quality_grad, dim3((xs + 63) / 64, (ys + 3) / 4, nq), dim3(256), 0, s, qbuf, xs, ys,
+	hipLaunchKernelGGL(k_quality_grad, dim3((xs + 63) / 64, (ys + SG_QGT - 1) / SG_QGT, nq), dim3(256), 0, s, qbuf, xs, ys,
 			qmax, acc);
 	HIPCHK(hipGetLastError());
 	std::vector<unsigned long long> h(3 * (size_t)nq);
