@@ -27,6 +27,7 @@ struct SgStackParams {
 	double sig0, sig1;
 	const int *shiftx, *shifty;		/* device [N] */
 	int dbg;				/* A/B timing knob (SG_HIST_DBG), 0 in production */
+	int prio;				/* histogram path: wave priority of the build phase (SG_HIST_PRIO) */
 	const int *hist_tab;			/* device: c1[hist_npad] = shifty*W*2 + 2*shiftx, then int16 sx2[hist_npad] = 2*shiftx */
 	int hist_npad;				/* N rounded up to a multiple of 16 */
 	int hist_maxsx;				/* max |shiftx| (interior-tile test of the histogram path) */
