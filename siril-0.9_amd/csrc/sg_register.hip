@@ -995,12 +995,14 @@ extern "C" int sg_register_dft_u16_device(sg_ctx *ctx, int dev_index, const uint
 	if (rc)
 		return rc;
 
-	/* batch of pairs per launch: 4 planes of S = 2048 (256 MB) measured best (16: +3 %) */
-	int B = (int)((size_t)(256u << 20) / (plane * sizeof(sg_c64)));
+	/* batch of pairs per launch: up to 2 GB of pair planes (32 at S = 2048). Half-spectrum
+	 * passes, configs[1]: 32 or 64 pairs 8.95-9.07 ms, 16: 9.08, 4: 9.22-9.32, 2: 9.02-9.15,
+	 * 1: 9.8 ms of registration (scripts/gpu_regbatch.sh) */
+	int B = (int)((size_t)(2048u << 20) / (plane * sizeof(sg_c64)));
 	if (B < 1)
 		B = 1;
-	if (B > 16)
-		B = 16;
+	if (B > 64)
+		B = 64;
 	if (const char *e = getenv("SG_REG_BATCH"))	/* A/B knob: pairs per launch */
 		B = atoi(e) > 0 ? atoi(e) : B;
 	const int npairs_total = (int)(todo.size() + 1) / 2;
