@@ -698,15 +698,24 @@ k_stack_reduce2(SgStackParams p) {
 	const uint32_t nrec = (uint32_t)p.H * (uint32_t)p.W * 2u;
 	const int N = p.N;
 	uint32_t acc_a = (p.method == 4) ? 65535u : 0u, acc_b = acc_a;
+	/* shifts of 64 frames at a time: one vector load per wave (lane l = frame f0 + l), read
+	 * back per frame with readlane, so a batch's sample loads do not wait on 32 scalar loads */
+	int vsx = 0, vsy = 0;
+	const int lane = threadIdx.x & 63;
 	for (int f0 = 0; f0 < N; f0 += 16) {
+		if ((f0 & 63) == 0 && p.use_shift) {
+			const int fl = f0 + lane < N ? f0 + lane : N - 1;
+			vsx = p.shiftx[fl];
+			vsy = p.shifty[fl];
+		}
 		uint32_t v[16];
 		int nxs[16];
 		bool yis[16], y0s[16];
 #pragma unroll
 		for (int m = 0; m < 16; m++) {
 			const int f = f0 + m < N ? f0 + m : N - 1;
-			const int sx = p.use_shift ? p.shiftx[f] : 0;
-			const int sy = p.use_shift ? p.shifty[f] : 0;
+			const int sx = p.use_shift ? __builtin_amdgcn_readlane(vsx, (f0 & 63) + m) : 0;
+			const int sy = p.use_shift ? __builtin_amdgcn_readlane(vsy, (f0 & 63) + m) : 0;
 			const int nx = x - sx, ny = R - sy;
 			nxs[m] = nx;
 			yis[m] = (unsigned)ny < (unsigned)p.H && f0 + m < N;
