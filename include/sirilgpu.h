@@ -150,6 +150,17 @@ int sg_register_dft_u16(sg_ctx *ctx, const uint16_t *sel, int nframes, int S, in
 int sg_register_dft_u16_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int nframes,
 		int S, int ref_image, const int *included, int *shiftx, int *shifty,
 		double *quality, void *stream);
+/*
+ * The same on a shard of the sequence's frames (frame sharding over GPUs):
+ * quality is left RAW (QualityEstimate per registered frame and the reference,
+ * src/algos/quality.c:46-218; NaN where no pixel passes the threshold), so the caller can
+ * gather every shard's values and apply normalizeQualityData (registration.c:163-176) with
+ * the reference's min/max loop over all frames (sirilgpu_dist.register_sharded).  Frames
+ * outside `included` are neither registered nor written.
+ */
+int sg_register_dft_u16_device_raw(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int nframes,
+		int S, int ref_image, const int *included, int *shiftx, int *shifty,
+		double *quality_raw, void *stream);
 
 /*
  * Perspective warp: replaces cvTransformImage (src/opencv/opencv.cpp:242-309) as the

@@ -938,9 +938,25 @@ static int ilog2(int v) {
 	return l;
 }
 
+static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int nframes, int S, int ref_image,
+		const int *included, int *shiftx, int *shifty, double *quality, void *stream, bool normalize_q);
+
 extern "C" int sg_register_dft_u16_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int nframes,
 		int S, int ref_image, const int *included, int *shiftx, int *shifty, double *quality,
 		void *stream) {
+	return reg_dft_device(ctx, dev_index, d_sel, nframes, S, ref_image, included, shiftx, shifty, quality, stream,
+			true);
+}
+
+extern "C" int sg_register_dft_u16_device_raw(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int nframes,
+		int S, int ref_image, const int *included, int *shiftx, int *shifty, double *quality_raw,
+		void *stream) {
+	return reg_dft_device(ctx, dev_index, d_sel, nframes, S, ref_image, included, shiftx, shifty, quality_raw,
+			stream, false);
+}
+
+static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int nframes, int S, int ref_image,
+		const int *included, int *shiftx, int *shifty, double *quality, void *stream, bool normalize_q) {
 	if (!ctx || dev_index < 0 || dev_index >= (int)ctx->dev.size() || !d_sel || !shiftx || !shifty || !quality)
 		return SG_ERR_GENERIC;
 	if (nframes < 1)
@@ -1150,6 +1166,12 @@ extern "C" int sg_register_dft_u16_device(sg_ctx *ctx, int dev_index, const uint
 
 	/* quality: q_min/q_max seeded by the reference frame, then frames in index order with
 	 * the reference's min() macro (src/core/siril.h), then normalizeQualityData */
+	if (!normalize_q) {	/* raw values of the processed frames (sharded registration) */
+		quality[ref_image] = qual[0];
+		for (size_t k = 0; k < todo.size(); k++)
+			quality[todo[k]] = qual[k + 1];
+		return SG_OK;
+	}
 	double q_min = qual[0], q_max = qual[0];
 	quality[ref_image] = qual[0];
 	for (size_t k = 0; k < todo.size(); k++) {

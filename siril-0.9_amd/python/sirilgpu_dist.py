@@ -8,9 +8,17 @@ rank reads its band (+ the rows its shifts reach) and writes its band of the out
 Only the 3x2 rejection counters (:1796-1817) are summed, the step time is max-reduced,
 and the output bands are gathered when the caller wants the whole image on one rank.
 
+Registration shards over FRAMES (each frame is registered against the reference
+independently, register_shift_dft src/registration/registration.c:182-400): rank r takes a
+contiguous block of frame indices, every rank computes the reference spectrum itself, and
+only the per-frame (shiftx, shifty, raw quality) are all-gathered; normalizeQualityData
+(:163-176, with the min/max loop of :384-392) then runs over all frames in index order on
+every rank, so the result equals the single-process one bit for bit.
+
 torch.distributed is plumbing here: "nccl" is RCCL over xGMI on the GPU node, "gloo" on
 CPU for the tests.  The stacking itself is whatever `stack_band` the caller passes (the
-C-ABI `sg_stack_u16_device` on a GPU).
+C-ABI `sg_stack_u16_device` on a GPU); the per-shard registration is `register_part`
+(`sg_register_dft_u16_device_raw` on a GPU).
 """
 import numpy as np
 
@@ -67,3 +75,62 @@ def stack_sharded(stack_band, height, dist, rank, world, device="cpu"):
     band, rej = stack_band(begin, end)
     img = gather_bands(band, begin, end, height, dist, world, device)
     return img, sum_counters(rej, dist, device)
+
+
+def frame_band(rank, world, nframes):
+    """Contiguous block [begin, end) of frame indices registered by `rank`."""
+    return row_band(rank, world, nframes)
+
+
+def normalize_quality(qraw, nframes, ref_image, included):
+    """The quality bookkeeping of register_shift_dft on all frames: q_min / q_max seeded by
+    the reference, the registered frames in index order with the reference's min() macro and
+    `>` test, then normalizeQualityData (registration.c:163-176) on the included frames."""
+    ref = ref_image if ref_image >= 0 else 0
+    quality = np.zeros(nframes, dtype=np.float64)
+    q_min = q_max = float(qraw[ref])
+    quality[ref] = qraw[ref]
+    for f in range(nframes):
+        if f == ref or (included is not None and not included[f]):
+            continue
+        qv = float(qraw[f])
+        quality[f] = qv
+        if qv > q_max:
+            q_max = qv
+        q_min = q_min if q_min < qv else qv
+    with np.errstate(divide="ignore", invalid="ignore"):     # x / 0.0 as in C: inf / NaN
+        for f in range(nframes):
+            if included is not None and not included[f]:
+                continue
+            quality[f] = quality[f] - q_min
+            quality[f] = quality[f] / np.float64(q_max - q_min)
+    return quality
+
+
+def register_sharded(register_part, nframes, ref_image, included, dist, rank, world, device="cpu"):
+    """Frame-sharded registration.  `register_part(included_local)` registers the frames
+    whose mask entry is set (plus the reference) and returns (shiftx, shifty, raw quality)
+    arrays of length nframes; this rank's mask is `included` restricted to its frame block.
+    Returns (shiftx, shifty, normalised quality) on every rank."""
+    import torch
+    ref = ref_image if ref_image >= 0 else 0
+    inc = np.ones(nframes, dtype=np.int32) if included is None else np.asarray(included, dtype=np.int32)
+    b, e = frame_band(rank, world, nframes)
+    mine = np.zeros(nframes, dtype=np.int32)
+    mine[b:e] = inc[b:e]
+    sx, sy, q = register_part(mine)
+    rows = np.zeros((3, nframes), dtype=np.float64)
+    rows[0], rows[1], rows[2] = sx, sy, q
+    t = _tensor(rows, device)
+    outs = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(outs, t)
+    gx = np.zeros(nframes, dtype=np.int32)
+    gy = np.zeros(nframes, dtype=np.int32)
+    gq = np.zeros(nframes, dtype=np.float64)
+    for r in range(world):
+        rb, re = frame_band(r, world, nframes)
+        o = outs[r].cpu().numpy()
+        gx[rb:re], gy[rb:re], gq[rb:re] = o[0, rb:re], o[1, rb:re], o[2, rb:re]
+    gq[ref] = outs[0].cpu().numpy()[2, ref]         # every rank measured the reference
+    gx[ref] = gy[ref] = 0
+    return gx, gy, normalize_quality(gq, nframes, ref, included)

@@ -52,3 +52,29 @@ def test_row_band_partition():
             assert all(bands[i][1] == bands[i + 1][0] for i in range(world - 1))
             sizes = [e - b for b, e in bands]
             assert max(sizes) - min(sizes) <= 1
+
+
+@pytest.mark.parametrize("world,ref,excl", [(2, 0, False), (3, 4, True)])
+def test_register_sharding_gloo(world, ref, excl, tmp_path):
+    """frame-sharded registration (sirilgpu_dist.register_sharded) reassembles the
+    single-process shifts and normalised qualities exactly"""
+    S, n = 32, 7
+    sel = orc.synth(n, 1, S, S, seed=23, maxshift=3)[:, 0].copy()
+    sel[:, 10:12, 14:16] = 45000
+    sel[2, 20:23, 5:8] = 60000          # a frame with a different quality
+    inc = np.array([1, 1, 0, 1, 1, 1, 0], dtype=np.int32) if excl else None
+    rx, ry, rq = orc.register_dft(sel, ref_image=ref, included=inc)
+    inp = tmp_path / "in.npz"
+    np.savez(inp, sel=sel, ref=np.array(ref), inc=inc if inc is not None else np.zeros(0, np.int32))
+    port = _free_port()
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_reg_worker.py")
+    procs = [subprocess.Popen([sys.executable, worker, str(r), str(world), str(port), str(inp),
+                               str(tmp_path / f"reg{r}.npz")]) for r in range(world)]
+    for p in procs:
+        assert p.wait(timeout=180) == 0
+    for r in range(world):
+        d = np.load(tmp_path / f"reg{r}.npz", allow_pickle=False)
+        keep = np.ones(n, bool) if inc is None else inc.astype(bool)
+        assert np.array_equal(d["sx"][keep], rx[keep]) and np.array_equal(d["sy"][keep], ry[keep]), r
+        q, rq_k = d["q"][keep], rq[keep]
+        assert np.array_equal(np.isnan(q), np.isnan(rq_k)) and np.array_equal(q[~np.isnan(q)], rq_k[~np.isnan(rq_k)])

@@ -70,3 +70,37 @@ def test_register_rejects_non_power_of_two(gpu_ctx):
     sel = np.zeros((2, 48, 48), dtype=np.uint16)
     with pytest.raises(RuntimeError):
         gpu_ctx.register_dft(sel)
+
+
+@pytest.mark.parametrize("world,ref", [(2, 0), (3, 5)])
+def test_register_raw_shards_reassemble(gpu_ctx, world, ref):
+    """sg_register_dft_u16_device_raw on frame shards (frames sharded over GPUs,
+    shifts / raw qualities gathered, normalizeQualityData over all frames) equals the
+    single-call sg_register_dft_u16 result exactly; shards run one after the other here (the
+    gloo test covers the all_gather path)."""
+    import torch
+    import sirilgpu_dist as sd
+    S, n = 128, 9
+    sel = orc.synth(n, 1, S, S, seed=99 + world, maxshift=6)[:, 0].copy()
+    sel[:, S // 3:S // 3 + 3, S // 2:S // 2 + 3] = 40000
+    sel[4, 10:14, 90:94] = 62000
+    gx, gy, gq = gpu_ctx.register_dft(sel, ref_image=ref)
+    d_sel = torch.from_numpy(sel.view(np.int16)).cuda()
+    sx = np.zeros(n, np.int32)
+    sy = np.zeros(n, np.int32)
+    qraw = np.zeros(n, np.float64)
+    for r in range(world):
+        b, e = sd.frame_band(r, world, n)
+        mine = np.zeros(n, np.int32)
+        mine[b:e] = 1
+        px, py, pq = gpu_ctx.register_dft_device(d_sel.data_ptr(), n, S, ref_image=ref, included=mine,
+                                                 raw_quality=True)
+        torch.cuda.synchronize()
+        sx[b:e], sy[b:e], qraw[b:e] = px[b:e], py[b:e], pq[b:e]
+        qraw[ref] = pq[ref]
+    sx[ref] = sy[ref] = 0
+    q = sd.normalize_quality(qraw, n, ref, None)
+    assert np.array_equal(sx, gx) and np.array_equal(sy, gy)
+    assert _same_q(q, gq), (q, gq)
+    # the raw values are QualityEstimate's (the oracle's, exactly)
+    assert _same_q(qraw, np.array([orc.quality(sel[f]) for f in range(n)]))
