@@ -726,7 +726,7 @@ k_reg_final(const SgBest *__restrict__ best, int S, int count, int *__restrict__
 
 /* SubSample (:223-234) of one 3x3 sample row, plus the running max of the middle rows
  * (the maxp[] loop :119-133 reduces to max over 0 < v < 65530) */
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(1024)
 k_quality_sub(const uint16_t *__restrict__ sel, const int *__restrict__ qframes, int S, int xs, int ys,
 		uint16_t *__restrict__ qbuf, unsigned int *__restrict__ qmax) {
 	/* SG_QROWS output rows per workgroup; a thread forms two adjacent outputs from three
@@ -907,7 +907,12 @@ static int reg_quality(sg_ctx *ctx, SgDevice &dv, hipStream_t s, const uint16_t 
 	unsigned int *qmax = (unsigned int *)(acc + 3 * nq);
 	HIPCHK(hipMemcpyAsync(d_frames, frames.data(), sizeof(int) * nq, hipMemcpyHostToDevice, s));
 	HIPCHK(hipMemsetAsync(dv.reg_qacc.p, 0, (size_t)nq * (3 * sizeof(unsigned long long) + sizeof(unsigned int)), s));
-	hipLaunchKernelGGL(k_quality_sub, dim3((ys + SG_QROWS - 1) / SG_QROWS, nq), dim3(256), 0, s, d_sel, d_frames, S,
+	/* one wave per workgroup, walking the row pairs: 283 us per 129 frames of 2048^2 against
+	 * 332 / 348 / 403 / 618 us with 128 / 192 / 256 / 384 threads (scripts/gpu_qsub.sh) */
+	int qthr = 64;
+	if (const char *e = getenv("SG_QSUB_THREADS"))	/* A/B knob: threads per subsample workgroup (64-multiple) */
+		qthr = atoi(e) >= 64 && atoi(e) <= 1024 ? atoi(e) / 64 * 64 : 256;
+	hipLaunchKernelGGL(k_quality_sub, dim3((ys + SG_QROWS - 1) / SG_QROWS, nq), dim3(qthr), 0, s, d_sel, d_frames, S,
 			xs, ys, qbuf, qmax);
 	HIPCHK(hipGetLastError());
 	hipLaunchKernelGGL(k_quality_grad, dim3((xs + 63) / 64, (ys + SG_QGT - 1) / SG_QGT, nq), dim3(256), 0, s, qbuf, xs, ys,
