@@ -837,7 +837,7 @@ k_quality_grad(const uint16_t *__restrict__ qbuf, int xs, int ys, const unsigned
 	const int tx = threadIdx.x & 63;
 	const int x = x0 + tx;
 	unsigned long long val = 0, pix = 0, cnt = 0;
-	for (int ty = threadIdx.x >> 6; ty < SG_QGT; ty += 4) {
+	for (int ty = threadIdx.x >> 6; ty < SG_QGT; ty += (int)(blockDim.x >> 6)) {
 	const int y = y0 + ty;
 	if (x >= xb && x < xs - xb && y >= yb && y < ys - yb) {
 		/* smoothed values on the 3x3 neighbourhood of (x, y) */
@@ -876,7 +876,7 @@ k_quality_grad(const uint16_t *__restrict__ qbuf, int xs, int ys, const unsigned
 	}
 	__syncthreads();
 	if (threadIdx.x == 0) {
-		for (int w = 1; w < 4; w++) {
+		for (int w = 1; w < (int)(blockDim.x >> 6); w++) {
 			val += sv[w];
 			pix += sp[w];
 			cnt += sc[w];
@@ -915,7 +915,12 @@ static int reg_quality(sg_ctx *ctx, SgDevice &dv, hipStream_t s, const uint16_t 
 	hipLaunchKernelGGL(k_quality_sub, dim3((ys + SG_QROWS - 1) / SG_QROWS, nq), dim3(qthr), 0, s, d_sel, d_frames, S,
 			xs, ys, qbuf, qmax);
 	HIPCHK(hipGetLastError());
-	hipLaunchKernelGGL(k_quality_grad, dim3((xs + 63) / 64, (ys + SG_QGT - 1) / SG_QGT, nq), dim3(256), 0, s, qbuf, xs, ys,
+	/* 2 waves per 64x16 tile: 214 us per 129 frames against 238 (4 waves) and 333 (1 wave),
+	 * scripts/gpu_qgrad.sh */
+	int gthr = 128;
+	if (const char *e = getenv("SG_QGRAD_THREADS"))	/* A/B knob: 64, 128 or 256 threads per gradient tile */
+		gthr = (atoi(e) == 64 || atoi(e) == 256) ? atoi(e) : 128;
+	hipLaunchKernelGGL(k_quality_grad, dim3((xs + 63) / 64, (ys + SG_QGT - 1) / SG_QGT, nq), dim3(gthr), 0, s, qbuf, xs, ys,
 			qmax, acc);
 	HIPCHK(hipGetLastError());
 	std::vector<unsigned long long> h(3 * (size_t)nq);
