@@ -7,10 +7,12 @@ NO_NORM, registration shifts applied) of 512 synthetic 4096x4096 u16 mono frames
 frames resident in HBM (generated on the device by include/sg_synth.h).
 
 One step = one sg_stack_u16_device() call over the whole 512-frame sequence.
-Multi-GPU (torchrun, one process per GPU): weak scaling by row bands -- rank r stacks its
-own 4096-row band of a (4096*G) x 4096 sequence of 512 frames; no data-path collective
-(each rank's band is written to its own output); the 6 rejection counters and the step
-times are all-reduced (max for time).
+Multi-GPU (torchrun, one process per GPU): weak scaling by row bands -- one sequence of
+512 frames of (4096*G) x 4096 with one set of registration shifts; rank r owns output rows
+[4096 r, 4096 (r+1)) and holds only the frame rows they read (its band plus the rows the
+shifts reach, sg_stack_desc.resident_rows); no data-path collective (each rank's band is
+written to its own output); the 6 rejection counters and the step times are all-reduced
+(max for time).
 
 Output: one JSON line on rank 0 (see README / DESIGN.md for the fields).
 """
@@ -229,17 +231,23 @@ def main():
     rej_mode = {"sigma": sg.SIGMA, "winsorized": sg.WINSORIZED, "none": sg.NO_REJEC,
                 "percentile": sg.PERCENTILE}[args.rejection]
     ctx = sg.Context([dev])
-    # this rank's band: rows [rank*H, (rank+1)*H) of a (H*world)-row sequence; the device
-    # buffer holds just the band, addressed through a biased base pointer
-    fstride = H * W + args.frame_pad
-    frames = torch.empty(N * fstride, dtype=torch.int16, device="cuda")
-    out = torch.empty(H * W, dtype=torch.int16, device="cuda")
-    ctx.synth_fill(frames.data_ptr(), N, 1, H, W, 0, H, 0x5151 + rank, args.maxshift, frame_stride=fstride)
-    shx, shy = synth_shifts_np(N, 0x5151 + rank, args.maxshift)
+    # one sequence of N frames of (H*world) x W; this rank owns output rows [rank*H,
+    # (rank+1)*H) and holds only the frame rows they read (the band plus the rows its
+    # registration shifts reach), addressed through a biased base pointer
+    Htot = H * world
+    shx, shy = synth_shifts_np(N, 0x5151, args.maxshift)
     if args.even_shifts:
         shx &= ~1
     if args.zero_shift:
         (shx if args.zero_shift == "x" else shy)[:] = 0
+    b, e = rank * H, (rank + 1) * H
+    lo, hi = max(0, b - int(shy.max())), min(Htot - 1, e - 1 - int(shy.min()))
+    nres = hi - lo + 1
+    fstride = nres * W + args.frame_pad
+    frames = torch.empty(N * fstride, dtype=torch.int16, device="cuda")
+    out = torch.empty(Htot * W, dtype=torch.int16, device="cuda")
+    base = frames.data_ptr() - lo * W * 2
+    ctx.synth_fill(base, N, 1, Htot, W, lo, hi + 1, 0x5151, args.maxshift, frame_stride=fstride)
     norm_mode, off, mul, scale = sg.NO_NORM, None, None, None
     if args.normalize != "none":
         # synthetic per-frame location / scale (the cached IKSS statistics), coefficients as
@@ -256,12 +264,12 @@ def main():
             norm_mode = sg.MULTIPLICATIVE_SCALING
             scale = scl[0] / scl
             mul = loc[0] / loc
-    desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=rej_mode, sig=(4.0, 3.0),
+    desc, keep = sg.make_desc(sg.MEAN, N, W, Htot, 1, rejection=rej_mode, sig=(4.0, 3.0),
                               shiftx=shx, shifty=shy, normalize=norm_mode, offset=off, mul=mul, scale=scale,
-                              max_thread=8, max_number_of_rows=H)
+                              max_thread=8, max_number_of_rows=Htot, resident_rows=(lo, hi + 1))
 
     def step():
-        return ctx.stack_device(desc, frames.data_ptr(), fstride, H * W, out.data_ptr(), 0, H)
+        return ctx.stack_device(desc, base, fstride, nres * W, out.data_ptr(), b, e)
 
     for _ in range(args.warmup):
         step()
@@ -307,7 +315,8 @@ def main():
             "vs_baseline": None,
             "dtype": "u16",
             "data": "synthetic (include/sg_synth.h, generated in HBM)",
-            "config": {"workload": f"sigma-clip stack {N}x{H}x{W} u16 mono per GPU (BASELINE configs[2])",
+            "config": {"workload": f"sigma-clip stack {N}x{H}x{W} u16 mono per GPU (BASELINE configs[2]"
+                                   + (")" if world == 1 else f"; one {N}x{Htot}x{W} sequence in {world} row bands)"),
                        "frames": N, "height": H, "width": W, "rejection": args.rejection,
                        "sig": [4.0, 3.0], "normalize": args.normalize, "parallelism": f"row-band x{world}"},
             "roofline": roofline(achieved, algo_bytes, N, H, W, args.rejection

@@ -76,7 +76,11 @@ typedef struct {
 	int max_thread;		/* com.max_thread: the reference's OpenMP team size */
 	int max_number_of_rows;	/* args->max_number_of_rows */
 	int kernel_path;	/* SG_PATH_*: 0 = automatic (no reference equivalent; testing/A-B) */
-	int reserved[5];
+	/* memory rows [resident_rows[0], resident_rows[1]) of every frame are present at
+	 * d_frames (sg_stack_u16_device); {0, 0} = all rows [0, height).  No reference
+	 * equivalent: it lets a rank hold only its row band plus the rows its shifts reach. */
+	int resident_rows[2];
+	int reserved[3];
 } sg_stack_desc;
 
 typedef struct sg_ctx sg_ctx;
@@ -100,12 +104,20 @@ int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *desc, sg_read_region_fn pull,
 
 /*
  * Device-resident stack (frames already in HBM).  d_frames holds frame i, channel c, memory
- * row r, column x at d_frames[i*frame_stride + c*plane_stride + r*width + x]; only rows
- * [row_begin - 32768.., row_end + ..) reachable through the shifts are read, so a rank that
- * owns a row band may pass a base pointer biased by -band_first_row*width.  Output rows
+ * row r, column x at d_frames[i*frame_stride + c*plane_stride + r*width + x].  Output rows
  * [row_begin, row_end) (memory order) of every channel are written to d_out (same indexing
  * as a [C][H][W] image).  `stream` is a hipStream_t (NULL = the context's stream of device
- * `dev_index`).  Synchronous unless async != 0.
+ * `dev_index`).  The call is synchronous.
+ *
+ * Row bands (one rank per band): the band's output rows read frame rows
+ * [row_begin - max(shifty), row_end - min(shifty)) (clipped to the frame), and those rows
+ * must lie inside desc->resident_rows (else SG_ERR_SIZE); a rank holding only them may pass a
+ * base pointer biased by -resident_rows[0]*width.  A rejection stack whose FIRST sigma pass
+ * breaks early (`N - r <= 4`, stacking.c:1684) reads the previous pixel's stale rejected[]
+ * (SURVEY §8a a3 iii); the previous pixel in the reference's OpenMP thread order can lie
+ * outside the band, and is then recomputed from the frames.  If its rows are not resident
+ * the call fails with SG_ERR_GENERIC instead of guessing: for such stacks (in practice
+ * small N with strong rejection) make the full frames resident.
  */
 int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_desc *desc,
 		const uint16_t *d_frames, int64_t frame_stride, int64_t plane_stride,

@@ -218,9 +218,13 @@ static hipError_t launch_sorted(int nreg, bool listed, dim3 grid, size_t lds, hi
 	return hipErrorInvalidValue;
 }
 
-extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
+/* SUM over row bands streamed by the host-pull path: the raw sums and the maximum carry
+ * across the band calls, the scaling runs once after the last band */
+enum { SUM_WHOLE = 0, SUM_FIRST_BAND = 1, SUM_MID_BAND = 2, SUM_LAST_BAND = 3 };
+
+static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		const uint16_t *d_frames, int64_t frame_stride, int64_t plane_stride, uint16_t *d_out,
-		int row_begin, int row_end, uint64_t rej[3][2], uint64_t *maxim_out, void *stream) {
+		int row_begin, int row_end, uint64_t rej[3][2], uint64_t *maxim_out, void *stream, int sum_mode) {
 	if (!ctx || !d || dev_index < 0 || dev_index >= (int)ctx->dev.size())
 		return SG_ERR_GENERIC;
 	SgDevice &dv = ctx->dev[dev_index];
@@ -255,6 +259,33 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 	p.use_shift = (d->method != SG_STACK_MEDIAN) && d->shiftx && d->shifty;
 	p.row_begin = row_begin;
 	p.row_end = row_end;
+	p.res_begin = 0;
+	p.res_end = H;
+	if (d->resident_rows[0] != 0 || d->resident_rows[1] != 0) {
+		p.res_begin = d->resident_rows[0];
+		p.res_end = d->resident_rows[1];
+		if (p.res_begin < 0 || p.res_end > H || p.res_begin >= p.res_end)
+			return set_err(ctx, SG_ERR_SIZE, "bad resident row range%s %ld", "", (long)p.res_begin);
+	}
+	p.sy_min = p.sy_max = 0;
+	if (p.use_shift) {
+		p.sy_min = p.sy_max = d->shifty[0];
+		for (int i = 1; i < N; i++) {
+			p.sy_min = std::min(p.sy_min, d->shifty[i]);
+			p.sy_max = std::max(p.sy_max, d->shifty[i]);
+		}
+	}
+	{
+		/* the frame rows the band's output rows read (R - shifty, :1550-1577) must be resident */
+		const int lo = (int)std::max<int64_t>(0, (int64_t)row_begin - p.sy_max);
+		const int hi = (int)std::min<int64_t>(H - 1, (int64_t)row_end - 1 - p.sy_min);
+		if (lo <= hi && (lo < p.res_begin || hi >= p.res_end)) {
+			char m[160];
+			snprintf(m, sizeof m, "frame rows %d..%d read by the band are not all resident (%d..%d)", lo, hi,
+					p.res_begin, p.res_end - 1);
+			return set_err(ctx, SG_ERR_SIZE, "%s%.0ld", m, 0);
+		}
+	}
 	{
 		const char *dbg = getenv("SG_HIST_DBG");
 		p.dbg = dbg ? atoi(dbg) : 0;
@@ -323,9 +354,11 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 	HIPCHK(ensure(dv.maxim, 64));
 	HIPCHK(hipMemsetAsync(dv.rej.p, 0, sizeof(unsigned long long) * SG_REJ_SHARDS * 6, s));
 	HIPCHK(hipMemsetAsync(dv.flag_count.p, 0, 64, s));
-	HIPCHK(hipMemsetAsync(dv.maxim.p, 0, 64, s));
+	if (sum_mode == SUM_WHOLE || sum_mode == SUM_FIRST_BAND)
+		HIPCHK(hipMemsetAsync(dv.maxim.p, 0, 64, s));
 	p.rej = (unsigned long long *)dv.rej.p;
 	p.flag_count = (unsigned int *)dv.flag_count.p;
+	p.walk_fault = p.flag_count + 1;
 	p.maxim = (unsigned int *)dv.maxim.p;
 
 	const bool sorted = (d->method == SG_STACK_MEDIAN) ||
@@ -511,8 +544,17 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 		HIPCHK(hipEventRecord(dv.ev[1], s));
 		ctx->stats.main_kernel_blocks = pairs ? (int)(grid2.x * grid2.y * grid2.z) : (int)(grid.x * grid.y * grid.z);
 		ctx->stats.launches = 1;
-		if (d->method == SG_STACK_SUM) {
-			hipLaunchKernelGGL(k_sum_finalize, grid, dim3(256), 0, s, p);
+		if (d->method == SG_STACK_SUM && (sum_mode == SUM_WHOLE || sum_mode == SUM_LAST_BAND)) {
+			/* the 65535/max scaling (:328-342) needs the maximum over the whole image: a
+			 * streamed sequence finalises every row once its last band is summed */
+			SgStackParams pf = p;
+			dim3 gf = grid;
+			if (sum_mode == SUM_LAST_BAND) {
+				pf.row_begin = 0;
+				pf.row_end = H;
+				gf.y = H;
+			}
+			hipLaunchKernelGGL(k_sum_finalize, gf, dim3(256), 0, s, pf);
 			HIPCHK(hipGetLastError());
 			ctx->stats.launches++;
 		}
@@ -520,11 +562,14 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 	HIPCHK(hipEventRecord(dv.ev[2], s));
 	/* counters back to the host */
 	std::vector<unsigned long long> shards(SG_REJ_SHARDS * 6);
-	unsigned int cnt[2] = {0, 0};
+	unsigned int cnt[3] = {0, 0, 0};	/* flag count, walk fault, sum maximum */
 	HIPCHK(hipMemcpyAsync(shards.data(), dv.rej.p, sizeof(unsigned long long) * shards.size(), hipMemcpyDeviceToHost, s));
-	HIPCHK(hipMemcpyAsync(cnt, dv.flag_count.p, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
-	HIPCHK(hipMemcpyAsync(cnt + 1, dv.maxim.p, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+	HIPCHK(hipMemcpyAsync(cnt, dv.flag_count.p, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+	HIPCHK(hipMemcpyAsync(cnt + 2, dv.maxim.p, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
 	HIPCHK(hipStreamSynchronize(s));
+	if (cnt[1])
+		return set_err(ctx, SG_ERR_GENERIC, "a first-pass early break needs the stale rejected[] of a pixel "
+				"whose frame rows are not resident; make the full frames resident%s%.0ld", "", 0);
 	if (p.dbg == 12)
 		sg_dbg_why_dump(s);
 	float ms = 0.f, ms2 = 0.f;
@@ -543,11 +588,35 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 			}
 	}
 	if (maxim_out)
-		*maxim_out = cnt[1];
+		*maxim_out = cnt[2];
 	return SG_OK;
 }
 
-/* host-pull path: frames come through seq_opened_read_region-shaped callbacks */
+extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
+		const uint16_t *d_frames, int64_t frame_stride, int64_t plane_stride, uint16_t *d_out,
+		int row_begin, int row_end, uint64_t rej[3][2], uint64_t *maxim_out, void *stream) {
+	return stack_device_core(ctx, dev_index, d, d_frames, frame_stride, plane_stride, d_out, row_begin,
+			row_end, rej, maxim_out, stream, SUM_WHOLE);
+}
+
+/* HBM the host-pull path may fill with frames: SG_HOST_BUDGET_BYTES (tests), else 85 % of
+ * the free device memory (plus what the context already holds for frames) */
+static size_t host_budget(SgDevice &dv) {
+	if (const char *e = getenv("SG_HOST_BUDGET_BYTES"))
+		return (size_t)atoll(e);
+	size_t fr = 0, tot = 0;
+	if (hipMemGetInfo(&fr, &tot) != hipSuccess)
+		return 0;
+	return (size_t)((double)(fr + dv.frames.size) * 0.85);
+}
+
+/*
+ * host-pull path: frames come through seq_opened_read_region-shaped callbacks.  Like the
+ * reference's row blocks (stacking.c:1397-1476, sized from the memory budget :1903-1915),
+ * a sequence larger than the HBM budget is stacked in row bands: for each band the rows
+ * its shifts reach are pulled for every frame (the reference's area.y += shifty reads,
+ * :1544-1577), uploaded through two pinned buffers, and stacked with those rows resident.
+ */
 extern "C" int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *d, sg_read_region_fn pull, void *user,
 		sg_should_continue_fn cont, void *cont_user, uint16_t *out, uint64_t rej[3][2],
 		uint64_t *maxim) {
@@ -560,42 +629,98 @@ extern "C" int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *d, sg_read_region_
 	if (W <= 0 || H <= 0 || C < 1 || C > 3)
 		return SG_ERR_SIZE;
 	HIPCHK(hipSetDevice(dv.id));
-	const size_t plane = (size_t)W * H;
+	/* frame rows a band reads: [b - sy_max, e - 1 - sy_min] */
+	const bool use_shift = d->method != SG_STACK_MEDIAN && d->shiftx && d->shifty;
+	int sy_min = 0, sy_max = 0;
+	for (int i = 0; use_shift && i < N; i++) {
+		sy_min = i ? std::min(sy_min, d->shifty[i]) : d->shifty[i];
+		sy_max = i ? std::max(sy_max, d->shifty[i]) : d->shifty[i];
+	}
+	const int64_t halo = std::min<int64_t>((int64_t)sy_max - sy_min, H);
+	const size_t row_bytes = (size_t)N * C * W * sizeof(uint16_t);	/* one row of every frame */
+	int band = H;
+	const size_t budget = host_budget(dv);
+	if ((size_t)H * row_bytes > budget) {
+		const int64_t fit = (int64_t)(budget / row_bytes) - halo;
+		if (fit < 1)
+			return set_err(ctx, SG_ERR_SIZE, "the sequence does not fit the device even one row at a "
+					"time%s%.0ld", "", 0);
+		band = (int)std::min<int64_t>(fit, H);
+	}
+	const int64_t rows_cap = std::min<int64_t>(band + halo, H);
+	const size_t plane = (size_t)rows_cap * W;
 	HIPCHK(ensure(dv.frames, plane * C * N * sizeof(uint16_t)));
-	HIPCHK(ensure(dv.out, plane * C * sizeof(uint16_t)));
+	HIPCHK(ensure(dv.out, (size_t)W * H * C * sizeof(uint16_t)));
 	if (dv.pinned_size < plane) {
 		for (int k = 0; k < 2; k++) {
 			if (dv.pinned[k])
 				(void)hipHostFree(dv.pinned[k]);
+			dv.pinned[k] = nullptr;
+			dv.pinned_size = 0;
 			HIPCHK(hipHostMalloc((void **)&dv.pinned[k], plane * sizeof(uint16_t) * 2));
 		}
 		dv.pinned_size = plane;
 	}
-	uint16_t *band = dv.pinned[0] + plane;	/* top-down band as returned by the reader */
-	sg_rect area = {0, 0, W, H};
+	if (rej)
+		for (int c = 0; c < 3; c++)
+			rej[c][0] = rej[c][1] = 0;
+	const int nbands = (H + band - 1) / band;
 	int k = 0;
-	for (int i = 0; i < N; i++) {
-		if (cont && !cont(cont_user))
-			return SG_ERR_GENERIC;	/* cancelled, like get_thread_run() */
-		for (int c = 0; c < C; c++) {
-			uint16_t *flip = dv.pinned[k];
-			HIPCHK(hipStreamSynchronize(dv.stream));	/* buffer k free again */
-			uint16_t *tb = flip + plane;
-			if (pull(user, c, i, tb, &area) < 0)
-				return set_err(ctx, SG_ERR_READ, "could not read frame%s %ld", "", i);
-			for (int t = 0; t < H; t++)
-				memcpy(flip + (size_t)(H - 1 - t) * W, tb + (size_t)t * W, W * sizeof(uint16_t));
-			HIPCHK(hipMemcpyAsync((uint16_t *)dv.frames.p + ((size_t)i * C + c) * plane, flip,
-					plane * sizeof(uint16_t), hipMemcpyHostToDevice, dv.stream));
-			k ^= 1;
+	bool used[2] = {false, false};
+	for (int bi = 0; bi < nbands; bi++) {
+		const int b = bi * band, e = std::min(H, b + band);
+		int lo = (int)std::max<int64_t>(0, (int64_t)b - sy_max);
+		int hi = (int)std::min<int64_t>(H - 1, (int64_t)e - 1 - sy_min);
+		if (lo > hi)	/* every row of the band is shifted out of the frames: nothing is read */
+			lo = hi = std::min(b, H - 1);
+		const int nres = hi - lo + 1;
+		const size_t bplane = (size_t)nres * W;
+		/* top-down area of memory rows lo..hi (the reference's region convention) */
+		const sg_rect area = {0, H - 1 - hi, W, nres};
+		/* two pinned buffers: the reader fills and flips one while the other's upload is
+		 * in flight; a buffer is reused once the event recorded after its upload fired */
+		for (int i = 0; i < N; i++) {
+			if (cont && !cont(cont_user)) {
+				(void)hipStreamSynchronize(dv.stream);
+				return SG_ERR_GENERIC;	/* cancelled, like get_thread_run() */
+			}
+			for (int c = 0; c < C; c++) {
+				uint16_t *flip = dv.pinned[k];
+				if (used[k])
+					HIPCHK(hipEventSynchronize(dv.io_ev[k]));	/* buffer k free again */
+				uint16_t *tb = flip + plane;	/* top-down band as returned by the reader */
+				if (pull(user, c, i, tb, &area) < 0) {
+					(void)hipStreamSynchronize(dv.stream);
+					return set_err(ctx, SG_ERR_READ, "could not read frame%s %ld", "", i);
+				}
+				for (int t = 0; t < nres; t++)
+					memcpy(flip + (size_t)(nres - 1 - t) * W, tb + (size_t)t * W, W * sizeof(uint16_t));
+				HIPCHK(hipMemcpyAsync((uint16_t *)dv.frames.p + ((size_t)i * C + c) * bplane, flip,
+						bplane * sizeof(uint16_t), hipMemcpyHostToDevice, dv.stream));
+				HIPCHK(hipEventRecord(dv.io_ev[k], dv.stream));
+				used[k] = true;
+				k ^= 1;
+			}
 		}
+		sg_stack_desc bd = *d;
+		bd.resident_rows[0] = lo;
+		bd.resident_rows[1] = hi + 1;
+		const int sum_mode = d->method != SG_STACK_SUM || nbands == 1 ? SUM_WHOLE
+			: bi == 0 ? SUM_FIRST_BAND : bi == nbands - 1 ? SUM_LAST_BAND : SUM_MID_BAND;
+		uint64_t brej[3][2];
+		/* base pointer biased so that memory row r of a frame plane sits at r*W */
+		const uint16_t *base = (const uint16_t *)dv.frames.p - (ptrdiff_t)lo * W;
+		int rc = stack_device_core(ctx, 0, &bd, base, (int64_t)bplane * C, (int64_t)bplane,
+				(uint16_t *)dv.out.p, b, e, brej, maxim, nullptr, sum_mode);
+		if (rc)
+			return rc;
+		if (rej)
+			for (int c = 0; c < 3; c++) {
+				rej[c][0] += brej[c][0];
+				rej[c][1] += brej[c][1];
+			}
 	}
-	(void)band;
-	int rc = sg_stack_u16_device(ctx, 0, d, (const uint16_t *)dv.frames.p, (int64_t)plane * C,
-			(int64_t)plane, (uint16_t *)dv.out.p, 0, H, rej, maxim, nullptr);
-	if (rc)
-		return rc;
-	HIPCHK(hipMemcpy(out, dv.out.p, plane * C * sizeof(uint16_t), hipMemcpyDeviceToHost));
+	HIPCHK(hipMemcpy(out, dv.out.p, (size_t)W * H * C * sizeof(uint16_t), hipMemcpyDeviceToHost));
 	return SG_OK;
 }
 

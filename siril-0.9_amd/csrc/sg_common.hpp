@@ -34,6 +34,9 @@ struct SgStackParams {
 	const double *hist_norm;		/* device: {scale, offset | mul} per frame (hist_npad pairs), normalised stacks */
 	const double *offset, *mul, *scale;	/* device [N] or null */
 	int row_begin, row_end;			/* memory rows to compute */
+	int res_begin, res_end;			/* memory rows present at `frames` (desc->resident_rows) */
+	int sy_min, sy_max;			/* range of shifty (0, 0 without shifts) */
+	unsigned int *walk_fault;		/* set when a stale-state chain needs rows that are not resident */
 	unsigned long long *rej;		/* [SG_REJ_SHARDS][3][2] */
 	unsigned int *flag_count;
 	unsigned int *flag_list;		/* encoded (c*H + R)*W + x */

@@ -623,6 +623,8 @@ k_stack_reduce(SgStackParams p) {
 	 * out-of-frame sample loads a valid dummy address and is masked), so each wave keeps 16
 	 * row reads in flight */
 	uint32_t acc = (p.method == 4) ? 65535u : 0u;
+	/* the dummy address: a resident row of frame 0 (the base may be biased to a band) */
+	const int64_t dummy = (int64_t)p.res_begin * p.W;
 	for (int f0 = 0; f0 < N; f0 += 16) {
 		uint32_t v[16], xin = 0, ok = 0;
 #pragma unroll
@@ -635,7 +637,7 @@ k_stack_reduce(SgStackParams p) {
 			bool ld = live && f0 + m < N && xi && yi;
 			if (p.method != 1 && nx == 0 && ny == 0)
 				ld = false;	/* `ii > 0`: source pixel 0 is never used (:307) */
-			const int64_t off = ld ? (int64_t)f * p.frame_stride + (int64_t)ny * p.W + nx : 0;
+			const int64_t off = ld ? (int64_t)f * p.frame_stride + (int64_t)ny * p.W + nx : dummy;
 			v[m] = plane[off];
 			v[m] = ld ? v[m] : 0u;
 			xin |= (uint32_t)(xi && f0 + m < N) << m;
@@ -1050,6 +1052,18 @@ __device__ int64_t chain_succ(const SgStackParams &p, const SgChainTables &t, in
 	return -1;
 }
 
+__device__ __forceinline__ bool chain_in_band(const SgStackParams &p, int64_t pix) {
+	const int R = (int)((pix / p.W) % p.H);
+	return R >= p.row_begin && R < p.row_end;
+}
+
+/* every frame row pixel `pix` reads (R - shifty, clipped to the frame) is resident */
+__device__ __forceinline__ bool chain_resident(const SgStackParams &p, int64_t pix) {
+	const int R = (int)((pix / p.W) % p.H);
+	const int lo = max(0, R - p.sy_max), hi = min(p.H - 1, R - p.sy_min);
+	return lo > hi || (lo >= p.res_begin && hi < p.res_end);
+}
+
 __device__ __forceinline__ void gather_stack(const SgStackParams &p, int64_t pix, uint16_t *stack) {
 	const int x = (int)(pix % p.W);
 	const int64_t cr = pix / p.W;
@@ -1421,7 +1435,11 @@ k_stack_replay(SgStackParams p) {
 /* phase 1: queued pixels (class LITERAL) replayed with an all-zero incoming rejected[];
  * a pixel whose first pass breaks early with N > 4 read its predecessor's stale entries
  * and is promoted to class CHAIN (no output).  phase 2: class CHAIN pixels replay the
- * chain from the last self-determined predecessor in reference thread order. */
+ * chain from the last self-determined predecessor in reference thread order.  Only pixels
+ * of the band [row_begin, row_end) were classified; a predecessor outside it is classified
+ * here (replayed from a zero rejected[]: a first pass without an early break writes every
+ * entry, so its final state is its own), and one whose rows are not resident stops the
+ * pixel with walk_fault set (the call then fails). */
 __global__ void __launch_bounds__(64)
 k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *scratch, int phase) {
 	const unsigned int nthreads = gridDim.x * blockDim.x;
@@ -1441,13 +1459,38 @@ k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *s
 			continue;	/* SG_CLS_DONE: finished by k_stack_replay */
 		uint32_t crej[2] = {0, 0};
 		int fbrk;
-		for (int k = 0; k < p.N; k++)
-			rejected[k] = 0;
-		if (phase == 2) {
+		if (phase == 1) {
+			for (int k = 0; k < p.N; k++)
+				rejected[k] = 0;
+		} else {
 			/* walk back to the last pixel whose final rejected[] is self-determined */
 			int64_t q = chain_pred(p, t, pix);
-			while (q >= 0 && p.flag_map[q] == SG_CLS_CHAIN)
+			bool fault = false;
+			while (q >= 0) {
+				if (chain_in_band(p, q)) {
+					if (p.flag_map[q] != SG_CLS_CHAIN)
+						break;
+				} else {
+					if (!chain_resident(p, q)) {
+						fault = true;
+						break;
+					}
+					uint32_t dummy[2] = {0, 0};
+					for (int k = 0; k < p.N; k++)
+						rejected[k] = 0;
+					gather_stack(p, q, stack);
+					literal_pixel(stack, rejected, wst, p.N, p.rejection, p.sig0, p.sig1, dummy, &fbrk);
+					if (!(fbrk && p.N > 4))
+						break;
+				}
 				q = chain_pred(p, t, q);
+			}
+			if (fault) {
+				*p.walk_fault = 1u;
+				continue;
+			}
+			for (int k = 0; k < p.N; k++)
+				rejected[k] = 0;
 			int64_t cur;
 			if (q >= 0) {
 				uint32_t dummy[2] = {0, 0};

@@ -40,7 +40,8 @@ class StackDesc(ctypes.Structure):
         ("max_thread", ctypes.c_int),
         ("max_number_of_rows", ctypes.c_int),
         ("kernel_path", ctypes.c_int),
-        ("reserved", ctypes.c_int * 5),
+        ("resident_rows", ctypes.c_int * 2),
+        ("reserved", ctypes.c_int * 3),
     ]
 
 
@@ -339,8 +340,9 @@ def _dptr(a):
 
 def make_desc(method, N, W, H, C, rejection=NO_REJEC, normalize=NO_NORM, sig=(4.0, 3.0),
               shiftx=None, shifty=None, offset=None, mul=None, scale=None, max_thread=8,
-              max_number_of_rows=0, kernel_path=PATH_AUTO):
-    """Build a StackDesc; returns (desc, keepalive) -- keep the arrays alive during the call."""
+              max_number_of_rows=0, kernel_path=PATH_AUTO, resident_rows=None):
+    """Build a StackDesc; returns (desc, keepalive) -- keep the arrays alive during the call.
+    resident_rows = (first, end) memory rows present at the device frames (None = all)."""
     keep = []
 
     def arr(a, dt):
@@ -360,6 +362,8 @@ def make_desc(method, N, W, H, C, rejection=NO_REJEC, normalize=NO_NORM, sig=(4.
     d.offset, d.mul, d.scale = _dptr(of), _dptr(mu), _dptr(sc)
     d.max_thread, d.max_number_of_rows = max_thread, max_number_of_rows
     d.kernel_path = kernel_path
+    if resident_rows is not None:
+        d.resident_rows[0], d.resident_rows[1] = int(resident_rows[0]), int(resident_rows[1])
     return d, keep
 
 

@@ -17,7 +17,7 @@ import sirilgpu_dist as sd  # noqa: E402
 def main():
     rank, world, port = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
     d = np.load(sys.argv[4], allow_pickle=False)
-    frames, sx, sy = d["frames"], d["sx"], d["sy"]
+    frames, sx, sy, sig = d["frames"], d["sx"], d["sy"], tuple(float(v) for v in d["sig"])
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -25,7 +25,7 @@ def main():
         H = frames.shape[2]
 
         def stack_band(b, e):
-            out, rej = onp.stack_rejection_1thread(frames, 2, (3.0, 3.0), sx, sy, rows=(b, e))
+            out, rej = onp.stack_rejection_1thread(frames, 2, sig, sx, sy, rows=(b, e))
             return out[:, b:e], rej
 
         img, rej = sd.stack_sharded(stack_band, H, dist, rank, world)

@@ -201,16 +201,21 @@ def reject_pixel(stack, rejected, rejection, sig, crej):
 def stack_rejection_1thread(frames, rejection, sig, shiftx=None, shifty=None, rows=None):
     """stack_mean_with_rejection with one OpenMP thread and one block per channel-quarter
     order (blocks top-down, channel-major); frames [N][C][H][W] memory order (bottom-up).
-    rows = (begin, end): only memory rows [begin, end) (a row band), others stay 0."""
+    rows = (begin, end): only memory rows [begin, end) (a row band) are written and counted,
+    others stay 0.  Every pixel the thread visits before the band is still stacked, so the
+    stale rejected[] a band pixel inherits (SURVEY a3 iii) is the full run's."""
     N, C, H, W = frames.shape
     out = np.zeros((C, H, W), dtype=np.uint16)
     rej = np.zeros((3, 2), dtype=np.uint64)
     rejected = [0] * N
+    last = None                         # (c, t) of the band's last pixel row in thread order
+    if rows is not None:
+        last = (C - 1, H - rows[0])
     for c in range(C):
         for t in range(H):              # top-down rows, as the block loop visits them
             R = H - 1 - t
-            if rows is not None and not (rows[0] <= R < rows[1]):
-                continue
+            if last is not None and (c, t) >= last:
+                break
             crej = [0, 0]
             for x in range(W):
                 col = []
@@ -223,6 +228,9 @@ def stack_rejection_1thread(frames, rejection, sig, shiftx=None, shifty=None, ro
                     sr = R - sy
                     col.append(int(frames[f, c, sr, x - sx]) if 0 <= sr < H else 0)
                 out[c, R, x] = reject_pixel(col, rejected, rejection, sig, crej)
+            if rows is not None and not (rows[0] <= R < rows[1]):
+                out[c, R] = 0           # before the band: stacked for its state only
+                continue
             rej[c, 0] += crej[0]
             rej[c, 1] += crej[1]
     return out, rej

@@ -23,14 +23,63 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_row_band_sharding_gloo(world, tmp_path):
-    N, C, H, W = 10, 1, 13, 9
-    frames = orc.synth(N, C, H, W, seed=17, maxshift=2)
-    sx, sy = orc.synth_shifts(N, seed=17, maxshift=2)
-    full, full_rej = onp.stack_rejection_1thread(frames, 2, (3.0, 3.0), sx, sy)
+def _band_fresh_state(frames, rejection, sig, sx, sy, b, e):
+    """rows [b, e) stacked as if the band started a new thread (zero rejected[]): what a
+    band that ignores the inherited stale state would produce"""
+    N, C, H, W = frames.shape
+    out = np.zeros((C, H, W), dtype=np.uint16)
+    rejected = [0] * N
+    for c in range(C):
+        for t in range(H - e, H - b):
+            R = H - 1 - t
+            for x in range(W):
+                col = []
+                for f in range(N):
+                    if sx[f] and not (0 <= x - sx[f] < W):
+                        col.append(0)
+                        continue
+                    sr = R - sy[f]
+                    col.append(int(frames[f, c, sr, x - sx[f]]) if 0 <= sr < H else 0)
+                out[c, R, x] = onp.reject_pixel(col, rejected, rejection, sig, [0, 0])
+    return out
+
+
+@pytest.mark.parametrize("world,case", [(2, "synth"), (3, "synth"), (2, "early"), (3, "early")])
+def test_row_band_sharding_gloo(world, case, tmp_path):
+    if case == "synth":
+        N, C, H, W, sig = 10, 1, 13, 9, (3.0, 3.0)
+        frames = orc.synth(N, C, H, W, seed=17, maxshift=2)
+        sx, sy = orc.synth_shifts(N, seed=17, maxshift=2)
+    else:
+        # small N, strong rejection: the first pixel of each band (thread order: top row,
+        # x = 0) breaks early in its first pass (N - r <= 4 after two low rejections) and so
+        # removes by its predecessor's stale rejected[5] = 1, left by the previous band's
+        # last pixel (a high outlier rejected in its first pass, none in its second)
+        N, C, H, W, sig = 6, 1, 12, 7, (1.0, 1.0)
+        rng = np.random.default_rng(5)
+        frames = rng.integers(900, 1100, size=(N, C, H, W)).astype(np.uint16)
+        m = rng.random(frames.shape)
+        frames[m < 0.1] = 65535
+        frames[m > 0.9] = 0
+        for r in range(world - 1):
+            b, e = sd.row_band(r, world, H)
+            frames[:, 0, e - 1, 0] = [0, 0, 1000, 1010, 1020, 1100]
+            frames[:, 0, e, W - 1] = [1000, 1000, 1000, 1000, 1000, 65535]
+        sx = np.zeros(N, np.int32)
+        sy = np.zeros(N, np.int32)
+    full, full_rej = onp.stack_rejection_1thread(frames, 2, sig, sx, sy)
+    rc, c_full, c_rej = orc.stack_rejection(frames, 2, sig=sig, shiftx=sx, shifty=sy, max_thread=1)
+    assert rc == 0 and np.array_equal(c_full, full) and np.array_equal(c_rej, full_rej)
+    if case == "early":
+        # the data must make the inherited state matter at some band edge
+        stale = False
+        for r in range(world - 1):
+            b, e = sd.row_band(r, world, H)
+            fresh = _band_fresh_state(frames, 2, sig, sx, sy, b, e)
+            stale |= not np.array_equal(fresh[:, b:e], full[:, b:e])
+        assert stale
     inp = tmp_path / "in.npz"
-    np.savez(inp, frames=frames, sx=sx, sy=sy)
+    np.savez(inp, frames=frames, sx=sx, sy=sy, sig=np.array(sig))
     port = _free_port()
     worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_worker.py")
     procs = [subprocess.Popen([sys.executable, worker, str(r), str(world), str(port), str(inp),
