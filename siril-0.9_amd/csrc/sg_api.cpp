@@ -50,6 +50,7 @@ extern "C" int sg_init(sg_ctx **out, int ndev, const int *devs) {
 		return SG_ERR_DEVICE;
 	sg_ctx *ctx = new sg_ctx();
 	memset(&ctx->stats, 0, sizeof ctx->stats);
+	ctx->knobs.read();
 	if (ndev <= 0)
 		ndev = 1;
 	for (int i = 0; i < ndev; i++) {
@@ -286,12 +287,8 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			return set_err(ctx, SG_ERR_SIZE, "%s%.0ld", m, 0);
 		}
 	}
-	{
-		const char *dbg = getenv("SG_HIST_DBG");
-		p.dbg = dbg ? atoi(dbg) : 0;
-		const char *pr = getenv("SG_HIST_PRIO");
-		p.prio = pr ? atoi(pr) : 1;	/* 1 measured best: 4.73 -> 4.58 ms (scripts/gpu_prio.sh) */
-	}
+	p.dbg = ctx->knobs.hist_dbg;
+	p.prio = ctx->knobs.hist_prio;	/* 1 measured best: 4.73 -> 4.58 ms (scripts/gpu_prio.sh) */
 
 	/* per-frame constants: shifts + normalisation coefficients */
 	const int Npad = (N + 15) & ~15;	/* histogram-path table: 64-byte aligned, padded */
@@ -428,20 +425,19 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			HIPCHK(hipMemsetAsync(redo_count, 0, sizeof(unsigned int), s));
 			HIPCHK(hipEventRecord(dv.ev[0], s));
 			const size_t nblk_h = (size_t)((W + 127) / 128) * nrows * C;	/* 128-pixel tiles */
-			const char *pad = getenv("SG_HIST_LDSPAD");	/* A/B: extra LDS per workgroup (occupancy) */
 			if (p.dbg == 14) {	/* A/B: report the resident workgroups per CU */
 				int per_cu = -1;
 				(void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_stack_hist<2, 0>, 256,
-						pad ? (size_t)atoi(pad) : 0);
+						(size_t)ctx->knobs.hist_ldspad);
 				hipDeviceProp_t prop;
 				(void)hipGetDeviceProperties(&prop, dv.id);
-				fprintf(stderr, "k_stack_hist: %d workgroups/CU (lds/CU %zu, lds/block max %zu, pad %s)\n", per_cu,
-						(size_t)prop.maxSharedMemoryPerMultiProcessor, (size_t)prop.sharedMemPerBlock, pad ? pad : "0");
+				fprintf(stderr, "k_stack_hist: %d workgroups/CU (lds/CU %zu, lds/block max %zu, pad %d)\n", per_cu,
+						(size_t)prop.maxSharedMemoryPerMultiProcessor, (size_t)prop.sharedMemPerBlock, ctx->knobs.hist_ldspad);
 			}
 			/* NORM: 0 none, 1 additive (round(v scale - offset)), 2 multiplicative (round(v scale mul)) */
 			const int norm = p.normalize == SG_NO_NORM ? 0 :
 				(p.normalize == SG_ADDITIVE || p.normalize == SG_ADDITIVE_SCALING) ? 1 : 2;
-			const size_t lds_pad = pad ? (size_t)atoi(pad) : 0;
+			const size_t lds_pad = (size_t)ctx->knobs.hist_ldspad;
 			const dim3 hg((unsigned)nblk_h), hb(256);
 			switch ((p.rejection == SG_WINSORIZED ? 10 : 0) + norm) {
 			case 0: hipLaunchKernelGGL((k_stack_hist<2, 0>), hg, hb, lds_pad, s, p, redo_count, redo_list); break;
@@ -462,9 +458,7 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			 * of rows near the frame border) goes through the sorted kernel, 64 pixels per
 			 * workgroup, once the count is back (measured: 22 k pixels faster in the replay,
 			 * 113 k slower) */
-			bool dev_route = N <= SG_REPLAY_MAXN;
-			if (const char *e = getenv("SG_REDO_REPLAY"))	/* A/B knob: 0 = always the sorted kernel */
-				dev_route = dev_route && atoi(e) != 0;
+			const bool dev_route = N <= SG_REPLAY_MAXN && ctx->knobs.redo_replay;
 			if (dev_route) {
 				hipLaunchKernelGGL(k_redo_to_literal, dim3(64), dim3(256), 0, s, p, (const unsigned int *)redo_list,
 						(const unsigned int *)redo_count, (unsigned int)SG_REDO_REPLAY_MAX);
@@ -531,9 +525,7 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		}
 		dim3 grid((W + 255) / 256, nrows, C);
 		/* pixel pairs per lane (dword loads) unless a plane is too large for a 31-bit offset */
-		bool pairs = W >= 2 && (uint64_t)W * (uint64_t)H * 2u < (1ull << 31);
-		if (const char *e = getenv("SG_REDUCE1"))	/* A/B knob: 1 = one pixel per lane */
-			pairs = pairs && atoi(e) == 0;
+		const bool pairs = W >= 2 && (uint64_t)W * (uint64_t)H * 2u < (1ull << 31) && !ctx->knobs.reduce1;
 		const dim3 grid2(((W + 1) / 2 + 255) / 256, nrows, C);
 		HIPCHK(hipEventRecord(dv.ev[0], s));
 		if (pairs)
@@ -601,9 +593,9 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 
 /* HBM the host-pull path may fill with frames: SG_HOST_BUDGET_BYTES (tests), else 85 % of
  * the free device memory (plus what the context already holds for frames) */
-static size_t host_budget(SgDevice &dv) {
-	if (const char *e = getenv("SG_HOST_BUDGET_BYTES"))
-		return (size_t)atoll(e);
+static size_t host_budget(const sg_ctx *ctx, SgDevice &dv) {
+	if (ctx->knobs.host_budget > 0)
+		return (size_t)ctx->knobs.host_budget;
 	size_t fr = 0, tot = 0;
 	if (hipMemGetInfo(&fr, &tot) != hipSuccess)
 		return 0;
@@ -639,7 +631,7 @@ extern "C" int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *d, sg_read_region_
 	const int64_t halo = std::min<int64_t>((int64_t)sy_max - sy_min, H);
 	const size_t row_bytes = (size_t)N * C * W * sizeof(uint16_t);	/* one row of every frame */
 	int band = H;
-	const size_t budget = host_budget(dv);
+	const size_t budget = host_budget(ctx, dv);
 	if ((size_t)H * row_bytes > budget) {
 		const int64_t fit = (int64_t)(budget / row_bytes) - halo;
 		if (fit < 1)

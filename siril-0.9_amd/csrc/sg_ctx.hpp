@@ -5,6 +5,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string>
 #include <vector>
 #include "../../include/sirilgpu.h"
@@ -37,10 +38,55 @@ struct SgDevice {
 	int io_ev_used[2] = {0, 0};
 };
 
+/* A/B and test knobs from the environment, read once when the context is created
+ * (sg_init): the product path never consults the environment per call.  An unset or
+ * invalid value gives the measured default. */
+static inline int sg_env_int(const char *name, int lo, int hi, int def) {
+	const char *e = getenv(name);
+	if (!e || !*e)
+		return def;
+	char *end = nullptr;
+	const long v = strtol(e, &end, 10);
+	return (*end == 0 && v >= lo && v <= hi) ? (int)v : def;
+}
+
+struct SgKnobs {
+	int hist_dbg = 0;		/* SG_HIST_DBG: k_stack_hist phase / timing A/B (0 = production) */
+	int hist_prio = 1;		/* SG_HIST_PRIO: build-phase wave priority (1 measured best, scripts/gpu_prio.sh) */
+	int hist_ldspad = 0;		/* SG_HIST_LDSPAD: extra LDS bytes per histogram workgroup (occupancy A/B) */
+	int redo_replay = 1;		/* SG_REDO_REPLAY: 0 = redo list always through the sorted kernel */
+	int reduce1 = 0;		/* SG_REDUCE1: 1 = one pixel per lane in the SUM/MAX/MIN/MEAN reduce */
+	long long host_budget = 0;	/* SG_HOST_BUDGET_BYTES: host-pull HBM budget (0 = 85 % of free HBM) */
+	int qsub_threads = 64;		/* SG_QSUB_THREADS: 64 measured best (scripts/gpu_qsub.sh) */
+	int qgrad_threads = 128;	/* SG_QGRAD_THREADS: 128 measured best (scripts/gpu_qgrad.sh) */
+	int reg_batch = 0;		/* SG_REG_BATCH: pairs per launch (0 = up to 2 GB of pair planes) */
+	int reg_cw = 0;			/* SG_REG_CW: columns per column-pass workgroup (0 = 8192 / S) */
+	int reg_path = 2;		/* SG_REG_PATH: registration pass order 0 / 1 / 2 */
+	int reg_xcd = 1;		/* SG_REG_XCD: 0 = column strips in dispatch order */
+	void read() {
+		hist_dbg = sg_env_int("SG_HIST_DBG", 0, 1000, 0);
+		hist_prio = sg_env_int("SG_HIST_PRIO", 0, 3, 1);
+		hist_ldspad = sg_env_int("SG_HIST_LDSPAD", 0, 160 * 1024, 0);
+		redo_replay = sg_env_int("SG_REDO_REPLAY", 0, 1, 1);
+		reduce1 = sg_env_int("SG_REDUCE1", 0, 1, 0);
+		if (const char *e = getenv("SG_HOST_BUDGET_BYTES"))
+			host_budget = atoll(e) > 0 ? atoll(e) : 0;
+		const int qs = sg_env_int("SG_QSUB_THREADS", 64, 1024, 64);
+		qsub_threads = qs % 64 == 0 ? qs : 64;
+		const int qg = sg_env_int("SG_QGRAD_THREADS", 64, 256, 128);
+		qgrad_threads = (qg == 64 || qg == 128 || qg == 256) ? qg : 128;
+		reg_batch = sg_env_int("SG_REG_BATCH", 1, 1024, 0);
+		reg_cw = sg_env_int("SG_REG_CW", 1, 64, 0);
+		reg_path = sg_env_int("SG_REG_PATH", 0, 2, 2);
+		reg_xcd = sg_env_int("SG_REG_XCD", 0, 1, 1);
+	}
+};
+
 struct sg_ctx {
 	std::vector<SgDevice> dev;
 	std::string err;
 	sg_stack_stats stats;
+	SgKnobs knobs;
 };
 
 static inline int set_err(sg_ctx *ctx, int code, const char *fmt, const char *a = "", long b = 0) {

@@ -27,6 +27,8 @@
 #include <string.h>
 #include <unistd.h>
 #include <stdlib.h>
+#include <new>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -68,7 +70,23 @@ static inline uint32_t le32(const unsigned char *p) {
 	return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
-extern "C" int sg_seq_open_ser(const char *path, sg_seq **out) {
+/* frame geometry from a file header: sides in [1, 2^20], and the raw frame size and the
+ * data of `frames` frames after `data_off` computed without overflow and present in a file
+ * of `file_size` bytes (a crafted header must not wrap the size check) */
+#define SG_MAX_SIDE (1 << 20)
+static bool sg_geom_ok(int64_t width, int64_t height, int layers, int bps, int64_t frames, int64_t data_off,
+		int64_t file_size, int64_t *frame_bytes) {
+	if (width < 1 || height < 1 || width > SG_MAX_SIDE || height > SG_MAX_SIDE || frames < 1 || data_off < 0)
+		return false;
+	int64_t fb, all, end;
+	if (__builtin_mul_overflow(width * height, (int64_t)layers * bps, &fb) ||
+			__builtin_mul_overflow(fb, frames, &all) || __builtin_add_overflow(all, data_off, &end))
+		return false;
+	*frame_bytes = fb;
+	return end <= file_size;
+}
+
+static int sg_seq_open_ser_impl(const char *path, sg_seq **out) {
 	if (!path || !out)
 		return SG_ERR_GENERIC;
 	*out = nullptr;
@@ -80,7 +98,11 @@ extern "C" int sg_seq_open_ser(const char *path, sg_seq **out) {
 		close(fd);
 		return SG_ERR_READ;
 	}
-	sg_seq *s = new sg_seq();
+	sg_seq *s = new (std::nothrow) sg_seq();
+	if (!s) {
+		close(fd);
+		return SG_ERR_SIZE;
+	}
 	s->kind = SG_SRC_SER;
 	s->debayer = -1;
 	/* the 7 little-endian ints at byte 14 (ser.c:312) */
@@ -95,21 +117,26 @@ extern "C" int sg_seq_open_ser(const char *path, sg_seq **out) {
 	s->bgr = s->color_id == 101;
 	s->layers = s->interleaved ? 3 : 1;	/* ser.c:332-335; CFA opened as mono */
 	s->enc = s->bytes_per_sample == 1 ? SG_ENC_U8 : (big ? SG_ENC_U16BE : SG_ENC_U16LE);
-	s->frame_bytes = (int64_t)s->width * s->height * s->layers * s->bytes_per_sample;
 	s->fd.push_back(fd);
 	s->data_off.push_back(178);
-	if (s->width <= 0 || s->height <= 0 || s->frames <= 0) {
+	/* frame_count == 0 repair of ser.c:341-347 is not done (the file is read-only here) */
+	const off_t size = lseek(fd, 0, SEEK_END);
+	if (!sg_geom_ok(s->width, s->height, s->layers, s->bytes_per_sample, s->frames, 178, (int64_t)size,
+				&s->frame_bytes)) {
 		sg_seq_close(s);
 		return SG_ERR_SIZE;
 	}
-	/* frame_count == 0 repair of ser.c:341-347 is not done (the file is read-only here) */
-	const off_t size = lseek(fd, 0, SEEK_END);
-	if (size < 178 + s->frame_bytes * (int64_t)s->frames) {
-		sg_seq_close(s);
-		return SG_ERR_READ;
-	}
 	*out = s;
 	return SG_OK;
+}
+
+/* C ABI entry points: no C++ exception (e.g. bad_alloc of a host buffer) crosses them */
+extern "C" int sg_seq_open_ser(const char *path, sg_seq **out) {
+	try {
+		return sg_seq_open_ser_impl(path, out);
+	} catch (const std::exception &) {
+		return SG_ERR_SIZE;
+	}
 }
 
 /* FITS primary header: 80-byte cards in 2880-byte blocks */
@@ -156,11 +183,13 @@ static int fits_header(int fd, int *bitpix, int *naxis, long naxes[3], double *b
 	}
 }
 
-extern "C" int sg_seq_open_fits(const char *const *paths, int nframes, sg_seq **out) {
+static int sg_seq_open_fits_impl(const char *const *paths, int nframes, sg_seq **out) {
 	if (!paths || nframes <= 0 || !out)
 		return SG_ERR_GENERIC;
 	*out = nullptr;
-	sg_seq *s = new sg_seq();
+	sg_seq *s = new (std::nothrow) sg_seq();
+	if (!s)
+		return SG_ERR_SIZE;
 	s->kind = SG_SRC_FITS;
 	s->debayer = -1;
 	for (int i = 0; i < nframes; i++) {
@@ -185,6 +214,13 @@ extern "C" int sg_seq_open_fits(const char *const *paths, int nframes, sg_seq **
 			return SG_ERR_GENERIC;	/* unsupported image type for this path */
 		}
 		const int layers = naxis == 3 ? (int)naxes[2] : 1;
+		/* NAXIS1 / NAXIS2 in range and the whole data unit present in the file */
+		int64_t fbytes;
+		if (!sg_geom_ok(naxes[0], naxes[1], layers, bitpix == 8 ? 1 : 2, 1, doff, (int64_t)lseek(fd, 0, SEEK_END),
+					&fbytes)) {
+			sg_seq_close(s);
+			return SG_ERR_SIZE;
+		}
 		if (i == 0) {
 			s->width = (int)naxes[0];
 			s->height = (int)naxes[1];
@@ -204,6 +240,14 @@ extern "C" int sg_seq_open_fits(const char *const *paths, int nframes, sg_seq **
 	s->frame_bytes = (int64_t)s->width * s->height * s->layers * s->bytes_per_sample;
 	*out = s;
 	return SG_OK;
+}
+
+extern "C" int sg_seq_open_fits(const char *const *paths, int nframes, sg_seq **out) {
+	try {
+		return sg_seq_open_fits_impl(paths, nframes, out);
+	} catch (const std::exception &) {
+		return SG_ERR_SIZE;
+	}
 }
 
 extern "C" void sg_seq_close(sg_seq *s) {
@@ -262,7 +306,7 @@ extern "C" int sg_seq_set_debayer(sg_seq *s, int pattern) {
 	return SG_OK;
 }
 
-extern "C" int sg_seq_read_region(void *user, int layer, int index, uint16_t *buffer, const sg_rect *area) {
+static int sg_seq_read_region_impl(void *user, int layer, int index, uint16_t *buffer, const sg_rect *area) {
 	const sg_seq *s = (const sg_seq *)user;
 	if (!s || !buffer || !area || index < 0 || index >= s->frames || layer < 0 || layer >= s->layers)
 		return -1;
@@ -304,7 +348,15 @@ extern "C" int sg_seq_read_region(void *user, int layer, int index, uint16_t *bu
 	return bad ? -1 : 0;
 }
 
-extern "C" int sg_seq_read_frame(const sg_seq *s, int index, uint16_t *out) {
+extern "C" int sg_seq_read_region(void *user, int layer, int index, uint16_t *buffer, const sg_rect *area) {
+	try {
+		return sg_seq_read_region_impl(user, layer, index, buffer, area);
+	} catch (const std::exception &) {
+		return SG_ERR_SIZE;
+	}
+}
+
+static int sg_seq_read_frame_impl(const sg_seq *s, int index, uint16_t *out) {
 	if (!s || !out || index < 0 || index >= s->frames || s->debayer >= 0)
 		return SG_ERR_GENERIC;
 	const int fd = s->kind == SG_SRC_SER ? s->fd[0] : s->fd[index];
@@ -329,6 +381,14 @@ extern "C" int sg_seq_read_frame(const sg_seq *s, int index, uint16_t *out) {
 				out[((size_t)c * H + r) * W + x] = conv_host(&raw[src], s->enc, &bad);
 			}
 	return bad ? SG_ERR_GENERIC : SG_OK;
+}
+
+extern "C" int sg_seq_read_frame(const sg_seq *s, int index, uint16_t *out) {
+	try {
+		return sg_seq_read_frame_impl(s, index, out);
+	} catch (const std::exception &) {
+		return SG_ERR_SIZE;
+	}
 }
 
 /* ------------------------------------------------------------------------------------

@@ -802,7 +802,7 @@ k_quality_grad(const uint16_t *__restrict__ qbuf, int xs, int ys, const unsigned
 	__shared__ unsigned long long sv[4], sp[4], sc[4];
 	/* a 64 x SG_QGT tile of outputs: stretched samples of the 68 x (SG_QGT + 4)
 	 * neighbourhood, then the smoothed values of the 66 x (SG_QGT + 2) one, each formed once
-	 * in LDS; each wave takes SG_QGT / 4 output rows */
+	 * in LDS; the blockDim.x / 64 waves take the output rows in turn */
 	__shared__ unsigned int st[SG_QGT + 4][68];
 	__shared__ int sms[SG_QGT + 2][66];
 	const int q = blockIdx.z;
@@ -909,17 +909,13 @@ static int reg_quality(sg_ctx *ctx, SgDevice &dv, hipStream_t s, const uint16_t 
 	HIPCHK(hipMemsetAsync(dv.reg_qacc.p, 0, (size_t)nq * (3 * sizeof(unsigned long long) + sizeof(unsigned int)), s));
 	/* one wave per workgroup, walking the row pairs: 283 us per 129 frames of 2048^2 against
 	 * 332 / 348 / 403 / 618 us with 128 / 192 / 256 / 384 threads (scripts/gpu_qsub.sh) */
-	int qthr = 64;
-	if (const char *e = getenv("SG_QSUB_THREADS"))	/* A/B knob: threads per subsample workgroup (64-multiple) */
-		qthr = atoi(e) >= 64 && atoi(e) <= 1024 ? atoi(e) / 64 * 64 : 256;
+	const int qthr = ctx->knobs.qsub_threads;	/* A/B knob SG_QSUB_THREADS */
 	hipLaunchKernelGGL(k_quality_sub, dim3((ys + SG_QROWS - 1) / SG_QROWS, nq), dim3(qthr), 0, s, d_sel, d_frames, S,
 			xs, ys, qbuf, qmax);
 	HIPCHK(hipGetLastError());
 	/* 2 waves per 64x16 tile: 214 us per 129 frames against 238 (4 waves) and 333 (1 wave),
 	 * scripts/gpu_qgrad.sh */
-	int gthr = 128;
-	if (const char *e = getenv("SG_QGRAD_THREADS"))	/* A/B knob: 64, 128 or 256 threads per gradient tile */
-		gthr = (atoi(e) == 64 || atoi(e) == 256) ? atoi(e) : 128;
+	const int gthr = ctx->knobs.qgrad_threads;	/* A/B knob SG_QGRAD_THREADS */
 	hipLaunchKernelGGL(k_quality_grad, dim3((xs + 63) / 64, (ys + SG_QGT - 1) / SG_QGT, nq), dim3(gthr), 0, s, qbuf, xs, ys,
 			qmax, acc);
 	HIPCHK(hipGetLastError());
@@ -1029,8 +1025,8 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		B = 1;
 	if (B > 64)
 		B = 64;
-	if (const char *e = getenv("SG_REG_BATCH"))	/* A/B knob: pairs per launch */
-		B = atoi(e) > 0 ? atoi(e) : B;
+	if (ctx->knobs.reg_batch > 0)	/* A/B knob SG_REG_BATCH: pairs per launch */
+		B = ctx->knobs.reg_batch;
 	const int npairs_total = (int)(todo.size() + 1) / 2;
 	if (B > npairs_total && npairs_total > 0)
 		B = npairs_total;
@@ -1040,8 +1036,8 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		CW = 1;
 	if (CW > 8)
 		CW = 8;
-	if (const char *e = getenv("SG_REG_CW"))	/* A/B knob: columns per column-pass workgroup */
-		CW = atoi(e) > 0 ? atoi(e) : CW;
+	if (ctx->knobs.reg_cw > 0)	/* A/B knob SG_REG_CW: columns per column-pass workgroup */
+		CW = ctx->knobs.reg_cw;
 	const size_t col_lds = (size_t)CW * (SG_PADN(S) + 1) * sizeof(sg_c64);
 	(void)hipFuncSetAttribute((const void *)k_reg_rows_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)row_lds);
 	(void)hipFuncSetAttribute((const void *)k_reg_rows_inv_argmax, hipFuncAttributeMaxDynamicSharedMemorySize, (int)row_lds);
@@ -1056,11 +1052,7 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	const int row_thr = thr_for(S), col_thr = thr_for(CW * S), xri_thr = thr_for(2 * S);
 	/* pass order: 2 = half spectra (3 plane passes), 1 = full spectra with the cross-power
 	 * fused into the inverse row pass (4), 0 = unfused (5) */
-	int path = 2;
-	if (const char *e = getenv("SG_REG_FUSED"))	/* A/B knob (older name): 0 = unfused */
-		path = atoi(e) != 0 ? 1 : 0;
-	if (const char *e = getenv("SG_REG_PATH"))	/* A/B knob: pass order */
-		path = atoi(e);
+	const int path = ctx->knobs.reg_path;	/* A/B knob SG_REG_PATH */
 	const bool fused = path == 1;
 	const bool half = path == 2;
 	/* half-spectrum columns: a strip stays inside one half (CW divides S/2) */
@@ -1073,9 +1065,7 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 			(int)row_lds);
 	(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower, hipFuncAttributeMaxDynamicSharedMemorySize,
 			(int)colh_lds);
-	int xcdmap = 1;
-	if (const char *e = getenv("SG_REG_XCD"))	/* A/B knob: 0 = strips in dispatch order */
-		xcdmap = atoi(e) != 0;
+	const int xcdmap = ctx->knobs.reg_xcd;	/* A/B knob SG_REG_XCD: 0 = strips in dispatch order */
 
 	HIPCHK(ensure(dv.reg_spec, plane * sizeof(sg_c64)));
 	HIPCHK(ensure(dv.reg_work, (size_t)(B > 1 ? B : 1) * plane * sizeof(sg_c64)));

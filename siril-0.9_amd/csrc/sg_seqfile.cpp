@@ -15,6 +15,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <new>
+#include <stdexcept>
 #include <string>
 #include <vector>
 #include "../../include/sirilgpu.h"
@@ -40,6 +42,29 @@ extern "C" void sg_seqfile_free(sg_seqfile *sf) {
 	delete sf;
 }
 
+/* per-image arrays of `number` images; false when they cannot be allocated (a malformed
+ * count must come back as an error code, not as an exception across the C ABI) */
+static bool sf_alloc(sg_seqfile *sf, int number) {
+	try {
+		sf->filenum.assign(number, 0);
+		sf->incl.assign(number, 0);
+		sf->has_stats.assign(number, 0);
+		sf->stats.assign((size_t)number * 10, 0.0);
+	} catch (const std::exception &) {
+		return false;
+	}
+	return true;
+}
+
+static bool reg_alloc(std::vector<SgRegRow> &rl, int number) {
+	try {
+		rl.assign(number, SgRegRow{0, 0, 0.f, 0.f, 0.f, 0.f, 0.0});
+	} catch (const std::exception &) {
+		return false;
+	}
+	return true;
+}
+
 extern "C" int sg_seqfile_read(const char *path, sg_seqfile **out) {
 	if (!path || !out)
 		return SG_ERR_GENERIC;
@@ -50,7 +75,11 @@ extern "C" int sg_seqfile_read(const char *path, sg_seqfile **out) {
 	FILE *f = fopen(fn.c_str(), "r");
 	if (!f)
 		return SG_ERR_READ;
-	sg_seqfile *sf = new sg_seqfile();
+	sg_seqfile *sf = new (std::nothrow) sg_seqfile();
+	if (!sf) {
+		fclose(f);
+		return SG_ERR_SIZE;
+	}
 	char line[512], filename[512];
 	bool allocated = false;
 	int i = 0, current_layer = -1;
@@ -62,15 +91,15 @@ extern "C" int sg_seqfile_read(const char *path, sg_seqfile **out) {
 		case 'S': {
 			const char *fmt = line[2] == '\'' ? "'%511[^']' %d %d %d %d %d" : "%511s %d %d %d %d %d";
 			if (sscanf(line + 2, fmt, filename, &sf->beg, &sf->number, &sf->selnum, &sf->fixed,
-						&sf->reference_image) != 6 || allocated || sf->number == 0) {
+						&sf->reference_image) != 6 || allocated || sf->number < 1) {
 				rc = SG_ERR_READ;
 				goto done;
 			}
 			sf->name = filename;
-			sf->filenum.assign(sf->number, 0);
-			sf->incl.assign(sf->number, 0);
-			sf->has_stats.assign(sf->number, 0);
-			sf->stats.assign((size_t)sf->number * 10, 0.0);
+			if (!sf_alloc(sf, sf->number)) {
+				rc = SG_ERR_SIZE;
+				goto done;
+			}
 			allocated = true;
 			break;
 		}
@@ -108,7 +137,10 @@ extern "C" int sg_seqfile_read(const char *path, sg_seqfile **out) {
 			}
 			std::vector<SgRegRow> &rl = sf->reg[current_layer];
 			if (rl.empty()) {
-				rl.assign(sf->number, SgRegRow{0, 0, 0.f, 0.f, 0.f, 0.f, 0.0});
+				if (!reg_alloc(rl, sf->number)) {
+					rc = SG_ERR_SIZE;
+					goto done;
+				}
 				i = 0;	/* the reference reuses the image counter (:147-150) */
 			}
 			if (i < sf->number) {
@@ -153,7 +185,9 @@ extern "C" int sg_seqfile_create(const char *name, int beg, int number, int fixe
 		int nb_layers, sg_seqfile **out) {
 	if (!name || !out || number < 1 || nb_layers < 1 || nb_layers > 10)
 		return SG_ERR_GENERIC;
-	sg_seqfile *sf = new sg_seqfile();
+	sg_seqfile *sf = new (std::nothrow) sg_seqfile();
+	if (!sf)
+		return SG_ERR_SIZE;
 	sf->name = name;
 	sf->beg = beg;
 	sf->number = number;
@@ -161,13 +195,14 @@ extern "C" int sg_seqfile_create(const char *name, int beg, int number, int fixe
 	sf->reference_image = reference_image;
 	sf->type = type;
 	sf->nb_layers = nb_layers;
-	sf->filenum.resize(number);
+	if (!sf_alloc(sf, number)) {
+		delete sf;
+		return SG_ERR_SIZE;
+	}
 	for (int k = 0; k < number; k++)
 		sf->filenum[k] = beg + k;
 	sf->incl.assign(number, 1);
 	sf->selnum = number;
-	sf->has_stats.assign(number, 0);
-	sf->stats.assign((size_t)number * 10, 0.0);
 	sf->reg.assign(nb_layers, std::vector<SgRegRow>());
 	*out = sf;
 	return SG_OK;
@@ -250,7 +285,8 @@ extern "C" int sg_seqfile_set_registration(sg_seqfile *sf, int layer, const int 
 	if (!sf || layer < 0 || layer >= (int)sf->reg.size() || !shiftx || !shifty)
 		return SG_ERR_GENERIC;
 	std::vector<SgRegRow> &rl = sf->reg[layer];
-	rl.assign(sf->number, SgRegRow{0, 0, 0.f, 0.f, 0.f, 0.f, 0.0});
+	if (!reg_alloc(rl, sf->number))
+		return SG_ERR_SIZE;
 	for (int k = 0; k < sf->number; k++) {
 		rl[k].shiftx = shiftx[k];
 		rl[k].shifty = shifty[k];

@@ -155,10 +155,12 @@ def test_band_rows_not_resident_rejected(gpu_ctx):
 
 
 def _with_budget(nbytes, fn):
+    """fn(ctx) on a context created under the budget knob (knobs are read at sg_init)"""
     old = os.environ.get("SG_HOST_BUDGET_BYTES")
     os.environ["SG_HOST_BUDGET_BYTES"] = str(nbytes)
     try:
-        return fn()
+        with sg.Context() as ctx:
+            return fn(ctx)
     finally:
         if old is None:
             del os.environ["SG_HOST_BUDGET_BYTES"]
@@ -185,8 +187,8 @@ def test_host_pull_streams_row_bands(gpu_ctx, method, rejection, band_rows):
     budget = N * C * W * 2 * (band_rows + halo)
     desc, keep = sg.make_desc(method, N, W, H, C, rejection=rejection, sig=sig, shiftx=sx, shifty=sy,
                               max_thread=4, max_number_of_rows=H)
-    rc, out, rej, maxim = _with_budget(budget, lambda: gpu_ctx.stack_host(desc, frames))
-    assert rc == 0, gpu_ctx.error()
+    rc, out, rej, maxim, err = _with_budget(budget, lambda c: c.stack_host(desc, frames) + (c.error(),))
+    assert rc == 0, err
     assert_same(out, ref, f"host bands method={method} rej={rejection} rows={band_rows}")
     assert np.array_equal(rej, rej_ref), (rej, rej_ref)
     if method == sg.SUM:
@@ -197,5 +199,5 @@ def test_host_pull_budget_too_small(gpu_ctx):
     N, C, H, W = 8, 1, 16, 32
     frames = orc.synth(N, C, H, W, seed=2, maxshift=3)
     desc, keep = sg.make_desc(sg.MEAN, N, W, H, C, rejection=sg.SIGMA)
-    rc, out, rej, _ = _with_budget(N * C * W * 2 - 1, lambda: gpu_ctx.stack_host(desc, frames))
-    assert rc == -2 and "fit" in gpu_ctx.error()
+    rc, out, rej, _, err = _with_budget(N * C * W * 2 - 1, lambda c: c.stack_host(desc, frames) + (c.error(),))
+    assert rc == -2 and "fit" in err

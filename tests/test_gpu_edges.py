@@ -26,10 +26,12 @@ pytestmark = pytest.mark.gpu
 
 
 def _with_env(name, value, fn):
+    """fn(ctx) on a context created while the knob is set (knobs are read at sg_init)"""
     old = os.environ.get(name)
     os.environ[name] = value
     try:
-        return fn()
+        with sg.Context() as ctx:
+            return fn(ctx)
     finally:
         if old is None:
             del os.environ[name]
@@ -60,7 +62,7 @@ def test_reduce_pairs_edges_sum_max_min(gpu_ctx, W, case, method):
     out, _, maxim = gpu_stack(gpu_ctx, frames, method, shiftx=sx, shifty=sy)
     assert_same(out, ref, f"pairs W={W} case={case} method={method}")
     out1, _, maxim1 = _with_env("SG_REDUCE1", "1",
-                                lambda: gpu_stack(gpu_ctx, frames, method, shiftx=sx, shifty=sy))
+                                lambda c: gpu_stack(c, frames, method, shiftx=sx, shifty=sy))
     assert_same(out, out1, "pairs vs one pixel per lane")
     if method == sg.SUM:
         assert maxim == mref == maxim1
@@ -100,7 +102,7 @@ def test_register_pass_orders_agree(gpu_ctx, S, n):
     sel = orc.synth(n, 1, S, S, seed=S + 3 * n, maxshift=12)[:, 0].copy()
     res = {}
     for path in ("0", "1", "2"):
-        res[path] = _with_env("SG_REG_PATH", path, lambda: gpu_ctx.register_dft(sel))
+        res[path] = _with_env("SG_REG_PATH", path, lambda c: c.register_dft(sel))
     for path in ("0", "1"):
         for k in range(3):
             assert np.array_equal(np.nan_to_num(res[path][k], nan=-7.0),

@@ -92,6 +92,27 @@ def test_bad_inputs(tmp_path):
     write_fits(q, fr, bitpix=16, bzero=0)
     with sg.Seq.open_fits([q]) as seq:
         assert seq.read_region(0, 0, 0, 0, 4, 4)[0] != 0
+    # crafted SER header: frame size x count overflows int64 / exceeds the file
+    with open(p, "r+b") as f:
+        f.seek(26)
+        f.write(np.array([0x7FFFFFFF, 0x7FFFFFFF, 16, 0x7FFFFFFF], dtype="<i4").tobytes())
+    with pytest.raises(OSError):
+        sg.Seq.open_ser(p)
+    # FITS with NAXIS1 = 0, and a FITS whose data unit is cut short
+    z = str(tmp_path / "z.fit")
+    write_fits(z, np.zeros((1, 4, 4), np.uint16))
+    raw = bytearray(open(z, "rb").read())
+    k = raw.find(b"NAXIS1  =")
+    raw[k + 10:k + 30] = b"%20d" % 0
+    open(z, "wb").write(bytes(raw))
+    with pytest.raises(OSError):
+        sg.Seq.open_fits([z])
+    c = str(tmp_path / "cut.fit")
+    write_fits(c, np.zeros((1, 64, 64), np.uint16))
+    with open(c, "r+b") as f:
+        f.truncate(2880 + 1000)
+    with pytest.raises(OSError):
+        sg.Seq.open_fits([c])
     # frames of different sizes in one FITS sequence
     a, b = str(tmp_path / "a.fit"), str(tmp_path / "b.fit")
     write_fits(a, np.zeros((1, 4, 4), np.uint16))

@@ -62,7 +62,10 @@ def test_write_read_round_trip(tmp_path):
 
 
 @pytest.mark.parametrize("bad", ["S 'x' 1 0 0 5 -1\nL 1\n", "L 1\nI 1 1\n", "S 'x' 1 1 1 5 -1\nL 1\nI 1 1 2 3\n",
-                                 "S 'x' 1 1 1 5 -1\nL 1\nR3 0 0 0 0 0 0 1\n"])
+                                 "S 'x' 1 1 1 5 -1\nL 1\nR3 0 0 0 0 0 0 1\n",
+                                 "S 'x' 1 -5 0 5 -1\nL 1\n",            # negative image count
+                                 "S 'x' 1 2 0 5 -1\nL -1\n",            # negative layer count
+                                 "S 'x' 1 2000000000 0 5 -1\nL 1\n"])   # allocation too large
 def test_malformed(tmp_path, bad):
     p = tmp_path / "bad.seq"
     p.write_text(bad)
