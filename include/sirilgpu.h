@@ -13,6 +13,9 @@
  *     seq_opened_read_region() returns (src/io/sequence.c:690-700).
  *   - Return codes mirror the reference: 0 ok, -1 generic/cancel/unsupported, -2 size or
  *     allocation error, -3 read failure (src/stacking/stacking.c:244-246,1212-1220).
+ *   - Device work runs on the context's own non-blocking HIP stream (or the stream passed
+ *     in): device buffers handed to a *_device call must be complete, i.e. the caller
+ *     synchronises whatever produced them on other streams (a torch fill, a copy) first.
  */
 #ifndef SIRILGPU_H
 #define SIRILGPU_H

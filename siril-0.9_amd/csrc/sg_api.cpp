@@ -26,8 +26,9 @@ struct SgChainTables {
 
 template <int NREG, bool LISTED>
 __global__ void k_stack_sorted(SgStackParams p, const unsigned int *list, const unsigned int *list_count);
-template <int REJ, int NORM>
-__global__ void k_stack_hist(SgStackParams p, unsigned int *redo_count, unsigned int *redo_list);
+template <int REJ, int NORM, int NI>
+__global__ void k_stack_hist(SgStackParams p, const int *tab, const int4 *norm, unsigned int *redo_count,
+		unsigned int *redo_list);
 void sg_dbg_why_dump(hipStream_t s);
 __global__ void k_stack_replay(SgStackParams p);
 __global__ void k_redo_to_literal(SgStackParams p, const unsigned int *list, const unsigned int *count,
@@ -424,28 +425,35 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			unsigned int *redo_list = redo_count + 16;
 			HIPCHK(hipMemsetAsync(redo_count, 0, sizeof(unsigned int), s));
 			HIPCHK(hipEventRecord(dv.ev[0], s));
-			const size_t nblk_h = (size_t)((W + 127) / 128) * nrows * C;	/* 128-pixel tiles */
+			/* NORM: 0 none, 1 additive (round(v scale - offset)), 2 multiplicative (round(v scale mul)) */
+			const int norm = p.normalize == SG_NO_NORM ? 0 :
+				(p.normalize == SG_ADDITIVE || p.normalize == SG_ADDITIVE_SCALING) ? 1 : 2;
+			/* tile = 128 NI pixels of a row, 4 NI waves: NI = 1 by default (sg_stack_hist.hip);
+			 * the A/B NI = 2 (SG_HIST_NI=2) exists without normalisation only (it spills there:
+			 * the per-sample double arithmetic of two pixel pairs) */
+			const int ni = (norm == 0 && ctx->knobs.hist_ni == 2) ? 2 : 1;
+			const size_t nblk_h = (size_t)((W + 128 * ni - 1) / (128 * ni)) * nrows * C;
 			if (p.dbg == 14) {	/* A/B: report the resident workgroups per CU */
 				int per_cu = -1;
-				(void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_stack_hist<2, 0>, 256,
-						(size_t)ctx->knobs.hist_ldspad);
+				(void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ni == 2 ? (const void *)k_stack_hist<2, 0, 2>
+						: (const void *)k_stack_hist<2, 0, 1>, 256 * ni, (size_t)ctx->knobs.hist_ldspad);
 				hipDeviceProp_t prop;
 				(void)hipGetDeviceProperties(&prop, dv.id);
 				fprintf(stderr, "k_stack_hist: %d workgroups/CU (lds/CU %zu, lds/block max %zu, pad %d)\n", per_cu,
 						(size_t)prop.maxSharedMemoryPerMultiProcessor, (size_t)prop.sharedMemPerBlock, ctx->knobs.hist_ldspad);
 			}
-			/* NORM: 0 none, 1 additive (round(v scale - offset)), 2 multiplicative (round(v scale mul)) */
-			const int norm = p.normalize == SG_NO_NORM ? 0 :
-				(p.normalize == SG_ADDITIVE || p.normalize == SG_ADDITIVE_SCALING) ? 1 : 2;
 			const size_t lds_pad = (size_t)ctx->knobs.hist_ldspad;
-			const dim3 hg((unsigned)nblk_h), hb(256);
-			switch ((p.rejection == SG_WINSORIZED ? 10 : 0) + norm) {
-			case 0: hipLaunchKernelGGL((k_stack_hist<2, 0>), hg, hb, lds_pad, s, p, redo_count, redo_list); break;
-			case 1: hipLaunchKernelGGL((k_stack_hist<2, 1>), hg, hb, lds_pad, s, p, redo_count, redo_list); break;
-			case 2: hipLaunchKernelGGL((k_stack_hist<2, 2>), hg, hb, lds_pad, s, p, redo_count, redo_list); break;
-			case 10: hipLaunchKernelGGL((k_stack_hist<4, 0>), hg, hb, lds_pad, s, p, redo_count, redo_list); break;
-			case 11: hipLaunchKernelGGL((k_stack_hist<4, 1>), hg, hb, lds_pad, s, p, redo_count, redo_list); break;
-			default: hipLaunchKernelGGL((k_stack_hist<4, 2>), hg, hb, lds_pad, s, p, redo_count, redo_list); break;
+			const dim3 hg((unsigned)nblk_h), hb(256 * ni);
+			switch ((p.rejection == SG_WINSORIZED ? 10 : 0) + norm + 100 * ni) {
+			case 100: hipLaunchKernelGGL((k_stack_hist<2, 0, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			case 101: hipLaunchKernelGGL((k_stack_hist<2, 1, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			case 102: hipLaunchKernelGGL((k_stack_hist<2, 2, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			case 110: hipLaunchKernelGGL((k_stack_hist<4, 0, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			case 111: hipLaunchKernelGGL((k_stack_hist<4, 1, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			case 112: hipLaunchKernelGGL((k_stack_hist<4, 2, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			case 200: hipLaunchKernelGGL((k_stack_hist<2, 0, 2>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			case 210: hipLaunchKernelGGL((k_stack_hist<4, 0, 2>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			default: return set_err(ctx, SG_ERR_GENERIC, "no histogram kernel for this case%s%.0ld", "", 0);
 			}
 			HIPCHK(hipGetLastError());
 			HIPCHK(hipEventRecord(dv.ev[1], s));
@@ -564,6 +572,12 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 				"whose frame rows are not resident; make the full frames resident%s%.0ld", "", 0);
 	if (p.dbg == 12)
 		sg_dbg_why_dump(s);
+	if (p.dbg == 16 && dv.redo.p) {	/* A/B: SIGMA fast finish queue (sg_stack_hist.hip) */
+		unsigned long long q = 0;
+		(void)hipMemcpy(&q, (unsigned int *)dv.redo.p + 8, sizeof q, hipMemcpyDeviceToHost);
+		(void)hipMemset((unsigned int *)dv.redo.p + 8, 0, sizeof q);
+		fprintf(stderr, "fast finish: %llu queued pixels in %llu tiles\n", q & ((1ull << 40) - 1), q >> 40);
+	}
 	float ms = 0.f, ms2 = 0.f;
 	HIPCHK(hipEventElapsedTime(&ms, dv.ev[0], dv.ev[1]));
 	HIPCHK(hipEventElapsedTime(&ms2, dv.ev[0], dv.ev[2]));

@@ -39,8 +39,15 @@
 
 #define SGH_BINS 256
 #define SGH_DW (SGH_BINS / 4)	/* band dwords per pixel */
-#define SGH_WAVES 4
-#define SGH_COLS 128		/* pixels per tile: lane l owns pixels 2l (col l) and 2l+1 (col 64+l) */
+/* A tile is NI * 128 pixels of one row, streamed by NI * 4 waves: every lane loads NI dwords
+ * (pixel pairs) per frame, instruction i covering the tile's 256-byte segment i.  Pixel pair i
+ * of lane l = pixels 128 i + 2 l (column 64 (2 i) + l) and 128 i + 2 l + 1 (column
+ * 64 (2 i + 1) + l).  NI = 2 reads each frame row as one contiguous 512-byte segment (a
+ * shifted row straddles 5 128-B lines per 512 B instead of 3 per 256 B: tools/bw_probe4.hip
+ * streams the 512 x 4096^2 sequence in 2.94 ms against 3.20 ms), but two 8-wave workgroups per
+ * CU overlap one tile's finish with the other's loads worse than four 4-wave ones: 4.62 ms
+ * against 4.22 ms for the whole kernel, so NI = 1 is the default (SG_HIST_NI=2 selects 2). */
+#define SGH_WAVES_PER_NI 4
 #define SGH_CENTER 16		/* frames used for the centre estimate */
 #ifndef SGH_NBUF
 #define SGH_NBUF 2		/* register buffers of 16 frames per wave (NBUF-1 blocks in flight while binning) */
@@ -56,10 +63,11 @@ typedef unsigned short sgh_u16x2 __attribute__((ext_vector_type(2)));
  *   h[half][64][l]               : samples outside the band (u32: zeros, 65535s; anything
  *                                  else sends the pixel to the redo list) */
 #define SGH_HROWS (SGH_DW + 1)
+template <int NI>
 struct SghLds {
-	uint32_t h[2][SGH_HROWS][64];
-	uint32_t nz[SGH_COLS], ns[SGH_COLS];	/* zeros / 65535s (all of them lie outside the band) */
-	uint32_t lo2[64];			/* band starts of the lane pixel pairs (u16 halves) */
+	uint32_t h[2 * NI][SGH_HROWS][64];
+	uint32_t nz[128 * NI], ns[128 * NI];	/* zeros / 65535s (all of them lie outside the band) */
+	uint32_t lo2[NI][64];			/* band starts of the lane pixel pairs (u16 halves) */
 };
 
 /* Finish-phase queries.  The band is cut into SGH_NGRP groups of SGH_GRP dwords (32 bins);
@@ -80,7 +88,7 @@ struct SghPix {
 	int lo;			/* value of bin 0, 1 <= lo <= 65279 */
 	int nz, ns, nb;		/* zeros, 65535s, band samples (nz + nb + ns == N) */
 	int col;
-	const SghLds *L;
+	const uint32_t *hb;	/* the tile's histogram h[0][0][0] */
 	uint32_t pc[SGH_NGRP], ps[SGH_NGRP], pss[SGH_NGRP];	/* band prefix before group g */
 	SghM Z;			/* moments of the zeros */
 	SghM T;			/* moments of all samples */
@@ -96,7 +104,7 @@ __device__ __forceinline__ uint32_t sgh_sel(const uint32_t (&t)[SGH_NGRP], int k
 }
 
 __device__ __forceinline__ void sgh_grp(const SghPix &P, int g, uint32_t (&d)[SGH_GRP]) {
-	const uint32_t *b = &P.L->h[P.col >> 6][g * SGH_GRP][P.col & 63];
+	const uint32_t *b = P.hb + ((P.col >> 6) * SGH_HROWS + g * SGH_GRP) * 64 + (P.col & 63);
 #pragma unroll
 	for (int k = 0; k < SGH_GRP; k++)
 		d[k] = b[k * 64];
@@ -318,9 +326,18 @@ struct SghTab16 {
 	int c1[16];
 	uint32_t sx2p[8];
 };
-__device__ __forceinline__ void sgh_tab16(const SgStackParams &p, int f0, SghTab16 &T) {
-	const int4 *q = (const int4 *)(p.hist_tab + f0);
-	const int4 *r = (const int4 *)(p.hist_tab + p.hist_npad + f0 / 2);
+/* the shift table and the normalisation pairs reach the kernel as __restrict__ kernel
+ * arguments (SghRo): nothing the kernel stores can alias them, so their uniform loads compile
+ * to scalar loads (s_load_dwordx16 / x8 / x4) instead of vector loads that would queue
+ * behind the frame loads in vmcnt order */
+struct SghRo {
+	const int *tab;		/* SgStackParams::hist_tab */
+	const int4 *norm;	/* SgStackParams::hist_norm as int4 pairs */
+	int npad;
+};
+__device__ __forceinline__ void sgh_tab16(const SghRo &ro, int f0, SghTab16 &T) {
+	const int4 *q = (const int4 *)(ro.tab + f0);
+	const int4 *r = (const int4 *)(ro.tab + ro.npad + f0 / 2);
 #pragma unroll
 	for (int i = 0; i < 4; i++) {
 		const int4 v = q[i];
@@ -351,25 +368,33 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t sgh_rsrc(const char *base, uin
  * straddling the left edge loads one pixel to the right and the binning moves the valid
  * pixel to the high half (<< 16), one straddling the right edge loads one pixel to the
  * left (>> 16); two fix bits per frame in `fix` */
-template <bool FULL, bool EDGE>
-__device__ __forceinline__ void sgh_loadblk(const SghFrame &F, const SghTab16 &T, int N, int f0, uint32_t (&dst)[16],
-		uint32_t &fix) {
+template <bool FULL, bool EDGE, int NI, int MB = 16, int MO = 0>
+__device__ __forceinline__ void sgh_loadblk(const SghFrame &F, const SghTab16 &T, int N, int f0,
+		uint32_t (&dst)[MB][NI], uint32_t (&fix)[NI]) {
 	const char *b = F.plane0 + (int64_t)f0 * F.fstride2;
-	if (EDGE)
-		fix = 0;
+	if (EDGE) {
 #pragma unroll
-	for (int m = 0; m < 16; m++) {
+		for (int i = 0; i < NI; i++)
+			fix[i] = 0;
+	}
+#pragma unroll
+	for (int m = 0; m < MB; m++) {
 		const uint32_t nrec = (FULL || f0 + m < N) ? F.plane_bytes : 0u;
-		const uint32_t k = (uint32_t)(F.rw2 - T.c1[m]);
-		uint32_t off = k + F.xa2;
-		if (EDGE) {
-			const int sx2 = (m & 1) ? ((int)T.sx2p[m >> 1] >> 16) : (int)(int16_t)(T.sx2p[m >> 1] & 0xFFFFu);
-			const uint32_t sca = F.xa2 - (uint32_t)sx2;
-			const bool bada = sca >= (uint32_t)F.w2, badb = sca + 2u >= (uint32_t)F.w2;
-			off = bada ? (badb ? 0x80000000u : off + 2u) : (badb ? off - 2u : off);
-			fix |= ((bada && !badb) ? 1u : ((!bada && badb) ? 2u : ((bada && badb) ? 3u : 0u))) << (2 * m);
+		const uint32_t k = (uint32_t)(F.rw2 - T.c1[MO + m]);
+#pragma unroll
+		for (int i = 0; i < NI; i++) {
+			const uint32_t xa2 = F.xa2 + 256u * i;	/* the lane's pair in segment i */
+			uint32_t off = k + xa2;
+			if (EDGE) {
+				const int mt = MO + m;
+				const int sx2 = (mt & 1) ? ((int)T.sx2p[mt >> 1] >> 16) : (int)(int16_t)(T.sx2p[mt >> 1] & 0xFFFFu);
+				const uint32_t sca = xa2 - (uint32_t)sx2;
+				const bool bada = sca >= (uint32_t)F.w2, badb = sca + 2u >= (uint32_t)F.w2;
+				off = bada ? (badb ? 0x80000000u : off + 2u) : (badb ? off - 2u : off);
+				fix[i] |= ((bada && !badb) ? 1u : ((!bada && badb) ? 2u : ((bada && badb) ? 3u : 0u))) << (2 * m);
+			}
+			dst[m][i] = __builtin_amdgcn_raw_buffer_load_b32(sgh_rsrc(b, nrec), (int)off, 0, 0);
 		}
-		dst[m] = __builtin_amdgcn_raw_buffer_load_b32(sgh_rsrc(b, nrec), (int)off, 0, 0);
 		b += F.fstride2;
 	}
 }
@@ -408,8 +433,8 @@ __device__ __forceinline__ uint32_t sgh_norm_pair(uint32_t v, double a, double b
 }
 
 /* per-frame normalisation pair {scale, offset | mul} (one scalar load) */
-__device__ __forceinline__ void sgh_coef(const SgStackParams &p, int f, double &a, double &b) {
-	const int4 v = ((const int4 *)p.hist_norm)[f];
+__device__ __forceinline__ void sgh_coef(const SghRo &ro, int f, double &a, double &b) {
+	const int4 v = ro.norm[f];
 	const int x = __builtin_amdgcn_readfirstlane(v.x), y = __builtin_amdgcn_readfirstlane(v.y);
 	const int z = __builtin_amdgcn_readfirstlane(v.z), w = __builtin_amdgcn_readfirstlane(v.w);
 	a = __hiloint2double(y, x);
@@ -491,7 +516,7 @@ __device__ __forceinline__ int sgh_value_at1(const SghPix &P, int g) {
 /* the SIGMA loop of sgh_sigma, split over a lane pair: half 0 owns the low side (median
  * rank g1, threshold a - 1, M(A - 1)), half 1 the high side (rank g2, threshold bt, M(B)) */
 __device__ __forceinline__ int sgh_sigma2(const SghPix &P, int N, double sl, double sh, int half, uint16_t *value,
-		uint32_t *rlo_out, uint32_t *rhi_out) {
+		uint32_t *rlo_out, uint32_t *rhi_out, int &passes) {
 	int A = 0, B = 65535, n = N, r = 0, nrem;
 	SghM MA = {0, 0, 0}, MB = P.T;
 	uint32_t rlo = 0, rhi = 0;
@@ -580,6 +605,7 @@ __device__ __forceinline__ int sgh_sigma2(const SghPix &P, int N, double sl, dou
 		r += L + H;
 		nrem = L + H;
 		n -= nrem;
+		passes++;
 	} while (nrem > 0 && n > 3);
 	const long long tot = (MB.s - MA.s) + (long long)n * P.lo;
 	*value = sg_round_to_WORD((double)tot / (double)n);
@@ -841,8 +867,8 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint
 
 /* pixel column `col` of the tile (x its image column); PAIR: lane pair half `half`, else one
  * lane per column (half = 0) */
-template <int REJ, bool PAIR>
-__device__ void sgh_finish2(const SgStackParams &p, SghLds &L, int col, int half, int lo, int R, int c, int x,
+template <int REJ, bool PAIR, int NI>
+__device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int half, int lo, int R, int c, int x,
 		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
 	const int lane = threadIdx.x & 63;
 	const int N = p.N;
@@ -852,6 +878,9 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds &L, int col, int half
 			p.out[((int64_t)c * p.H + R) * p.W + x] = (uint16_t)(hc[0] + L.nz[col]);
 		return;
 	}
+	/* A/B timeline (dbg 11): cycles of the prefix and of the pass loop, passes per wave */
+	const uint64_t c0 = p.dbg == 11 ? __builtin_readcyclecounter() : 0;
+	int passes = 0;
 	/* prefix: this lane's 4 groups, then the partner's 4 (PAIR), or all 8 */
 	constexpr int NG = PAIR ? SGH_NGRP / 2 : SGH_NGRP;
 	uint32_t gc[NG], gs[NG], gss[NG];
@@ -894,10 +923,11 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds &L, int col, int half
 	P.ns = (int)L.ns[col];
 	P.nb = (int)cum;
 	P.col = col;
-	P.L = &L;
+	P.hb = &L.h[0][0][0];
 	int cls = SG_CLS_OK;
 	uint16_t value = 0;
 	uint32_t rlo = 0, rhi = 0;
+	const uint64_t c1 = p.dbg == 11 ? __builtin_readcyclecounter() : 0;
 	if (x < p.W) {
 		if (p.dbg == 1) {
 			value = (uint16_t)(s32 + ss32);
@@ -911,15 +941,16 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds &L, int col, int half
 			P.T.c = N;
 			P.T.s = (long long)s32 + P.Z.s + ds * P.ns;
 			P.T.ss = (unsigned long long)ss32 + P.Z.ss + (unsigned long long)(ds * ds) * (unsigned long long)P.ns;
-			if (REJ == 4)
+			if (REJ == 4 || !PAIR)
 				cls = sgh_winsorized(P, N, p.sig0, p.sig1, &value, &rlo, &rhi);
 			else
-				cls = sgh_sigma2(P, N, p.sig0, p.sig1, half, &value, &rlo, &rhi);
+				cls = sgh_sigma2(P, N, p.sig0, p.sig1, half, &value, &rlo, &rhi, passes);
 		}
 		const int64_t pix = ((int64_t)c * p.H + R) * p.W + x;
 		if (!half) {
 			if (cls == SG_CLS_OK) {
-				p.out[pix] = value;
+				if (p.dbg != 11)	/* the timeline A/B keeps its stamps in the output buffer */
+					p.out[pix] = value;
 			} else {
 				const unsigned int slot = atomicAdd(redo_count, 1u);
 				redo_list[slot] = (unsigned int)pix;
@@ -928,98 +959,121 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds &L, int col, int half
 		if (cls != SG_CLS_OK || half)
 			rlo = rhi = 0;
 	}
+	if (p.dbg == 11 && NI == 2) {
+		const uint64_t c2 = __builtin_readcyclecounter();
+		int pmax = passes, psum = passes;
+		for (int o = 32; o > 0; o >>= 1) {
+			pmax = max(pmax, __shfl_xor(pmax, o, 64));
+			psum += __shfl_xor(psum, o, 64);
+		}
+		if (lane == 0) {
+			uint64_t *tw = (uint64_t *)p.out + (size_t)blockIdx.x * 32 + 4 + 3 * (threadIdx.x >> 6);
+			tw[0] = c1 - c0;
+			tw[1] = c2 - c1;
+			tw[2] = (uint64_t)pmax | ((uint64_t)psum << 16);
+		}
+	}
 	unsigned long long a = rlo, b = rhi;
 	for (int o = 32; o > 0; o >>= 1) {
 		a += __shfl_down(a, o, 64);
 		b += __shfl_down(b, o, 64);
 	}
 	if (lane == 0 && (a | b)) {
-		unsigned long long *sh = p.rej + ((size_t)((blockIdx.x * 4 + (col >> 5)) % SG_REJ_SHARDS) * 6 + c * 2);
+		unsigned long long *sh = p.rej + ((size_t)((blockIdx.x * 8 + (col >> 5)) % SG_REJ_SHARDS) * 6 + c * 2);
 		atomicAdd(sh, a);
 		atomicAdd(sh + 1, b);
 	}
 }
 
 /* one wave's share of the tile's histogram build: 16-frame blocks, wave w bins blocks w,
- * w+4, w+8, ... in order, with NBUF named register buffers: a buffer is refilled with the
- * wave's block NBUF steps ahead right after it has been binned, so NBUF-1 blocks stay in
- * flight during the binning; the shift table of that block is fetched (scalar loads)
- * before the binning.  No block is loaded twice.  Frames 0..15 (wave 0's first block) are
- * the centre sample: wave 0 sorts them and publishes the band starts through LDS while the
- * other waves' first blocks are in flight (one barrier, which also covers the clear). */
-template <bool EDGE, int NBUF, int NORM>
-__device__ __forceinline__ void sgh_build(const SgStackParams &p, SghLds &L, const SghFrame &F, int wave, int lane,
-		int &lo_a, int &lo_b, uint32_t &nonzero, uint32_t &nsat, int &counted) {
+ * w+WAVES, w+2 WAVES, ... in order, with NBUF named register buffers: a buffer is refilled with
+ * the wave's block NBUF steps ahead right after it has been binned, so NBUF-1 blocks stay in
+ * flight during the binning; the shift table of that block is fetched (scalar loads) before
+ * the binning.  No block is loaded twice.  Frames 0..15 (wave 0's first block) are the centre
+ * sample: wave 0 sorts them and publishes the band starts through LDS while the other waves'
+ * first blocks are in flight (one barrier, which also covers the clear). */
+template <bool EDGE, int NBUF, int NORM, int NI>
+__device__ __forceinline__ void sgh_build(const SgStackParams &p, const SghRo &ro, SghLds<NI> &L, const SghFrame &F,
+		int wave, int lane,
+		uint32_t (&lo2)[NI], uint32_t (&nonzero)[NI], uint32_t (&nsat)[NI], int &counted) {
 	constexpr int M = 16;		/* frames per block */
-	constexpr int STEP = M * SGH_WAVES;
+	constexpr int WAVES = SGH_WAVES_PER_NI * NI;
+	constexpr int STEP = M * WAVES;
 	constexpr int AHEAD = NBUF * STEP;
 	const int N = p.N;
 	uint32_t *const h = &L.h[0][0][0];
 	const uint32_t l4 = (uint32_t)lane * 4u;
-	uint32_t buf[NBUF][M], fix[NBUF];
+	uint32_t buf[NBUF][M][NI], fix[NBUF][NI];
 	SghTab16 T;
-	auto loadblk = [&](int f0, uint32_t (&dst)[M], uint32_t &fx) {
+	auto loadblk = [&](int f0, uint32_t (&dst)[M][NI], uint32_t (&fx)[NI]) {
 		if (f0 + M <= N)
-			sgh_loadblk<true, EDGE>(F, T, N, f0, dst, fx);
+			sgh_loadblk<true, EDGE, NI>(F, T, N, f0, dst, fx);
 		else
-			sgh_loadblk<false, EDGE>(F, T, N, f0, dst, fx);
+			sgh_loadblk<false, EDGE, NI>(F, T, N, f0, dst, fx);
 	};
 	int f[NBUF];
 #pragma unroll
 	for (int k = 0; k < NBUF; k++) {
 		f[k] = M * wave + k * STEP;
-		fix[k] = 0;
+#pragma unroll
+		for (int i = 0; i < NI; i++)
+			fix[k][i] = 0;
 		if (f[k] < N) {
-			sgh_tab16(p, f[k], T);
+			sgh_tab16(ro, f[k], T);
 			loadblk(f[k], buf[k], fix[k]);
 		}
 	}
 	if (wave == 0) {
-		uint32_t p16[SGH_CENTER];
 #pragma unroll
-		for (int m = 0; m < SGH_CENTER; m++) {
-			p16[m] = sgh_fixup<EDGE>(buf[0][m], fix[0], m);
-			if (NORM) {
-				double a, b;
-				sgh_coef(p, m, a, b);
-				p16[m] = sgh_norm_pair<NORM, EDGE>(p16[m], a, b, fix[0], m);
+		for (int i = 0; i < NI; i++) {
+			uint32_t p16[SGH_CENTER];
+#pragma unroll
+			for (int m = 0; m < SGH_CENTER; m++) {
+				p16[m] = sgh_fixup<EDGE>(buf[0][m][i], fix[0][i], m);
+				if (NORM) {
+					double a, b;
+					sgh_coef(ro, m, a, b);
+					p16[m] = sgh_norm_pair<NORM, EDGE>(p16[m], a, b, fix[0][i], m);
+				}
 			}
+			int la, lb;
+			sgh_centre2(p16, la, lb);
+			L.lo2[i][lane] = (uint32_t)la | ((uint32_t)lb << 16);
 		}
-		int la, lb;
-		sgh_centre2(p16, la, lb);
-		L.lo2[lane] = (uint32_t)la | ((uint32_t)lb << 16);
 	}
 	__syncthreads();	/* histogram cleared, band starts published */
-	{
-		const uint32_t l2 = L.lo2[lane];
-		lo_a = (int)(l2 & 0xFFFFu);
-		lo_b = (int)(l2 >> 16);
-	}
-	const uint32_t lo2 = (uint32_t)lo_a | ((uint32_t)lo_b << 16);
+#pragma unroll
+	for (int i = 0; i < NI; i++)
+		lo2[i] = L.lo2[i][lane];
 	const bool loads_only = p.dbg == 3;
-	auto binblk = [&](int f0, const uint32_t (&raw)[M], uint32_t fx) {
+	auto binblk = [&](int f0, const uint32_t (&raw)[M][NI], const uint32_t (&fx)[NI]) {
 		if (loads_only) {
 #pragma unroll
 			for (int m = 0; m < M; m++)
-				nonzero ^= raw[m];
+#pragma unroll
+				for (int i = 0; i < NI; i++)
+					nonzero[i] ^= raw[m][i];
 		} else {
 #pragma unroll
 			for (int m = 0; m < M; m++) {
 				if (f0 + M <= N || f0 + m < N) {
-					uint32_t v = sgh_fixup<EDGE>(raw[m], fx, m);
-					if (NORM) {
-						double a, b;
-						sgh_coef(p, f0 + m, a, b);
-						v = sgh_norm_pair<NORM, EDGE>(v, a, b, fx, m);
+					double a = 0.0, b = 0.0;
+					if (NORM)
+						sgh_coef(ro, f0 + m, a, b);
+#pragma unroll
+					for (int i = 0; i < NI; i++) {
+						uint32_t v = sgh_fixup<EDGE>(raw[m][i], fx[i], m);
+						if (NORM)
+							v = sgh_norm_pair<NORM, EDGE>(v, a, b, fx[i], m);
+						sgh_bin_pair(h + i * (2 * SGH_HROWS * 64), l4, lo2[i], v, nonzero[i], nsat[i]);
 					}
-					sgh_bin_pair(h, l4, lo2, v, nonzero, nsat);
 				}
 			}
 		}
 		counted += (N - f0 < M ? N - f0 : M);
 	};
 	if (f[0] + AHEAD < N)
-		sgh_tab16(p, f[0] + AHEAD, T);
+		sgh_tab16(ro, f[0] + AHEAD, T);
 	while (f[0] < N) {
 #pragma unroll
 		for (int k = 0; k < NBUF; k++) {
@@ -1033,18 +1087,169 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, SghLds &L, con
 			const int kn = (k + 1) % NBUF;
 			const int tn = f[kn] + AHEAD;	/* the next buffer's refill */
 			if (f[kn] < N && tn < N)
-				sgh_tab16(p, tn, T);
+				sgh_tab16(ro, tn, T);
 		}
 	}
 }
 
-template <int REJ, int NORM>	/* REJ 2 = SIGMA, 4 = WINSORIZED; NORM 0 none, 1 additive, 2 multiplicative */
-__global__ void __launch_bounds__(64 * SGH_WAVES)
-k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
-	__shared__ SghLds L;
+/* the same build with 8-frame half blocks (NI = 2: two dword loads per lane and frame):
+ * wave w bins the 16-frame blocks w, w + WAVES, ... in order, each as two halves; NB blocks
+ * (2 NB half buffers) are in flight, so while one half is binned 2 NB - 1 halves keep
+ * loading (with two 8-wave workgroups per CU, one workgroup's loads must carry the CU while
+ * the other runs its finish).  The shift table of a block is fetched once for both halves.
+ * Wave 0's first block (frames 0..15) is the centre sample. */
+#ifndef SGH_NB
+#define SGH_NB 1	/* 2: 4.85 vs 4.62 ms (NI = 2, scripts/gpu_r2i.sh) */
+#endif
+
+template <bool EDGE, int NORM, int NI, int NB>
+__device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const SghRo &ro, SghLds<NI> &L, const SghFrame &F,
+		int wave, int lane, uint32_t (&lo2)[NI], uint32_t (&nonzero)[NI], uint32_t (&nsat)[NI], int &counted) {
+	constexpr int MB = 8;
+	constexpr int WAVES = SGH_WAVES_PER_NI * NI;
+	constexpr int STEP = 16 * WAVES;	/* frames between a wave's consecutive blocks */
+	const int N = p.N;
+	uint32_t *const h = &L.h[0][0][0];
+	const uint32_t l4 = (uint32_t)lane * 4u;
+	uint32_t buf[NB][2][MB][NI], fix[NB][2][NI];
+	SghTab16 T;
+	/* half hh (frames f16 + 8 hh ..) of the block at f16, bounds-checked unless whole */
+	auto loadh = [&](int f16, int hh, uint32_t (&dst)[MB][NI], uint32_t (&fx)[NI]) {
+		if (f16 + 16 <= N) {
+			if (hh == 0)
+				sgh_loadblk<true, EDGE, NI, MB, 0>(F, T, N, f16, dst, fx);
+			else
+				sgh_loadblk<true, EDGE, NI, MB, 8>(F, T, N, f16 + 8, dst, fx);
+		} else {
+			if (hh == 0)
+				sgh_loadblk<false, EDGE, NI, MB, 0>(F, T, N, f16, dst, fx);
+			else
+				sgh_loadblk<false, EDGE, NI, MB, 8>(F, T, N, f16 + 8, dst, fx);
+		}
+	};
+	int f16 = 16 * wave;
+#pragma unroll
+	for (int b = 0; b < NB; b++) {
+		const int fb = f16 + b * STEP;
+#pragma unroll
+		for (int i = 0; i < NI; i++)
+			fix[b][0][i] = fix[b][1][i] = 0;
+		if (fb < N) {
+			sgh_tab16(ro, fb, T);
+			loadh(fb, 0, buf[b][0], fix[b][0]);
+			loadh(fb, 1, buf[b][1], fix[b][1]);
+		}
+	}
+	const bool nocentre = p.dbg == 15;	/* A/B: loads only, no centre and no start barrier */
+	if (wave == 0 && !nocentre) {
+#pragma unroll
+		for (int i = 0; i < NI; i++) {
+			uint32_t p16[SGH_CENTER];
+#pragma unroll
+			for (int m = 0; m < SGH_CENTER; m++) {
+				const int mm = m & (MB - 1), hh = m / MB;
+				p16[m] = sgh_fixup<EDGE>(buf[0][hh][mm][i], fix[0][hh][i], mm);
+				if (NORM) {
+					double a, b;
+					sgh_coef(ro, m, a, b);
+					p16[m] = sgh_norm_pair<NORM, EDGE>(p16[m], a, b, fix[0][hh][i], mm);
+				}
+			}
+			int la, lb;
+			sgh_centre2(p16, la, lb);
+			L.lo2[i][lane] = (uint32_t)la | ((uint32_t)lb << 16);
+		}
+	}
+	if (!nocentre)
+		__syncthreads();	/* histogram cleared, band starts published */
+#pragma unroll
+	for (int i = 0; i < NI; i++)
+		lo2[i] = nocentre ? 0u : L.lo2[i][lane];
+	const bool loads_only = p.dbg == 3 || nocentre;
+	/* bin one half (frames f0 .. f0 + 7), per-frame bounds when it is not whole */
+	auto binh = [&](int f0, const uint32_t (&raw)[MB][NI], const uint32_t (&fx)[NI], bool whole) {
+		if (loads_only) {
+#pragma unroll
+			for (int m = 0; m < MB; m++)
+#pragma unroll
+				for (int i = 0; i < NI; i++)
+					nonzero[i] ^= raw[m][i];
+		} else {
+#pragma unroll
+			for (int m = 0; m < MB; m++) {
+				if (whole || f0 + m < N) {
+					double a = 0.0, b = 0.0;
+					if (NORM)
+						sgh_coef(ro, f0 + m, a, b);
+#pragma unroll
+					for (int i = 0; i < NI; i++) {
+						uint32_t v = sgh_fixup<EDGE>(raw[m][i], fx[i], m);
+						if (NORM)
+							v = sgh_norm_pair<NORM, EDGE>(v, a, b, fx[i], m);
+						sgh_bin_pair(h + i * (2 * SGH_HROWS * 64), l4, lo2[i], v, nonzero[i], nsat[i]);
+					}
+				}
+			}
+		}
+		const int nf = N - f0;
+		counted += whole ? MB : (nf < 0 ? 0 : (nf < MB ? nf : MB));
+	};
+	/* steady state, straight-line: the NB blocks in hand and their refills all whole.
+	 * sched_barrier keeps each refill right after the binning of its buffer (the scheduler
+	 * otherwise hoists the next half's binning above the refill, and its vmcnt waits then
+	 * drain every load before any new one issues) */
+	while (f16 + (2 * NB - 1) * STEP + 16 <= N) {
+#pragma unroll
+		for (int b = 0; b < NB; b++) {
+			const int fb = f16 + b * STEP, nx = fb + NB * STEP;
+			sgh_tab16(ro, nx, T);
+			binh(fb, buf[b][0], fix[b][0], true);
+			__builtin_amdgcn_sched_barrier(0);
+			sgh_loadblk<true, EDGE, NI, MB, 0>(F, T, N, nx, buf[b][0], fix[b][0]);
+			__builtin_amdgcn_sched_barrier(0);
+			binh(fb + 8, buf[b][1], fix[b][1], true);
+			__builtin_amdgcn_sched_barrier(0);
+			sgh_loadblk<true, EDGE, NI, MB, 8>(F, T, N, nx + 8, buf[b][1], fix[b][1]);
+			__builtin_amdgcn_sched_barrier(0);
+		}
+		f16 += NB * STEP;
+	}
+	/* the remaining blocks, in order, with bounds */
+	while (f16 < N) {
+#pragma unroll
+		for (int b = 0; b < NB; b++) {
+			const int fb = f16 + b * STEP, nx = fb + NB * STEP;
+			if (fb >= N)
+				break;
+			if (nx < N)
+				sgh_tab16(ro, nx, T);
+			binh(fb, buf[b][0], fix[b][0], fb + 16 <= N);
+			if (nx < N)
+				loadh(nx, 0, buf[b][0], fix[b][0]);
+			binh(fb + 8, buf[b][1], fix[b][1], fb + 16 <= N);
+			if (nx < N)
+				loadh(nx, 1, buf[b][1], fix[b][1]);
+		}
+		f16 += NB * STEP;
+	}
+}
+
+/* REJ 2 = SIGMA, 4 = WINSORIZED; NORM 0 none, 1 additive, 2 multiplicative; NI pixel pairs
+ * per lane (tile of 128 NI pixels, 4 NI waves).  Two 8-wave workgroups (69 KB of LDS each)
+ * or four 4-wave ones (34.5 KB) per CU: 16 waves, at most 128 VGPRs. */
+template <int REJ, int NORM, int NI>
+__global__ void __launch_bounds__(64 * SGH_WAVES_PER_NI * NI, 4)
+k_stack_hist(SgStackParams p, const int *__restrict__ tab, const int4 *__restrict__ norm,
+		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
+	constexpr int WAVES = SGH_WAVES_PER_NI * NI, COLS = 128 * NI;
+	SghRo ro;
+	ro.tab = tab;
+	ro.norm = norm;
+	ro.npad = p.hist_npad;
+	__shared__ SghLds<NI> L;
 	const int tid = threadIdx.x, lane = tid & 63;
 	const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-	const int ntx = (p.W + SGH_COLS - 1) / SGH_COLS;
+	const int ntx = (p.W + COLS - 1) / COLS;
 	const int nrows = p.row_end - p.row_begin;
 	/* XCD-aware tile order: the dispatcher deals workgroups round-robin to the 8 XCDs, so
 	 * XCD k gets a contiguous run of tiles (whole rows: neighbouring tiles share the 128-B
@@ -1056,10 +1261,10 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 	bid /= ntx;
 	const int R = p.row_begin + (bid % nrows);
 	const int c = bid / nrows;
-	const int x0 = xt * SGH_COLS;
-	bool interior = x0 >= p.hist_maxsx && x0 + SGH_COLS + p.hist_maxsx <= p.W;
+	const int x0 = xt * COLS;
+	bool interior = x0 >= p.hist_maxsx && x0 + COLS + p.hist_maxsx <= p.W;
 	if (p.dbg == 4)		/* A/B: every full tile on the dword path (wrong edges) */
-		interior = x0 + SGH_COLS <= p.W;
+		interior = x0 + COLS <= p.W;
 	if (p.dbg == 5 && !interior)	/* A/B: skip the edge tiles */
 		return;
 	SghFrame F;
@@ -1070,16 +1275,28 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 	F.rw2 = R * p.W * 2;
 	F.xa2 = (uint32_t)(x0 + 2 * lane) * 2u;
 
-	for (int i = tid; i < 2 * SGH_HROWS * 64; i += 64 * SGH_WAVES)
+	for (int i = tid; i < 2 * NI * SGH_HROWS * 64; i += 64 * WAVES)
 		(&L.h[0][0][0])[i] = 0;
-	if (tid < SGH_COLS) {
-		L.nz[tid] = 0;
-		L.ns[tid] = 0;
+	for (int i = tid; i < COLS; i += 64 * WAVES) {
+		L.nz[i] = 0;
+		L.ns[i] = 0;
 	}
 	/* no barrier here: sgh_build issues its first loads, then its barrier covers the clear */
+	/* A/B timeline (SG_HIST_DBG=11, NI = 2): per tile, s_memrealtime (100 MHz) at entry,
+	 * after the build barrier and at the end of every wave's finish, written into the
+	 * output buffer as u64 [tile][4] (the image is garbage in this mode) */
+	uint64_t *const tl = (uint64_t *)p.out + (size_t)blockIdx.x * 32;
+	const bool timeline = NI == 2 && p.dbg == 11;
+	if (timeline && tid == 0) {
+		tl[0] = __builtin_amdgcn_s_memrealtime();
+		tl[3] = 0;
+	}
 
-	uint32_t nonzero = 0, nsat = 0;
-	int counted = 0, lo_a, lo_b;
+	uint32_t nonzero[NI], nsat[NI], lo2[NI];
+#pragma unroll
+	for (int i = 0; i < NI; i++)
+		nonzero[i] = nsat[i] = 0;
+	int counted = 0;
 	/* the loading phase at a raised wave priority (SgStackParams::prio, default 1), so the
 	 * waves that keep loads in flight issue ahead of other tiles' finish phases on the same
 	 * SIMD: 4.73 -> 4.58 ms on configs[2]; 2 (priority 3) and 3 (finish raised instead) are
@@ -1088,42 +1305,71 @@ k_stack_hist(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned in
 		__builtin_amdgcn_s_setprio(1);
 	else if (p.prio == 2)
 		__builtin_amdgcn_s_setprio(3);
-	if (interior)
-		sgh_build<false, SGH_NBUF, NORM>(p, L, F, wave, lane, lo_a, lo_b, nonzero, nsat, counted);
-	else
-		sgh_build<true, SGH_NBUF, NORM>(p, L, F, wave, lane, lo_a, lo_b, nonzero, nsat, counted);
+	if (NI == 1) {
+		if (interior)
+			sgh_build<false, SGH_NBUF, NORM, NI>(p, ro, L, F, wave, lane, lo2, nonzero, nsat, counted);
+		else
+			sgh_build<true, SGH_NBUF, NORM, NI>(p, ro, L, F, wave, lane, lo2, nonzero, nsat, counted);
+	} else {
+		if (interior)
+			sgh_build_half<false, NORM, NI, SGH_NB>(p, ro, L, F, wave, lane, lo2, nonzero, nsat, counted);
+		else
+			sgh_build_half<true, NORM, NI, SGH_NB>(p, ro, L, F, wave, lane, lo2, nonzero, nsat, counted);
+	}
 	if (counted) {
-		atomicAdd(&L.nz[lane], (uint32_t)counted - (nonzero & 0xFFFFu));
-		atomicAdd(&L.nz[64 + lane], (uint32_t)counted - (nonzero >> 16));
-		atomicAdd(&L.ns[lane], nsat & 0xFFFFu);
-		atomicAdd(&L.ns[64 + lane], nsat >> 16);
+#pragma unroll
+		for (int i = 0; i < NI; i++) {
+			atomicAdd(&L.nz[128 * i + lane], (uint32_t)counted - (nonzero[i] & 0xFFFFu));
+			atomicAdd(&L.nz[128 * i + 64 + lane], (uint32_t)counted - (nonzero[i] >> 16));
+			atomicAdd(&L.ns[128 * i + lane], nsat[i] & 0xFFFFu);
+			atomicAdd(&L.ns[128 * i + 64 + lane], nsat[i] >> 16);
+		}
 	}
 	__syncthreads();
+	if (timeline && tid == 0)
+		tl[1] = __builtin_amdgcn_s_memrealtime();
 	if (p.prio == 3)
 		__builtin_amdgcn_s_setprio(1);	/* A/B: the finish raised instead */
 	else if (p.prio)
 		__builtin_amdgcn_s_setprio(0);
+	/* column col = 64 g + l of the tile: pixel pair i = g >> 1 of lane l, half g & 1, i.e.
+	 * image column x0 + 128 i + 2 l + (g & 1); its band start is the half of lo2[i][l] */
+	auto col_x = [&](int col) { return x0 + 128 * (col >> 7) + 2 * (col & 63) + ((col >> 6) & 1); };
+	auto col_lo = [&](int col) { return (int)((L.lo2[col >> 7][col & 63] >> (16 * ((col >> 6) & 1))) & 0xFFFFu); };
 	if (REJ == 4) {
 		/* WINSORIZED: the finish is VALU-bound and both lanes of a pair would run the same
-		 * loop, so waves 0 / 1 take one pixel column per lane (the even / odd image columns)
-		 * and waves 2 / 3 leave their SIMD slots to other tiles */
-		if (wave >= 2)
+		 * loop, so half of the waves take one pixel column per lane and the others leave
+		 * their SIMD slots to other tiles */
+		if (wave >= WAVES / 2)
 			return;
-		sgh_finish2<REJ, false>(p, L, 64 * wave + lane, 0, wave ? lo_b : lo_a, R, c, x0 + 2 * lane + wave,
-				redo_count, redo_list);
+		const int col = 64 * wave + lane;
+		sgh_finish2<REJ, false, NI>(p, L, col, 0, col_lo(col), R, c, col_x(col), redo_count, redo_list);
 		return;
 	}
-	/* every wave finishes 32 pixel columns, a lane pair per column; the band start of column
-	 * col is held by lane col & 63 of every wave (each wave computed the centres) */
+	/* every wave finishes 32 pixel columns, a lane pair per column */
 	const int col = 32 * wave + (lane >> 1), half = lane & 1;
-	const int lo = __shfl(wave < 2 ? lo_a : lo_b, col & 63, 64);
-	sgh_finish2<REJ, true>(p, L, col, half, lo, R, c, x0 + 2 * (col & 63) + (col >> 6), redo_count, redo_list);
+	sgh_finish2<REJ, true, NI>(p, L, col, half, col_lo(col), R, c, col_x(col), redo_count, redo_list);
+	if (timeline && lane == 0) {
+		const uint64_t t = __builtin_amdgcn_s_memrealtime();
+		if (wave == 0)
+			tl[2] = t;
+		atomicMax((unsigned long long *)&tl[3], (unsigned long long)t);
+	}
 }
 
-
-template __global__ void k_stack_hist<2, 0>(SgStackParams, unsigned int *, unsigned int *);
-template __global__ void k_stack_hist<2, 1>(SgStackParams, unsigned int *, unsigned int *);
-template __global__ void k_stack_hist<2, 2>(SgStackParams, unsigned int *, unsigned int *);
-template __global__ void k_stack_hist<4, 0>(SgStackParams, unsigned int *, unsigned int *);
-template __global__ void k_stack_hist<4, 1>(SgStackParams, unsigned int *, unsigned int *);
-template __global__ void k_stack_hist<4, 2>(SgStackParams, unsigned int *, unsigned int *);
+template __global__ void k_stack_hist<2, 0, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);
+template __global__ void k_stack_hist<2, 1, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);
+template __global__ void k_stack_hist<2, 2, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);
+template __global__ void k_stack_hist<4, 0, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);
+template __global__ void k_stack_hist<4, 1, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);
+template __global__ void k_stack_hist<4, 2, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);
+template __global__ void k_stack_hist<2, 0, 2>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);
+template __global__ void k_stack_hist<4, 0, 2>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);

@@ -24,7 +24,9 @@ pytestmark = pytest.mark.gpu
 
 def _dev(a):
     import torch
-    return torch.from_numpy(np.ascontiguousarray(a).view(np.int16)).cuda()
+    t = torch.from_numpy(np.ascontiguousarray(a).view(np.int16)).cuda()
+    torch.cuda.synchronize()        # the library runs on its own (non-blocking) stream
+    return t
 
 
 def _oracle(frames, method, rejection, sig, sx, sy, max_thread):
@@ -52,6 +54,7 @@ def _stack_bands(ctx, frames, method, rejection, sig, sx, sy, max_thread, world,
     import torch
     N, C, H, W = frames.shape
     d_out = torch.zeros(C * H * W, dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()        # the zero fill must land before the library's stream writes
     rej = np.zeros((3, 2), np.uint64)
     full = _dev(frames) if resident == "full" else None
     for r in range(world):
@@ -133,6 +136,7 @@ def test_band_stale_state_needs_resident_rows(gpu_ctx):
     b, e = sd.row_band(0, world, H)
     band = _dev(frames[:, :, b:e])
     d_out = torch.zeros(H * W, dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
     desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=sg.SIGMA, sig=(1.0, 1.0), shiftx=z, shifty=z,
                               max_thread=1, max_number_of_rows=H, resident_rows=(b, e))
     with pytest.raises(RuntimeError, match="resident"):
@@ -148,6 +152,7 @@ def test_band_rows_not_resident_rejected(gpu_ctx):
     b, e = 10, 20
     band = _dev(frames[:, :, b:e])          # no halo
     d_out = torch.zeros(H * W, dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
     desc, keep = sg.make_desc(sg.MEAN, N, W, H, C, rejection=sg.SIGMA, shiftx=sx, shifty=sy,
                               max_number_of_rows=H, resident_rows=(b, e))
     with pytest.raises(RuntimeError, match="not all resident"):

@@ -86,6 +86,7 @@ def test_register_raw_shards_reassemble(gpu_ctx, world, ref):
     sel[4, 10:14, 90:94] = 62000
     gx, gy, gq = gpu_ctx.register_dft(sel, ref_image=ref)
     d_sel = torch.from_numpy(sel.view(np.int16)).cuda()
+    torch.cuda.synchronize()
     sx = np.zeros(n, np.int32)
     sy = np.zeros(n, np.int32)
     qraw = np.zeros(n, np.float64)

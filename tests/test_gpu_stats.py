@@ -47,6 +47,7 @@ def test_ikss_matches_oracle(gpu_ctx):
     frames = _frames()
     N, C, H, W = frames.shape
     d = torch.from_numpy(frames.view(np.int16).reshape(-1).copy()).cuda()
+    torch.cuda.synchronize()
     rc, loc, scl = gpu_ctx.frame_stats_ikss(d.data_ptr(), N, C, H, W)
     assert rc == 0, gpu_ctx.error()
     for i in range(N):
@@ -61,6 +62,7 @@ def test_ikss_empty_frame_fails(gpu_ctx):
     frames = np.zeros((2, 1, 16, 16), dtype=np.uint16)
     frames[1, 0, 3, 3] = 9
     d = torch.from_numpy(frames.view(np.int16).reshape(-1).copy()).cuda()
+    torch.cuda.synchronize()
     rc, loc, scl = gpu_ctx.frame_stats_ikss(d.data_ptr(), 2, 1, 16, 16)
     assert rc != 0
     assert orc.statistics_ikss(frames[0])[0] != 0

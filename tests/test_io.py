@@ -131,6 +131,7 @@ def test_load_device(tmp_path, gpu_ctx, name, kw, C):
     with _open(tmp_path, name, kw, frames) as seq:
         stride = C * H * W + 7                          # frames land at a caller stride
         d = torch.zeros(N * stride, dtype=torch.int16, device="cuda")
+        torch.cuda.synchronize()    # the library decodes on its own (non-blocking) stream
         gpu_ctx.load_seq_device(seq, d.data_ptr(), frame_stride=stride)
         got = d.cpu().numpy().view(np.uint16).reshape(N, stride)[:, :C * H * W].reshape(N, C, H, W)
         assert np.array_equal(got, frames)
@@ -161,6 +162,7 @@ def test_stack_from_files(tmp_path, gpu_ctx, fmt):
         assert np.array_equal(rej, rej_ref)
         d = torch.zeros(N * C * H * W, dtype=torch.int16, device="cuda")
         o = torch.zeros(C * H * W, dtype=torch.int16, device="cuda")
+        torch.cuda.synchronize()
         gpu_ctx.load_seq_device(seq, d.data_ptr())
         rej2, _ = gpu_ctx.stack_device(desc, d.data_ptr(), C * H * W, H * W, o.data_ptr(), 0, H)
         assert np.array_equal(o.cpu().numpy().view(np.uint16).reshape(C, H, W), ref)
@@ -221,6 +223,7 @@ def test_debayer_load_device(tmp_path, gpu_ctx, color_id, forced, depth):
         rc, _ = seq.read_region(0, 0, 0, 0, W, 4)
         assert rc != 0                                   # host reads are not provided
         d = torch.zeros(N * 3 * H * W, dtype=torch.int16, device="cuda")
+        torch.cuda.synchronize()    # else the zero fill can land after the decode (flaky zeros)
         gpu_ctx.load_seq_device(seq, d.data_ptr())
         got = d.cpu().numpy().view(np.uint16).reshape(N, 3, H, W)
     for i in range(N):
