@@ -221,8 +221,11 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        # SG_BENCH_REHEARSE=1 (testing only): every rank on cuda:0 over gloo, to rehearse the
+        # multi-rank flow on a one-GPU box; the driver's runs use one GPU per rank over RCCL
+        rehearse = os.environ.get("SG_BENCH_REHEARSE") == "1"
+        torch.cuda.set_device(0 if rehearse else local)
+        dist.init_process_group("gloo" if rehearse else "nccl")
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
@@ -294,8 +297,9 @@ def main():
     elapsed = time.perf_counter() - t0
     if dist:
         import sirilgpu_dist as sd
-        elapsed = sd.max_time(elapsed, dist, device="cuda")
-        rej_tot = sd.sum_counters(rej_tot, dist, device="cuda")
+        cdev = "cpu" if os.environ.get("SG_BENCH_REHEARSE") == "1" else "cuda"
+        elapsed = sd.max_time(elapsed, dist, device=cdev)
+        rej_tot = sd.sum_counters(rej_tot, dist, device=cdev)
     ms_step = elapsed / args.steps * 1e3
     frames_per_s = N * world / (elapsed / args.steps)
     kavg = sum(kms) / len(kms)
