@@ -1,0 +1,24 @@
+#!/bin/bash
+# fast sigma + pipelined median read (SGH_SIGMA_V=3, lib/) against the round-2 loop (lib_ab1):
+# sigma accuracy probe, GPU tests, alternating bench A/B
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+O=gpurun_out/${1:-r2t}
+mkdir -p $O
+timeout -k 10 120 ./tools/sigma_probe > $O/sigma_probe.log 2>&1; rc=$?; cat $O/sigma_probe.log | grep -v amdgpu.ids
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 $O/pytest_gpu.log | cut -c1-300
+[ $rc -eq 0 ] || exit $rc
+run() {  # name, env...
+  local n=$1; shift
+  env "$@" timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline > $O/$n.log 2>&1 || { echo "$n failed"; tail -20 $O/$n.log; exit 3; }
+  echo "$n $(grep '^{' $O/$n.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["kernel_ms"], d["roofline"]["frac"], d["redo_pixels"])')"
+}
+L1=$PWD/siril-0.9_amd/lib_ab1/libsirilgpu.so
+for rep in 1 2 3; do
+  run new_$rep
+  run old_$rep SG_LIB_PATH=$L1
+done
+timeout -k 10 300 python bench.py --workload winsorized-rgb --steps 3 --warmup 1 --no-cpu-baseline > $O/wins_new.log 2>&1 && grep "^{" $O/wins_new.log | cut -c1-160

@@ -243,19 +243,17 @@ __device__ __forceinline__ void sgh_value_at2(const SghPix &P, int g1, int g2, i
 	}
 }
 
+/* ceil(x) clamped to [0, 65536] (NaN -> 0), floor(x) clamped to [-1, 65535] (NaN -> 65535);
+ * written as selects so the pass loop stays one basic block */
 __device__ __forceinline__ int sgh_ceil_clamp(double x) {
-	if (!(x > 0.0))
-		return 0;
-	if (x > 65536.0)
-		return 65536;
-	return (int)ceil(x);
+	double y = x > 0.0 ? x : 0.0;
+	y = y > 65536.0 ? 65536.0 : y;
+	return (int)ceil(y);
 }
 __device__ __forceinline__ int sgh_floor_clamp(double x) {
-	if (!(x < 65535.0))
-		return 65535;
-	if (x < -1.0)
-		return -1;
-	return (int)floor(x);
+	double y = x < 65535.0 ? x : 65535.0;
+	y = y < -1.0 ? -1.0 : y;
+	return (int)floor(y);
 }
 
 /* centre estimate of the two pixels of a lane from 16 samples each (16-bit halves of
@@ -500,6 +498,17 @@ __device__ __forceinline__ uint64_t sgh_x64(uint64_t v) {
 	return (uint64_t)sgh_x((uint32_t)v) | ((uint64_t)sgh_x((uint32_t)(v >> 32)) << 32);
 }
 
+/* sum over the wave (all lanes active): row_shr 1, 2, 4, 8 with zero fill leave each 16-lane
+ * row's total in its lane 15 */
+__device__ __forceinline__ uint32_t sgh_wave_sum(uint32_t x) {
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);
+	return (uint32_t)__builtin_amdgcn_readlane((int)x, 15) + (uint32_t)__builtin_amdgcn_readlane((int)x, 31) +
+		(uint32_t)__builtin_amdgcn_readlane((int)x, 47) + (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
 /* value at global rank g (single rank) */
 __device__ __forceinline__ int sgh_value_at1(const SghPix &P, int g) {
 	const int r = g - P.nz;
@@ -511,6 +520,154 @@ __device__ __forceinline__ int sgh_value_at1(const SghPix &P, int g) {
 	uint32_t d[SGH_GRP];
 	sgh_grp(P, grp, d);
 	return in ? sgh_locate(P, grp, d, sgh_sel(P.pc, grp), (uint32_t)r) : (r < 0 ? 0 : 65535);
+}
+
+/* sigma = sqrt(num / (n (n - 1))) of the kept set (0 for num <= 0), as 2 num h with
+ * h = 0.5 / sqrt(num n (n - 1)) refined twice from the hardware v_rsq_f64 (coupled Newton
+ * steps on s ~ sqrt(x), h ~ 0.5 / sqrt(x): an initial relative error e becomes ~2 e^4, so a
+ * few ulp in all), 8 dependent fp64 operations instead of the ~26 of an IEEE division and
+ * square root.  The decisions keep a rounding band of 1e-13 relative (SGH_BAND), ~500 times
+ * the error.  num < 2^53: num <= n^2 65535^2 / 4. */
+__device__ __forceinline__ double sgh_sigma_fast(long long num, int n) {
+	const double nd = (double)(num > 0 ? num : 1);
+	const double x = nd * ((double)n * (double)(n - 1));
+	const double y = __builtin_amdgcn_rsq(x);
+	double h = 0.5 * y, s = x * y;
+	double r = fma(-s, h, 0.5);
+	s = fma(s, r, s);
+	h = fma(h, r, h);
+	r = fma(-s, h, 0.5);
+	h = fma(h, r, h);
+	const double sig = (nd + nd) * h;
+	return num > 0 ? sig : 0.0;
+}
+
+/* a median rank query split in two: the group read is issued one pass ahead (the next
+ * pass's ranks are known once the clip counts are), the locate runs when the value is needed */
+struct SghMed {
+	int r, grp;
+	uint32_t d[SGH_GRP];
+};
+__device__ __forceinline__ void sgh_med_issue(const SghPix &P, int g, SghMed &m) {
+	m.r = g - P.nz;
+	int grp = 0;
+#pragma unroll
+	for (int k = 1; k < SGH_NGRP; k++)
+		grp += (int)P.pc[k] <= m.r ? 1 : 0;
+	m.grp = grp;
+	sgh_grp(P, grp, m.d);
+}
+__device__ __forceinline__ int sgh_med_value(const SghPix &P, const SghMed &m) {
+	const bool in = m.r >= 0 && m.r < P.nb;
+	const int v = sgh_locate(P, m.grp, m.d, sgh_sel(P.pc, m.grp), (uint32_t)m.r);
+	return in ? v : (m.r < 0 ? 0 : 65535);
+}
+
+#ifndef SGH_SIGMA_V
+#define SGH_SIGMA_V 3
+#endif
+
+/* sgh_sigma2 restructured for the critical path of a pass: the median's group read is
+ * issued during the previous pass (before its moments), sigma comes from sgh_sigma_fast, and
+ * the clamps, moments and their selects are straight-line code, so one pass is one basic
+ * block the scheduler can overlap (fp64 chain against LDS latency).  Same decisions, same
+ * exits as sgh_sigma2. */
+__device__ __forceinline__ int sgh_sigma3(const SghPix &P, int N, double sl, double sh, int half, uint16_t *value,
+		uint32_t *rlo_out, uint32_t *rhi_out, int &passes) {
+	int A = 0, B = 65535, n = N, r = 0, nrem;
+	SghM MA = {0, 0, 0}, MB = P.T;
+	uint32_t rlo = 0, rhi = 0;
+	SghMed md;
+	sgh_med_issue(P, half ? N / 2 : (N - 1) / 2, md);
+	do {
+		const long long S = MB.s - MA.s;
+		const unsigned long long SS = MB.ss - MA.ss;
+		const long long num = (long long)n * (long long)SS - S * S;
+		const bool exact0 = (num == 0);
+		const double sigma = sgh_sigma_fast(num, n);
+		const int g1 = MA.c + (n - 1) / 2, g2 = MA.c + n / 2;
+		const int mv = sgh_med_value(P, md);
+		const int mo = (int)sgh_x((uint32_t)mv);
+		const int m1 = half ? mo : mv, m2 = half ? mv : mo;
+		const double median = (g1 == g2) ? (double)m1 : (double)(m1 + m2) / 2.0;
+		const double tl = sl * sigma, th = sh * sigma;
+		const double blo = median - tl, bhi = median + th;
+		const double tol = exact0 ? 0.0 : SGH_BAND * (fabs(median) + fabs(tl) + fabs(th) + 1.0);
+		int a = sgh_ceil_clamp(blo - tol);
+		a = a < A ? A : a;
+		int bt = sgh_floor_clamp(bhi + tol);
+		bt = bt > B ? B : bt;
+		SghQ q;
+		sgh_q_load(P, half ? bt : a - 1, q);
+		const int cm = sgh_q_count(P, q), co = (int)sgh_x((uint32_t)cm);
+		const int cnt_a = half ? co : cm, cnt_bt = half ? cm : co;
+		uint32_t amb = 0;
+		if (!exact0) {
+			if (!half) {
+				int amb1 = sgh_floor_clamp(blo + tol);
+				amb1 = amb1 > B ? B : amb1;
+				amb = (a <= amb1 && sgh_cnt_le(P, amb1) - cnt_a > 0) ? 1u : 0u;
+			} else {
+				int amb0 = sgh_ceil_clamp(bhi - tol);
+				amb0 = amb0 < A ? A : amb0;
+				amb = (amb0 <= bt && cnt_bt - sgh_cnt_le(P, amb0 - 1) > 0) ? 1u : 0u;
+			}
+		}
+		if (amb | sgh_x(amb))
+			return 1;
+		const int L = cnt_a - MA.c, H = MB.c - cnt_bt;
+		if (L + H > n)
+			return 1;
+		/* `if (N - r <= 4) break;` inside the clipping loop (:1684) */
+		const int need = n - 4 - r;
+		int fb = -1;
+		if (need <= 0)
+			fb = 0;
+		else if (L >= need)
+			fb = need - 1;
+		else if (L + H >= need)
+			fb = (n - H) + (need - L) - 1;
+		if (fb >= 0 && fb < n - 1)
+			return 1;
+		/* the next pass's median ranks: kept count n - L - H starting at rank cnt_a (or MA.c) */
+		{
+			const int ca = L ? cnt_a : MA.c, nn = n - L - H;
+			sgh_med_issue(P, ca + (half ? nn / 2 : (nn - 1) / 2), md);
+		}
+		/* moments of this lane's bound; field-wise selects (a select of whole structs becomes
+		 * a scratch access) */
+		const SghM Mq = sgh_q_moments(P, q);
+		const bool mine = half ? (H != 0) : (L != 0);
+		const int mc = mine ? Mq.c : (half ? MB.c : MA.c);
+		const long long ms = mine ? Mq.s : (half ? MB.s : MA.s);
+		const unsigned long long mss = mine ? Mq.ss : (half ? MB.ss : MA.ss);
+		const int oc = (int)sgh_x((uint32_t)mc);
+		const long long os = (long long)sgh_x64((uint64_t)ms);
+		const unsigned long long oss = sgh_x64(mss);
+		if (L) {
+			A = a;
+			MA.c = half ? oc : mc;
+			MA.s = half ? os : ms;
+			MA.ss = half ? oss : mss;
+		}
+		if (H) {
+			B = bt;
+			MB.c = half ? mc : oc;
+			MB.s = half ? ms : os;
+			MB.ss = half ? mss : oss;
+		}
+		rlo += L;
+		rhi += H;
+		r += L + H;
+		nrem = L + H;
+		n -= nrem;
+		passes++;
+	} while (nrem > 0 && n > 3);
+	const long long tot = (MB.s - MA.s) + (long long)n * P.lo;
+	*value = sg_round_to_WORD((double)tot / (double)n);
+	*rlo_out = rlo;
+	*rhi_out = rhi;
+	return SG_CLS_OK;
 }
 
 /* the SIGMA loop of sgh_sigma, split over a lane pair: half 0 owns the low side (median
@@ -943,6 +1100,8 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 			P.T.ss = (unsigned long long)ss32 + P.Z.ss + (unsigned long long)(ds * ds) * (unsigned long long)P.ns;
 			if (REJ == 4 || !PAIR)
 				cls = sgh_winsorized(P, N, p.sig0, p.sig1, &value, &rlo, &rhi);
+			else if (SGH_SIGMA_V == 3)
+				cls = sgh_sigma3(P, N, p.sig0, p.sig1, half, &value, &rlo, &rhi, passes);
 			else
 				cls = sgh_sigma2(P, N, p.sig0, p.sig1, half, &value, &rlo, &rhi, passes);
 		}
@@ -973,11 +1132,10 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 			tw[2] = (uint64_t)pmax | ((uint64_t)psum << 16);
 		}
 	}
-	unsigned long long a = rlo, b = rhi;
-	for (int o = 32; o > 0; o >>= 1) {
-		a += __shfl_down(a, o, 64);
-		b += __shfl_down(b, o, 64);
-	}
+	/* wave sums of the rejection counts (each lane's count <= N, so a wave's sum of 32 pixel
+	 * counts fits 32 bits for any N the kernel takes): DPP row sums + 4 readlanes instead of
+	 * six dependent ds_bpermute rounds */
+	const unsigned long long a = sgh_wave_sum(rlo), b = sgh_wave_sum(rhi);
 	if (lane == 0 && (a | b)) {
 		unsigned long long *sh = p.rej + ((size_t)((blockIdx.x * 8 + (col >> 5)) % SG_REJ_SHARDS) * 6 + c * 2);
 		atomicAdd(sh, a);
@@ -1092,7 +1250,8 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, const SghRo &r
 	}
 }
 
-/* the same build with 8-frame half blocks (NI = 2: two dword loads per lane and frame):
+/* the same build with 8-frame half blocks (the default for NI = 1, SGH_HALF1; NI = 2 loads
+ * two dwords per lane and frame):
  * wave w bins the 16-frame blocks w, w + WAVES, ... in order, each as two halves; NB blocks
  * (2 NB half buffers) are in flight, so while one half is binned 2 NB - 1 halves keep
  * loading (with two 8-wave workgroups per CU, one workgroup's loads must carry the CU while
@@ -1100,6 +1259,13 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, const SghRo &r
  * Wave 0's first block (frames 0..15) is the centre sample. */
 #ifndef SGH_NB
 #define SGH_NB 1	/* 2: 4.85 vs 4.62 ms (NI = 2, scripts/gpu_r2i.sh) */
+#endif
+/* NI = 1 also streams half blocks (scripts/gpu_r2u.sh, two alternating rounds on one box:
+ * 4.111-4.119 ms against 4.179-4.186 for the 16-frame build, NB = 1 and 2 equal; the 16-frame
+ * build with a third buffer 4.23-4.24): the straight-line steady loop with sched_barriers keeps
+ * every refill right behind its binning */
+#ifndef SGH_HALF1
+#define SGH_HALF1 1
 #endif
 
 template <bool EDGE, int NORM, int NI, int NB>
@@ -1305,7 +1471,7 @@ k_stack_hist(SgStackParams p, const int *__restrict__ tab, const int4 *__restric
 		__builtin_amdgcn_s_setprio(1);
 	else if (p.prio == 2)
 		__builtin_amdgcn_s_setprio(3);
-	if (NI == 1) {
+	if (NI == 1 && !SGH_HALF1) {
 		if (interior)
 			sgh_build<false, SGH_NBUF, NORM, NI>(p, ro, L, F, wave, lane, lo2, nonzero, nsat, counted);
 		else
