@@ -128,8 +128,43 @@ __device__ __forceinline__ void sgh_dw_moments(uint32_t dd, uint32_t &c, uint32_
 	ss = __builtin_amdgcn_udot2(__builtin_bit_cast(sgh_u16x2v, hi), (sgh_u16x2v){q2, q3}, ss, false);
 }
 
+/* the same moments with the squared weights split into bytes: j = 4 K + b < 32, j^2 < 1024,
+ * so sum j^2 c_j = sum lo8(j^2) c_j + 256 sum hi8(j^2) c_j, two u8 dot products per dword
+ * (the high one only for K >= 4, where j^2 >= 256) instead of two byte unpacks and two u16
+ * dot products: 29 instead of 48 VALU per group */
+template <int K>
+__device__ __forceinline__ void sgh_dw_moments_b(uint32_t dd, uint32_t &c, uint32_t &s, uint32_t &sl, uint32_t &sh) {
+	constexpr uint32_t j0 = 4 * K, j1 = j0 + 1, j2 = j0 + 2, j3 = j0 + 3;
+	constexpr uint32_t w1 = j0 | (j1 << 8) | (j2 << 16) | (j3 << 24);
+	constexpr uint32_t wl = ((j0 * j0) & 0xFFu) | (((j1 * j1) & 0xFFu) << 8) | (((j2 * j2) & 0xFFu) << 16) |
+		(((j3 * j3) & 0xFFu) << 24);
+	constexpr uint32_t wh = ((j0 * j0) >> 8) | (((j1 * j1) >> 8) << 8) | (((j2 * j2) >> 8) << 16) | (((j3 * j3) >> 8) << 24);
+	c = __builtin_amdgcn_sad_u8(dd, 0u, c);
+	s = __builtin_amdgcn_udot4(dd, w1, s, false);
+	sl = __builtin_amdgcn_udot4(dd, wl, sl, false);
+	if (wh != 0u)
+		sh = __builtin_amdgcn_udot4(dd, wh, sh, false);
+}
+
+#ifndef SGH_MOM_BYTES
+#define SGH_MOM_BYTES 1
+#endif
+
 __device__ __forceinline__ void sgh_grp_moments(const uint32_t (&d)[SGH_GRP], uint32_t &c, uint32_t &s, uint32_t &ss) {
 	static_assert(SGH_GRP == 8, "unrolled for 8 dwords");
+	if (SGH_MOM_BYTES) {
+		uint32_t sl = 0, sh = 0;
+		sgh_dw_moments_b<0>(d[0], c, s, sl, sh);
+		sgh_dw_moments_b<1>(d[1], c, s, sl, sh);
+		sgh_dw_moments_b<2>(d[2], c, s, sl, sh);
+		sgh_dw_moments_b<3>(d[3], c, s, sl, sh);
+		sgh_dw_moments_b<4>(d[4], c, s, sl, sh);
+		sgh_dw_moments_b<5>(d[5], c, s, sl, sh);
+		sgh_dw_moments_b<6>(d[6], c, s, sl, sh);
+		sgh_dw_moments_b<7>(d[7], c, s, sl, sh);
+		ss += sl + (sh << 8);
+		return;
+	}
 	sgh_dw_moments<0>(d[0], c, s, ss);
 	sgh_dw_moments<1>(d[1], c, s, ss);
 	sgh_dw_moments<2>(d[2], c, s, ss);
@@ -1498,6 +1533,27 @@ k_stack_hist(SgStackParams p, const int *__restrict__ tab, const int4 *__restric
 		__builtin_amdgcn_s_setprio(1);	/* A/B: the finish raised instead */
 	else if (p.prio)
 		__builtin_amdgcn_s_setprio(0);
+#if defined(SGH_PROBE_VALU) || defined(SGH_PROBE_SLEEP)
+	{	/* sensitivity probes (A/B builds only): extra finish VALU, or extra finish latency */
+#ifdef SGH_PROBE_VALU
+		float z0 = (float)lane, z1 = z0 + 1.f, z2 = z0 + 2.f, z3 = z0 + 3.f;
+#pragma unroll 1
+		for (int k = 0; k < SGH_PROBE_VALU / 16; k++) {
+#pragma unroll
+			for (int u = 0; u < 4; u++) {
+				z0 = z0 * 1.0001f + 0.5f;
+				z1 = z1 * 1.0001f + 0.5f;
+				z2 = z2 * 1.0001f + 0.5f;
+				z3 = z3 * 1.0001f + 0.5f;
+			}
+		}
+		if (z0 + z1 + z2 + z3 == 1.2345f)
+			p.out[0] = 1;
+#else
+		__builtin_amdgcn_s_sleep(SGH_PROBE_SLEEP);
+#endif
+	}
+#endif
 	/* column col = 64 g + l of the tile: pixel pair i = g >> 1 of lane l, half g & 1, i.e.
 	 * image column x0 + 128 i + 2 l + (g & 1); its band start is the half of lo2[i][l] */
 	auto col_x = [&](int col) { return x0 + 128 * (col >> 7) + 2 * (col & 63) + ((col >> 6) & 1); };
