@@ -89,7 +89,11 @@ struct SghPix {
 	int nz, ns, nb;		/* zeros, 65535s, band samples (nz + nb + ns == N) */
 	int col;
 	const uint32_t *hb;	/* the tile's histogram h[0][0][0] */
-	uint32_t pc[SGH_NGRP], ps[SGH_NGRP], pss[SGH_NGRP];	/* band prefix before group g */
+	/* band prefix (count, sum, sum of squares of t) before group g, kept at index g ^ hx: a lane
+	 * of a pair holds its own 4 groups first (hx = 4 for the high half), so the exchange of
+	 * the halves' prefixes needs no reordering */
+	uint32_t pc[SGH_NGRP], ps[SGH_NGRP], pss[SGH_NGRP];
+	int hx;
 	SghM Z;			/* moments of the zeros */
 	SghM T;			/* moments of all samples */
 };
@@ -101,6 +105,19 @@ __device__ __forceinline__ uint32_t sgh_sel(const uint32_t (&t)[SGH_NGRP], int k
 	const uint32_t a0 = b0 ? t[1] : t[0], a1 = b0 ? t[3] : t[2], a2 = b0 ? t[5] : t[4], a3 = b0 ? t[7] : t[6];
 	const uint32_t c0 = b1 ? a1 : a0, c1 = b1 ? a3 : a2;
 	return b2 ? c1 : c0;
+}
+/* prefix entry of group g */
+__device__ __forceinline__ uint32_t sgh_pre(const SghPix &P, const uint32_t (&t)[SGH_NGRP], int g) {
+	return sgh_sel(t, g ^ P.hx);
+}
+/* the band group holding band rank r (0 for r < 0): the number of groups g >= 1 whose
+ * prefix count is <= r, counted over the 8 entries in any order (group 0's prefix is 0) */
+__device__ __forceinline__ int sgh_grp_of(const SghPix &P, int r) {
+	int grp = r >= 0 ? -1 : 0;
+#pragma unroll
+	for (int k = 0; k < SGH_NGRP; k++)
+		grp += (int)P.pc[k] <= r ? 1 : 0;
+	return grp;
 }
 
 __device__ __forceinline__ void sgh_grp(const SghPix &P, int g, uint32_t (&d)[SGH_GRP]) {
@@ -179,32 +196,38 @@ __device__ __forceinline__ void sgh_grp_moments(const uint32_t (&d)[SGH_GRP], ui
  * read once; the count is cheap and the moments are only formed for the passes that
  * actually remove samples */
 struct SghQ {
-	int v, t, g;
-	uint32_t d[SGH_GRP];	/* the group's dwords, masked to bins <= t */
+	int v, t, g, kb;
+	uint32_t d[SGH_GRP];	/* the group's dwords below the boundary dword kb, others 0 */
+	uint32_t bd;		/* the boundary dword (group dword kb, the one holding bin t), masked to bins <= t */
 };
 
+/* the group is read as 8 dwords plus the boundary dword once more (one more LDS read, no
+ * select tree): dwords k < kb are kept whole with one compare + select each, the boundary
+ * dword is masked to its bins <= t and enters the sums separately */
 __device__ __forceinline__ void sgh_q_load(const SghPix &P, int v, SghQ &q) {
 	int t = v - P.lo;
 	t = t < -1 ? -1 : (t > SGH_BINS - 1 ? SGH_BINS - 1 : t);
 	q.v = v;
 	q.t = t;
-	q.g = (t < 0 ? 0 : t) >> 5;
+	const int tc = t < 0 ? 0 : t;
+	q.g = tc >> 5;
 	sgh_grp(P, q.g, q.d);
-	const int jt = t >> 2;	/* -1 for t = -1: nothing counted */
-	const int sh = ((t & 3) + 1) * 8;
-	const uint32_t mt = sh >= 32 ? 0xFFFFFFFFu : ((1u << sh) - 1u);
+	q.bd = P.hb[((P.col >> 6) * SGH_HROWS + (tc >> 2)) * 64 + (P.col & 63)];
+	const int kb = (t >> 2) - q.g * SGH_GRP;	/* -1 for t = -1: nothing counted */
+	q.kb = kb;
 #pragma unroll
-	for (int k = 0; k < SGH_GRP; k++) {
-		const int j = q.g * SGH_GRP + k;
-		q.d[k] &= (j < jt ? 0xFFFFFFFFu : (j == jt ? mt : 0u));
-	}
+	for (int k = 0; k < SGH_GRP; k++)
+		q.d[k] = k < kb ? q.d[k] : 0u;
+	const uint32_t mt = 0xFFFFFFFFu >> (24 - 8 * (t & 3));
+	q.bd = t >= 0 ? (q.bd & mt) : 0u;
 }
 
 __device__ __forceinline__ int sgh_q_count(const SghPix &P, const SghQ &q) {
-	uint32_t c = sgh_sel(P.pc, q.g);
+	uint32_t c = sgh_pre(P, P.pc, q.g);
 #pragma unroll
 	for (int k = 0; k < SGH_GRP; k++)
 		c = __builtin_amdgcn_sad_u8(q.d[k], 0u, c);
+	c = __builtin_amdgcn_sad_u8(q.bd, 0u, c);
 	if (q.v < 0)
 		return 0;
 	if (q.v >= 65535)
@@ -215,11 +238,20 @@ __device__ __forceinline__ int sgh_q_count(const SghPix &P, const SghQ &q) {
 __device__ __forceinline__ SghM sgh_q_moments(const SghPix &P, const SghQ &q) {
 	uint32_t c = 0, s = 0, ss = 0;
 	sgh_grp_moments(q.d, c, s, ss);
+	/* the boundary dword: bins j = 4 kb + b, j^2 = (4 kb)^2 + 2 (4 kb) b + b^2 */
+	const uint32_t cb = __builtin_amdgcn_sad_u8(q.bd, 0u, 0u);
+	const uint32_t sb = __builtin_amdgcn_udot4(q.bd, 0x03020100u, 0u, false);
+	const uint32_t qb = __builtin_amdgcn_udot4(q.bd, 0x09040100u, 0u, false);
+	/* 24-bit multiplies throughout (all factors < 2^24: k4 <= 28, b0 <= 224, c <= 32 * 255) */
+	const uint32_t k4 = 4u * (uint32_t)(q.kb < 0 ? 0 : q.kb);
+	ss += qb + __umul24(2u * k4, sb) + __umul24(__umul24(k4, k4), cb);
+	s += sb + __umul24(k4, cb);
+	c += cb;
 	const uint32_t b0 = (uint32_t)q.g * (4u * SGH_GRP);	/* first bin of the group */
 	SghM m;
-	m.c = P.nz + (int)(sgh_sel(P.pc, q.g) + c);
-	m.s = P.Z.s + (long long)(sgh_sel(P.ps, q.g) + s + b0 * c);
-	m.ss = P.Z.ss + (unsigned long long)(sgh_sel(P.pss, q.g) + ss + 2u * b0 * s + b0 * b0 * c);
+	m.c = P.nz + (int)(sgh_pre(P, P.pc, q.g) + c);
+	m.s = P.Z.s + (long long)(sgh_pre(P, P.ps, q.g) + s + __umul24(b0, c));
+	m.ss = P.Z.ss + (unsigned long long)(sgh_pre(P, P.pss, q.g) + ss + __umul24(2u * b0, s) + __umul24(__umul24(b0, b0), c));
 	if (q.v < 0) {
 		m.c = 0;
 		m.s = 0;
@@ -258,21 +290,16 @@ __device__ __forceinline__ int sgh_locate(const SghPix &P, int g, const uint32_t
 __device__ __forceinline__ void sgh_value_at2(const SghPix &P, int g1, int g2, int &m1, int &m2) {
 	const int r1 = g1 - P.nz, r2 = g2 - P.nz;
 	const bool in1 = r1 >= 0 && r1 < P.nb, in2 = r2 >= 0 && r2 < P.nb;
-	int grp1 = 0, grp2 = 0;
-#pragma unroll
-	for (int k = 1; k < SGH_NGRP; k++) {
-		grp1 += (int)P.pc[k] <= r1 ? 1 : 0;
-		grp2 += (int)P.pc[k] <= r2 ? 1 : 0;
-	}
+	const int grp1 = sgh_grp_of(P, r1), grp2 = sgh_grp_of(P, r2);
 	uint32_t d[SGH_GRP];
 	sgh_grp(P, grp1, d);
-	const uint32_t base1 = sgh_sel(P.pc, grp1);
+	const uint32_t base1 = sgh_pre(P, P.pc, grp1);
 	m1 = in1 ? sgh_locate(P, grp1, d, base1, (uint32_t)r1) : (r1 < 0 ? 0 : 65535);
 	if (in2 && grp2 == grp1) {
 		m2 = sgh_locate(P, grp1, d, base1, (uint32_t)r2);
 	} else if (in2) {
 		sgh_grp(P, grp2, d);
-		m2 = sgh_locate(P, grp2, d, sgh_sel(P.pc, grp2), (uint32_t)r2);
+		m2 = sgh_locate(P, grp2, d, sgh_pre(P, P.pc, grp2), (uint32_t)r2);
 	} else {
 		m2 = r2 < 0 ? 0 : 65535;
 	}
@@ -548,13 +575,10 @@ __device__ __forceinline__ uint32_t sgh_wave_sum(uint32_t x) {
 __device__ __forceinline__ int sgh_value_at1(const SghPix &P, int g) {
 	const int r = g - P.nz;
 	const bool in = r >= 0 && r < P.nb;
-	int grp = 0;
-#pragma unroll
-	for (int k = 1; k < SGH_NGRP; k++)
-		grp += (int)P.pc[k] <= r ? 1 : 0;
+	const int grp = sgh_grp_of(P, r);
 	uint32_t d[SGH_GRP];
 	sgh_grp(P, grp, d);
-	return in ? sgh_locate(P, grp, d, sgh_sel(P.pc, grp), (uint32_t)r) : (r < 0 ? 0 : 65535);
+	return in ? sgh_locate(P, grp, d, sgh_pre(P, P.pc, grp), (uint32_t)r) : (r < 0 ? 0 : 65535);
 }
 
 /* sigma = sqrt(num / (n (n - 1))) of the kept set (0 for num <= 0), as 2 num h with
@@ -585,16 +609,12 @@ struct SghMed {
 };
 __device__ __forceinline__ void sgh_med_issue(const SghPix &P, int g, SghMed &m) {
 	m.r = g - P.nz;
-	int grp = 0;
-#pragma unroll
-	for (int k = 1; k < SGH_NGRP; k++)
-		grp += (int)P.pc[k] <= m.r ? 1 : 0;
-	m.grp = grp;
-	sgh_grp(P, grp, m.d);
+	m.grp = sgh_grp_of(P, m.r);
+	sgh_grp(P, m.grp, m.d);
 }
 __device__ __forceinline__ int sgh_med_value(const SghPix &P, const SghMed &m) {
 	const bool in = m.r >= 0 && m.r < P.nb;
-	const int v = sgh_locate(P, m.grp, m.d, sgh_sel(P.pc, m.grp), (uint32_t)m.r);
+	const int v = sgh_locate(P, m.grp, m.d, sgh_pre(P, P.pc, m.grp), (uint32_t)m.r);
 	return in ? v : (m.r < 0 ? 0 : 65535);
 }
 
@@ -1084,30 +1104,56 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 		for (int j = 0; j < SGH_GRP; j++)
 			d[j] = hc[64 * (g * SGH_GRP + j)];
 		sgh_grp_moments(d, cc, s, ss);
+		/* 24-bit multiplies (v_mul_u32_u24, full rate): b0 <= 224, cc <= 32 * 255, s < 2^18 */
 		const uint32_t b0 = (uint32_t)g * (4u * SGH_GRP);
 		gc[k] = cc;
-		gs[k] = s + b0 * cc;
-		gss[k] = ss + 2u * b0 * s + b0 * b0 * cc;
+		gs[k] = s + __umul24(b0, cc);
+		gss[k] = ss + __umul24(2u * b0, s) + __umul24(__umul24(b0, b0), cc);
 	}
 	SghPix P;
-	uint32_t cum = 0, s32 = 0, ss32 = 0;
+	uint32_t cum = 0, s32 = 0, ss32 = 0;	/* band totals */
+	if constexpr (PAIR) {
+		/* exclusive prefix of the lane's own 4 groups, offset by the low half's totals in the
+		 * high half; the partner's 4 entries follow at index 4..7 (SghPix::hx) */
+		uint32_t oc = 0, os = 0, oss = 0;
 #pragma unroll
-	for (int g = 0; g < SGH_NGRP; g++) {
-		P.pc[g] = cum;
-		P.ps[g] = s32;
-		P.pss[g] = ss32;
-		if constexpr (PAIR) {
-			const int k = g % (SGH_NGRP / 2);
-			const bool mine = (g >= SGH_NGRP / 2) == (half != 0);
-			const uint32_t oc = sgh_x(gc[k]), os = sgh_x(gs[k]), oss = sgh_x(gss[k]);
-			cum += mine ? gc[k] : oc;
-			s32 += mine ? gs[k] : os;
-			ss32 += mine ? gss[k] : oss;
-		} else {
+		for (int k = 0; k < NG; k++) {
+			P.pc[k] = oc;
+			P.ps[k] = os;
+			P.pss[k] = oss;
+			oc += gc[k];
+			os += gs[k];
+			oss += gss[k];
+		}
+		const uint32_t xc = sgh_x(oc), xs = sgh_x(os), xss = sgh_x(oss);
+		const uint32_t fc = half ? xc : 0u, fs = half ? xs : 0u, fss = half ? xss : 0u;
+#pragma unroll
+		for (int k = 0; k < NG; k++) {
+			P.pc[k] += fc;
+			P.ps[k] += fs;
+			P.pss[k] += fss;
+		}
+#pragma unroll
+		for (int k = 0; k < NG; k++) {
+			P.pc[NG + k] = sgh_x(P.pc[k]);
+			P.ps[NG + k] = sgh_x(P.ps[k]);
+			P.pss[NG + k] = sgh_x(P.pss[k]);
+		}
+		cum = oc + xc;
+		s32 = os + xs;
+		ss32 = oss + xss;
+		P.hx = half ? NG : 0;
+	} else {
+#pragma unroll
+		for (int g = 0; g < SGH_NGRP; g++) {
+			P.pc[g] = cum;
+			P.ps[g] = s32;
+			P.pss[g] = ss32;
 			cum += gc[g];
 			s32 += gs[g];
 			ss32 += gss[g];
 		}
+		P.hx = 0;
 	}
 	const int oob = (int)hc[64 * SGH_DW];
 	P.lo = lo;
