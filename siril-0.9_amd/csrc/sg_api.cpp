@@ -414,11 +414,12 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		const int ntx = (W + SG_TILE_W - 1) / SG_TILE_W;
 		const size_t nblk = (size_t)ntx * nrows * C;
 		const size_t lds = (size_t)N * SG_STAGE_STRIDE * 2;
-		/* histogram fast path (sg_stack_hist.hip): SIGMA / WINSORIZED, any normalisation, N >= 16 */
+		/* histogram fast path (sg_stack_hist.hip): SIGMA / WINSORIZED, any normalisation,
+		 * 16 <= N <= 65535 (per-lane zero / 65535 counters are 16-bit halves) */
 		const int path = d->kernel_path;
 		const bool hist = path != SG_PATH_SORTED && d->method == SG_STACK_MEAN &&
 			(d->rejection == SG_SIGMA || d->rejection == SG_WINSORIZED) &&
-			N >= 16 && hist_addr_ok;
+			N >= 16 && N <= 65535 && hist_addr_ok;
 		if (hist) {
 			HIPCHK(ensure(dv.redo, sizeof(unsigned int) * (npix_launch + 16)));
 			unsigned int *redo_count = (unsigned int *)dv.redo.p;

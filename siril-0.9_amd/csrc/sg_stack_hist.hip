@@ -543,8 +543,10 @@ __device__ __forceinline__ void sgh_bin_pair(uint32_t *h, uint32_t l4, uint32_t 
 	const uint32_t i0 = 1u << (t8 & 31u), i1 = 1u << ((t8 >> 16) & 31u);
 	atomicAdd((uint32_t *)((char *)h + a0), i0);
 	atomicAdd((uint32_t *)((char *)h + sizeof(uint32_t) * SGH_HROWS * 64 + a1), i1);
-	nonzero = sgh_pk_add(nonzero, sgh_pk_min(vv, 0x00010001u));
-	nsat = sgh_pk_add(nsat, sgh_pk_sub_sat(vv, 0xFFFEFFFEu));
+	/* plain u32 adds (no carry crosses the halves: a lane counts at most N / 4 frames), so
+	 * the compiler folds the adds of consecutive frames into v_add3_u32 */
+	nonzero += sgh_pk_min(vv, 0x00010001u);
+	nsat += sgh_pk_sub_sat(vv, 0xFFFEFFFEu);
 }
 
 /* ------------------------------------------------------------------------------------
