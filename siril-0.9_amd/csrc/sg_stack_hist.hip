@@ -377,6 +377,7 @@ struct SghFrame {
 	int rw2;			/* R * W * 2 */
 	int w2;				/* W * 2 */
 	uint32_t xa2;			/* 2 * x of the lane's first pixel */
+	uint32_t x02;			/* 2 * x0, the tile's first column */
 };
 
 /* shift table of the 16 frames f0..f0+15 (f0 % 16 == 0): c1 = shifty*W*2 + 2*shiftx (one
@@ -453,7 +454,17 @@ __device__ __forceinline__ void sgh_loadblk(const SghFrame &F, const SghTab16 &T
 				off = bada ? (badb ? 0x80000000u : off + 2u) : (badb ? off - 2u : off);
 				fix[i] |= ((bada && !badb) ? 1u : ((!bada && badb) ? 2u : ((bada && badb) ? 3u : 0u))) << (2 * m);
 			}
-			dst[m][i] = __builtin_amdgcn_raw_buffer_load_b32(sgh_rsrc(b, nrec), (int)off, 0, 0);
+			/* interior tiles: the frame's term (R - sy) W 2 + 2 (x0 - sx), the shifted start of
+			 * the tile's row segment, goes in the SGPR offset and the lane's voffset 4 l + 256 i
+			 * stays fixed (no VALU per load).  The segment start is >= 0 for a row inside the
+			 * frame (x0 >= max |sx| in an interior tile) and < 0 for a row above it; gfx950
+			 * bounds-checks the unsigned sum voffset + soffset without wrapping
+			 * (tools/soffset_probe.hip), so the latter (2^32 + start as unsigned) reads 0 */
+			if (EDGE)
+				dst[m][i] = __builtin_amdgcn_raw_buffer_load_b32(sgh_rsrc(b, nrec), (int)off, 0, 0);
+			else
+				dst[m][i] = __builtin_amdgcn_raw_buffer_load_b32(sgh_rsrc(b, nrec), (int)(xa2 - F.x02),
+						(int)(k + F.x02), 0);
 		}
 		b += F.fstride2;
 	}
@@ -1523,6 +1534,7 @@ k_stack_hist(SgStackParams p, const int *__restrict__ tab, const int4 *__restric
 	F.w2 = p.W * 2;
 	F.rw2 = R * p.W * 2;
 	F.xa2 = (uint32_t)(x0 + 2 * lane) * 2u;
+	F.x02 = (uint32_t)x0 * 2u;
 
 	for (int i = tid; i < 2 * NI * SGH_HROWS * 64; i += 64 * WAVES)
 		(&L.h[0][0][0])[i] = 0;
