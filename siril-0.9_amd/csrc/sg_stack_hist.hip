@@ -167,18 +167,20 @@ __device__ __forceinline__ void sgh_dw_moments_b(uint32_t dd, uint32_t &c, uint3
 #define SGH_MOM_BYTES 1
 #endif
 
+template <bool COUNT = true>
 __device__ __forceinline__ void sgh_grp_moments(const uint32_t (&d)[SGH_GRP], uint32_t &c, uint32_t &s, uint32_t &ss) {
 	static_assert(SGH_GRP == 8, "unrolled for 8 dwords");
 	if (SGH_MOM_BYTES) {
-		uint32_t sl = 0, sh = 0;
-		sgh_dw_moments_b<0>(d[0], c, s, sl, sh);
-		sgh_dw_moments_b<1>(d[1], c, s, sl, sh);
-		sgh_dw_moments_b<2>(d[2], c, s, sl, sh);
-		sgh_dw_moments_b<3>(d[3], c, s, sl, sh);
-		sgh_dw_moments_b<4>(d[4], c, s, sl, sh);
-		sgh_dw_moments_b<5>(d[5], c, s, sl, sh);
-		sgh_dw_moments_b<6>(d[6], c, s, sl, sh);
-		sgh_dw_moments_b<7>(d[7], c, s, sl, sh);
+		uint32_t sl = 0, sh = 0, cx = 0;
+		uint32_t &cc = COUNT ? c : cx;	/* !COUNT: the caller has the count already */
+		sgh_dw_moments_b<0>(d[0], cc, s, sl, sh);
+		sgh_dw_moments_b<1>(d[1], cc, s, sl, sh);
+		sgh_dw_moments_b<2>(d[2], cc, s, sl, sh);
+		sgh_dw_moments_b<3>(d[3], cc, s, sl, sh);
+		sgh_dw_moments_b<4>(d[4], cc, s, sl, sh);
+		sgh_dw_moments_b<5>(d[5], cc, s, sl, sh);
+		sgh_dw_moments_b<6>(d[6], cc, s, sl, sh);
+		sgh_dw_moments_b<7>(d[7], cc, s, sl, sh);
 		ss += sl + (sh << 8);
 		return;
 	}
@@ -199,6 +201,7 @@ struct SghQ {
 	int v, t, g, kb;
 	uint32_t d[SGH_GRP];	/* the group's dwords below the boundary dword kb, others 0 */
 	uint32_t bd;		/* the boundary dword (group dword kb, the one holding bin t), masked to bins <= t */
+	uint32_t cp;		/* band samples <= t inside the group (d and bd) */
 };
 
 /* the group is read as 8 dwords plus the boundary dword once more (one more LDS read, no
@@ -220,14 +223,15 @@ __device__ __forceinline__ void sgh_q_load(const SghPix &P, int v, SghQ &q) {
 		q.d[k] = k < kb ? q.d[k] : 0u;
 	const uint32_t mt = 0xFFFFFFFFu >> (24 - 8 * (t & 3));
 	q.bd = t >= 0 ? (q.bd & mt) : 0u;
-}
-
-__device__ __forceinline__ int sgh_q_count(const SghPix &P, const SghQ &q) {
-	uint32_t c = sgh_pre(P, P.pc, q.g);
+	uint32_t c = __builtin_amdgcn_sad_u8(q.bd, 0u, 0u);
 #pragma unroll
 	for (int k = 0; k < SGH_GRP; k++)
 		c = __builtin_amdgcn_sad_u8(q.d[k], 0u, c);
-	c = __builtin_amdgcn_sad_u8(q.bd, 0u, c);
+	q.cp = c;
+}
+
+__device__ __forceinline__ int sgh_q_count(const SghPix &P, const SghQ &q) {
+	const uint32_t c = sgh_pre(P, P.pc, q.g) + q.cp;
 	if (q.v < 0)
 		return 0;
 	if (q.v >= 65535)
@@ -236,8 +240,8 @@ __device__ __forceinline__ int sgh_q_count(const SghPix &P, const SghQ &q) {
 }
 
 __device__ __forceinline__ SghM sgh_q_moments(const SghPix &P, const SghQ &q) {
-	uint32_t c = 0, s = 0, ss = 0;
-	sgh_grp_moments(q.d, c, s, ss);
+	uint32_t c = q.cp, s = 0, ss = 0;
+	sgh_grp_moments<false>(q.d, c, s, ss);
 	/* the boundary dword: bins j = 4 kb + b, j^2 = (4 kb)^2 + 2 (4 kb) b + b^2 */
 	const uint32_t cb = __builtin_amdgcn_sad_u8(q.bd, 0u, 0u);
 	const uint32_t sb = __builtin_amdgcn_udot4(q.bd, 0x03020100u, 0u, false);
@@ -246,7 +250,6 @@ __device__ __forceinline__ SghM sgh_q_moments(const SghPix &P, const SghQ &q) {
 	const uint32_t k4 = 4u * (uint32_t)(q.kb < 0 ? 0 : q.kb);
 	ss += qb + __umul24(2u * k4, sb) + __umul24(__umul24(k4, k4), cb);
 	s += sb + __umul24(k4, cb);
-	c += cb;
 	const uint32_t b0 = (uint32_t)q.g * (4u * SGH_GRP);	/* first bin of the group */
 	SghM m;
 	m.c = P.nz + (int)(sgh_pre(P, P.pc, q.g) + c);
