@@ -855,14 +855,25 @@ __device__ __forceinline__ int sgh_sigma2(const SghPix &P, int N, double sl, dou
 __device__ __forceinline__ double sgh_sd_rel(int n, long long S, long long SS, bool *e0) {
 	const long long num = (long long)n * SS - S * S;
 	*e0 = (num == 0);
-	return num <= 0 ? 0.0 : sqrt((double)num / ((double)n * (double)(n - 1)));
+	return sgh_sigma_fast(num, n);
 }
-/* the same with 1 / (n (n - 1)) precomputed: within 2 ulp of sgh_sd_rel, far inside the
+/* sqrt(x) for x > 0 from v_rsq_f64 and two coupled Newton steps (as sgh_sigma_fast) */
+__device__ __forceinline__ double sgh_sqrt_fast(double x) {
+	const double y = __builtin_amdgcn_rsq(x);
+	double h = 0.5 * y, s = x * y;
+	double r = fma(-s, h, 0.5);
+	s = fma(s, r, s);
+	h = fma(h, r, h);
+	r = fma(-s, h, 0.5);
+	return fma(s, r, s);
+}
+/* the same with 1 / (n (n - 1)) precomputed: within a few ulp of sgh_sd_rel, far inside the
  * rounding band every decision keeps */
 __device__ __forceinline__ double sgh_sd_rel_inv(int n, long long S, long long SS, double inn, bool *e0) {
 	const long long num = (long long)n * SS - S * S;
 	*e0 = (num == 0);
-	return num <= 0 ? 0.0 : sqrt((double)num * inn);
+	const double v = sgh_sqrt_fast((double)(num > 0 ? num : 1) * inn);
+	return num > 0 ? v : 0.0;
 }
 
 /* round_to_WORD(m) decision ambiguous (m within tol of 0, 65535 or a .5) */
@@ -906,6 +917,18 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint
 	int A = 0, B = 65535, n = N, r = 0, nrem;
 	SghM MA = {0, 0, 0}, MB = P.T;
 	uint32_t rlo = 0, rhi = 0;
+	/* # samples <= v of the low- and high-side threshold queries, cached per side: once sigma
+	 * settles the integer thresholds repeat from one inner iteration to the next, and a wave
+	 * skips the histogram read when none of its lanes misses */
+	int cv0 = -2, ck0 = 0, cv1 = -2, ck1 = 0;
+	auto cnt_cached = [&](int v, int side) -> int {
+		int &cv = side ? cv1 : cv0, &ck = side ? ck1 : ck0;
+		if (v != cv) {
+			ck = sgh_cnt_le(P, v);
+			cv = v;
+		}
+		return ck;
+	};
 	do {
 		const long long S = MB.s - MA.s;
 		const long long SS = (long long)(MB.ss - MA.ss);
@@ -933,13 +956,13 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint
 			/* # w elements <= v (integer v in [-1, 65535]); "< thr" is "<= ceil(thr) - 1" and
 			 * "<= thr" is "<= floor(thr)", so both sides of a rounding band usually name the
 			 * same v and one count serves both */
-			auto w_le = [&](int v) {
+			auto w_le = [&](int v, int side) {
 				int c = (Lw && vlo <= v) ? Lw : 0;
 				if (nin > 0 && v >= ulo) {
 					if (v >= uhi) {
 						c += nin;
 					} else {
-						int k = sgh_cnt_le(P, v);
+						int k = cnt_cached(v, side);
 						k = k < MIA.c ? MIA.c : (k > MIB.c ? MIB.c : k);
 						c += k - MIA.c;
 					}
@@ -958,11 +981,11 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint
 			};
 			const int a1 = v_lt(m0 - tol), a2 = v_le(m0 + tol);
 			const int b1 = v_le(m1d + tol), b2 = v_lt(m1d - tol);
-			const int clo = w_le(a1);
-			if (!sig_e0 && a2 != a1 && clo != w_le(a2))
+			const int clo = w_le(a1, 0);
+			if (!sig_e0 && a2 != a1 && clo != w_le(a2, 0))
 				return 1;
-			const int chi = n - w_le(b1);
-			if (!sig_e0 && b2 != b1 && chi != n - w_le(b2))
+			const int chi = n - w_le(b1, 1);
+			if (!sig_e0 && b2 != b1 && chi != n - w_le(b2, 1))
 				return 1;
 			if (clo + chi > n)
 				return 1;
