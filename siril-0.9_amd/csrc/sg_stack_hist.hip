@@ -700,32 +700,34 @@ __device__ __forceinline__ int sgh_sigma3(const SghPix &P, int N, double sl, dou
 			fb = (n - H) + (need - L) - 1;
 		if (fb >= 0 && fb < n - 1)
 			return 1;
-		/* the next pass's median ranks: kept count n - L - H starting at rank cnt_a (or MA.c) */
-		{
+		/* a pass that removes nothing is the last one: no next median, no moments (both lanes
+		 * of a pair take the branch together, so the exchanges inside see an active partner) */
+		if (L | H) {
+			/* the next pass's median ranks: kept count n - L - H starting at rank cnt_a (or MA.c) */
 			const int ca = L ? cnt_a : MA.c, nn = n - L - H;
 			sgh_med_issue(P, ca + (half ? nn / 2 : (nn - 1) / 2), md);
-		}
-		/* moments of this lane's bound; field-wise selects (a select of whole structs becomes
-		 * a scratch access) */
-		const SghM Mq = sgh_q_moments(P, q);
-		const bool mine = half ? (H != 0) : (L != 0);
-		const int mc = mine ? Mq.c : (half ? MB.c : MA.c);
-		const long long ms = mine ? Mq.s : (half ? MB.s : MA.s);
-		const unsigned long long mss = mine ? Mq.ss : (half ? MB.ss : MA.ss);
-		const int oc = (int)sgh_x((uint32_t)mc);
-		const long long os = (long long)sgh_x64((uint64_t)ms);
-		const unsigned long long oss = sgh_x64(mss);
-		if (L) {
-			A = a;
-			MA.c = half ? oc : mc;
-			MA.s = half ? os : ms;
-			MA.ss = half ? oss : mss;
-		}
-		if (H) {
-			B = bt;
-			MB.c = half ? mc : oc;
-			MB.s = half ? ms : os;
-			MB.ss = half ? mss : oss;
+			/* moments of this lane's bound; field-wise selects (a select of whole structs
+			 * becomes a scratch access) */
+			const SghM Mq = sgh_q_moments(P, q);
+			const bool mine = half ? (H != 0) : (L != 0);
+			const int mc = mine ? Mq.c : (half ? MB.c : MA.c);
+			const long long ms = mine ? Mq.s : (half ? MB.s : MA.s);
+			const unsigned long long mss = mine ? Mq.ss : (half ? MB.ss : MA.ss);
+			const int oc = (int)sgh_x((uint32_t)mc);
+			const long long os = (long long)sgh_x64((uint64_t)ms);
+			const unsigned long long oss = sgh_x64(mss);
+			if (L) {
+				A = a;
+				MA.c = half ? oc : mc;
+				MA.s = half ? os : ms;
+				MA.ss = half ? oss : mss;
+			}
+			if (H) {
+				B = bt;
+				MB.c = half ? mc : oc;
+				MB.s = half ? ms : os;
+				MB.ss = half ? mss : oss;
+			}
 		}
 		rlo += L;
 		rhi += H;
