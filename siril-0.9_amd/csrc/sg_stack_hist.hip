@@ -649,18 +649,19 @@ __device__ __forceinline__ int sgh_sigma3(const SghPix &P, int N, double sl, dou
 	SghM MA = {0, 0, 0}, MB = P.T;
 	uint32_t rlo = 0, rhi = 0;
 	SghMed md;
-	sgh_med_issue(P, half ? N / 2 : (N - 1) / 2, md);
+	sgh_med_issue(P, (int)((unsigned)(half ? N : N - 1) >> 1), md);
 	do {
 		const long long S = MB.s - MA.s;
 		const unsigned long long SS = MB.ss - MA.ss;
 		const long long num = (long long)n * (long long)SS - S * S;
 		const bool exact0 = (num == 0);
 		const double sigma = sgh_sigma_fast(num, n);
-		const int g1 = MA.c + (n - 1) / 2, g2 = MA.c + n / 2;
+		/* n >= 4: the halvings as unsigned shifts; the median as (m1 + m2) * 0.5 (exact), with
+		 * m2 = m1 for odd n, so no branch */
 		const int mv = sgh_med_value(P, md);
 		const int mo = (int)sgh_x((uint32_t)mv);
-		const int m1 = half ? mo : mv, m2 = half ? mv : mo;
-		const double median = (g1 == g2) ? (double)m1 : (double)(m1 + m2) / 2.0;
+		const int m1 = half ? mo : mv, m2 = (n & 1) ? m1 : (half ? mv : mo);
+		const double median = (double)(m1 + m2) * 0.5;
 		const double tl = sl * sigma, th = sh * sigma;
 		const double blo = median - tl, bhi = median + th;
 		const double tol = exact0 ? 0.0 : SGH_BAND * (fabs(median) + fabs(tl) + fabs(th) + 1.0);
@@ -705,7 +706,7 @@ __device__ __forceinline__ int sgh_sigma3(const SghPix &P, int N, double sl, dou
 		if (L | H) {
 			/* the next pass's median ranks: kept count n - L - H starting at rank cnt_a (or MA.c) */
 			const int ca = L ? cnt_a : MA.c, nn = n - L - H;
-			sgh_med_issue(P, ca + (half ? nn / 2 : (nn - 1) / 2), md);
+			sgh_med_issue(P, ca + (int)((unsigned)(half ? nn : nn - 1) >> 1), md);
 			/* moments of this lane's bound; field-wise selects (a select of whole structs
 			 * becomes a scratch access) */
 			const SghM Mq = sgh_q_moments(P, q);
