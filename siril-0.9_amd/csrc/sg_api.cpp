@@ -337,9 +337,19 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		 * (multiplicative), read with one scalar load per frame */
 		const bool additive = p.normalize == SG_ADDITIVE || p.normalize == SG_ADDITIVE_SCALING;
 		nm.resize(3 * N + 2 * Npad, 0.0);
+		/* additive: when every offset - 0.5 is exact (TwoSum error 0), the pair carries
+		 * offset - 0.5 and the kernel folds round_to_WORD's + 0.5 into the subtraction
+		 * (NORM 3: trunc(v scale - (offset - 0.5)), one fp64 add per sample less; equal to
+		 * trunc((v scale - offset) + 0.5) whenever the fold is exact, tests/test_norm_fold.py) */
+		bool fold = additive;
+		for (int i = 0; fold && i < N; i++) {
+			const double b = nm[i], c = b - 0.5, bb = c - b;
+			fold = ((b - (c - bb)) + (-0.5 - bb)) == 0.0;
+		}
+		p.hist_norm_fold = fold ? 1 : 0;
 		for (int i = 0; i < N; i++) {
 			nm[3 * N + 2 * i] = nm[2 * N + i];
-			nm[3 * N + 2 * i + 1] = additive ? nm[i] : nm[N + i];
+			nm[3 * N + 2 * i + 1] = additive ? (fold ? nm[i] - 0.5 : nm[i]) : nm[N + i];
 		}
 		HIPCHK(hipMemcpyAsync(dv.norm.p, nm.data(), sizeof(double) * nm.size(), hipMemcpyHostToDevice, s));
 		p.hist_norm = (const double *)dv.norm.p + 3 * N;
@@ -426,9 +436,10 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			unsigned int *redo_list = redo_count + 16;
 			HIPCHK(hipMemsetAsync(redo_count, 0, sizeof(unsigned int), s));
 			HIPCHK(hipEventRecord(dv.ev[0], s));
-			/* NORM: 0 none, 1 additive (round(v scale - offset)), 2 multiplicative (round(v scale mul)) */
+			/* NORM: 0 none, 1 additive (round(v scale - offset)), 2 multiplicative (round(v scale mul)),
+			 * 3 additive with the folded + 0.5 */
 			const int norm = p.normalize == SG_NO_NORM ? 0 :
-				(p.normalize == SG_ADDITIVE || p.normalize == SG_ADDITIVE_SCALING) ? 1 : 2;
+				(p.normalize == SG_ADDITIVE || p.normalize == SG_ADDITIVE_SCALING) ? (p.hist_norm_fold ? 3 : 1) : 2;
 			/* tile = 128 NI pixels of a row, 4 NI waves: NI = 1 by default (sg_stack_hist.hip);
 			 * the A/B NI = 2 (SG_HIST_NI=2) exists without normalisation only (it spills there:
 			 * the per-sample double arithmetic of two pixel pairs) */
@@ -449,9 +460,11 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			case 100: hipLaunchKernelGGL((k_stack_hist<2, 0, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 101: hipLaunchKernelGGL((k_stack_hist<2, 1, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 102: hipLaunchKernelGGL((k_stack_hist<2, 2, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			case 103: hipLaunchKernelGGL((k_stack_hist<2, 3, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 110: hipLaunchKernelGGL((k_stack_hist<4, 0, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 111: hipLaunchKernelGGL((k_stack_hist<4, 1, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 112: hipLaunchKernelGGL((k_stack_hist<4, 2, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			case 113: hipLaunchKernelGGL((k_stack_hist<4, 3, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 200: hipLaunchKernelGGL((k_stack_hist<2, 0, 2>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 210: hipLaunchKernelGGL((k_stack_hist<4, 0, 2>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			default: return set_err(ctx, SG_ERR_GENERIC, "no histogram kernel for this case%s%.0ld", "", 0);

@@ -30,6 +30,7 @@ struct SgStackParams {
 	int prio;				/* histogram path: wave priority of the build phase (SG_HIST_PRIO) */
 	const int *hist_tab;			/* device: c1[hist_npad] = shifty*W*2 + 2*shiftx, then int16 sx2[hist_npad] = 2*shiftx */
 	int hist_npad;				/* N rounded up to a multiple of 16 */
+	int hist_norm_fold;			/* additive pairs carry offset - 0.5 (NORM 3 kernels) */
 	int hist_maxsx;				/* max |shiftx| (interior-tile test of the histogram path) */
 	const double *hist_norm;		/* device: {scale, offset | mul} per frame (hist_npad pairs), normalised stacks */
 	const double *offset, *mul, *scale;	/* device [N] or null */

@@ -482,7 +482,8 @@ __device__ __forceinline__ uint32_t sgh_fixup(uint32_t v, uint32_t fix, int m) {
 }
 
 /* normalisation of a loaded pixel pair (:1635-1652): NORM 1 = round_to_WORD(v scale - offset),
- * 2 = round_to_WORD(v scale mul), in the reference's double operations; rows outside the
+ * 2 = round_to_WORD(v scale mul), 3 = NORM 1 with the + 0.5 folded into the offset, in the
+ * reference's double operations; rows outside the
  * frame (read as 0) are normalised like read samples, but columns outside the image (EDGE
  * fix codes 1..3) stay 0, as the x shift writes 0 straight into the stack (:1628-1632) */
 template <int NORM, bool EDGE>
@@ -493,9 +494,11 @@ __device__ __forceinline__ uint32_t sgh_norm_pair(uint32_t v, double a, double b
 	 * negative values to 0 (y <= 0 gives y + 0.5 <= 0.5, truncated to 0 either way) */
 	auto g = [&](uint32_t x) -> uint32_t {
 		const double t = (double)x * a;
-		const double y = NORM == 1 ? t - b : t * b;
+		/* NORM 3: b = offset - 0.5 (exact, checked on the host), so trunc(t - b) is
+		 * trunc(round(t - offset) + 0.5) of the reference with one add less */
+		const double y = NORM == 3 ? t - b : (NORM == 1 ? t - b : t * b) + 0.5;
 		uint32_t r;
-		asm("v_cvt_u32_f64 %0, %1" : "=v"(r) : "v"(y + 0.5));
+		asm("v_cvt_u32_f64 %0, %1" : "=v"(r) : "v"(y));
 		return r < 65535u ? r : 65535u;
 	};
 	uint32_t r = g(v & 0xFFFFu) | (g(v >> 16) << 16);
@@ -1673,6 +1676,10 @@ template __global__ void k_stack_hist<2, 0, 1>(SgStackParams, const int *, const
 template __global__ void k_stack_hist<2, 1, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
 		unsigned int *);
 template __global__ void k_stack_hist<2, 2, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);
+template __global__ void k_stack_hist<2, 3, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);
+template __global__ void k_stack_hist<4, 3, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
 		unsigned int *);
 template __global__ void k_stack_hist<4, 0, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
 		unsigned int *);

@@ -211,6 +211,38 @@ def test_hist_path_normalization(gpu_ctx, normalize, rejection):
     assert st.chain_pixels <= (2 * border + 0.05 * H) * W, st.chain_pixels
 
 
+@pytest.mark.parametrize("rejection", [sg.SIGMA, sg.WINSORIZED])
+@pytest.mark.parametrize("tiny", [False, True])
+def test_hist_path_additive_fold(gpu_ctx, rejection, tiny):
+    """additive normalisation with every offset - 0.5 exact takes the folded kernel (NORM 3);
+    one offset of 1e-30 (offset - 0.5 inexact) sends the whole stack to the unfolded one
+    (NORM 1); both must equal the oracle.  Offsets include half-integers, where
+    round_to_WORD's + 0.5 lands exactly on integers."""
+    N, H, W = 36, 40, 300
+    frames = orc.synth(N, 1, H, W, seed=77, maxshift=8)
+    sx, sy = orc.synth_shifts(N, seed=77, maxshift=8)
+    rng = np.random.default_rng(78)
+    off = np.round(rng.uniform(-60, 60, N) * 2) / 2          # half-integers
+    off[1::3] += rng.uniform(-0.01, 0.01, len(off[1::3]))
+    if tiny:
+        off[5] = 1e-30
+    scale = 1.0 + rng.uniform(-0.03, 0.03, N)
+    scale[0] = 1.0
+    mul = np.ones(N)
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=rejection, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                              normalize=sg.ADDITIVE_SCALING, offset=off, mul=mul, scale=scale, max_thread=2,
+                              max_number_of_rows=H)
+    rc, out, rej, _ = gpu_ctx.stack_host(desc, np.ascontiguousarray(frames))
+    assert rc == 0, gpu_ctx.error()
+    assert gpu_ctx.stats().path == 1
+    rc, ref, rej_ref = orc.stack_rejection(frames, rejection, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                                           normalize=sg.ADDITIVE_SCALING, offset=off, mul=mul, scale=scale,
+                                           max_thread=2)
+    assert rc == 0
+    assert_same(out, ref, f"additive fold tiny={tiny} rej={rejection}")
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+
+
 @pytest.mark.parametrize("shifts", [True, False])
 @pytest.mark.parametrize("W", [700, 1024])
 def test_hist_path_interior_tiles(gpu_ctx, W, shifts):
