@@ -923,6 +923,9 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint
 	int A = 0, B = 65535, n = N, r = 0, nrem;
 	SghM MA = {0, 0, 0}, MB = P.T;
 	uint32_t rlo = 0, rhi = 0;
+#ifdef SGH_WINS_ITERS
+	*rlo_out = 0;
+#endif
 	/* # samples <= v of the low- and high-side threshold queries, cached per side: once sigma
 	 * settles the integer thresholds repeat from one inner iteration to the next, and a wave
 	 * skips the histogram read when none of its lanes misses */
@@ -956,6 +959,9 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint
 		for (int guard = 0;; guard++) {
 			if (guard > 4096)
 				return 1;
+#ifdef SGH_WINS_ITERS	/* A/B probe build: inner iterations (low 16 bits) and outer passes (high) */
+			(*rlo_out)++;
+#endif
 			const double m0 = median - 1.5 * sigma, m1d = median + 1.5 * sigma;
 			const double tol = sig_e0 ? 0.0 : SGH_BAND * (fabs(median) + 1.5 * sigma + 1.0);
 			const int nin = n - Lw - Hw;
@@ -1117,7 +1123,9 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint
 	} while (nrem > 0 && n > 3);
 	const long long tot = (MB.s - MA.s) + (long long)n * P.lo;
 	*value = sg_round_to_WORD((double)tot / (double)n);
+#ifndef SGH_WINS_ITERS
 	*rlo_out = rlo;
+#endif
 	*rhi_out = rhi;
 	return SG_CLS_OK;
 }
@@ -1224,10 +1232,21 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 			P.T.c = N;
 			P.T.s = (long long)s32 + P.Z.s + ds * P.ns;
 			P.T.ss = (unsigned long long)ss32 + P.Z.ss + (unsigned long long)(ds * ds) * (unsigned long long)P.ns;
-			if (REJ == 4 || !PAIR)
+			if (REJ == 4 || !PAIR) {
 				cls = sgh_winsorized(P, N, p.sig0, p.sig1, &value, &rlo, &rhi);
-			else if (SGH_SIGMA_V == 3)
+#ifdef SGH_WINS_ITERS
+				value = (uint16_t)rlo;	/* A/B probe build: the image holds the inner iteration counts */
+				cls = SG_CLS_OK;
+				rlo = rhi = 0;
+#endif
+			} else if (SGH_SIGMA_V == 3) {
 				cls = sgh_sigma3(P, N, p.sig0, p.sig1, half, &value, &rlo, &rhi, passes);
+#ifdef SGH_SIGMA_PASSES	/* A/B probe build: the image holds the pass counts */
+				value = (uint16_t)passes;
+				cls = SG_CLS_OK;
+				rlo = rhi = 0;
+#endif
+			}
 			else
 				cls = sgh_sigma2(P, N, p.sig0, p.sig1, half, &value, &rlo, &rhi, passes);
 		}
