@@ -127,28 +127,12 @@ __device__ __forceinline__ void sgh_grp(const SghPix &P, int g, uint32_t (&d)[SG
 		d[k] = b[k * 64];
 }
 
-typedef unsigned short sgh_u16x2v __attribute__((ext_vector_type(2)));
 
-/* moments of the bins of one group, relative to the group's first bin: the dword k of the
- * group holds bins 4k..4k+3, so sum (4k+b) c_b is a u8 dot product and sum (4k+b)^2 c_b
- * two u16 dot products on the unpacked byte pairs (all weights compile-time constants) */
-template <int K>
-__device__ __forceinline__ void sgh_dw_moments(uint32_t dd, uint32_t &c, uint32_t &s, uint32_t &ss) {
-	constexpr uint32_t w1 = (uint32_t)(4 * K) | ((uint32_t)(4 * K + 1) << 8) | ((uint32_t)(4 * K + 2) << 16) |
-		((uint32_t)(4 * K + 3) << 24);
-	constexpr unsigned short q0 = (unsigned short)((4 * K) * (4 * K)), q1 = (unsigned short)((4 * K + 1) * (4 * K + 1));
-	constexpr unsigned short q2 = (unsigned short)((4 * K + 2) * (4 * K + 2)), q3 = (unsigned short)((4 * K + 3) * (4 * K + 3));
-	c = __builtin_amdgcn_sad_u8(dd, 0u, c);
-	s = __builtin_amdgcn_udot4(dd, w1, s, false);
-	const uint32_t lo = __builtin_amdgcn_perm(dd, dd, 0x0c010c00u), hi = __builtin_amdgcn_perm(dd, dd, 0x0c030c02u);
-	ss = __builtin_amdgcn_udot2(__builtin_bit_cast(sgh_u16x2v, lo), (sgh_u16x2v){q0, q1}, ss, false);
-	ss = __builtin_amdgcn_udot2(__builtin_bit_cast(sgh_u16x2v, hi), (sgh_u16x2v){q2, q3}, ss, false);
-}
-
-/* the same moments with the squared weights split into bytes: j = 4 K + b < 32, j^2 < 1024,
- * so sum j^2 c_j = sum lo8(j^2) c_j + 256 sum hi8(j^2) c_j, two u8 dot products per dword
- * (the high one only for K >= 4, where j^2 >= 256) instead of two byte unpacks and two u16
- * dot products: 29 instead of 48 VALU per group */
+/* moments of the bins of one group, relative to the group's first bin: the dword K of the
+ * group holds bins j = 4 K + b; sum j c_j is a u8 dot product on constant weights, and with
+ * j < 32, j^2 < 1024, sum j^2 c_j = sum lo8(j^2) c_j + 256 sum hi8(j^2) c_j: two more u8 dot
+ * products per dword (the high one only for K >= 4, where j^2 >= 256) - 29 VALU per 8-dword
+ * group against 48 with the bytes unpacked to u16 for v_dot2_u32_u16 (round 1) */
 template <int K>
 __device__ __forceinline__ void sgh_dw_moments_b(uint32_t dd, uint32_t &c, uint32_t &s, uint32_t &sl, uint32_t &sh) {
 	constexpr uint32_t j0 = 4 * K, j1 = j0 + 1, j2 = j0 + 2, j3 = j0 + 3;
@@ -163,35 +147,20 @@ __device__ __forceinline__ void sgh_dw_moments_b(uint32_t dd, uint32_t &c, uint3
 		sh = __builtin_amdgcn_udot4(dd, wh, sh, false);
 }
 
-#ifndef SGH_MOM_BYTES
-#define SGH_MOM_BYTES 1
-#endif
-
 template <bool COUNT = true>
 __device__ __forceinline__ void sgh_grp_moments(const uint32_t (&d)[SGH_GRP], uint32_t &c, uint32_t &s, uint32_t &ss) {
 	static_assert(SGH_GRP == 8, "unrolled for 8 dwords");
-	if (SGH_MOM_BYTES) {
-		uint32_t sl = 0, sh = 0, cx = 0;
-		uint32_t &cc = COUNT ? c : cx;	/* !COUNT: the caller has the count already */
-		sgh_dw_moments_b<0>(d[0], cc, s, sl, sh);
-		sgh_dw_moments_b<1>(d[1], cc, s, sl, sh);
-		sgh_dw_moments_b<2>(d[2], cc, s, sl, sh);
-		sgh_dw_moments_b<3>(d[3], cc, s, sl, sh);
-		sgh_dw_moments_b<4>(d[4], cc, s, sl, sh);
-		sgh_dw_moments_b<5>(d[5], cc, s, sl, sh);
-		sgh_dw_moments_b<6>(d[6], cc, s, sl, sh);
-		sgh_dw_moments_b<7>(d[7], cc, s, sl, sh);
-		ss += sl + (sh << 8);
-		return;
-	}
-	sgh_dw_moments<0>(d[0], c, s, ss);
-	sgh_dw_moments<1>(d[1], c, s, ss);
-	sgh_dw_moments<2>(d[2], c, s, ss);
-	sgh_dw_moments<3>(d[3], c, s, ss);
-	sgh_dw_moments<4>(d[4], c, s, ss);
-	sgh_dw_moments<5>(d[5], c, s, ss);
-	sgh_dw_moments<6>(d[6], c, s, ss);
-	sgh_dw_moments<7>(d[7], c, s, ss);
+	uint32_t sl = 0, sh = 0, cx = 0;
+	uint32_t &cc = COUNT ? c : cx;	/* !COUNT: the caller has the count already */
+	sgh_dw_moments_b<0>(d[0], cc, s, sl, sh);
+	sgh_dw_moments_b<1>(d[1], cc, s, sl, sh);
+	sgh_dw_moments_b<2>(d[2], cc, s, sl, sh);
+	sgh_dw_moments_b<3>(d[3], cc, s, sl, sh);
+	sgh_dw_moments_b<4>(d[4], cc, s, sl, sh);
+	sgh_dw_moments_b<5>(d[5], cc, s, sl, sh);
+	sgh_dw_moments_b<6>(d[6], cc, s, sl, sh);
+	sgh_dw_moments_b<7>(d[7], cc, s, sl, sh);
+	ss += sl + (sh << 8);
 }
 
 /* a prefix query "samples with value <= v" (v in [-1, 65535]): the group of the band bin is
@@ -637,15 +606,12 @@ __device__ __forceinline__ int sgh_med_value(const SghPix &P, const SghMed &m) {
 	return in ? v : (m.r < 0 ? 0 : 65535);
 }
 
-#ifndef SGH_SIGMA_V
-#define SGH_SIGMA_V 3
-#endif
-
-/* sgh_sigma2 restructured for the critical path of a pass: the median's group read is
- * issued during the previous pass (before its moments), sigma comes from sgh_sigma_fast, and
- * the clamps, moments and their selects are straight-line code, so one pass is one basic
- * block the scheduler can overlap (fp64 chain against LDS latency).  Same decisions, same
- * exits as sgh_sigma2. */
+/* the SIGMA loop (:1674-1695 + sigma_clipping :1148-1161) on the histogram, split over a lane
+ * pair: half 0 owns the low side (median rank g1, threshold a - 1, M(A - 1)), half 1 the high
+ * side (rank g2, threshold bt, M(B)).  The median's group read is issued during the previous
+ * pass, sigma comes from sgh_sigma_fast, and the clamps and selects are straight-line code, so
+ * a pass is one basic block (round 2: the loop's VALU count, not its dependency chain, is what
+ * the kernel pays for; scripts/gpu_r2t.sh, gpu_r2w.sh). */
 __device__ __forceinline__ int sgh_sigma3(const SghPix &P, int N, double sl, double sh, int half, uint16_t *value,
 		uint32_t *rlo_out, uint32_t *rhi_out, int &passes) {
 	int A = 0, B = 65535, n = N, r = 0, nrem;
@@ -731,107 +697,6 @@ __device__ __forceinline__ int sgh_sigma3(const SghPix &P, int N, double sl, dou
 				MB.c = half ? mc : oc;
 				MB.s = half ? ms : os;
 				MB.ss = half ? mss : oss;
-			}
-		}
-		rlo += L;
-		rhi += H;
-		r += L + H;
-		nrem = L + H;
-		n -= nrem;
-		passes++;
-	} while (nrem > 0 && n > 3);
-	const long long tot = (MB.s - MA.s) + (long long)n * P.lo;
-	*value = sg_round_to_WORD((double)tot / (double)n);
-	*rlo_out = rlo;
-	*rhi_out = rhi;
-	return SG_CLS_OK;
-}
-
-/* the SIGMA loop of sgh_sigma, split over a lane pair: half 0 owns the low side (median
- * rank g1, threshold a - 1, M(A - 1)), half 1 the high side (rank g2, threshold bt, M(B)) */
-__device__ __forceinline__ int sgh_sigma2(const SghPix &P, int N, double sl, double sh, int half, uint16_t *value,
-		uint32_t *rlo_out, uint32_t *rhi_out, int &passes) {
-	int A = 0, B = 65535, n = N, r = 0, nrem;
-	SghM MA = {0, 0, 0}, MB = P.T;
-	uint32_t rlo = 0, rhi = 0;
-	do {
-		const long long S = MB.s - MA.s;
-		const unsigned long long SS = MB.ss - MA.ss;
-		const long long num = (long long)n * (long long)SS - S * S;
-		const bool exact0 = (num == 0);
-		const double sigma = num <= 0 ? 0.0 : sqrt((double)num / ((double)n * (double)(n - 1)));
-		const int g1 = MA.c + (n - 1) / 2, g2 = MA.c + n / 2;
-		const int mv = sgh_value_at1(P, half ? g2 : g1);
-		const int mo = (int)sgh_x((uint32_t)mv);
-		const int m1 = half ? mo : mv, m2 = half ? mv : mo;
-		const double median = (g1 == g2) ? (double)m1 : (double)(m1 + m2) / 2.0;
-		const double tl = sl * sigma, th = sh * sigma;
-		const double blo = median - tl, bhi = median + th;
-		const double tol = exact0 ? 0.0 : SGH_BAND * (fabs(median) + fabs(tl) + fabs(th) + 1.0);
-		int a = sgh_ceil_clamp(blo - tol);
-		if (a < A)
-			a = A;
-		int bt = sgh_floor_clamp(bhi + tol);
-		if (bt > B)
-			bt = B;
-		SghQ q;
-		sgh_q_load(P, half ? bt : a - 1, q);
-		const int cm = sgh_q_count(P, q), co = (int)sgh_x((uint32_t)cm);
-		const int cnt_a = half ? co : cm, cnt_bt = half ? cm : co;
-		uint32_t amb = 0;
-		if (!exact0) {
-			if (!half) {
-				int amb1 = sgh_floor_clamp(blo + tol);
-				if (amb1 > B)
-					amb1 = B;
-				amb = (a <= amb1 && sgh_cnt_le(P, amb1) - cnt_a > 0) ? 1u : 0u;
-			} else {
-				int amb0 = sgh_ceil_clamp(bhi - tol);
-				if (amb0 < A)
-					amb0 = A;
-				amb = (amb0 <= bt && cnt_bt - sgh_cnt_le(P, amb0 - 1) > 0) ? 1u : 0u;
-			}
-		}
-		if (amb | sgh_x(amb))
-			return 1;
-		const int L = cnt_a - MA.c, H = MB.c - cnt_bt;
-		if (L + H > n)
-			return 1;
-		/* `if (N - r <= 4) break;` inside the clipping loop (:1684) */
-		const int need = n - 4 - r;
-		int fb = -1;
-		if (need <= 0)
-			fb = 0;
-		else if (L >= need)
-			fb = need - 1;
-		else if (L + H >= need)
-			fb = (n - H) + (need - L) - 1;
-		if (fb >= 0 && fb < n - 1)
-			return 1;
-		if (L | H) {
-			/* field-wise selects: a select of whole structs becomes a scratch access */
-			SghM Mm;
-			if (half ? H : L) {
-				Mm = sgh_q_moments(P, q);
-			} else {
-				Mm.c = half ? MB.c : MA.c;
-				Mm.s = half ? MB.s : MA.s;
-				Mm.ss = half ? MB.ss : MA.ss;
-			}
-			const int oc = (int)sgh_x((uint32_t)Mm.c);
-			const long long os = (long long)sgh_x64((uint64_t)Mm.s);
-			const unsigned long long oss = sgh_x64(Mm.ss);
-			if (L) {
-				A = a;
-				MA.c = half ? oc : Mm.c;
-				MA.s = half ? os : Mm.s;
-				MA.ss = half ? oss : Mm.ss;
-			}
-			if (H) {
-				B = bt;
-				MB.c = half ? Mm.c : oc;
-				MB.s = half ? Mm.s : os;
-				MB.ss = half ? Mm.ss : oss;
 			}
 		}
 		rlo += L;
@@ -1239,7 +1104,7 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 				cls = SG_CLS_OK;
 				rlo = rhi = 0;
 #endif
-			} else if (SGH_SIGMA_V == 3) {
+			} else {
 				cls = sgh_sigma3(P, N, p.sig0, p.sig1, half, &value, &rlo, &rhi, passes);
 #ifdef SGH_SIGMA_PASSES	/* A/B probe build: the image holds the pass counts */
 				value = (uint16_t)passes;
@@ -1247,8 +1112,6 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 				rlo = rhi = 0;
 #endif
 			}
-			else
-				cls = sgh_sigma2(P, N, p.sig0, p.sig1, half, &value, &rlo, &rhi, passes);
 		}
 		const int64_t pix = ((int64_t)c * p.H + R) * p.W + x;
 		if (!half) {
