@@ -48,7 +48,9 @@
  * CU overlap one tile's finish with the other's loads worse than four 4-wave ones: 4.62 ms
  * against 4.22 ms for the whole kernel, so NI = 1 is the default (SG_HIST_NI=2 selects 2). */
 #define SGH_WAVES_PER_NI 4
+#ifndef SGH_CENTER
 #define SGH_CENTER 16		/* frames used for the centre estimate */
+#endif
 #ifndef SGH_NBUF
 #define SGH_NBUF 2		/* register buffers of 16 frames per wave (NBUF-1 blocks in flight while binning) */
 #endif
@@ -68,6 +70,7 @@ struct SghLds {
 	uint32_t h[2 * NI][SGH_HROWS][64];
 	uint32_t nz[128 * NI], ns[128 * NI];	/* zeros / 65535s (all of them lie outside the band) */
 	uint32_t lo2[NI][64];			/* band starts of the lane pixel pairs (u16 halves) */
+	uint32_t cs[NI][8][64];			/* wave 1's first 8 frames for the band centre (SGH_CENTER2W) */
 };
 
 /* Finish-phase queries.  The band is cut into SGH_NGRP groups of SGH_GRP dwords (32 bins);
@@ -1275,6 +1278,13 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, const SghRo &r
 #ifndef SGH_HALF1
 #define SGH_HALF1 1
 #endif
+/* band centre from the first half blocks of waves 0 and 1 (frames 0..7, 16..23) instead of
+ * wave 0's whole first block: 3.88 -> 3.74 ms (scripts/gpu_r3n.sh), the start barrier no
+ * longer waits for a second half block to land (8 frames alone: 3.64 ms but a noisier centre
+ * sends 35 k pixels to the redo list, scripts/gpu_r3m.sh) */
+#ifndef SGH_CENTER2W
+#define SGH_CENTER2W 1
+#endif
 
 template <bool EDGE, int NORM, int NI, int NB>
 __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const SghRo &ro, SghLds<NI> &L, const SghFrame &F,
@@ -1315,7 +1325,46 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
 		}
 	}
 	const bool nocentre = p.dbg == 15;	/* A/B: loads only, no centre and no start barrier */
-	if (wave == 0 && !nocentre) {
+	static_assert(!SGH_CENTER2W || SGH_CENTER == 2 * MB, "two half blocks make the centre sample");
+	if (SGH_CENTER2W && !nocentre) {
+		/* the centre sample is the first half block of wave 0 (frames 0..7) and of wave 1
+		 * (frames 16..23): both land with the kernel's first loads, so the start barrier does
+		 * not wait for a second half block */
+		if (wave == 1) {
+#pragma unroll
+			for (int i = 0; i < NI; i++)
+#pragma unroll
+				for (int m = 0; m < MB; m++) {
+					uint32_t v = sgh_fixup<EDGE>(buf[0][0][m][i], fix[0][0][i], m);
+					if (NORM) {
+						double a, b;
+						sgh_coef(ro, f16 + m, a, b);
+						v = sgh_norm_pair<NORM, EDGE>(v, a, b, fix[0][0][i], m);
+					}
+					L.cs[i][m][lane] = v;
+				}
+		}
+		__syncthreads();
+		if (wave == 0) {
+#pragma unroll
+			for (int i = 0; i < NI; i++) {
+				uint32_t p16[SGH_CENTER];
+#pragma unroll
+				for (int m = 0; m < MB; m++) {
+					p16[m] = sgh_fixup<EDGE>(buf[0][0][m][i], fix[0][0][i], m);
+					if (NORM) {
+						double a, b;
+						sgh_coef(ro, m, a, b);
+						p16[m] = sgh_norm_pair<NORM, EDGE>(p16[m], a, b, fix[0][0][i], m);
+					}
+					p16[MB + m] = L.cs[i][m][lane];
+				}
+				int la, lb;
+				sgh_centre2(p16, la, lb);
+				L.lo2[i][lane] = (uint32_t)la | ((uint32_t)lb << 16);
+			}
+		}
+	} else if (wave == 0 && !nocentre) {
 #pragma unroll
 		for (int i = 0; i < NI; i++) {
 			uint32_t p16[SGH_CENTER];
