@@ -66,7 +66,7 @@ typedef unsigned short sgh_u16x2 __attribute__((ext_vector_type(2)));
  *                                  else sends the pixel to the redo list) */
 #define SGH_HROWS (SGH_DW + 1)
 template <int NI>
-struct SghLds {
+struct alignas(16) SghLds {
 	uint32_t h[2 * NI][SGH_HROWS][64];
 	uint32_t nz[128 * NI], ns[128 * NI];	/* zeros / 65535s (all of them lie outside the band) */
 	uint32_t lo2[NI][64];			/* band starts of the lane pixel pairs (u16 halves) */
@@ -1154,6 +1154,26 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 	}
 }
 
+/* clear the tile's histogram and counters with 16-byte stores (called after the first frame
+ * loads are issued, so their latency covers it; the build's start barrier orders it before
+ * the first atomic) */
+template <int NI>
+__device__ __forceinline__ void sgh_clear(SghLds<NI> &L) {
+	constexpr int NH = 2 * NI * SGH_HROWS * 64 / 4, NC = 128 * NI / 4, T = 256 * NI;
+	uint4 *h = (uint4 *)&L.h[0][0][0];
+	const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+	for (int k = 0; k < (NH + T - 1) / T; k++) {
+		const int i = (int)threadIdx.x + k * T;
+		if (i < NH)
+			h[i] = z;
+	}
+	if ((int)threadIdx.x < NC) {
+		((uint4 *)L.nz)[threadIdx.x] = z;
+		((uint4 *)L.ns)[threadIdx.x] = z;
+	}
+}
+
 /* one wave's share of the tile's histogram build: 16-frame blocks, wave w bins blocks w,
  * w+WAVES, w+2 WAVES, ... in order, with NBUF named register buffers: a buffer is refilled with
  * the wave's block NBUF steps ahead right after it has been binned, so NBUF-1 blocks stay in
@@ -1192,6 +1212,7 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, const SghRo &r
 			loadblk(f[k], buf[k], fix[k]);
 		}
 	}
+	sgh_clear(L);
 	if (wave == 0) {
 #pragma unroll
 		for (int i = 0; i < NI; i++) {
@@ -1324,6 +1345,7 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
 			loadh(fb, 1, buf[b][1], fix[b][1]);
 		}
 	}
+	sgh_clear(L);
 	const bool nocentre = p.dbg == 15;	/* A/B: loads only, no centre and no start barrier */
 	static_assert(!SGH_CENTER2W || SGH_CENTER == 2 * MB, "two half blocks make the centre sample");
 	if (SGH_CENTER2W && !nocentre) {
@@ -1499,13 +1521,8 @@ k_stack_hist(SgStackParams p, const int *__restrict__ tab, const int4 *__restric
 	F.xa2 = (uint32_t)(x0 + 2 * lane) * 2u;
 	F.x02 = (uint32_t)x0 * 2u;
 
-	for (int i = tid; i < 2 * NI * SGH_HROWS * 64; i += 64 * WAVES)
-		(&L.h[0][0][0])[i] = 0;
-	for (int i = tid; i < COLS; i += 64 * WAVES) {
-		L.nz[i] = 0;
-		L.ns[i] = 0;
-	}
-	/* no barrier here: sgh_build issues its first loads, then its barrier covers the clear */
+	/* the histogram and the zero / 65535 counters are cleared by the build right after it has
+	 * issued its first frame loads (sgh_clear), and its start barrier covers the clear */
 	/* A/B timeline (SG_HIST_DBG=11, NI = 2): per tile, s_memrealtime (100 MHz) at entry,
 	 * after the build barrier and at the end of every wave's finish, written into the
 	 * output buffer as u64 [tile][4] (the image is garbage in this mode) */
