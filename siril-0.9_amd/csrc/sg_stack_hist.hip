@@ -1158,7 +1158,9 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
  * loads are issued, so their latency covers it; the build's start barrier orders it before
  * the first atomic) */
 template <int NI>
-__device__ __forceinline__ void sgh_clear(SghLds<NI> &L) {
+__device__ __forceinline__ void sgh_clear(SghLds<NI> &L, bool wait_prev) {
+	if (wait_prev)
+		__syncthreads();	/* the previous tile's finish is done with L */
 	constexpr int NH = 2 * NI * SGH_HROWS * 64 / 4, NC = 128 * NI / 4, T = 256 * NI;
 	uint4 *h = (uint4 *)&L.h[0][0][0];
 	const uint4 z = make_uint4(0u, 0u, 0u, 0u);
@@ -1184,7 +1186,7 @@ __device__ __forceinline__ void sgh_clear(SghLds<NI> &L) {
 template <bool EDGE, int NBUF, int NORM, int NI>
 __device__ __forceinline__ void sgh_build(const SgStackParams &p, const SghRo &ro, SghLds<NI> &L, const SghFrame &F,
 		int wave, int lane,
-		uint32_t (&lo2)[NI], uint32_t (&nonzero)[NI], uint32_t (&nsat)[NI], int &counted) {
+		uint32_t (&lo2)[NI], uint32_t (&nonzero)[NI], uint32_t (&nsat)[NI], int &counted, bool wait_prev) {
 	constexpr int M = 16;		/* frames per block */
 	constexpr int WAVES = SGH_WAVES_PER_NI * NI;
 	constexpr int STEP = M * WAVES;
@@ -1212,7 +1214,7 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, const SghRo &r
 			loadblk(f[k], buf[k], fix[k]);
 		}
 	}
-	sgh_clear(L);
+	sgh_clear(L, wait_prev);
 	if (wave == 0) {
 #pragma unroll
 		for (int i = 0; i < NI; i++) {
@@ -1309,7 +1311,8 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, const SghRo &r
 
 template <bool EDGE, int NORM, int NI, int NB>
 __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const SghRo &ro, SghLds<NI> &L, const SghFrame &F,
-		int wave, int lane, uint32_t (&lo2)[NI], uint32_t (&nonzero)[NI], uint32_t (&nsat)[NI], int &counted) {
+		int wave, int lane, uint32_t (&lo2)[NI], uint32_t (&nonzero)[NI], uint32_t (&nsat)[NI], int &counted,
+		bool wait_prev) {
 	constexpr int MB = 8;
 	constexpr int WAVES = SGH_WAVES_PER_NI * NI;
 	constexpr int STEP = 16 * WAVES;	/* frames between a wave's consecutive blocks */
@@ -1345,7 +1348,7 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
 			loadh(fb, 1, buf[b][1], fix[b][1]);
 		}
 	}
-	sgh_clear(L);
+	sgh_clear(L, wait_prev);
 	const bool nocentre = p.dbg == 15;	/* A/B: loads only, no centre and no start barrier */
 	static_assert(!SGH_CENTER2W || SGH_CENTER == 2 * MB, "two half blocks make the centre sample");
 	if (SGH_CENTER2W && !nocentre) {
@@ -1482,26 +1485,17 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
 /* REJ 2 = SIGMA, 4 = WINSORIZED; NORM 0 none, 1 additive, 2 multiplicative; NI pixel pairs
  * per lane (tile of 128 NI pixels, 4 NI waves).  Two 8-wave workgroups (69 KB of LDS each)
  * or four 4-wave ones (34.5 KB) per CU: 16 waves, at most 128 VGPRs. */
+/* one tile: bid = its index in (channel, row, 128 NI-column tile) order; wait_prev: a tile after
+ * the first one of this workgroup, whose first frame loads may be issued while other waves of
+ * the workgroup still finish the previous tile (the clear waits for them) */
 template <int REJ, int NORM, int NI>
-__global__ void __launch_bounds__(64 * SGH_WAVES_PER_NI * NI, 4)
-k_stack_hist(SgStackParams p, const int *__restrict__ tab, const int4 *__restrict__ norm,
+__device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro, SghLds<NI> &L, int bid, bool wait_prev,
 		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
 	constexpr int WAVES = SGH_WAVES_PER_NI * NI, COLS = 128 * NI;
-	SghRo ro;
-	ro.tab = tab;
-	ro.norm = norm;
-	ro.npad = p.hist_npad;
-	__shared__ SghLds<NI> L;
 	const int tid = threadIdx.x, lane = tid & 63;
 	const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 	const int ntx = (p.W + COLS - 1) / COLS;
 	const int nrows = p.row_end - p.row_begin;
-	/* XCD-aware tile order: the dispatcher deals workgroups round-robin to the 8 XCDs, so
-	 * XCD k gets a contiguous run of tiles (whole rows: neighbouring tiles share the 128-B
-	 * lines their shifted rows straddle in that XCD's L2, and the slower image-edge tiles
-	 * spread evenly instead of all landing on XCDs 0 and 7) */
-	const int nblk = (int)gridDim.x, xcd = (int)blockIdx.x & 7, q = nblk >> 3, rem = nblk & 7;
-	int bid = xcd * q + (xcd < rem ? xcd : rem) + ((int)blockIdx.x >> 3);
 	const int xt = bid % ntx;
 	bid /= ntx;
 	const int R = p.row_begin + (bid % nrows);
@@ -1548,14 +1542,14 @@ k_stack_hist(SgStackParams p, const int *__restrict__ tab, const int4 *__restric
 		__builtin_amdgcn_s_setprio(3);
 	if (NI == 1 && !SGH_HALF1) {
 		if (interior)
-			sgh_build<false, SGH_NBUF, NORM, NI>(p, ro, L, F, wave, lane, lo2, nonzero, nsat, counted);
+			sgh_build<false, SGH_NBUF, NORM, NI>(p, ro, L, F, wave, lane, lo2, nonzero, nsat, counted, wait_prev);
 		else
-			sgh_build<true, SGH_NBUF, NORM, NI>(p, ro, L, F, wave, lane, lo2, nonzero, nsat, counted);
+			sgh_build<true, SGH_NBUF, NORM, NI>(p, ro, L, F, wave, lane, lo2, nonzero, nsat, counted, wait_prev);
 	} else {
 		if (interior)
-			sgh_build_half<false, NORM, NI, SGH_NB>(p, ro, L, F, wave, lane, lo2, nonzero, nsat, counted);
+			sgh_build_half<false, NORM, NI, SGH_NB>(p, ro, L, F, wave, lane, lo2, nonzero, nsat, counted, wait_prev);
 		else
-			sgh_build_half<true, NORM, NI, SGH_NB>(p, ro, L, F, wave, lane, lo2, nonzero, nsat, counted);
+			sgh_build_half<true, NORM, NI, SGH_NB>(p, ro, L, F, wave, lane, lo2, nonzero, nsat, counted, wait_prev);
 	}
 	if (counted) {
 #pragma unroll
@@ -1617,6 +1611,33 @@ k_stack_hist(SgStackParams p, const int *__restrict__ tab, const int4 *__restric
 			tl[2] = t;
 		atomicMax((unsigned long long *)&tl[3], (unsigned long long)t);
 	}
+}
+
+/* REJ 2 = SIGMA, 4 = WINSORIZED; NORM 0 none, 1 additive, 2 multiplicative, 3 additive with the
+ * folded + 0.5; NI pixel pairs per lane (tile of 128 NI pixels, 4 NI waves).  Two 8-wave
+ * workgroups (69 KB of LDS each) or four 4-wave ones (36 KB) per CU: 16 waves, at most 128
+ * VGPRs. */
+template <int REJ, int NORM, int NI>
+__global__ void __launch_bounds__(64 * SGH_WAVES_PER_NI * NI, 4)
+k_stack_hist(SgStackParams p, const int *__restrict__ tab, const int4 *__restrict__ norm,
+		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
+	SghRo ro;
+	ro.tab = tab;
+	ro.norm = norm;
+	ro.npad = p.hist_npad;
+	__shared__ SghLds<NI> L;
+	/* XCD-aware tile order: the dispatcher deals workgroups round-robin to the 8 XCDs, so
+	 * XCD k gets a contiguous run of tiles (whole rows: neighbouring tiles share the 128-B
+	 * lines their shifted rows straddle in that XCD's L2, and the slower image-edge tiles
+	 * spread evenly instead of all landing on XCDs 0 and 7) */
+	const int nblk = (int)gridDim.x, xcd = (int)blockIdx.x & 7, q = nblk >> 3, rem = nblk & 7;
+	const int vb = xcd * q + (xcd < rem ? xcd : rem) + ((int)blockIdx.x >> 3);
+	const int ntiles = ((p.W + 128 * NI - 1) / (128 * NI)) * (p.row_end - p.row_begin) * p.C;
+	/* one tile per workgroup: stacking 2 or 4 consecutive tiles per workgroup (the next
+	 * tile's first loads overlapping the previous finish) measured 5.0 / 4.9 ms against 3.58
+	 * (scripts/gpu_r3p.sh; the tile loop also costs registers: 128 VGPRs + scratch) */
+	if (vb < ntiles)
+		sgh_tile<REJ, NORM, NI>(p, ro, L, vb, false, redo_count, redo_list);
 }
 
 template __global__ void k_stack_hist<2, 0, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
