@@ -1496,6 +1496,7 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 	const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 	const int ntx = (p.W + COLS - 1) / COLS;
 	const int nrows = p.row_end - p.row_begin;
+	/* (the divisions are off the critical path: shifts instead measured equal, scripts/gpu_r3r.sh) */
 	const int xt = bid % ntx;
 	bid /= ntx;
 	const int R = p.row_begin + (bid % nrows);
