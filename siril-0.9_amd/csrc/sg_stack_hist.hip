@@ -524,8 +524,38 @@ __device__ __forceinline__ uint32_t sgh_pk_shl(uint32_t a, int n) {
  * 64) for anything below or above the band; row t >> 2 is at byte 256 (t >> 2), i.e. byte 1
  * of t << 6 (one byte permute each), the counter byte is t & 3, so the increment is
  * 1 << 8 (t & 3) = 1 << (8 t mod 32).  Zeros and 65535s are counted per half. */
+/* The packed ops are written as vector builtins: the hazard recognizer cannot see into inline
+ * asm and pads every asm result with an s_nop before its first use (31 per 8-frame half block
+ * in the round-2 build).  The two counter constants (1, 65534 per half) come in as opaque SGPRs
+ * (sgh_opaque, set once per tile), because LLVM rewrites a packed min(v, 1) / sat(v - 65534)
+ * with literal operands into per-half compares and selects. */
+#ifndef SGH_BIN_ASM
+#define SGH_BIN_ASM 0
+#endif
+#ifndef SGH_BIN2
+#define SGH_BIN2 1	/* interior whole half blocks bin two frames at a time (sgh_bin_pair2) */
+#endif
+__device__ __forceinline__ uint32_t sgh_opaque(uint32_t k) {
+	uint32_t r;
+	asm volatile("s_mov_b32 %0, %1" : "=s"(r) : "i"(k));
+	return r;
+}
 __device__ __forceinline__ void sgh_bin_pair(uint32_t *h, uint32_t l4, uint32_t lo2, uint32_t vv,
-		uint32_t &nonzero, uint32_t &nsat) {
+		uint32_t &nonzero, uint32_t &nsat, uint32_t k1 = 0x00010001u, uint32_t ksat = 0xFFFEFFFEu) {
+#if !SGH_BIN_ASM
+	const sgh_u16x2 v16 = __builtin_bit_cast(sgh_u16x2, vv);
+	const sgh_u16x2 tt = __builtin_elementwise_min(v16 - __builtin_bit_cast(sgh_u16x2, lo2), (sgh_u16x2){256, 256});
+	const uint32_t t64 = __builtin_bit_cast(uint32_t, (sgh_u16x2)(tt << (sgh_u16x2){6, 6}));
+	const uint32_t t8 = __builtin_bit_cast(uint32_t, (sgh_u16x2)(tt << (sgh_u16x2){3, 3}));
+	const uint32_t a0 = __builtin_amdgcn_perm(t64, l4, 0x0c0c0500u), a1 = __builtin_amdgcn_perm(t64, l4, 0x0c0c0700u);
+	const uint32_t i0 = 1u << (t8 & 31u), i1 = 1u << ((t8 >> 16) & 31u);
+	atomicAdd((uint32_t *)((char *)h + a0), i0);
+	atomicAdd((uint32_t *)((char *)h + sizeof(uint32_t) * SGH_HROWS * 64 + a1), i1);
+	nonzero += __builtin_bit_cast(uint32_t, __builtin_elementwise_min(v16, __builtin_bit_cast(sgh_u16x2, k1)));
+	nsat += __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(v16, __builtin_bit_cast(sgh_u16x2, ksat)));
+#else
+	(void)k1;
+	(void)ksat;
 	const uint32_t t = sgh_pk_min(sgh_pk_sub_wrap(vv, lo2), 0x01000100u);
 	const uint32_t t64 = sgh_pk_shl(t, 6), t8 = sgh_pk_shl(t, 3);
 	const uint32_t a0 = __builtin_amdgcn_perm(t64, l4, 0x0c0c0500u), a1 = __builtin_amdgcn_perm(t64, l4, 0x0c0c0700u);
@@ -536,6 +566,37 @@ __device__ __forceinline__ void sgh_bin_pair(uint32_t *h, uint32_t l4, uint32_t 
 	 * the compiler folds the adds of consecutive frames into v_add3_u32 */
 	nonzero += sgh_pk_min(vv, 0x00010001u);
 	nsat += sgh_pk_sub_sat(vv, 0xFFFEFFFEu);
+#endif
+}
+
+/* two frames of one pixel pair, their independent packed ops interleaved: a packed op that
+ * reads the previous op's result needs a wait state (s_nop) on gfx950, the other frame's op
+ * fills it */
+__device__ __forceinline__ void sgh_bin_pair2(uint32_t *h, uint32_t l4, uint32_t lo2, uint32_t va, uint32_t vb,
+		uint32_t &nonzero, uint32_t &nsat, uint32_t k1, uint32_t ksat) {
+	const sgh_u16x2 a16 = __builtin_bit_cast(sgh_u16x2, va), b16 = __builtin_bit_cast(sgh_u16x2, vb);
+	const sgh_u16x2 l16 = __builtin_bit_cast(sgh_u16x2, lo2), c256 = {256, 256};
+	/* sched_barriers between the stages: the scheduler otherwise serialises the two frames again
+	 * (it minimises live registers) and the wait states come back */
+	const sgh_u16x2 da = a16 - l16, db = b16 - l16;
+	__builtin_amdgcn_sched_barrier(0);
+	const sgh_u16x2 ta = __builtin_elementwise_min(da, c256), tb = __builtin_elementwise_min(db, c256);
+	__builtin_amdgcn_sched_barrier(0);
+	const uint32_t a64 = __builtin_bit_cast(uint32_t, (sgh_u16x2)(ta << (sgh_u16x2){6, 6}));
+	const uint32_t b64 = __builtin_bit_cast(uint32_t, (sgh_u16x2)(tb << (sgh_u16x2){6, 6}));
+	const uint32_t a8 = __builtin_bit_cast(uint32_t, (sgh_u16x2)(ta << (sgh_u16x2){3, 3}));
+	const uint32_t b8 = __builtin_bit_cast(uint32_t, (sgh_u16x2)(tb << (sgh_u16x2){3, 3}));
+	__builtin_amdgcn_sched_barrier(0);
+	char *const h1 = (char *)h + sizeof(uint32_t) * SGH_HROWS * 64;
+	atomicAdd((uint32_t *)((char *)h + __builtin_amdgcn_perm(a64, l4, 0x0c0c0500u)), 1u << (a8 & 31u));
+	atomicAdd((uint32_t *)(h1 + __builtin_amdgcn_perm(a64, l4, 0x0c0c0700u)), 1u << ((a8 >> 16) & 31u));
+	atomicAdd((uint32_t *)((char *)h + __builtin_amdgcn_perm(b64, l4, 0x0c0c0500u)), 1u << (b8 & 31u));
+	atomicAdd((uint32_t *)(h1 + __builtin_amdgcn_perm(b64, l4, 0x0c0c0700u)), 1u << ((b8 >> 16) & 31u));
+	const sgh_u16x2 k1v = __builtin_bit_cast(sgh_u16x2, k1), ksv = __builtin_bit_cast(sgh_u16x2, ksat);
+	nonzero += __builtin_bit_cast(uint32_t, __builtin_elementwise_min(a16, k1v)) +
+		__builtin_bit_cast(uint32_t, __builtin_elementwise_min(b16, k1v));
+	nsat += __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(a16, ksv)) +
+		__builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(b16, ksv));
 }
 
 /* ------------------------------------------------------------------------------------
@@ -1319,6 +1380,7 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
 	const int N = p.N;
 	uint32_t *const h = &L.h[0][0][0];
 	const uint32_t l4 = (uint32_t)lane * 4u;
+	const uint32_t k1 = sgh_opaque(0x00010001u), ksat = sgh_opaque(0xFFFEFFFEu);
 	uint32_t buf[NB][2][MB][NI], fix[NB][2][NI];
 	SghTab16 T;
 	/* half hh (frames f16 + 8 hh ..) of the block at f16, bounds-checked unless whole */
@@ -1422,6 +1484,13 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
 #pragma unroll
 				for (int i = 0; i < NI; i++)
 					nonzero[i] ^= raw[m][i];
+		} else if (SGH_BIN2 && !NORM && !EDGE && whole) {
+#pragma unroll
+			for (int m = 0; m < MB; m += 2)
+#pragma unroll
+				for (int i = 0; i < NI; i++)
+					sgh_bin_pair2(h + i * (2 * SGH_HROWS * 64), l4, lo2[i], raw[m][i], raw[m + 1][i], nonzero[i],
+							nsat[i], k1, ksat);
 		} else {
 #pragma unroll
 			for (int m = 0; m < MB; m++) {
@@ -1434,7 +1503,7 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
 						uint32_t v = sgh_fixup<EDGE>(raw[m][i], fx[i], m);
 						if (NORM)
 							v = sgh_norm_pair<NORM, EDGE>(v, a, b, fx[i], m);
-						sgh_bin_pair(h + i * (2 * SGH_HROWS * 64), l4, lo2[i], v, nonzero[i], nsat[i]);
+						sgh_bin_pair(h + i * (2 * SGH_HROWS * 64), l4, lo2[i], v, nonzero[i], nsat[i], k1, ksat);
 					}
 				}
 			}
