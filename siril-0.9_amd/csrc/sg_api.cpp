@@ -81,16 +81,19 @@ extern "C" void sg_shutdown(sg_ctx *ctx) {
 	for (auto &d : ctx->dev) {
 		(void)hipSetDevice(d.id);
 		(void)hipStreamSynchronize(d.stream);
-		SgBuf *bufs[] = {&d.flag_list, &d.flag_map, &d.flag_count, &d.rej, &d.sum_buf, &d.maxim,
-			&d.shifts, &d.norm, &d.tables, &d.scratch, &d.frames, &d.out, &d.reg_sel, &d.reg_spec,
+		SgBuf *bufs[] = {&d.flag_list, &d.flag_map, &d.sum_buf, &d.scratch, &d.frames, &d.out, &d.reg_sel, &d.reg_spec,
 			&d.reg_work, &d.reg_tw, &d.reg_best, &d.reg_qbuf, &d.reg_qacc, &d.redo, &d.zeros,
-			&d.io_raw, &d.io_bad, &d.warp_tab, &d.stats_buf};
+			&d.io_raw, &d.io_bad, &d.warp_tab, &d.stats_buf, &d.inb, &d.ctr};
 		for (SgBuf *b : bufs)
 			if (b->p)
 				(void)hipFree(b->p);
 		for (int k = 0; k < 2; k++)
 			if (d.pinned[k])
 				(void)hipHostFree(d.pinned[k]);
+		if (d.stage_h)
+			(void)hipHostFree(d.stage_h);
+		if (d.ctr_h)
+			(void)hipHostFree(d.ctr_h);
 		for (int k = 0; k < 2; k++) {
 			if (d.io_stage[k])
 				(void)hipHostFree(d.io_stage[k]);
@@ -293,15 +296,17 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 
 	/* per-frame constants: shifts + normalisation coefficients */
 	const int Npad = (N + 15) & ~15;	/* histogram-path table: 64-byte aligned, padded */
-	/* layout: c1[Npad] int, sx2[Npad] int16, shiftx[N], shifty[N] */
-	HIPCHK(ensure(dv.shifts, sizeof(int) * (Npad + Npad / 2 + 2 * N)));
-	HIPCHK(ensure(dv.norm, sizeof(double) * (3 * N + 2 * Npad)));
+	/* layout: c1[Npad] int, sx2[Npad] int16, shiftx[N], shifty[N]; the call's inputs (this
+	 * table, the normalisation coefficients, the chain tables) reach the device in one copy
+	 * (flush_inputs, right before the first kernel) */
+	std::vector<int> sh(Npad + Npad / 2 + 2 * N, 0);
+	std::vector<double> nm;
+	std::vector<int> tables;
 	/* the histogram path addresses a frame plane with 32-bit offsets: (R - sy) W 2 must fit */
 	bool hist_addr_ok = (int64_t)H * W * 2 <= (1ll << 30);
 	{
 		/* per frame c1 = shifty*W*2 + 2*shiftx and sx2 = 2*shiftx for the histogram path
 		 * (zeros when there is no registration data), then the plain shift arrays */
-		std::vector<int> sh(Npad + Npad / 2 + 2 * N, 0);
 		int16_t *sx2 = (int16_t *)(sh.data() + Npad);
 		p.hist_maxsx = 0;
 		for (int i = 0; p.use_shift && i < N; i++) {
@@ -318,16 +323,9 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			memcpy(sh.data() + Npad + Npad / 2, d->shiftx, sizeof(int) * N);
 			memcpy(sh.data() + Npad + Npad / 2 + N, d->shifty, sizeof(int) * N);
 		}
-		HIPCHK(hipMemcpyAsync(dv.shifts.p, sh.data(), sizeof(int) * sh.size(), hipMemcpyHostToDevice, s));
-		p.hist_tab = (const int *)dv.shifts.p;
-		p.hist_npad = Npad;
-		if (p.use_shift) {
-			p.shiftx = p.hist_tab + Npad + Npad / 2;
-			p.shifty = p.shiftx + N;
-		}
 	}
 	if (p.normalize) {
-		std::vector<double> nm(3 * N);
+		nm.resize(3 * N);
 		for (int i = 0; i < N; i++) {
 			nm[i] = d->offset ? d->offset[i] : 0.0;
 			nm[N + i] = d->mul ? d->mul[i] : 1.0;
@@ -351,29 +349,83 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			nm[3 * N + 2 * i] = nm[2 * N + i];
 			nm[3 * N + 2 * i + 1] = additive ? (fold ? nm[i] - 0.5 : nm[i]) : nm[N + i];
 		}
-		HIPCHK(hipMemcpyAsync(dv.norm.p, nm.data(), sizeof(double) * nm.size(), hipMemcpyHostToDevice, s));
-		p.hist_norm = (const double *)dv.norm.p + 3 * N;
-		p.offset = (const double *)dv.norm.p;
-		p.mul = p.offset + N;
-		p.scale = p.offset + 2 * N;
 	}
-	HIPCHK(ensure(dv.rej, sizeof(unsigned long long) * SG_REJ_SHARDS * 6));
-	HIPCHK(ensure(dv.flag_count, 64));
-	HIPCHK(ensure(dv.maxim, 64));
-	HIPCHK(hipMemsetAsync(dv.rej.p, 0, sizeof(unsigned long long) * SG_REJ_SHARDS * 6, s));
-	HIPCHK(hipMemsetAsync(dv.flag_count.p, 0, 64, s));
-	if (sum_mode == SUM_WHOLE || sum_mode == SUM_FIRST_BAND)
-		HIPCHK(hipMemsetAsync(dv.maxim.p, 0, 64, s));
-	p.rej = (unsigned long long *)dv.rej.p;
-	p.flag_count = (unsigned int *)dv.flag_count.p;
+	SgChainTables ct;
+	memset(&ct, 0, sizeof ct);
+	/* one pinned host block -> one device block; sets the kernels' pointers into it */
+	auto flush_inputs = [&]() -> int {
+		const size_t b_sh = sizeof(int) * sh.size(), o_nm = (b_sh + 255) & ~(size_t)255;
+		const size_t b_nm = sizeof(double) * nm.size(), o_tb = (o_nm + b_nm + 255) & ~(size_t)255;
+		const size_t tot = o_tb + sizeof(int) * tables.size();
+		if (dv.stage_pending) {	/* an earlier call's copy may still read the host block */
+			HIPCHK(hipEventSynchronize(dv.ev[3]));
+			dv.stage_pending = false;
+		}
+		if (dv.stage_h_size < tot) {
+			if (dv.stage_h)
+				(void)hipHostFree(dv.stage_h);
+			dv.stage_h = nullptr;
+			dv.stage_h_size = 0;
+			HIPCHK(hipHostMalloc(&dv.stage_h, tot));
+			dv.stage_h_size = tot;
+		}
+		HIPCHK(ensure(dv.inb, tot));
+		char *hb = (char *)dv.stage_h;
+		memcpy(hb, sh.data(), b_sh);
+		if (b_nm)
+			memcpy(hb + o_nm, nm.data(), b_nm);
+		if (!tables.empty())
+			memcpy(hb + o_tb, tables.data(), sizeof(int) * tables.size());
+		HIPCHK(hipMemcpyAsync(dv.inb.p, dv.stage_h, tot, hipMemcpyHostToDevice, s));
+		HIPCHK(hipEventRecord(dv.ev[3], s));
+		dv.stage_pending = true;
+		const char *db = (const char *)dv.inb.p;
+		p.hist_tab = (const int *)db;
+		p.hist_npad = Npad;
+		if (p.use_shift) {
+			p.shiftx = p.hist_tab + Npad + Npad / 2;
+			p.shifty = p.shiftx + N;
+		}
+		if (p.normalize) {
+			p.offset = (const double *)(db + o_nm);
+			p.mul = p.offset + N;
+			p.scale = p.offset + 2 * N;
+			p.hist_norm = p.offset + 3 * N;
+		}
+		if (!tables.empty()) {
+			const int *tb = (const int *)(db + o_tb);
+			ct.blk_of_row = tb;
+			ct.blk_channel = tb + (size_t)C * H;
+			ct.blk_start = ct.blk_channel + ct.nblocks;
+			ct.blk_end = ct.blk_start + ct.nblocks;
+			ct.blk_first = ct.blk_end + ct.nblocks;
+		}
+		return SG_OK;
+	};
+	/* counters: rejection shards, then {flag count, walk fault, redo count} and the sum maximum
+	 * 64 bytes further (kept across the bands of a streamed SUM); one memset, one read-back */
+	const size_t REJB = sizeof(unsigned long long) * SG_REJ_SHARDS * 6, CTRB = REJB + 128;
+	HIPCHK(ensure(dv.ctr, CTRB));
+	if (!dv.ctr_h)
+		HIPCHK(hipHostMalloc(&dv.ctr_h, CTRB));
+	const bool clear_max = sum_mode == SUM_WHOLE || sum_mode == SUM_FIRST_BAND;
+	HIPCHK(hipMemsetAsync(dv.ctr.p, 0, clear_max ? CTRB : REJB + 64, s));
+	p.rej = (unsigned long long *)dv.ctr.p;
+	p.flag_count = (unsigned int *)((char *)dv.ctr.p + REJB);
 	p.walk_fault = p.flag_count + 1;
-	p.maxim = (unsigned int *)dv.maxim.p;
+	p.maxim = (unsigned int *)((char *)dv.ctr.p + REJB + 64);
+	const unsigned int *ctr_flags = (const unsigned int *)((const char *)dv.ctr_h + REJB);
+	bool have_counts = false;
+	auto readback = [&]() -> int {
+		HIPCHK(hipMemcpyAsync(dv.ctr_h, dv.ctr.p, CTRB, hipMemcpyDeviceToHost, s));
+		HIPCHK(hipStreamSynchronize(s));
+		dv.stage_pending = false;
+		have_counts = true;
+		return SG_OK;
+	};
 
 	const bool sorted = (d->method == SG_STACK_MEDIAN) ||
 		(d->method == SG_STACK_MEAN && d->rejection != SG_NO_REJEC);
-	std::vector<int> tables;
-	SgChainTables ct;
-	memset(&ct, 0, sizeof ct);
 	if (sorted) {
 		const int nreg = pick_nreg(N);
 		unsigned int *late_redo = nullptr, *late_list = nullptr;	/* redo list routed on the device */
@@ -411,15 +463,9 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			for (long b = b0; b < b1; b++)
 				bfi[b] = (int)b0;
 		}
-		HIPCHK(ensure(dv.tables, sizeof(int) * tables.size()));
-		HIPCHK(hipMemcpyAsync(dv.tables.p, tables.data(), sizeof(int) * tables.size(), hipMemcpyHostToDevice, s));
-		const int *tb = (const int *)dv.tables.p;
-		ct.blk_of_row = tb;
-		ct.blk_channel = tb + (size_t)C * H;
-		ct.blk_start = ct.blk_channel + nb;
-		ct.blk_end = ct.blk_start + nb;
-		ct.blk_first = ct.blk_end + nb;
 		ct.nblocks = nb;
+		if (int rc = flush_inputs())
+			return rc;
 
 		const int ntx = (W + SG_TILE_W - 1) / SG_TILE_W;
 		const size_t nblk = (size_t)ntx * nrows * C;
@@ -432,9 +478,8 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			N >= 16 && N <= 65535 && hist_addr_ok;
 		if (hist) {
 			HIPCHK(ensure(dv.redo, sizeof(unsigned int) * (npix_launch + 16)));
-			unsigned int *redo_count = (unsigned int *)dv.redo.p;
-			unsigned int *redo_list = redo_count + 16;
-			HIPCHK(hipMemsetAsync(redo_count, 0, sizeof(unsigned int), s));
+			unsigned int *redo_count = p.flag_count + 2;	/* cleared with the counters */
+			unsigned int *redo_list = (unsigned int *)dv.redo.p + 16;
 			HIPCHK(hipEventRecord(dv.ev[0], s));
 			/* NORM: 0 none, 1 additive (round(v scale - offset)), 2 multiplicative (round(v scale mul)),
 			 * 3 additive with the folded + 0.5 */
@@ -527,12 +572,15 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		if (int rc = launch_tail())
 			return rc;
 		if (late_redo) {
-			/* the device left a long redo list alone: the sorted kernel, then the tail again */
-			unsigned int nredo = 0;
-			HIPCHK(hipMemcpyAsync(&nredo, late_redo, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
-			HIPCHK(hipStreamSynchronize(s));
+			/* the redo count comes back with the counters (no extra round trip); only a long
+			 * list the device left alone needs the sorted kernel, the tail and a second read */
+			HIPCHK(hipEventRecord(dv.ev[2], s));
+			if (int rc = readback())
+				return rc;
+			const unsigned int nredo = ctr_flags[2];
 			ctx->stats.chain_pixels = nredo;
 			if (nredo > SG_REDO_REPLAY_MAX) {
+				have_counts = false;
 				HIPCHK(launch_sorted(nreg, true, dim3((nredo + SG_TILE_W - 1) / SG_TILE_W), lds, s, p, late_list,
 						late_redo));
 				ctx->stats.launches++;
@@ -541,6 +589,8 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			}
 		}
 	} else {
+		if (int rc = flush_inputs())
+			return rc;
 		if (d->method == SG_STACK_SUM) {
 			HIPCHK(ensure(dv.sum_buf, sizeof(uint32_t) * npix_img));
 			p.sum_buf = (uint32_t *)dv.sum_buf.p;
@@ -573,25 +623,18 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			ctx->stats.launches++;
 		}
 	}
-	HIPCHK(hipEventRecord(dv.ev[2], s));
-	/* counters back to the host */
-	std::vector<unsigned long long> shards(SG_REJ_SHARDS * 6);
-	unsigned int cnt[3] = {0, 0, 0};	/* flag count, walk fault, sum maximum */
-	HIPCHK(hipMemcpyAsync(shards.data(), dv.rej.p, sizeof(unsigned long long) * shards.size(), hipMemcpyDeviceToHost, s));
-	HIPCHK(hipMemcpyAsync(cnt, dv.flag_count.p, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, s));
-	HIPCHK(hipMemcpyAsync(cnt + 2, dv.maxim.p, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
-	HIPCHK(hipStreamSynchronize(s));
+	if (!have_counts) {
+		HIPCHK(hipEventRecord(dv.ev[2], s));
+		if (int rc = readback())	/* counters back to the host */
+			return rc;
+	}
+	const unsigned long long *shards = (const unsigned long long *)dv.ctr_h;
+	const unsigned int cnt[3] = {ctr_flags[0], ctr_flags[1], ctr_flags[16]};	/* flag count, walk fault, sum maximum */
 	if (cnt[1])
 		return set_err(ctx, SG_ERR_GENERIC, "a first-pass early break needs the stale rejected[] of a pixel "
 				"whose frame rows are not resident; make the full frames resident%s%.0ld", "", 0);
 	if (p.dbg == 12)
 		sg_dbg_why_dump(s);
-	if (p.dbg == 16 && dv.redo.p) {	/* A/B: SIGMA fast finish queue (sg_stack_hist.hip) */
-		unsigned long long q = 0;
-		(void)hipMemcpy(&q, (unsigned int *)dv.redo.p + 8, sizeof q, hipMemcpyDeviceToHost);
-		(void)hipMemset((unsigned int *)dv.redo.p + 8, 0, sizeof q);
-		fprintf(stderr, "fast finish: %llu queued pixels in %llu tiles\n", q & ((1ull << 40) - 1), q >> 40);
-	}
 	float ms = 0.f, ms2 = 0.f;
 	HIPCHK(hipEventElapsedTime(&ms, dv.ev[0], dv.ev[1]));
 	HIPCHK(hipEventElapsedTime(&ms2, dv.ev[0], dv.ev[2]));

@@ -21,11 +21,22 @@ struct SgDevice {
 	int id = 0;
 	hipStream_t stream = nullptr;
 	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-	SgBuf flag_list, flag_map, flag_count, rej, sum_buf, maxim, shifts, norm, tables, scratch, frames, out, stats_buf;
+	SgBuf flag_list, flag_map, sum_buf, scratch, frames, out, stats_buf;
 	/* registration workspaces (sg_register.hip) */
 	SgBuf reg_sel, reg_spec, reg_work, reg_tw, reg_best, reg_qbuf, reg_qacc;
 	SgBuf redo;	/* redo list of the histogram stacking path */
 	SgBuf zeros;	/* zero page for out-of-frame sample loads */
+	/* stacking call inputs (shift table, normalisation coefficients, chain tables) packed into
+	 * one pinned host block and one device block: one H2D copy per call; ev[3] marks the copy
+	 * done before the host block is rewritten */
+	SgBuf inb;
+	void *stage_h = nullptr;
+	size_t stage_h_size = 0;
+	bool stage_pending = false;
+	/* stacking counters (rejection shards, flag / redo counts, sum maximum) in one device block,
+	 * cleared by one memset and read back by one D2H copy into ctr_h (pinned) */
+	SgBuf ctr;
+	void *ctr_h = nullptr;
 	uint16_t *pinned[2] = {nullptr, nullptr};
 	size_t pinned_size = 0;
 	/* file decode path (sg_io.hip): pinned staging of raw frames, device raw buffers */

@@ -1160,6 +1160,70 @@ __device__ void replay_sort(uint16_t *a, int n, int lane) {
 		}
 }
 
+/* the same sort with the array in registers: element e = 64 k + lane in x[k]; partners 64 or
+ * more apart are in the lane's own registers, closer ones one lane shuffle away, so a stage is
+ * KM independent compare-exchanges instead of KM dependent LDS round trips (the LDS version
+ * above dominated the replay of a 512-frame pixel).  The sorted array is unique for u16 keys,
+ * so the result is the same array. */
+template <int KM>
+__device__ __forceinline__ void replay_sort_reg(uint16_t *a, int n, int lane) {
+	constexpr int P = 64 * KM;
+	uint32_t x[KM];
+#pragma unroll
+	for (int k = 0; k < KM; k++) {
+		const int e = 64 * k + lane;
+		x[k] = e < n ? a[e] : 0xFFFFu;
+	}
+#pragma unroll
+	for (int kk = 2; kk <= P; kk <<= 1) {
+#pragma unroll
+		for (int j = kk >> 1; j > 0; j >>= 1) {
+			if (j >= 64) {
+				const int jr = j >> 6;
+#pragma unroll
+				for (int k = 0; k < KM; k++) {
+					if ((k & jr) == 0) {
+						const bool up = ((64 * k + lane) & kk) == 0;
+						const uint32_t u = x[k], v = x[k | jr];
+						const uint32_t mn = u < v ? u : v, mx = u < v ? v : u;
+						x[k] = up ? mn : mx;
+						x[k | jr] = up ? mx : mn;
+					}
+				}
+			} else {
+				const bool lower = (lane & j) == 0;
+#pragma unroll
+				for (int k = 0; k < KM; k++) {
+					const bool up = ((64 * k + lane) & kk) == 0;
+					const uint32_t y = (uint32_t)__shfl_xor((int)x[k], j, 64);
+					const uint32_t mn = x[k] < y ? x[k] : y, mx = x[k] < y ? y : x[k];
+					x[k] = (lower == up) ? mn : mx;
+				}
+			}
+		}
+	}
+#pragma unroll
+	for (int k = 0; k < KM; k++) {
+		const int e = 64 * k + lane;
+		if (e < n)
+			a[e] = (uint16_t)x[k];
+	}
+	__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+__device__ __forceinline__ void replay_sort_any(uint16_t *a, int n, int lane) {
+	if (n <= 64)
+		replay_sort_reg<1>(a, n, lane);
+	else if (n <= 128)
+		replay_sort_reg<2>(a, n, lane);
+	else if (n <= 256)
+		replay_sort_reg<4>(a, n, lane);
+	else if (n <= 512)
+		replay_sort_reg<8>(a, n, lane);
+	else
+		replay_sort(a, n, lane);
+}
+
 __device__ __forceinline__ double replay_median(const uint16_t *a, int n) {
 	const int lhs = (n - 1) / 2, rhs = n / 2;
 	if (lhs == rhs)
@@ -1204,7 +1268,7 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 		}
 		const uint16_t *src = iter == 1 ? L.orig : L.stack;	/* this pass's sd input */
 		if (iter == 1)
-			replay_sort(L.stack, N, lane);
+			replay_sort_any(L.stack, N, lane);
 		double median = replay_median(L.stack, N);
 		if (type == 4) {
 			for (int j = lane; j < N; j += 64)

@@ -392,6 +392,10 @@ __device__ __forceinline__ void sgh_tab16(const SghRo &ro, int f0, SghTab16 &T) 
 	}
 }
 
+/* cache policy bits of the frame loads (A/B builds: -DSGH_LOAD_AUX=...; 0 = default policy) */
+#ifndef SGH_LOAD_AUX
+#define SGH_LOAD_AUX 0
+#endif
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t sgh_rsrc(const char *base, uint32_t nrec) {
 	return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)nrec, 0x00020000);
 }
@@ -436,10 +440,10 @@ __device__ __forceinline__ void sgh_loadblk(const SghFrame &F, const SghTab16 &T
 			 * bounds-checks the unsigned sum voffset + soffset without wrapping
 			 * (tools/soffset_probe.hip), so the latter (2^32 + start as unsigned) reads 0 */
 			if (EDGE)
-				dst[m][i] = __builtin_amdgcn_raw_buffer_load_b32(sgh_rsrc(b, nrec), (int)off, 0, 0);
+				dst[m][i] = __builtin_amdgcn_raw_buffer_load_b32(sgh_rsrc(b, nrec), (int)off, 0, SGH_LOAD_AUX);
 			else
 				dst[m][i] = __builtin_amdgcn_raw_buffer_load_b32(sgh_rsrc(b, nrec), (int)(xa2 - F.x02),
-						(int)(k + F.x02), 0);
+						(int)(k + F.x02), SGH_LOAD_AUX);
 		}
 		b += F.fstride2;
 	}
