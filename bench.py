@@ -36,7 +36,7 @@ def parse():
                     help="sigma = BASELINE configs[2] (the metric's configuration, default); "
                          "register-mean = configs[1]; winsorized-rgb = configs[4] at one GPU")
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--frames", type=int, default=512)
     ap.add_argument("--width", type=int, default=4096)
     ap.add_argument("--height", type=int, default=4096)

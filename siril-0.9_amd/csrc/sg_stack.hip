@@ -147,6 +147,9 @@ __device__ __forceinline__ double exact_sd(int n, uint64_t S, uint64_t SS, bool 
 
 /* A/B diagnostics (SG_HIST_DBG=12): why pixels leave the sorted path */
 __device__ unsigned int g_sg_why[32];
+/* k_stack_replay timing (SG_HIST_DBG=12): max cycles of a pixel (total, gather, sort), pixels,
+ * fp80 sd recomputations, passes (sums) */
+__device__ unsigned long long g_sg_rprof[16];
 #define SG_WHY(k) (atomicAdd(&g_sg_why[k], 1u), SG_CLS_LITERAL)
 
 struct SgRejState {
@@ -1090,12 +1093,17 @@ __device__ __forceinline__ void gather_stack(const SgStackParams &p, int64_t pix
  * it sorted, and quicksort_s of a sorted array is the identity; the Winsorized copy stays
  * sorted under clamping.
  */
+#define SG_REPLAY_FASTN 512	/* SIGMA fast passes (replay_sigma_fast) up to this many frames */
 struct SgReplayLds {
 	uint16_t stack[SG_REPLAY_MAXN];
 	uint16_t w[SG_REPLAY_MAXN];
 	uint16_t wprev[SG_REPLAY_MAXN];	/* w before the current clamp (exact-mode recomputation) */
 	uint16_t orig[SG_REPLAY_MAXN];	/* the first pass's stack in frame order */
 	int8_t rej[SG_REPLAY_MAXN];
+	uint32_t p1[SG_REPLAY_FASTN + 1];	/* prefix sums of the sorted stack (SIGMA fast passes) */
+	unsigned long long p2[SG_REPLAY_FASTN + 1];
+	int nsd, npass, handover;	/* fp80 recomputations, passes, fast-path handovers (SG_HIST_DBG=12 timing) */
+	unsigned long long t_sort, t_fast;
 };
 
 __device__ __forceinline__ int wave_excl_scan(int v, int lane) {
@@ -1165,6 +1173,19 @@ __device__ void replay_sort(uint16_t *a, int n, int lane) {
  * KM independent compare-exchanges instead of KM dependent LDS round trips (the LDS version
  * above dominated the replay of a 512-frame pixel).  The sorted array is unique for u16 keys,
  * so the result is the same array. */
+template <int KM, int JR>
+__device__ __forceinline__ void replay_cx_reg(uint32_t (&x)[KM], int kk, int lane) {
+#pragma unroll
+	for (int k = 0; k < KM; k++) {
+		if ((k & JR) == 0 && (k | JR) < KM) {
+			const bool up = ((64 * k + lane) & kk) == 0;
+			const uint32_t u = x[k], v = x[k | JR];
+			const uint32_t mn = u < v ? u : v, mx = u < v ? v : u;
+			x[k] = up ? mn : mx;
+			x[k | JR] = up ? mx : mn;
+		}
+	}
+}
 template <int KM>
 __device__ __forceinline__ void replay_sort_reg(uint16_t *a, int n, int lane) {
 	constexpr int P = 64 * KM;
@@ -1174,22 +1195,24 @@ __device__ __forceinline__ void replay_sort_reg(uint16_t *a, int n, int lane) {
 		const int e = 64 * k + lane;
 		x[k] = e < n ? a[e] : 0xFFFFu;
 	}
-#pragma unroll
+	/* the stage loops stay loops (the kernel runs once per call, its code cold in the
+	 * instruction cache: a fully unrolled network is ~2 K instructions); only the per-register
+	 * work of a stage is unrolled */
+#pragma unroll 1
 	for (int kk = 2; kk <= P; kk <<= 1) {
-#pragma unroll
+#pragma unroll 1
 		for (int j = kk >> 1; j > 0; j >>= 1) {
 			if (j >= 64) {
-				const int jr = j >> 6;
-#pragma unroll
-				for (int k = 0; k < KM; k++) {
-					if ((k & jr) == 0) {
-						const bool up = ((64 * k + lane) & kk) == 0;
-						const uint32_t u = x[k], v = x[k | jr];
-						const uint32_t mn = u < v ? u : v, mx = u < v ? v : u;
-						x[k] = up ? mn : mx;
-						x[k | jr] = up ? mx : mn;
-					}
-				}
+				if (j == 64)
+					replay_cx_reg<KM, 1>(x, kk, lane);
+				else if (j == 128)
+					replay_cx_reg<KM, 2>(x, kk, lane);
+				else if (j == 256)
+					replay_cx_reg<KM, 4>(x, kk, lane);
+				else if (j == 512)
+					replay_cx_reg<KM, 8>(x, kk, lane);
+				else
+					replay_cx_reg<KM, 16>(x, kk, lane);
 			} else {
 				const bool lower = (lane & j) == 0;
 #pragma unroll
@@ -1212,13 +1235,7 @@ __device__ __forceinline__ void replay_sort_reg(uint16_t *a, int n, int lane) {
 }
 
 __device__ __forceinline__ void replay_sort_any(uint16_t *a, int n, int lane) {
-	if (n <= 64)
-		replay_sort_reg<1>(a, n, lane);
-	else if (n <= 128)
-		replay_sort_reg<2>(a, n, lane);
-	else if (n <= 256)
-		replay_sort_reg<4>(a, n, lane);
-	else if (n <= 512)
+	if (n <= 512)	/* one instance: smaller stacks sort padded (less code to fetch) */
 		replay_sort_reg<8>(a, n, lane);
 	else
 		replay_sort(a, n, lane);
@@ -1239,6 +1256,189 @@ __device__ __forceinline__ double replay_gsl_sd(const uint16_t *a, int n, int la
 		v = lit_sd(a, n);
 	return __shfl(v, 0, 64);
 }
+__device__ __forceinline__ double replay_gsl_sd(SgReplayLds &L, const uint16_t *a, int n, int lane) {
+	if (lane == 0)
+		L.nsd++;
+	return replay_gsl_sd(a, n, lane);
+}
+
+/* sg_gather of a pixel's N <= SG_REPLAY_FASTN samples with every load in flight at once: the
+ * shifts of all 8 frames of a lane first, then all 8 samples (the plain loop waits for two
+ * dependent loads per frame) */
+__device__ __forceinline__ void replay_gather_batched(const SgStackParams &p, uint16_t *dst, int c, int R, int x,
+		int lane) {
+	constexpr int KM = SG_REPLAY_FASTN / 64;
+	int sx[KM], sy[KM];
+#pragma unroll
+	for (int k = 0; k < KM; k++) {
+		const int f = 64 * k + lane;
+		sx[k] = sy[k] = 0;
+		if (p.use_shift && f < p.N) {
+			sx[k] = p.shiftx[f];
+			sy[k] = p.shifty[f];
+		}
+	}
+	uint16_t v[KM];
+	bool colok[KM];
+#pragma unroll
+	for (int k = 0; k < KM; k++) {
+		const int f = 64 * k + lane;
+		const int sr = R - sy[k], sc = x - sx[k];
+		colok[k] = (unsigned)sc < (unsigned)p.W;
+		v[k] = 0;
+		if (f < p.N && colok[k] && (unsigned)sr < (unsigned)p.H)
+			v[k] = p.frames[(int64_t)f * p.frame_stride + (int64_t)c * p.plane_stride + (int64_t)sr * p.W + sc];
+	}
+#pragma unroll
+	for (int k = 0; k < KM; k++) {
+		const int f = 64 * k + lane;
+		if (f < p.N)
+			dst[f] = colok[k] ? sg_normalize(p, f, v[k]) : (uint16_t)0;
+	}
+}
+
+__device__ __forceinline__ unsigned long long wave_excl_scan_u64(unsigned long long v, int lane) {
+	unsigned long long x = v;
+#pragma unroll
+	for (int o = 1; o < 64; o <<= 1) {
+		const unsigned long long t = __shfl_up(x, o, 64);
+		if (lane >= o)
+			x += t;
+	}
+	return x - v;
+}
+
+/* SIGMA passes on the sorted stack while no decision is ambiguous and no early break fires:
+ * the stack is sorted, low clips are its smallest values and high clips its largest, so
+ * without a break every pass trims a prefix and a suffix and the kept set stays the
+ * contiguous range [lo, hi) of the sorted array.  Moments come from prefix sums formed once,
+ * the median is two reads, the clip counts are ballots; decisions are the general loop's, in
+ * the same double arithmetic with the same band.  rejected[] is written as the general loop
+ * leaves it (this pass's decisions by position), so the loop can hand a pass it cannot decide
+ * (returns 0: ambiguous, or an early break) to the general loop with the state it expects:
+ * the range is compacted to the front and N, r, passes and counters carry over.
+ * Returns 1 when the pixel is finished (value and counters set). */
+__device__ int replay_sigma_fast(SgReplayLds &L, int &N, int &r, int &iter, double sl, double sh, int lane,
+		uint32_t &clo, uint32_t &chi, uint16_t *value) {
+	constexpr int KM = SG_REPLAY_FASTN / 64;
+	{	/* prefix sums over the sorted stack, 8 consecutive samples per lane */
+		uint32_t a = 0;
+		unsigned long long b = 0;
+		uint32_t v[KM];
+#pragma unroll
+		for (int k = 0; k < KM; k++) {
+			const int e = KM * lane + k;
+			v[k] = e < N ? L.stack[e] : 0u;
+			a += v[k];
+			b += (unsigned long long)v[k] * v[k];
+		}
+		uint32_t ea = (uint32_t)wave_excl_scan((int)a, lane);
+		unsigned long long eb = wave_excl_scan_u64(b, lane);
+		if (lane == 0) {
+			L.p1[0] = 0;
+			L.p2[0] = 0;
+		}
+#pragma unroll
+		for (int k = 0; k < KM; k++) {
+			const int e = KM * lane + k;
+			ea += v[k];
+			eb += (unsigned long long)v[k] * v[k];
+			if (e < N) {
+				L.p1[e + 1] = ea;
+				L.p2[e + 1] = eb;
+			}
+		}
+		__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+	}
+	int lo = 0, hi = N;
+	uint32_t fl = 0, fh = 0;	/* clip counts of the fast passes (wave-uniform) */
+	bool handover = false;
+	for (;;) {
+		const int n = hi - lo;
+		const uint64_t S = (uint64_t)(L.p1[hi] - L.p1[lo]), SS = L.p2[hi] - L.p2[lo];
+		bool e0;
+		const double sigma = exact_sd(n, S, SS, &e0);
+		const double median = replay_median(L.stack + lo, n);
+		const double tl = sl * sigma, th = sh * sigma;
+		const double blo = median - tl, bhi = median + th;
+		const double tol = e0 ? 0.0 : SG_BAND * (fabs(median) + fabs(tl) + fabs(th) + 1.0);
+		int amb = 0, cl = 0, ch = 0;
+#pragma unroll
+		for (int k = 0; k < KM; k++) {
+			const int e = 64 * k + lane;
+			const bool in = e >= lo && e < hi;
+			const double x = in ? (double)L.stack[e] : 0.0;
+			if (in && tol > 0.0 && ((x >= blo - tol && x <= blo + tol) || (x >= bhi - tol && x <= bhi + tol)))
+				amb = 1;
+			const bool low = in && (median - x > tl), high = in && !low && (x - median > th);
+			cl += (int)__popcll(__ballot(low));
+			ch += (int)__popcll(__ballot(high));
+		}
+		if (wave_or(amb)) {
+			handover = true;
+			break;
+		}
+		/* the general loop's first frame fb with n - (r + rejections in [0, fb]) <= 4 */
+		const int need = n - 4 - r;
+		int fb = n - 1;
+		if (need <= 0)
+			fb = 0;
+		else if (cl >= need)
+			fb = need - 1;
+		else if (cl + ch >= need)
+			fb = (n - ch) + (need - cl) - 1;
+		if (fb < n - 1) {
+			handover = true;
+			break;
+		}
+		iter++;
+		if (lane == 0)
+			L.npass++;
+#pragma unroll
+		for (int k = 0; k < KM; k++) {
+			const int j = 64 * k + lane;
+			if (j < n)
+				L.rej[j] = j < cl ? (int8_t)-1 : (j >= n - ch ? (int8_t)1 : (int8_t)0);
+		}
+		r += cl + ch;
+		fl += (uint32_t)cl;
+		fh += (uint32_t)ch;
+		lo += cl;
+		hi -= ch;
+		if (!(cl + ch > 0 && hi - lo > 3))
+			break;
+	}
+	if (!handover) {
+		N = hi - lo;
+		*value = sg_round_to_WORD((double)(L.p1[hi] - L.p1[lo]) / (double)N);
+		clo = fl;	/* totals */
+		chi = fh;
+		return 1;
+	}
+	/* the general loop keeps per-lane partial counts and sums them over the wave at the end */
+	clo = lane == 0 ? fl : 0u;
+	chi = lane == 0 ? fh : 0u;
+	/* compact [lo, hi) to the front for the general loop */
+	const int n = hi - lo;
+	if (lo > 0) {
+		uint16_t kv[KM];
+#pragma unroll
+		for (int k = 0; k < KM; k++) {
+			const int e = 64 * k + lane;
+			kv[k] = e < n ? L.stack[lo + e] : 0;
+		}
+		__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+		for (int k = 0; k < KM; k++) {
+			const int e = 64 * k + lane;
+			if (e < n)
+				L.stack[e] = kv[k];
+		}
+	}
+	__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+	N = n;
+	return 0;
+}
 
 /* returns 1 on success (value / counters set), 0 = leave the pixel to the literal path
  * (first pass broken early, or the Winsorize guard).  Each sigma comes from exact integer
@@ -1252,23 +1452,47 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 		uint32_t *rlo, uint32_t *rhi) {
 	int N = N0, r = 0, n, iter = 0;
 	uint32_t clo = 0, chi = 0;
-	for (int j = lane; j < N0; j += 64)
-		L.rej[j] = 0;
+	if (N0 <= SG_REPLAY_FASTN) {
+#pragma unroll
+		for (int k = 0; k < SG_REPLAY_FASTN / 64; k++) {
+			const int j = 64 * k + lane;
+			if (j < N0) {
+				L.rej[j] = 0;
+				L.orig[j] = L.stack[j];	/* frame order: the first pass's sd input */
+			}
+		}
+	} else {
+		for (int j = lane; j < N0; j += 64) {
+			L.rej[j] = 0;
+			L.orig[j] = L.stack[j];
+		}
+	}
+	__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+	replay_sort_any(L.stack, N, lane);	/* the quicksort_s of the first pass; later passes keep it sorted */
+	if (lane == 0)
+		L.t_sort = __builtin_readcyclecounter();
+	if (type == 2 && N <= SG_REPLAY_FASTN) {
+		const int done = replay_sigma_fast(L, N, r, iter, sl, sh, lane, clo, chi, value);
+		if (lane == 0) {
+			L.t_fast = __builtin_readcyclecounter();
+			L.handover = !done;
+		}
+		if (done) {
+			*rlo = clo;
+			*rhi = chi;
+			return 1;
+		}
+	}
 	do {
 		iter++;
+		if (lane == 0)
+			L.npass++;
 		uint64_t S, SS;
 		replay_moments(L.stack, N, lane, S, SS);
 		bool e0;
 		double sigma = exact_sd(N, S, SS, &e0);
 		bool sx = false;
-		if (iter == 1) {
-			for (int j = lane; j < N; j += 64)
-				L.orig[j] = L.stack[j];	/* frame order: the first pass's sd input */
-			__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-		}
-		const uint16_t *src = iter == 1 ? L.orig : L.stack;	/* this pass's sd input */
-		if (iter == 1)
-			replay_sort_any(L.stack, N, lane);
+		const uint16_t *src = iter == 1 ? L.orig : L.stack;	/* this pass's sd input (sorted after pass 1) */
 		double median = replay_median(L.stack, N);
 		if (type == 4) {
 			for (int j = lane; j < N; j += 64)
@@ -1298,7 +1522,7 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 					if (amb || (clamped_lo && round_ambiguous(m0, tol + 1e-9 * tol)) ||
 							(clamped_hi && round_ambiguous(m1, tol + 1e-9 * tol))) {
 						sx = true;
-						sigma = from_w ? 1.134 * replay_gsl_sd(L.w, N, lane) : replay_gsl_sd(src, N, lane);
+						sigma = from_w ? 1.134 * replay_gsl_sd(L, L.w, N, lane) : replay_gsl_sd(L, src, N, lane);
 						m0 = median - 1.5 * sigma;
 						m1 = median + 1.5 * sigma;
 					}
@@ -1334,9 +1558,9 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 				const double q = fabs(sigma - sigma0) / sigma0;
 				if (fabs(q - 0.0005) <= 1e-9 * 0.0005 + SG_BAND * (1.0 + q)) {
 					const double s0 = s0x ? sigma0
-							      : prev_from_w ? 1.134 * replay_gsl_sd(L.wprev, N, lane)
-									    : replay_gsl_sd(src, N, lane);
-					sigma = 1.134 * replay_gsl_sd(L.w, N, lane);
+							      : prev_from_w ? 1.134 * replay_gsl_sd(L, L.wprev, N, lane)
+									    : replay_gsl_sd(L, src, N, lane);
+					sigma = 1.134 * replay_gsl_sd(L, L.w, N, lane);
 					sx = true;
 					if (!((fabs(sigma - s0) / s0) > 0.0005))
 						break;
@@ -1373,7 +1597,7 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 				break;
 			/* recompute this pass's sigma the reference's way and decide again, exactly */
 			sx = true;
-			sigma = type == 4 ? 1.134 * replay_gsl_sd(L.w, N, lane) : replay_gsl_sd(src, N, lane);
+			sigma = type == 4 ? 1.134 * replay_gsl_sd(L, L.w, N, lane) : replay_gsl_sd(L, src, N, lane);
 		}
 		/* first frame fb with N - (r + #rejections in [0, fb]) <= 4 */
 		const int before = wave_excl_scan(cnt, lane);
@@ -1477,12 +1701,44 @@ k_stack_replay(SgStackParams p) {
 		const int x = (int)(pix % p.W);
 		const int64_t cr = pix / p.W;
 		const int R = (int)(cr % p.H), c = (int)(cr / p.H);
-		for (int f = lane; f < p.N; f += 64)
-			L.stack[f] = sg_gather(p, f, c, R, x);
+		const unsigned long long t0 = __builtin_readcyclecounter();
+		if (p.N <= SG_REPLAY_FASTN)
+			replay_gather_batched(p, L.stack, c, R, x, lane);
+		else
+			for (int f = lane; f < p.N; f += 64)
+				L.stack[f] = sg_gather(p, f, c, R, x);
 		__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+		const unsigned long long t1 = __builtin_readcyclecounter();
+		if (lane == 0) {
+			L.nsd = 0;
+			L.npass = 0;
+			L.handover = 0;
+			L.t_sort = t1;
+			L.t_fast = t1;
+		}
 		uint16_t v;
 		uint32_t rl, rh;
-		if (!replay_pixel(L, p.N, p.rejection, p.sig0, p.sig1, lane, &v, &rl, &rh))
+		const int ok = replay_pixel(L, p.N, p.rejection, p.sig0, p.sig1, lane, &v, &rl, &rh);
+		if (p.dbg == 12 && lane == 0) {
+			const unsigned long long t2 = __builtin_readcyclecounter();
+			atomicMax(&g_sg_rprof[0], t2 - t0);
+			atomicMax(&g_sg_rprof[1], t1 - t0);
+			atomicMax(&g_sg_rprof[2], L.t_sort - t1);
+			atomicAdd(&g_sg_rprof[3], 1ull);
+			atomicAdd(&g_sg_rprof[4], (unsigned long long)L.nsd);
+			atomicAdd(&g_sg_rprof[5], (unsigned long long)L.npass);
+			atomicMax(&g_sg_rprof[6], (unsigned long long)L.nsd);
+			if (L.nsd == 0)
+				atomicMax(&g_sg_rprof[7], t2 - t0);
+			atomicAdd(&g_sg_rprof[8], t2 - t0);
+			atomicAdd(&g_sg_rprof[9], t1 - t0);
+			atomicAdd(&g_sg_rprof[10], L.t_sort - t1);
+			atomicAdd(&g_sg_rprof[11], L.t_fast - L.t_sort);
+			atomicAdd(&g_sg_rprof[12], (unsigned long long)L.handover);
+			atomicMax(&g_sg_rprof[13], L.t_fast - L.t_sort);
+			atomicMax(&g_sg_rprof[14], (unsigned long long)L.npass);
+		}
+		if (!ok)
 			continue;
 		if (lane == 0) {
 			p.out[pix] = v;
@@ -1630,4 +1886,15 @@ void sg_dbg_why_dump(hipStream_t s) {
 	fprintf(stderr, "\n");
 	memset(h, 0, sizeof h);
 	(void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_sg_why), h, sizeof h, 0, hipMemcpyHostToDevice, s);
+	unsigned long long r[16];
+	if (hipMemcpyFromSymbolAsync(r, HIP_SYMBOL(g_sg_rprof), sizeof r, 0, hipMemcpyDeviceToHost, s) != hipSuccess ||
+			hipStreamSynchronize(s) != hipSuccess)
+		return;
+	fprintf(stderr, "replay: %llu pixels, max cycles %llu (gather %llu, sort %llu), fp80 sd %llu (max %llu per pixel), "
+			"passes %llu, max cycles without fp80 %llu\n", r[3], r[0], r[1], r[2], r[4], r[6], r[5], r[7]);
+	if (r[3])
+		fprintf(stderr, "replay means: total %llu gather %llu sort %llu fast %llu (max %llu), handovers %llu, max passes %llu\n",
+				r[8] / r[3], r[9] / r[3], r[10] / r[3], r[11] / r[3], r[13], r[12], r[14]);
+	memset(r, 0, sizeof r);
+	(void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_sg_rprof), r, sizeof r, 0, hipMemcpyHostToDevice, s);
 }
