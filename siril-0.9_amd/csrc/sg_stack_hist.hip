@@ -48,6 +48,21 @@
  * CU overlap one tile's finish with the other's loads worse than four 4-wave ones: 4.62 ms
  * against 4.22 ms for the whole kernel, so NI = 1 is the default (SG_HIST_NI=2 selects 2). */
 #define SGH_WAVES_PER_NI 4
+/* waves per 256-pixel tile (NI = 2, the A/B SG_HIST_NI=2): 8, or 4 (-DSGH_WAVES_NI2=4: each
+ * lane loads both dwords of a 512-byte row segment, two 4-wave workgroups per CU with up to
+ * 256 VGPRs).  Measured (scripts/gpu_r4h.sh, profiles/r02x_ab_ni2_waves.log): 4 waves 5.02-5.08
+ * ms (loads only 3.36), 8 waves 4.37 ms, the 128-pixel default 3.50 ms (loads only 3.23) */
+#ifndef SGH_WAVES_NI2
+#define SGH_WAVES_NI2 8
+#endif
+#ifndef SGH_NB2
+#define SGH_NB2 1	/* blocks in flight for NI = 2 (4 waves: NB2 = 2 5.08 ms, 1 5.02 ms) */
+#endif
+template <int NI>
+struct SghCfg {
+	static constexpr int WAVES = NI == 1 ? SGH_WAVES_PER_NI : SGH_WAVES_NI2;
+	static constexpr int WPE = NI == 1 ? 4 : (SGH_WAVES_NI2 == 4 ? 2 : 4);	/* waves per SIMD (launch bound) */
+};
 #ifndef SGH_CENTER
 #define SGH_CENTER 16		/* frames used for the centre estimate */
 #endif
@@ -1226,7 +1241,7 @@ template <int NI>
 __device__ __forceinline__ void sgh_clear(SghLds<NI> &L, bool wait_prev) {
 	if (wait_prev)
 		__syncthreads();	/* the previous tile's finish is done with L */
-	constexpr int NH = 2 * NI * SGH_HROWS * 64 / 4, NC = 128 * NI / 4, T = 256 * NI;
+	constexpr int NH = 2 * NI * SGH_HROWS * 64 / 4, NC = 128 * NI / 4, T = 64 * SghCfg<NI>::WAVES;
 	uint4 *h = (uint4 *)&L.h[0][0][0];
 	const uint4 z = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
@@ -1253,7 +1268,7 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, const SghRo &r
 		int wave, int lane,
 		uint32_t (&lo2)[NI], uint32_t (&nonzero)[NI], uint32_t (&nsat)[NI], int &counted, bool wait_prev) {
 	constexpr int M = 16;		/* frames per block */
-	constexpr int WAVES = SGH_WAVES_PER_NI * NI;
+	constexpr int WAVES = SghCfg<NI>::WAVES;
 	constexpr int STEP = M * WAVES;
 	constexpr int AHEAD = NBUF * STEP;
 	const int N = p.N;
@@ -1379,7 +1394,7 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
 		int wave, int lane, uint32_t (&lo2)[NI], uint32_t (&nonzero)[NI], uint32_t (&nsat)[NI], int &counted,
 		bool wait_prev) {
 	constexpr int MB = 8;
-	constexpr int WAVES = SGH_WAVES_PER_NI * NI;
+	constexpr int WAVES = SghCfg<NI>::WAVES;
 	constexpr int STEP = 16 * WAVES;	/* frames between a wave's consecutive blocks */
 	const int N = p.N;
 	uint32_t *const h = &L.h[0][0][0];
@@ -1564,7 +1579,7 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
 template <int REJ, int NORM, int NI>
 __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro, SghLds<NI> &L, int bid, bool wait_prev,
 		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
-	constexpr int WAVES = SGH_WAVES_PER_NI * NI, COLS = 128 * NI;
+	constexpr int WAVES = SghCfg<NI>::WAVES, COLS = 128 * NI;
 	const int tid = threadIdx.x, lane = tid & 63;
 	const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 	const int ntx = (p.W + COLS - 1) / COLS;
@@ -1621,9 +1636,11 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 			sgh_build<true, SGH_NBUF, NORM, NI>(p, ro, L, F, wave, lane, lo2, nonzero, nsat, counted, wait_prev);
 	} else {
 		if (interior)
-			sgh_build_half<false, NORM, NI, SGH_NB>(p, ro, L, F, wave, lane, lo2, nonzero, nsat, counted, wait_prev);
+			sgh_build_half<false, NORM, NI, NI == 1 ? SGH_NB : SGH_NB2>(p, ro, L, F, wave, lane, lo2, nonzero, nsat,
+					counted, wait_prev);
 		else
-			sgh_build_half<true, NORM, NI, SGH_NB>(p, ro, L, F, wave, lane, lo2, nonzero, nsat, counted, wait_prev);
+			sgh_build_half<true, NORM, NI, NI == 1 ? SGH_NB : SGH_NB2>(p, ro, L, F, wave, lane, lo2, nonzero, nsat,
+					counted, wait_prev);
 	}
 	if (counted) {
 #pragma unroll
@@ -1670,15 +1687,15 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 		/* WINSORIZED: the finish is VALU-bound and both lanes of a pair would run the same
 		 * loop, so half of the waves take one pixel column per lane and the others leave
 		 * their SIMD slots to other tiles */
-		if (wave >= WAVES / 2)
-			return;
-		const int col = 64 * wave + lane;
-		sgh_finish2<REJ, false, NI>(p, L, col, 0, col_lo(col), R, c, col_x(col), redo_count, redo_list);
+		for (int col = 64 * wave + lane; col < COLS; col += 64 * WAVES)
+			sgh_finish2<REJ, false, NI>(p, L, col, 0, col_lo(col), R, c, col_x(col), redo_count, redo_list);
 		return;
 	}
 	/* every wave finishes 32 pixel columns, a lane pair per column */
-	const int col = 32 * wave + (lane >> 1), half = lane & 1;
-	sgh_finish2<REJ, true, NI>(p, L, col, half, col_lo(col), R, c, col_x(col), redo_count, redo_list);
+	const int half = lane & 1;
+	int col = 32 * wave + (lane >> 1);
+	for (; col < COLS; col += 32 * WAVES)
+		sgh_finish2<REJ, true, NI>(p, L, col, half, col_lo(col), R, c, col_x(col), redo_count, redo_list);
 	if (timeline && lane == 0) {
 		const uint64_t t = __builtin_amdgcn_s_memrealtime();
 		if (wave == 0)
@@ -1692,7 +1709,7 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
  * workgroups (69 KB of LDS each) or four 4-wave ones (36 KB) per CU: 16 waves, at most 128
  * VGPRs. */
 template <int REJ, int NORM, int NI>
-__global__ void __launch_bounds__(64 * SGH_WAVES_PER_NI * NI, 4)
+__global__ void __launch_bounds__(64 * SghCfg<NI>::WAVES, SghCfg<NI>::WPE)
 k_stack_hist(SgStackParams p, const int *__restrict__ tab, const int4 *__restrict__ norm,
 		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
 	SghRo ro;
@@ -1734,3 +1751,8 @@ template __global__ void k_stack_hist<2, 0, 2>(SgStackParams, const int *, const
 		unsigned int *);
 template __global__ void k_stack_hist<4, 0, 2>(SgStackParams, const int *, const int4 *, unsigned int *,
 		unsigned int *);
+
+/* threads per histogram workgroup (the host's launch shape) */
+int sgh_block_threads(int ni) {
+	return ni == 2 ? 64 * SghCfg<2>::WAVES : 64 * SghCfg<1>::WAVES;
+}
