@@ -302,7 +302,7 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 	 * (flush_inputs, right before the first kernel) */
 	std::vector<int> sh(Npad + Npad / 2 + 2 * N, 0);
 	std::vector<double> nm;
-	std::vector<int> tables;
+	std::vector<int> tables, ztab;
 	/* the histogram path addresses a frame plane with 32-bit offsets: (R - sy) W 2 must fit */
 	bool hist_addr_ok = (int64_t)H * W * 2 <= (1ll << 30);
 	{
@@ -351,13 +351,62 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			nm[3 * N + 2 * i + 1] = additive ? (fold ? nm[i] - 0.5 : nm[i]) : nm[N + i];
 		}
 	}
+	/* additive normalisation with shifts: a row whose shifted source row leaves frame f holds
+	 * f's normalised zero round_to_WORD(0 scale - offset) (:1550-1577 zero fill, then
+	 * :1635-1652); the histogram path takes those values per border row from this table
+	 * (SghPix::zmax) instead of sending the rows to the redo list */
+	if (p.use_shift && (p.normalize == SG_ADDITIVE || p.normalize == SG_ADDITIVE_SCALING)) {
+		int k1 = std::max(0, p.sy_max), k2 = std::max(0, -p.sy_min);
+		if (k1 + k2 >= H) {
+			k1 = H;
+			k2 = 0;
+		}
+		ztab.assign((size_t)8 * (k1 + k2), 0);
+		bool any = false;
+		for (int t = 0; t < k1 + k2; t++) {
+			const int R = t < k1 ? t : H - k2 + (t - k1);
+			int zc = 0, zs = 0, zmin = 65535, zmax = 0;
+			long long zss = 0;
+			for (int f = 0; f < N; f++) {
+				const int sr = R - d->shifty[f];
+				if (sr >= 0 && sr < H)
+					continue;
+				const double x = 0.0 * nm[2 * N + f] - nm[f];	/* v scale - offset at v = 0 */
+				const int z = x <= 0.0 ? 0 : (x > 65535.0 ? 65535 : (int)(x + 0.5));
+				if (z == 0 || z == 65535)
+					continue;
+				zc++;
+				zs += z;
+				zss += (long long)z * z;
+				zmin = std::min(zmin, z);
+				zmax = std::max(zmax, z);
+			}
+			if (!zc)
+				continue;
+			any = true;
+			int *e = &ztab[(size_t)8 * t];
+			e[0] = zc;
+			e[1] = zs;
+			e[2] = (int)(uint32_t)(zss & 0xFFFFFFFFll);
+			e[3] = (int)(zss >> 32);
+			e[4] = zmin;
+			e[5] = zmax;
+		}
+		if (any) {
+			p.ztab_k1 = k1;
+			p.ztab_k2 = k2;
+		} else {
+			ztab.clear();
+		}
+	}
 	SgChainTables ct;
 	memset(&ct, 0, sizeof ct);
 	/* one pinned host block -> one device block; sets the kernels' pointers into it */
 	auto flush_inputs = [&]() -> int {
 		const size_t b_sh = sizeof(int) * sh.size(), o_nm = (b_sh + 255) & ~(size_t)255;
 		const size_t b_nm = sizeof(double) * nm.size(), o_tb = (o_nm + b_nm + 255) & ~(size_t)255;
-		const size_t tot = o_tb + sizeof(int) * tables.size();
+		const size_t o_zt = (o_tb + sizeof(int) * tables.size() + 255) & ~(size_t)255;
+		const size_t tot = o_zt + sizeof(int) * ztab.size();
 		if (dv.stage_pending) {	/* an earlier call's copy may still read the host block */
 			HIPCHK(hipEventSynchronize(dv.ev[3]));
 			dv.stage_pending = false;
@@ -377,6 +426,8 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			memcpy(hb + o_nm, nm.data(), b_nm);
 		if (!tables.empty())
 			memcpy(hb + o_tb, tables.data(), sizeof(int) * tables.size());
+		if (!ztab.empty())
+			memcpy(hb + o_zt, ztab.data(), sizeof(int) * ztab.size());
 		HIPCHK(hipMemcpyAsync(dv.inb.p, dv.stage_h, tot, hipMemcpyHostToDevice, s));
 		HIPCHK(hipEventRecord(dv.ev[3], s));
 		dv.stage_pending = true;
@@ -393,6 +444,7 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			p.scale = p.offset + 2 * N;
 			p.hist_norm = p.offset + 3 * N;
 		}
+		p.ztab = ztab.empty() ? nullptr : (const int *)(db + o_zt);
 		if (!tables.empty()) {
 			const int *tb = (const int *)(db + o_tb);
 			ct.blk_of_row = tb;

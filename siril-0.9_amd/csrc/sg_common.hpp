@@ -33,6 +33,12 @@ struct SgStackParams {
 	int hist_norm_fold;			/* additive pairs carry offset - 0.5 (NORM 3 kernels) */
 	int hist_maxsx;				/* max |shiftx| (interior-tile test of the histogram path) */
 	const double *hist_norm;		/* device: {scale, offset | mul} per frame (hist_npad pairs), normalised stacks */
+	/* additive normalisation with shifts: per border row (rows 0 .. ztab_k1 - 1, then
+	 * H - ztab_k2 .. H - 1) the normalised zeros round_to_WORD(-offset_f) of the frames whose
+	 * shifted row leaves the frame, those that are neither 0 nor 65535: int[8] {count, sum,
+	 * sum of squares lo, hi, min, max, 0, 0} (null: none) */
+	const int *ztab;
+	int ztab_k1, ztab_k2;
 	const double *offset, *mul, *scale;	/* device [N] or null */
 	int row_begin, row_end;			/* memory rows to compute */
 	int res_begin, res_end;			/* memory rows present at `frames` (desc->resident_rows) */

@@ -112,7 +112,9 @@ struct SghPix {
 	 * the halves' prefixes needs no reordering */
 	uint32_t pc[SGH_NGRP], ps[SGH_NGRP], pss[SGH_NGRP];
 	int hx;
-	SghM Z;			/* moments of the zeros */
+	SghM Z;			/* moments of the zeros (and of the border row's normalised zeros, ztab) */
+	int zmax;		/* > 0: the below-band samples include normalised zeros up to this value;
+				 * a count query at v in [0, zmax) or a rank among them is not decided here */
 	SghM T;			/* moments of all samples */
 };
 
@@ -695,8 +697,11 @@ __device__ __forceinline__ int sgh_med_value(const SghPix &P, const SghMed &m) {
  * pass, sigma comes from sgh_sigma_fast, and the clamps and selects are straight-line code, so
  * a pass is one basic block (round 2: the loop's VALU count, not its dependency chain, is what
  * the kernel pays for; scripts/gpu_r2t.sh, gpu_r2w.sh). */
+template <bool ZT>
 __device__ __forceinline__ int sgh_sigma3(const SghPix &P, int N, double sl, double sh, int half, uint16_t *value,
 		uint32_t *rlo_out, uint32_t *rhi_out, int &passes) {
+	/* a query the below-band normalised zeros make undecidable here (ZT: additive normalisation) */
+	auto zbad = [&](int v) { return ZT && v >= 0 && v < P.zmax; };
 	int A = 0, B = 65535, n = N, r = 0, nrem;
 	SghM MA = {0, 0, 0}, MB = P.T;
 	uint32_t rlo = 0, rhi = 0;
@@ -711,6 +716,7 @@ __device__ __forceinline__ int sgh_sigma3(const SghPix &P, int N, double sl, dou
 		/* n >= 4: the halvings as unsigned shifts; the median as (m1 + m2) * 0.5 (exact), with
 		 * m2 = m1 for odd n, so no branch */
 		const int mv = sgh_med_value(P, md);
+		uint32_t zb = (ZT && P.zmax && md.r < 0) ? 1u : 0u;	/* a median rank among the below-band samples */
 		const int mo = (int)sgh_x((uint32_t)mv);
 		const int m1 = half ? mo : mv, m2 = (n & 1) ? m1 : (half ? mv : mo);
 		const double median = (double)(m1 + m2) * 0.5;
@@ -723,6 +729,8 @@ __device__ __forceinline__ int sgh_sigma3(const SghPix &P, int N, double sl, dou
 		bt = bt > B ? B : bt;
 		SghQ q;
 		sgh_q_load(P, half ? bt : a - 1, q);
+		if (zbad(half ? bt : a - 1))
+			zb = 1u;
 		const int cm = sgh_q_count(P, q), co = (int)sgh_x((uint32_t)cm);
 		const int cnt_a = half ? co : cm, cnt_bt = half ? cm : co;
 		uint32_t amb = 0;
@@ -731,12 +739,17 @@ __device__ __forceinline__ int sgh_sigma3(const SghPix &P, int N, double sl, dou
 				int amb1 = sgh_floor_clamp(blo + tol);
 				amb1 = amb1 > B ? B : amb1;
 				amb = (a <= amb1 && sgh_cnt_le(P, amb1) - cnt_a > 0) ? 1u : 0u;
+				if (a <= amb1 && zbad(amb1))
+					zb = 1u;
 			} else {
 				int amb0 = sgh_ceil_clamp(bhi - tol);
 				amb0 = amb0 < A ? A : amb0;
 				amb = (amb0 <= bt && cnt_bt - sgh_cnt_le(P, amb0 - 1) > 0) ? 1u : 0u;
+				if (amb0 <= bt && zbad(amb0 - 1))
+					zb = 1u;
 			}
 		}
+		amb |= zb;
 		if (amb | sgh_x(amb))
 			return 1;
 		const int L = cnt_a - MA.c, H = MB.c - cnt_bt;
@@ -1080,9 +1093,9 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint
 
 /* pixel column `col` of the tile (x its image column); PAIR: lane pair half `half`, else one
  * lane per column (half = 0) */
-template <int REJ, bool PAIR, int NI>
+template <int REJ, bool PAIR, int NI, bool ZT = false>
 __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int half, int lo, int R, int c, int x,
-		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
+		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list, bool zrow = false) {
 	const int lane = threadIdx.x & 63;
 	const int N = p.N;
 	const uint32_t *hc = &L.h[col >> 6][0][col & 63];	/* dword j at hc[64 j] */
@@ -1157,6 +1170,24 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 		P.hx = 0;
 	}
 	const int oob = (int)hc[64 * SGH_DW];
+	/* ZT (SIGMA with additive normalisation): this row's normalised zeros of frames shifted out
+	 * of it, from the host's border-row table (SgStackParams::ztab).  Interior tiles only
+	 * (zrow): at the image edges a frame shifted out in both directions gives 0 instead (the x
+	 * shift's zero is not normalised, :1628-1632), and the sample count alone cannot tell one
+	 * such frame from an unrelated out-of-band sample */
+	int zc = 0, zs = 0, zmax = 0;
+	long long zss = 0;
+	if (ZT && REJ == 2 && zrow && p.ztab) {
+		const int t = R < p.ztab_k1 ? R : (R >= p.H - p.ztab_k2 ? p.ztab_k1 + (R - (p.H - p.ztab_k2)) : -1);
+		if (t >= 0) {
+			const int *e = p.ztab + 8 * t;
+			zc = e[0];
+			zs = e[1];
+			zss = (long long)(uint32_t)e[2] | ((long long)e[3] << 32);
+			zmax = e[5];
+		}
+	}
+	P.zmax = 0;
 	P.lo = lo;
 	P.nz = (int)L.nz[col];
 	P.ns = (int)L.ns[col];
@@ -1170,13 +1201,22 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 	if (x < p.W) {
 		if (p.dbg == 1) {
 			value = (uint16_t)(s32 + ss32);
-		} else if (P.nb + oob != N || oob != P.nz + P.ns) {
-			cls = 1;	/* out-of-band sample other than 0 / 65535, or a wrapped u8 counter */
+		} else if (P.nb + oob != N || oob != P.nz + P.ns + zc || (zc && zmax >= lo)) {
+			cls = 1;	/* out-of-band sample other than 0 / 65535 (or than this row's normalised
+				 * zeros), or a wrapped u8 counter */
 		} else {
 			const long long dz = -(long long)lo, ds = 65535 - (long long)lo;
 			P.Z.c = P.nz;
 			P.Z.s = dz * P.nz;
 			P.Z.ss = (unsigned long long)(dz * dz) * (unsigned long long)P.nz;
+			if (zc) {	/* the normalised zeros join the below-band samples */
+				const long long l = lo;
+				P.Z.c += zc;
+				P.Z.s += (long long)zs - (long long)zc * l;
+				P.Z.ss += (unsigned long long)(zss - 2 * l * (long long)zs + (long long)zc * l * l);
+				P.nz += zc;
+				P.zmax = zmax;
+			}
 			P.T.c = N;
 			P.T.s = (long long)s32 + P.Z.s + ds * P.ns;
 			P.T.ss = (unsigned long long)ss32 + P.Z.ss + (unsigned long long)(ds * ds) * (unsigned long long)P.ns;
@@ -1188,7 +1228,7 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 				rlo = rhi = 0;
 #endif
 			} else {
-				cls = sgh_sigma3(P, N, p.sig0, p.sig1, half, &value, &rlo, &rhi, passes);
+				cls = sgh_sigma3<ZT>(P, N, p.sig0, p.sig1, half, &value, &rlo, &rhi, passes);
 #ifdef SGH_SIGMA_PASSES	/* A/B probe build: the image holds the pass counts */
 				value = (uint16_t)passes;
 				cls = SG_CLS_OK;
@@ -1695,7 +1735,8 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 	const int half = lane & 1;
 	int col = 32 * wave + (lane >> 1);
 	for (; col < COLS; col += 32 * WAVES)
-		sgh_finish2<REJ, true, NI>(p, L, col, half, col_lo(col), R, c, col_x(col), redo_count, redo_list);
+		sgh_finish2<REJ, true, NI, NORM == 1 || NORM == 3>(p, L, col, half, col_lo(col), R, c, col_x(col), redo_count,
+				redo_list, interior);
 	if (timeline && lane == 0) {
 		const uint64_t t = __builtin_amdgcn_s_memrealtime();
 		if (wave == 0)
