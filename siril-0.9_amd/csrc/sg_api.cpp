@@ -487,7 +487,8 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		const size_t npix_launch = (size_t)C * nrows * W;
 		HIPCHK(ensure(dv.flag_list, sizeof(unsigned int) * npix_launch));
 		HIPCHK(ensure(dv.flag_map, npix_img));
-		HIPCHK(hipMemsetAsync(dv.flag_map.p, 0, npix_img, s));
+		/* flag_map is cleared right after the main kernel is queued (only the kernels after it
+		 * read it), so the clear is not ahead of the histogram kernel's launch */
 		p.flag_list = (unsigned int *)dv.flag_list.p;
 		p.flag_cap = (unsigned int)npix_launch;
 		p.flag_map = (uint8_t *)dv.flag_map.p;
@@ -569,6 +570,7 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			}
 			HIPCHK(hipGetLastError());
 			HIPCHK(hipEventRecord(dv.ev[1], s));
+			HIPCHK(hipMemsetAsync(dv.flag_map.p, 0, npix_img, s));
 			ctx->stats.path = 1;
 			ctx->stats.main_kernel_blocks = (int)nblk;
 			ctx->stats.launches = 1;
@@ -598,6 +600,7 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 				}
 			}
 		} else {
+			HIPCHK(hipMemsetAsync(dv.flag_map.p, 0, npix_img, s));
 			HIPCHK(hipEventRecord(dv.ev[0], s));
 			HIPCHK(launch_sorted(nreg, false, dim3((unsigned)nblk), lds, s, p, nullptr, nullptr));
 			HIPCHK(hipEventRecord(dv.ev[1], s));
