@@ -75,6 +75,7 @@ struct SgKnobs {
 	int reg_cw = 0;			/* SG_REG_CW: columns per column-pass workgroup (0 = 8192 / S) */
 	int reg_path = 2;		/* SG_REG_PATH: registration pass order 0 / 1 / 2 */
 	int reg_xcd = 1;		/* SG_REG_XCD: 0 = column strips in dispatch order */
+	int reg_pb = 1;			/* SG_REG_PB: pairs per strip block of the fused column pass (1 = pair-major) */
 	void read() {
 		hist_dbg = sg_env_int("SG_HIST_DBG", 0, 1000, 0);
 		hist_prio = sg_env_int("SG_HIST_PRIO", 0, 3, 1);
@@ -92,6 +93,7 @@ struct SgKnobs {
 		reg_cw = sg_env_int("SG_REG_CW", 1, 64, 0);
 		reg_path = sg_env_int("SG_REG_PATH", 0, 2, 2);
 		reg_xcd = sg_env_int("SG_REG_XCD", 0, 1, 1);
+		reg_pb = sg_env_int("SG_REG_PB", 1, 64, 1);
 	}
 };
 

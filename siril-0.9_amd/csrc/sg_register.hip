@@ -551,10 +551,21 @@ __device__ __forceinline__ sg_c64 sg_rconj(sg_c64 r, sg_c64 f) {
  * forward FFT instead spills (128 VGPRs at 4 waves per SIMD). */
 __global__ void __launch_bounds__(1024)
 k_reg_cols_xpower(sg_c64 *__restrict__ work, const sg_c64 *__restrict__ spec, int S, int CW,
-		const sg_c64 *__restrict__ tw, int xcdmap) {
+		const sg_c64 *__restrict__ tw, int xcdmap, int pb) {
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 	sg_c64 *buf = (sg_c64 *)smem;
-	const int x0 = sg_xcd_strip(blockIdx.x, gridDim.x, xcdmap) * CW, pair = blockIdx.y;
+	int x0 = sg_xcd_strip(blockIdx.x, gridDim.x, xcdmap) * CW, pair = blockIdx.y;
+	/* pb > 1: blocks of pb pairs per strip dispatched back to back on one XCD (strip-major
+	 * inside a pair block), so the strip's reference-spectrum columns are read from HBM once per
+	 * block and from that XCD's L2 by the block's other pairs, while neighbouring strips of one
+	 * pair still run close together (their 64-B rows share 128-B lines) */
+	const int ns = gridDim.x, np = gridDim.y;
+	if (pb > 1 && xcdmap && (ns & 7) == 0 && np % pb == 0) {
+		const int id = blockIdx.x + ns * blockIdx.y, xcd = id & 7, local = id >> 3, s8 = ns >> 3;
+		const int strip = xcd * s8 + (local / pb) % s8;
+		pair = (local / (pb * s8)) * pb + local % pb;
+		x0 = strip * CW;
+	}
 	const int bstride = SG_PADN(S) + 1, H = S >> 1;
 	sg_c64 *base = work + (size_t)pair * S * S + x0;
 	auto slot = [&](int c, int r) -> sg_c64 & { return buf[(size_t)c * bstride + sg_pad(r)]; };
@@ -1113,7 +1124,7 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 					d_fb + p0, S, tw, work);
 			HIPCHK(hipGetLastError());
 			hipLaunchKernelGGL(k_reg_cols_xpower, dim3(S / CWh, np), dim3(colh_thr), colh_lds, s, work,
-					(const sg_c64 *)spec, S, CWh, tw, xcdmap);
+					(const sg_c64 *)spec, S, CWh, tw, xcdmap, ctx->knobs.reg_pb);
 			HIPCHK(hipGetLastError());
 			hipLaunchKernelGGL(k_reg_rows_inv_half_argmax, dim3(S, np), dim3(row_thr), row_lds, s,
 					(const sg_c64 *)work, S, tw, best);
