@@ -86,6 +86,7 @@ struct alignas(16) SghLds {
 	uint32_t nz[128 * NI], ns[128 * NI];	/* zeros / 65535s (all of them lie outside the band) */
 	uint32_t lo2[NI][64];			/* band starts of the lane pixel pairs (u16 halves) */
 	uint32_t cs[NI][8][64];			/* wave 1's first 8 frames for the band centre (SGH_CENTER2W) */
+	uint8_t perm[128];			/* WINSORIZED finish order of the columns (SGH_WINS_ORDER) */
 };
 
 /* Finish-phase queries.  The band is cut into SGH_NGRP groups of SGH_GRP dwords (32 bins);
@@ -1227,6 +1228,11 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 				cls = SG_CLS_OK;
 				rlo = rhi = 0;
 #endif
+#ifdef SGH_WINS_FEAT	/* A/B probe build: the image holds min(zeros, 255) << 8 | min(65535s, 255) */
+				value = (uint16_t)(((P.nz < 255 ? P.nz : 255) << 8) | (P.ns < 255 ? P.ns : 255));
+				cls = SG_CLS_OK;
+				rlo = rhi = 0;
+#endif
 			} else {
 				cls = sgh_sigma3<ZT>(P, N, p.sig0, p.sig1, half, &value, &rlo, &rhi, passes);
 #ifdef SGH_SIGMA_PASSES	/* A/B probe build: the image holds the pass counts */
@@ -1427,6 +1433,9 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, const SghRo &r
  * sends 35 k pixels to the redo list, scripts/gpu_r3m.sh) */
 #ifndef SGH_CENTER2W
 #define SGH_CENTER2W 1
+#endif
+#ifndef SGH_WINS_ORDER
+#define SGH_WINS_ORDER 1	/* WINSORIZED finish: columns with zeros / 65535s first (sgh_tile) */
 #endif
 
 template <bool EDGE, int NORM, int NI, int NB>
@@ -1726,7 +1735,29 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 	if (REJ == 4) {
 		/* WINSORIZED: the finish is VALU-bound and both lanes of a pair would run the same
 		 * loop, so half of the waves take one pixel column per lane and the others leave
-		 * their SIMD slots to other tiles */
+		 * their SIMD slots to other tiles.  A wave runs the inner loop as often as its slowest
+		 * pixel needs, and a pixel holding a zero or a 65535 sample needs ~10 iterations against
+		 * ~3 (scripts/wins_predict.py, profiles/r02z_wins_predict.log), so those columns are
+		 * finished by wave 0 first and the rest after them (the sum of the two waves' maxima
+		 * 26.4 -> 21.5 iterations per tile on configs[4]'s data) */
+		if (SGH_WINS_ORDER && NI == 1) {
+			if (wave == 0) {
+				const int ca = lane, cb = 64 + lane;
+				const bool sa = (L.nz[ca] | L.ns[ca]) != 0u, sb = (L.nz[cb] | L.ns[cb]) != 0u;
+				const uint64_t ma = __ballot(sa), mb = __ballot(sb);
+				const uint64_t lt = (1ull << lane) - 1ull;
+				const int na = __popcll(ma), ns = na + __popcll(mb);
+				const int ra = __popcll(ma & lt), rb = __popcll(mb & lt);
+				L.perm[sa ? ra : ns + (lane - ra)] = (uint8_t)ca;
+				L.perm[sb ? na + rb : ns + (64 - na) + (lane - rb)] = (uint8_t)cb;
+			}
+			__syncthreads();
+			if (wave >= 2)
+				return;
+			const int col = L.perm[64 * wave + lane];
+			sgh_finish2<REJ, false, NI>(p, L, col, 0, col_lo(col), R, c, col_x(col), redo_count, redo_list);
+			return;
+		}
 		for (int col = 64 * wave + lane; col < COLS; col += 64 * WAVES)
 			sgh_finish2<REJ, false, NI>(p, L, col, 0, col_lo(col), R, c, col_x(col), redo_count, redo_list);
 		return;
