@@ -1094,6 +1094,9 @@ __device__ __forceinline__ void gather_stack(const SgStackParams &p, int64_t pix
  * sorted under clamping.
  */
 #define SG_REPLAY_FASTN 512	/* SIGMA fast passes (replay_sigma_fast) up to this many frames */
+#ifndef SG_REPLAY_WFAST
+#define SG_REPLAY_WFAST 1	/* WINSORIZED passes on the same fast path (replay_winsor_inner) */
+#endif
 struct SgReplayLds {
 	uint16_t stack[SG_REPLAY_MAXN];
 	uint16_t w[SG_REPLAY_MAXN];
@@ -1318,8 +1321,97 @@ __device__ __forceinline__ unsigned long long wave_excl_scan_u64(unsigned long l
  * (returns 0: ambiguous, or an early break) to the general loop with the state it expects:
  * the range is compacted to the front and N, r, passes and counters carry over.
  * Returns 1 when the pixel is finished (value and counters set). */
+/* WINSORIZED inner loop of one pass (:1710-1729 + Winsorized :1163-1168) on the sorted kept
+ * range [lo, hi), mirroring replay_pixel's type-4 loop decision for decision: the clamped copy w
+ * is kept as Lw copies of vlo, the range's own values [lo + Lw, hi - Hw), Hw copies of vhi (a
+ * clamp either re-clamps all earlier copies of a side or none of them, so one value per side
+ * suffices); its moments come from the prefix sums, its median from two positions, the
+ * counts below m0 / above m1 from ballots.  Returns 0 where the general loop would recompute
+ * a sigma the reference's way (ambiguous clamp or convergence decision) or give up (guard):
+ * the pass then goes to the general loop.  On 1, median / sigma / e0 are the pass's
+ * Winsorized values. */
+__device__ int replay_winsor_inner(SgReplayLds &L, int lo, int hi, int lane, double &median, double &sigma, bool &e0) {
+	constexpr int KM = SG_REPLAY_FASTN / 64;
+	const int n = hi - lo;
+	int Lw = 0, Hw = 0;
+	uint32_t vlo = 0, vhi = 0;
+	bool sig_e0 = e0;
+	auto w_at = [&](int k) -> double {	/* element k of the sorted w */
+		return (double)(k < Lw ? vlo : (k >= n - Hw ? vhi : (uint32_t)L.stack[lo + k]));
+	};
+	for (int guard = 0;; guard++) {
+		if (guard > 100000)
+			return 0;
+		const double m0 = median - 1.5 * sigma, m1 = median + 1.5 * sigma;
+		const double tol = sig_e0 ? 0.0 : SG_BAND * (fabs(median) + 1.5 * sigma + 1.0);
+		/* inner values below m0 / above m1, ambiguity over every element of w */
+		int amb = 0, nlo = 0, nhi = 0;
+#pragma unroll
+		for (int k = 0; k < KM; k++) {
+			const int e = 64 * k + lane;
+			const bool in = e >= lo + Lw && e < hi - Hw;
+			const double x = in ? (double)L.stack[e] : 0.0;
+			if (in && !sig_e0 && ((x >= m0 - tol && x <= m0 + tol) || (x >= m1 - tol && x <= m1 + tol)))
+				amb = 1;
+			nlo += (int)__popcll(__ballot(in && x < m0));
+			nhi += (int)__popcll(__ballot(in && !(x < m0) && x > m1));
+		}
+		amb = wave_or(amb);
+		const double xl = (double)vlo, xh = (double)vhi;
+		if (Lw && !sig_e0 && ((xl >= m0 - tol && xl <= m0 + tol) || (xl >= m1 - tol && xl <= m1 + tol)))
+			amb = 1;
+		if (Hw && !sig_e0 && ((xh >= m0 - tol && xh <= m0 + tol) || (xh >= m1 - tol && xh <= m1 + tol)))
+			amb = 1;
+		const bool lo_c = Lw && xl < m0, hi_c = Hw && !(xh < m0) && xh > m1;
+		const bool clamped_lo = nlo > 0 || lo_c, clamped_hi = nhi > 0 || hi_c;
+		if (amb || (clamped_lo && round_ambiguous(m0, tol + 1e-9 * tol)) ||
+				(clamped_hi && round_ambiguous(m1, tol + 1e-9 * tol)))
+			return 0;
+		/* the copies of a side either all move (their value is past the new bound) or stay */
+		if (Lw && !lo_c && xl > m1)
+			return 0;	/* (cannot happen: vlo < vhi; kept for safety) */
+		if (Hw && !hi_c && xh < m0)
+			return 0;
+		const uint32_t nvlo = sg_round_to_WORD(m0), nvhi = sg_round_to_WORD(m1);
+		if (clamped_lo) {
+			if (Lw && !lo_c)
+				return 0;	/* inner values below m0 while the old copies are not: w leaves this form */
+			Lw += nlo;
+			vlo = nvlo;
+		}
+		if (clamped_hi) {
+			if (Hw && !hi_c)
+				return 0;
+			Hw += nhi;
+			vhi = nvhi;
+		}
+		if (Lw + Hw > n)
+			return 0;
+		median = (n & 1) ? w_at((n - 1) / 2) : (w_at((n - 1) / 2) + w_at(n / 2)) / 2.0;
+		const uint64_t Sw = (uint64_t)Lw * vlo + (uint64_t)Hw * vhi + (uint64_t)(L.p1[hi - Hw] - L.p1[lo + Lw]);
+		const uint64_t SSw = (uint64_t)Lw * vlo * vlo + (uint64_t)Hw * vhi * vhi + (L.p2[hi - Hw] - L.p2[lo + Lw]);
+		const double sigma0 = sigma;
+		const bool e00 = sig_e0;
+		bool we0;
+		sigma = 1.134 * exact_sd(n, Sw, SSw, &we0);
+		sig_e0 = we0;
+		if (e00) {
+			if (we0)
+				break;	/* 0/0 = NaN: the loop exits */
+			continue;	/* x/0 = inf > 0.0005 */
+		}
+		const double q = fabs(sigma - sigma0) / sigma0;
+		if (fabs(q - 0.0005) <= 1e-9 * 0.0005 + SG_BAND * (1.0 + q))
+			return 0;
+		if (!(q > 0.0005))
+			break;
+	}
+	e0 = sig_e0;
+	return 1;
+}
+
 __device__ int replay_sigma_fast(SgReplayLds &L, int &N, int &r, int &iter, double sl, double sh, int lane,
-		uint32_t &clo, uint32_t &chi, uint16_t *value) {
+		uint32_t &clo, uint32_t &chi, uint16_t *value, int type = 2) {
 	constexpr int KM = SG_REPLAY_FASTN / 64;
 	{	/* prefix sums over the sorted stack, 8 consecutive samples per lane */
 		uint32_t a = 0;
@@ -1357,8 +1449,12 @@ __device__ int replay_sigma_fast(SgReplayLds &L, int &N, int &r, int &iter, doub
 		const int n = hi - lo;
 		const uint64_t S = (uint64_t)(L.p1[hi] - L.p1[lo]), SS = L.p2[hi] - L.p2[lo];
 		bool e0;
-		const double sigma = exact_sd(n, S, SS, &e0);
-		const double median = replay_median(L.stack + lo, n);
+		double sigma = exact_sd(n, S, SS, &e0);
+		double median = replay_median(L.stack + lo, n);
+		if (type == 4 && !replay_winsor_inner(L, lo, hi, lane, median, sigma, e0)) {
+			handover = true;
+			break;
+		}
 		const double tl = sl * sigma, th = sh * sigma;
 		const double blo = median - tl, bhi = median + th;
 		const double tol = e0 ? 0.0 : SG_BAND * (fabs(median) + fabs(tl) + fabs(th) + 1.0);
@@ -1471,8 +1567,8 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 	replay_sort_any(L.stack, N, lane);	/* the quicksort_s of the first pass; later passes keep it sorted */
 	if (lane == 0)
 		L.t_sort = __builtin_readcyclecounter();
-	if (type == 2 && N <= SG_REPLAY_FASTN) {
-		const int done = replay_sigma_fast(L, N, r, iter, sl, sh, lane, clo, chi, value);
+	if ((type == 2 || (type == 4 && SG_REPLAY_WFAST)) && N <= SG_REPLAY_FASTN) {
+		const int done = replay_sigma_fast(L, N, r, iter, sl, sh, lane, clo, chi, value, type);
 		if (lane == 0) {
 			L.t_fast = __builtin_readcyclecounter();
 			L.handover = !done;
