@@ -1544,6 +1544,10 @@ __device__ int replay_sigma_fast(SgReplayLds &L, int &N, int &r, int &iter, doub
  * current sigma is the reference's own value).  Every sigma is a function of an integer
  * array, and the arrays depend on earlier sigmas only through discrete decisions, so the
  * next sigma starts from exact moments again. */
+/* PMAX: positions per lane of the general loop's per-lane chunks (8 for N <= 512, so the chunk
+ * arrays d[] / kv[] are indexed statically and stay in registers; 32 up to SG_REPLAY_MAXN,
+ * where they live in scratch) */
+template <int PMAX>
 __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double sh, int lane, uint16_t *value,
 		uint32_t *rlo, uint32_t *rhi) {
 	int N = N0, r = 0, n, iter = 0;
@@ -1670,14 +1674,15 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 		/* decisions, frame order, with the early break */
 		const int per = (N + 63) / 64, j0 = lane * per;
 		int cnt = 0;
-		int8_t d[SG_REPLAY_MAXN / 64];
+		int8_t d[PMAX];
 		for (int attempt = 0; attempt < 2; attempt++) {
 			const double tl = sl * sigma, th = sh * sigma;
 			const double blo = median - tl, bhi = median + th;
 			const double tol = (e0 || sx) ? 0.0 : SG_BAND * (fabs(median) + fabs(tl) + fabs(th) + 1.0);
 			int amb = 0;
 			cnt = 0;
-			for (int k = 0; k < per; k++) {
+#pragma unroll
+			for (int k = 0; k < PMAX && k < per; k++) {
 				const int j = j0 + k;
 				int8_t v = 0;
 				if (j < N) {
@@ -1700,14 +1705,16 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 		int fb_lane = N;
 		{
 			int c = r + before;
-			for (int k = 0; k < per; k++) {
+			bool found = false;
+#pragma unroll
+			for (int k = 0; k < PMAX; k++) {	/* no early exit, so the loop unrolls */
 				const int j = j0 + k;
-				if (j >= N)
-					break;
-				c += d[k] != 0;
-				if (N - c <= 4) {
-					fb_lane = j;
-					break;
+				if (k < per && j < N && !found) {
+					c += d[k] != 0;
+					if (N - c <= 4) {
+						fb_lane = j;
+						found = true;
+					}
 				}
 			}
 		}
@@ -1722,7 +1729,8 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 		if (iter == 1 && fb < N - 1)
 			return 0;	/* stale entries of the previous pixel */
 		int nrej = 0;
-		for (int k = 0; k < per; k++) {
+#pragma unroll
+		for (int k = 0; k < PMAX && k < per; k++) {
 			const int j = j0 + k;
 			if (j <= fb) {
 				L.rej[j] = d[k];
@@ -1735,8 +1743,9 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 		__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 		/* order-preserving removal of every position j < N with rejected[j] != 0 */
 		int keep = 0;
-		uint16_t kv[SG_REPLAY_MAXN / 64];
-		for (int k = 0; k < per; k++) {
+		uint16_t kv[PMAX];
+#pragma unroll
+		for (int k = 0; k < PMAX && k < per; k++) {
 			const int j = j0 + k;
 			kv[k] = j < N ? L.stack[j] : 0;
 			keep += (j < N && L.rej[j] == 0);
@@ -1744,7 +1753,8 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 		int pos = wave_excl_scan(keep, lane);
 		const int kept = (int)wave_sum_u64((uint64_t)keep);
 		__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-		for (int k = 0; k < per; k++) {
+#pragma unroll
+		for (int k = 0; k < PMAX && k < per; k++) {
 			const int j = j0 + k;
 			if (j < N && L.rej[j] == 0)
 				L.stack[pos++] = kv[k];
@@ -1814,7 +1824,10 @@ k_stack_replay(SgStackParams p) {
 		}
 		uint16_t v;
 		uint32_t rl, rh;
-		const int ok = replay_pixel(L, p.N, p.rejection, p.sig0, p.sig1, lane, &v, &rl, &rh);
+		const int ok = p.N <= SG_REPLAY_FASTN ? replay_pixel<SG_REPLAY_FASTN / 64>(L, p.N, p.rejection, p.sig0, p.sig1,
+									     lane, &v, &rl, &rh)
+						     : replay_pixel<SG_REPLAY_MAXN / 64>(L, p.N, p.rejection, p.sig0, p.sig1,
+									     lane, &v, &rl, &rh);
 		if (p.dbg == 12 && lane == 0) {
 			const unsigned long long t2 = __builtin_readcyclecounter();
 			atomicMax(&g_sg_rprof[0], t2 - t0);
