@@ -1330,7 +1330,8 @@ __device__ __forceinline__ unsigned long long wave_excl_scan_u64(unsigned long l
  * a sigma the reference's way (ambiguous clamp or convergence decision) or give up (guard):
  * the pass then goes to the general loop.  On 1, median / sigma / e0 are the pass's
  * Winsorized values. */
-__device__ int replay_winsor_inner(SgReplayLds &L, int lo, int hi, int lane, double &median, double &sigma, bool &e0) {
+__device__ int replay_winsor_inner(SgReplayLds &L, const uint32_t (&xs)[SG_REPLAY_FASTN / 64], int lo, int hi,
+		int lane, double &median, double &sigma, bool &e0) {
 	constexpr int KM = SG_REPLAY_FASTN / 64;
 	const int n = hi - lo;
 	int Lw = 0, Hw = 0;
@@ -1350,13 +1351,13 @@ __device__ int replay_winsor_inner(SgReplayLds &L, int lo, int hi, int lane, dou
 		for (int k = 0; k < KM; k++) {
 			const int e = 64 * k + lane;
 			const bool in = e >= lo + Lw && e < hi - Hw;
-			const double x = in ? (double)L.stack[e] : 0.0;
+			const double x = (double)xs[k];
 			if (in && !sig_e0 && ((x >= m0 - tol && x <= m0 + tol) || (x >= m1 - tol && x <= m1 + tol)))
 				amb = 1;
 			nlo += (int)__popcll(__ballot(in && x < m0));
 			nhi += (int)__popcll(__ballot(in && !(x < m0) && x > m1));
 		}
-		amb = wave_or(amb);
+		amb = __ballot(amb) != 0ull;	/* one instruction instead of six lane shuffles */
 		const double xl = (double)vlo, xh = (double)vhi;
 		if (Lw && !sig_e0 && ((xl >= m0 - tol && xl <= m0 + tol) || (xl >= m1 - tol && xl <= m1 + tol)))
 			amb = 1;
@@ -1442,6 +1443,14 @@ __device__ int replay_sigma_fast(SgReplayLds &L, int &N, int &r, int &iter, doub
 		}
 		__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 	}
+	/* the sorted stack in registers (element 64 k + lane in xs[k]): the passes below do not
+	 * move it, so every pass and Winsorize iteration reads registers instead of LDS */
+	uint32_t xs[KM];
+#pragma unroll
+	for (int k = 0; k < KM; k++) {
+		const int e = 64 * k + lane;
+		xs[k] = e < N ? (uint32_t)L.stack[e] : 0u;
+	}
 	int lo = 0, hi = N;
 	uint32_t fl = 0, fh = 0;	/* clip counts of the fast passes (wave-uniform) */
 	bool handover = false;
@@ -1451,7 +1460,7 @@ __device__ int replay_sigma_fast(SgReplayLds &L, int &N, int &r, int &iter, doub
 		bool e0;
 		double sigma = exact_sd(n, S, SS, &e0);
 		double median = replay_median(L.stack + lo, n);
-		if (type == 4 && !replay_winsor_inner(L, lo, hi, lane, median, sigma, e0)) {
+		if (type == 4 && !replay_winsor_inner(L, xs, lo, hi, lane, median, sigma, e0)) {
 			handover = true;
 			break;
 		}
@@ -1463,14 +1472,14 @@ __device__ int replay_sigma_fast(SgReplayLds &L, int &N, int &r, int &iter, doub
 		for (int k = 0; k < KM; k++) {
 			const int e = 64 * k + lane;
 			const bool in = e >= lo && e < hi;
-			const double x = in ? (double)L.stack[e] : 0.0;
+			const double x = (double)xs[k];
 			if (in && tol > 0.0 && ((x >= blo - tol && x <= blo + tol) || (x >= bhi - tol && x <= bhi + tol)))
 				amb = 1;
 			const bool low = in && (median - x > tl), high = in && !low && (x - median > th);
 			cl += (int)__popcll(__ballot(low));
 			ch += (int)__popcll(__ballot(high));
 		}
-		if (wave_or(amb)) {
+		if (__ballot(amb) != 0ull) {
 			handover = true;
 			break;
 		}
