@@ -1,0 +1,72 @@
+#!/bin/bash
+# The one GPU runner (replaces round 1/2's per-experiment launchers; they live in git history
+# before round 3).  Run on the box through gpurun:
+#   gpurun --timeout 900 -- 'bash scripts/gpu.sh OUT STEP [STEP ...]'
+# Results go to gpurun_out/OUT/.  Steps run in order; the first failing step ends the run
+# (no GPU step runs after a fault, an abort or a time limit).
+#   test[=K]                    pytest -m gpu (optionally -k K), per-test timeout 200 s
+#   smoke                       __graft_entry__.smoke()
+#   bench=NAME[:ARGS]           python bench.py ARGS -> NAME.log + one summary line
+#   env=NAME:VAR=V[;VAR=V]:ARGS the same with an environment (A/B: SG_* knobs, SG_LIB_PATH)
+#   prof=NAME[:ARGS]            rocprofv3 --kernel-trace --stats of bench.py ARGS -> NAME/
+#   pmc=NAME[:ARGS]             FETCH_SIZE and WRITE_SIZE passes (own runs) -> NAME_traffic.json
+#   py=NAME:SCRIPT[:ARGS]       python SCRIPT ARGS -> NAME.log
+# ARGS use ',' between words (bench=cfg1:--workload,register-mean).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+export TMPDIR=/tmp
+O=gpurun_out/${1:?output directory}
+shift
+mkdir -p "$O"
+
+fail() { echo "FAILED: $1"; [ -f "$2" ] && tail -30 "$2"; exit 3; }
+summary() {
+  grep '^{' "$1" | tail -1 | python3 -c 'import json,sys
+d=json.loads(sys.stdin.read())
+r=d.get("roofline",{})
+print(d.get("value"), d.get("unit"), "ms/step", d.get("ms_per_step"), "kernel", d.get("kernel_ms", d.get("stage_ms")), "frac", r.get("frac"))'
+}
+
+for step in "$@"; do
+  kind=${step%%=*}
+  spec=${step#*=}
+  [ "$kind" = "$step" ] && spec=""
+  case $kind in
+    test)
+      k=(); [ -n "$spec" ] && k=(-k "$spec")
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread "${k[@]}" \
+        > "$O/pytest_gpu.log" 2>&1 || fail test "$O/pytest_gpu.log"
+      tail -1 "$O/pytest_gpu.log" ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || fail smoke "$O/smoke.log"
+      tail -1 "$O/smoke.log" ;;
+    bench)
+      name=${spec%%:*}; args=""; [ "$name" != "$spec" ] && args=${spec#*:}
+      timeout -k 10 600 python bench.py ${args//,/ } > "$O/$name.log" 2>&1 || fail "bench $name" "$O/$name.log"
+      echo "$name: $(summary "$O/$name.log")" ;;
+    env)
+      name=${spec%%:*}; rest=${spec#*:}; vars=${rest%%:*}; args=""; [ "$vars" != "$rest" ] && args=${rest#*:}
+      timeout -k 10 600 env ${vars//;/ } python bench.py ${args//,/ } > "$O/$name.log" 2>&1 || fail "env $name" "$O/$name.log"
+      echo "$name: $(summary "$O/$name.log")" ;;
+    prof)
+      name=${spec%%:*}; args=""; [ "$name" != "$spec" ] && args=${spec#*:}
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/$name" -o run -- \
+        python3 bench.py ${args//,/ } > "$O/$name.log" 2>&1 || fail "prof $name" "$O/$name.log"
+      echo "$name: $(summary "$O/$name.log")" ;;
+    pmc)
+      name=${spec%%:*}; args=""; [ "$name" != "$spec" ] && args=${spec#*:}
+      for grp in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 180 rocprofv3 --pmc $grp --output-format csv -d "$O/${name}_$grp" -o run -- \
+          python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ${args//,/ } > "$O/${name}_$grp.log" 2>&1 \
+          || fail "pmc $grp" "$O/${name}_$grp.log"
+      done
+      python3 scripts/pmc_traffic.py "$O/${name}_FETCH_SIZE" "$O/${name}_WRITE_SIZE" "${PMC_KERNEL:-k_stack_hist}" \
+        "$O/${name}_traffic.json" || fail "pmc parse" ;;
+    py)
+      name=${spec%%:*}; rest=${spec#*:}; script=${rest%%:*}; args=""; [ "$script" != "$rest" ] && args=${rest#*:}
+      timeout -k 10 900 python -u "$script" ${args//,/ } > "$O/$name.log" 2>&1 || fail "py $name" "$O/$name.log"
+      tail -3 "$O/$name.log" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "all steps ok"

@@ -365,8 +365,8 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		bool any = false;
 		for (int t = 0; t < k1 + k2; t++) {
 			const int R = t < k1 ? t : H - k2 + (t - k1);
-			int zc = 0, zs = 0, zmin = 65535, zmax = 0;
-			long long zss = 0;
+			int zc = 0, zmin = 65535, zmax = 0;
+			long long zs = 0, zss = 0;	/* 64-bit: N up to 65535 normalised zeros up to 65534 */
 			for (int f = 0; f < N; f++) {
 				const int sr = R - d->shifty[f];
 				if (sr >= 0 && sr < H)
@@ -386,7 +386,8 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			any = true;
 			int *e = &ztab[(size_t)8 * t];
 			e[0] = zc;
-			e[1] = zs;
+			e[1] = (int)(uint32_t)(zs & 0xFFFFFFFFll);
+			e[6] = (int)(zs >> 32);
 			e[2] = (int)(uint32_t)(zss & 0xFFFFFFFFll);
 			e[3] = (int)(zss >> 32);
 			e[4] = zmin;
@@ -687,7 +688,7 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 	const unsigned long long *shards = (const unsigned long long *)dv.ctr_h;
 	const unsigned int cnt[3] = {ctr_flags[0], ctr_flags[1], ctr_flags[16]};	/* flag count, walk fault, sum maximum */
 	if (cnt[1])
-		return set_err(ctx, SG_ERR_GENERIC, "a first-pass early break needs the stale rejected[] of a pixel "
+		return set_err(ctx, SG_ERR_WALK, "a first-pass early break needs the stale rejected[] of a pixel "
 				"whose frame rows are not resident; make the full frames resident%s%.0ld", "", 0);
 	if (p.dbg == 12)
 		sg_dbg_why_dump(s);
@@ -714,19 +715,31 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		const uint16_t *d_frames, int64_t frame_stride, int64_t plane_stride, uint16_t *d_out,
 		int row_begin, int row_end, uint64_t rej[3][2], uint64_t *maxim_out, void *stream) {
-	return stack_device_core(ctx, dev_index, d, d_frames, frame_stride, plane_stride, d_out, row_begin,
+	const int rc = stack_device_core(ctx, dev_index, d, d_frames, frame_stride, plane_stride, d_out, row_begin,
 			row_end, rej, maxim_out, stream, SUM_WHOLE);
+	return rc == SG_ERR_WALK ? SG_ERR_GENERIC : rc;
 }
 
-/* HBM the host-pull path may fill with frames: SG_HOST_BUDGET_BYTES (tests), else 85 % of
- * the free device memory (plus what the context already holds for frames) */
-static size_t host_budget(const sg_ctx *ctx, SgDevice &dv) {
+/* device bytes a stack call holds besides the frames: the output image (2 B per sample),
+ * flag list and redo list (4 + 4 B), flag map (1 B), SUM's u32 sums (4 B), the literal
+ * kernel's scratch and the small tables */
+static size_t fixed_device_bytes(int N, int W, int H, int C) {
+	const size_t npix = (size_t)C * H * W;
+	return npix * 15 + (size_t)SG_LIT_THREADS * (((size_t)N * 5 + 15) & ~(size_t)15) + ((size_t)4 << 20);
+}
+
+/* HBM the host-pull path may fill with frames: SG_HOST_BUDGET_BYTES (tests: the frame budget
+ * itself), else 85 % of the free device memory (plus what the context already holds for
+ * frames) less the call's other buffers */
+static size_t host_budget(const sg_ctx *ctx, SgDevice &dv, int N, int W, int H, int C) {
 	if (ctx->knobs.host_budget > 0)
 		return (size_t)ctx->knobs.host_budget;
 	size_t fr = 0, tot = 0;
 	if (hipMemGetInfo(&fr, &tot) != hipSuccess)
 		return 0;
-	return (size_t)((double)(fr + dv.frames.size) * 0.85);
+	const size_t b = (size_t)((double)(fr + dv.frames.size + dv.out.size) * 0.85);
+	const size_t fixed = fixed_device_bytes(N, W, H, C);
+	return b > fixed ? b - fixed : 0;
 }
 
 /*
@@ -758,7 +771,7 @@ extern "C" int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *d, sg_read_region_
 	const int64_t halo = std::min<int64_t>((int64_t)sy_max - sy_min, H);
 	const size_t row_bytes = (size_t)N * C * W * sizeof(uint16_t);	/* one row of every frame */
 	int band = H;
-	const size_t budget = host_budget(ctx, dv);
+	const size_t budget = host_budget(ctx, dv, N, W, H, C);
 	if ((size_t)H * row_bytes > budget) {
 		const int64_t fit = (int64_t)(budget / row_bytes) - halo;
 		if (fit < 1)
@@ -783,13 +796,19 @@ extern "C" int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *d, sg_read_region_
 	if (rej)
 		for (int c = 0; c < 3; c++)
 			rej[c][0] = rej[c][1] = 0;
-	const int nbands = (H + band - 1) / band;
+	const bool banded = band < H;
 	int k = 0;
 	bool used[2] = {false, false};
-	for (int bi = 0; bi < nbands; bi++) {
-		const int b = bi * band, e = std::min(H, b + band);
+	/* extra: rows above the band kept resident besides the halo.  A first-pass early break
+	 * inherits the stale rejected[] of the previous pixel of the reference's OpenMP thread
+	 * (stacking.c:1684), i.e. of the pixel one memory row up (rows run top-down inside a
+	 * block); when that pixel lies above the band the core reports it (SG_ERR_WALK) and the
+	 * band is retried narrower with more rows above it resident (same total rows) */
+	int extra = 0;
+	for (int b = 0; b < H;) {
+		const int e = std::min(H, b + std::max(1, band - extra));
 		int lo = (int)std::max<int64_t>(0, (int64_t)b - sy_max);
-		int hi = (int)std::min<int64_t>(H - 1, (int64_t)e - 1 - sy_min);
+		int hi = (int)std::min<int64_t>(H - 1, (int64_t)e - 1 - sy_min + extra);
 		if (lo > hi)	/* every row of the band is shifted out of the frames: nothing is read */
 			lo = hi = std::min(b, H - 1);
 		const int nres = hi - lo + 1;
@@ -824,20 +843,25 @@ extern "C" int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *d, sg_read_region_
 		sg_stack_desc bd = *d;
 		bd.resident_rows[0] = lo;
 		bd.resident_rows[1] = hi + 1;
-		const int sum_mode = d->method != SG_STACK_SUM || nbands == 1 ? SUM_WHOLE
-			: bi == 0 ? SUM_FIRST_BAND : bi == nbands - 1 ? SUM_LAST_BAND : SUM_MID_BAND;
+		const int sum_mode = d->method != SG_STACK_SUM || !banded ? SUM_WHOLE
+			: b == 0 ? SUM_FIRST_BAND : e == H ? SUM_LAST_BAND : SUM_MID_BAND;
 		uint64_t brej[3][2];
 		/* base pointer biased so that memory row r of a frame plane sits at r*W */
 		const uint16_t *base = (const uint16_t *)dv.frames.p - (ptrdiff_t)lo * W;
 		int rc = stack_device_core(ctx, 0, &bd, base, (int64_t)bplane * C, (int64_t)bplane,
 				(uint16_t *)dv.out.p, b, e, brej, maxim, nullptr, sum_mode);
+		if (rc == SG_ERR_WALK && banded && hi < H - 1 && band - extra > 1) {
+			extra = std::min(band - 1, extra ? 2 * extra : 4);
+			continue;	/* same band start, narrower band, more rows above resident */
+		}
 		if (rc)
-			return rc;
+			return rc == SG_ERR_WALK ? SG_ERR_GENERIC : rc;
 		if (rej)
 			for (int c = 0; c < 3; c++) {
 				rej[c][0] += brej[c][0];
 				rej[c][1] += brej[c][1];
 			}
+		b = e;
 	}
 	HIPCHK(hipMemcpy(out, dv.out.p, (size_t)W * H * C * sizeof(uint16_t), hipMemcpyDeviceToHost));
 	return SG_OK;

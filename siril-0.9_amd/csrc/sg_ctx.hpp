@@ -104,6 +104,10 @@ struct sg_ctx {
 	SgKnobs knobs;
 };
 
+/* internal: a stale-state chain left the resident rows (mapped to SG_ERR_GENERIC at the ABI;
+ * the host-pull path retries the band with more rows resident) */
+#define SG_ERR_WALK -20
+
 static inline int set_err(sg_ctx *ctx, int code, const char *fmt, const char *a = "", long b = 0) {
 	char buf[512];
 	snprintf(buf, sizeof buf, fmt, a, b);

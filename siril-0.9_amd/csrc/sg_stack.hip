@@ -150,6 +150,13 @@ __device__ unsigned int g_sg_why[32];
 /* k_stack_replay timing (SG_HIST_DBG=12): max cycles of a pixel (total, gather, sort), pixels,
  * fp80 sd recomputations, passes (sums) */
 __device__ unsigned long long g_sg_rprof[16];
+/* the replay's per-pixel timing / counting (cycle counter reads, LDS bookkeeping) only in a
+ * probe build (make EXTRA=-DSG_REPLAY_PROF, read by SG_HIST_DBG=12); production builds carry none */
+#ifdef SG_REPLAY_PROF
+#define SG_RPROF(...) __VA_ARGS__
+#else
+#define SG_RPROF(...)
+#endif
 #define SG_WHY(k) (atomicAdd(&g_sg_why[k], 1u), SG_CLS_LITERAL)
 
 struct SgRejState {
@@ -1260,8 +1267,7 @@ __device__ __forceinline__ double replay_gsl_sd(const uint16_t *a, int n, int la
 	return __shfl(v, 0, 64);
 }
 __device__ __forceinline__ double replay_gsl_sd(SgReplayLds &L, const uint16_t *a, int n, int lane) {
-	if (lane == 0)
-		L.nsd++;
+	SG_RPROF(if (lane == 0) L.nsd++;)
 	return replay_gsl_sd(a, n, lane);
 }
 
@@ -1497,8 +1503,7 @@ __device__ int replay_sigma_fast(SgReplayLds &L, int &N, int &r, int &iter, doub
 			break;
 		}
 		iter++;
-		if (lane == 0)
-			L.npass++;
+		SG_RPROF(if (lane == 0) L.npass++;)
 #pragma unroll
 		for (int k = 0; k < KM; k++) {
 			const int j = 64 * k + lane;
@@ -1578,14 +1583,13 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 	}
 	__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 	replay_sort_any(L.stack, N, lane);	/* the quicksort_s of the first pass; later passes keep it sorted */
-	if (lane == 0)
-		L.t_sort = __builtin_readcyclecounter();
+	SG_RPROF(if (lane == 0) L.t_sort = __builtin_readcyclecounter();)
 	if ((type == 2 || (type == 4 && SG_REPLAY_WFAST)) && N <= SG_REPLAY_FASTN) {
 		const int done = replay_sigma_fast(L, N, r, iter, sl, sh, lane, clo, chi, value, type);
-		if (lane == 0) {
+		SG_RPROF(if (lane == 0) {
 			L.t_fast = __builtin_readcyclecounter();
 			L.handover = !done;
-		}
+		})
 		if (done) {
 			*rlo = clo;
 			*rhi = chi;
@@ -1594,8 +1598,7 @@ __device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double 
 	}
 	do {
 		iter++;
-		if (lane == 0)
-			L.npass++;
+		SG_RPROF(if (lane == 0) L.npass++;)
 		uint64_t S, SS;
 		replay_moments(L.stack, N, lane, S, SS);
 		bool e0;
@@ -1816,27 +1819,28 @@ k_stack_replay(SgStackParams p) {
 		const int x = (int)(pix % p.W);
 		const int64_t cr = pix / p.W;
 		const int R = (int)(cr % p.H), c = (int)(cr / p.H);
-		const unsigned long long t0 = __builtin_readcyclecounter();
+		SG_RPROF(const unsigned long long t0 = __builtin_readcyclecounter();)
 		if (p.N <= SG_REPLAY_FASTN)
 			replay_gather_batched(p, L.stack, c, R, x, lane);
 		else
 			for (int f = lane; f < p.N; f += 64)
 				L.stack[f] = sg_gather(p, f, c, R, x);
 		__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-		const unsigned long long t1 = __builtin_readcyclecounter();
+		SG_RPROF(const unsigned long long t1 = __builtin_readcyclecounter();
 		if (lane == 0) {
 			L.nsd = 0;
 			L.npass = 0;
 			L.handover = 0;
 			L.t_sort = t1;
 			L.t_fast = t1;
-		}
+		})
 		uint16_t v;
 		uint32_t rl, rh;
 		const int ok = p.N <= SG_REPLAY_FASTN ? replay_pixel<SG_REPLAY_FASTN / 64>(L, p.N, p.rejection, p.sig0, p.sig1,
 									     lane, &v, &rl, &rh)
 						     : replay_pixel<SG_REPLAY_MAXN / 64>(L, p.N, p.rejection, p.sig0, p.sig1,
 									     lane, &v, &rl, &rh);
+#ifdef SG_REPLAY_PROF
 		if (p.dbg == 12 && lane == 0) {
 			const unsigned long long t2 = __builtin_readcyclecounter();
 			atomicMax(&g_sg_rprof[0], t2 - t0);
@@ -1856,6 +1860,7 @@ k_stack_replay(SgStackParams p) {
 			atomicMax(&g_sg_rprof[13], L.t_fast - L.t_sort);
 			atomicMax(&g_sg_rprof[14], (unsigned long long)L.npass);
 		}
+#endif
 		if (!ok)
 			continue;
 		if (lane == 0) {

@@ -1176,14 +1176,14 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 	 * (zrow): at the image edges a frame shifted out in both directions gives 0 instead (the x
 	 * shift's zero is not normalised, :1628-1632), and the sample count alone cannot tell one
 	 * such frame from an unrelated out-of-band sample */
-	int zc = 0, zs = 0, zmax = 0;
-	long long zss = 0;
+	int zc = 0, zmax = 0;
+	long long zs = 0, zss = 0;
 	if (ZT && REJ == 2 && zrow && p.ztab) {
 		const int t = R < p.ztab_k1 ? R : (R >= p.H - p.ztab_k2 ? p.ztab_k1 + (R - (p.H - p.ztab_k2)) : -1);
 		if (t >= 0) {
 			const int *e = p.ztab + 8 * t;
 			zc = e[0];
-			zs = e[1];
+			zs = (long long)(uint32_t)e[1] | ((long long)e[6] << 32);
 			zss = (long long)(uint32_t)e[2] | ((long long)e[3] << 32);
 			zmax = e[5];
 		}
@@ -1213,8 +1213,8 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 			if (zc) {	/* the normalised zeros join the below-band samples */
 				const long long l = lo;
 				P.Z.c += zc;
-				P.Z.s += (long long)zs - (long long)zc * l;
-				P.Z.ss += (unsigned long long)(zss - 2 * l * (long long)zs + (long long)zc * l * l);
+				P.Z.s += zs - (long long)zc * l;
+				P.Z.ss += (unsigned long long)(zss - 2 * l * zs + (long long)zc * l * l);
 				P.nz += zc;
 				P.zmax = zmax;
 			}

@@ -206,3 +206,23 @@ def test_host_pull_budget_too_small(gpu_ctx):
     desc, keep = sg.make_desc(sg.MEAN, N, W, H, C, rejection=sg.SIGMA)
     rc, out, rej, _, err = _with_budget(N * C * W * 2 - 1, lambda c: c.stack_host(desc, frames) + (c.error(),))
     assert rc == -2 and "fit" in err
+
+
+@pytest.mark.parametrize("max_thread", [1, 2])
+def test_host_pull_band_inherits_stale_state(gpu_ctx, max_thread):
+    """host-pull row bands whose first pixel breaks early in its first pass and inherits the
+    stale rejected[] of the pixel one memory row above the band (src/stacking/stacking.c:1684):
+    the band is retried narrower with rows above it resident, the result equals the oracle"""
+    world, H, W, N = 2, 12, 70, 6
+    frames = _early_break_frames(world, H, W, N)
+    z = np.zeros(N, np.int32)
+    sig = (1.0, 1.0)
+    ref, rej_ref = _oracle(frames, sg.MEAN, sg.SIGMA, sig, z, z, max_thread)
+    b, e = sd.row_band(0, world, H)
+    budget = N * W * 2 * (e - b)            # bands of exactly the planted band's rows
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=sg.SIGMA, sig=sig, shiftx=z, shifty=z,
+                              max_thread=max_thread, max_number_of_rows=H)
+    rc, out, rej, _, err = _with_budget(budget, lambda c: c.stack_host(desc, frames) + (c.error(),))
+    assert rc == 0, err
+    assert_same(out, ref, f"host bands with stale state, thr={max_thread}")
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
