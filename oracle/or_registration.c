@@ -19,8 +19,63 @@
 #include <stdint.h>
 #include "oracle.h"
 
+/* out-of-place 1-D complex DFT of length n (input stride `is`): recursive mixed radix by
+ * decimation in time over the smallest prime factor p of n (n = p m: p sub-transforms of the
+ * decimated sequences, combined with twiddles exp(sign 2 pi i k / n)); a prime n is summed
+ * directly in O(n^2).  Plain double, FFTW's sign convention. */
+static void dft_rec(const double *xr, const double *xi, int is, double *yr, double *yi, int n, int sign) {
+	if (n == 1) {
+		yr[0] = xr[0];
+		yi[0] = xi[0];
+		return;
+	}
+	int p = 2;
+	while (p * p <= n && n % p)
+		p++;
+	if (n % p)
+		p = n;	/* prime */
+	if (p == n) {
+		for (int k = 0; k < n; k++) {
+			double sr = 0, si = 0;
+			for (int t = 0; t < n; t++) {
+				const double a = sign * 2.0 * M_PI * (double)(((long)k * t) % n) / n;
+				const double c = cos(a), s = sin(a);
+				sr += xr[(size_t)t * is] * c - xi[(size_t)t * is] * s;
+				si += xr[(size_t)t * is] * s + xi[(size_t)t * is] * c;
+			}
+			yr[k] = sr;
+			yi[k] = si;
+		}
+		return;
+	}
+	const int m = n / p;
+	/* sub-transform q (inputs x[q], x[q+p], ...) into y[q m .. q m + m) */
+	for (int q = 0; q < p; q++)
+		dft_rec(xr + (size_t)q * is, xi + (size_t)q * is, is * p, yr + (size_t)q * m, yi + (size_t)q * m, m, sign);
+	double *tr = malloc((size_t)n * sizeof(double)), *ti = malloc((size_t)n * sizeof(double));
+	for (int k = 0; k < m; k++)
+		for (int s = 0; s < p; s++) {
+			/* X[k + s m] = sum_q W_n^{q (k + s m)} Y_q[k] */
+			const int kk = k + s * m;
+			double sr = 0, si = 0;
+			for (int q = 0; q < p; q++) {
+				const double a = sign * 2.0 * M_PI * (double)(((long)q * kk) % n) / n;
+				const double c = cos(a), sn = sin(a);
+				const double ur = yr[(size_t)q * m + k], ui = yi[(size_t)q * m + k];
+				sr += ur * c - ui * sn;
+				si += ur * sn + ui * c;
+			}
+			tr[kk] = sr;
+			ti[kk] = si;
+		}
+	memcpy(yr, tr, (size_t)n * sizeof(double));
+	memcpy(yi, ti, (size_t)n * sizeof(double));
+	free(tr);
+	free(ti);
+}
+
 /* in-place 1-D complex DFT of length n with stride 1 (radix-2 if n is a power of two,
- * otherwise direct O(n^2) summation in double) */
+ * otherwise the recursive mixed radix above) */
 static void dft1d(double *re, double *im, int n, int sign, double *wre, double *wim) {
 	if ((n & (n - 1)) == 0) {
 		/* bit reversal */
@@ -55,16 +110,7 @@ static void dft1d(double *re, double *im, int n, int sign, double *wre, double *
 		}
 	} else {
 		double *tr = malloc(n * sizeof(double)), *ti = malloc(n * sizeof(double));
-		for (int k = 0; k < n; k++) {
-			double sr = 0, si = 0;
-			for (int t = 0; t < n; t++) {
-				double a = sign * 2.0 * M_PI * (double)(((long)k * t) % n) / n;
-				sr += re[t] * cos(a) - im[t] * sin(a);
-				si += re[t] * sin(a) + im[t] * cos(a);
-			}
-			tr[k] = sr;
-			ti[k] = si;
-		}
+		dft_rec(re, im, 1, tr, ti, n, sign);
 		memcpy(re, tr, n * sizeof(double));
 		memcpy(im, ti, n * sizeof(double));
 		free(tr);
@@ -312,4 +358,17 @@ int or_register_shift_dft(const uint16_t *sel, int nframes, int S, int ref_image
 	}
 	free(inr); free(ini); free(ar); free(ai);
 	return 0;
+}
+
+/* The exact value behind one entry of the reference's correlation plane: FFTW_BACKWARD of
+ * FFT(ref) conj(FFT(img)) (registration.c:326-334) is S^2 sum_n ref(n + k) img(n) (circular,
+ * row-major k = ky S + kx); the sum is an integer below 2^56 for S <= 4096. */
+long long or_xcorr_at(const uint16_t *ref, const uint16_t *img, int S, int ky, int kx) {
+	long long acc = 0;
+	for (int y = 0; y < S; y++) {
+		const uint16_t *rr = ref + (size_t)((y + ky) % S) * S, *ir = img + (size_t)y * S;
+		for (int x = 0; x < S; x++)
+			acc += (long long)rr[(x + kx) % S] * ir[x];
+	}
+	return acc;
 }

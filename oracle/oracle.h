@@ -26,6 +26,8 @@
 
 #ifdef __cplusplus
 extern "C" {
+void or_synth_window(uint16_t *out, int nframes, int c, int y0, int x0, int h, int w, uint64_t seed,
+		int maxshift);
 #endif
 
 /* src/stacking/stacking.h:14-21 */
@@ -87,6 +89,11 @@ int or_register_shift_dft(const uint16_t *sel, int nframes, int S, int ref_image
 double or_quality_estimate(const uint16_t *buffer, int width, int height);
 /* 2-D unnormalised complex DFT in double, sign -1 forward (FFTW_FORWARD) / +1 backward */
 void or_dft2d(double *re, double *im, int S, int sign);
+/* exact circular cross-correlation sum_n ref(n + k) img(n) at shift k = (ky, kx) (int64) */
+long long or_xcorr_at(const uint16_t *ref, const uint16_t *img, int S, int ky, int kx);
+
+void or_synth_window(uint16_t *out, int nframes, int c, int y0, int x0, int h, int w, uint64_t seed,
+		int maxshift);
 
 #ifdef __cplusplus
 }

@@ -56,6 +56,10 @@ def load():
     lib.or_compute_normalization.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, P, P]
     lib.or_statistics_ikss.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P]
     lib.or_statistics_ikss.restype = ctypes.c_int
+    lib.or_synth_window.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_uint64, ctypes.c_int]
+    lib.or_xcorr_at.argtypes = [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.or_xcorr_at.restype = ctypes.c_longlong
     _lib = lib
     return lib
 
@@ -138,6 +142,23 @@ def synth(nframes, C, H, W, seed=1, maxshift=16, row_begin=0, row_end=None):
     frames = np.zeros((nframes, C, H, W), dtype=np.uint16)
     lib.or_synth_fill(_p(frames), nframes, C, H, W, row_begin, row_end, seed, maxshift)
     return frames
+
+
+def synth_window(nframes, c, y0, x0, h, w, seed=1, maxshift=16):
+    """channel c, memory rows [y0, y0+h), columns [x0, x0+w) of every synthetic frame: [N][h][w]"""
+    lib = load()
+    out = np.zeros((nframes, h, w), dtype=np.uint16)
+    lib.or_synth_window(_p(out), nframes, c, y0, x0, h, w, seed, maxshift)
+    return out
+
+
+def xcorr_at(ref, img, ky, kx):
+    """exact sum_n ref(n + k) img(n) (circular) at k = (ky, kx): the integer behind the
+    reference's correlation-plane entry (divided by S^2)"""
+    lib = load()
+    ref = np.ascontiguousarray(ref, dtype=np.uint16)
+    img = np.ascontiguousarray(img, dtype=np.uint16)
+    return int(lib.or_xcorr_at(_p(ref), _p(img), ref.shape[0], ky % ref.shape[0], kx % ref.shape[0]))
 
 
 def synth_shifts(nframes, seed=1, maxshift=16):

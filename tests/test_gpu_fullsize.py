@@ -1,14 +1,23 @@
-"""The headline workload at its full size (BASELINE configs[2]: SIGMA (4, 3) stack of 512
-synthetic 4096 x 4096 frames with registration shifts, the bench's generator and shifts),
-checked bit for bit against the C oracle on sampled row bands.
+"""Every BASELINE.json configuration at its full size, on the GPU, checked against the C
+oracle and against golden registration results (tests/golden/make_golden_fullsize.py).
 
-The oracle stacks a band of rows as a standalone image: the reference's y shift is a
-translation with zero fill outside the frame (src/stacking/stacking.c:1550-1577), so output
-rows [b, e) of the full image equal the oracle's rows of the band image [b - 16, e + 16)
-(|shifty| <= 16) whenever that band lies inside the frame or shares the frame border.  Bands:
-the top and bottom rows (out-of-frame zero fill) and a middle band.  At N = 512 the first
-clipping pass never breaks early, so no pixel depends on the previous pixel's stale
-rejected[] (the band's thread order cannot matter)."""
+  configs[0]  stack_summing of 16 x 1024 x 1024 u16 mono FITS files, from the files
+  configs[1]  128 x 2048 x 2048 u16 mono SER file: device load, full-frame DFT registration,
+              NO_REJEC mean stack with the found shifts (device and host-pull paths)
+  configs[2]  SIGMA (4, 3) stack of 512 x 4096 x 4096, the WHOLE image against the oracle
+  configs[3]  the same stack as 8 row bands (the multi-GPU partition, band-only residency
+              windows) equal to the one-call image
+  configs[4]  256 x 3 x 4000 x 6000: DFT registration of layer 1's centred 2048 selection,
+              WINSORIZED (4, 3) stack of all three channels with those shifts, sampled row bands
+              of every channel against the oracle
+
+Frames are the synthetic sequence of include/sg_synth.h (generated in HBM by the library,
+and by the oracle for the golden files).  At these frame counts no first sigma pass breaks
+early, so the oracle's OpenMP thread order (which only matters for stale rejected[]) cannot
+change a pixel, and a row band of the oracle's image equals the oracle run on that band plus
+its 16-row shift halo (the y shift is a translation with zero fill,
+src/stacking/stacking.c:1550-1577).
+"""
 import os
 import sys
 
@@ -17,65 +26,193 @@ import pytest
 
 import oracle_lib as orc
 import sirilgpu as sg
+import sirilgpu_dist as sd
+from seq_files import write_fits, write_ser
 
 pytestmark = pytest.mark.gpu
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
-def test_sigma_full_size_bands_match_oracle(gpu_ctx):
+def normalize_quality(raw, ref_image=0, included=None):
+    """normalizeQualityData (src/registration/registration.c:163-176) with q_min / q_max as
+    register_shift_dft forms them (:270-324: seeded by the reference, then frames in index
+    order, siril.h's min() macro)"""
+    n = len(raw)
+    inc = np.ones(n, bool) if included is None else np.asarray(included, bool)
+    q_min = q_max = raw[ref_image]
+    for f in range(n):
+        if f == ref_image or not inc[f]:
+            continue
+        q = raw[f]
+        if q > q_max:
+            q_max = q
+        q_min = q_min if q_min < q else q
+    out = raw.copy()
+    for f in range(n):
+        if inc[f]:
+            out[f] = (raw[f] - q_min) / (q_max - q_min)
+    return out
+
+
+def _free():
+    import torch
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
+def test_cfg0_fits_summing_from_files(tmp_path, gpu_ctx):
+    """configs[0]: stack_summing (src/stacking/stacking.c:196-355) of 16 x 1024^2 FITS files with
+    registration shifts, fed by the library's FITS region reader (host-pull) and by the device
+    decode path; the 65535/max scaling applies (16 frames of ~1000 ADU)"""
+    import torch
+    N, C, H, W, M = 16, 1, 1024, 1024, 16
+    frames = orc.synth(N, C, H, W, seed=0xF175, maxshift=M)
+    sx, sy = orc.synth_shifts(N, seed=0xF175, maxshift=M)
+    paths = []
+    for i in range(N):
+        p = str(tmp_path / f"light_{i + 1:05d}.fit")
+        write_fits(p, frames[i])
+        paths.append(p)
+    rc, ref, mref = orc.stack_sum(frames, sx, sy)
+    assert rc == 0 and mref > 65535
+    desc, keep = sg.make_desc(sg.SUM, N, W, H, C, shiftx=sx, shifty=sy)
+    with sg.Seq.open_fits(paths) as seq:
+        rc, out, _, maxim = gpu_ctx.stack_seq(desc, seq)
+        assert rc == 0, gpu_ctx.error()
+        assert maxim == mref
+        assert np.array_equal(out, ref)
+        d = torch.zeros(N * C * H * W, dtype=torch.int16, device="cuda")
+        o = torch.zeros(C * H * W, dtype=torch.int16, device="cuda")
+        torch.cuda.synchronize()
+        gpu_ctx.load_seq_device(seq, d.data_ptr())
+        _, m2 = gpu_ctx.stack_device(desc, d.data_ptr(), C * H * W, H * W, o.data_ptr(), 0, H)
+        assert m2 == mref
+        assert np.array_equal(o.cpu().numpy().view(np.uint16).reshape(C, H, W), ref)
+    assert ref[0, 0, 0] == 0          # pixel 0 is never accumulated (:307)
+
+
+def test_cfg1_ser_register_mean(tmp_path, gpu_ctx):
+    """configs[1]: a 128 x 2048^2 SER file written the way ser_write_frame_from_fit does,
+    decoded into HBM, registered on the full frame, mean-stacked with the found shifts"""
+    import torch
+    g = np.load(os.path.join(GOLDEN, "register_cfg1.npz"))
+    N, C, H, W, layer, S, y0, x0, seed, M = (int(v) for v in g["geometry"])
+    fr = torch.empty(N * H * W, dtype=torch.int16, device="cuda")
+    gpu_ctx.synth_fill(fr.data_ptr(), N, 1, H, W, 0, H, seed, M)
+    frames = fr.cpu().numpy().view(np.uint16).reshape(N, 1, H, W)
+    path = str(tmp_path / "cfg1.ser")
+    write_ser(path, frames, depth=16)
+    loaded = torch.zeros(N * H * W, dtype=torch.int16, device="cuda")
+    with sg.Seq.open_ser(path) as seq:
+        assert seq.shape == (N, 1, H, W)
+        torch.cuda.synchronize()
+        gpu_ctx.load_seq_device(seq, loaded.data_ptr())
+        assert torch.equal(loaded, fr), "SER decode differs from the generated frames"
+        # registration (full-frame selection: the decoded frames themselves)
+        sx, sy, q = gpu_ctx.register_dft_device(loaded.data_ptr(), N, S)
+        assert np.array_equal(sx, g["shiftx"]) and np.array_equal(sy, g["shifty"]), "shifts differ from golden"
+        _, _, qraw = gpu_ctx.register_dft_device(loaded.data_ptr(), N, S, raw_quality=True)
+        assert np.array_equal(qraw, g["quality_raw"]), "raw quality differs from golden"
+        assert np.array_equal(q, normalize_quality(g["quality_raw"])), "normalised quality differs"
+        # NO_REJEC mean with the found shifts, device path and host-pull path (the SER region reader)
+        rc, ref, _ = orc.stack_rejection(frames, sg.NO_REJEC, shiftx=sx, shifty=sy, max_thread=16)
+        assert rc == 0
+        desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=sg.NO_REJEC, shiftx=sx, shifty=sy,
+                                  max_thread=16, max_number_of_rows=H)
+        o = torch.zeros(H * W, dtype=torch.int16, device="cuda")
+        torch.cuda.synchronize()
+        gpu_ctx.stack_device(desc, loaded.data_ptr(), H * W, H * W, o.data_ptr(), 0, H)
+        assert np.array_equal(o.cpu().numpy().view(np.uint16).reshape(1, H, W), ref)
+        rc, out, _, _ = gpu_ctx.stack_seq(desc, seq)
+        assert rc == 0, gpu_ctx.error()
+        assert np.array_equal(out, ref)
+    del fr, loaded, o
+    _free()
+
+
+def _sigma_cfg2(gpu_ctx):
     import torch
     import bench
     N, H, W, M = 512, 4096, 4096, 16
     frames = torch.empty(N * H * W, dtype=torch.int16, device="cuda")
-    out = torch.zeros(H * W, dtype=torch.int16, device="cuda")
-    torch.cuda.synchronize()
     gpu_ctx.synth_fill(frames.data_ptr(), N, 1, H, W, 0, H, 0x5151, M)
     sx, sy = bench.synth_shifts_np(N, 0x5151, M)
-    assert int(np.abs(sy).max()) <= M
+    return frames, sx, sy, (N, H, W, M)
+
+
+def test_cfg2_sigma_whole_image_and_cfg3_bands(gpu_ctx):
+    """configs[2] (the headline workload): the whole 512 x 4096^2 SIGMA (4, 3) image and the
+    rejection counters against the oracle; configs[3]'s partition (8 row bands, each call with
+    only its band's rows + shift halo declared resident) equal to the one-call image"""
+    import torch
+    frames, sx, sy, (N, H, W, M) = _sigma_cfg2(gpu_ctx)
     desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=sg.SIGMA, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
                               max_thread=16, max_number_of_rows=H)
-    rej, _ = gpu_ctx.stack_device(desc, frames.data_ptr(), H * W, H * W, out.data_ptr(), 0, H)
-    torch.cuda.synchronize()
-    img = out.cpu().numpy().view(np.uint16).reshape(H, W)
-    fr = frames.view(N, H, W)
-    for b, e in [(0, 64), (2016, 2080), (H - 64, H)]:
-        lo, hi = max(0, b - M), min(H, e + M)
-        band = fr[:, lo:hi, :].cpu().numpy().view(np.uint16)[:, None]
-        # 4 row blocks of >= 20 rows (max_number_of_rows / max_thread = 24): every block is
-        # taller than the shifts, as the reference needs (its offset bug)
-        rc, ref, _ = orc.stack_rejection(band, sg.SIGMA, sig=(4.0, 3.0), shiftx=sx, shifty=sy, max_thread=16,
-                                         max_number_of_rows=16 * 24)
-        assert rc == 0
-        got, want = img[b:e], ref[0, b - lo:e - lo]
-        bad = np.argwhere(got != want)
-        assert bad.size == 0, f"rows {b}..{e}: {len(bad)} pixels differ, first {bad[:3].tolist()}"
-    # the whole image: every pixel written, values in the synthetic range
-    assert int(img.min()) > 0 and np.isfinite(img).all()
-
-
-def test_winsorized_full_size_bands_match_oracle(gpu_ctx):
-    """configs[4]'s frame size and rejection (256 frames of 6000 x 4000, WINSORIZED (4, 3)),
-    one channel, sampled row bands against the oracle"""
-    import torch
-    import bench
-    N, H, W, M = 256, 4000, 6000, 16
-    frames = torch.empty(N * H * W, dtype=torch.int16, device="cuda")
     out = torch.zeros(H * W, dtype=torch.int16, device="cuda")
     torch.cuda.synchronize()
-    gpu_ctx.synth_fill(frames.data_ptr(), N, 1, H, W, 0, H, 0x7777, M)
-    sx, sy = bench.synth_shifts_np(N, 0x7777, M)
-    desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=sg.WINSORIZED, sig=(4.0, 3.0), shiftx=sx,
-                              shifty=sy, max_thread=16, max_number_of_rows=H)
-    gpu_ctx.stack_device(desc, frames.data_ptr(), H * W, H * W, out.data_ptr(), 0, H)
-    torch.cuda.synchronize()
+    rej, _ = gpu_ctx.stack_device(desc, frames.data_ptr(), H * W, H * W, out.data_ptr(), 0, H)
     img = out.cpu().numpy().view(np.uint16).reshape(H, W)
-    fr = frames.view(N, H, W)
-    for b, e in [(0, 64), (1968, 2032), (H - 64, H)]:
-        lo, hi = max(0, b - M), min(H, e + M)
-        band = fr[:, lo:hi, :].cpu().numpy().view(np.uint16)[:, None]
-        rc, ref, _ = orc.stack_rejection(band, sg.WINSORIZED, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
-                                         max_thread=16, max_number_of_rows=16 * 24)
-        assert rc == 0
-        got, want = img[b:e], ref[0, b - lo:e - lo]
-        bad = np.argwhere(got != want)
-        assert bad.size == 0, f"rows {b}..{e}: {len(bad)} pixels differ, first {bad[:3].tolist()}"
+    # configs[3]: 8 bands, each with a resident window of its rows + halo (no copies: the
+    # window is declared on the whole buffer, so any read outside it is refused, not served)
+    G = 8
+    out8 = torch.zeros(H * W, dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
+    rej8 = np.zeros((3, 2), np.uint64)
+    for r in range(G):
+        b, e = sd.row_band(r, G, H)
+        lo, hi = max(0, b - int(sy.max())), min(H - 1, e - 1 - int(sy.min()))
+        d8, k8 = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=sg.SIGMA, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                              max_thread=16, max_number_of_rows=H, resident_rows=(lo, hi + 1))
+        rj, _ = gpu_ctx.stack_device(d8, frames.data_ptr(), H * W, H * W, out8.data_ptr(), b, e)
+        rej8 += rj
+    assert torch.equal(out8, out), "8-band stack differs from the one-call stack"
+    assert np.array_equal(rej8, rej)
+    host = frames.cpu().numpy().view(np.uint16).reshape(N, 1, H, W)
+    del frames, out, out8
+    _free()
+    rc, ref, rej_ref = orc.stack_rejection(host, sg.SIGMA, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                                           max_thread=16, max_number_of_rows=H)
+    assert rc == 0
+    bad = np.argwhere(img != ref[0])
+    assert bad.size == 0, f"{len(bad)} pixels differ from the oracle, first {bad[:3].tolist()}"
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+
+
+def test_cfg4_rgb_register_and_winsorized(gpu_ctx):
+    """configs[4] on one GPU: 256 x 3 x 4000 x 6000 frames in HBM, DFT registration of layer 1's
+    centred 2048 selection (golden shifts and qualities), WINSORIZED (4, 3) stack of all three
+    channels with the found shifts, 3 row bands of every channel against the oracle"""
+    import torch
+    g = np.load(os.path.join(GOLDEN, "register_cfg4.npz"))
+    N, C, H, W, layer, S, y0, x0, seed, M = (int(v) for v in g["geometry"])
+    frames = torch.empty(N * C * H * W, dtype=torch.int16, device="cuda")
+    gpu_ctx.synth_fill(frames.data_ptr(), N, C, H, W, 0, H, seed, M)
+    fv = frames.view(N, C, H, W)
+    sel = fv[:, layer, y0:y0 + S, x0:x0 + S].contiguous()     # seq_read_frame_part of layer 1
+    torch.cuda.synchronize()
+    sx, sy, q = gpu_ctx.register_dft_device(sel.data_ptr(), N, S)
+    assert np.array_equal(sx, g["shiftx"]) and np.array_equal(sy, g["shifty"]), "shifts differ from golden"
+    _, _, qraw = gpu_ctx.register_dft_device(sel.data_ptr(), N, S, raw_quality=True)
+    assert np.array_equal(qraw, g["quality_raw"])
+    assert np.array_equal(q, normalize_quality(g["quality_raw"]))
+    del sel
+    out = torch.zeros(C * H * W, dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, C, rejection=sg.WINSORIZED, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                              max_thread=16, max_number_of_rows=H)
+    gpu_ctx.stack_device(desc, frames.data_ptr(), C * H * W, H * W, out.data_ptr(), 0, H)
+    img = out.cpu().numpy().view(np.uint16).reshape(C, H, W)
+    for c in range(C):
+        for b, e in [(0, 32), (H // 2 - 16, H // 2 + 16), (H - 32, H)]:
+            lo, hi = max(0, b - M), min(H, e + M)
+            band = fv[:, c, lo:hi, :].cpu().numpy().view(np.uint16)[:, None]
+            rc, ref, _ = orc.stack_rejection(band, sg.WINSORIZED, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                                             max_thread=16, max_number_of_rows=16 * 24)
+            assert rc == 0
+            got, want = img[c, b:e], ref[0, b - lo:e - lo]
+            bad = np.argwhere(got != want)
+            assert bad.size == 0, f"channel {c} rows {b}..{e}: {len(bad)} pixels differ, first {bad[:3].tolist()}"
+    del frames, out, fv
+    _free()
