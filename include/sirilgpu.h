@@ -149,6 +149,9 @@ int sg_get_last_stats(const sg_ctx *ctx, sg_stack_stats *st);
  */
 int sg_frame_stats_ikss_device(sg_ctx *ctx, int dev_index, const uint16_t *d_frames, int nframes, int C,
 		int H, int W, int64_t frame_stride, double *location, double *scale, void *stream);
+/* the same on host frames (what seq_get_imstats computes from a loaded frame) */
+int sg_frame_stats_ikss(sg_ctx *ctx, const uint16_t *frames, int nframes, int C, int H, int W,
+		double *location, double *scale);
 /* compute_normalization (src/stacking/stacking.c:125-190): offset / mul / scale [nframes]
  * from per-frame location / scale (host arithmetic; ref_image -1 = 0) */
 int sg_compute_normalization(int mode, int nframes, int ref_image, const double *location,

@@ -36,6 +36,18 @@ int sg_seq_get_info(const sg_seq *seq, sg_seq_info *info);
  * `layer` of frame `index` (ser_read_opened_partial src/io/ser.c:772-971,
  * read_opened_fits_partial src/io/image_format_fits.c:581-635); 0 ok, -1 failure */
 int sg_seq_read_region(void *seq, int layer, int index, uint16_t *buffer, const sg_rect *area);
+/*
+ * seq_read_frame_part (src/io/sequence.c:567-609): the registration selection `area` (display
+ * coordinates: x, y of the top-left corner, y counted from the top) of channel `layer` of frame
+ * `index`, written bottom-up (Siril memory order, area->w x area->h) as register_shift_dft
+ * receives it.  FITS (readfits_partial, src/io/image_format_fits.c:462-574): file rows
+ * fpixel[1] = ry - y - h .. ry - y - 1 (:512), ONE ROW LOWER than the region reader's
+ * ry - y - h + 1 .. ry - y (:601); a selection touching the bottom display row gives
+ * fpixel[1] = 0, which cfitsio refuses -> SG_ERR_READ.  SER (ser_read_frame + flip +
+ * extract_region_from_fits :1167-1192, demosaiced first when sg_seq_set_debayer is on):
+ * memory rows ry - y - h .. ry - y - 1.  0 / SG_ERR_*
+ */
+int sg_seq_read_selection(const sg_seq *seq, int layer, int index, const sg_rect *area, uint16_t *out);
 /* seq_read_frame (src/io/sequence.c): whole frame, planar, bottom-up (Siril memory order) */
 int sg_seq_read_frame(const sg_seq *seq, int index, uint16_t *out);
 /* frames [first, first+count) decoded on the device into d_frames[f*frame_stride + ...]
@@ -51,8 +63,11 @@ int sg_seq_load_device(sg_ctx *ctx, int dev_index, const sg_seq *seq, int first,
  * sg_seq_load_device demosaics on the device (borders 0, as the reference leaves them).
  * pattern: SG_BAYER_* (the sensor_pattern order of src/core/siril.h:266-271), or -1 = the
  * one the SER ColorID names (use_bayer_header, retrieveSERBayerPattern ser.c:453-471).
- * Host reads (sg_seq_read_region / sg_seq_read_frame) of a demosaiced sequence are not
- * provided and fail with SG_ERR_GENERIC. 0, or SG_ERR_GENERIC for a non-CFA sequence. */
+ * Host reads demosaic too: sg_seq_read_region returns the layer of the demosaiced band as
+ * ser_read_opened_partial's CFA branch does (src/io/ser.c:820-913: a widened area demosaiced,
+ * then cropped), so a CFA SER can be stacked through sg_stack_u16; sg_seq_read_frame and
+ * sg_seq_read_selection demosaic the frame like ser_read_frame.
+ * 0, or SG_ERR_GENERIC for a non-CFA sequence. */
 enum { SG_BAYER_RGGB = 0, SG_BAYER_BGGR = 1, SG_BAYER_GBRG = 2, SG_BAYER_GRBG = 3 };
 int sg_seq_set_debayer(sg_seq *seq, int pattern);
 

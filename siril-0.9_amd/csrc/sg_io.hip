@@ -306,15 +306,58 @@ extern "C" int sg_seq_set_debayer(sg_seq *s, int pattern) {
 	return SG_OK;
 }
 
+/* bayer_Bilinear (src/algos/demosaicing.c:89-176) on the host for top-down rows [ty0, ty1),
+ * columns [x0, x0 + w) of one layer of a CFA frame: the per-pixel rule of k_debayer_frames
+ * (a red / blue centre: the 4 greens and the 4 diagonal opposites, (sum + 2) >> 2; a green
+ * centre: its row's pair and the column's pair, (a + b + 1) >> 1; the one-pixel image border
+ * stays 0).  This is what ser_read_opened_partial's CFA branch (src/io/ser.c:820-913) returns:
+ * it demosaics an area widened by get_debayer_area (demosaicing.c:787-859, even offsets, so
+ * the pattern phase is kept; the widened area's own border ring only reaches the output where
+ * it is the image border), then extracts the layer.  Rows y - 1 .. y + h are read. */
+static int debayer_rows_host(const sg_seq *s, int index, int layer, int ty0, int ty1, int x0, int w, uint16_t *out) {
+	const int W = s->width, H = s->height, bps = s->bytes_per_sample;
+	const int r0 = ty0 - 1 < 0 ? 0 : ty0 - 1, r1 = ty1 + 1 > H ? H : ty1 + 1;
+	const int64_t base = s->data_off[0] + s->frame_bytes * (int64_t)index;
+	std::vector<unsigned char> raw((size_t)(r1 - r0) * W * bps);
+	if (rd_exact(s->fd[0], raw.data(), raw.size(), base + (int64_t)r0 * W * bps))
+		return -1;
+	int bad = 0;
+	auto at = [&](int yy, int xx) -> int {
+		return conv_host(&raw[((size_t)(yy - r0) * W + xx) * bps], s->enc, &bad);
+	};
+	static const int cell[4][2][2] = {{{0, 1}, {1, 2}}, {{2, 1}, {1, 0}}, {{1, 2}, {0, 1}}, {{1, 0}, {2, 1}}};
+	const int pat = s->debayer;
+	for (int ty = ty0; ty < ty1; ty++)
+		for (int x = x0; x < x0 + w; x++) {
+			int rgb[3] = {0, 0, 0};
+			if (ty >= 1 && ty <= H - 2 && x >= 1 && x <= W - 2) {
+				const int col = cell[pat][ty & 1][x & 1];
+				const int c = at(ty, x);
+				if (col != 1) {
+					rgb[col] = c;
+					rgb[1] = (at(ty - 1, x) + at(ty, x - 1) + at(ty, x + 1) + at(ty + 1, x) + 2) >> 2;
+					rgb[2 - col] = (at(ty - 1, x - 1) + at(ty - 1, x + 1) + at(ty + 1, x - 1) + at(ty + 1, x + 1) + 2) >> 2;
+				} else {
+					const int rowc = cell[pat][ty & 1][(x + 1) & 1];
+					rgb[1] = c;
+					rgb[rowc] = (at(ty, x - 1) + at(ty, x + 1) + 1) >> 1;
+					rgb[2 - rowc] = (at(ty - 1, x) + at(ty + 1, x) + 1) >> 1;
+				}
+			}
+			out[(size_t)(ty - ty0) * w + (x - x0)] = (uint16_t)rgb[layer];
+		}
+	return bad ? -1 : 0;
+}
+
 static int sg_seq_read_region_impl(void *user, int layer, int index, uint16_t *buffer, const sg_rect *area) {
 	const sg_seq *s = (const sg_seq *)user;
 	if (!s || !buffer || !area || index < 0 || index >= s->frames || layer < 0 || layer >= s->layers)
 		return -1;
-	if (s->debayer >= 0)
-		return -1;	/* demosaicing runs on the device only (sg_seq_load_device) */
 	if (area->x < 0 || area->y < 0 || area->w <= 0 || area->h <= 0 || area->x + area->w > s->width ||
 			area->y + area->h > s->height)
 		return -1;
+	if (s->debayer >= 0)	/* CFA SER opened with demosaicing: top-down rows y .. y+h-1 */
+		return debayer_rows_host(s, index, layer, area->y, area->y + area->h, area->x, area->w, buffer);
 	const int bps = s->bytes_per_sample;
 	const int fd = s->kind == SG_SRC_SER ? s->fd[0] : s->fd[index];
 	const int64_t base = s->kind == SG_SRC_SER ? s->data_off[0] + s->frame_bytes * (int64_t)index : s->data_off[index];
@@ -357,8 +400,19 @@ extern "C" int sg_seq_read_region(void *user, int layer, int index, uint16_t *bu
 }
 
 static int sg_seq_read_frame_impl(const sg_seq *s, int index, uint16_t *out) {
-	if (!s || !out || index < 0 || index >= s->frames || s->debayer >= 0)
+	if (!s || !out || index < 0 || index >= s->frames)
 		return SG_ERR_GENERIC;
+	if (s->debayer >= 0) {	/* ser_read_frame: debayer() then fits_flip_top_to_bottom (ser.c:730,758) */
+		const int W = s->width, H = s->height;
+		std::vector<uint16_t> td((size_t)W * H);
+		for (int c = 0; c < 3; c++) {
+			if (debayer_rows_host(s, index, c, 0, H, 0, W, td.data()))
+				return SG_ERR_READ;
+			for (int r = 0; r < H; r++)
+				memcpy(out + ((size_t)c * H + r) * W, td.data() + (size_t)(H - 1 - r) * W, (size_t)W * sizeof(uint16_t));
+		}
+		return SG_OK;
+	}
 	const int fd = s->kind == SG_SRC_SER ? s->fd[0] : s->fd[index];
 	const int64_t base = s->kind == SG_SRC_SER ? s->data_off[0] + s->frame_bytes * (int64_t)index : s->data_off[index];
 	std::vector<unsigned char> raw((size_t)s->frame_bytes);
@@ -386,6 +440,57 @@ static int sg_seq_read_frame_impl(const sg_seq *s, int index, uint16_t *out) {
 extern "C" int sg_seq_read_frame(const sg_seq *s, int index, uint16_t *out) {
 	try {
 		return sg_seq_read_frame_impl(s, index, out);
+	} catch (const std::exception &) {
+		return SG_ERR_SIZE;
+	}
+}
+
+/* seq_read_frame_part (src/io/sequence.c:567-609): the selection `area` (display coordinates,
+ * y from the top) of one layer, bottom-up.  FITS: readfits_partial (image_format_fits.c:462-574)
+ * reads file rows fpixel[1] = ry - y - h .. lpixel[1] = ry - y - 1 (1-based, :512-516), no
+ * reversal: one row LOWER than the region reader's ry - y - h + 1 .. ry - y (:601-604); cfitsio
+ * refuses fpixel < 1 or lpixel > naxes (a selection touching the bottom display row fails, and
+ * so does the reference's registration on FITS).  SER: ser_read_frame (full frame, debayered
+ * for a CFA SER opened with demosaicing, flipped bottom-up) + extract_region_from_fits
+ * (:1167-1192): memory rows ry - y - h .. ry - y - 1. */
+static int sg_seq_read_selection_impl(const sg_seq *s, int layer, int index, const sg_rect *a, uint16_t *out) {
+	if (!s || !a || !out || index < 0 || index >= s->frames || layer < 0 || layer >= s->layers || a->w < 1 || a->h < 1)
+		return SG_ERR_GENERIC;
+	const int W = s->width, H = s->height, bps = s->bytes_per_sample;
+	int bad = 0;
+	if (s->kind == SG_SRC_FITS) {
+		const long f1 = (long)H - a->y - a->h, l1 = (long)H - a->y - 1;	/* 1-based file rows */
+		if (a->x < 0 || a->x + a->w > W || f1 < 1 || l1 > H)
+			return SG_ERR_READ;
+		const int64_t plane = (int64_t)W * H * bps;
+		std::vector<unsigned char> raw((size_t)a->w * bps);
+		for (int r = 0; r < a->h; r++) {
+			const int64_t frow = f1 - 1 + r;	/* 0-based file row = memory row */
+			if (rd_exact(s->fd[index], raw.data(), raw.size(), s->data_off[index] + plane * layer + (frow * W + a->x) * bps))
+				return SG_ERR_READ;
+			for (int x = 0; x < a->w; x++)
+				out[(size_t)r * a->w + x] = conv_host(&raw[(size_t)x * bps], s->enc, &bad);
+		}
+		return bad ? SG_ERR_GENERIC : SG_OK;
+	}
+	/* SER: memory rows m0 .. m0 + h - 1 are top-down rows H-1-m0 .. ; extract_region_from_fits
+	 * has no bounds check (reading outside is undefined there): refused here */
+	const int m0 = H - a->y - a->h;
+	if (a->x < 0 || a->x + a->w > W || a->y < 0 || m0 < 0)
+		return SG_ERR_GENERIC;
+	std::vector<uint16_t> td((size_t)a->w * a->h);
+	const sg_rect band = {a->x, a->y, a->w, a->h};	/* top-down rows y .. y + h - 1 */
+	const int rc = sg_seq_read_region_impl((void *)s, layer, index, td.data(), &band);
+	if (rc)
+		return SG_ERR_READ;
+	for (int r = 0; r < a->h; r++)	/* memory row m0 + r = top-down row y + h - 1 - r */
+		memcpy(out + (size_t)r * a->w, td.data() + (size_t)(a->h - 1 - r) * a->w, (size_t)a->w * sizeof(uint16_t));
+	return SG_OK;
+}
+
+extern "C" int sg_seq_read_selection(const sg_seq *s, int layer, int index, const sg_rect *area, uint16_t *out) {
+	try {
+		return sg_seq_read_selection_impl(s, layer, index, area, out);
 	} catch (const std::exception &) {
 		return SG_ERR_SIZE;
 	}

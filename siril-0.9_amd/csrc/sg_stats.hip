@@ -371,3 +371,27 @@ extern "C" int sg_compute_normalization(int mode, int nframes, int ref_image, co
 		}
 	return SG_OK;
 }
+
+/* host frames: one frame at a time through the context's frame buffer (the reference computes
+ * the statistics of one loaded frame at a time too, seq_get_imstats) */
+extern "C" int sg_frame_stats_ikss(sg_ctx *ctx, const uint16_t *frames, int nframes, int C, int H, int W,
+		double *location, double *scale) {
+	if (!ctx || ctx->dev.empty() || !frames || nframes < 1 || C < 1 || C > 3 || H < 1 || W < 1 || !location ||
+			!scale)
+		return SG_ERR_GENERIC;
+	SgDevice &dv = ctx->dev[0];
+	HIPCHK(hipSetDevice(dv.id));
+	const size_t fbytes = (size_t)C * H * W * sizeof(uint16_t);
+	HIPCHK(ensure(dv.reg_sel, fbytes));
+	int ret = SG_OK;
+	for (int f = 0; f < nframes; f++) {
+		HIPCHK(hipMemcpyAsync(dv.reg_sel.p, frames + (size_t)f * C * H * W, fbytes, hipMemcpyHostToDevice, dv.stream));
+		const int rc = sg_frame_stats_ikss_device(ctx, 0, (const uint16_t *)dv.reg_sel.p, 1, C, H, W, 0, location + f,
+				scale + f, nullptr);
+		if (rc == SG_ERR_GENERIC)
+			ret = SG_ERR_GENERIC;	/* a frame without non-zero pixel: keep going, report */
+		else if (rc)
+			return rc;
+	}
+	return ret;
+}

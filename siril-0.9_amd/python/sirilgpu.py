@@ -20,6 +20,7 @@ NO_NORM, ADDITIVE, MULTIPLICATIVE, ADDITIVE_SCALING, MULTIPLICATIVE_SCALING = ra
 PATH_AUTO, PATH_SORTED = 0, 1
 
 SG_OK = 0
+SG_ERR_GENERIC, SG_ERR_SIZE, SG_ERR_READ, SG_ERR_DEVICE = -1, -2, -3, -10
 
 
 class StackDesc(ctypes.Structure):
@@ -135,6 +136,11 @@ def load():
     lib.sg_seq_read_region.restype = ctypes.c_int
     lib.sg_seq_read_frame.argtypes = [P, ctypes.c_int, ctypes.POINTER(ctypes.c_uint16)]
     lib.sg_seq_read_frame.restype = ctypes.c_int
+    lib.sg_seq_read_selection.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(Rect),
+                                          ctypes.POINTER(ctypes.c_uint16)]
+    lib.sg_seq_read_selection.restype = ctypes.c_int
+    lib.sg_frame_stats_ikss.argtypes = [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P]
+    lib.sg_frame_stats_ikss.restype = ctypes.c_int
     lib.sg_seq_load_device.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int64, P]
     lib.sg_seq_load_device.restype = ctypes.c_int
     lib.sg_frame_stats_ikss_device.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -320,6 +326,13 @@ class Seq:
         buf = np.zeros((h, w), dtype=np.uint16)
         rc = self.lib.sg_seq_read_region(self.h, layer, index, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)),
                                          ctypes.byref(Rect(x, y, w, h)))
+        return rc, buf
+
+    def read_selection(self, layer, index, x, y, w, h):
+        """seq_read_frame_part: the selection (display coordinates) bottom-up; (rc, array[h][w])"""
+        buf = np.zeros((h, w), dtype=np.uint16)
+        rc = self.lib.sg_seq_read_selection(self.h, layer, index, ctypes.byref(Rect(x, y, w, h)),
+                                            buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)))
         return rc, buf
 
     def read_frame(self, index):

@@ -220,8 +220,14 @@ def test_debayer_load_device(tmp_path, gpu_ctx, color_id, forced, depth):
     with sg.Seq.open_ser(path) as seq:
         seq.set_debayer(forced)
         assert seq.shape == (N, 3, H, W)
-        rc, _ = seq.read_region(0, 0, 0, 0, W, 4)
-        assert rc != 0                                   # host reads are not provided
+        # host reads demosaic too (ser_read_opened_partial's CFA branch, ser.c:820-913)
+        for layer in range(3):
+            for y, h in [(0, 4), (5, 7), (H - 3, 3)]:
+                rc, band = seq.read_region(layer, 1, 0, y, W, h)
+                assert rc == 0
+                mem = dr.debayer_frame_memory_order(frames[1, 0, ::-1, :], tile)
+                assert np.array_equal(band, mem[layer, H - 1 - (y + np.arange(h))]), (layer, y, h)
+        assert np.array_equal(seq.read_frame(2), dr.debayer_frame_memory_order(frames[2, 0, ::-1, :], tile))
         d = torch.zeros(N * 3 * H * W, dtype=torch.int16, device="cuda")
         torch.cuda.synchronize()    # else the zero fill can land after the decode (flaky zeros)
         gpu_ctx.load_seq_device(seq, d.data_ptr())
@@ -229,3 +235,83 @@ def test_debayer_load_device(tmp_path, gpu_ctx, color_id, forced, depth):
     for i in range(N):
         topdown = frames[i, 0, ::-1, :]                  # the SER file's row order
         assert np.array_equal(got[i], dr.debayer_frame_memory_order(topdown, tile)), i
+
+
+# ---- seq_read_frame_part: the registration selection (FITS vs SER off-by-one) ----
+
+def test_selection_fits_vs_ser_off_by_one(tmp_path):
+    """sg_seq_read_selection == the committed fixture (tests/golden/make_selection_fixture.py
+    restates readfits_partial :512-516 and extract_region_from_fits :1167-1192): the FITS
+    selection sits one memory row below the SER one, and a selection touching the bottom
+    display row fails on FITS only"""
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "selection_offbyone.npz"))
+    frame = g["frame"]
+    frames = np.stack([frame, frame[:, ::-1, :]])           # two frames, index 0 is the fixture's
+    with _open(tmp_path, "fits_rgb", dict(bitpix=16), frames) as fits, \
+            _open(tmp_path, "ser_rgb", dict(depth=16), frames) as ser:
+        for k, (layer, x, y, w, h) in enumerate(g["selections"]):
+            rc, got = ser.read_selection(int(layer), 0, int(x), int(y), int(w), int(h))
+            assert rc == 0 and np.array_equal(got, g[f"ser_{k}"]), k
+            rc, got = fits.read_selection(int(layer), 0, int(x), int(y), int(w), int(h))
+            if bool(g[f"fits_ok_{k}"]):
+                assert rc == 0 and np.array_equal(got, g[f"fits_{k}"]), k
+                # FITS reads the SER selection moved one row down (memory row - 1)
+                H = frame.shape[1]
+                assert np.array_equal(got[1:], g[f"ser_{k}"][:-1])
+            else:
+                assert rc == sg.SG_ERR_READ, (k, rc)
+        # out-of-frame and bad-layer selections are refused
+        assert ser.read_selection(3, 0, 0, 0, 2, 2)[0] != 0
+        assert ser.read_selection(0, 0, 10, 0, 2, 2)[0] != 0
+
+
+def test_selection_cfa_ser_demosaiced(tmp_path):
+    """a CFA SER opened with demosaicing: the selection is extracted from the demosaiced,
+    flipped frame (ser_read_frame :708-758 + extract_region_from_fits)"""
+    import debayer_ref as dr
+    N, H, W = 2, 14, 18
+    rng = np.random.default_rng(3)
+    frames = rng.integers(0, 65536, size=(N, 1, H, W)).astype(np.uint16)
+    path = str(tmp_path / "cfa.ser")
+    write_ser(path, frames, depth=16, color_id=8)
+    with sg.Seq.open_ser(path) as seq:
+        seq.set_debayer(-1)
+        mem = dr.debayer_frame_memory_order(frames[1, 0, ::-1, :], dr.BAYER_RGGB)
+        for layer, x, y, w, h in [(1, 2, 3, 8, 8), (0, 0, 0, 18, 14), (2, 5, 6, 8, 8)]:
+            rc, got = seq.read_selection(layer, 1, x, y, w, h)
+            assert rc == 0
+            assert np.array_equal(got, mem[layer, H - y - h:H - y, x:x + w]), (layer, x, y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("band_rows", [0, 5])
+def test_stack_cfa_ser_host_pull(tmp_path, gpu_ctx, band_rows):
+    """a CFA SER stacked through sg_stack_u16 with the library's region reader demosaicing each
+    band (the reference's ser_read_opened_partial CFA branch, src/io/ser.c:820-913), whole or
+    in 5-row bands under an HBM budget: == the oracle on the demosaiced frames"""
+    import debayer_ref as dr
+    N, H, W = 12, 26, 40
+    mono = orc.synth(N, 1, H, W, seed=19, maxshift=3)
+    sx, sy = orc.synth_shifts(N, seed=19, maxshift=3)
+    path = str(tmp_path / "cfa_stack.ser")
+    write_ser(path, mono, depth=16, color_id=11)                 # BGGR
+    rgb = np.stack([dr.debayer_frame_memory_order(mono[i, 0, ::-1, :], dr.BAYER_BGGR) for i in range(N)])
+    rc, ref, rej_ref = orc.stack_rejection(rgb, sg.SIGMA, sig=(3.0, 3.0), shiftx=sx, shifty=sy, max_thread=4)
+    assert rc == 0
+    old = os.environ.get("SG_HOST_BUDGET_BYTES")
+    if band_rows:
+        os.environ["SG_HOST_BUDGET_BYTES"] = str(N * 3 * W * 2 * (band_rows + int(sy.max() - sy.min())))
+    try:
+        with sg.Context() as ctx, sg.Seq.open_ser(path) as seq:
+            seq.set_debayer(-1)
+            desc, keep = sg.make_desc(sg.MEAN, N, W, H, 3, rejection=sg.SIGMA, sig=(3.0, 3.0), shiftx=sx,
+                                      shifty=sy, max_thread=4, max_number_of_rows=H)
+            rc, out, rej, _ = ctx.stack_seq(desc, seq)
+            assert rc == 0, ctx.error()
+    finally:
+        if old is None:
+            os.environ.pop("SG_HOST_BUDGET_BYTES", None)
+        else:
+            os.environ["SG_HOST_BUDGET_BYTES"] = old
+    assert np.array_equal(out, ref)
+    assert np.array_equal(rej, rej_ref)
