@@ -1,0 +1,282 @@
+/*
+ * siril_glue.c - the reference-side binding: the BODIES of Siril 0.9's stackers and of
+ * register_shift_dft, replaced by calls into libsirilgpu.so (include/sirilgpu.h).  Signatures
+ * are the reference's (stack_method, src/stacking/stacking.h:8,64-68; registration_function,
+ * src/registration/registration.h:9,60), so every caller (start_stacking :1871-1927,
+ * stackall_worker src/core/command.c:1404-1451, register_thread_func registration.c:1180-1185)
+ * is unchanged.  This file uses only reference names (seq_opened_read_region,
+ * seq_read_frame_part, compute_normalization, get_registration_layer, get_thread_run, gfit,
+ * com): inside Siril it compiles against the real headers; here siril_compat.h restates the
+ * data model and siril_env.c stands in for the rest of Siril (GTK-free).
+ */
+#include <stdlib.h>
+#include <string.h>
+#include "siril_compat.h"
+#include "sirilgpu.h"
+
+#ifndef _
+#define _(s) (s)
+#endif
+
+/* one context for the process (in Siril: created in initialize_stacking_methods()) */
+static sg_ctx *gpu_ctx;
+
+sg_ctx *siril_gpu_context(void) {
+	if (!gpu_ctx && sg_init(&gpu_ctx, 0, NULL) != SG_OK)
+		gpu_ctx = NULL;
+	return gpu_ctx;
+}
+
+void siril_gpu_release(void) {
+	if (gpu_ctx)
+		sg_shutdown(gpu_ctx);
+	gpu_ctx = NULL;
+}
+
+/* seq_opened_read_region has the callback's shape; the user data carries the sequence and
+ * the stacked position -> sequence index map (image_indices[]) */
+struct pull_user {
+	sequence *seq;
+	const int *indices;
+};
+
+static int pull_region(void *u, int layer, int index, uint16_t *buffer, const sg_rect *area) {
+	const struct pull_user *p = (const struct pull_user *)u;
+	rectangle r = { area->x, area->y, area->w, area->h };
+	return seq_opened_read_region(p->seq, layer, p->indices[index], buffer, &r);
+}
+
+static int keep_going(void *u) {
+	(void)u;
+	return get_thread_run();
+}
+
+/* gfit takes ownership of the planar bottom-up result, as the reference's
+ * copyfits(fit, &gfit, CP_FORMAT) + data hand-over does (stacking.c:1820-1827, :778-785) */
+static void hand_over_to_gfit(WORD *out, const sequence *seq) {
+	const unsigned int W = seq->rx, H = seq->ry;
+	const int C = seq->nb_layers;
+	if (gfit.data)
+		free(gfit.data);
+	gfit.rx = W;
+	gfit.ry = H;
+	gfit.naxes[0] = W;
+	gfit.naxes[1] = H;
+	gfit.naxes[2] = C;
+	gfit.naxis = C == 3 ? 3 : 2;
+	gfit.bitpix = USHORT_IMG;
+	gfit.data = out;
+	gfit.pdata[RLAYER] = out;
+	gfit.pdata[GLAYER] = C == 3 ? out + (size_t)W * H : out;
+	gfit.pdata[BLAYER] = C == 3 ? out + (size_t)W * H * 2 : out;
+	gfit.exposure = 0.0;	/* the EXPTIME sum of FITS headers is not carried by this path */
+}
+
+/*
+ * The common body: frames indices[0..nb) of args->seq, shifts from the registration layer
+ * (:1546-1548, :1624-1626; median ignores them :703-722), normalisation coefficients from
+ * compute_normalization (:1337, mean and median only), rejection counters logged as
+ * :1811-1817, result handed to gfit.
+ */
+static int gpu_stack(struct stacking_args *args, int method, const int *indices, int nb, uint64_t *maxim_out) {
+	sequence *seq = args->seq;
+	int i, rc, reglayer = get_registration_layer();
+	int *sx = NULL, *sy = NULL;
+	norm_coeff coeff = { NULL, NULL, NULL };
+	uint64_t rej[3][2] = { { 0, 0 }, { 0, 0 }, { 0, 0 } };
+	sg_ctx *ctx = siril_gpu_context();
+	if (!ctx) {
+		siril_log_message(_("No GPU available for stacking.\n"));
+		return -1;
+	}
+	if (nb < 2) {
+		siril_log_message(_("Select at least two frames for stacking. Aborting.\n"));
+		return -1;
+	}
+	const int norm_used = method == SG_STACK_MEAN || method == SG_STACK_MEDIAN;
+	if (norm_used) {
+		coeff.offset = malloc(nb * sizeof(double));
+		coeff.mul = malloc(nb * sizeof(double));
+		coeff.scale = malloc(nb * sizeof(double));
+		if (!coeff.offset || !coeff.mul || !coeff.scale || compute_normalization(args, &coeff, args->normalize)) {
+			rc = -1;
+			goto end;
+		}
+	}
+	if (method != SG_STACK_MEDIAN && reglayer != -1 && seq->regparam && seq->regparam[reglayer]) {
+		sx = malloc(nb * sizeof(int));
+		sy = malloc(nb * sizeof(int));
+		for (i = 0; i < nb; i++) {
+			sx[i] = seq->regparam[reglayer][indices[i]].shiftx;
+			sy[i] = seq->regparam[reglayer][indices[i]].shifty;
+		}
+	}
+	sg_stack_desc d;
+	memset(&d, 0, sizeof d);
+	d.method = method;
+	d.rejection = method == SG_STACK_MEAN ? (int)args->type_of_rejection : SG_NO_REJEC;
+	d.normalize = norm_used ? (int)args->normalize : SG_NO_NORM;
+	d.sig[0] = args->sig[0];
+	d.sig[1] = args->sig[1];
+	d.nb_frames = nb;
+	d.width = (int)seq->rx;
+	d.height = (int)seq->ry;
+	d.nb_layers = seq->nb_layers;
+	d.shiftx = sx;
+	d.shifty = sy;
+	if (norm_used && args->normalize != NO_NORM) {
+		d.offset = coeff.offset;
+		d.mul = coeff.mul;
+		d.scale = coeff.scale;
+	}
+	d.max_thread = com.max_thread;
+	d.max_number_of_rows = args->max_number_of_rows;
+	{
+		struct pull_user u = { seq, indices };
+		WORD *out = malloc((size_t)d.width * d.height * d.nb_layers * sizeof(WORD));
+		if (!out) {
+			rc = -2;
+			goto end;
+		}
+		rc = sg_stack_u16(ctx, &d, pull_region, &u, keep_going, NULL, out, rej, maxim_out);
+		if (rc) {
+			siril_log_message("%s\n", sg_last_error(ctx));
+			free(out);
+			goto end;
+		}
+		if (method == SG_STACK_MEAN) {
+			const double nb_tot = (double)d.width * d.height * nb;
+			for (i = 0; i < d.nb_layers; i++)
+				siril_log_message(_("Pixel rejection in channel #%d: %.3lf%% - %.3lf%%\n"), i,
+						rej[i][0] / nb_tot * 100.0, rej[i][1] / nb_tot * 100.0);
+		}
+		hand_over_to_gfit(out, seq);
+	}
+end:
+	free(sx);
+	free(sy);
+	free(coeff.offset);
+	free(coeff.mul);
+	free(coeff.scale);
+	if (rc)
+		siril_log_message(_("Stacking failed.\n"));
+	return rc;
+}
+
+int stack_mean_with_rejection(struct stacking_args *args) {
+	if (args->seq->type != SEQ_REGULAR && args->seq->type != SEQ_SER) {	/* :1212-1216 */
+		siril_log_message(_("Rejection stacking is only supported for FITS images and SER sequences.\n"));
+		return -1;
+	}
+	return gpu_stack(args, SG_STACK_MEAN, args->image_indices, args->nb_images_to_stack, NULL);
+}
+
+int stack_median(struct stacking_args *args) {
+	return gpu_stack(args, SG_STACK_MEDIAN, args->image_indices, args->nb_images_to_stack, NULL);
+}
+
+/* stack_summing / addmax / addmin walk the whole sequence through filtering_criterion
+ * (:223-232, :864-873, :1019-1028) rather than image_indices[] */
+static int gpu_stack_filtered(struct stacking_args *args, int method, uint64_t *maxim) {
+	sequence *seq = args->seq;
+	int j, nb = 0, rc;
+	int *idx = malloc((seq->number > 0 ? seq->number : 1) * sizeof(int));
+	if (!idx)
+		return -1;
+	for (j = 0; j < seq->number; j++)
+		if (args->filtering_criterion(seq, j, args->filtering_parameter))
+			idx[nb++] = j;
+	if (nb <= 1) {
+		siril_log_message(_("No frame selected for stacking (select at least 2). Aborting.\n"));
+		free(idx);
+		return -1;
+	}
+	rc = gpu_stack(args, method, idx, nb, maxim);
+	free(idx);
+	return rc;
+}
+
+int stack_summing(struct stacking_args *args) {
+	uint64_t maxim = 0;
+	const int rc = gpu_stack_filtered(args, SG_STACK_SUM, &maxim);
+	if (!rc)	/* gfit.hi = round_to_WORD(maxim) (:326) */
+		gfit.hi = maxim > 65535 ? 65535 : (WORD)maxim;
+	return rc;
+}
+
+int stack_addmax(struct stacking_args *args) {
+	return gpu_stack_filtered(args, SG_STACK_MAX, NULL);
+}
+
+int stack_addmin(struct stacking_args *args) {
+	return gpu_stack_filtered(args, SG_STACK_MIN, NULL);
+}
+
+/*
+ * register_shift_dft (src/registration/registration.c:182-400): the same selection reads
+ * (seq_read_frame_part of args->layer, :236-244, :301-306), the DFT + arg-max + quality on the
+ * GPU, regdata written for the reference frame and every processed frame (others keep what
+ * they had: zero for a new array, :210-220), quality normalised over the processed frames.
+ */
+int register_shift_dft(struct registration_args *args) {
+	sequence *seq = args->seq;
+	const int n = seq->number, S = args->selection.w;
+	int f, rc;
+	sg_ctx *ctx = siril_gpu_context();
+	if (!ctx || args->selection.w != args->selection.h)
+		return -1;
+	if (!seq->regparam) {
+		siril_log_message("regparam should have been created before\n");
+		return -1;
+	}
+	const int ref = seq->reference_image == -1 ? 0 : seq->reference_image;
+	uint16_t *sel = malloc((size_t)n * S * S * sizeof(uint16_t));
+	int *inc = malloc(n * sizeof(int)), *sx = calloc(n, sizeof(int)), *sy = calloc(n, sizeof(int));
+	double *q = calloc(n, sizeof(double));
+	if (!sel || !inc || !sx || !sy || !q) {
+		rc = -2;
+		goto end;
+	}
+	for (f = 0; f < n; f++) {
+		inc[f] = args->process_all_frames || seq->imgparam[f].incl;
+		if (!inc[f] && f != ref)
+			continue;
+		fits fit;
+		memset(&fit, 0, sizeof fit);
+		if (seq_read_frame_part(seq, args->layer, f, &fit, &args->selection, FALSE)) {
+			siril_log_message(_("Could not load partial image %d\n"), f);
+			clearfits(&fit);
+			rc = 1;	/* :373-381 (the reference frame: :238-244 returns its status) */
+			goto end;
+		}
+		memcpy(sel + (size_t)f * S * S, fit.data, (size_t)S * S * sizeof(WORD));
+		clearfits(&fit);
+	}
+	rc = sg_register_dft_u16(ctx, sel, n, S, ref, inc, sx, sy, q);
+	if (rc) {
+		siril_log_message("%s\n", sg_last_error(ctx));
+		goto end;
+	}
+	{
+		regdata *rd = seq->regparam[args->layer] ? seq->regparam[args->layer] : calloc(n, sizeof(regdata));
+		if (!rd) {
+			rc = -2;
+			goto end;
+		}
+		for (f = 0; f < n; f++)
+			if (inc[f] || f == ref) {
+				rd[f].shiftx = sx[f];
+				rd[f].shifty = sy[f];
+				rd[f].quality = q[f];
+			}
+		seq->regparam[args->layer] = rd;
+	}
+	siril_log_message(_("Registration finished.\n"));
+end:
+	free(sel);
+	free(inc);
+	free(sx);
+	free(sy);
+	free(q);
+	return rc;
+}

@@ -18,7 +18,10 @@ import oracle_lib as orc
 import oracle_numpy as onp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-GOLDEN = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "*.npz")))
+ALL_GOLDEN = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "*.npz")))
+# the oracle-generated fixtures (make_golden.py); register_cfg* (make_golden_fullsize.py, numpy FFT)
+# and selection_offbyone (make_selection_fixture.py) have their own tests below and in test_io.py
+GOLDEN = [p for p in ALL_GOLDEN if not os.path.basename(p).startswith(("register_cfg", "selection_"))]
 
 
 def _opt(d, k):
@@ -271,3 +274,18 @@ int main(void) {
     subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-I", inc, str(src), "-o", str(exe), "-lm"], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
+
+
+@pytest.mark.parametrize("name", ["register_cfg1", "register_cfg4"])
+def test_fullsize_registration_golden_consistent(name):
+    """the full-size registration fixtures (numpy FFT, tests/golden/make_golden_fullsize.py):
+    shifts recover the generator's translations, the winner is far from a tie, and the oracle's
+    QualityEstimate reproduces the raw qualities of the first frames"""
+    g = np.load(os.path.join(ROOT, "tests", "golden", name + ".npz"), allow_pickle=False)
+    N, C, H, W, layer, S, y0, x0, seed, M = (int(v) for v in g["geometry"])
+    ex, ey = orc.synth_shifts(N, seed=seed, maxshift=M)
+    assert np.array_equal(g["shiftx"], ex) and np.array_equal(g["shifty"], ey)
+    assert g["margin"][1:].min() > 1e-6
+    sel = orc.synth_window(3, layer, y0, x0, S, S, seed=seed, maxshift=M)
+    for f in range(3):
+        assert orc.quality(sel[f]) == g["quality_raw"][f]

@@ -1,0 +1,165 @@
+"""The reference-side binding compiled and exercised: harness/siril_glue.c holds the bodies of
+stack_summing / stack_mean_with_rejection / stack_median / stack_addmax / stack_addmin and
+register_shift_dft with the reference's signatures (struct stacking_args *,
+struct registration_args *, restated GTK-free in harness/siril_compat.h), calling
+libsirilgpu.so.  harness_stack() builds struct stacking_args the way start_stacking
+(src/stacking/stacking.c:1871-1927) does and calls args->method(&args) from C; the result is
+read back from gfit (the ownership hand-off of :1820-1827) and compared with the oracle."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import harness_lib as hl
+import oracle_lib as orc
+from seq_files import write_fits, write_ser
+
+SUM, MEAN, MEDIAN, MAX, MIN = 0, 1, 2, 3, 4
+NO_REJEC, PERCENTILE, SIGMA, SIGMEDIAN, WINSORIZED, LINEARFIT = range(6)
+
+
+def test_harness_builds_and_exports():
+    """CPU: the glue and its environment link against libsirilgpu.so and export the
+    reference's entry points"""
+    lib = hl.load()
+    for name in ["stack_summing", "stack_mean_with_rejection", "stack_median", "stack_addmax", "stack_addmin",
+                 "register_shift_dft", "seq_opened_read_region", "seq_read_frame_part", "compute_normalization"]:
+        assert hasattr(lib, name), name
+    assert os.path.exists(hl.CLI)
+
+
+def _seq_files(tmp_path, frames, fmt):
+    if fmt == "ser":
+        p = str(tmp_path / "h.ser")
+        write_ser(p, frames, depth=16)
+        return hl.Sequence.ser(p)
+    paths = []
+    for i in range(frames.shape[0]):
+        p = str(tmp_path / f"h_{i + 1:05d}.fit")
+        write_fits(p, frames[i])
+        paths.append(p)
+    return hl.Sequence.fits(paths)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", ["ser", "fits"])
+@pytest.mark.parametrize("rejection", [SIGMA, WINSORIZED, LINEARFIT, NO_REJEC])
+def test_stack_mean_with_rejection_from_c(tmp_path, fmt, rejection):
+    """stack_mean_with_rejection(&args) called from C with registration shifts on the
+    registration layer and 3 of 20 frames excluded (stack_filter_included) == the oracle on
+    the included frames"""
+    lib = hl.load()
+    N, C, H, W = 20, 1, 40, 72
+    frames = orc.synth(N, C, H, W, seed=90 + rejection, maxshift=5)
+    sx, sy = orc.synth_shifts(N, seed=90 + rejection, maxshift=5)
+    excl = [3, 11, 17]
+    keep = [i for i in range(N) if i not in excl]
+    sig = (3.0, 3.0)
+    rc, ref, _ = orc.stack_rejection(frames[keep], rejection, sig=sig, shiftx=sx[keep], shifty=sy[keep],
+                                     max_thread=4)
+    assert rc == 0
+    lib.harness_set_max_thread(4)
+    with _seq_files(tmp_path, frames, fmt) as seq:
+        for i in excl:
+            lib.harness_set_included(seq.h, i, 0)
+        seq.set_regdata(0, sx, sy)
+        lib.harness_set_registration_layer(0)
+        rc = lib.harness_stack(seq.h, MEAN, rejection, 0, sig[0], sig[1], 1, 0)
+        lib.harness_set_registration_layer(-1)
+        assert rc == 0
+        assert np.array_equal(hl.gfit(), ref)
+
+
+@pytest.mark.gpu
+def test_stack_summing_median_max_min_from_c(tmp_path):
+    """stack_summing (gfit.hi = the sum maximum), stack_median with additive + scaling
+    normalisation from statistics computed on the GPU, stack_addmax / stack_addmin"""
+    lib = hl.load()
+    N, C, H, W = 12, 1, 32, 48
+    frames = orc.synth(N, C, H, W, seed=7, maxshift=4)
+    sx, sy = orc.synth_shifts(N, seed=7, maxshift=4)
+    with _seq_files(tmp_path, frames, "fits") as seq:
+        seq.set_regdata(0, sx, sy)
+        lib.harness_set_registration_layer(0)
+        assert lib.harness_stack(seq.h, SUM, 0, 0, 0.0, 0.0, 0, 0) == 0
+        rc, ref, mref = orc.stack_sum(frames, sx, sy)
+        assert np.array_equal(hl.gfit(), ref) and lib.harness_gfit_hi() == min(mref, 65535)
+        for m, is_max in [(MAX, True), (MIN, False)]:
+            assert lib.harness_stack(seq.h, m, 0, 0, 0.0, 0.0, 0, 0) == 0
+            rc, ref = orc.stack_maxmin(frames, is_max, sx, sy)
+            assert np.array_equal(hl.gfit(), ref)
+        lib.harness_set_registration_layer(-1)
+        # median with ADDITIVE_SCALING: statistics of each frame (IKSS, layer 0) as the oracle
+        loc = np.zeros(N)
+        scl = np.zeros(N)
+        for i in range(N):
+            rcs, loc[i], scl[i] = orc.statistics_ikss(frames[i])
+            assert rcs == 0
+        off, mul, sc = orc.compute_normalization(3, loc, scl)
+        rc, ref = orc.stack_median(frames, normalize=3, offset=off, mul=mul, scale=sc, max_thread=4)
+        assert lib.harness_stack(seq.h, MEDIAN, 0, 3, 0.0, 0.0, 0, 0) == 0
+        assert np.array_equal(hl.gfit(), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", ["ser", "fits"])
+def test_register_shift_dft_from_c(tmp_path, fmt):
+    """register_shift_dft(&args) from C: selections read with seq_read_frame_part (FITS one row
+    lower than SER, readfits_partial :512), shifts and normalised qualities == the oracle on the
+    selections the reference would read; frames excluded keep zero regdata"""
+    lib = hl.load()
+    N, C, H, W, S = 9, 1, 80, 96, 64
+    frames = orc.synth(N, C, H, W, seed=23, maxshift=5)
+    x, y = 10, 6                        # display coordinates of the selection
+    m0 = H - y - S - (1 if fmt == "fits" else 0)     # its first memory row
+    sel = frames[:, 0, m0:m0 + S, x:x + S]
+    inc = np.ones(N, np.int32)
+    inc[4] = 0
+    rx, ry, rq = orc.register_dft(sel, ref_image=2, included=inc)
+    with _seq_files(tmp_path, frames, fmt) as seq:
+        lib.harness_set_reference_image(seq.h, 2)
+        lib.harness_set_included(seq.h, 4, 0)
+        assert lib.harness_register(seq.h, 0, x, y, S, 0) == 0
+        gx, gy, gq = seq.regdata(0, N)
+    m = inc.astype(bool)
+    assert np.array_equal(gx[m], rx[m]) and np.array_equal(gy[m], ry[m])
+    assert np.array_equal(gq[m], rq[m])
+    assert gx[4] == 0 and gy[4] == 0 and gq[4] == 0
+
+
+@pytest.mark.gpu
+def test_register_fits_selection_touching_bottom_fails(tmp_path):
+    """a selection touching the bottom display row: fpixel[1] = 0 on FITS -> the read and the
+    registration fail (the reference's behaviour), while SER registers"""
+    lib = hl.load()
+    N, H, W, S = 4, 64, 64, 32
+    frames = orc.synth(N, 1, H, W, seed=5, maxshift=3)
+    with _seq_files(tmp_path, frames, "fits") as seq:
+        assert lib.harness_register(seq.h, 0, 0, H - S, S, 1) != 0
+    with _seq_files(tmp_path, frames, "ser") as seq:
+        assert lib.harness_register(seq.h, 0, 0, H - S, S, 1) == 0
+
+
+@pytest.mark.gpu
+def test_cli_register_and_stack(tmp_path):
+    """siril_cli: open a SER, register layer 0 on a centred selection, sigma-clip stack with
+    the shifts, save the FITS: the saved image == the oracle with the oracle's shifts"""
+    N, H, W, S = 16, 96, 128, 64
+    frames = orc.synth(N, 1, H, W, seed=61, maxshift=6)
+    p = str(tmp_path / "c.ser")
+    write_ser(p, frames, depth=16)
+    x, y = (W - S) // 2, (H - S) // 2
+    m0 = H - y - S
+    rx, ry, _ = orc.register_dft(frames[:, 0, m0:m0 + S, x:x + S])
+    rc, ref, _ = orc.stack_rejection(frames, SIGMA, sig=(4.0, 3.0), shiftx=rx, shifty=ry, max_thread=16)
+    out = str(tmp_path / "out.fit")
+    r = subprocess.run([hl.CLI, "--ser", p, "--register", "0", str(x), str(y), str(S), "--stack", "mean",
+                        "--rejection", "sigma", "--sig", "4", "3", "-o", out], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    import sirilgpu as sg
+    with sg.Seq.open_fits([out]) as s:
+        got = s.read_frame(0)
+    assert np.array_equal(got, ref)
