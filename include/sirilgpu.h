@@ -136,6 +136,9 @@ typedef struct {
 	uint64_t launches;	/* kernels launched by the main path */
 	int main_kernel_blocks;
 	int path;		/* main path of a MEAN stack: 1 = histogram (k_stack_hist), 0 = other */
+	/* last registration: frames whose correlation maximum was a near tie, decided by exact
+	 * integer correlations / left to the FFT arg-max (more candidates than the cap) */
+	uint64_t reg_ties_resolved, reg_ties_unresolved;
 } sg_stack_stats;
 int sg_get_last_stats(const sg_ctx *ctx, sg_stack_stats *st);
 
@@ -160,8 +163,11 @@ int sg_compute_normalization(int mode, int nframes, int ref_image, const double 
 /*
  * DFT registration: replaces register_shift_dft (src/registration/registration.c:182-400).
  * d_sel / sel hold nframes bottom-up S x S selections (what seq_read_frame_part returns,
- * src/io/sequence.c:567-609).  included may be NULL (process_all_frames).  Outputs the
- * integer shifts and the normalised quality (normalizeQualityData :163-176) per frame.
+ * src/io/sequence.c:567-609), any side 4 <= S <= 4096 (FFTW plans every size, :251-257).
+ * included may be NULL (process_all_frames).  Outputs the integer shifts and the normalised
+ * quality (normalizeQualityData :163-176) per frame.  A correlation maximum whose runner-up
+ * lies within the FFT tolerance is decided by exact integer correlations (sg_stack_stats
+ * reg_ties_*).
  */
 int sg_register_dft_u16(sg_ctx *ctx, const uint16_t *sel, int nframes, int S, int ref_image,
 		const int *included, int *shiftx, int *shifty, double *quality);

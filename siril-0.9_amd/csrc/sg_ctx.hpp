@@ -73,7 +73,7 @@ struct SgKnobs {
 	int qgrad_threads = 128;	/* SG_QGRAD_THREADS: 128 measured best (scripts/gpu_qgrad.sh) */
 	int reg_batch = 0;		/* SG_REG_BATCH: pairs per launch (0 = up to 2 GB of pair planes) */
 	int reg_cw = 0;			/* SG_REG_CW: columns per column-pass workgroup (0 = 8192 / S) */
-	int reg_path = 2;		/* SG_REG_PATH: registration pass order 0 / 1 / 2 */
+	int reg_path = 2;		/* SG_REG_PATH: registration pass order 0 / 1 / 2, 3 = the generic passes */
 	int reg_xcd = 1;		/* SG_REG_XCD: 0 = column strips in dispatch order */
 	int reg_pb = 1;			/* SG_REG_PB: pairs per strip block of the fused column pass (1 = pair-major) */
 	void read() {
@@ -91,7 +91,7 @@ struct SgKnobs {
 		qgrad_threads = (qg == 64 || qg == 128 || qg == 256) ? qg : 128;
 		reg_batch = sg_env_int("SG_REG_BATCH", 1, 1024, 0);
 		reg_cw = sg_env_int("SG_REG_CW", 1, 64, 0);
-		reg_path = sg_env_int("SG_REG_PATH", 0, 2, 2);
+		reg_path = sg_env_int("SG_REG_PATH", 0, 3, 2);
 		reg_xcd = sg_env_int("SG_REG_XCD", 0, 1, 1);
 		reg_pb = sg_env_int("SG_REG_PB", 1, 64, 1);
 	}

@@ -1,0 +1,356 @@
+/*
+ * sg_fft.hpp - device FFT building blocks of the DFT registration (sg_register.hip: power-of-
+ * two sides, sg_register_gen.hip: any side): complex double arithmetic, in-register small DFTs,
+ * Stockham auto-sort passes in LDS, the fused memory-in / memory-out transform, and the top-2
+ * arg-max used to detect near ties of the correlation maximum.
+ */
+#pragma once
+#include "sg_common.hpp"
+#include <math.h>
+#include <type_traits>
+
+typedef double2 sg_c64;
+
+__device__ __forceinline__ int sg_bitrev(int x, int logn) {
+	return (int)(__brev((unsigned)x) >> (32 - logn));
+}
+
+/* ------------------------------------------------------------------------------------
+ * nb independent length-n FFTs held in LDS (transform b at buf + b*bstride), natural order
+ * in and out: Stockham auto-sort passes of radix 8 (then 4 / 2 for the remaining factor),
+ * each thread taking whole radix-R butterflies in registers (a 2048-point transform is 4
+ * LDS round trips instead of 11).  tw: see sg_twiddle; the inverse uses
+ * conjugate twiddles (unnormalised, FFTW_BACKWARD).
+ * ------------------------------------------------------------------------------------ */
+/* LDS element index with one pad slot per 8 elements: the Stockham stores of the first
+ * passes (stride 8 and 64 elements between neighbouring threads) would otherwise hit the
+ * same banks 8- to 32-fold */
+__device__ __forceinline__ int sg_pad(int i) {
+	return i + (i >> 3);
+}
+#define SG_PADN(n) ((n) + ((n) >> 3))
+
+__device__ __forceinline__ sg_c64 sg_cmul(sg_c64 a, sg_c64 b) {
+	return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ sg_c64 sg_cadd(sg_c64 a, sg_c64 b) {
+	return make_double2(a.x + b.x, a.y + b.y);
+}
+__device__ __forceinline__ sg_c64 sg_csub(sg_c64 a, sg_c64 b) {
+	return make_double2(a.x - b.x, a.y - b.y);
+}
+/* multiply by -i (forward) or +i (inverse) */
+__device__ __forceinline__ sg_c64 sg_mul_mi(sg_c64 a, bool inv) {
+	return inv ? make_double2(-a.y, a.x) : make_double2(a.y, -a.x);
+}
+
+/* in-register DFT of R = 2, 4, 8 points (natural order in and out) */
+template <int R, int RV>
+__device__ __forceinline__ void sg_dft_small(sg_c64 (&v)[RV], bool inv) {
+	if constexpr (R == 2) {
+		const sg_c64 a = v[0], b = v[1];
+		v[0] = sg_cadd(a, b);
+		v[1] = sg_csub(a, b);
+		return;
+	}
+	else if constexpr (R == 4) {
+		const sg_c64 a0 = sg_cadd(v[0], v[2]), a1 = sg_csub(v[0], v[2]);
+		const sg_c64 b0 = sg_cadd(v[1], v[3]), b1 = sg_mul_mi(sg_csub(v[1], v[3]), inv);
+		v[0] = sg_cadd(a0, b0);
+		v[2] = sg_csub(a0, b0);
+		v[1] = sg_cadd(a1, b1);
+		v[3] = sg_csub(a1, b1);
+		return;
+	} else {
+	/* R = 8: radix-2 DIF into two 4-point DFTs */
+	const double h = 0.70710678118654752440;
+	sg_c64 e[4], o[4];
+#pragma unroll
+	for (int k = 0; k < 4; k++) {
+		e[k] = sg_cadd(v[k], v[k + 4]);
+		o[k] = sg_csub(v[k], v[k + 4]);
+	}
+	/* o[k] *= W8^k */
+	o[1] = inv ? make_double2(h * (o[1].x - o[1].y), h * (o[1].x + o[1].y))
+		   : make_double2(h * (o[1].x + o[1].y), h * (o[1].y - o[1].x));
+	o[2] = sg_mul_mi(o[2], inv);
+	o[3] = inv ? make_double2(-h * (o[3].x + o[3].y), h * (o[3].x - o[3].y))
+		   : make_double2(h * (o[3].y - o[3].x), -h * (o[3].x + o[3].y));
+	sg_dft_small<4>(e, inv);
+	sg_dft_small<4>(o, inv);
+	const sg_c64 *E = e, *O = o;
+#pragma unroll
+	for (int k = 0; k < 4; k++) {
+		v[2 * k] = E[k];
+		v[2 * k + 1] = O[k];
+	}
+	}
+}
+
+/* tw holds the full circle twice: tw[k] = exp(-2 pi i k / n) and tw[n + k] = its conjugate
+ * (the inverse), k < n, built on the host from the half-circle values by exact negation /
+ * conjugation, so a twiddle is one load with no select (the direction is uniform) */
+__device__ __forceinline__ sg_c64 sg_twiddle(const sg_c64 *__restrict__ tw, int n, int k, bool inv) {
+	return (inv ? tw + n : tw)[k];
+}
+
+template <int R>
+__device__ __forceinline__ void sg_stockham_pass(sg_c64 *buf, int n, int nb, int bstride, int Ns,
+		const sg_c64 *__restrict__ tw, bool inv) {
+	constexpr int MAXI = 8 / R;	/* work items per thread: nb * n <= 8 * blockDim (host-sized launches) */
+	const int per = n / R, items = nb * per;
+	sg_c64 v[MAXI][R], w[MAXI][R];
+	const bool twiddled = Ns > 1;	/* the first pass (Ns = 1) multiplies by w^0 = 1 only */
+	/* load every item's R inputs before anyone stores (in-place pass); the twiddles are
+	 * fetched here too, so their latency overlaps the barrier wait */
+#pragma unroll
+	for (int it = 0; it < MAXI; it++) {
+		const int t = threadIdx.x + it * blockDim.x;
+		if (t < items) {
+			const int b = t / per, j = t - b * per;
+			const sg_c64 *x = buf + (size_t)b * bstride;
+#pragma unroll
+			for (int r = 0; r < R; r++)
+				v[it][r] = x[sg_pad(j + r * per)];
+			if (twiddled) {
+				const int jm = j & (Ns - 1);
+				const int kstep = jm * (n / (Ns * R));
+#pragma unroll
+				for (int r = 1; r < R; r++)
+					w[it][r] = sg_twiddle(tw, n, r * kstep, inv);
+			}
+		}
+	}
+	__syncthreads();
+#pragma unroll
+	for (int it = 0; it < MAXI; it++) {
+		const int t = threadIdx.x + it * blockDim.x;
+		if (t < items) {
+			const int b = t / per, j = t - b * per;
+			const int jm = j & (Ns - 1);
+			if (twiddled) {
+#pragma unroll
+				for (int r = 1; r < R; r++)
+					v[it][r] = sg_cmul(v[it][r], w[it][r]);
+			}
+			sg_dft_small<R, R>(v[it], inv);
+			sg_c64 *y = buf + (size_t)b * bstride;
+			const int base = (j - jm) * R + jm;
+#pragma unroll
+			for (int r = 0; r < R; r++)
+				y[sg_pad(base + r * Ns)] = v[it][r];
+		}
+	}
+	__syncthreads();
+}
+
+__device__ __forceinline__ void sg_lds_fft(sg_c64 *buf, int n, int logn, int nb, int bstride, const sg_c64 *__restrict__ tw,
+		bool inverse) {
+	(void)logn;
+	__syncthreads();
+	int Ns = 1;
+	while (Ns < n) {
+		const int rem = n / Ns;
+		if (rem >= 8) {
+			sg_stockham_pass<8>(buf, n, nb, bstride, Ns, tw, inverse);
+			Ns *= 8;
+		} else if (rem == 4) {
+			sg_stockham_pass<4>(buf, n, nb, bstride, Ns, tw, inverse);
+			Ns *= 4;
+		} else {
+			sg_stockham_pass<2>(buf, n, nb, bstride, Ns, tw, inverse);
+			Ns *= 2;
+		}
+	}
+}
+
+/* The same transform with its first pass reading the input straight from memory and its
+ * last pass writing the output straight to memory (ld(b, i) / st(b, i, v): element i of
+ * transform b): two LDS round trips and four barriers fewer than staging through LDS.
+ * Work items of these two passes are batch-minor (item t -> b = t % nb), so neighbouring
+ * lanes of a column strip touch neighbouring columns of one row (64-B row segments).
+ * The arithmetic is that of sg_lds_fft, operation for operation (n < 16, a single pass:
+ * staged through LDS). */
+/* LDS_IN: ld reads this same LDS buffer (element i of transform b at its padded slot), so
+ * the first pass loads everything before anyone stores.  A st that writes element i back
+ * to its own slot is race-free as is: the last pass's thread reads exactly the slots it
+ * writes. */
+template <bool LDS_IN = false, class LD, class ST>
+__device__ __forceinline__ void sg_fft_io(sg_c64 *buf, int n, int nb, int bstride, const sg_c64 *__restrict__ tw,
+		bool inv, LD ld, ST st) {
+	if (n < 16) {
+		for (int t = threadIdx.x; t < nb * n; t += blockDim.x)
+			buf[(size_t)(t % nb) * bstride + sg_pad(t / nb)] = ld(t % nb, t / nb);
+		sg_lds_fft(buf, n, 0, nb, bstride, tw, inv);
+		for (int t = threadIdx.x; t < nb * n; t += blockDim.x)
+			st(t % nb, t / nb, buf[(size_t)(t % nb) * bstride + sg_pad(t / nb)]);
+		return;
+	}
+	/* first pass: radix 8, Ns = 1 (no twiddles) */
+	{
+		const int per = n >> 3, items = nb * per;
+		const int t = threadIdx.x;
+		const bool act = t < items;
+		const int b = act ? t % nb : 0, j = act ? t / nb : 0;
+		sg_c64 v[8];
+		if (act) {
+#pragma unroll
+			for (int r = 0; r < 8; r++)
+				v[r] = ld(b, j + r * per);
+		}
+		if (LDS_IN)
+			__syncthreads();
+		if (act) {
+			sg_dft_small<8, 8>(v, inv);
+			sg_c64 *y = buf + (size_t)b * bstride;
+#pragma unroll
+			for (int r = 0; r < 8; r++)
+				y[sg_pad(j * 8 + r)] = v[r];
+		}
+	}
+	__syncthreads();
+	int Ns = 8;
+	/* middle passes in LDS (sg_lds_fft's radix sequence: 8 while n / Ns >= 8, then 4 or 2),
+	 * leaving the last one */
+	while (n / Ns > 8) {
+		sg_stockham_pass<8>(buf, n, nb, bstride, Ns, tw, inv);
+		Ns *= 8;
+	}
+	const int rl = n / Ns;
+	auto last = [&](auto RC) {
+		constexpr int R = decltype(RC)::value;
+		constexpr int MAXI = 8 / R;
+		const int per = n / R, items = nb * per;
+#pragma unroll
+		for (int it = 0; it < MAXI; it++) {
+			const int t = threadIdx.x + it * blockDim.x;
+			if (t < items) {
+				const int b = t % nb, j = t / nb;
+				const sg_c64 *x = buf + (size_t)b * bstride;
+				sg_c64 v[R];
+#pragma unroll
+				for (int r = 0; r < R; r++)
+					v[r] = x[sg_pad(j + r * per)];
+#pragma unroll
+				for (int r = 1; r < R; r++)
+					v[r] = sg_cmul(v[r], sg_twiddle(tw, n, r * j, inv));
+				sg_dft_small<R, R>(v, inv);
+#pragma unroll
+				for (int r = 0; r < R; r++)
+					st(b, j + r * per, v[r]);
+			}
+		}
+	};
+	if (rl == 8)
+		last(std::integral_constant<int, 8>());
+	else if (rl == 4)
+		last(std::integral_constant<int, 4>());
+	else
+		last(std::integral_constant<int, 2>());
+}
+
+
+/* ---------------------------------------------------------------------------------------
+ * top-2 arg-max: the best (value, index) -- larger value, ties -> lower index, the
+ * reference's first strict maximum (registration.c:337-343) -- and the best value at any
+ * OTHER index.  Partials cover disjoint index sets, so merging keeps both exact.
+ * ------------------------------------------------------------------------------------- */
+struct SgTop2 {
+	double v, v2;
+	int i, pad;
+};
+
+__device__ __forceinline__ void sg_top2_init(SgTop2 &t) {
+	t.v = -INFINITY;
+	t.v2 = -INFINITY;
+	t.i = 0x7fffffff;
+	t.pad = 0;
+}
+
+__device__ __forceinline__ void sg_top2_merge(SgTop2 &a, double v, double v2, int i) {
+	if (v > a.v || (v == a.v && i < a.i)) {
+		a.v2 = fmax(a.v, v2);
+		a.v = v;
+		a.i = i;
+	} else {
+		a.v2 = fmax(a.v2, v);
+	}
+}
+
+__device__ __forceinline__ void sg_top2_add(SgTop2 &a, double v, int i) {
+	sg_top2_merge(a, v, -INFINITY, i);
+}
+
+__device__ __forceinline__ void sg_top2_wave(SgTop2 &a) {
+	for (int o = 32; o > 0; o >>= 1) {
+		const double v = __shfl_down(a.v, o, 64), v2 = __shfl_down(a.v2, o, 64);
+		const int i = __shfl_down(a.i, o, 64);
+		sg_top2_merge(a, v, v2, i);
+	}
+}
+
+/* per-pair arg-max partial of the two frames a (real part) and b (imaginary part) */
+struct SgBest {
+	SgTop2 a, b;
+};
+
+/* block reduction of a and b; thread 0 returns the block's result in (a, b).  `sh` holds 16
+ * waves' partials. */
+__device__ __forceinline__ void sg_best_block(SgTop2 &a, SgTop2 &b, SgBest *sh) {
+	sg_top2_wave(a);
+	sg_top2_wave(b);
+	const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+	if ((threadIdx.x & 63) == 0) {
+		sh[wave].a = a;
+		sh[wave].b = b;
+	}
+	__syncthreads();
+	if (threadIdx.x == 0)
+		for (int w = 1; w < nw; w++) {
+			sg_top2_merge(a, sh[w].a.v, sh[w].a.v2, sh[w].a.i);
+			sg_top2_merge(b, sh[w].b.v, sh[w].b.v2, sh[w].b.i);
+		}
+}
+
+/* sum of squares of one row of a (and b) into the frames' energies */
+__device__ __forceinline__ void sg_energy_add(unsigned long long ea, unsigned long long eb, int fa, int fb,
+		unsigned long long *energy) {
+	__shared__ unsigned long long se[2][16];
+	for (int o = 32; o > 0; o >>= 1) {
+		ea += __shfl_down(ea, o, 64);
+		eb += __shfl_down(eb, o, 64);
+	}
+	const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+	if ((threadIdx.x & 63) == 0) {
+		se[0][wave] = ea;
+		se[1][wave] = eb;
+	}
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		for (int w = 1; w < nw; w++) {
+			ea += se[0][w];
+			eb += se[1][w];
+		}
+		atomicAdd(energy + fa, ea);
+		if (fb >= 0)
+			atomicAdd(energy + fb, eb);
+	}
+}
+
+
+/* candidates of a near tie: the indices whose FFT correlation reaches max - tol, for an exact
+ * integer recomputation (k_reg_exact); capped, an overflow leaves the frame unresolved */
+#define SG_CAND_CAP 64
+struct SgCand {
+	unsigned int count;
+	int idx[SG_CAND_CAP];
+	long long exact[SG_CAND_CAP];
+};
+
+__device__ __forceinline__ void sg_cand_push(SgCand *c, double v, double thr, int idx) {
+	if (v >= thr) {
+		const unsigned int k = atomicAdd(&c->count, 1u);
+		if (k < SG_CAND_CAP)
+			c->idx[k] = idx;
+	}
+}

@@ -12,267 +12,32 @@
  *   - the two cross-power spectra are packed back as P = R conj F_a + i R conj F_b, whose
  *     inverse is c_a + i c_b (both correlations are real): one forward and one inverse
  *     complex 2-D FFT per PAIR of frames;
- *   - FFTs are radix-2 in LDS in double precision (rows: one workgroup per row; columns:
- *     one workgroup per strip of CW columns), twiddles from a host table;
- *   - the inverse row pass fuses the per-row arg-max (first index on ties), a tiny kernel
+ *   - power-of-two sides: Stockham passes of radix 8 (then 4 / 2) in LDS in double precision
+ *     on half spectra (rows: one workgroup per row; columns: one workgroup per strip of CW
+ *     columns), twiddles from a host table; any other side: mixed radix 8/4/2/3/5/7, or
+ *     Bluestein's chirp-z for a prime factor above 7, with transposed column passes;
+ *   - the inverse row pass fuses a per-row TOP-2 arg-max (first index on ties), a tiny kernel
  *     reduces the rows in order.
- * Only the arg-max leaves the device, so results equal the reference wherever the top two
- * correlation values are separated by more than the FFT rounding of either side (the exact
- * correlations are integers; FFTW's own choice between exactly tied integers is not
- * specified — "parity unpinned" there).  S must be a power of two.
+ * Near ties: when the runner-up lies within 2^-32 S^2 ||ref|| ||img|| of the maximum (far
+ * above fp64 FFT rounding), every index within that tolerance is listed and its exact integer
+ * correlation computed; the largest wins, the lowest index among exact equals.  So shifts equal
+ * the reference wherever FFTW's rounding does not decide between exactly equal correlations
+ * (FFTW's choice there is unspecified: "parity unpinned").
  */
 #include "sg_common.hpp"
 #include "sg_ctx.hpp"
+#include "sg_fft.hpp"
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
 #include <type_traits>
 #include <vector>
 
-typedef double2 sg_c64;
-
-__device__ __forceinline__ int sg_bitrev(int x, int logn) {
-	return (int)(__brev((unsigned)x) >> (32 - logn));
-}
-
-/* ------------------------------------------------------------------------------------
- * nb independent length-n FFTs held in LDS (transform b at buf + b*bstride), natural order
- * in and out: Stockham auto-sort passes of radix 8 (then 4 / 2 for the remaining factor),
- * each thread taking whole radix-R butterflies in registers (a 2048-point transform is 4
- * LDS round trips instead of 11).  tw: see sg_twiddle; the inverse uses
- * conjugate twiddles (unnormalised, FFTW_BACKWARD).
- * ------------------------------------------------------------------------------------ */
-/* LDS element index with one pad slot per 8 elements: the Stockham stores of the first
- * passes (stride 8 and 64 elements between neighbouring threads) would otherwise hit the
- * same banks 8- to 32-fold */
-__device__ __forceinline__ int sg_pad(int i) {
-	return i + (i >> 3);
-}
-#define SG_PADN(n) ((n) + ((n) >> 3))
-
-__device__ __forceinline__ sg_c64 sg_cmul(sg_c64 a, sg_c64 b) {
-	return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
-__device__ __forceinline__ sg_c64 sg_cadd(sg_c64 a, sg_c64 b) {
-	return make_double2(a.x + b.x, a.y + b.y);
-}
-__device__ __forceinline__ sg_c64 sg_csub(sg_c64 a, sg_c64 b) {
-	return make_double2(a.x - b.x, a.y - b.y);
-}
-/* multiply by -i (forward) or +i (inverse) */
-__device__ __forceinline__ sg_c64 sg_mul_mi(sg_c64 a, bool inv) {
-	return inv ? make_double2(-a.y, a.x) : make_double2(a.y, -a.x);
-}
-
-/* in-register DFT of R = 2, 4, 8 points (natural order in and out) */
-template <int R, int RV>
-__device__ __forceinline__ void sg_dft_small(sg_c64 (&v)[RV], bool inv) {
-	if constexpr (R == 2) {
-		const sg_c64 a = v[0], b = v[1];
-		v[0] = sg_cadd(a, b);
-		v[1] = sg_csub(a, b);
-		return;
-	}
-	else if constexpr (R == 4) {
-		const sg_c64 a0 = sg_cadd(v[0], v[2]), a1 = sg_csub(v[0], v[2]);
-		const sg_c64 b0 = sg_cadd(v[1], v[3]), b1 = sg_mul_mi(sg_csub(v[1], v[3]), inv);
-		v[0] = sg_cadd(a0, b0);
-		v[2] = sg_csub(a0, b0);
-		v[1] = sg_cadd(a1, b1);
-		v[3] = sg_csub(a1, b1);
-		return;
-	} else {
-	/* R = 8: radix-2 DIF into two 4-point DFTs */
-	const double h = 0.70710678118654752440;
-	sg_c64 e[4], o[4];
-#pragma unroll
-	for (int k = 0; k < 4; k++) {
-		e[k] = sg_cadd(v[k], v[k + 4]);
-		o[k] = sg_csub(v[k], v[k + 4]);
-	}
-	/* o[k] *= W8^k */
-	o[1] = inv ? make_double2(h * (o[1].x - o[1].y), h * (o[1].x + o[1].y))
-		   : make_double2(h * (o[1].x + o[1].y), h * (o[1].y - o[1].x));
-	o[2] = sg_mul_mi(o[2], inv);
-	o[3] = inv ? make_double2(-h * (o[3].x + o[3].y), h * (o[3].x - o[3].y))
-		   : make_double2(h * (o[3].y - o[3].x), -h * (o[3].x + o[3].y));
-	sg_dft_small<4>(e, inv);
-	sg_dft_small<4>(o, inv);
-	const sg_c64 *E = e, *O = o;
-#pragma unroll
-	for (int k = 0; k < 4; k++) {
-		v[2 * k] = E[k];
-		v[2 * k + 1] = O[k];
-	}
-	}
-}
-
-/* tw holds the full circle twice: tw[k] = exp(-2 pi i k / n) and tw[n + k] = its conjugate
- * (the inverse), k < n, built on the host from the half-circle values by exact negation /
- * conjugation, so a twiddle is one load with no select (the direction is uniform) */
-__device__ __forceinline__ sg_c64 sg_twiddle(const sg_c64 *__restrict__ tw, int n, int k, bool inv) {
-	return (inv ? tw + n : tw)[k];
-}
-
-template <int R>
-__device__ __forceinline__ void sg_stockham_pass(sg_c64 *buf, int n, int nb, int bstride, int Ns,
-		const sg_c64 *__restrict__ tw, bool inv) {
-	constexpr int MAXI = 8 / R;	/* work items per thread: nb * n <= 8 * blockDim (host-sized launches) */
-	const int per = n / R, items = nb * per;
-	sg_c64 v[MAXI][R], w[MAXI][R];
-	const bool twiddled = Ns > 1;	/* the first pass (Ns = 1) multiplies by w^0 = 1 only */
-	/* load every item's R inputs before anyone stores (in-place pass); the twiddles are
-	 * fetched here too, so their latency overlaps the barrier wait */
-#pragma unroll
-	for (int it = 0; it < MAXI; it++) {
-		const int t = threadIdx.x + it * blockDim.x;
-		if (t < items) {
-			const int b = t / per, j = t - b * per;
-			const sg_c64 *x = buf + (size_t)b * bstride;
-#pragma unroll
-			for (int r = 0; r < R; r++)
-				v[it][r] = x[sg_pad(j + r * per)];
-			if (twiddled) {
-				const int jm = j & (Ns - 1);
-				const int kstep = jm * (n / (Ns * R));
-#pragma unroll
-				for (int r = 1; r < R; r++)
-					w[it][r] = sg_twiddle(tw, n, r * kstep, inv);
-			}
-		}
-	}
-	__syncthreads();
-#pragma unroll
-	for (int it = 0; it < MAXI; it++) {
-		const int t = threadIdx.x + it * blockDim.x;
-		if (t < items) {
-			const int b = t / per, j = t - b * per;
-			const int jm = j & (Ns - 1);
-			if (twiddled) {
-#pragma unroll
-				for (int r = 1; r < R; r++)
-					v[it][r] = sg_cmul(v[it][r], w[it][r]);
-			}
-			sg_dft_small<R, R>(v[it], inv);
-			sg_c64 *y = buf + (size_t)b * bstride;
-			const int base = (j - jm) * R + jm;
-#pragma unroll
-			for (int r = 0; r < R; r++)
-				y[sg_pad(base + r * Ns)] = v[it][r];
-		}
-	}
-	__syncthreads();
-}
-
-__device__ __forceinline__ void sg_lds_fft(sg_c64 *buf, int n, int logn, int nb, int bstride, const sg_c64 *__restrict__ tw,
-		bool inverse) {
-	(void)logn;
-	__syncthreads();
-	int Ns = 1;
-	while (Ns < n) {
-		const int rem = n / Ns;
-		if (rem >= 8) {
-			sg_stockham_pass<8>(buf, n, nb, bstride, Ns, tw, inverse);
-			Ns *= 8;
-		} else if (rem == 4) {
-			sg_stockham_pass<4>(buf, n, nb, bstride, Ns, tw, inverse);
-			Ns *= 4;
-		} else {
-			sg_stockham_pass<2>(buf, n, nb, bstride, Ns, tw, inverse);
-			Ns *= 2;
-		}
-	}
-}
-
-/* The same transform with its first pass reading the input straight from memory and its
- * last pass writing the output straight to memory (ld(b, i) / st(b, i, v): element i of
- * transform b): two LDS round trips and four barriers fewer than staging through LDS.
- * Work items of these two passes are batch-minor (item t -> b = t % nb), so neighbouring
- * lanes of a column strip touch neighbouring columns of one row (64-B row segments).
- * The arithmetic is that of sg_lds_fft, operation for operation (n < 16, a single pass:
- * staged through LDS). */
-/* LDS_IN: ld reads this same LDS buffer (element i of transform b at its padded slot), so
- * the first pass loads everything before anyone stores.  A st that writes element i back
- * to its own slot is race-free as is: the last pass's thread reads exactly the slots it
- * writes. */
-template <bool LDS_IN = false, class LD, class ST>
-__device__ __forceinline__ void sg_fft_io(sg_c64 *buf, int n, int nb, int bstride, const sg_c64 *__restrict__ tw,
-		bool inv, LD ld, ST st) {
-	if (n < 16) {
-		for (int t = threadIdx.x; t < nb * n; t += blockDim.x)
-			buf[(size_t)(t % nb) * bstride + sg_pad(t / nb)] = ld(t % nb, t / nb);
-		sg_lds_fft(buf, n, 0, nb, bstride, tw, inv);
-		for (int t = threadIdx.x; t < nb * n; t += blockDim.x)
-			st(t % nb, t / nb, buf[(size_t)(t % nb) * bstride + sg_pad(t / nb)]);
-		return;
-	}
-	/* first pass: radix 8, Ns = 1 (no twiddles) */
-	{
-		const int per = n >> 3, items = nb * per;
-		const int t = threadIdx.x;
-		const bool act = t < items;
-		const int b = act ? t % nb : 0, j = act ? t / nb : 0;
-		sg_c64 v[8];
-		if (act) {
-#pragma unroll
-			for (int r = 0; r < 8; r++)
-				v[r] = ld(b, j + r * per);
-		}
-		if (LDS_IN)
-			__syncthreads();
-		if (act) {
-			sg_dft_small<8, 8>(v, inv);
-			sg_c64 *y = buf + (size_t)b * bstride;
-#pragma unroll
-			for (int r = 0; r < 8; r++)
-				y[sg_pad(j * 8 + r)] = v[r];
-		}
-	}
-	__syncthreads();
-	int Ns = 8;
-	/* middle passes in LDS (sg_lds_fft's radix sequence: 8 while n / Ns >= 8, then 4 or 2),
-	 * leaving the last one */
-	while (n / Ns > 8) {
-		sg_stockham_pass<8>(buf, n, nb, bstride, Ns, tw, inv);
-		Ns *= 8;
-	}
-	const int rl = n / Ns;
-	auto last = [&](auto RC) {
-		constexpr int R = decltype(RC)::value;
-		constexpr int MAXI = 8 / R;
-		const int per = n / R, items = nb * per;
-#pragma unroll
-		for (int it = 0; it < MAXI; it++) {
-			const int t = threadIdx.x + it * blockDim.x;
-			if (t < items) {
-				const int b = t % nb, j = t / nb;
-				const sg_c64 *x = buf + (size_t)b * bstride;
-				sg_c64 v[R];
-#pragma unroll
-				for (int r = 0; r < R; r++)
-					v[r] = x[sg_pad(j + r * per)];
-#pragma unroll
-				for (int r = 1; r < R; r++)
-					v[r] = sg_cmul(v[r], sg_twiddle(tw, n, r * j, inv));
-				sg_dft_small<R, R>(v, inv);
-#pragma unroll
-				for (int r = 0; r < R; r++)
-					st(b, j + r * per, v[r]);
-			}
-		}
-	};
-	if (rl == 8)
-		last(std::integral_constant<int, 8>());
-	else if (rl == 4)
-		last(std::integral_constant<int, 4>());
-	else
-		last(std::integral_constant<int, 2>());
-}
-
 /* row pass of the forward transform of a + i b (b = -1: zero imaginary part) */
 __global__ void __launch_bounds__(512)
 k_reg_rows_fwd(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const int *__restrict__ fb,
-		int S, int logS, const sg_c64 *__restrict__ tw, sg_c64 *__restrict__ work) {
+		int S, int logS, const sg_c64 *__restrict__ tw, sg_c64 *__restrict__ work,
+		unsigned long long *__restrict__ energy) {
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 	sg_c64 *buf = (sg_c64 *)smem;
 	const int row = blockIdx.x, pair = blockIdx.y;
@@ -281,10 +46,17 @@ k_reg_rows_fwd(const uint16_t *__restrict__ sel, const int *__restrict__ fa, con
 	const int b = fb[pair];
 	const uint16_t *pb = b >= 0 ? sel + (size_t)b * plane + (size_t)row * S : nullptr;
 	sg_c64 *out = work + (size_t)pair * plane + (size_t)row * S;
+	unsigned long long ea = 0, eb = 0;
 	(void)logS;
 	sg_fft_io(buf, S, 1, S, tw, false,
-			[&](int, int i) { return make_double2((double)pa[i], pb ? (double)pb[i] : 0.0); },
+			[&](int, int i) {
+				const unsigned int va = pa[i], vb = pb ? pb[i] : 0u;
+				ea += (unsigned long long)(va * va);
+				eb += (unsigned long long)(vb * vb);
+				return make_double2((double)va, (double)vb);
+			},
 			[&](int, int i, sg_c64 v) { out[i] = v; });
+	sg_energy_add(ea, eb, fa[pair], b, energy);
 }
 
 /* strip of workgroup `id` out of n: the dispatcher deals workgroups round-robin over the 8
@@ -383,114 +155,59 @@ k_reg_xpower_rows_inv(sg_c64 *__restrict__ work, const sg_c64 *__restrict__ spec
 			[&](int b, int i, sg_c64 v) { Z[(size_t)(b ? my : ky) * S + i] = v; });
 }
 
-/* better (value, index): larger value, ties -> lower index (first strict max, :337-343) */
-__device__ __forceinline__ void sg_argmax_merge(double &v, int &i, double v2, int i2) {
-	if (v2 > v || (v2 == v && i2 < i)) {
-		v = v2;
-		i = i2;
-	}
-}
-
-struct SgBest {
-	double va, vb;
-	int ia, ib;
-};
-
-/* inverse row pass fused with the per-row arg-max of the real (frame a) and imaginary
+/* inverse row pass fused with the per-row top-2 arg-max of the real (frame a) and imaginary
  * (frame b) parts */
 __global__ void __launch_bounds__(512)
 k_reg_rows_inv_argmax(const sg_c64 *__restrict__ work, int S, int logS, const sg_c64 *__restrict__ tw,
 		SgBest *__restrict__ best) {
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 	sg_c64 *buf = (sg_c64 *)smem;
-	__shared__ double rv[2][8];
-	__shared__ int ri[2][8];
+	__shared__ SgBest red[8];
 	const int row = blockIdx.x, pair = blockIdx.y;
 	const sg_c64 *in = work + (size_t)pair * S * S + (size_t)row * S;
-	double va = -INFINITY, vb = -INFINITY;
-	int ia = 0x7fffffff, ib = 0x7fffffff;
+	SgTop2 ta, tb;
+	sg_top2_init(ta);
+	sg_top2_init(tb);
 	(void)logS;
 	sg_fft_io(buf, S, 1, S, tw, true, [&](int, int j) { return in[j]; },
 			[&](int, int j, sg_c64 c) {
 				const int idx = row * S + j;
-				sg_argmax_merge(va, ia, c.x, idx);
-				sg_argmax_merge(vb, ib, c.y, idx);
+				sg_top2_add(ta, c.x, idx);
+				sg_top2_add(tb, c.y, idx);
 			});
-	for (int o = 32; o > 0; o >>= 1) {
-		const double va2 = __shfl_down(va, o, 64), vb2 = __shfl_down(vb, o, 64);
-		const int ia2 = __shfl_down(ia, o, 64), ib2 = __shfl_down(ib, o, 64);
-		sg_argmax_merge(va, ia, va2, ia2);
-		sg_argmax_merge(vb, ib, vb2, ib2);
-	}
-	const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-	if ((threadIdx.x & 63) == 0) {
-		rv[0][wave] = va;
-		ri[0][wave] = ia;
-		rv[1][wave] = vb;
-		ri[1][wave] = ib;
-	}
-	__syncthreads();
+	sg_best_block(ta, tb, red);
 	if (threadIdx.x == 0) {
-		for (int w = 1; w < nw; w++) {
-			sg_argmax_merge(va, ia, rv[0][w], ri[0][w]);
-			sg_argmax_merge(vb, ib, rv[1][w], ri[1][w]);
-		}
-		SgBest r;
-		r.va = va;
-		r.ia = ia;
-		r.vb = vb;
-		r.ib = ib;
-		best[(size_t)pair * S + row] = r;
+		best[(size_t)pair * S + row].a = ta;
+		best[(size_t)pair * S + row].b = tb;
 	}
 }
 
-/* inverse column pass fused with the arg-max of the real (frame a) and imaginary (frame b)
- * parts over the strip: nothing is written back */
+/* inverse column pass fused with the top-2 arg-max of the real (frame a) and imaginary
+ * (frame b) parts over the strip: nothing is written back */
 __global__ void __launch_bounds__(1024)
 k_reg_cols_inv_argmax(const sg_c64 *__restrict__ work, int S, int logS, int CW, const sg_c64 *__restrict__ tw,
 		SgBest *__restrict__ best, int xcdmap) {
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 	sg_c64 *buf = (sg_c64 *)smem;
-	__shared__ double rv[2][16];
-	__shared__ int ri[2][16];
+	__shared__ SgBest red[16];
 	const int strip = sg_xcd_strip(blockIdx.x, gridDim.x, xcdmap);
 	const int x0 = strip * CW, pair = blockIdx.y;
 	const int bstride = SG_PADN(S) + 1;
 	const sg_c64 *base = work + (size_t)pair * S * S + x0;
-	double va = -INFINITY, vb = -INFINITY;
-	int ia = 0x7fffffff, ib = 0x7fffffff;
+	SgTop2 ta, tb;
+	sg_top2_init(ta);
+	sg_top2_init(tb);
 	(void)logS;
 	sg_fft_io(buf, S, CW, bstride, tw, true, [&](int c, int r) { return base[(size_t)r * S + c]; },
 			[&](int c, int r, sg_c64 v) {
 				const int lin = r * S + x0 + c;
-				sg_argmax_merge(va, ia, v.x, lin);
-				sg_argmax_merge(vb, ib, v.y, lin);
+				sg_top2_add(ta, v.x, lin);
+				sg_top2_add(tb, v.y, lin);
 			});
-	for (int o = 32; o > 0; o >>= 1) {
-		const double va2 = __shfl_down(va, o, 64), vb2 = __shfl_down(vb, o, 64);
-		const int ia2 = __shfl_down(ia, o, 64), ib2 = __shfl_down(ib, o, 64);
-		sg_argmax_merge(va, ia, va2, ia2);
-		sg_argmax_merge(vb, ib, vb2, ib2);
-	}
-	const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-	if ((threadIdx.x & 63) == 0) {
-		rv[0][wave] = va;
-		ri[0][wave] = ia;
-		rv[1][wave] = vb;
-		ri[1][wave] = ib;
-	}
-	__syncthreads();
+	sg_best_block(ta, tb, red);
 	if (threadIdx.x == 0) {
-		for (int w = 1; w < nw; w++) {
-			sg_argmax_merge(va, ia, rv[0][w], ri[0][w]);
-			sg_argmax_merge(vb, ib, rv[1][w], ri[1][w]);
-		}
-		SgBest r;
-		r.va = va;
-		r.ia = ia;
-		r.vb = vb;
-		r.ib = ib;
-		best[(size_t)pair * gridDim.x + strip] = r;
+		best[(size_t)pair * gridDim.x + strip].a = ta;
+		best[(size_t)pair * gridDim.x + strip].b = tb;
 	}
 }
 
@@ -513,7 +230,7 @@ k_reg_cols_inv_argmax(const sg_c64 *__restrict__ work, int S, int logS, int CW, 
  * ------------------------------------------------------------------------------------- */
 __global__ void __launch_bounds__(512)
 k_reg_rows_fwd_half(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const int *__restrict__ fb,
-		int S, const sg_c64 *__restrict__ tw, sg_c64 *__restrict__ work) {
+		int S, const sg_c64 *__restrict__ tw, sg_c64 *__restrict__ work, unsigned long long *__restrict__ energy) {
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 	sg_c64 *buf = (sg_c64 *)smem;
 	const int row = blockIdx.x, pair = blockIdx.y, H = S >> 1;
@@ -522,10 +239,16 @@ k_reg_rows_fwd_half(const uint16_t *__restrict__ sel, const int *__restrict__ fa
 	const int b = fb[pair];
 	const uint16_t *pb = b >= 0 ? sel + (size_t)b * plane + (size_t)row * S : nullptr;
 	sg_c64 *out = work + (size_t)pair * plane + (size_t)row * S;
+	unsigned long long ea = 0, eb = 0;
 	sg_fft_io(buf, S, 1, S, tw, false,
-			[&](int, int i) { return make_double2((double)pa[i], pb ? (double)pb[i] : 0.0); },
+			[&](int, int i) {
+				const unsigned int va = pa[i], vb = pb ? pb[i] : 0u;
+				ea += (unsigned long long)(va * va);
+				eb += (unsigned long long)(vb * vb);
+				return make_double2((double)va, (double)vb);
+			},
 			[&](int, int i, sg_c64 v) { buf[sg_pad(i)] = v; });
-	__syncthreads();
+	sg_energy_add(ea, eb, fa[pair], b, energy);	/* its __syncthreads also orders the LDS writes */
 	for (int k = threadIdx.x; k < H; k += blockDim.x) {
 		const sg_c64 zk = buf[sg_pad(k)], zm = buf[sg_pad(k ? S - k : H)];
 		sg_c64 A, B;
@@ -620,17 +343,85 @@ k_reg_cols_xpower(sg_c64 *__restrict__ work, const sg_c64 *__restrict__ spec, in
 			[&](int c, int r, sg_c64 v) { base[(size_t)r * S + c] = v; });
 }
 
+/* per-pair result of a registration batch (frame a = the real part, frame b = the imaginary) */
+struct SgRegOut {
+	int sx[2], sy[2];	/* the shifts (:344-351) */
+	int idx[2];		/* arg-max (row-major) */
+	int amb[2];		/* near tie: the runner-up lies within `tol` of the maximum */
+	double v[2], v2[2], thr[2];	/* maximum, runner-up, max - tol */
+};
+
+/* tolerance of a correlation value: 2^-32 S^2 ||ref|| ||img|| (the unnormalised inverse scales
+ * the exact correlation sum_n ref(n+k) img(n) by S^2, and by Cauchy-Schwarz no entry exceeds
+ * S^2 ||ref|| ||img||); fp64 FFT rounding of the three transforms stays many orders of
+ * magnitude below it, so a maximum that beats every other entry by more than tol is the
+ * exact maximum */
+__device__ __forceinline__ double sg_reg_tol(int S, unsigned long long eref, unsigned long long eimg) {
+	return ldexp((double)S * (double)S * sqrt((double)eref) * sqrt((double)eimg), -32);
+}
+
+/* per pair: reduce the row / strip partials in order, convert to (shiftx, shifty) (:344-351),
+ * flag near ties against the frames' energies */
+__global__ void __launch_bounds__(256)
+k_reg_final(const SgBest *__restrict__ best, int S, int count, const int *__restrict__ fa,
+		const int *__restrict__ fb, int ref, const unsigned long long *__restrict__ energy,
+		SgRegOut *__restrict__ out) {
+	__shared__ SgBest red[4];
+	const int pair = blockIdx.x;
+	SgTop2 ta, tb;
+	sg_top2_init(ta);
+	sg_top2_init(tb);
+	for (int r = threadIdx.x; r < count; r += blockDim.x) {
+		const SgBest b = best[(size_t)pair * count + r];
+		sg_top2_merge(ta, b.a.v, b.a.v2, b.a.i);
+		sg_top2_merge(tb, b.b.v, b.b.v2, b.b.i);
+	}
+	sg_best_block(ta, tb, red);
+	if (threadIdx.x == 0) {
+		SgRegOut o;
+		const SgTop2 t[2] = {ta, tb};
+		const int fr[2] = {fa[pair], fb[pair]};
+		for (int k = 0; k < 2; k++) {
+			int sy = t[k].i / S, sx = t[k].i % S;
+			if (sy > S / 2)
+				sy -= S;
+			if (sx > S / 2)
+				sx -= S;
+			o.sx[k] = sx;
+			o.sy[k] = sy;
+			o.idx[k] = t[k].i;
+			o.v[k] = t[k].v;
+			o.v2[k] = t[k].v2;
+			const double tol = fr[k] >= 0 ? sg_reg_tol(S, energy[ref], energy[fr[k]]) : 0.0;
+			o.thr[k] = t[k].v - tol;
+			o.amb[k] = fr[k] >= 0 && !(t[k].v - t[k].v2 > tol);
+		}
+		out[pair] = o;
+	}
+}
+
+/* CAND: instead of the arg-max, append every index whose correlation reaches the pair's
+ * threshold (SgRegOut::thr, near ties only) to the candidate list of its frame */
+template <bool CAND>
 __global__ void __launch_bounds__(512)
 k_reg_rows_inv_half_argmax(const sg_c64 *__restrict__ work, int S, const sg_c64 *__restrict__ tw,
-		SgBest *__restrict__ best) {
+		SgBest *__restrict__ best, const SgRegOut *__restrict__ res, SgCand *__restrict__ cand) {
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 	sg_c64 *buf = (sg_c64 *)smem;
-	__shared__ double rv[2][8];
-	__shared__ int ri[2][8];
+	__shared__ SgBest red[8];
 	const int row = blockIdx.x, pair = blockIdx.y, H = S >> 1;
 	const sg_c64 *in = work + (size_t)pair * S * S + (size_t)row * S;
-	double va = -INFINITY, vb = -INFINITY;
-	int ia = 0x7fffffff, ib = 0x7fffffff;
+	SgTop2 ta, tb;
+	sg_top2_init(ta);
+	sg_top2_init(tb);
+	double thr[2] = {INFINITY, INFINITY};
+	if (CAND) {
+		const SgRegOut r = res[pair];
+		if (!r.amb[0] && !r.amb[1])
+			return;
+		thr[0] = r.amb[0] ? r.thr[0] : INFINITY;
+		thr[1] = r.amb[1] ? r.thr[1] : INFINITY;
+	}
 	sg_fft_io(buf, S, 1, S, tw, true,
 			[&](int, int i) {
 				sg_c64 qa, qb;
@@ -650,79 +441,20 @@ k_reg_rows_inv_half_argmax(const sg_c64 *__restrict__ work, int S, const sg_c64 
 			},
 			[&](int, int j, sg_c64 c) {
 				const int idx = row * S + j;
-				sg_argmax_merge(va, ia, c.x, idx);
-				sg_argmax_merge(vb, ib, c.y, idx);
+				if (CAND) {
+					sg_cand_push(cand + 2 * pair, c.x, thr[0], idx);
+					sg_cand_push(cand + 2 * pair + 1, c.y, thr[1], idx);
+					return;
+				}
+				sg_top2_add(ta, c.x, idx);
+				sg_top2_add(tb, c.y, idx);
 			});
-	for (int o = 32; o > 0; o >>= 1) {
-		const double va2 = __shfl_down(va, o, 64), vb2 = __shfl_down(vb, o, 64);
-		const int ia2 = __shfl_down(ia, o, 64), ib2 = __shfl_down(ib, o, 64);
-		sg_argmax_merge(va, ia, va2, ia2);
-		sg_argmax_merge(vb, ib, vb2, ib2);
-	}
-	const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-	if ((threadIdx.x & 63) == 0) {
-		rv[0][wave] = va;
-		ri[0][wave] = ia;
-		rv[1][wave] = vb;
-		ri[1][wave] = ib;
-	}
-	__syncthreads();
+	if (CAND)
+		return;
+	sg_best_block(ta, tb, red);
 	if (threadIdx.x == 0) {
-		for (int w = 1; w < nw; w++) {
-			sg_argmax_merge(va, ia, rv[0][w], ri[0][w]);
-			sg_argmax_merge(vb, ib, rv[1][w], ri[1][w]);
-		}
-		SgBest r;
-		r.va = va;
-		r.ia = ia;
-		r.vb = vb;
-		r.ib = ib;
-		best[(size_t)pair * S + row] = r;
-	}
-}
-
-/* per pair: reduce the row maxima and convert to (shiftx, shifty) (:344-351) */
-__global__ void __launch_bounds__(256)
-k_reg_final(const SgBest *__restrict__ best, int S, int count, int *__restrict__ out /* [pair][4] */) {
-	__shared__ double rv[2][4];
-	__shared__ int ri[2][4];
-	const int pair = blockIdx.x;
-	double va = -INFINITY, vb = -INFINITY;
-	int ia = 0x7fffffff, ib = 0x7fffffff;
-	for (int r = threadIdx.x; r < count; r += blockDim.x) {
-		const SgBest b = best[(size_t)pair * count + r];
-		sg_argmax_merge(va, ia, b.va, b.ia);
-		sg_argmax_merge(vb, ib, b.vb, b.ib);
-	}
-	for (int o = 32; o > 0; o >>= 1) {
-		const double va2 = __shfl_down(va, o, 64), vb2 = __shfl_down(vb, o, 64);
-		const int ia2 = __shfl_down(ia, o, 64), ib2 = __shfl_down(ib, o, 64);
-		sg_argmax_merge(va, ia, va2, ia2);
-		sg_argmax_merge(vb, ib, vb2, ib2);
-	}
-	const int wave = threadIdx.x >> 6;
-	if ((threadIdx.x & 63) == 0) {
-		rv[0][wave] = va;
-		ri[0][wave] = ia;
-		rv[1][wave] = vb;
-		ri[1][wave] = ib;
-	}
-	__syncthreads();
-	if (threadIdx.x == 0) {
-		for (int w = 1; w < (int)(blockDim.x >> 6); w++) {
-			sg_argmax_merge(va, ia, rv[0][w], ri[0][w]);
-			sg_argmax_merge(vb, ib, rv[1][w], ri[1][w]);
-		}
-		const int idx[2] = {ia, ib};
-		for (int k = 0; k < 2; k++) {
-			int sy = idx[k] / S, sx = idx[k] % S;
-			if (sy > S / 2)
-				sy -= S;
-			if (sx > S / 2)
-				sx -= S;
-			out[pair * 4 + 2 * k] = sx;
-			out[pair * 4 + 2 * k + 1] = sy;
-		}
+		best[(size_t)pair * S + row].a = ta;
+		best[(size_t)pair * S + row].b = tb;
 	}
 }
 
@@ -754,10 +486,17 @@ k_quality_sub(const uint16_t *__restrict__ sel, const int *__restrict__ qframes,
 			const int j = j0 + jj < ys ? j0 + jj : ys - 1;
 #pragma unroll
 			for (int y = 0; y < 3; y++) {
-				const uint32_t *p = (const uint32_t *)(frame + (size_t)(3 * j + y) * S + 6 * k);
-				d[jj][y][0] = p[0];
-				d[jj][y][1] = p[1];
-				d[jj][y][2] = p[2];
+				const uint16_t *q16 = frame + (size_t)(3 * j + y) * S + 6 * k;
+				if (!(S & 1)) {	/* even side: the 12 bytes are dword aligned */
+					const uint32_t *p = (const uint32_t *)q16;
+					d[jj][y][0] = p[0];
+					d[jj][y][1] = p[1];
+					d[jj][y][2] = p[2];
+				} else {
+					d[jj][y][0] = (uint32_t)q16[0] | ((uint32_t)q16[1] << 16);
+					d[jj][y][1] = (uint32_t)q16[2] | ((uint32_t)q16[3] << 16);
+					d[jj][y][2] = (uint32_t)q16[4] | ((uint32_t)q16[5] << 16);
+				}
 			}
 		}
 #pragma unroll
@@ -901,6 +640,343 @@ k_quality_grad(const uint16_t *__restrict__ qbuf, int xs, int ys, const unsigned
 	}
 }
 
+/* ---------------------------------------------------------------------------------------
+ * Any selection side (FFTW plans every S, registration.c:251-257): mixed-radix Stockham
+ * passes (radix 8, 4, 2, 3, 5, 7) in LDS, one line per workgroup, ping-pong between two LDS
+ * buffers; a side with a prime factor above 7 goes through Bluestein's chirp-z transform
+ * (X_k = c_k sum_j (x_j c_j) conj(c_{k-j}), c_j = exp(-i pi j^2 / n), as an M-point power-of-two
+ * convolution, M >= 2n - 1).  Columns are transformed as rows of the transposed plane:
+ *   rows(u16 -> spectrum) -> transpose -> rows -> cross power -> inverse rows -> transpose ->
+ *   inverse rows + top-2 arg-max.
+ * Same unnormalised FFTW_FORWARD / FFTW_BACKWARD convention and pair packing (a + i b) as the
+ * power-of-two passes; the cross power works on the transposed spectra directly (the mirror of
+ * (r, c) is ((S - r) % S, (S - c) % S) in either layout).
+ * ------------------------------------------------------------------------------------- */
+#define SG_GEN_MAXPASS 16
+struct SgGenPlan {
+	int n, npass;
+	int radix[SG_GEN_MAXPASS];
+	int bluestein, m;	/* Bluestein: convolution length m (power of two) */
+};
+
+/* cos / sin of 2 pi m / R, m < R (R = 3, 5, 7) */
+template <int R>
+__device__ __forceinline__ void sg_unit(int m, double &c, double &s) {
+	if (m == 0) {
+		c = 1.0;
+		s = 0.0;
+		return;
+	}
+	const int mm = m <= R / 2 ? m : R - m;
+	const double sg = m <= R / 2 ? 1.0 : -1.0;
+	if constexpr (R == 3) {
+		c = -0.5;
+		s = 0.86602540378443864676;
+	} else if constexpr (R == 5) {
+		c = mm == 1 ? 0.30901699437494742410 : -0.80901699437494742410;
+		s = mm == 1 ? 0.95105651629515357212 : 0.58778525229247312917;
+	} else {
+		c = mm == 1 ? 0.62348980185873353053 : (mm == 2 ? -0.22252093395631440429 : -0.90096886790241912624);
+		s = mm == 1 ? 0.78183148246802980871 : (mm == 2 ? 0.97492791218182360702 : 0.43388373911755812048);
+	}
+	s *= sg;
+}
+
+/* in-register DFT of an odd prime R: y_k = sum_j v_j w^{jk}, w = exp(-+2 pi i / R) */
+template <int R>
+__device__ __forceinline__ void sg_dft_odd(sg_c64 (&v)[R], bool inv) {
+	sg_c64 y[R];
+#pragma unroll
+	for (int k = 0; k < R; k++) {
+		double re = 0.0, im = 0.0;
+#pragma unroll
+		for (int j = 0; j < R; j++) {
+			double c, sn;
+			sg_unit<R>((j * k) % R, c, sn);
+			if (inv)
+				sn = -sn;
+			/* v_j (c - i sn) */
+			re += v[j].x * c + v[j].y * sn;
+			im += v[j].y * c - v[j].x * sn;
+		}
+		y[k] = make_double2(re, im);
+	}
+#pragma unroll
+	for (int k = 0; k < R; k++)
+		v[k] = y[k];
+}
+
+/* one Stockham pass of radix R, src -> dst (padded LDS indices), items strided over the block */
+template <int R>
+__device__ __forceinline__ void sg_gen_pass(const sg_c64 *src, sg_c64 *dst, int n, int Ns, const sg_c64 *__restrict__ tw,
+		bool inv) {
+	const int per = n / R, tstep = n / (Ns * R);
+	for (int j = threadIdx.x; j < per; j += blockDim.x) {
+		const int k = j % Ns;
+		sg_c64 v[R];
+#pragma unroll
+		for (int r = 0; r < R; r++)
+			v[r] = src[sg_pad(j + r * per)];
+		if (Ns > 1) {
+#pragma unroll
+			for (int r = 1; r < R; r++)
+				v[r] = sg_cmul(v[r], sg_twiddle(tw, n, r * k * tstep, inv));
+		}
+		if constexpr (R == 2 || R == 4 || R == 8)
+			sg_dft_small<R, R>(v, inv);
+		else
+			sg_dft_odd<R>(v, inv);
+		const int base = (j - k) * R + k;
+#pragma unroll
+		for (int r = 0; r < R; r++)
+			dst[sg_pad(base + r * Ns)] = v[r];
+	}
+	__syncthreads();
+}
+
+/* the line in b0 (written and synchronised by the caller) transformed; returns the buffer
+ * holding the result (b0 or b1) */
+__device__ sg_c64 *sg_gen_fft_mixed(sg_c64 *b0, sg_c64 *b1, const SgGenPlan &pl, const sg_c64 *__restrict__ tw, bool inv) {
+	sg_c64 *src = b0, *dst = b1;
+	int Ns = 1;
+	for (int q = 0; q < pl.npass; q++) {
+		const int R = pl.radix[q];
+		switch (R) {
+		case 8: sg_gen_pass<8>(src, dst, pl.n, Ns, tw, inv); break;
+		case 4: sg_gen_pass<4>(src, dst, pl.n, Ns, tw, inv); break;
+		case 2: sg_gen_pass<2>(src, dst, pl.n, Ns, tw, inv); break;
+		case 3: sg_gen_pass<3>(src, dst, pl.n, Ns, tw, inv); break;
+		case 5: sg_gen_pass<5>(src, dst, pl.n, Ns, tw, inv); break;
+		default: sg_gen_pass<7>(src, dst, pl.n, Ns, tw, inv); break;
+		}
+		Ns *= R;
+		sg_c64 *t = src;
+		src = dst;
+		dst = t;
+	}
+	return src;
+}
+
+/* Bluestein: x (n values at buf[pad(0..n)], written and synchronised by the caller) -> X in
+ * place.  The inverse is conj(forward(conj x)).  twm: twiddles of the m-point transforms,
+ * chirp: c_j (j < n), bhat: FFT_m of b (b_j = conj c_|j|, wrapped). */
+__device__ void sg_gen_fft_bluestein(sg_c64 *buf, const SgGenPlan &pl, const sg_c64 *__restrict__ twm,
+		const sg_c64 *__restrict__ chirp, const sg_c64 *__restrict__ bhat, bool inv) {
+	const int n = pl.n, m = pl.m;
+	for (int j = threadIdx.x; j < m; j += blockDim.x) {
+		sg_c64 a = make_double2(0.0, 0.0);
+		if (j < n) {
+			sg_c64 x = buf[sg_pad(j)];
+			if (inv)
+				x.y = -x.y;
+			a = sg_cmul(x, chirp[j]);
+		}
+		buf[sg_pad(j)] = a;
+	}
+	sg_lds_fft(buf, m, 0, 1, m, twm, false);
+	for (int j = threadIdx.x; j < m; j += blockDim.x)
+		buf[sg_pad(j)] = sg_cmul(buf[sg_pad(j)], bhat[j]);
+	sg_lds_fft(buf, m, 0, 1, m, twm, true);
+	const double sc = 1.0 / (double)m;	/* exact: m is a power of two */
+	for (int j = threadIdx.x; j < n; j += blockDim.x) {
+		sg_c64 y = sg_cmul(buf[sg_pad(j)], chirp[j]);
+		y.x *= sc;
+		y.y *= sc;
+		if (inv)
+			y.y = -y.y;
+		buf[sg_pad(j)] = y;
+	}
+	__syncthreads();
+}
+
+struct SgGenTables {
+	const sg_c64 *tw, *twm, *chirp, *bhat;
+};
+
+enum { SG_GEN_FWD_U16 = 0, SG_GEN_C2C = 1, SG_GEN_INV_ARGMAX = 2, SG_GEN_INV_CAND = 3 };
+
+/* one row of pair blockIdx.y: mode FWD_U16 (u16 rows of frames fa / fb packed a + i b, forward,
+ * energies), C2C (in place, forward or inverse), INV_ARGMAX (inverse, top-2 arg-max over the
+ * row), INV_CAND (inverse, candidates of a near tie) */
+__global__ void __launch_bounds__(1024)
+k_gen_rows(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const int *__restrict__ fb,
+		sg_c64 *__restrict__ data, int S, SgGenPlan pl, SgGenTables tb, int mode, int inverse,
+		unsigned long long *__restrict__ energy, SgBest *__restrict__ best, const SgRegOut *__restrict__ res,
+		SgCand *__restrict__ cand) {
+	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+	__shared__ SgBest red[16];
+	sg_c64 *b0 = (sg_c64 *)smem, *b1 = b0 + SG_PADN(S);
+	const int row = blockIdx.x, pair = blockIdx.y;
+	sg_c64 *line = data + ((size_t)pair * S + row) * S;
+	const bool inv = mode >= SG_GEN_INV_ARGMAX || (mode == SG_GEN_C2C && inverse);
+	double thr[2] = {INFINITY, INFINITY};
+	if (mode == SG_GEN_INV_CAND) {
+		const SgRegOut r = res[pair];
+		if (!r.amb[0] && !r.amb[1])
+			return;
+		thr[0] = r.amb[0] ? r.thr[0] : INFINITY;
+		thr[1] = r.amb[1] ? r.thr[1] : INFINITY;
+	}
+	if (mode == SG_GEN_FWD_U16) {
+		const size_t plane = (size_t)S * S;
+		const uint16_t *pa = sel + (size_t)fa[pair] * plane + (size_t)row * S;
+		const int b = fb[pair];
+		const uint16_t *pb = b >= 0 ? sel + (size_t)b * plane + (size_t)row * S : nullptr;
+		unsigned long long ea = 0, eb = 0;
+		for (int i = threadIdx.x; i < S; i += blockDim.x) {
+			const unsigned int va = pa[i], vb = pb ? pb[i] : 0u;
+			ea += (unsigned long long)(va * va);
+			eb += (unsigned long long)(vb * vb);
+			b0[sg_pad(i)] = make_double2((double)va, (double)vb);
+		}
+		sg_energy_add(ea, eb, fa[pair], b, energy);	/* synchronises */
+	} else {
+		for (int i = threadIdx.x; i < S; i += blockDim.x)
+			b0[sg_pad(i)] = line[i];
+		__syncthreads();
+	}
+	sg_c64 *out = b0;
+	if (pl.bluestein)
+		sg_gen_fft_bluestein(b0, pl, tb.twm, tb.chirp, tb.bhat, inv);
+	else
+		out = sg_gen_fft_mixed(b0, b1, pl, tb.tw, inv);
+	if (mode <= SG_GEN_C2C) {
+		for (int i = threadIdx.x; i < S; i += blockDim.x)
+			line[i] = out[sg_pad(i)];
+		return;
+	}
+	SgTop2 ta, tbv;
+	sg_top2_init(ta);
+	sg_top2_init(tbv);
+	for (int j = threadIdx.x; j < S; j += blockDim.x) {
+		const sg_c64 c = out[sg_pad(j)];
+		const int idx = row * S + j;
+		if (mode == SG_GEN_INV_CAND) {
+			sg_cand_push(cand + 2 * pair, c.x, thr[0], idx);
+			sg_cand_push(cand + 2 * pair + 1, c.y, thr[1], idx);
+		} else {
+			sg_top2_add(ta, c.x, idx);
+			sg_top2_add(tbv, c.y, idx);
+		}
+	}
+	if (mode == SG_GEN_INV_CAND)
+		return;
+	sg_best_block(ta, tbv, red);
+	if (threadIdx.x == 0) {
+		best[(size_t)pair * S + row].a = ta;
+		best[(size_t)pair * S + row].b = tbv;
+	}
+}
+
+/* out[pair][x][y] = in[pair][y][x] (32 x 32 tiles in LDS) */
+__global__ void __launch_bounds__(256)
+k_gen_transpose(const sg_c64 *__restrict__ in, sg_c64 *__restrict__ out, int S) {
+	__shared__ sg_c64 tile[32][33];
+	const size_t plane = (size_t)S * S;
+	const sg_c64 *src = in + (size_t)blockIdx.z * plane;
+	sg_c64 *dst = out + (size_t)blockIdx.z * plane;
+	const int x0 = blockIdx.x * 32, y0 = blockIdx.y * 32;
+	for (int r = threadIdx.y; r < 32; r += 8) {
+		const int y = y0 + r, x = x0 + threadIdx.x;
+		if (y < S && x < S)
+			tile[r][threadIdx.x] = src[(size_t)y * S + x];
+	}
+	__syncthreads();
+	for (int r = threadIdx.y; r < 32; r += 8) {
+		const int x = x0 + r, y = y0 + threadIdx.x;
+		if (y < S && x < S)
+			dst[(size_t)x * S + y] = tile[threadIdx.x][r];
+	}
+}
+
+/* separate the packed spectra and form the packed cross-power spectrum, in place, for any S
+ * (k_reg_xpower with modular mirrors) */
+__global__ void __launch_bounds__(256)
+k_gen_xpower(sg_c64 *__restrict__ work, const sg_c64 *__restrict__ spec, int S) {
+	const size_t plane = (size_t)S * S;
+	sg_c64 *Z = work + (size_t)blockIdx.y * plane;
+	for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < plane; i += (size_t)gridDim.x * blockDim.x) {
+		const int r = (int)(i / S), c = (int)(i - (size_t)r * S);
+		const size_t m = (size_t)(r ? S - r : 0) * S + (c ? S - c : 0);
+		if (m < i)
+			continue;
+		const sg_c64 zk = Z[i], zm = Z[m];
+		Z[i] = sg_xpower_at(zk, zm, spec[i]);
+		if (m != i)
+			Z[m] = sg_xpower_at(zm, zk, spec[m]);
+	}
+}
+
+/* exact sum_n ref(n + k) img(n) (circular) at every candidate k of a near tie (below 2^56) */
+__global__ void __launch_bounds__(256)
+k_reg_exact(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const int *__restrict__ fb, int ref, int S,
+		SgCand *__restrict__ cand) {
+	__shared__ unsigned long long part[4];
+	const int c = blockIdx.x, slot = blockIdx.y;
+	SgCand *cd = cand + slot;
+	const unsigned int cnt = cd->count;
+	if (cnt > SG_CAND_CAP || (unsigned)c >= cnt)
+		return;
+	const int frame = (slot & 1) ? fb[slot >> 1] : fa[slot >> 1];
+	if (frame < 0)
+		return;
+	const int k = cd->idx[c], ky = k / S, kx = k - ky * S;
+	const uint16_t *R = sel + (size_t)ref * S * S, *I = sel + (size_t)frame * S * S;
+	unsigned long long acc = 0;
+	for (int y = 0; y < S; y++) {
+		const int yr = y + ky < S ? y + ky : y + ky - S;
+		const uint16_t *rr = R + (size_t)yr * S, *ir = I + (size_t)y * S;
+		for (int x = threadIdx.x; x < S; x += blockDim.x) {
+			const int xr = x + kx < S ? x + kx : x + kx - S;
+			acc += (unsigned long long)((unsigned int)rr[xr] * (unsigned int)ir[x]);
+		}
+	}
+	for (int o = 32; o > 0; o >>= 1)
+		acc += __shfl_down(acc, o, 64);
+	if ((threadIdx.x & 63) == 0)
+		part[threadIdx.x >> 6] = acc;
+	__syncthreads();
+	if (threadIdx.x == 0)
+		cd->exact[c] = (long long)(part[0] + part[1] + part[2] + part[3]);
+}
+
+/* a near tie decided by the exact correlations: the largest, lowest index among equals
+ * (amb 2 = resolved; 3 = more candidates than SG_CAND_CAP: the FFT arg-max stays) */
+__global__ void __launch_bounds__(64)
+k_reg_resolve(const SgCand *__restrict__ cand, int S, int np, SgRegOut *__restrict__ out) {
+	const int pair = blockIdx.x * blockDim.x + threadIdx.x;
+	if (pair >= np)
+		return;
+	SgRegOut o = out[pair];
+	for (int k = 0; k < 2; k++) {
+		if (o.amb[k] != 1)
+			continue;
+		const SgCand *cd = cand + 2 * pair + k;
+		const unsigned int cnt = cd->count;
+		if (cnt < 1 || cnt > SG_CAND_CAP) {
+			o.amb[k] = 3;
+			continue;
+		}
+		int bi = cd->idx[0];
+		long long bv = cd->exact[0];
+		for (unsigned int c = 1; c < cnt; c++)
+			if (cd->exact[c] > bv || (cd->exact[c] == bv && cd->idx[c] < bi)) {
+				bv = cd->exact[c];
+				bi = cd->idx[c];
+			}
+		int sy = bi / S, sx = bi % S;
+		if (sy > S / 2)
+			sy -= S;
+		if (sx > S / 2)
+			sx -= S;
+		o.idx[k] = bi;
+		o.sx[k] = sx;
+		o.sy[k] = sy;
+		o.amb[k] = 2;
+	}
+	out[pair] = o;
+}
+
 static int reg_quality(sg_ctx *ctx, SgDevice &dv, hipStream_t s, const uint16_t *d_sel, int S,
 		const std::vector<int> &frames, std::vector<double> &qual) {
 	const int nq = (int)frames.size();
@@ -955,6 +1031,68 @@ static int ilog2(int v) {
 	return l;
 }
 
+/* forward full circle exp(-2 pi i k / n), k < n, then its conjugate (the inverse), as the
+ * device transforms read them (sg_twiddle).  Power of two: the half circle, negated exactly
+ * for k >= n/2; otherwise every k directly. */
+static void make_twiddles(int n, std::vector<double> &tw) {
+	tw.assign(4 * (size_t)n, 0.0);
+	const bool pow2 = (n & (n - 1)) == 0;
+	for (int k = 0; k < (pow2 ? n / 2 : n); k++) {
+		const double a = -2.0 * M_PI * (double)k / (double)n;
+		const double c = cos(a), sn = sin(a);
+		const int nk = pow2 ? 2 : 1;
+		const int kk[2] = {k, k + n / 2};
+		const double sg[2] = {1.0, -1.0};
+		for (int h = 0; h < nk; h++) {
+			tw[2 * kk[h]] = sg[h] * c;
+			tw[2 * kk[h] + 1] = sg[h] * sn;
+			tw[2 * (n + kk[h])] = sg[h] * c;
+			tw[2 * (n + kk[h]) + 1] = -(sg[h] * sn);
+		}
+	}
+}
+
+/* radices of an n-point mixed-radix plan (8, 4, 2, 3, 5, 7); false: a prime factor > 7 */
+static bool make_plan(int n, SgGenPlan &pl) {
+	memset(&pl, 0, sizeof pl);
+	pl.n = n;
+	int r = n;
+	const int rad[6] = {8, 4, 2, 3, 5, 7};
+	for (int q = 0; q < 6; q++)
+		while (r % rad[q] == 0 && pl.npass < SG_GEN_MAXPASS) {
+			pl.radix[pl.npass++] = rad[q];
+			r /= rad[q];
+		}
+	return r == 1;
+}
+
+/* in-place radix-2 complex DFT on the host (Bluestein's chirp spectrum, computed once per call) */
+static void host_fft_pow2(std::vector<double> &re, std::vector<double> &im, int n) {
+	for (int i = 1, j = 0; i < n; i++) {
+		int bit = n >> 1;
+		for (; j & bit; bit >>= 1)
+			j ^= bit;
+		j ^= bit;
+		if (i < j) {
+			std::swap(re[i], re[j]);
+			std::swap(im[i], im[j]);
+		}
+	}
+	for (int len = 2; len <= n; len <<= 1) {
+		for (int i = 0; i < n; i += len)
+			for (int k = 0; k < len / 2; k++) {
+				const double a = -2.0 * M_PI * (double)k / (double)len;
+				const double wr = cos(a), wi = sin(a);
+				const double xr = re[i + k + len / 2], xi = im[i + k + len / 2];
+				const double vr = xr * wr - xi * wi, vi = xr * wi + xi * wr;
+				re[i + k + len / 2] = re[i + k] - vr;
+				im[i + k + len / 2] = im[i + k] - vi;
+				re[i + k] += vr;
+				im[i + k] += vi;
+			}
+	}
+}
+
 static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int nframes, int S, int ref_image,
 		const int *included, int *shiftx, int *shifty, double *quality, void *stream, bool normalize_q);
 
@@ -978,9 +1116,8 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		return SG_ERR_GENERIC;
 	if (nframes < 1)
 		return set_err(ctx, SG_ERR_GENERIC, "no frame to register%s%ld", "", nframes);
-	if (S < 8 || S > 4096 || (S & (S - 1)))
-		return set_err(ctx, SG_ERR_SIZE, "DFT registration needs a power-of-two selection side "
-				"between 8 and 4096%s (got %ld)", "", S);
+	if (S < 4 || S > 4096)
+		return set_err(ctx, SG_ERR_SIZE, "DFT registration takes selection sides 4 to 4096%s (got %ld)", "", S);
 	if (ref_image < 0)
 		ref_image = 0;	/* seq->reference_image == -1 -> 0 (:212-215) */
 	if (ref_image >= nframes)
@@ -990,6 +1127,14 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	hipStream_t s = stream ? (hipStream_t)stream : dv.stream;
 	const int logS = ilog2(S);
 	const size_t plane = (size_t)S * S;
+	/* power-of-two sides take the fused half-spectrum passes; any other side the generic
+	 * mixed-radix / Bluestein passes (SG_REG_PATH=3 forces those for a power of two, A/B) */
+	const int path = ctx->knobs.reg_path;	/* A/B knob SG_REG_PATH */
+	const bool generic = (S & (S - 1)) != 0 || S < 8 || path == 3;
+	const bool fused = !generic && path == 1;
+	const bool half = !generic && path == 2;
+	const bool resolvable = generic || half;	/* paths with a candidate pass */
+	ctx->stats.reg_ties_resolved = ctx->stats.reg_ties_unresolved = 0;
 
 	/* frames to register, in index order (the reference skips ref and excluded frames) */
 	std::vector<int> todo;
@@ -997,27 +1142,62 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		if (f != ref_image && (!included || included[f]))
 			todo.push_back(f);
 
-	/* twiddles exp(-2 pi i k / S) */
-	HIPCHK(ensure(dv.reg_tw, sizeof(sg_c64) * 2 * S));
+	/* tables: twiddles exp(-2 pi i k / S); generic path: its plan, and for Bluestein the
+	 * m-point twiddles, the chirp c_j = exp(-i pi j^2 / S) and FFT_m(b) */
+	SgGenPlan pl;
+	memset(&pl, 0, sizeof pl);
+	SgGenTables tbl;
+	memset(&tbl, 0, sizeof tbl);
 	{
-		/* forward full circle (k >= S/2: the negated half-circle value), then its conjugate */
-		std::vector<double> tw(4 * (size_t)S);
-		for (int k = 0; k < S / 2; k++) {
-			const double a = -2.0 * M_PI * (double)k / (double)S;
-			const double c = cos(a), sn = sin(a);
-			const int kk[2] = {k, k + S / 2};
-			const double sg[2] = {1.0, -1.0};
-			for (int h = 0; h < 2; h++) {
-				tw[2 * kk[h]] = sg[h] * c;
-				tw[2 * kk[h] + 1] = sg[h] * sn;
-				tw[2 * (S + kk[h])] = sg[h] * c;
-				tw[2 * (S + kk[h]) + 1] = -(sg[h] * sn);
+		std::vector<double> tw;
+		make_twiddles(S, tw);
+		size_t total = tw.size();
+		std::vector<double> twm, ch, bh;
+		if (generic && !make_plan(S, pl)) {
+			pl.bluestein = 1;
+			pl.m = 1;
+			while (pl.m < 2 * S - 1)
+				pl.m <<= 1;
+			const int m = pl.m;
+			make_twiddles(m, twm);
+			ch.assign(2 * (size_t)S, 0.0);
+			std::vector<double> br(m, 0.0), bi(m, 0.0);
+			for (int j = 0; j < S; j++) {
+				const long long q = ((long long)j * j) % (2ll * S);	/* j^2 mod 2S keeps the angle exact */
+				const double a = -M_PI * (double)q / (double)S;
+				ch[2 * j] = cos(a);
+				ch[2 * j + 1] = sin(a);
+				br[j] = ch[2 * j];
+				bi[j] = -ch[2 * j + 1];	/* b_j = conj c_j */
+				if (j) {
+					br[m - j] = br[j];
+					bi[m - j] = bi[j];
+				}
 			}
+			host_fft_pow2(br, bi, m);
+			bh.assign(2 * (size_t)m, 0.0);
+			for (int k = 0; k < m; k++) {
+				bh[2 * k] = br[k];
+				bh[2 * k + 1] = bi[k];
+			}
+			total += twm.size() + ch.size() + bh.size();
 		}
-		HIPCHK(hipMemcpyAsync(dv.reg_tw.p, tw.data(), sizeof(double) * 4 * S, hipMemcpyHostToDevice, s));
-		HIPCHK(hipStreamSynchronize(s));
+		HIPCHK(ensure(dv.reg_tw, sizeof(double) * total));
+		double *d = (double *)dv.reg_tw.p;
+		HIPCHK(hipMemcpyAsync(d, tw.data(), sizeof(double) * tw.size(), hipMemcpyHostToDevice, s));
+		tbl.tw = (const sg_c64 *)d;
+		if (pl.bluestein) {
+			double *d2 = d + tw.size(), *d3 = d2 + twm.size(), *d4 = d3 + ch.size();
+			HIPCHK(hipMemcpyAsync(d2, twm.data(), sizeof(double) * twm.size(), hipMemcpyHostToDevice, s));
+			HIPCHK(hipMemcpyAsync(d3, ch.data(), sizeof(double) * ch.size(), hipMemcpyHostToDevice, s));
+			HIPCHK(hipMemcpyAsync(d4, bh.data(), sizeof(double) * bh.size(), hipMemcpyHostToDevice, s));
+			tbl.twm = (const sg_c64 *)d2;
+			tbl.chirp = (const sg_c64 *)d3;
+			tbl.bhat = (const sg_c64 *)d4;
+		}
+		HIPCHK(hipStreamSynchronize(s));	/* the host vectors die here */
 	}
-	const sg_c64 *tw = (const sg_c64 *)dv.reg_tw.p;
+	const sg_c64 *tw = tbl.tw;
 
 	/* quality of the reference and of every registered frame */
 	std::vector<int> qframes;
@@ -1028,10 +1208,11 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	if (rc)
 		return rc;
 
-	/* batch of pairs per launch: up to 2 GB of pair planes (32 at S = 2048). Half-spectrum
-	 * passes, configs[1]: 32 or 64 pairs 8.95-9.07 ms, 16: 9.08, 4: 9.22-9.32, 2: 9.02-9.15,
-	 * 1: 9.8 ms of registration (scripts/gpu_regbatch.sh) */
-	int B = (int)((size_t)(2048u << 20) / (plane * sizeof(sg_c64)));
+	/* pairs per launch: up to 2 GB of pair planes (32 at S = 2048 on the half path). Half-
+	 * spectrum passes, configs[1]: 32 or 64 pairs 8.95-9.07 ms, 16: 9.08, 4: 9.22-9.32, 2:
+	 * 9.02-9.15, 1: 9.8 ms of registration (round-2 gpu_regbatch.sh) */
+	const size_t pair_bytes = plane * sizeof(sg_c64) * (generic ? 2 : 1);	/* generic: + transposed plane */
+	int B = (int)((size_t)(2048u << 20) / pair_bytes);
 	if (B < 1)
 		B = 1;
 	if (B > 64)
@@ -1050,49 +1231,68 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	if (ctx->knobs.reg_cw > 0)	/* A/B knob SG_REG_CW: columns per column-pass workgroup */
 		CW = ctx->knobs.reg_cw;
 	const size_t col_lds = (size_t)CW * (SG_PADN(S) + 1) * sizeof(sg_c64);
-	(void)hipFuncSetAttribute((const void *)k_reg_rows_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)row_lds);
-	(void)hipFuncSetAttribute((const void *)k_reg_rows_inv_argmax, hipFuncAttributeMaxDynamicSharedMemorySize, (int)row_lds);
-	(void)hipFuncSetAttribute((const void *)k_reg_cols, hipFuncAttributeMaxDynamicSharedMemorySize, (int)col_lds);
-	(void)hipFuncSetAttribute((const void *)k_reg_cols_inv_argmax, hipFuncAttributeMaxDynamicSharedMemorySize,
-			(int)col_lds);
-	(void)hipFuncSetAttribute((const void *)k_reg_xpower_rows_inv, hipFuncAttributeMaxDynamicSharedMemorySize,
-			(int)(2 * row_lds));
 	/* threads: 8 elements per thread in every LDS FFT (sg_stockham_pass's register budget),
 	 * at least one wave */
 	auto thr_for = [](int elems) { return elems / 8 < 64 ? 64 : elems / 8; };
 	const int row_thr = thr_for(S), col_thr = thr_for(CW * S), xri_thr = thr_for(2 * S);
-	/* pass order: 2 = half spectra (3 plane passes), 1 = full spectra with the cross-power
-	 * fused into the inverse row pass (4), 0 = unfused (5) */
-	const int path = ctx->knobs.reg_path;	/* A/B knob SG_REG_PATH */
-	const bool fused = path == 1;
-	const bool half = path == 2;
 	/* half-spectrum columns: a strip stays inside one half (CW divides S/2) */
 	const int CWh = CW < S / 2 ? CW : S / 2;
 	const size_t colh_lds = (size_t)CWh * (SG_PADN(S) + 1) * sizeof(sg_c64);
 	const int colh_thr = thr_for(CWh * S);
-	(void)hipFuncSetAttribute((const void *)k_reg_rows_fwd_half, hipFuncAttributeMaxDynamicSharedMemorySize,
-			(int)row_lds);
-	(void)hipFuncSetAttribute((const void *)k_reg_rows_inv_half_argmax, hipFuncAttributeMaxDynamicSharedMemorySize,
-			(int)row_lds);
-	(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower, hipFuncAttributeMaxDynamicSharedMemorySize,
-			(int)colh_lds);
 	const int xcdmap = ctx->knobs.reg_xcd;	/* A/B knob SG_REG_XCD: 0 = strips in dispatch order */
+	/* generic rows: Bluestein needs m/8 threads (sg_lds_fft), the mixed passes take 256 */
+	const int gen_thr = pl.bluestein ? (pl.m / 8 < 64 ? 64 : pl.m / 8) : 256;
+	const size_t gen_lds = pl.bluestein ? (size_t)SG_PADN(pl.m) * sizeof(sg_c64) : 2 * row_lds;
+	if (!generic) {
+		(void)hipFuncSetAttribute((const void *)k_reg_rows_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)row_lds);
+		(void)hipFuncSetAttribute((const void *)k_reg_rows_inv_argmax, hipFuncAttributeMaxDynamicSharedMemorySize,
+				(int)row_lds);
+		(void)hipFuncSetAttribute((const void *)k_reg_cols, hipFuncAttributeMaxDynamicSharedMemorySize, (int)col_lds);
+		(void)hipFuncSetAttribute((const void *)k_reg_cols_inv_argmax, hipFuncAttributeMaxDynamicSharedMemorySize,
+				(int)col_lds);
+		(void)hipFuncSetAttribute((const void *)k_reg_xpower_rows_inv, hipFuncAttributeMaxDynamicSharedMemorySize,
+				(int)(2 * row_lds));
+		(void)hipFuncSetAttribute((const void *)k_reg_rows_fwd_half, hipFuncAttributeMaxDynamicSharedMemorySize,
+				(int)row_lds);
+		(void)hipFuncSetAttribute((const void *)k_reg_rows_inv_half_argmax<false>,
+				hipFuncAttributeMaxDynamicSharedMemorySize, (int)row_lds);
+		(void)hipFuncSetAttribute((const void *)k_reg_rows_inv_half_argmax<true>,
+				hipFuncAttributeMaxDynamicSharedMemorySize, (int)row_lds);
+		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower, hipFuncAttributeMaxDynamicSharedMemorySize,
+				(int)colh_lds);
+	} else {
+		(void)hipFuncSetAttribute((const void *)k_gen_rows, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gen_lds);
+	}
 
-	HIPCHK(ensure(dv.reg_spec, plane * sizeof(sg_c64)));
-	HIPCHK(ensure(dv.reg_work, (size_t)(B > 1 ? B : 1) * plane * sizeof(sg_c64)));
-	/* row maxima of one batch, then per pair: 4 result ints, frame a, frame b (all pairs of
-	 * the call, uploaded once; results read back once) */
+	/* device workspace: reference spectrum, pair planes, per-row partials, then (all pairs
+	 * of the call, uploaded once / read back once) the pair table, the per-pair results,
+	 * the frames' energies (two sets: the main passes and the near-tie re-run) and the
+	 * near-tie candidates of one batch */
 	const int NP = npairs_total > 0 ? npairs_total : 1;
-	HIPCHK(ensure(dv.reg_best, (size_t)(B > 1 ? B : 1) * S * sizeof(SgBest) + (size_t)(NP + 1) * 6 * sizeof(int) + 64));
+	const int Bc = B > 1 ? B : 1;
+	HIPCHK(ensure(dv.reg_spec, plane * sizeof(sg_c64)));
+	HIPCHK(ensure(dv.reg_work, (size_t)Bc * pair_bytes));
+	const size_t o_out = ((size_t)Bc * S * sizeof(SgBest) + 255) & ~(size_t)255;
+	const size_t o_fab = o_out + (((size_t)(NP + 1) * sizeof(SgRegOut) + 255) & ~(size_t)255);
+	const size_t o_en = o_fab + (((size_t)(NP + 1) * 4 * sizeof(int) + 255) & ~(size_t)255);
+	const size_t o_cand = o_en + (((size_t)nframes * 2 * sizeof(unsigned long long) + 255) & ~(size_t)255);
+	const size_t o_res2 = o_cand + (((size_t)Bc * 2 * sizeof(SgCand) + 255) & ~(size_t)255);
+	const size_t ws = o_res2 + (size_t)(NP + 1) * sizeof(SgRegOut);
+	HIPCHK(ensure(dv.reg_best, ws));
+	char *wsp = (char *)dv.reg_best.p;
 	sg_c64 *spec = (sg_c64 *)dv.reg_spec.p, *work = (sg_c64 *)dv.reg_work.p;
-	SgBest *best = (SgBest *)dv.reg_best.p;
-	int *d_out = (int *)(best + (size_t)(B > 1 ? B : 1) * S);
-	int *d_fa = d_out + 4 * (NP + 1);
-	int *d_fb = d_fa + (NP + 1);
+	sg_c64 *work2 = work + (size_t)Bc * plane;	/* generic path: transposed planes */
+	SgBest *best = (SgBest *)wsp;
+	SgRegOut *d_out = (SgRegOut *)(wsp + o_out), *d_res2 = (SgRegOut *)(wsp + o_res2);
+	int *d_fa = (int *)(wsp + o_fab), *d_fb = d_fa + (NP + 1), *d_fa2 = d_fb + (NP + 1), *d_fb2 = d_fa2 + (NP + 1);
+	unsigned long long *energy = (unsigned long long *)(wsp + o_en), *energy2 = energy + nframes;
+	SgCand *cand = (SgCand *)(wsp + o_cand);
+	HIPCHK(hipMemsetAsync(energy, 0, sizeof(unsigned long long) * 2 * nframes, s));
 
 	/* pair k = frames todo[2k], todo[2k+1] (-1: odd count, imaginary part zero); slot NP is
 	 * the reference spectrum's (ref_image, -1) */
-	std::vector<int> hfa(NP + 1), hfb(NP + 1), hout(4 * (size_t)NP);
+	std::vector<int> hfa(NP + 1), hfb(NP + 1);
+	std::vector<SgRegOut> hout((size_t)NP);
 	for (int k = 0; k < npairs_total; k++) {
 		hfa[k] = todo[2 * k];
 		hfb[k] = (2 * (size_t)k + 1 < todo.size()) ? todo[2 * k + 1] : -1;
@@ -1101,16 +1301,47 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	hfb[NP] = -1;
 	HIPCHK(hipMemcpyAsync(d_fa, hfa.data(), sizeof(int) * (NP + 1), hipMemcpyHostToDevice, s));
 	HIPCHK(hipMemcpyAsync(d_fb, hfb.data(), sizeof(int) * (NP + 1), hipMemcpyHostToDevice, s));
-	/* reference spectrum R = FFT2(ref) (half layout: the A' half only) */
-	if (half) {
+
+	const dim3 tgrid((S + 31) / 32, (S + 31) / 32);
+	/* generic passes up to the cross power's inverse: transposed spectrum of the rows of `fa`
+	 * / `fb` pairs -> `work` holds the pairs' inverse column transforms in row layout */
+	auto gen_forward = [&](const int *fa, const int *fb, int np, unsigned long long *en) -> int {
+		hipLaunchKernelGGL(k_gen_rows, dim3(S, np), dim3(gen_thr), gen_lds, s, d_sel, fa, fb, work, S, pl, tbl,
+				(int)SG_GEN_FWD_U16, 0, en, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
+		HIPCHK(hipGetLastError());
+		hipLaunchKernelGGL(k_gen_transpose, dim3(tgrid.x, tgrid.y, np), dim3(32, 8), 0, s, (const sg_c64 *)work, work2, S);
+		HIPCHK(hipGetLastError());
+		hipLaunchKernelGGL(k_gen_rows, dim3(S, np), dim3(gen_thr), gen_lds, s, d_sel, fa, fb, work2, S, pl, tbl,
+				(int)SG_GEN_C2C, 0, en, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
+		HIPCHK(hipGetLastError());
+		hipLaunchKernelGGL(k_gen_xpower, dim3(1024, np), dim3(256), 0, s, work2, (const sg_c64 *)spec, S);
+		HIPCHK(hipGetLastError());
+		hipLaunchKernelGGL(k_gen_rows, dim3(S, np), dim3(gen_thr), gen_lds, s, d_sel, fa, fb, work2, S, pl, tbl,
+				(int)SG_GEN_C2C, 1, en, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
+		HIPCHK(hipGetLastError());
+		hipLaunchKernelGGL(k_gen_transpose, dim3(tgrid.x, tgrid.y, np), dim3(32, 8), 0, s, (const sg_c64 *)work2, work, S);
+		HIPCHK(hipGetLastError());
+		return SG_OK;
+	};
+
+	/* reference spectrum R = FFT2(ref) (half layout: the A' half only; generic: transposed) */
+	if (generic) {
+		hipLaunchKernelGGL(k_gen_rows, dim3(S, 1), dim3(gen_thr), gen_lds, s, d_sel, d_fa + NP, d_fb + NP, work, S, pl,
+				tbl, (int)SG_GEN_FWD_U16, 0, energy, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
+		HIPCHK(hipGetLastError());
+		hipLaunchKernelGGL(k_gen_transpose, dim3(tgrid.x, tgrid.y, 1), dim3(32, 8), 0, s, (const sg_c64 *)work, spec, S);
+		HIPCHK(hipGetLastError());
+		hipLaunchKernelGGL(k_gen_rows, dim3(S, 1), dim3(gen_thr), gen_lds, s, d_sel, d_fa + NP, d_fb + NP, spec, S, pl,
+				tbl, (int)SG_GEN_C2C, 0, energy, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
+	} else if (half) {
 		hipLaunchKernelGGL(k_reg_rows_fwd_half, dim3(S, 1), dim3(row_thr), row_lds, s, d_sel, d_fa + NP, d_fb + NP,
-				S, tw, spec);
+				S, tw, spec, energy);
 		HIPCHK(hipGetLastError());
 		hipLaunchKernelGGL(k_reg_cols, dim3(S / 2 / CWh, 1), dim3(colh_thr), colh_lds, s, spec, S, logS, CWh, tw, 0,
 				xcdmap);
 	} else {
 		hipLaunchKernelGGL(k_reg_rows_fwd, dim3(S, 1), dim3(row_thr), row_lds, s, d_sel, d_fa + NP, d_fb + NP, S,
-				logS, tw, spec);
+				logS, tw, spec, energy);
 		HIPCHK(hipGetLastError());
 		hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, 1), dim3(col_thr), col_lds, s, spec, S, logS, CW, tw, 0, xcdmap);
 	}
@@ -1119,59 +1350,120 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	shifty[ref_image] = 0;
 	for (int p0 = 0; p0 < npairs_total; p0 += B) {
 		const int np = npairs_total - p0 < B ? npairs_total - p0 : B;
-		if (half) {
+		int count = S;	/* row partials per pair */
+		if (generic) {
+			if (int r = gen_forward(d_fa + p0, d_fb + p0, np, energy))
+				return r;
+			hipLaunchKernelGGL(k_gen_rows, dim3(S, np), dim3(gen_thr), gen_lds, s, d_sel, d_fa + p0, d_fb + p0, work, S,
+					pl, tbl, (int)SG_GEN_INV_ARGMAX, 1, energy, best, (const SgRegOut *)nullptr,
+					(SgCand *)nullptr);
+		} else if (half) {
 			hipLaunchKernelGGL(k_reg_rows_fwd_half, dim3(S, np), dim3(row_thr), row_lds, s, d_sel, d_fa + p0,
-					d_fb + p0, S, tw, work);
+					d_fb + p0, S, tw, work, energy);
 			HIPCHK(hipGetLastError());
 			hipLaunchKernelGGL(k_reg_cols_xpower, dim3(S / CWh, np), dim3(colh_thr), colh_lds, s, work,
 					(const sg_c64 *)spec, S, CWh, tw, xcdmap, ctx->knobs.reg_pb);
 			HIPCHK(hipGetLastError());
-			hipLaunchKernelGGL(k_reg_rows_inv_half_argmax, dim3(S, np), dim3(row_thr), row_lds, s,
-					(const sg_c64 *)work, S, tw, best);
-			HIPCHK(hipGetLastError());
-			hipLaunchKernelGGL(k_reg_final, dim3(np), dim3(256), 0, s, (const SgBest *)best, S, S, d_out + 4 * p0);
-			HIPCHK(hipGetLastError());
-			continue;
-		}
-		hipLaunchKernelGGL(k_reg_rows_fwd, dim3(S, np), dim3(row_thr), row_lds, s, d_sel, d_fa + p0, d_fb + p0, S,
-				logS, tw, work);
-		HIPCHK(hipGetLastError());
-		hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, np), dim3(col_thr), col_lds, s, work, S, logS, CW, tw, 0,
-				xcdmap);
-		HIPCHK(hipGetLastError());
-		if (fused) {
-			/* cross-power + inverse rows (row pairs ky, -ky), then inverse columns with the
-			 * arg-max: two plane round trips fewer than the unfused order */
-			hipLaunchKernelGGL(k_reg_xpower_rows_inv, dim3(S / 2 + 1, np), dim3(xri_thr), 2 * row_lds, s, work,
-					(const sg_c64 *)spec, S, logS, tw);
-			HIPCHK(hipGetLastError());
-			hipLaunchKernelGGL(k_reg_cols_inv_argmax, dim3(S / CW, np), dim3(col_thr), col_lds, s,
-					(const sg_c64 *)work, S, logS, CW, tw, best, xcdmap);
-			HIPCHK(hipGetLastError());
-			hipLaunchKernelGGL(k_reg_final, dim3(np), dim3(256), 0, s, (const SgBest *)best, S, S / CW,
-					d_out + 4 * p0);
+			hipLaunchKernelGGL(k_reg_rows_inv_half_argmax<false>, dim3(S, np), dim3(row_thr), row_lds, s,
+					(const sg_c64 *)work, S, tw, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
 		} else {
-			hipLaunchKernelGGL(k_reg_xpower, dim3(1024, np), dim3(256), 0, s, work, (const sg_c64 *)spec, S);
+			hipLaunchKernelGGL(k_reg_rows_fwd, dim3(S, np), dim3(row_thr), row_lds, s, d_sel, d_fa + p0, d_fb + p0, S,
+					logS, tw, work, energy);
 			HIPCHK(hipGetLastError());
-			hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, np), dim3(col_thr), col_lds, s, work, S, logS, CW, tw, 1,
+			hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, np), dim3(col_thr), col_lds, s, work, S, logS, CW, tw, 0,
 					xcdmap);
 			HIPCHK(hipGetLastError());
-			hipLaunchKernelGGL(k_reg_rows_inv_argmax, dim3(S, np), dim3(row_thr), row_lds, s, (const sg_c64 *)work,
-					S, logS, tw, best);
-			HIPCHK(hipGetLastError());
-			hipLaunchKernelGGL(k_reg_final, dim3(np), dim3(256), 0, s, (const SgBest *)best, S, S, d_out + 4 * p0);
+			if (fused) {
+				/* cross-power + inverse rows (row pairs ky, -ky), then inverse columns with the
+				 * arg-max: two plane round trips fewer than the unfused order */
+				hipLaunchKernelGGL(k_reg_xpower_rows_inv, dim3(S / 2 + 1, np), dim3(xri_thr), 2 * row_lds, s, work,
+						(const sg_c64 *)spec, S, logS, tw);
+				HIPCHK(hipGetLastError());
+				hipLaunchKernelGGL(k_reg_cols_inv_argmax, dim3(S / CW, np), dim3(col_thr), col_lds, s,
+						(const sg_c64 *)work, S, logS, CW, tw, best, xcdmap);
+				count = S / CW;
+			} else {
+				hipLaunchKernelGGL(k_reg_xpower, dim3(1024, np), dim3(256), 0, s, work, (const sg_c64 *)spec, S);
+				HIPCHK(hipGetLastError());
+				hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, np), dim3(col_thr), col_lds, s, work, S, logS, CW, tw, 1,
+						xcdmap);
+				HIPCHK(hipGetLastError());
+				hipLaunchKernelGGL(k_reg_rows_inv_argmax, dim3(S, np), dim3(row_thr), row_lds, s,
+						(const sg_c64 *)work, S, logS, tw, best);
+			}
 		}
+		HIPCHK(hipGetLastError());
+		hipLaunchKernelGGL(k_reg_final, dim3(np), dim3(256), 0, s, (const SgBest *)best, S, count,
+				(const int *)d_fa + p0, (const int *)d_fb + p0, ref_image, (const unsigned long long *)energy,
+				d_out + p0);
 		HIPCHK(hipGetLastError());
 	}
 	if (npairs_total > 0)
-		HIPCHK(hipMemcpyAsync(hout.data(), d_out, sizeof(int) * 4 * npairs_total, hipMemcpyDeviceToHost, s));
+		HIPCHK(hipMemcpyAsync(hout.data(), d_out, sizeof(SgRegOut) * npairs_total, hipMemcpyDeviceToHost, s));
 	HIPCHK(hipStreamSynchronize(s));
+
+	/* near ties (the runner-up within the FFT tolerance of the maximum): re-run those pairs,
+	 * list every index within the tolerance, compute their exact integer correlations and
+	 * take the largest (lowest index among exact equals) */
+	std::vector<int> amb;
+	for (int k = 0; k < npairs_total; k++)
+		if (hout[k].amb[0] || hout[k].amb[1])
+			amb.push_back(k);
+	if (!amb.empty() && resolvable) {
+		const int na = (int)amb.size();
+		std::vector<int> afa(na), afb(na);
+		std::vector<SgRegOut> ares(na);
+		for (int i = 0; i < na; i++) {
+			afa[i] = hfa[amb[i]];
+			afb[i] = hfb[amb[i]];
+			ares[i] = hout[amb[i]];
+		}
+		HIPCHK(hipMemcpyAsync(d_fa2, afa.data(), sizeof(int) * na, hipMemcpyHostToDevice, s));
+		HIPCHK(hipMemcpyAsync(d_fb2, afb.data(), sizeof(int) * na, hipMemcpyHostToDevice, s));
+		HIPCHK(hipMemcpyAsync(d_res2, ares.data(), sizeof(SgRegOut) * na, hipMemcpyHostToDevice, s));
+		for (int p0 = 0; p0 < na; p0 += B) {
+			const int np = na - p0 < B ? na - p0 : B;
+			HIPCHK(hipMemsetAsync(cand, 0, sizeof(SgCand) * 2 * np, s));
+			if (generic) {
+				if (int r = gen_forward(d_fa2 + p0, d_fb2 + p0, np, energy2))
+					return r;
+				hipLaunchKernelGGL(k_gen_rows, dim3(S, np), dim3(gen_thr), gen_lds, s, d_sel, d_fa2 + p0, d_fb2 + p0,
+						work, S, pl, tbl, (int)SG_GEN_INV_CAND, 1, energy2, best, (const SgRegOut *)(d_res2 + p0),
+						cand);
+			} else {
+				hipLaunchKernelGGL(k_reg_rows_fwd_half, dim3(S, np), dim3(row_thr), row_lds, s, d_sel, d_fa2 + p0,
+						d_fb2 + p0, S, tw, work, energy2);
+				HIPCHK(hipGetLastError());
+				hipLaunchKernelGGL(k_reg_cols_xpower, dim3(S / CWh, np), dim3(colh_thr), colh_lds, s, work,
+						(const sg_c64 *)spec, S, CWh, tw, xcdmap, ctx->knobs.reg_pb);
+				HIPCHK(hipGetLastError());
+				hipLaunchKernelGGL(k_reg_rows_inv_half_argmax<true>, dim3(S, np), dim3(row_thr), row_lds, s,
+						(const sg_c64 *)work, S, tw, best, (const SgRegOut *)(d_res2 + p0), cand);
+			}
+			HIPCHK(hipGetLastError());
+			hipLaunchKernelGGL(k_reg_exact, dim3(SG_CAND_CAP, 2 * np), dim3(256), 0, s, d_sel, (const int *)d_fa2 + p0,
+					(const int *)d_fb2 + p0, ref_image, S, cand);
+			HIPCHK(hipGetLastError());
+			hipLaunchKernelGGL(k_reg_resolve, dim3((np + 63) / 64), dim3(64), 0, s, (const SgCand *)cand, S, np,
+					d_res2 + p0);
+			HIPCHK(hipGetLastError());
+		}
+		HIPCHK(hipMemcpyAsync(ares.data(), d_res2, sizeof(SgRegOut) * na, hipMemcpyDeviceToHost, s));
+		HIPCHK(hipStreamSynchronize(s));
+		for (int i = 0; i < na; i++)
+			hout[amb[i]] = ares[i];
+	}
 	for (int k = 0; k < npairs_total; k++) {
-		shiftx[hfa[k]] = hout[4 * k];
-		shifty[hfa[k]] = hout[4 * k + 1];
-		if (hfb[k] >= 0) {
-			shiftx[hfb[k]] = hout[4 * k + 2];
-			shifty[hfb[k]] = hout[4 * k + 3];
+		const int fr[2] = {hfa[k], hfb[k]};
+		for (int h = 0; h < 2; h++) {
+			if (fr[h] < 0)
+				continue;
+			shiftx[fr[h]] = hout[k].sx[h];
+			shifty[fr[h]] = hout[k].sy[h];
+			if (hout[k].amb[h] == 2)
+				ctx->stats.reg_ties_resolved++;
+			else if (hout[k].amb[h])
+				ctx->stats.reg_ties_unresolved++;
 		}
 	}
 

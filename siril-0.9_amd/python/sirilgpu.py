@@ -55,6 +55,8 @@ class StackStats(ctypes.Structure):
         ("launches", ctypes.c_uint64),
         ("main_kernel_blocks", ctypes.c_int),
         ("path", ctypes.c_int),
+        ("reg_ties_resolved", ctypes.c_uint64),
+        ("reg_ties_unresolved", ctypes.c_uint64),
     ]
 
 

@@ -66,10 +66,132 @@ def test_register_golden(gpu_ctx):
     assert _same_q(gq, d["quality"])
 
 
-def test_register_rejects_non_power_of_two(gpu_ctx):
-    sel = np.zeros((2, 48, 48), dtype=np.uint16)
-    with pytest.raises(RuntimeError):
-        gpu_ctx.register_dft(sel)
+# ---- any selection side (FFTW plans every S, registration.c:251-257) ----
+
+def _numpy_shifts(sel, ref=0):
+    """register_shift_dft's arg-max with an independent FFT (numpy pocketfft, float64)"""
+    n, S, _ = sel.shape
+    R = np.fft.fft2(sel[ref].astype(np.float64))
+    sx, sy = np.zeros(n, np.int32), np.zeros(n, np.int32)
+    for f in range(n):
+        if f == ref:
+            continue
+        c = np.fft.ifft2(R * np.conj(np.fft.fft2(sel[f].astype(np.float64)))).real
+        k = int(np.argmax(c))
+        y, x = divmod(k, S)
+        sy[f] = y - S if y > S // 2 else y
+        sx[f] = x - S if x > S // 2 else x
+    return sx, sy
+
+
+@pytest.mark.parametrize("S", [6, 12, 48, 97, 100, 105, 120])
+def test_register_any_side_matches_oracle(gpu_ctx, S):
+    """mixed radix (2, 3, 5, 7 factors) and Bluestein (97: prime) against the oracle's
+    mixed-radix DFT, shifts and qualities exactly"""
+    n = 5
+    sel = orc.synth(n, 1, S, S, seed=S + 3, maxshift=min(7, S // 4))[:, 0].copy()
+    sel[:, S // 3:S // 3 + 2, S // 2:S // 2 + 2] = 40000
+    gx, gy, gq = gpu_ctx.register_dft(sel)
+    rx, ry, rq = orc.register_dft(sel)
+    assert np.array_equal(gx, rx) and np.array_equal(gy, ry), (S, gx, rx, gy, ry)
+    assert _same_q(gq, rq), (gq, rq)
+
+
+@pytest.mark.parametrize("S", [1500, 1009, 1234])
+def test_register_large_non_power_of_two(gpu_ctx, S):
+    """1500 = 2^2 3 5^3 (mixed radix), 1009 (prime) and 1234 = 2 x 617 (Bluestein, m = 4096):
+    the synthetic translations are recovered and equal an independent numpy FFT's arg-max;
+    qualities equal the oracle's QualityEstimate"""
+    n, M = 6, 12
+    sel = orc.synth(n, 1, S, S, seed=S, maxshift=M)[:, 0].copy()
+    gx, gy, gq = gpu_ctx.register_dft(sel, ref_image=0)
+    ex, ey = orc.synth_shifts(n, seed=S, maxshift=M)
+    nx, ny = _numpy_shifts(sel)
+    assert np.array_equal(gx, nx) and np.array_equal(gy, ny), (gx, nx, gy, ny)
+    assert np.array_equal(gx, ex) and np.array_equal(gy, ey)
+    rq = np.array([orc.quality(sel[f]) for f in range(n)])
+    q_min = q_max = rq[0]                   # normalizeQualityData with register_shift_dft's min / max
+    for q in rq[1:]:
+        q_max = q if q > q_max else q_max
+        q_min = q_min if q_min < q else q
+    assert _same_q(gq, (rq - q_min) / (q_max - q_min))
+
+
+def test_register_generic_path_on_power_of_two(gpu_ctx):
+    """SG_REG_PATH=3 sends a power-of-two side through the generic passes: same shifts and
+    qualities as the fused half-spectrum passes"""
+    S, n = 256, 7
+    sel = orc.synth(n, 1, S, S, seed=77, maxshift=9)[:, 0].copy()
+    gx, gy, gq = gpu_ctx.register_dft(sel)
+    os.environ["SG_REG_PATH"] = "3"
+    try:
+        with sg.Context() as c3:
+            hx, hy, hq = c3.register_dft(sel)
+    finally:
+        del os.environ["SG_REG_PATH"]
+    assert np.array_equal(gx, hx) and np.array_equal(gy, hy) and _same_q(gq, hq)
+
+
+def _periodic_pair(S, dx, dy, seed):
+    """ref periodic with period S/2 along x, img = ref circularly translated by (dy, dx):
+    the correlation has two exactly equal maxima, at kx and kx + S/2"""
+    rng = np.random.default_rng(seed)
+    half = rng.integers(500, 3000, size=(S, S // 2)).astype(np.int64)
+    ref = np.concatenate([half, half], axis=1)
+    img = np.roll(ref, (dy, dx), axis=(0, 1))
+    return ref, img
+
+
+@pytest.mark.parametrize("S", [64, 60])
+def test_register_exact_tie_takes_lowest_index(gpu_ctx, S):
+    """an exact tie between two correlation maxima is detected (top-2 margin) and decided by
+    exact integer correlations: the lowest row-major index wins (FFTW's own choice between
+    exactly equal values is unspecified -- parity unpinned)"""
+    ref, img = _periodic_pair(S, 3, 5, seed=S)
+    sel = np.stack([ref, img]).astype(np.uint16)
+    gx, gy, _ = gpu_ctx.register_dft(sel)
+    st = gpu_ctx.stats()
+    # exact correlations at the two candidates: c(k) = sum_n ref(n + k) img(n)
+    k1 = ((-5) % S, (-3) % S)
+    k2 = (k1[0], (k1[1] + S // 2) % S)
+    e1, e2 = orc.xcorr_at(ref, img, *k1), orc.xcorr_at(ref, img, *k2)
+    assert e1 == e2
+    lo = min(k1[0] * S + k1[1], k2[0] * S + k2[1])
+    y, x = divmod(lo, S)
+    assert (gx[1], gy[1]) == (x - S if x > S // 2 else x, y - S if y > S // 2 else y)
+    assert st.reg_ties_resolved >= 1
+
+
+def test_register_near_tie_takes_exact_maximum(gpu_ctx):
+    """two maxima differing by exactly 1 in the integer correlation (a cross term of two
+    single-pixel +1 perturbations, one in each frame, lands on the later one): flagged and
+    decided by the exact correlation -> the later index"""
+    S, dx, dy = 64, 3, 5
+    ref, img = _periodic_pair(S, dx, dy, seed=9)
+    k1 = ((-dy) % S, (-dx) % S)
+    k2 = (k1[0], (k1[1] + S // 2) % S)
+    first, second = sorted([k1, k2], key=lambda k: k[0] * S + k[1])
+    n0 = (7, 11)
+    m0 = ((n0[0] + second[0]) % S, (n0[1] + second[1]) % S)     # m0 - n0 = the later maximum
+    ref = ref.copy()
+    img = img.copy()
+    ref[m0] += 1
+    img[n0] += 1
+    ea, eb = orc.xcorr_at(ref, img, *first), orc.xcorr_at(ref, img, *second)
+    assert eb - ea == 1
+    sel = np.stack([ref, img]).astype(np.uint16)
+    gx, gy, _ = gpu_ctx.register_dft(sel)
+    y, x = second
+    assert (gx[1], gy[1]) == (x - S if x > S // 2 else x, y - S if y > S // 2 else y)
+    assert gpu_ctx.stats().reg_ties_resolved >= 1
+
+
+def test_register_flat_frames_unresolved(gpu_ctx):
+    """constant frames: every shift ties; more candidates than the cap, so the FFT arg-max
+    stands and both registered frames are reported unresolved"""
+    sel = np.full((3, 32, 32), 1234, np.uint16)
+    gpu_ctx.register_dft(sel)
+    assert gpu_ctx.stats().reg_ties_unresolved == 2
 
 
 @pytest.mark.parametrize("world,ref", [(2, 0), (3, 5)])
