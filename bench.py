@@ -1,20 +1,24 @@
 #!/usr/bin/env python3
 """bench.py - frames/s stacked (4096x4096 u16, sigma-clip) + achieved HBM GB/s on MI355X.
 
-BASELINE.json metric, measured on BASELINE.json configs[2] (the configuration the metric
-is quoted on that fits one GPU): sigma-clip rejection stack (SIGMA, sig = (4, 3),
-NO_NORM, registration shifts applied) of 512 synthetic 4096x4096 u16 mono frames,
-frames resident in HBM (generated on the device by include/sg_synth.h).
+BASELINE.json metric.  Workloads (frames synthetic, include/sg_synth.h, generated in HBM):
+  sigma (default)  configs[2] at one GPU: SIGMA (4, 3) stack of 512 x 4096 x 4096 u16 mono with
+                   registration shifts.  At N GPUs (torchrun, one process per GPU) configs[3],
+                   STRONG scaling: the same one 512-frame sequence split into N row bands of
+                   4096/N rows (the reference's own block partition, stacking.c:1397-1476, lifted
+                   to GPUs); each rank holds its band + the rows its shifts reach, stacks it, and
+                   the output bands are gathered to rank 0 over RCCL inside the timed region with
+                   the rejection counters all-reduced.  --scaling weak: each rank stacks a full
+                   4096-row band of one (4096 N)-row sequence (no gather).
+  register-mean    configs[1]: DFT registration of 128 full 2048 x 2048 frames + NO_REJEC mean.
+  winsorized-rgb   configs[4]: 256 x 3 x 4000 x 6000, DFT registration of layer 1's centred 2048
+                   selection + WINSORIZED (4, 3).  At N GPUs: registration sharded over frames (each
+                   rank its block + the reference, shifts all-gathered, normalizeQualityData over all
+                   frames), the stack over row bands, output gathered to rank 0.
+  sum-fits         configs[0]: stack_summing of 16 x 1024 x 1024 u16 FITS files, end to end from the
+                   files (host-pull path: reads + PCIe + kernels), the CPU reference configuration.
 
-One step = one sg_stack_u16_device() call over the whole 512-frame sequence.
-Multi-GPU (torchrun, one process per GPU): weak scaling by row bands -- one sequence of
-512 frames of (4096*G) x 4096 with one set of registration shifts; rank r owns output rows
-[4096 r, 4096 (r+1)) and holds only the frame rows they read (its band plus the rows the
-shifts reach, sg_stack_desc.resident_rows); no data-path collective (each rank's band is
-written to its own output); the 6 rejection counters and the step times are all-reduced
-(max for time).
-
-Output: one JSON line on rank 0 (see README / DESIGN.md for the fields).
+One step = one pass of the workload.  Rank 0 prints ONE JSON line (fields: README / DESIGN.md).
 """
 import argparse
 import json
@@ -32,9 +36,12 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", choices=["sigma", "register-mean", "winsorized-rgb"], default="sigma",
-                    help="sigma = BASELINE configs[2] (the metric's configuration, default); "
-                         "register-mean = configs[1]; winsorized-rgb = configs[4] at one GPU")
+    ap.add_argument("--workload", choices=["sigma", "register-mean", "winsorized-rgb", "sum-fits"], default="sigma",
+                    help="sigma = BASELINE configs[2] (1 GPU) / configs[3] (N GPUs, default); register-mean = "
+                         "configs[1]; winsorized-rgb = configs[4]; sum-fits = configs[0]")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="sigma at N GPUs: strong = one 4096-row sequence in N bands + gather (configs[3]); "
+                         "weak = a 4096-row band per GPU")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--frames", type=int, default=512)
@@ -80,20 +87,34 @@ def synth_shifts_np(N, seed, maxshift):
     return shx, shy
 
 
+def cpu_model():
+    """the host CPU's model name (lscpu's 'Model name', from /proc/cpuinfo)"""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _omp_threads(n):
+    import ctypes
+    try:
+        ctypes.CDLL("libgomp.so.1").omp_set_num_threads(n)
+    except OSError:
+        pass
+
+
 def cpu_baseline(args, N, W):
-    """Oracle (C restatement of the reference stacker, -O2 -fopenmp, the reference's block
-    partition and OpenMP schedule) on a bounded sample of the same workload."""
-    import numpy as np
+    """configs[2]: the oracle (C restatement of stack_mean_with_rejection, -O2 -fopenmp, the
+    reference's block partition and OpenMP schedule) on a bounded sample of the same workload"""
     import oracle_lib as orc
     rows = min(args.cpu_rows, args.height)
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-    lib = orc.load()
-    try:
-        import ctypes
-        ctypes.CDLL("libgomp.so.1").omp_set_num_threads(threads)
-    except OSError:
-        pass
-    # the same synthetic scene and registration shifts as the GPU run, rows [0, rows)
+    orc.load()
+    _omp_threads(threads)
     frames = orc.synth(N, 1, rows, W, seed=0x5151, maxshift=16)
     sx, sy = orc.synth_shifts(N, seed=0x5151, maxshift=16)
     t0 = time.perf_counter()
@@ -103,20 +124,56 @@ def cpu_baseline(args, N, W):
     del frames
     frac = rows / args.height
     return {"value": round(N * frac / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(),
             "sample": f"oracle stack_mean_with_rejection SIGMA(4,3), {N} frames x {rows} rows x {W} "
                       f"cols ({threads} OpenMP threads); frames/s scaled by {rows}/{args.height} rows",
             "seconds": round(dt, 3), "rc": rc}
 
 
-def roofline(achieved, algo_bytes, N, H, W, rejection):
+def cpu_baseline_config(args, workload, N, C, H, W, S, layer):
+    """configs[1] / configs[4]: the oracle's register_shift_dft (its DFT: radix-2 rows and
+    columns, one thread -- the reference runs FFTW per frame in an OpenMP loop over frames,
+    :276-279, so per-frame time / threads is its rate) on a few frames, and its stacker
+    (NO_REJEC mean / WINSORIZED, 16 threads) on a row sample; the step estimate is
+    N x t_register_frame / threads + t_stack scaled to the full image"""
+    import numpy as np
+    import oracle_lib as orc
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    orc.load()
+    _omp_threads(threads)
+    nreg = 3
+    y0, x0 = (H - S) // 2, (W - S) // 2
+    sel = orc.synth_window(nreg, layer, y0, x0, S, S, seed=0x5EED, maxshift=16)
+    t0 = time.perf_counter()
+    orc.register_dft(sel)                 # the reference's spectrum + (nreg - 1) registered frames
+    t_reg = (time.perf_counter() - t0) / (nreg - 1)
+    rows = min(64 if workload == "winsorized-rgb" else 256, H)
+    frames = orc.synth(N, C, rows, W, seed=0x5EED, maxshift=16)
+    sx, sy = orc.synth_shifts(N, seed=0x5EED, maxshift=16)
+    rej = 4 if workload == "winsorized-rgb" else 0
+    t0 = time.perf_counter()
+    orc.stack_rejection(frames, rej, sig=(4.0, 3.0), shiftx=sx, shifty=sy, max_thread=threads, max_number_of_rows=rows)
+    t_stack = (time.perf_counter() - t0) * H / rows
+    del frames
+    step = N * t_reg / threads + t_stack
+    return {"value": round(N / step, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(),
+            "sample": f"oracle register_shift_dft on {nreg} frames of {S}^2 ({t_reg:.2f} s per frame, one thread, "
+                      f"divided by {threads} for the reference's OpenMP loop over frames) + oracle "
+                      f"{'WINSORIZED' if rej else 'NO_REJEC mean'} on {rows} of {H} rows x {C} channels "
+                      f"({threads} threads, scaled)",
+            "seconds_register_per_frame": round(t_reg, 3), "seconds_stack_scaled": round(t_stack, 3)}
+
+
+def roofline(achieved, algo_bytes, N, H, W, rejection, with_traffic=True):
     """roofline object of the dominant kernel (k_stack_hist for sigma): achieved = algorithmic
     bytes per launch / HIP-event kernel time; traffic = HBM bytes per launch from the
-    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of the same workload (scripts/gpu_pmc_traffic.sh
-    -> profiles/traffic_<workload>.json, corrected per MI355X_MICROARCH.md), when present"""
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of the same workload (scripts/gpu.sh pmc ->
+    profiles/traffic_<workload>.json, corrected per MI355X_MICROARCH.md), when present"""
     r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None}
     path = os.path.join(ROOT, "profiles", f"traffic_{rejection}_{N}x{H}x{W}.json")
-    if os.path.exists(path):
+    if with_traffic and os.path.exists(path):
         with open(path) as f:
             t = json.load(f)
         r["traffic"] = int(t["traffic_bytes"])
@@ -126,186 +183,172 @@ def roofline(achieved, algo_bytes, N, H, W, rejection):
     return r
 
 
-def main_config(args):
-    """BASELINE configs[1] (register-mean: DFT registration of 128 full 2048x2048 SER-like
-    frames + NO_REJEC mean stack with the found shifts) and configs[4] (winsorized-rgb: 256
-    3-plane 6000x4000 frames, DFT registration of a centred 2048x2048 selection of layer 1,
-    WINSORIZED (4, 3) stack), one GPU, frames resident in HBM.  One step = registration +
-    stack; the stage times are reported beside the step time."""
-    import numpy as np
+class Dist:
+    """one process per GPU (torchrun): RCCL ("nccl") on the node; SG_BENCH_REHEARSE=1 (testing
+    only) runs every rank on cuda:0 over gloo with CPU staging of the collectives"""
+
+    def __init__(self):
+        import torch
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.rehearse = os.environ.get("SG_BENCH_REHEARSE") == "1"
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            torch.cuda.set_device(0 if self.rehearse else local)
+            dist.init_process_group("gloo" if self.rehearse else "nccl")
+            self.dist = dist
+        else:
+            torch.cuda.set_device(0)
+        self.cdev = "cpu" if self.rehearse else "cuda"
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max_time(self, t):
+        import sirilgpu_dist as sd
+        return sd.max_time(t, self.dist, device=self.cdev) if self.dist else t
+
+    def gather_to_root(self, band, out_list):
+        """rank 0 receives every rank's equal-sized band tensor (RCCL gather: each peer sends its
+        band straight to rank 0 over its own xGMI link)"""
+        if self.rehearse:
+            import torch
+            b = band.cpu()
+            lst = [torch.empty_like(b) for _ in range(self.world)] if self.rank == 0 else None
+            self.dist.gather(b, gather_list=lst, dst=0)
+            if self.rank == 0:
+                for o, t in zip(out_list, lst):
+                    o.copy_(t)
+        else:
+            self.dist.gather(band, gather_list=out_list if self.rank == 0 else None, dst=0)
+
+    def sum_counters(self, rej):
+        import numpy as np
+        import torch
+        t = torch.as_tensor(np.asarray(rej, dtype=np.int64).reshape(-1), device=self.cdev)
+        self.dist.all_reduce(t)
+        return t
+
+    def all_floats(self, x):
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64, device=self.cdev)
+        if not self.dist:
+            return [float(x)]
+        outs = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(outs, t)
+        return [float(o.item()) for o in outs]
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def timed(steps, warmup, step, D):
     import torch
-    import sirilgpu as sg
-    torch.cuda.set_device(0)
-    ctx = sg.Context([0])
-    if args.workload == "register-mean":
-        N, C, H, W, S, layer, rej, cfg = 128, 1, 2048, 2048, 2048, 0, sg.NO_REJEC, "BASELINE configs[1]"
-    else:
-        N, C, H, W, S, layer, rej, cfg = 256, 3, 4000, 6000, 2048, 1, sg.WINSORIZED, "BASELINE configs[4], 1 GPU"
-    fstride = C * H * W
-    frames = torch.empty(N * fstride, dtype=torch.int16, device="cuda")
-    out = torch.empty(C * H * W, dtype=torch.int16, device="cuda")
-    ctx.synth_fill(frames.data_ptr(), N, C, H, W, 0, H, 0x5EED, 16)
-    fv = frames.view(N, C, H, W)
-    y0, x0 = (H - S) // 2, (W - S) // 2
-
-    def step():
-        t0 = time.perf_counter()
-        if S == H and S == W and C == 1:
-            sel = frames                      # full-frame selection: the frames themselves
-        else:                                 # seq_read_frame_part of layer `layer`
-            sel = fv[:, layer, y0:y0 + S, x0:x0 + S].contiguous()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        sx, sy, q = ctx.register_dft_device(sel.data_ptr(), N, S)
-        torch.cuda.synchronize()
-        t2 = time.perf_counter()
-        desc, keep = sg.make_desc(sg.MEAN, N, W, H, C, rejection=rej, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
-                                  max_thread=8, max_number_of_rows=H)
-        rejc, _ = ctx.stack_device(desc, frames.data_ptr(), fstride, H * W, out.data_ptr(), 0, H)
-        torch.cuda.synchronize()
-        t3 = time.perf_counter()
-        return (t1 - t0, t2 - t1, t3 - t2), ctx.stats(), sx, sy
-
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    stages = np.zeros(3)
-    kms = []
-    for _ in range(args.steps):
-        st, stats, sx, sy = step()
-        stages += np.array(st)
-        kms.append(stats.kernel_ms)
+    D.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    stages /= args.steps
-    # registration shifts must recover the synthetic translations (frame 0 = reference)
-    ex, ey = synth_shifts_np(N, 0x5EED, 16)
-    reg_ok = bool(np.array_equal(sx, ex) and np.array_equal(sy, ey))
-    kavg = sum(kms) / len(kms)
-    stack_bytes = N * C * H * W * 2 + C * H * W * 2
-    achieved = stack_bytes / (kavg * 1e-3) / 1e9
-    reg_bytes = N * S * S * 58          # stated 2-pass c64 FFT model, SURVEY.md section 8(d)
-    res = {
-        "metric": "frames/sec stacked (registration + stack) + achieved HBM GB/s",
-        "value": round(N / (elapsed / args.steps), 2), "unit": "frames/s", "n_gpus": 1,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u16",
-        "data": "synthetic (include/sg_synth.h, generated in HBM)",
-        "config": {"workload": f"{args.workload} {N}x{C}x{H}x{W} ({cfg})", "frames": N, "layers": C,
-                   "height": H, "width": W, "selection": S, "register_layer": layer,
-                   "rejection": "none" if rej == sg.NO_REJEC else "winsorized"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "stack"},
-        "stage_ms": {"selection": round(stages[0] * 1e3, 3), "register": round(stages[1] * 1e3, 3),
-                     "stack": round(stages[2] * 1e3, 3), "stack_kernel": round(kavg, 3)},
-        "register_GBps_model": round(reg_bytes / stages[1] / 1e9, 1),
-        "slow_pixels": int(stats.slow_pixels), "redo_pixels": int(stats.chain_pixels),
-        "register_shifts_exact": reg_ok,
-    }
-    print(json.dumps(res), flush=True)
-    ctx.close()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    D.barrier()
+    torch.cuda.synchronize()
+    return D.max_time(time.perf_counter() - t0)
 
 
-def main():
-    args = parse()
-    if args.workload != "sigma":
-        return main_config(args)
+def main_sigma(args):
     import numpy as np
     import torch
     import sirilgpu as sg
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        # SG_BENCH_REHEARSE=1 (testing only): every rank on cuda:0 over gloo, to rehearse the
-        # multi-rank flow on a one-GPU box; the driver's runs use one GPU per rank over RCCL
-        rehearse = os.environ.get("SG_BENCH_REHEARSE") == "1"
-        torch.cuda.set_device(0 if rehearse else local)
-        dist.init_process_group("gloo" if rehearse else "nccl")
-    else:
-        torch.cuda.set_device(0)
+    import sirilgpu_dist as sd
+    D = Dist()
+    world, rank = D.world, D.rank
     dev = torch.cuda.current_device()
-
     N, W, H = args.frames, args.width, args.height
     rej_mode = {"sigma": sg.SIGMA, "winsorized": sg.WINSORIZED, "none": sg.NO_REJEC,
                 "percentile": sg.PERCENTILE}[args.rejection]
     ctx = sg.Context([dev])
-    # one sequence of N frames of (H*world) x W; this rank owns output rows [rank*H,
-    # (rank+1)*H) and holds only the frame rows they read (the band plus the rows its
-    # registration shifts reach), addressed through a biased base pointer
-    Htot = H * world
+    strong = args.scaling == "strong" or world == 1
+    # strong: one sequence of N frames of H x W in `world` row bands; weak: one sequence of
+    # N frames of (H*world) x W, a full H-row band per rank.  Each rank holds only the frame
+    # rows its band reads (band + shift halo), addressed through a biased base pointer.
+    Htot = H if strong else H * world
     shx, shy = synth_shifts_np(N, 0x5151, args.maxshift)
     if args.even_shifts:
         shx &= ~1
     if args.zero_shift:
         (shx if args.zero_shift == "x" else shy)[:] = 0
-    b, e = rank * H, (rank + 1) * H
+    b, e = sd.row_band(rank, world, H) if strong else (rank * H, (rank + 1) * H)
     lo, hi = max(0, b - int(shy.max())), min(Htot - 1, e - 1 - int(shy.min()))
     nres = hi - lo + 1
     fstride = nres * W + args.frame_pad
     frames = torch.empty(N * fstride, dtype=torch.int16, device="cuda")
-    out = torch.empty(Htot * W, dtype=torch.int16, device="cuda")
     base = frames.data_ptr() - lo * W * 2
     ctx.synth_fill(base, N, 1, Htot, W, lo, hi + 1, 0x5151, args.maxshift, frame_stride=fstride)
+    hband = -(-H // world) if strong else H
+    band_out = torch.zeros(hband * W, dtype=torch.int16, device="cuda")
+    out_base = band_out.data_ptr() - b * W * 2          # the library writes rows [b, e) of the image
+    gathered = None
+    if strong and world > 1 and rank == 0:
+        gathered = [torch.empty(hband * W, dtype=torch.int16, device="cuda") for _ in range(world)]
     norm_mode, off, mul, scale = sg.NO_NORM, None, None, None
     if args.normalize != "none":
         # synthetic per-frame location / scale (the cached IKSS statistics), coefficients as
         # compute_normalization (src/stacking/stacking.c:79-190) forms them, reference frame 0
-        # (the synthetic frames share one background, so their statistics differ only by noise)
         i = np.arange(N, dtype=np.float64)
         loc = 1000.0 + 0.6 * np.sin(0.37 * i)
         scl = 30.0 + 0.3 * np.cos(0.23 * i)
+        scale = scl[0] / scl
         if args.normalize == "additive-scaling":
             norm_mode = sg.ADDITIVE_SCALING
-            scale = scl[0] / scl
             off = scale * loc - loc[0]
         else:
             norm_mode = sg.MULTIPLICATIVE_SCALING
-            scale = scl[0] / scl
             mul = loc[0] / loc
     desc, keep = sg.make_desc(sg.MEAN, N, W, Htot, 1, rejection=rej_mode, sig=(4.0, 3.0),
                               shiftx=shx, shifty=shy, normalize=norm_mode, offset=off, mul=mul, scale=scale,
                               max_thread=8, max_number_of_rows=Htot, resident_rows=(lo, hi + 1))
+    torch.cuda.synchronize()
+    kms = []
+    state = {}
 
     def step():
-        return ctx.stack_device(desc, base, fstride, nres * W, out.data_ptr(), b, e)
+        rej, _ = ctx.stack_device(desc, base, fstride, nres * W, out_base, b, e)
+        kms.append(ctx.stats().kernel_ms)
+        state["rej"] = rej
+        if strong and world > 1:
+            D.gather_to_root(band_out, gathered)        # output bands -> rank 0 (RCCL over xGMI)
+            state["rej_t"] = D.sum_counters(rej)        # rejection counters, :1796-1817
 
-    for _ in range(args.warmup):
-        step()
-    kms, slow, redo = [], 0, 0
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    rej_tot = None
-    for _ in range(args.steps):
-        rej, _ = step()
-        st = ctx.stats()
-        kms.append(st.kernel_ms)
-        slow = st.slow_pixels
-        redo = st.chain_pixels
-        rej_tot = rej
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        import sirilgpu_dist as sd
-        cdev = "cpu" if os.environ.get("SG_BENCH_REHEARSE") == "1" else "cuda"
-        elapsed = sd.max_time(elapsed, dist, device=cdev)
-        rej_tot = sd.sum_counters(rej_tot, dist, device=cdev)
-    ms_step = elapsed / args.steps * 1e3
-    frames_per_s = N * world / (elapsed / args.steps)
+    elapsed = timed(args.steps, args.warmup, step, D)
+    st = ctx.stats()
+    kms = kms[args.warmup:]
     kavg = sum(kms) / len(kms)
-    algo_bytes = N * H * W * 2 + H * W * 2
+    per_rank_kms = D.all_floats(kavg)
+    rej_tot = state["rej"]
+    if world > 1:
+        rej_tot = (state["rej_t"].cpu().numpy() if strong else sd.sum_counters(rej_tot, D.dist, device=D.cdev))
+    ms_step = elapsed / args.steps * 1e3
+    frames_per_s = N * (1 if strong else world) / (elapsed / args.steps)
+    algo_bytes = N * (e - b) * W * 2 + (e - b) * W * 2     # this rank's launch: its band's samples + output
     achieved = algo_bytes / (kavg * 1e-3) / 1e9
     if rank == 0:
+        if world == 1:
+            workload = f"sigma-clip stack {N}x{H}x{W} u16 mono (BASELINE configs[2])"
+            par = "1 GPU"
+        elif strong:
+            workload = (f"sigma-clip stack {N}x{H}x{W} u16 mono in {world} row bands of {hband} rows, output "
+                        f"gathered to rank 0 (BASELINE configs[3])")
+            par = f"row-band x{world}, RCCL gather"
+        else:
+            workload = f"sigma-clip stack {N}x{H}x{W} u16 mono per GPU, one {N}x{Htot}x{W} sequence in {world} bands"
+            par = f"row-band x{world} (weak)"
         res = {
             "metric": "frames/sec stacked (4096x4096 u16, sigma-clip) + achieved HBM GB/s",
             "value": round(frames_per_s, 2),
@@ -315,27 +358,216 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "u16",
             "data": "synthetic (include/sg_synth.h, generated in HBM)",
-            "config": {"workload": f"sigma-clip stack {N}x{H}x{W} u16 mono per GPU (BASELINE configs[2]"
-                                   + (")" if world == 1 else f"; one {N}x{Htot}x{W} sequence in {world} row bands)"),
-                       "frames": N, "height": H, "width": W, "rejection": args.rejection,
-                       "sig": [4.0, 3.0], "normalize": args.normalize, "parallelism": f"row-band x{world}"},
+            "config": {"workload": workload, "frames": N, "height": H, "width": W, "rejection": args.rejection,
+                       "sig": [4.0, 3.0], "normalize": args.normalize, "parallelism": par},
             "roofline": roofline(achieved, algo_bytes, N, H, W, args.rejection
-                                 if args.normalize == "none" else f"{args.rejection}_{args.normalize}"),
+                                 if args.normalize == "none" else f"{args.rejection}_{args.normalize}",
+                                 with_traffic=world == 1),
             "kernel_ms": round(kavg, 3),
-            "slow_pixels": int(slow),
-            "redo_pixels": int(redo),
-            "rejected": [int(x) for x in rej_tot.reshape(-1)[:2]],
+            "slow_pixels": int(st.slow_pixels),
+            "redo_pixels": int(st.chain_pixels),
+            "rejected": [int(x) for x in np.asarray(rej_tot).reshape(-1)[:2]],
         }
+        if world > 1:
+            res["per_rank_kernel_ms"] = [round(x, 3) for x in per_rank_kms]
+            res["rows_per_rank"] = e - b
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(args, N, W)
         print(json.dumps(res), flush=True)
     ctx.close()
-    if dist:
-        dist.destroy_process_group()
+    D.close()
+
+
+def main_config(args):
+    """configs[1] (register-mean) and configs[4] (winsorized-rgb): one step = registration +
+    stack; at N GPUs the registration is sharded over frames and the stack over row bands"""
+    import numpy as np
+    import torch
+    import sirilgpu as sg
+    import sirilgpu_dist as sd
+    D = Dist()
+    world, rank = D.world, D.rank
+    dev = torch.cuda.current_device()
+    ctx = sg.Context([dev])
+    if args.workload == "register-mean":
+        N, C, H, W, S, layer, rej, cfg = 128, 1, 2048, 2048, 2048, 0, sg.NO_REJEC, "BASELINE configs[1]"
+    else:
+        N, C, H, W, S, layer, rej, cfg = 256, 3, 4000, 6000, 2048, 1, sg.WINSORIZED, "BASELINE configs[4]"
+    seed, M = 0x5EED, 16
+    y0, x0 = (H - S) // 2, (W - S) // 2
+    ex, ey = synth_shifts_np(N, seed, M)
+    # registration shard: the reference (frame 0) + this rank's frame block (without frame 0),
+    # layer `layer`'s selection rows of every channel up to `layer` held compactly
+    fb, fe = sd.frame_band(rank, world, N)
+    mine = [f for f in range(fb, fe) if f != 0]
+    nsel = 1 + len(mine)
+    Cs = layer + 1
+    selsrc = torch.empty(nsel * Cs * S * W, dtype=torch.int16, device="cuda")
+    sbase = selsrc.data_ptr() - y0 * W * 2
+    ctx.synth_fill(sbase, 1, Cs, H, W, y0, y0 + S, seed, M, frame_stride=Cs * S * W, plane_stride=S * W)
+    if mine:
+        ctx.synth_fill(sbase + Cs * S * W * 2, len(mine), Cs, H, W, y0, y0 + S, seed, M, frame_stride=Cs * S * W,
+                       plane_stride=S * W, first_frame=mine[0])
+    selv = selsrc.view(nsel, Cs, S, W)
+    # stack shard: row band of every frame (band + shift halo), all channels
+    b, e = sd.row_band(rank, world, H)
+    lo, hi = max(0, b - int(ey.max())), min(H - 1, e - 1 - int(ey.min()))
+    nres = hi - lo + 1
+    fstride = C * nres * W
+    frames = torch.empty(N * fstride, dtype=torch.int16, device="cuda")
+    fbase = frames.data_ptr() - lo * W * 2
+    ctx.synth_fill(fbase, N, C, H, W, lo, hi + 1, seed, M, frame_stride=fstride, plane_stride=nres * W)
+    hband = -(-H // world)
+    # the library writes rows [b, e) of every channel of a [C][H][W] image; the channels' bands
+    # are packed into one send buffer for the gather
+    out_img = torch.zeros(C * H * W, dtype=torch.int16, device="cuda")
+    band_out = torch.zeros(C * hband * W, dtype=torch.int16, device="cuda")
+    gathered = None
+    if world > 1 and rank == 0:
+        gathered = [torch.empty(C * hband * W, dtype=torch.int16, device="cuda") for _ in range(world)]
+    torch.cuda.synchronize()
+    stage = np.zeros(3)
+    kms = []
+    out = {}
+
+    def step():
+        t0 = time.perf_counter()
+        sel = selv[:, layer, :, x0:x0 + S].contiguous()     # seq_read_frame_part of layer `layer`
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        lx, ly, lq = ctx.register_dft_device(sel.data_ptr(), nsel, S, raw_quality=world > 1)
+        if world > 1:
+            rows = np.zeros((3, N))
+            for k, f in enumerate(mine):
+                rows[:, f] = lx[k + 1], ly[k + 1], lq[k + 1]
+            if rank == 0:
+                rows[2, 0] = lq[0]
+            t = torch.as_tensor(rows, device=D.cdev)
+            D.dist.all_reduce(t)                          # disjoint frame blocks: the sum is the gather
+            rows = t.cpu().numpy()
+            sx, sy = rows[0].astype(np.int32), rows[1].astype(np.int32)
+            q = sd.normalize_quality(rows[2], N, 0, None)
+        else:
+            sx, sy, q = lx, ly, lq
+        t2 = time.perf_counter()
+        desc, keep = sg.make_desc(sg.MEAN, N, W, H, C, rejection=rej, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                                  max_thread=8, max_number_of_rows=H, resident_rows=(lo, hi + 1))
+        rj, _ = ctx.stack_device(desc, fbase, fstride, nres * W, out_img.data_ptr(), b, e)
+        kms.append(ctx.stats().kernel_ms)
+        if world > 1:
+            band_out.view(C, hband, W)[:, :e - b].copy_(out_img.view(C, H, W)[:, b:e])
+            D.gather_to_root(band_out, gathered)
+            D.sum_counters(rj)
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        stage[:] += (t1 - t0, t2 - t1, t3 - t2)
+        out["sx"], out["sy"] = sx, sy
+
+    for _ in range(args.warmup):
+        step()
+    stage[:] = 0
+    kms.clear()
+    elapsed = timed(args.steps, 0, step, D)
+    stage /= args.steps
+    reg_ok = bool(np.array_equal(out["sx"], ex) and np.array_equal(out["sy"], ey))
+    kavg = sum(kms) / len(kms)
+    stack_bytes = N * C * (e - b) * W * 2 + C * (e - b) * W * 2
+    achieved = stack_bytes / (kavg * 1e-3) / 1e9
+    reg_bytes = nsel * S * S * 58          # stated 2-pass c64 FFT model, SURVEY.md section 8(d)
+    if rank == 0:
+        res = {
+            "metric": "frames/sec stacked (registration + stack) + achieved HBM GB/s",
+            "value": round(N / (elapsed / args.steps), 2), "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u16",
+            "data": "synthetic (include/sg_synth.h, generated in HBM)",
+            "config": {"workload": f"{args.workload} {N}x{C}x{H}x{W} ({cfg})", "frames": N, "layers": C,
+                       "height": H, "width": W, "selection": S, "register_layer": layer,
+                       "rejection": "none" if rej == sg.NO_REJEC else "winsorized",
+                       "parallelism": "1 GPU" if world == 1 else
+                       f"registration frame-sharded x{world} + stack row-band x{world}, RCCL gather"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "stack"},
+            "stage_ms": {"selection": round(stage[0] * 1e3, 3), "register": round(stage[1] * 1e3, 3),
+                         "stack": round(stage[2] * 1e3, 3), "stack_kernel": round(kavg, 3)},
+            "register_GBps_model": round(reg_bytes / stage[1] / 1e9, 1),
+            "register_shifts_exact": reg_ok,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            res["cpu_baseline"] = cpu_baseline_config(args, args.workload, N, C, H, W, S, layer)
+        print(json.dumps(res), flush=True)
+    ctx.close()
+    D.close()
+
+
+def main_sum(args):
+    """configs[0]: stack_summing of 16 x 1024^2 u16 mono FITS frames, end to end from the files
+    through the library's FITS region reader (sg_stack_u16, the drop-in host-pull path)"""
+    import tempfile
+    import numpy as np
+    import oracle_lib as orc
+    import sirilgpu as sg
+    from seq_files import write_fits
+    D = Dist()
+    N, C, H, W, M = 16, 1, 1024, 1024, 16
+    frames = orc.synth(N, C, H, W, seed=0xF175, maxshift=M)
+    sx, sy = orc.synth_shifts(N, seed=0xF175, maxshift=M)
+    ctx = sg.Context([0])
+    with tempfile.TemporaryDirectory() as tmp:
+        paths = []
+        for i in range(N):
+            p = os.path.join(tmp, f"light_{i + 1:05d}.fit")
+            write_fits(p, frames[i])
+            paths.append(p)
+        desc, keep = sg.make_desc(sg.SUM, N, W, H, C, shiftx=sx, shifty=sy)
+        with sg.Seq.open_fits(paths) as seq:
+            res_out = {}
+
+            def step():
+                rc, out, _, maxim = ctx.stack_seq(desc, seq)
+                assert rc == 0, ctx.error()
+                res_out["out"] = out
+
+            elapsed = timed(args.steps, args.warmup, step, D)
+    rc, ref, _ = orc.stack_sum(frames, sx, sy)
+    ok = bool(np.array_equal(res_out["out"], ref))
+    res = {
+        "metric": "frames/sec stacked (stack_summing, end to end from FITS files)",
+        "value": round(N / (elapsed / args.steps), 2), "unit": "frames/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u16",
+        "data": "synthetic frames written as FITS files (BITPIX 16, BZERO 32768) in a temporary directory",
+        "config": {"workload": f"stack_summing {N}x{H}x{W} u16 mono FITS (BASELINE configs[0]), host-pull from "
+                               f"files (reads + decode + PCIe + kernels)", "parallelism": "1 GPU"},
+        "matches_oracle": ok,
+    }
+    if not args.no_cpu_baseline:
+        _omp_threads(1)
+        t0 = time.perf_counter()
+        reps = 5
+        for _ in range(reps):
+            orc.stack_sum(frames, sx, sy)
+        dt = (time.perf_counter() - t0) / reps
+        res["cpu_baseline"] = {"value": round(N / dt, 2), "unit": "frames/s", "cores": 1, "kind": "port",
+                               "cpu_model": cpu_model(),
+                               "sample": f"oracle stack_summing (single thread, as the reference's :196-355), the "
+                                         f"same {N} frames RAM-resident ({reps} runs)"}
+    print(json.dumps(res), flush=True)
+    ctx.close()
+    D.close()
+
+
+def main():
+    args = parse()
+    if args.workload == "sigma":
+        return main_sigma(args)
+    if args.workload == "sum-fits":
+        return main_sum(args)
+    return main_config(args)
 
 
 if __name__ == "__main__":

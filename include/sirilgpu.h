@@ -208,6 +208,13 @@ int sg_warp_u16_device(sg_ctx *ctx, int dev_index, const uint16_t *d_in, int wid
 int sg_synth_fill_device(sg_ctx *ctx, int dev_index, uint16_t *d_frames, int nframes,
 		int nb_layers, int height, int width, int row_begin, int row_end, uint64_t seed,
 		int maxshift, int64_t frame_stride, void *stream);
+/* the same for frames [first_frame, first_frame + nframes) of the sequence, written from d_frames
+ * (a rank's block of a frame-sharded sequence), channel c at c * plane_stride (0 = height *
+ * width): row r of channel c of local frame f at d_frames[f*frame_stride + c*plane_stride + r*width]
+ * (a band-resident layout passes a base pointer biased by -row_begin*width) */
+int sg_synth_fill_frames_device(sg_ctx *ctx, int dev_index, uint16_t *d_frames, int first_frame,
+		int nframes, int nb_layers, int height, int width, int row_begin, int row_end, uint64_t seed,
+		int maxshift, int64_t frame_stride, int64_t plane_stride, void *stream);
 
 #ifdef __cplusplus
 }

@@ -11,6 +11,8 @@
 #   prof=NAME[:ARGS]            rocprofv3 --kernel-trace --stats of bench.py ARGS -> NAME/
 #   pmc=NAME[:ARGS]             FETCH_SIZE and WRITE_SIZE passes (own runs) -> NAME_traffic.json
 #   py=NAME:SCRIPT[:ARGS]       python SCRIPT ARGS -> NAME.log
+#   dist=NAME:NPROC[:ARGS]      bench.py under torchrun with NPROC ranks on this one GPU
+#                               (SG_BENCH_REHEARSE=1: gloo collectives; a rehearsal of the multi-GPU flow)
 # ARGS use ',' between words (bench=cfg1:--workload,register-mean).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
@@ -62,6 +64,12 @@ for step in "$@"; do
       done
       python3 scripts/pmc_traffic.py "$O/${name}_FETCH_SIZE" "$O/${name}_WRITE_SIZE" "${PMC_KERNEL:-k_stack_hist}" \
         "$O/${name}_traffic.json" || fail "pmc parse" ;;
+    dist)
+      name=${spec%%:*}; rest=${spec#*:}; np=${rest%%:*}; args=""; [ "$np" != "$rest" ] && args=${rest#*:}
+      SG_BENCH_REHEARSE=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$np" \
+        --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus "$np" ${args//,/ } > "$O/$name.log" 2>&1 \
+        || fail "dist $name" "$O/$name.log"
+      echo "$name: $(summary "$O/$name.log")" ;;
     py)
       name=${spec%%:*}; rest=${spec#*:}; script=${rest%%:*}; args=""; [ "$script" != "$rest" ] && args=${rest#*:}
       timeout -k 10 900 python -u "$script" ${args//,/ } > "$O/$name.log" 2>&1 || fail "py $name" "$O/$name.log"

@@ -38,8 +38,8 @@ __global__ void k_stack_reduce(SgStackParams p);
 __global__ void k_stack_reduce2(SgStackParams p);
 __global__ void k_sum_finalize(SgStackParams p);
 __global__ void k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *scratch, int phase);
-__global__ void k_synth_fill(uint16_t *frames, int nframes, int C, int H, int W, int row_begin,
-		int row_end, uint64_t seed, int maxshift, int64_t frame_stride);
+__global__ void k_synth_fill(uint16_t *frames, int first_frame, int nframes, int C, int H, int W, int row_begin,
+		int row_end, uint64_t seed, int maxshift, int64_t frame_stride, int64_t plane_stride);
 
 #include "sg_ctx.hpp"
 
@@ -867,18 +867,26 @@ extern "C" int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *d, sg_read_region_
 	return SG_OK;
 }
 
-extern "C" int sg_synth_fill_device(sg_ctx *ctx, int dev_index, uint16_t *d_frames, int nframes,
-		int nb_layers, int height, int width, int row_begin, int row_end, uint64_t seed,
-		int maxshift, int64_t frame_stride, void *stream) {
-	if (!ctx || dev_index < 0 || dev_index >= (int)ctx->dev.size())
+extern "C" int sg_synth_fill_frames_device(sg_ctx *ctx, int dev_index, uint16_t *d_frames, int first_frame,
+		int nframes, int nb_layers, int height, int width, int row_begin, int row_end, uint64_t seed,
+		int maxshift, int64_t frame_stride, int64_t plane_stride, void *stream) {
+	if (!ctx || dev_index < 0 || dev_index >= (int)ctx->dev.size() || first_frame < 0)
 		return SG_ERR_GENERIC;
 	SgDevice &dv = ctx->dev[dev_index];
 	HIPCHK(hipSetDevice(dv.id));
 	hipStream_t s = stream ? (hipStream_t)stream : dv.stream;
-	hipLaunchKernelGGL(k_synth_fill, dim3(8192), dim3(256), 0, s, d_frames, nframes, nb_layers,
+	hipLaunchKernelGGL(k_synth_fill, dim3(8192), dim3(256), 0, s, d_frames, first_frame, nframes, nb_layers,
 			height, width, row_begin, row_end, seed, maxshift,
-			frame_stride > 0 ? frame_stride : (int64_t)nb_layers * height * width);
+			frame_stride > 0 ? frame_stride : (int64_t)nb_layers * height * width,
+			plane_stride > 0 ? plane_stride : (int64_t)height * width);
 	HIPCHK(hipGetLastError());
 	HIPCHK(hipStreamSynchronize(s));
 	return SG_OK;
+}
+
+extern "C" int sg_synth_fill_device(sg_ctx *ctx, int dev_index, uint16_t *d_frames, int nframes,
+		int nb_layers, int height, int width, int row_begin, int row_end, uint64_t seed,
+		int maxshift, int64_t frame_stride, void *stream) {
+	return sg_synth_fill_frames_device(ctx, dev_index, d_frames, 0, nframes, nb_layers, height, width, row_begin,
+			row_end, seed, maxshift, frame_stride, 0, stream);
 }

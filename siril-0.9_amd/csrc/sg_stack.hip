@@ -1978,8 +1978,8 @@ k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *s
 #include "../../include/sg_synth.h"
 
 __global__ void __launch_bounds__(256)
-k_synth_fill(uint16_t *frames, int nframes, int C, int H, int W, int row_begin, int row_end,
-		uint64_t seed, int maxshift, int64_t frame_stride) {
+k_synth_fill(uint16_t *frames, int first_frame, int nframes, int C, int H, int W, int row_begin, int row_end,
+		uint64_t seed, int maxshift, int64_t frame_stride, int64_t plane_stride) {
 	const int nrows = row_end - row_begin;
 	const int64_t total = (int64_t)nframes * C * nrows * W;
 	for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
@@ -1991,7 +1991,8 @@ k_synth_fill(uint16_t *frames, int nframes, int C, int H, int W, int row_begin, 
 		const int c = (int)(t % C);
 		const int f = (int)(t / C);
 		const int R = row_begin + rr;
-		frames[(int64_t)f * frame_stride + ((int64_t)c * H + R) * W + x] = sg_synth_pixel(seed, f, c, R, x, maxshift);
+		frames[(int64_t)f * frame_stride + (int64_t)c * plane_stride + (int64_t)R * W + x] =
+			sg_synth_pixel(seed, first_frame + f, c, R, x, maxshift);
 	}
 }
 

@@ -118,6 +118,10 @@ def load():
                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                                          ctypes.c_int, ctypes.c_int64, P]
     lib.sg_synth_fill_device.restype = ctypes.c_int
+    lib.sg_synth_fill_frames_device.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_uint64, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, P]
+    lib.sg_synth_fill_frames_device.restype = ctypes.c_int
     lib.sg_register_dft_u16.argtypes = [P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, P]
     lib.sg_register_dft_u16.restype = ctypes.c_int
     lib.sg_register_dft_u16_device.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -534,10 +538,11 @@ class Context:
         return sx, sy, q
 
     def synth_fill(self, d_frames, nframes, C, H, W, row_begin, row_end, seed, maxshift, dev_index=0,
-                   frame_stride=0):
-        rc = self.lib.sg_synth_fill_device(self.ctx, dev_index, ctypes.c_void_p(d_frames), nframes, C, H, W,
-                                           row_begin, row_end, seed, maxshift, frame_stride, None)
-        self.check(rc, "sg_synth_fill_device")
+                   frame_stride=0, first_frame=0, plane_stride=0):
+        rc = self.lib.sg_synth_fill_frames_device(self.ctx, dev_index, ctypes.c_void_p(d_frames), first_frame, nframes,
+                                                  C, H, W, row_begin, row_end, seed, maxshift, frame_stride,
+                                                  plane_stride, None)
+        self.check(rc, "sg_synth_fill_frames_device")
 
 
 def compute_normalization(mode, location, scale, ref_image=0):

@@ -204,7 +204,7 @@ def test_cfg4_rgb_register_and_winsorized(gpu_ctx):
     gpu_ctx.stack_device(desc, frames.data_ptr(), C * H * W, H * W, out.data_ptr(), 0, H)
     img = out.cpu().numpy().view(np.uint16).reshape(C, H, W)
     for c in range(C):
-        for b, e in [(0, 32), (H // 2 - 16, H // 2 + 16), (H - 32, H)]:
+        for b, e in [(0, 64), (H // 2 - 32, H // 2 + 32), (H - 64, H)]:
             lo, hi = max(0, b - M), min(H, e + M)
             band = fv[:, c, lo:hi, :].cpu().numpy().view(np.uint16)[:, None]
             rc, ref, _ = orc.stack_rejection(band, sg.WINSORIZED, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
