@@ -139,6 +139,7 @@ typedef struct {
 	/* last registration: frames whose correlation maximum was a near tie, decided by exact
 	 * integer correlations / left to the FFT arg-max (more candidates than the cap) */
 	uint64_t reg_ties_resolved, reg_ties_unresolved;
+	uint64_t reg_fp64_reruns;	/* pairs of the fp32 passes re-run in fp64 (near ties at fp32 tolerance) */
 } sg_stack_stats;
 int sg_get_last_stats(const sg_ctx *ctx, sg_stack_stats *st);
 

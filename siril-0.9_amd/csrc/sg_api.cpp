@@ -83,7 +83,7 @@ extern "C" void sg_shutdown(sg_ctx *ctx) {
 		(void)hipSetDevice(d.id);
 		(void)hipStreamSynchronize(d.stream);
 		SgBuf *bufs[] = {&d.flag_list, &d.flag_map, &d.sum_buf, &d.scratch, &d.frames, &d.out, &d.reg_sel, &d.reg_spec,
-			&d.reg_work, &d.reg_tw, &d.reg_best, &d.reg_qbuf, &d.reg_qacc, &d.redo, &d.zeros,
+			&d.reg_work, &d.reg_tw, &d.reg_tw32, &d.reg_best, &d.reg_qbuf, &d.reg_qacc, &d.redo, &d.zeros,
 			&d.io_raw, &d.io_bad, &d.warp_tab, &d.stats_buf, &d.inb, &d.ctr};
 		for (SgBuf *b : bufs)
 			if (b->p)

@@ -23,7 +23,7 @@ struct SgDevice {
 	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 	SgBuf flag_list, flag_map, sum_buf, scratch, frames, out, stats_buf;
 	/* registration workspaces (sg_register.hip) */
-	SgBuf reg_sel, reg_spec, reg_work, reg_tw, reg_best, reg_qbuf, reg_qacc;
+	SgBuf reg_sel, reg_spec, reg_work, reg_tw, reg_tw32, reg_best, reg_qbuf, reg_qacc;
 	SgBuf redo;	/* redo list of the histogram stacking path */
 	SgBuf zeros;	/* zero page for out-of-frame sample loads */
 	/* stacking call inputs (shift table, normalisation coefficients, chain tables) packed into
@@ -76,6 +76,8 @@ struct SgKnobs {
 	int reg_path = 2;		/* SG_REG_PATH: registration pass order 0 / 1 / 2, 3 = the generic passes */
 	int reg_xcd = 1;		/* SG_REG_XCD: 0 = column strips in dispatch order */
 	int reg_pb = 1;			/* SG_REG_PB: pairs per strip block of the fused column pass (1 = pair-major) */
+	int reg_fp = 32;		/* SG_REG_FP: 32 = fp32 half-spectrum passes, near ties re-run in fp64; 64 = fp64 only */
+	int reg_cw32 = 4;		/* SG_REG_CW32: columns per strip of the fp32 column pass (4: 32-B row segments, no spill; 8: 64-B segments, 16 elements per thread) */
 	void read() {
 		hist_dbg = sg_env_int("SG_HIST_DBG", 0, 1000, 0);
 		hist_prio = sg_env_int("SG_HIST_PRIO", 0, 3, 1);
@@ -94,6 +96,8 @@ struct SgKnobs {
 		reg_path = sg_env_int("SG_REG_PATH", 0, 3, 2);
 		reg_xcd = sg_env_int("SG_REG_XCD", 0, 1, 1);
 		reg_pb = sg_env_int("SG_REG_PB", 1, 64, 1);
+		reg_fp = sg_env_int("SG_REG_FP", 32, 64, 32) == 64 ? 64 : 32;
+		reg_cw32 = sg_env_int("SG_REG_CW32", 1, 16, 4);
 	}
 };
 

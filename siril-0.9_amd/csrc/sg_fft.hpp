@@ -30,32 +30,49 @@ __device__ __forceinline__ int sg_pad(int i) {
 }
 #define SG_PADN(n) ((n) + ((n) >> 3))
 
-__device__ __forceinline__ sg_c64 sg_cmul(sg_c64 a, sg_c64 b) {
-	return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+/* complex arithmetic for C = double2 (the default, every path) or float2 (the fp32 power-of-two
+ * passes, whose near ties are re-run in fp64) */
+template <class C> struct SgReal;
+template <> struct SgReal<double2> { typedef double T; };
+template <> struct SgReal<float2> { typedef float T; };
+template <class C>
+__device__ __forceinline__ C sg_mk(typename SgReal<C>::T x, typename SgReal<C>::T y) {
+	C r;
+	r.x = x;
+	r.y = y;
+	return r;
 }
-__device__ __forceinline__ sg_c64 sg_cadd(sg_c64 a, sg_c64 b) {
-	return make_double2(a.x + b.x, a.y + b.y);
+template <class C>
+__device__ __forceinline__ C sg_cmul(C a, C b) {
+	return sg_mk<C>(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
-__device__ __forceinline__ sg_c64 sg_csub(sg_c64 a, sg_c64 b) {
-	return make_double2(a.x - b.x, a.y - b.y);
+template <class C>
+__device__ __forceinline__ C sg_cadd(C a, C b) {
+	return sg_mk<C>(a.x + b.x, a.y + b.y);
+}
+template <class C>
+__device__ __forceinline__ C sg_csub(C a, C b) {
+	return sg_mk<C>(a.x - b.x, a.y - b.y);
 }
 /* multiply by -i (forward) or +i (inverse) */
-__device__ __forceinline__ sg_c64 sg_mul_mi(sg_c64 a, bool inv) {
-	return inv ? make_double2(-a.y, a.x) : make_double2(a.y, -a.x);
+template <class C>
+__device__ __forceinline__ C sg_mul_mi(C a, bool inv) {
+	return inv ? sg_mk<C>(-a.y, a.x) : sg_mk<C>(a.y, -a.x);
 }
 
 /* in-register DFT of R = 2, 4, 8 points (natural order in and out) */
-template <int R, int RV>
-__device__ __forceinline__ void sg_dft_small(sg_c64 (&v)[RV], bool inv) {
+template <int R, int RV, class C>
+__device__ __forceinline__ void sg_dft_small(C (&v)[RV], bool inv) {
+	typedef typename SgReal<C>::T T;
 	if constexpr (R == 2) {
-		const sg_c64 a = v[0], b = v[1];
+		const C a = v[0], b = v[1];
 		v[0] = sg_cadd(a, b);
 		v[1] = sg_csub(a, b);
 		return;
 	}
 	else if constexpr (R == 4) {
-		const sg_c64 a0 = sg_cadd(v[0], v[2]), a1 = sg_csub(v[0], v[2]);
-		const sg_c64 b0 = sg_cadd(v[1], v[3]), b1 = sg_mul_mi(sg_csub(v[1], v[3]), inv);
+		const C a0 = sg_cadd(v[0], v[2]), a1 = sg_csub(v[0], v[2]);
+		const C b0 = sg_cadd(v[1], v[3]), b1 = sg_mul_mi(sg_csub(v[1], v[3]), inv);
 		v[0] = sg_cadd(a0, b0);
 		v[2] = sg_csub(a0, b0);
 		v[1] = sg_cadd(a1, b1);
@@ -63,22 +80,22 @@ __device__ __forceinline__ void sg_dft_small(sg_c64 (&v)[RV], bool inv) {
 		return;
 	} else {
 	/* R = 8: radix-2 DIF into two 4-point DFTs */
-	const double h = 0.70710678118654752440;
-	sg_c64 e[4], o[4];
+	const T h = (T)0.70710678118654752440;
+	C e[4], o[4];
 #pragma unroll
 	for (int k = 0; k < 4; k++) {
 		e[k] = sg_cadd(v[k], v[k + 4]);
 		o[k] = sg_csub(v[k], v[k + 4]);
 	}
 	/* o[k] *= W8^k */
-	o[1] = inv ? make_double2(h * (o[1].x - o[1].y), h * (o[1].x + o[1].y))
-		   : make_double2(h * (o[1].x + o[1].y), h * (o[1].y - o[1].x));
+	o[1] = inv ? sg_mk<C>(h * (o[1].x - o[1].y), h * (o[1].x + o[1].y))
+		   : sg_mk<C>(h * (o[1].x + o[1].y), h * (o[1].y - o[1].x));
 	o[2] = sg_mul_mi(o[2], inv);
-	o[3] = inv ? make_double2(-h * (o[3].x + o[3].y), h * (o[3].x - o[3].y))
-		   : make_double2(h * (o[3].y - o[3].x), -h * (o[3].x + o[3].y));
+	o[3] = inv ? sg_mk<C>(-h * (o[3].x + o[3].y), h * (o[3].x - o[3].y))
+		   : sg_mk<C>(h * (o[3].y - o[3].x), -h * (o[3].x + o[3].y));
 	sg_dft_small<4>(e, inv);
 	sg_dft_small<4>(o, inv);
-	const sg_c64 *E = e, *O = o;
+	const C *E = e, *O = o;
 #pragma unroll
 	for (int k = 0; k < 4; k++) {
 		v[2 * k] = E[k];
@@ -90,16 +107,17 @@ __device__ __forceinline__ void sg_dft_small(sg_c64 (&v)[RV], bool inv) {
 /* tw holds the full circle twice: tw[k] = exp(-2 pi i k / n) and tw[n + k] = its conjugate
  * (the inverse), k < n, built on the host from the half-circle values by exact negation /
  * conjugation, so a twiddle is one load with no select (the direction is uniform) */
-__device__ __forceinline__ sg_c64 sg_twiddle(const sg_c64 *__restrict__ tw, int n, int k, bool inv) {
+template <class C>
+__device__ __forceinline__ C sg_twiddle(const C *__restrict__ tw, int n, int k, bool inv) {
 	return (inv ? tw + n : tw)[k];
 }
 
-template <int R>
-__device__ __forceinline__ void sg_stockham_pass(sg_c64 *buf, int n, int nb, int bstride, int Ns,
-		const sg_c64 *__restrict__ tw, bool inv) {
-	constexpr int MAXI = 8 / R;	/* work items per thread: nb * n <= 8 * blockDim (host-sized launches) */
+template <int R, int EPT = 8, class C>
+__device__ __forceinline__ void sg_stockham_pass(C *buf, int n, int nb, int bstride, int Ns,
+		const C *__restrict__ tw, bool inv) {
+	constexpr int MAXI = EPT / R;	/* work items per thread: nb * n <= EPT * blockDim (host-sized launches) */
 	const int per = n / R, items = nb * per;
-	sg_c64 v[MAXI][R], w[MAXI][R];
+	C v[MAXI][R], w[MAXI][R];
 	const bool twiddled = Ns > 1;	/* the first pass (Ns = 1) multiplies by w^0 = 1 only */
 	/* load every item's R inputs before anyone stores (in-place pass); the twiddles are
 	 * fetched here too, so their latency overlaps the barrier wait */
@@ -108,7 +126,7 @@ __device__ __forceinline__ void sg_stockham_pass(sg_c64 *buf, int n, int nb, int
 		const int t = threadIdx.x + it * blockDim.x;
 		if (t < items) {
 			const int b = t / per, j = t - b * per;
-			const sg_c64 *x = buf + (size_t)b * bstride;
+			const C *x = buf + (size_t)b * bstride;
 #pragma unroll
 			for (int r = 0; r < R; r++)
 				v[it][r] = x[sg_pad(j + r * per)];
@@ -134,7 +152,7 @@ __device__ __forceinline__ void sg_stockham_pass(sg_c64 *buf, int n, int nb, int
 					v[it][r] = sg_cmul(v[it][r], w[it][r]);
 			}
 			sg_dft_small<R, R>(v[it], inv);
-			sg_c64 *y = buf + (size_t)b * bstride;
+			C *y = buf + (size_t)b * bstride;
 			const int base = (j - jm) * R + jm;
 #pragma unroll
 			for (int r = 0; r < R; r++)
@@ -144,7 +162,8 @@ __device__ __forceinline__ void sg_stockham_pass(sg_c64 *buf, int n, int nb, int
 	__syncthreads();
 }
 
-__device__ __forceinline__ void sg_lds_fft(sg_c64 *buf, int n, int logn, int nb, int bstride, const sg_c64 *__restrict__ tw,
+template <int EPT = 8, class C>
+__device__ __forceinline__ void sg_lds_fft(C *buf, int n, int logn, int nb, int bstride, const C *__restrict__ tw,
 		bool inverse) {
 	(void)logn;
 	__syncthreads();
@@ -152,13 +171,13 @@ __device__ __forceinline__ void sg_lds_fft(sg_c64 *buf, int n, int logn, int nb,
 	while (Ns < n) {
 		const int rem = n / Ns;
 		if (rem >= 8) {
-			sg_stockham_pass<8>(buf, n, nb, bstride, Ns, tw, inverse);
+			sg_stockham_pass<8, EPT>(buf, n, nb, bstride, Ns, tw, inverse);
 			Ns *= 8;
 		} else if (rem == 4) {
-			sg_stockham_pass<4>(buf, n, nb, bstride, Ns, tw, inverse);
+			sg_stockham_pass<4, EPT>(buf, n, nb, bstride, Ns, tw, inverse);
 			Ns *= 4;
 		} else {
-			sg_stockham_pass<2>(buf, n, nb, bstride, Ns, tw, inverse);
+			sg_stockham_pass<2, EPT>(buf, n, nb, bstride, Ns, tw, inverse);
 			Ns *= 2;
 		}
 	}
@@ -175,37 +194,46 @@ __device__ __forceinline__ void sg_lds_fft(sg_c64 *buf, int n, int logn, int nb,
  * the first pass loads everything before anyone stores.  A st that writes element i back
  * to its own slot is race-free as is: the last pass's thread reads exactly the slots it
  * writes. */
-template <bool LDS_IN = false, class LD, class ST>
-__device__ __forceinline__ void sg_fft_io(sg_c64 *buf, int n, int nb, int bstride, const sg_c64 *__restrict__ tw,
+template <bool LDS_IN = false, int EPT = 8, class C, class LD, class ST>
+__device__ __forceinline__ void sg_fft_io(C *buf, int n, int nb, int bstride, const C *__restrict__ tw,
 		bool inv, LD ld, ST st) {
 	if (n < 16) {
 		for (int t = threadIdx.x; t < nb * n; t += blockDim.x)
 			buf[(size_t)(t % nb) * bstride + sg_pad(t / nb)] = ld(t % nb, t / nb);
-		sg_lds_fft(buf, n, 0, nb, bstride, tw, inv);
+		sg_lds_fft<EPT>(buf, n, 0, nb, bstride, tw, inv);
 		for (int t = threadIdx.x; t < nb * n; t += blockDim.x)
 			st(t % nb, t / nb, buf[(size_t)(t % nb) * bstride + sg_pad(t / nb)]);
 		return;
 	}
-	/* first pass: radix 8, Ns = 1 (no twiddles) */
+	/* first pass: radix 8, Ns = 1 (no twiddles); EPT / 8 items per thread, all loaded before
+	 * any is stored */
 	{
+		constexpr int FI = EPT / 8;
 		const int per = n >> 3, items = nb * per;
-		const int t = threadIdx.x;
-		const bool act = t < items;
-		const int b = act ? t % nb : 0, j = act ? t / nb : 0;
-		sg_c64 v[8];
-		if (act) {
+		C v[FI][8];
 #pragma unroll
-			for (int r = 0; r < 8; r++)
-				v[r] = ld(b, j + r * per);
+		for (int it = 0; it < FI; it++) {
+			const int t = threadIdx.x + it * blockDim.x;
+			if (t < items) {
+				const int b = t % nb, j = t / nb;
+#pragma unroll
+				for (int r = 0; r < 8; r++)
+					v[it][r] = ld(b, j + r * per);
+			}
 		}
 		if (LDS_IN)
 			__syncthreads();
-		if (act) {
-			sg_dft_small<8, 8>(v, inv);
-			sg_c64 *y = buf + (size_t)b * bstride;
 #pragma unroll
-			for (int r = 0; r < 8; r++)
-				y[sg_pad(j * 8 + r)] = v[r];
+		for (int it = 0; it < FI; it++) {
+			const int t = threadIdx.x + it * blockDim.x;
+			if (t < items) {
+				const int b = t % nb, j = t / nb;
+				sg_dft_small<8, 8>(v[it], inv);
+				C *y = buf + (size_t)b * bstride;
+#pragma unroll
+				for (int r = 0; r < 8; r++)
+					y[sg_pad(j * 8 + r)] = v[it][r];
+			}
 		}
 	}
 	__syncthreads();
@@ -213,21 +241,21 @@ __device__ __forceinline__ void sg_fft_io(sg_c64 *buf, int n, int nb, int bstrid
 	/* middle passes in LDS (sg_lds_fft's radix sequence: 8 while n / Ns >= 8, then 4 or 2),
 	 * leaving the last one */
 	while (n / Ns > 8) {
-		sg_stockham_pass<8>(buf, n, nb, bstride, Ns, tw, inv);
+		sg_stockham_pass<8, EPT>(buf, n, nb, bstride, Ns, tw, inv);
 		Ns *= 8;
 	}
 	const int rl = n / Ns;
 	auto last = [&](auto RC) {
 		constexpr int R = decltype(RC)::value;
-		constexpr int MAXI = 8 / R;
+		constexpr int MAXI = EPT / R;
 		const int per = n / R, items = nb * per;
 #pragma unroll
 		for (int it = 0; it < MAXI; it++) {
 			const int t = threadIdx.x + it * blockDim.x;
 			if (t < items) {
 				const int b = t % nb, j = t / nb;
-				const sg_c64 *x = buf + (size_t)b * bstride;
-				sg_c64 v[R];
+				const C *x = buf + (size_t)b * bstride;
+				C v[R];
 #pragma unroll
 				for (int r = 0; r < R; r++)
 					v[r] = x[sg_pad(j + r * per)];

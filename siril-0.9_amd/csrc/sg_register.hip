@@ -70,17 +70,17 @@ __device__ __forceinline__ int sg_xcd_strip(int id, int n, int xcdmap) {
 }
 
 /* column pass (forward or inverse) over strips of CW adjacent columns */
+template <class C, int EPT = 8>
 __global__ void __launch_bounds__(1024)
-k_reg_cols(sg_c64 *__restrict__ work, int S, int logS, int CW, const sg_c64 *__restrict__ tw, int inverse,
-		int xcdmap) {
+k_reg_cols(C *__restrict__ work, int S, int logS, int CW, const C *__restrict__ tw, int inverse, int xcdmap) {
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-	sg_c64 *buf = (sg_c64 *)smem;
+	C *buf = (C *)smem;
 	const int x0 = sg_xcd_strip(blockIdx.x, gridDim.x, xcdmap) * CW, pair = blockIdx.y;
 	const int bstride = SG_PADN(S) + 1;
-	sg_c64 *base = work + (size_t)pair * S * S + x0;
+	C *base = work + (size_t)pair * S * S + x0;
 	(void)logS;
-	sg_fft_io(buf, S, CW, bstride, tw, inverse != 0, [&](int c, int r) { return base[(size_t)r * S + c]; },
-			[&](int c, int r, sg_c64 v) { base[(size_t)r * S + c] = v; });
+	sg_fft_io<false, EPT>(buf, S, CW, bstride, tw, inverse != 0, [&](int c, int r) { return base[(size_t)r * S + c]; },
+			[&](int c, int r, C v) { base[(size_t)r * S + c] = v; });
 }
 
 /* one term of the packed cross-power spectrum at (ky, kx): zk = Z(ky, kx),
@@ -228,36 +228,38 @@ k_reg_cols_inv_argmax(const sg_c64 *__restrict__ work, int S, int logS, int CW, 
  * Same unnormalised FFTW_BACKWARD result as the full complex transforms; plane traffic per
  * pair 84 B per pixel instead of 116.
  * ------------------------------------------------------------------------------------- */
+template <class C>
 __global__ void __launch_bounds__(512)
 k_reg_rows_fwd_half(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const int *__restrict__ fb,
-		int S, const sg_c64 *__restrict__ tw, sg_c64 *__restrict__ work, unsigned long long *__restrict__ energy) {
+		int S, const C *__restrict__ tw, C *__restrict__ work, unsigned long long *__restrict__ energy) {
+	typedef typename SgReal<C>::T T;
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-	sg_c64 *buf = (sg_c64 *)smem;
+	C *buf = (C *)smem;
 	const int row = blockIdx.x, pair = blockIdx.y, H = S >> 1;
 	const size_t plane = (size_t)S * S;
 	const uint16_t *pa = sel + (size_t)fa[pair] * plane + (size_t)row * S;
 	const int b = fb[pair];
 	const uint16_t *pb = b >= 0 ? sel + (size_t)b * plane + (size_t)row * S : nullptr;
-	sg_c64 *out = work + (size_t)pair * plane + (size_t)row * S;
+	C *out = work + (size_t)pair * plane + (size_t)row * S;
 	unsigned long long ea = 0, eb = 0;
 	sg_fft_io(buf, S, 1, S, tw, false,
 			[&](int, int i) {
 				const unsigned int va = pa[i], vb = pb ? pb[i] : 0u;
 				ea += (unsigned long long)(va * va);
 				eb += (unsigned long long)(vb * vb);
-				return make_double2((double)va, (double)vb);
+				return sg_mk<C>((T)va, (T)vb);
 			},
-			[&](int, int i, sg_c64 v) { buf[sg_pad(i)] = v; });
+			[&](int, int i, C v) { buf[sg_pad(i)] = v; });
 	sg_energy_add(ea, eb, fa[pair], b, energy);	/* its __syncthreads also orders the LDS writes */
 	for (int k = threadIdx.x; k < H; k += blockDim.x) {
-		const sg_c64 zk = buf[sg_pad(k)], zm = buf[sg_pad(k ? S - k : H)];
-		sg_c64 A, B;
+		const C zk = buf[sg_pad(k)], zm = buf[sg_pad(k ? S - k : H)];
+		C A, B;
 		if (k == 0) {
-			A = make_double2(zk.x, zm.x);	/* A(0) + i A(S/2) */
-			B = make_double2(zk.y, zm.y);
+			A = sg_mk<C>(zk.x, zm.x);	/* A(0) + i A(S/2) */
+			B = sg_mk<C>(zk.y, zm.y);
 		} else {
-			A = make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
-			B = make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x));
+			A = sg_mk<C>((T)0.5 * (zk.x + zm.x), (T)0.5 * (zk.y - zm.y));
+			B = sg_mk<C>((T)0.5 * (zk.y + zm.y), (T)-0.5 * (zk.x - zm.x));
 		}
 		out[k] = A;
 		out[H + k] = B;
@@ -265,18 +267,20 @@ k_reg_rows_fwd_half(const uint16_t *__restrict__ sel, const int *__restrict__ fa
 }
 
 /* R conj F */
-__device__ __forceinline__ sg_c64 sg_rconj(sg_c64 r, sg_c64 f) {
-	return make_double2(r.x * f.x + r.y * f.y, r.y * f.x - r.x * f.y);
+template <class C>
+__device__ __forceinline__ C sg_rconj(C r, C f) {
+	return sg_mk<C>(r.x * f.x + r.y * f.y, r.y * f.x - r.x * f.y);
 }
 
 /* The reference-spectrum loads of all 8 cross-power items of a thread are issued together
  * (launches are sized so that CW * S = 8 * blockDim, thr_for).  Issuing them before the
  * forward FFT instead spills (128 VGPRs at 4 waves per SIMD). */
+template <class C, int EPT = 8>
 __global__ void __launch_bounds__(1024)
-k_reg_cols_xpower(sg_c64 *__restrict__ work, const sg_c64 *__restrict__ spec, int S, int CW,
-		const sg_c64 *__restrict__ tw, int xcdmap, int pb) {
+k_reg_cols_xpower(C *__restrict__ work, const C *__restrict__ spec, int S, int CW,
+		const C *__restrict__ tw, int xcdmap, int pb) {
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-	sg_c64 *buf = (sg_c64 *)smem;
+	C *buf = (C *)smem;
 	int x0 = sg_xcd_strip(blockIdx.x, gridDim.x, xcdmap) * CW, pair = blockIdx.y;
 	/* pb > 1: blocks of pb pairs per strip dispatched back to back on one XCD (strip-major
 	 * inside a pair block), so the strip's reference-spectrum columns are read from HBM once per
@@ -289,18 +293,19 @@ k_reg_cols_xpower(sg_c64 *__restrict__ work, const sg_c64 *__restrict__ spec, in
 		pair = (local / (pb * s8)) * pb + local % pb;
 		x0 = strip * CW;
 	}
+	typedef typename SgReal<C>::T T;
 	const int bstride = SG_PADN(S) + 1, H = S >> 1;
-	sg_c64 *base = work + (size_t)pair * S * S + x0;
-	auto slot = [&](int c, int r) -> sg_c64 & { return buf[(size_t)c * bstride + sg_pad(r)]; };
-	constexpr int NI = 8;
+	C *base = work + (size_t)pair * S * S + x0;
+	auto slot = [&](int c, int r) -> C & { return buf[(size_t)c * bstride + sg_pad(r)]; };
+	constexpr int NI = EPT;
 	const int items = CW * S;
-	sg_c64 rk[NI], rm[NI];
+	C rk[NI], rm[NI];
 	auto fetch = [&]() {
 #pragma unroll
 		for (int it = 0; it < NI; it++) {
 			const int t = threadIdx.x + it * blockDim.x;
-			rk[it] = make_double2(0.0, 0.0);
-			rm[it] = make_double2(0.0, 0.0);
+			rk[it] = sg_mk<C>((T)0, (T)0);
+			rm[it] = sg_mk<C>((T)0, (T)0);
 			if (t < items) {
 				const int c = t % CW, ky = t / CW, kx = (x0 + c) & (H - 1);
 				rk[it] = spec[(size_t)ky * S + kx];
@@ -309,8 +314,8 @@ k_reg_cols_xpower(sg_c64 *__restrict__ work, const sg_c64 *__restrict__ spec, in
 			}
 		}
 	};
-	sg_fft_io(buf, S, CW, bstride, tw, false, [&](int c, int r) { return base[(size_t)r * S + c]; },
-			[&](int c, int r, sg_c64 v) { slot(c, r) = v; });
+	sg_fft_io<false, EPT>(buf, S, CW, bstride, tw, false, [&](int c, int r) { return base[(size_t)r * S + c]; },
+			[&](int c, int r, C v) { slot(c, r) = v; });
 	fetch();
 	__syncthreads();
 #pragma unroll
@@ -328,19 +333,19 @@ k_reg_cols_xpower(sg_c64 *__restrict__ work, const sg_c64 *__restrict__ spec, in
 		const int m = (S - ky) & (S - 1);
 		if (m < ky)
 			continue;
-		const sg_c64 zk = slot(c, ky), zm = slot(c, m), r1 = rk[it], r2 = rm[it];
-		const sg_c64 f0 = make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
-		const sg_c64 fn = make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x));
-		const sg_c64 r0 = make_double2(0.5 * (r1.x + r2.x), 0.5 * (r1.y - r2.y));
-		const sg_c64 rn = make_double2(0.5 * (r1.y + r2.y), -0.5 * (r1.x - r2.x));
-		const sg_c64 p0 = sg_rconj(r0, f0), pn = sg_rconj(rn, fn);
-		slot(c, ky) = make_double2(p0.x - pn.y, p0.y + pn.x);
+		const C zk = slot(c, ky), zm = slot(c, m), r1 = rk[it], r2 = rm[it];
+		const C f0 = sg_mk<C>((T)0.5 * (zk.x + zm.x), (T)0.5 * (zk.y - zm.y));
+		const C fn = sg_mk<C>((T)0.5 * (zk.y + zm.y), (T)-0.5 * (zk.x - zm.x));
+		const C r0 = sg_mk<C>((T)0.5 * (r1.x + r2.x), (T)0.5 * (r1.y - r2.y));
+		const C rn = sg_mk<C>((T)0.5 * (r1.y + r2.y), (T)-0.5 * (r1.x - r2.x));
+		const C p0 = sg_rconj(r0, f0), pn = sg_rconj(rn, fn);
+		slot(c, ky) = sg_mk<C>(p0.x - pn.y, p0.y + pn.x);
 		if (m != ky)	/* P0(-k) = conj P0(k), PN(-k) = conj PN(k) */
-			slot(c, m) = make_double2(p0.x + pn.y, pn.x - p0.y);
+			slot(c, m) = sg_mk<C>(p0.x + pn.y, pn.x - p0.y);
 	}
 	__syncthreads();
-	sg_fft_io<true>(buf, S, CW, bstride, tw, true, [&](int c, int r) { return slot(c, r); },
-			[&](int c, int r, sg_c64 v) { base[(size_t)r * S + c] = v; });
+	sg_fft_io<true, EPT>(buf, S, CW, bstride, tw, true, [&](int c, int r) { return slot(c, r); },
+			[&](int c, int r, C v) { base[(size_t)r * S + c] = v; });
 }
 
 /* per-pair result of a registration batch (frame a = the real part, frame b = the imaginary) */
@@ -351,20 +356,22 @@ struct SgRegOut {
 	double v[2], v2[2], thr[2];	/* maximum, runner-up, max - tol */
 };
 
-/* tolerance of a correlation value: 2^-32 S^2 ||ref|| ||img|| (the unnormalised inverse scales
- * the exact correlation sum_n ref(n+k) img(n) by S^2, and by Cauchy-Schwarz no entry exceeds
- * S^2 ||ref|| ||img||); fp64 FFT rounding of the three transforms stays many orders of
- * magnitude below it, so a maximum that beats every other entry by more than tol is the
- * exact maximum */
-__device__ __forceinline__ double sg_reg_tol(int S, unsigned long long eref, unsigned long long eimg) {
-	return ldexp((double)S * (double)S * sqrt((double)eref) * sqrt((double)eimg), -32);
+/* tolerance of a correlation value: 2^tol_exp S^2 ||ref|| ||img|| (the unnormalised inverse
+ * scales the exact correlation sum_n ref(n+k) img(n) by S^2, and by Cauchy-Schwarz no entry
+ * exceeds S^2 ||ref|| ||img||).  fp64 passes: 2^-32, many orders of magnitude above their
+ * rounding; fp32 passes: 2^-15 = 3.1e-5, against a measured worst error of 2.8e-7 of that scale
+ * at S = 2048 (scipy's complex64 FFT, the synthetic pair) and a log2(S^2) eps32 bound of 1.3e-6
+ * per transform.  A maximum that beats every other entry by more than tol is the exact
+ * maximum. */
+__device__ __forceinline__ double sg_reg_tol(int S, unsigned long long eref, unsigned long long eimg, int tol_exp) {
+	return ldexp((double)S * (double)S * sqrt((double)eref) * sqrt((double)eimg), tol_exp);
 }
 
 /* per pair: reduce the row / strip partials in order, convert to (shiftx, shifty) (:344-351),
  * flag near ties against the frames' energies */
 __global__ void __launch_bounds__(256)
 k_reg_final(const SgBest *__restrict__ best, int S, int count, const int *__restrict__ fa,
-		const int *__restrict__ fb, int ref, const unsigned long long *__restrict__ energy,
+		const int *__restrict__ fb, int ref, const unsigned long long *__restrict__ energy, int tol_exp,
 		SgRegOut *__restrict__ out) {
 	__shared__ SgBest red[4];
 	const int pair = blockIdx.x;
@@ -392,7 +399,7 @@ k_reg_final(const SgBest *__restrict__ best, int S, int count, const int *__rest
 			o.idx[k] = t[k].i;
 			o.v[k] = t[k].v;
 			o.v2[k] = t[k].v2;
-			const double tol = fr[k] >= 0 ? sg_reg_tol(S, energy[ref], energy[fr[k]]) : 0.0;
+			const double tol = fr[k] >= 0 ? sg_reg_tol(S, energy[ref], energy[fr[k]], tol_exp) : 0.0;
 			o.thr[k] = t[k].v - tol;
 			o.amb[k] = fr[k] >= 0 && !(t[k].v - t[k].v2 > tol);
 		}
@@ -402,15 +409,16 @@ k_reg_final(const SgBest *__restrict__ best, int S, int count, const int *__rest
 
 /* CAND: instead of the arg-max, append every index whose correlation reaches the pair's
  * threshold (SgRegOut::thr, near ties only) to the candidate list of its frame */
-template <bool CAND>
+template <class C, bool CAND>
 __global__ void __launch_bounds__(512)
-k_reg_rows_inv_half_argmax(const sg_c64 *__restrict__ work, int S, const sg_c64 *__restrict__ tw,
+k_reg_rows_inv_half_argmax(const C *__restrict__ work, int S, const C *__restrict__ tw,
 		SgBest *__restrict__ best, const SgRegOut *__restrict__ res, SgCand *__restrict__ cand) {
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-	sg_c64 *buf = (sg_c64 *)smem;
+	C *buf = (C *)smem;
 	__shared__ SgBest red[8];
 	const int row = blockIdx.x, pair = blockIdx.y, H = S >> 1;
-	const sg_c64 *in = work + (size_t)pair * S * S + (size_t)row * S;
+	const C *in = work + (size_t)pair * S * S + (size_t)row * S;
+	typedef typename SgReal<C>::T T;
 	SgTop2 ta, tb;
 	sg_top2_init(ta);
 	sg_top2_init(tb);
@@ -424,22 +432,22 @@ k_reg_rows_inv_half_argmax(const sg_c64 *__restrict__ work, int S, const sg_c64 
 	}
 	sg_fft_io(buf, S, 1, S, tw, true,
 			[&](int, int i) {
-				sg_c64 qa, qb;
+				C qa, qb;
 				if ((i & (H - 1)) == 0) {	/* kx = 0 or S/2: the packed real pair */
-					const sg_c64 a = in[0], b = in[H];
-					qa = make_double2(i ? a.y : a.x, 0.0);
-					qb = make_double2(i ? b.y : b.x, 0.0);
+					const C a = in[0], b = in[H];
+					qa = sg_mk<C>(i ? a.y : a.x, (T)0);
+					qb = sg_mk<C>(i ? b.y : b.x, (T)0);
 				} else if (i < H) {
 					qa = in[i];
 					qb = in[H + i];
 				} else {
-					const sg_c64 a = in[S - i], b = in[H + S - i];
-					qa = make_double2(a.x, -a.y);
-					qb = make_double2(b.x, -b.y);
+					const C a = in[S - i], b = in[H + S - i];
+					qa = sg_mk<C>(a.x, -a.y);
+					qb = sg_mk<C>(b.x, -b.y);
 				}
-				return make_double2(qa.x - qb.y, qa.y + qb.x);
+				return sg_mk<C>(qa.x - qb.y, qa.y + qb.x);
 			},
-			[&](int, int j, sg_c64 c) {
+			[&](int, int j, C c) {
 				const int idx = row * S + j;
 				if (CAND) {
 					sg_cand_push(cand + 2 * pair, c.x, thr[0], idx);
@@ -1134,7 +1142,7 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	const bool fused = !generic && path == 1;
 	const bool half = !generic && path == 2;
 	const bool resolvable = generic || half;	/* paths with a candidate pass */
-	ctx->stats.reg_ties_resolved = ctx->stats.reg_ties_unresolved = 0;
+	ctx->stats.reg_ties_resolved = ctx->stats.reg_ties_unresolved = ctx->stats.reg_fp64_reruns = 0;
 
 	/* frames to register, in index order (the reference skips ref and excluded frames) */
 	std::vector<int> todo;
@@ -1208,10 +1216,17 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	if (rc)
 		return rc;
 
-	/* pairs per launch: up to 2 GB of pair planes (32 at S = 2048 on the half path). Half-
-	 * spectrum passes, configs[1]: 32 or 64 pairs 8.95-9.07 ms, 16: 9.08, 4: 9.22-9.32, 2:
-	 * 9.02-9.15, 1: 9.8 ms of registration (round-2 gpu_regbatch.sh) */
-	const size_t pair_bytes = plane * sizeof(sg_c64) * (generic ? 2 : 1);	/* generic: + transposed plane */
+	/* precision of the main passes: the power-of-two half-spectrum passes run in fp32
+	 * (SG_REG_FP=32, default: half the plane bytes and LDS), and a pair whose correlation
+	 * maximum is a near tie at fp32 tolerance is re-run in fp64 (the arg-max is then exactly
+	 * the fp64 one wherever fp64 is not itself near a tie; those go to the exact integer
+	 * correlations).  The other pass orders and the generic path are fp64. */
+	const bool fp32 = half && ctx->knobs.reg_fp == 32;
+	const size_t esz = fp32 ? sizeof(float2) : sizeof(sg_c64);
+	/* pairs per launch: up to 2 GB of pair planes (32 at S = 2048 on the fp64 half path).
+	 * Half-spectrum passes, configs[1]: 32 or 64 pairs 8.95-9.07 ms, 16: 9.08, 4: 9.22-9.32,
+	 * 2: 9.02-9.15, 1: 9.8 ms of registration (round-2 gpu_regbatch.sh) */
+	const size_t pair_bytes = plane * esz * (generic ? 2 : 1);	/* generic: + transposed plane */
 	int B = (int)((size_t)(2048u << 20) / pair_bytes);
 	if (B < 1)
 		B = 1;
@@ -1222,7 +1237,10 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	const int npairs_total = (int)(todo.size() + 1) / 2;
 	if (B > npairs_total && npairs_total > 0)
 		B = npairs_total;
-	const size_t row_lds = (size_t)SG_PADN(S) * sizeof(sg_c64);
+	const int Bc = B > 1 ? B : 1;
+	/* fp64 re-runs of near ties in the same work buffer */
+	const int B64 = fp32 ? (int)std::max<size_t>(1, (size_t)Bc * pair_bytes / (plane * sizeof(sg_c64))) : Bc;
+	const size_t row_lds = (size_t)SG_PADN(S) * sizeof(sg_c64), row_lds32 = (size_t)SG_PADN(S) * sizeof(float2);
 	int CW = 8192 / S;
 	if (CW < 1)
 		CW = 1;
@@ -1231,14 +1249,21 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	if (ctx->knobs.reg_cw > 0)	/* A/B knob SG_REG_CW: columns per column-pass workgroup */
 		CW = ctx->knobs.reg_cw;
 	const size_t col_lds = (size_t)CW * (SG_PADN(S) + 1) * sizeof(sg_c64);
-	/* threads: 8 elements per thread in every LDS FFT (sg_stockham_pass's register budget),
-	 * at least one wave */
+	/* threads: 8 elements per thread in every fp64 LDS FFT (sg_stockham_pass's register
+	 * budget), 16 in the fp32 column pass; at least one wave, at most 1024 */
 	auto thr_for = [](int elems) { return elems / 8 < 64 ? 64 : elems / 8; };
 	const int row_thr = thr_for(S), col_thr = thr_for(CW * S), xri_thr = thr_for(2 * S);
 	/* half-spectrum columns: a strip stays inside one half (CW divides S/2) */
 	const int CWh = CW < S / 2 ? CW : S / 2;
 	const size_t colh_lds = (size_t)CWh * (SG_PADN(S) + 1) * sizeof(sg_c64);
 	const int colh_thr = thr_for(CWh * S);
+	/* fp32 columns: CW32 columns per strip (8: 64-B row segments), 16 elements per thread */
+	int CW32 = ctx->knobs.reg_cw32;
+	while (CW32 > 1 && (CW32 > S / 2 || CW32 * S > 16 * 1024))
+		CW32 >>= 1;
+	const int ept32 = CW32 * S / 1024 > 8 ? 16 : 8;
+	const int colh_thr32 = std::max(64, CW32 * S / ept32);
+	const size_t colh_lds32 = (size_t)CW32 * (SG_PADN(S) + 1) * sizeof(float2);
 	const int xcdmap = ctx->knobs.reg_xcd;	/* A/B knob SG_REG_XCD: 0 = strips in dispatch order */
 	/* generic rows: Bluestein needs m/8 threads (sg_lds_fft), the mixed passes take 256 */
 	const int gen_thr = pl.bluestein ? (pl.m / 8 < 64 ? 64 : pl.m / 8) : 256;
@@ -1247,40 +1272,53 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		(void)hipFuncSetAttribute((const void *)k_reg_rows_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)row_lds);
 		(void)hipFuncSetAttribute((const void *)k_reg_rows_inv_argmax, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)row_lds);
-		(void)hipFuncSetAttribute((const void *)k_reg_cols, hipFuncAttributeMaxDynamicSharedMemorySize, (int)col_lds);
+		(void)hipFuncSetAttribute((const void *)k_reg_cols<sg_c64, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+				(int)col_lds);
 		(void)hipFuncSetAttribute((const void *)k_reg_cols_inv_argmax, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)col_lds);
 		(void)hipFuncSetAttribute((const void *)k_reg_xpower_rows_inv, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)(2 * row_lds));
-		(void)hipFuncSetAttribute((const void *)k_reg_rows_fwd_half, hipFuncAttributeMaxDynamicSharedMemorySize,
+		(void)hipFuncSetAttribute((const void *)k_reg_rows_fwd_half<sg_c64>, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)row_lds);
-		(void)hipFuncSetAttribute((const void *)k_reg_rows_inv_half_argmax<false>,
+		(void)hipFuncSetAttribute((const void *)k_reg_rows_inv_half_argmax<sg_c64, false>,
 				hipFuncAttributeMaxDynamicSharedMemorySize, (int)row_lds);
-		(void)hipFuncSetAttribute((const void *)k_reg_rows_inv_half_argmax<true>,
+		(void)hipFuncSetAttribute((const void *)k_reg_rows_inv_half_argmax<sg_c64, true>,
 				hipFuncAttributeMaxDynamicSharedMemorySize, (int)row_lds);
-		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower, hipFuncAttributeMaxDynamicSharedMemorySize,
+		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower<sg_c64, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)colh_lds);
+		(void)hipFuncSetAttribute((const void *)k_reg_rows_fwd_half<float2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+				(int)row_lds32);
+		(void)hipFuncSetAttribute((const void *)k_reg_rows_inv_half_argmax<float2, false>,
+				hipFuncAttributeMaxDynamicSharedMemorySize, (int)row_lds32);
+		(void)hipFuncSetAttribute((const void *)k_reg_cols<float2, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+				(int)colh_lds32);
+		(void)hipFuncSetAttribute((const void *)k_reg_cols<float2, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+				(int)colh_lds32);
+		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower<float2, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+				(int)colh_lds32);
+		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower<float2, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+				(int)colh_lds32);
 	} else {
 		(void)hipFuncSetAttribute((const void *)k_gen_rows, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gen_lds);
 	}
 
-	/* device workspace: reference spectrum, pair planes, per-row partials, then (all pairs
-	 * of the call, uploaded once / read back once) the pair table, the per-pair results,
-	 * the frames' energies (two sets: the main passes and the near-tie re-run) and the
-	 * near-tie candidates of one batch */
+	/* device workspace: reference spectrum (fp64, and fp32 behind it), pair planes, per-row
+	 * partials, then (all pairs of the call, uploaded once / read back once) the pair table,
+	 * the per-pair results, the frames' energies (two sets: the main passes and the near-tie
+	 * re-runs) and the near-tie candidates of one batch */
 	const int NP = npairs_total > 0 ? npairs_total : 1;
-	const int Bc = B > 1 ? B : 1;
-	HIPCHK(ensure(dv.reg_spec, plane * sizeof(sg_c64)));
+	HIPCHK(ensure(dv.reg_spec, plane * sizeof(sg_c64) + (fp32 ? plane * sizeof(float2) : 0)));
 	HIPCHK(ensure(dv.reg_work, (size_t)Bc * pair_bytes));
-	const size_t o_out = ((size_t)Bc * S * sizeof(SgBest) + 255) & ~(size_t)255;
+	const size_t o_out = ((size_t)std::max(Bc, B64) * S * sizeof(SgBest) + 255) & ~(size_t)255;
 	const size_t o_fab = o_out + (((size_t)(NP + 1) * sizeof(SgRegOut) + 255) & ~(size_t)255);
 	const size_t o_en = o_fab + (((size_t)(NP + 1) * 4 * sizeof(int) + 255) & ~(size_t)255);
 	const size_t o_cand = o_en + (((size_t)nframes * 2 * sizeof(unsigned long long) + 255) & ~(size_t)255);
-	const size_t o_res2 = o_cand + (((size_t)Bc * 2 * sizeof(SgCand) + 255) & ~(size_t)255);
+	const size_t o_res2 = o_cand + (((size_t)std::max(Bc, B64) * 2 * sizeof(SgCand) + 255) & ~(size_t)255);
 	const size_t ws = o_res2 + (size_t)(NP + 1) * sizeof(SgRegOut);
 	HIPCHK(ensure(dv.reg_best, ws));
 	char *wsp = (char *)dv.reg_best.p;
 	sg_c64 *spec = (sg_c64 *)dv.reg_spec.p, *work = (sg_c64 *)dv.reg_work.p;
+	float2 *spec32 = (float2 *)((char *)dv.reg_spec.p + plane * sizeof(sg_c64)), *work32 = (float2 *)dv.reg_work.p;
 	sg_c64 *work2 = work + (size_t)Bc * plane;	/* generic path: transposed planes */
 	SgBest *best = (SgBest *)wsp;
 	SgRegOut *d_out = (SgRegOut *)(wsp + o_out), *d_res2 = (SgRegOut *)(wsp + o_res2);
@@ -1288,6 +1326,19 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	unsigned long long *energy = (unsigned long long *)(wsp + o_en), *energy2 = energy + nframes;
 	SgCand *cand = (SgCand *)(wsp + o_cand);
 	HIPCHK(hipMemsetAsync(energy, 0, sizeof(unsigned long long) * 2 * nframes, s));
+	/* fp32 twiddles, rounded from the fp64 table (behind the fp64 tables in reg_tw) */
+	const float2 *tw32 = nullptr;
+	if (fp32) {
+		HIPCHK(ensure(dv.reg_tw32, 2 * (size_t)S * sizeof(float2)));
+		std::vector<double> t64;
+		make_twiddles(S, t64);
+		std::vector<float> t32(t64.size());
+		for (size_t i = 0; i < t64.size(); i++)
+			t32[i] = (float)t64[i];
+		HIPCHK(hipMemcpyAsync(dv.reg_tw32.p, t32.data(), sizeof(float) * t32.size(), hipMemcpyHostToDevice, s));
+		HIPCHK(hipStreamSynchronize(s));
+		tw32 = (const float2 *)dv.reg_tw32.p;
+	}
 
 	/* pair k = frames todo[2k], todo[2k+1] (-1: odd count, imaginary part zero); slot NP is
 	 * the reference spectrum's (ref_image, -1) */
@@ -1323,6 +1374,50 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		HIPCHK(hipGetLastError());
 		return SG_OK;
 	};
+	/* half-spectrum passes of the pairs (fa, fb)[0, np): the reference spectrum (spec) of the
+	 * precision (fp64 or fp32), `mode` 0 = top-2 arg-max into best, 1 = near-tie candidates */
+	auto half_spec64 = [&]() -> int {
+		hipLaunchKernelGGL(k_reg_rows_fwd_half<sg_c64>, dim3(S, 1), dim3(row_thr), row_lds, s, d_sel, d_fa + NP,
+				d_fb + NP, S, tw, spec, energy2);
+		HIPCHK(hipGetLastError());
+		hipLaunchKernelGGL((k_reg_cols<sg_c64, 8>), dim3(S / 2 / CWh, 1), dim3(colh_thr), colh_lds, s, spec, S, logS,
+				CWh, tw, 0, xcdmap);
+		HIPCHK(hipGetLastError());
+		return SG_OK;
+	};
+	auto half64 = [&](const int *fa, const int *fb, int np, unsigned long long *en, int mode, const SgRegOut *res)
+			-> int {
+		hipLaunchKernelGGL(k_reg_rows_fwd_half<sg_c64>, dim3(S, np), dim3(row_thr), row_lds, s, d_sel, fa, fb, S, tw,
+				work, en);
+		HIPCHK(hipGetLastError());
+		hipLaunchKernelGGL((k_reg_cols_xpower<sg_c64, 8>), dim3(S / CWh, np), dim3(colh_thr), colh_lds, s, work,
+				(const sg_c64 *)spec, S, CWh, tw, xcdmap, ctx->knobs.reg_pb);
+		HIPCHK(hipGetLastError());
+		if (mode)
+			hipLaunchKernelGGL((k_reg_rows_inv_half_argmax<sg_c64, true>), dim3(S, np), dim3(row_thr), row_lds, s,
+					(const sg_c64 *)work, S, tw, best, res, cand);
+		else
+			hipLaunchKernelGGL((k_reg_rows_inv_half_argmax<sg_c64, false>), dim3(S, np), dim3(row_thr), row_lds, s,
+					(const sg_c64 *)work, S, tw, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
+		HIPCHK(hipGetLastError());
+		return SG_OK;
+	};
+	auto half32 = [&](const int *fa, const int *fb, int np, unsigned long long *en) -> int {
+		hipLaunchKernelGGL(k_reg_rows_fwd_half<float2>, dim3(S, np), dim3(row_thr), row_lds32, s, d_sel, fa, fb, S,
+				tw32, work32, en);
+		HIPCHK(hipGetLastError());
+		if (ept32 == 16)
+			hipLaunchKernelGGL((k_reg_cols_xpower<float2, 16>), dim3(S / CW32, np), dim3(colh_thr32), colh_lds32, s,
+					work32, (const float2 *)spec32, S, CW32, tw32, xcdmap, 1);
+		else
+			hipLaunchKernelGGL((k_reg_cols_xpower<float2, 8>), dim3(S / CW32, np), dim3(colh_thr32), colh_lds32, s,
+					work32, (const float2 *)spec32, S, CW32, tw32, xcdmap, 1);
+		HIPCHK(hipGetLastError());
+		hipLaunchKernelGGL((k_reg_rows_inv_half_argmax<float2, false>), dim3(S, np), dim3(row_thr), row_lds32, s,
+				(const float2 *)work32, S, tw32, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
+		HIPCHK(hipGetLastError());
+		return SG_OK;
+	};
 
 	/* reference spectrum R = FFT2(ref) (half layout: the A' half only; generic: transposed) */
 	if (generic) {
@@ -1333,21 +1428,33 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		HIPCHK(hipGetLastError());
 		hipLaunchKernelGGL(k_gen_rows, dim3(S, 1), dim3(gen_thr), gen_lds, s, d_sel, d_fa + NP, d_fb + NP, spec, S, pl,
 				tbl, (int)SG_GEN_C2C, 0, energy, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
-	} else if (half) {
-		hipLaunchKernelGGL(k_reg_rows_fwd_half, dim3(S, 1), dim3(row_thr), row_lds, s, d_sel, d_fa + NP, d_fb + NP,
-				S, tw, spec, energy);
+	} else if (fp32) {
+		hipLaunchKernelGGL(k_reg_rows_fwd_half<float2>, dim3(S, 1), dim3(row_thr), row_lds32, s, d_sel, d_fa + NP,
+				d_fb + NP, S, tw32, spec32, energy);
 		HIPCHK(hipGetLastError());
-		hipLaunchKernelGGL(k_reg_cols, dim3(S / 2 / CWh, 1), dim3(colh_thr), colh_lds, s, spec, S, logS, CWh, tw, 0,
-				xcdmap);
+		if (ept32 == 16)
+			hipLaunchKernelGGL((k_reg_cols<float2, 16>), dim3(S / 2 / CW32, 1), dim3(colh_thr32), colh_lds32, s, spec32,
+					S, logS, CW32, tw32, 0, xcdmap);
+		else
+			hipLaunchKernelGGL((k_reg_cols<float2, 8>), dim3(S / 2 / CW32, 1), dim3(colh_thr32), colh_lds32, s, spec32,
+					S, logS, CW32, tw32, 0, xcdmap);
+	} else if (half) {
+		hipLaunchKernelGGL(k_reg_rows_fwd_half<sg_c64>, dim3(S, 1), dim3(row_thr), row_lds, s, d_sel, d_fa + NP,
+				d_fb + NP, S, tw, spec, energy);
+		HIPCHK(hipGetLastError());
+		hipLaunchKernelGGL((k_reg_cols<sg_c64, 8>), dim3(S / 2 / CWh, 1), dim3(colh_thr), colh_lds, s, spec, S, logS,
+				CWh, tw, 0, xcdmap);
 	} else {
 		hipLaunchKernelGGL(k_reg_rows_fwd, dim3(S, 1), dim3(row_thr), row_lds, s, d_sel, d_fa + NP, d_fb + NP, S,
 				logS, tw, spec, energy);
 		HIPCHK(hipGetLastError());
-		hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, 1), dim3(col_thr), col_lds, s, spec, S, logS, CW, tw, 0, xcdmap);
+		hipLaunchKernelGGL((k_reg_cols<sg_c64, 8>), dim3(S / CW, 1), dim3(col_thr), col_lds, s, spec, S, logS, CW, tw, 0,
+				xcdmap);
 	}
 	HIPCHK(hipGetLastError());
 	shiftx[ref_image] = 0;
 	shifty[ref_image] = 0;
+	const int tol_main = fp32 ? -15 : -32;
 	for (int p0 = 0; p0 < npairs_total; p0 += B) {
 		const int np = npairs_total - p0 < B ? npairs_total - p0 : B;
 		int count = S;	/* row partials per pair */
@@ -1357,21 +1464,18 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 			hipLaunchKernelGGL(k_gen_rows, dim3(S, np), dim3(gen_thr), gen_lds, s, d_sel, d_fa + p0, d_fb + p0, work, S,
 					pl, tbl, (int)SG_GEN_INV_ARGMAX, 1, energy, best, (const SgRegOut *)nullptr,
 					(SgCand *)nullptr);
+		} else if (fp32) {
+			if (int r = half32(d_fa + p0, d_fb + p0, np, energy))
+				return r;
 		} else if (half) {
-			hipLaunchKernelGGL(k_reg_rows_fwd_half, dim3(S, np), dim3(row_thr), row_lds, s, d_sel, d_fa + p0,
-					d_fb + p0, S, tw, work, energy);
-			HIPCHK(hipGetLastError());
-			hipLaunchKernelGGL(k_reg_cols_xpower, dim3(S / CWh, np), dim3(colh_thr), colh_lds, s, work,
-					(const sg_c64 *)spec, S, CWh, tw, xcdmap, ctx->knobs.reg_pb);
-			HIPCHK(hipGetLastError());
-			hipLaunchKernelGGL(k_reg_rows_inv_half_argmax<false>, dim3(S, np), dim3(row_thr), row_lds, s,
-					(const sg_c64 *)work, S, tw, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
+			if (int r = half64(d_fa + p0, d_fb + p0, np, energy, 0, nullptr))
+				return r;
 		} else {
 			hipLaunchKernelGGL(k_reg_rows_fwd, dim3(S, np), dim3(row_thr), row_lds, s, d_sel, d_fa + p0, d_fb + p0, S,
 					logS, tw, work, energy);
 			HIPCHK(hipGetLastError());
-			hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, np), dim3(col_thr), col_lds, s, work, S, logS, CW, tw, 0,
-					xcdmap);
+			hipLaunchKernelGGL((k_reg_cols<sg_c64, 8>), dim3(S / CW, np), dim3(col_thr), col_lds, s, work, S, logS, CW,
+					tw, 0, xcdmap);
 			HIPCHK(hipGetLastError());
 			if (fused) {
 				/* cross-power + inverse rows (row pairs ky, -ky), then inverse columns with the
@@ -1385,8 +1489,8 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 			} else {
 				hipLaunchKernelGGL(k_reg_xpower, dim3(1024, np), dim3(256), 0, s, work, (const sg_c64 *)spec, S);
 				HIPCHK(hipGetLastError());
-				hipLaunchKernelGGL(k_reg_cols, dim3(S / CW, np), dim3(col_thr), col_lds, s, work, S, logS, CW, tw, 1,
-						xcdmap);
+				hipLaunchKernelGGL((k_reg_cols<sg_c64, 8>), dim3(S / CW, np), dim3(col_thr), col_lds, s, work, S, logS,
+						CW, tw, 1, xcdmap);
 				HIPCHK(hipGetLastError());
 				hipLaunchKernelGGL(k_reg_rows_inv_argmax, dim3(S, np), dim3(row_thr), row_lds, s,
 						(const sg_c64 *)work, S, logS, tw, best);
@@ -1394,7 +1498,7 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		}
 		HIPCHK(hipGetLastError());
 		hipLaunchKernelGGL(k_reg_final, dim3(np), dim3(256), 0, s, (const SgBest *)best, S, count,
-				(const int *)d_fa + p0, (const int *)d_fb + p0, ref_image, (const unsigned long long *)energy,
+				(const int *)d_fa + p0, (const int *)d_fb + p0, ref_image, (const unsigned long long *)energy, tol_main,
 				d_out + p0);
 		HIPCHK(hipGetLastError());
 	}
@@ -1402,17 +1506,20 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		HIPCHK(hipMemcpyAsync(hout.data(), d_out, sizeof(SgRegOut) * npairs_total, hipMemcpyDeviceToHost, s));
 	HIPCHK(hipStreamSynchronize(s));
 
-	/* near ties (the runner-up within the FFT tolerance of the maximum): re-run those pairs,
-	 * list every index within the tolerance, compute their exact integer correlations and
-	 * take the largest (lowest index among exact equals) */
-	std::vector<int> amb;
-	for (int k = 0; k < npairs_total; k++)
-		if (hout[k].amb[0] || hout[k].amb[1])
-			amb.push_back(k);
-	if (!amb.empty() && resolvable) {
+	/* near ties (the runner-up within the tolerance of the maximum): re-run those pairs.  After
+	 * fp32 passes, first in fp64 (a fresh arg-max at the fp64 tolerance); what is still a near
+	 * tie then lists every index within the tolerance, computes their exact integer
+	 * correlations and takes the largest (lowest index among exact equals) */
+	auto ambiguous = [&](std::vector<int> &amb) {
+		amb.clear();
+		for (int k = 0; k < npairs_total; k++)
+			if (hout[k].amb[0] == 1 || hout[k].amb[1] == 1)
+				amb.push_back(k);
+	};
+	auto upload_subset = [&](const std::vector<int> &amb, std::vector<SgRegOut> &ares) -> int {
 		const int na = (int)amb.size();
 		std::vector<int> afa(na), afb(na);
-		std::vector<SgRegOut> ares(na);
+		ares.resize(na);
 		for (int i = 0; i < na; i++) {
 			afa[i] = hfa[amb[i]];
 			afb[i] = hfb[amb[i]];
@@ -1421,8 +1528,41 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		HIPCHK(hipMemcpyAsync(d_fa2, afa.data(), sizeof(int) * na, hipMemcpyHostToDevice, s));
 		HIPCHK(hipMemcpyAsync(d_fb2, afb.data(), sizeof(int) * na, hipMemcpyHostToDevice, s));
 		HIPCHK(hipMemcpyAsync(d_res2, ares.data(), sizeof(SgRegOut) * na, hipMemcpyHostToDevice, s));
-		for (int p0 = 0; p0 < na; p0 += B) {
-			const int np = na - p0 < B ? na - p0 : B;
+		HIPCHK(hipStreamSynchronize(s));	/* the host vectors die here */
+		return SG_OK;
+	};
+	std::vector<int> amb;
+	std::vector<SgRegOut> ares;
+	ambiguous(amb);
+	if (!amb.empty() && fp32) {
+		/* fp64 re-run: the fp64 reference spectrum, then the pairs' fp64 passes and arg-max */
+		if (int r = upload_subset(amb, ares))
+			return r;
+		if (int r = half_spec64())
+			return r;
+		const int na = (int)amb.size();
+		for (int p0 = 0; p0 < na; p0 += B64) {
+			const int np = na - p0 < B64 ? na - p0 : B64;
+			if (int r = half64(d_fa2 + p0, d_fb2 + p0, np, energy2, 0, nullptr))
+				return r;
+			hipLaunchKernelGGL(k_reg_final, dim3(np), dim3(256), 0, s, (const SgBest *)best, S, S,
+					(const int *)d_fa2 + p0, (const int *)d_fb2 + p0, ref_image, (const unsigned long long *)energy,
+					-32, d_res2 + p0);
+			HIPCHK(hipGetLastError());
+		}
+		HIPCHK(hipMemcpyAsync(ares.data(), d_res2, sizeof(SgRegOut) * na, hipMemcpyDeviceToHost, s));
+		HIPCHK(hipStreamSynchronize(s));
+		for (int i = 0; i < na; i++)
+			hout[amb[i]] = ares[i];
+		ctx->stats.reg_fp64_reruns += (uint64_t)na;
+		ambiguous(amb);
+	}
+	if (!amb.empty() && resolvable) {
+		if (int r = upload_subset(amb, ares))
+			return r;
+		const int na = (int)amb.size();
+		for (int p0 = 0; p0 < na; p0 += B64) {
+			const int np = na - p0 < B64 ? na - p0 : B64;
 			HIPCHK(hipMemsetAsync(cand, 0, sizeof(SgCand) * 2 * np, s));
 			if (generic) {
 				if (int r = gen_forward(d_fa2 + p0, d_fb2 + p0, np, energy2))
@@ -1431,14 +1571,9 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 						work, S, pl, tbl, (int)SG_GEN_INV_CAND, 1, energy2, best, (const SgRegOut *)(d_res2 + p0),
 						cand);
 			} else {
-				hipLaunchKernelGGL(k_reg_rows_fwd_half, dim3(S, np), dim3(row_thr), row_lds, s, d_sel, d_fa2 + p0,
-						d_fb2 + p0, S, tw, work, energy2);
-				HIPCHK(hipGetLastError());
-				hipLaunchKernelGGL(k_reg_cols_xpower, dim3(S / CWh, np), dim3(colh_thr), colh_lds, s, work,
-						(const sg_c64 *)spec, S, CWh, tw, xcdmap, ctx->knobs.reg_pb);
-				HIPCHK(hipGetLastError());
-				hipLaunchKernelGGL(k_reg_rows_inv_half_argmax<true>, dim3(S, np), dim3(row_thr), row_lds, s,
-						(const sg_c64 *)work, S, tw, best, (const SgRegOut *)(d_res2 + p0), cand);
+				/* the fp64 spectrum exists on the fp64 half path, and after the fp64 re-run */
+				if (int r = half64(d_fa2 + p0, d_fb2 + p0, np, energy2, 1, (const SgRegOut *)(d_res2 + p0)))
+					return r;
 			}
 			HIPCHK(hipGetLastError());
 			hipLaunchKernelGGL(k_reg_exact, dim3(SG_CAND_CAP, 2 * np), dim3(256), 0, s, d_sel, (const int *)d_fa2 + p0,

@@ -57,6 +57,7 @@ class StackStats(ctypes.Structure):
         ("path", ctypes.c_int),
         ("reg_ties_resolved", ctypes.c_uint64),
         ("reg_ties_unresolved", ctypes.c_uint64),
+        ("reg_fp64_reruns", ctypes.c_uint64),
     ]
 
 

@@ -132,6 +132,25 @@ def test_register_generic_path_on_power_of_two(gpu_ctx):
     assert np.array_equal(gx, hx) and np.array_equal(gy, hy) and _same_q(gq, hq)
 
 
+@pytest.mark.parametrize("S", [256, 2048])
+def test_register_fp32_passes_match_fp64(gpu_ctx, S):
+    """the fp32 half-spectrum passes (default, SG_REG_FP=32) give the fp64 passes' shifts and
+    qualities: a maximum is decided in fp32 only when it beats every other entry by more than
+    the fp32 tolerance, otherwise the pair is re-run in fp64"""
+    n = 9 if S == 256 else 5
+    sel = orc.synth(n, 1, S, S, seed=S + 11, maxshift=12)[:, 0].copy()
+    gx, gy, gq = gpu_ctx.register_dft(sel)
+    os.environ["SG_REG_FP"] = "64"
+    try:
+        with sg.Context() as c64:
+            hx, hy, hq = c64.register_dft(sel)
+    finally:
+        del os.environ["SG_REG_FP"]
+    assert np.array_equal(gx, hx) and np.array_equal(gy, hy) and _same_q(gq, hq)
+    ex, ey = orc.synth_shifts(n, seed=S + 11, maxshift=12)
+    assert np.array_equal(gx, ex) and np.array_equal(gy, ey)
+
+
 def _periodic_pair(S, dx, dy, seed):
     """ref periodic with period S/2 along x, img = ref circularly translated by (dy, dx):
     the correlation has two exactly equal maxima, at kx and kx + S/2"""
@@ -160,6 +179,8 @@ def test_register_exact_tie_takes_lowest_index(gpu_ctx, S):
     y, x = divmod(lo, S)
     assert (gx[1], gy[1]) == (x - S if x > S // 2 else x, y - S if y > S // 2 else y)
     assert st.reg_ties_resolved >= 1
+    if S == 64 and os.environ.get("SG_REG_FP", "32") == "32":
+        assert st.reg_fp64_reruns >= 1          # the fp32 passes handed the pair to fp64 first
 
 
 def test_register_near_tie_takes_exact_maximum(gpu_ctx):
