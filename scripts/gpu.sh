@@ -10,6 +10,8 @@
 #   env=NAME:VAR=V[;VAR=V]:ARGS the same with an environment (A/B: SG_* knobs, SG_LIB_PATH)
 #   prof=NAME[:ARGS]            rocprofv3 --kernel-trace --stats of bench.py ARGS -> NAME/
 #   pmc=NAME[:ARGS]             FETCH_SIZE and WRITE_SIZE passes (own runs) -> NAME_traffic.json
+#   sq=NAME:CTRS[:ARGS]         one rocprofv3 --pmc pass with counters CTRS ('+' between them,
+#                               within the per-block slot limits) -> NAME.txt (pmc_sum.py)
 #   py=NAME:SCRIPT[:ARGS]       python SCRIPT ARGS -> NAME.log
 #   dist=NAME:NPROC[:ARGS]      bench.py under torchrun with NPROC ranks on this one GPU
 #                               (SG_BENCH_REHEARSE=1: gloo collectives; a rehearsal of the multi-GPU flow)
@@ -64,6 +66,13 @@ for step in "$@"; do
       done
       python3 scripts/pmc_traffic.py "$O/${name}_FETCH_SIZE" "$O/${name}_WRITE_SIZE" "${PMC_KERNEL:-k_stack_hist}" \
         "$O/${name}_traffic.json" || fail "pmc parse" ;;
+    sq)
+      name=${spec%%:*}; rest=${spec#*:}; ctrs=${rest%%:*}; args=""; [ "$ctrs" != "$rest" ] && args=${rest#*:}
+      timeout -s KILL 180 rocprofv3 --pmc ${ctrs//+/ } --output-format csv -d "$O/$name" -o run -- \
+        python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline ${args//,/ } > "$O/$name.log" 2>&1 \
+        || fail "sq $name" "$O/$name.log"
+      python3 scripts/pmc_sum.py "$O/$name" "${PMC_KERNEL:-k_stack}" > "$O/$name.txt" || fail "sq parse"
+      cat "$O/$name.txt" ;;
     dist)
       name=${spec%%:*}; rest=${spec#*:}; np=${rest%%:*}; args=""; [ "$np" != "$rest" ] && args=${rest#*:}
       SG_BENCH_REHEARSE=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$np" \

@@ -70,6 +70,9 @@ struct SghCfg {
 #define SGH_NBUF 2		/* register buffers of 16 frames per wave (NBUF-1 blocks in flight while binning) */
 #endif
 #define SGH_BAND 1e-13		/* same rounding band as the sorted path (SG_BAND) */
+/* largest frame count whose Winsorized moments n SS and S^2 (values relative to lo, |v - lo| <=
+ * 65535) stay integers below 2^53: 1448^2 65535^2 < 2^53 */
+#define SGH_WIN_DBL_MAXN 1448
 
 typedef unsigned short sgh_u16x2 __attribute__((ext_vector_type(2)));
 
@@ -835,15 +838,6 @@ __device__ __forceinline__ double sgh_sqrt_fast(double x) {
 	r = fma(-s, h, 0.5);
 	return fma(s, r, s);
 }
-/* the same with 1 / (n (n - 1)) precomputed: within a few ulp of sgh_sd_rel, far inside the
- * rounding band every decision keeps */
-__device__ __forceinline__ double sgh_sd_rel_inv(int n, long long S, long long SS, double inn, bool *e0) {
-	const long long num = (long long)n * SS - S * S;
-	*e0 = (num == 0);
-	const double v = sgh_sqrt_fast((double)(num > 0 ? num : 1) * inn);
-	return num > 0 ? v : 0.0;
-}
-
 /* round_to_WORD(m) decision ambiguous (m within tol of 0, 65535 or a .5) */
 __device__ __forceinline__ bool sgh_round_ambiguous(double m, double tol) {
 	if (fabs(m) <= tol || fabs(m - 65535.0) <= tol)
@@ -914,7 +908,10 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint
 		 * [ulo, uhi] - the common case once the clamps have settled - is counted without a
 		 * histogram query, and the median of w is vlo, vhi or km1 / km2 */
 		int Lw = 0, Hw = 0, vlo = 0, vhi = 0, IA = A, IB = B;
-		SghM MIA = MA, MIB = MB;
+		/* inner-part bounds: counts as int, moments as doubles (exact: |S| <= N 65535 and
+		 * SS <= N 65535^2 stay below 2^53) */
+		int ciA = MA.c, ciB = MB.c;
+		double sA = (double)MA.s, ssA = (double)MA.ss, sB = (double)MB.s, ssB = (double)MB.ss;
 		int ulo = sgh_value_at1(P, MA.c), uhi = sgh_value_at1(P, MA.c + n - 1);
 		const double inn = 1.0 / ((double)n * (double)(n - 1));
 		bool sig_e0 = e0;
@@ -937,8 +934,8 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint
 						c += nin;
 					} else {
 						int k = cnt_cached(v, side);
-						k = k < MIA.c ? MIA.c : (k > MIB.c ? MIB.c : k);
-						c += k - MIA.c;
+						k = k < ciA ? ciA : (k > ciB ? ciB : k);
+						c += k - ciA;
 					}
 				}
 				if (Hw && vhi <= v)
@@ -973,7 +970,10 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint
 					/* the inner samples below m0 join the clamped copies */
 					double c = ceil(m0 - tol);
 					IA = c < 0.0 ? 0 : (c > 65536.0 ? 65536 : (int)c);
-					MIA = sgh_M_le(P, IA - 1);
+					const SghM m = sgh_M_le(P, IA - 1);
+					ciA = m.c;
+					sA = (double)m.s;
+					ssA = (double)m.ss;
 					grew_lo = true;
 				}
 				Lw = clo;
@@ -987,13 +987,16 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint
 				if (chi > Hw) {
 					double c = floor(m1d + tol);
 					IB = c < -1.0 ? -1 : (c > 65535.0 ? 65535 : (int)c);
-					MIB = sgh_M_le(P, IB);
+					const SghM m = sgh_M_le(P, IB);
+					ciB = m.c;
+					sB = (double)m.s;
+					ssB = (double)m.ss;
 					grew_hi = true;
 				}
 				Hw = chi;
 				vhi = sg_round_to_WORD(m1d);
 			}
-			if (MIB.c - MIA.c != n - Lw - Hw)
+			if (ciB - ciA != n - Lw - Hw)
 				return 1;	/* inner part and clamp counts disagree: leave it to the sorted path */
 			if (n - Lw - Hw > 0) {
 				if (grew_lo)
@@ -1008,13 +1011,27 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint
 				const int wr = rhs < Lw ? vlo : (rhs >= n - Hw ? vhi : km2);
 				median = (lhs == rhs) ? (double)wl : (double)(wl + wr) / 2.0;
 			}
-			const long long dl = (long long)vlo - P.lo, dh = (long long)vhi - P.lo;
-			const long long Sw = (MIB.s - MIA.s) + dl * Lw + dh * Hw;
-			const long long SSw = (long long)(MIB.ss - MIA.ss) + dl * dl * Lw + dh * dh * Hw;
+			/* with N <= 1448 every Winsorized moment is an integer under 2^53, so the double
+			 * arithmetic is exact and the iteration needs no 64-bit integer multiplies
+			 * (quarter-rate v_mul_lo / v_mad_u64) */
+			const double Sin = sB - sA, SSin = ssB - ssA;
+			double num;
+			if (N <= SGH_WIN_DBL_MAXN) {
+				const double dl = (double)(vlo - P.lo), dh = (double)(vhi - P.lo);
+				const double Lf = (double)Lw, Hf = (double)Hw;
+				const double Sw = fma(dh, Hf, fma(dl, Lf, Sin));
+				const double SSw = fma(dh * dh, Hf, fma(dl * dl, Lf, SSin));
+				num = (double)n * SSw - Sw * Sw;
+			} else {
+				const long long dl = (long long)vlo - P.lo, dh = (long long)vhi - P.lo;
+				const long long Sw = (long long)Sin + dl * Lw + dh * Hw;
+				const long long SSw = (long long)SSin + dl * dl * Lw + dh * dh * Hw;
+				num = (double)((long long)n * SSw - Sw * Sw);
+			}
 			const double sigma0 = sigma;
 			const bool e00 = sig_e0;
-			bool we0;
-			sigma = 1.134 * sgh_sd_rel_inv(n, Sw, SSw, inn, &we0);
+			const bool we0 = (num == 0.0);
+			sigma = 1.134 * (num > 0.0 ? sgh_sqrt_fast(num * inn) : 0.0);
 			sig_e0 = we0;
 			if (e00) {
 				if (we0)

@@ -100,7 +100,7 @@ def test_register_any_side_matches_oracle(gpu_ctx, S):
 @pytest.mark.parametrize("S", [1500, 1009, 1234])
 def test_register_large_non_power_of_two(gpu_ctx, S):
     """1500 = 2^2 3 5^3 (mixed radix), 1009 (prime) and 1234 = 2 x 617 (Bluestein, m = 4096):
-    the synthetic translations are recovered and equal an independent numpy FFT's arg-max;
+    the arg-max equals an independent numpy FFT's (translations recovered to a pixel);
     qualities equal the oracle's QualityEstimate"""
     n, M = 6, 12
     sel = orc.synth(n, 1, S, S, seed=S, maxshift=M)[:, 0].copy()
@@ -108,7 +108,9 @@ def test_register_large_non_power_of_two(gpu_ctx, S):
     ex, ey = orc.synth_shifts(n, seed=S, maxshift=M)
     nx, ny = _numpy_shifts(sel)
     assert np.array_equal(gx, nx) and np.array_equal(gy, ny), (gx, nx, gy, ny)
-    assert np.array_equal(gx, ex) and np.array_equal(gy, ey)
+    # the arg-max is the parity target; the synthetic translation itself is only recovered to
+    # within a pixel (the scene is not periodic: at S = 1009 two frames' peaks sit one off)
+    assert np.abs(gx - ex).max() <= 1 and np.abs(gy - ey).max() <= 1, (gx, ex, gy, ey)
     rq = np.array([orc.quality(sel[f]) for f in range(n)])
     q_min = q_max = rq[0]                   # normalizeQualityData with register_shift_dft's min / max
     for q in rq[1:]:
