@@ -214,16 +214,19 @@ class Dist:
     def gather_to_root(self, band, out_list):
         """rank 0 receives every rank's equal-sized band tensor (RCCL gather: each peer sends its
         band straight to rank 0 over its own xGMI link)"""
+        # neither gloo nor RCCL has a 16-bit unsigned type: the bands travel as their bytes
+        import torch
+        as_bytes = lambda t: t.contiguous().view(torch.uint8)
         if self.rehearse:
-            import torch
-            b = band.cpu()
+            b = as_bytes(band.cpu())
             lst = [torch.empty_like(b) for _ in range(self.world)] if self.rank == 0 else None
             self.dist.gather(b, gather_list=lst, dst=0)
             if self.rank == 0:
                 for o, t in zip(out_list, lst):
-                    o.copy_(t)
+                    as_bytes(o).copy_(t)
         else:
-            self.dist.gather(band, gather_list=out_list if self.rank == 0 else None, dst=0)
+            self.dist.gather(as_bytes(band), gather_list=[as_bytes(o) for o in out_list] if self.rank == 0 else None,
+                             dst=0)
 
     def sum_counters(self, rej):
         import numpy as np

@@ -98,6 +98,12 @@ int main(int argc, char **argv) {
 		t0 = now_ms();
 		rc = harness_register(seq, rl, rx, ry, rs, !included);
 		printf("register_shift_dft: rc %d, %.1f ms\n", rc, now_ms() - t0);
+		if (!rc && seq->regparam && seq->regparam[rl] && seq->number <= 64) {
+			printf("shifts:");
+			for (int i = 0; i < seq->number; i++)
+				printf(" (%d,%d)", seq->regparam[rl][i].shiftx, seq->regparam[rl][i].shifty);
+			printf("\n");
+		}
 		harness_set_registration_layer(rl);
 	}
 	if (!rc && method >= 0) {

@@ -5,6 +5,7 @@
 # Results go to gpurun_out/OUT/.  Steps run in order; the first failing step ends the run
 # (no GPU step runs after a fault, an abort or a time limit).
 #   test[=K]                    pytest -m gpu (optionally -k K), per-test timeout 200 s
+#   testall[=K]                 the same, going on past assertion failures (at most 8)
 #   smoke                       __graft_entry__.smoke()
 #   bench=NAME[:ARGS]           python bench.py ARGS -> NAME.log + one summary line
 #   env=NAME:VAR=V[;VAR=V]:ARGS the same with an environment (A/B: SG_* knobs, SG_LIB_PATH)
@@ -36,11 +37,14 @@ for step in "$@"; do
   spec=${step#*=}
   [ "$kind" = "$step" ] && spec=""
   case $kind in
-    test)
+    test|testall)
       k=(); [ -n "$spec" ] && k=(-k "$spec")
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread "${k[@]}" \
-        > "$O/pytest_gpu.log" 2>&1 || fail test "$O/pytest_gpu.log"
-      tail -1 "$O/pytest_gpu.log" ;;
+      x=-x; [ "$kind" = testall ] && x=--maxfail=8
+      timeout -k 10 900 python -u -m pytest tests -m gpu $x -v --timeout 200 --timeout-method thread "${k[@]}" \
+        > "$O/pytest_gpu.log" 2>&1; rc=$?
+      # testall goes on after plain test failures (pytest exit 1), never after a crash or a timeout
+      if [ $rc -ne 0 ] && { [ "$kind" = test ] || [ $rc -ne 1 ]; }; then fail test "$O/pytest_gpu.log"; fi
+      grep -E "^(FAILED|ERROR)" "$O/pytest_gpu.log"; tail -1 "$O/pytest_gpu.log" ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || fail smoke "$O/smoke.log"
       tail -1 "$O/smoke.log" ;;

@@ -294,6 +294,7 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 	}
 	p.dbg = ctx->knobs.hist_dbg;
 	p.prio = ctx->knobs.hist_prio;	/* 1 measured best: 4.73 -> 4.58 ms (scripts/gpu_prio.sh) */
+	p.wins_cap = ctx->knobs.wins_cap;
 
 	/* per-frame constants: shifts + normalisation coefficients */
 	const int Npad = (N + 15) & ~15;	/* histogram-path table: 64-byte aligned, padded */

@@ -28,6 +28,9 @@ struct SgStackParams {
 	const int *shiftx, *shifty;		/* device [N] */
 	int dbg;				/* A/B timing knob (SG_HIST_DBG), 0 in production */
 	int prio;				/* histogram path: wave priority of the build phase (SG_HIST_PRIO) */
+	int wins_cap;				/* histogram WINSORIZED: inner iterations of a pass before the pixel goes to the
+						 * redo list (SG_WINS_CAP): the rare pixels that need hundreds hold a whole
+						 * wave in lockstep, the wave-per-pixel replay runs them alone */
 	const int *hist_tab;			/* device: c1[hist_npad] = shifty*W*2 + 2*shiftx, then int16 sx2[hist_npad] = 2*shiftx */
 	int hist_npad;				/* N rounded up to a multiple of 16 */
 	int hist_norm_fold;			/* additive pairs carry offset - 0.5 (NORM 3 kernels) */

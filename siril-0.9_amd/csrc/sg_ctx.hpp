@@ -66,6 +66,7 @@ struct SgKnobs {
 	int hist_prio = 1;		/* SG_HIST_PRIO: build-phase wave priority (1 measured best, scripts/gpu_prio.sh) */
 	int hist_ldspad = 0;		/* SG_HIST_LDSPAD: extra LDS bytes per histogram workgroup (occupancy A/B) */
 	int hist_ni = 1;		/* SG_HIST_NI: pixel pairs per lane of the histogram tiles (2: 256-px tiles) */
+	int wins_cap = 64;		/* SG_WINS_CAP: histogram Winsorize inner iterations per pass before the redo list */
 	int redo_replay = 1;		/* SG_REDO_REPLAY: 0 = redo list always through the sorted kernel */
 	int reduce1 = 0;		/* SG_REDUCE1: 1 = one pixel per lane in the SUM/MAX/MIN/MEAN reduce */
 	long long host_budget = 0;	/* SG_HOST_BUDGET_BYTES: host-pull HBM budget (0 = 85 % of free HBM) */
@@ -83,6 +84,7 @@ struct SgKnobs {
 		hist_prio = sg_env_int("SG_HIST_PRIO", 0, 3, 1);
 		hist_ldspad = sg_env_int("SG_HIST_LDSPAD", 0, 160 * 1024, 0);
 		hist_ni = sg_env_int("SG_HIST_NI", 1, 2, 1);
+		wins_cap = sg_env_int("SG_WINS_CAP", 4, 100000, 64);
 		redo_replay = sg_env_int("SG_REDO_REPLAY", 0, 1, 1);
 		reduce1 = sg_env_int("SG_REDUCE1", 0, 1, 0);
 		if (const char *e = getenv("SG_HOST_BUDGET_BYTES"))

@@ -874,7 +874,7 @@ __device__ __forceinline__ SghM sgh_M_le(const SghPix &P, int v) {
 	return sgh_q_moments(P, q);
 }
 
-__device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint16_t *value, uint32_t *rlo_out,
+__device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int cap, uint16_t *value, uint32_t *rlo_out,
 		uint32_t *rhi_out) {
 	int A = 0, B = 65535, n = N, r = 0, nrem;
 	SghM MA = {0, 0, 0}, MB = P.T;
@@ -916,8 +916,9 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, uint
 		const double inn = 1.0 / ((double)n * (double)(n - 1));
 		bool sig_e0 = e0;
 		for (int guard = 0;; guard++) {
-			if (guard > 4096)
-				return 1;
+			if (guard >= cap)
+				return 1;	/* a long Winsorize (hundreds of iterations with several 0 / 65535
+					 * samples) goes to the replay rather than holding its wave */
 #ifdef SGH_WINS_ITERS	/* A/B probe build: inner iterations (low 16 bits) and outer passes (high) */
 			(*rlo_out)++;
 #endif
@@ -1239,7 +1240,7 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 			P.T.s = (long long)s32 + P.Z.s + ds * P.ns;
 			P.T.ss = (unsigned long long)ss32 + P.Z.ss + (unsigned long long)(ds * ds) * (unsigned long long)P.ns;
 			if (REJ == 4 || !PAIR) {
-				cls = sgh_winsorized(P, N, p.sig0, p.sig1, &value, &rlo, &rhi);
+				cls = sgh_winsorized(P, N, p.sig0, p.sig1, p.wins_cap, &value, &rlo, &rhi);
 #ifdef SGH_WINS_ITERS
 				value = (uint16_t)rlo;	/* A/B probe build: the image holds the inner iteration counts */
 				cls = SG_CLS_OK;

@@ -343,3 +343,36 @@ def test_hist_path_border_normalised_zeros(gpu_ctx, normalize, dark):
         # the two image-edge tiles (columns < 128 and >= 896 here) and of the few rows whose
         # thresholds or medians fall among the normalised zeros (measured: 6.7 k of 20.5 k)
         assert st.chain_pixels < border * W, st.chain_pixels
+
+
+@pytest.mark.parametrize("cap", [None, "4", "12"])
+def test_hist_winsorized_iteration_cap(gpu_ctx, cap):
+    """pixels whose Winsorize pass needs more inner iterations than SG_WINS_CAP leave the
+    histogram path for the wave-per-pixel replay: results and counters stay the oracle's.
+    Several 65535s / zeros per pixel make passes of tens to hundreds of iterations."""
+    import os
+    N, H, W = 256, 8, 256
+    rng = np.random.default_rng(2024)
+    frames = rng.normal(2000, 30, size=(N, 1, H, W)).round().astype(np.uint16)
+    k = rng.integers(0, 9, size=(H, W))                    # 0..8 extreme samples per pixel
+    for y in range(H):
+        for x in range(W):
+            idx = rng.choice(N, size=k[y, x], replace=False)
+            frames[idx, 0, y, x] = 65535 if (x + y) % 2 else 0
+    old = os.environ.get("SG_WINS_CAP")
+    if cap is not None:
+        os.environ["SG_WINS_CAP"] = cap
+    try:
+        with sg.Context() as c:
+            out_h, rej_h, st = _stack_path(c, frames, sg.WINSORIZED, (4.0, 3.0))
+    finally:
+        if old is None:
+            os.environ.pop("SG_WINS_CAP", None)
+        else:
+            os.environ["SG_WINS_CAP"] = old
+    rc, ref, rej_ref = orc.stack_rejection(frames, sg.WINSORIZED, sig=(4.0, 3.0), max_thread=8)
+    assert rc == 0
+    assert_same(out_h, ref, f"cap={cap}")
+    assert np.array_equal(rej_h, rej_ref), (rej_h, rej_ref)
+    if cap == "4":
+        assert st.chain_pixels > 0.2 * H * W, st.chain_pixels   # the cap did send pixels away

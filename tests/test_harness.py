@@ -112,6 +112,7 @@ def test_register_shift_dft_from_c(tmp_path, fmt):
     lib = hl.load()
     N, C, H, W, S = 9, 1, 80, 96, 64
     frames = orc.synth(N, C, H, W, seed=23, maxshift=5)
+    frames[:, :, 30:33, 40:43] = 40000  # structure for QualityEstimate
     x, y = 10, 6                        # display coordinates of the selection
     m0 = H - y - S - (1 if fmt == "fits" else 0)     # its first memory row
     sel = frames[:, 0, m0:m0 + S, x:x + S]
@@ -125,7 +126,8 @@ def test_register_shift_dft_from_c(tmp_path, fmt):
         gx, gy, gq = seq.regdata(0, N)
     m = inc.astype(bool)
     assert np.array_equal(gx[m], rx[m]) and np.array_equal(gy[m], ry[m])
-    assert np.array_equal(gq[m], rq[m])
+    assert np.array_equal(gq[m], rq[m], equal_nan=True)
+    assert not np.isnan(rq[m]).all()                # the bright spot gives a real quality map
     assert gx[4] == 0 and gy[4] == 0 and gq[4] == 0
 
 
@@ -162,4 +164,5 @@ def test_cli_register_and_stack(tmp_path):
     import sirilgpu as sg
     with sg.Seq.open_fits([out]) as s:
         got = s.read_frame(0)
-    assert np.array_equal(got, ref)
+    bad = np.argwhere(got != ref)
+    assert len(bad) == 0, (len(bad), bad[:8].tolist(), r.stdout, rx.tolist(), ry.tolist())
