@@ -275,8 +275,8 @@ __device__ __forceinline__ C sg_rconj(C r, C f) {
 /* The reference-spectrum loads of all 8 cross-power items of a thread are issued together
  * (launches are sized so that CW * S = 8 * blockDim, thr_for).  Issuing them before the
  * forward FFT instead spills (128 VGPRs at 4 waves per SIMD). */
-template <class C, int EPT = 8>
-__global__ void __launch_bounds__(1024)
+template <class C, int EPT = 8, int WPE = 1>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_reg_cols_xpower(C *__restrict__ work, const C *__restrict__ spec, int S, int CW,
 		const C *__restrict__ tw, int xcdmap, int pb) {
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -299,18 +299,17 @@ k_reg_cols_xpower(C *__restrict__ work, const C *__restrict__ spec, int S, int C
 	auto slot = [&](int c, int r) -> C & { return buf[(size_t)c * bstride + sg_pad(r)]; };
 	constexpr int NI = EPT;
 	const int items = CW * S;
-	C rk[NI], rm[NI];
+	/* the reference's packed column 0 (a strip starting at kx = 0 of either half) also needs
+	 * R(-ky): read where it is used, so the other strips keep no second register array */
+	C rk[NI];
 	auto fetch = [&]() {
 #pragma unroll
 		for (int it = 0; it < NI; it++) {
 			const int t = threadIdx.x + it * blockDim.x;
 			rk[it] = sg_mk<C>((T)0, (T)0);
-			rm[it] = sg_mk<C>((T)0, (T)0);
 			if (t < items) {
 				const int c = t % CW, ky = t / CW, kx = (x0 + c) & (H - 1);
 				rk[it] = spec[(size_t)ky * S + kx];
-				if (!kx)
-					rm[it] = spec[(size_t)((S - ky) & (S - 1)) * S];
 			}
 		}
 	};
@@ -333,7 +332,7 @@ k_reg_cols_xpower(C *__restrict__ work, const C *__restrict__ spec, int S, int C
 		const int m = (S - ky) & (S - 1);
 		if (m < ky)
 			continue;
-		const C zk = slot(c, ky), zm = slot(c, m), r1 = rk[it], r2 = rm[it];
+		const C zk = slot(c, ky), zm = slot(c, m), r1 = rk[it], r2 = spec[(size_t)m * S];
 		const C f0 = sg_mk<C>((T)0.5 * (zk.x + zm.x), (T)0.5 * (zk.y - zm.y));
 		const C fn = sg_mk<C>((T)0.5 * (zk.y + zm.y), (T)-0.5 * (zk.x - zm.x));
 		const C r0 = sg_mk<C>((T)0.5 * (r1.x + r2.x), (T)0.5 * (r1.y - r2.y));
@@ -1264,6 +1263,7 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	const int ept32 = CW32 * S / 1024 > 8 ? 16 : 8;
 	const int colh_thr32 = std::max(64, CW32 * S / ept32);
 	const size_t colh_lds32 = (size_t)CW32 * (SG_PADN(S) + 1) * sizeof(float2);
+	const int colocc = ctx->knobs.reg_colocc;
 	const int xcdmap = ctx->knobs.reg_xcd;	/* A/B knob SG_REG_XCD: 0 = strips in dispatch order */
 	/* generic rows: Bluestein needs m/8 threads (sg_lds_fft), the mixed passes take 256 */
 	const int gen_thr = pl.bluestein ? (pl.m / 8 < 64 ? 64 : pl.m / 8) : 256;
@@ -1295,6 +1295,8 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		(void)hipFuncSetAttribute((const void *)k_reg_cols<float2, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)colh_lds32);
 		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower<float2, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+				(int)colh_lds32);
+		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower<float2, 8, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)colh_lds32);
 		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower<float2, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)colh_lds32);
@@ -1408,6 +1410,9 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		HIPCHK(hipGetLastError());
 		if (ept32 == 16)
 			hipLaunchKernelGGL((k_reg_cols_xpower<float2, 16>), dim3(S / CW32, np), dim3(colh_thr32), colh_lds32, s,
+					work32, (const float2 *)spec32, S, CW32, tw32, xcdmap, 1);
+		else if (colocc)	/* A/B SG_REG_COLOCC=1: 64 VGPRs (8 waves / SIMD, two 1024-thread workgroups per CU) */
+			hipLaunchKernelGGL((k_reg_cols_xpower<float2, 8, 8>), dim3(S / CW32, np), dim3(colh_thr32), colh_lds32, s,
 					work32, (const float2 *)spec32, S, CW32, tw32, xcdmap, 1);
 		else
 			hipLaunchKernelGGL((k_reg_cols_xpower<float2, 8>), dim3(S / CW32, np), dim3(colh_thr32), colh_lds32, s,
