@@ -12,17 +12,19 @@
  *   - the two cross-power spectra are packed back as P = R conj F_a + i R conj F_b, whose
  *     inverse is c_a + i c_b (both correlations are real): one forward and one inverse
  *     complex 2-D FFT per PAIR of frames;
- *   - power-of-two sides: Stockham passes of radix 8 (then 4 / 2) in LDS in double precision
- *     on half spectra (rows: one workgroup per row; columns: one workgroup per strip of CW
- *     columns), twiddles from a host table; any other side: mixed radix 8/4/2/3/5/7, or
- *     Bluestein's chirp-z for a prime factor above 7, with transposed column passes;
+ *   - power-of-two sides: Stockham passes of radix 8 (then 4 / 2) in LDS on half spectra
+ *     (rows: one workgroup per row; columns: one workgroup per strip of CW columns), in fp32
+ *     by default, fp64 for the pairs re-run below (SG_REG_FP=64: fp64 throughout), twiddles
+ *     from host tables; any other side: mixed radix 8/4/2/3/5/7, or Bluestein's chirp-z for
+ *     a prime factor above 7, with transposed column passes, in fp64;
  *   - the inverse row pass fuses a per-row TOP-2 arg-max (first index on ties), a tiny kernel
  *     reduces the rows in order.
- * Near ties: when the runner-up lies within 2^-32 S^2 ||ref|| ||img|| of the maximum (far
- * above fp64 FFT rounding), every index within that tolerance is listed and its exact integer
- * correlation computed; the largest wins, the lowest index among exact equals.  So shifts equal
- * the reference wherever FFTW's rounding does not decide between exactly equal correlations
- * (FFTW's choice there is unspecified: "parity unpinned").
+ * Near ties: a maximum is decided where it beats the runner-up by more than the pass's error
+ * bound, 2^-15 S^2 ||ref|| ||img|| in fp32 (the pair then re-runs in fp64) and 2^-32 in fp64
+ * (far above fp64 FFT rounding: every index within it is listed and its exact integer
+ * correlation computed; the largest wins, the lowest index among exact equals).  So shifts
+ * equal the reference wherever FFTW's rounding does not decide between exactly equal
+ * correlations (FFTW's choice there is unspecified: "parity unpinned").
  */
 #include "sg_common.hpp"
 #include "sg_ctx.hpp"

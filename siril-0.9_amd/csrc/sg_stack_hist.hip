@@ -951,8 +951,20 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 				const double c = floor(thr);
 				return c < -1.0 ? -1 : (c > 65535.0 ? 65535 : (int)c);
 			};
-			const int a1 = v_lt(m0 - tol), a2 = v_le(m0 + tol);
-			const int b1 = v_le(m1d + tol), b2 = v_lt(m1d - tol);
+			/* the common case as one floor per side: when m lies more than 2 t (t = the
+			 * rounding check's band, >= tol) from every integer and from every half-integer,
+			 * ceil(m - tol) - 1 = floor(m + tol) = floor(m), round_to_WORD(m) is decided and
+			 * not ambiguous; otherwise the thresholds come from the general formulas */
+			const double t2 = 2.0 * (tol + 1e-9 * tol);
+			const double fl0 = floor(m0), fr0 = m0 - fl0, fl1 = floor(m1d), fr1 = m1d - fl1;
+			const bool fast0 = fr0 > t2 && fr0 < 1.0 - t2 && fabs(fr0 - 0.5) > t2;
+			const bool fast1 = fr1 > t2 && fr1 < 1.0 - t2 && fabs(fr1 - 0.5) > t2;
+			auto clampv = [](double c) { return c < -1.0 ? -1 : (c > 65535.0 ? 65535 : (int)c); };
+			auto round_fast = [](double m, double fl, double fr) -> int {
+				return m <= 0.0 ? 0 : (m > 65535.0 ? 65535 : (int)fl + (fr > 0.5 ? 1 : 0));
+			};
+			const int a1 = fast0 ? clampv(fl0) : v_lt(m0 - tol), a2 = fast0 ? a1 : v_le(m0 + tol);
+			const int b1 = fast1 ? clampv(fl1) : v_le(m1d + tol), b2 = fast1 ? b1 : v_lt(m1d - tol);
 			const int clo = w_le(a1, 0);
 			if (!sig_e0 && a2 != a1 && clo != w_le(a2, 0))
 				return 1;
@@ -963,7 +975,7 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 				return 1;
 			bool grew_lo = false, grew_hi = false;
 			if (clo > 0) {
-				if (sgh_round_ambiguous(m0, tol + 1e-9 * tol))
+				if (!fast0 && sgh_round_ambiguous(m0, tol + 1e-9 * tol))
 					return 1;
 				if (clo < Lw || clo > n - Hw)
 					return 1;
@@ -978,10 +990,10 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 					grew_lo = true;
 				}
 				Lw = clo;
-				vlo = sg_round_to_WORD(m0);
+				vlo = fast0 ? round_fast(m0, fl0, fr0) : sg_round_to_WORD(m0);
 			}
 			if (chi > 0) {
-				if (sgh_round_ambiguous(m1d, tol + 1e-9 * tol))
+				if (!fast1 && sgh_round_ambiguous(m1d, tol + 1e-9 * tol))
 					return 1;
 				if (chi < Hw || chi > n - Lw)
 					return 1;
@@ -995,7 +1007,7 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 					grew_hi = true;
 				}
 				Hw = chi;
-				vhi = sg_round_to_WORD(m1d);
+				vhi = fast1 ? round_fast(m1d, fl1, fr1) : sg_round_to_WORD(m1d);
 			}
 			if (ciB - ciA != n - Lw - Hw)
 				return 1;	/* inner part and clamp counts disagree: leave it to the sorted path */
@@ -1301,11 +1313,11 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 /* clear the tile's histogram and counters with 16-byte stores (called after the first frame
  * loads are issued, so their latency covers it; the build's start barrier orders it before
  * the first atomic) */
-template <int NI>
+template <int NI, int BW = SghCfg<NI>::WAVES>
 __device__ __forceinline__ void sgh_clear(SghLds<NI> &L, bool wait_prev) {
 	if (wait_prev)
 		__syncthreads();	/* the previous tile's finish is done with L */
-	constexpr int NH = 2 * NI * SGH_HROWS * 64 / 4, NC = 128 * NI / 4, T = 64 * SghCfg<NI>::WAVES;
+	constexpr int NH = 2 * NI * SGH_HROWS * 64 / 4, NC = 128 * NI / 4, T = 64 * BW;
 	uint4 *h = (uint4 *)&L.h[0][0][0];
 	const uint4 z = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
@@ -1456,12 +1468,12 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, const SghRo &r
 #define SGH_WINS_ORDER 1	/* WINSORIZED finish: columns with zeros / 65535s first (sgh_tile) */
 #endif
 
-template <bool EDGE, int NORM, int NI, int NB>
+template <bool EDGE, int NORM, int NI, int NB, int BW = SghCfg<NI>::WAVES>
 __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const SghRo &ro, SghLds<NI> &L, const SghFrame &F,
 		int wave, int lane, uint32_t (&lo2)[NI], uint32_t (&nonzero)[NI], uint32_t (&nsat)[NI], int &counted,
 		bool wait_prev) {
 	constexpr int MB = 8;
-	constexpr int WAVES = SghCfg<NI>::WAVES;
+	constexpr int WAVES = BW;	/* the waves building the tile */
 	constexpr int STEP = 16 * WAVES;	/* frames between a wave's consecutive blocks */
 	const int N = p.N;
 	uint32_t *const h = &L.h[0][0][0];
@@ -1496,7 +1508,7 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
 			loadh(fb, 1, buf[b][1], fix[b][1]);
 		}
 	}
-	sgh_clear(L, wait_prev);
+	sgh_clear<NI, BW>(L, wait_prev);
 	const bool nocentre = p.dbg == 15;	/* A/B: loads only, no centre and no start barrier */
 	static_assert(!SGH_CENTER2W || SGH_CENTER == 2 * MB, "two half blocks make the centre sample");
 	if (SGH_CENTER2W && !nocentre) {
@@ -1845,4 +1857,121 @@ template __global__ void k_stack_hist<4, 0, 2>(SgStackParams, const int *, const
 /* threads per histogram workgroup (the host's launch shape) */
 int sgh_block_threads(int ni) {
 	return ni == 2 ? 64 * SghCfg<2>::WAVES : 64 * SghCfg<1>::WAVES;
+}
+
+/* ------------------------------------------------------------------------------------
+ * Wave-specialised persistent SIGMA kernel (SG_HIST_WS=1, no normalisation).  One 8-wave
+ * workgroup per CU walks its tiles of 256 pixels (512-byte row segments, the faster stream
+ * floor, tools/bw_probe4.hip) with TWO histograms in LDS: in step k waves 0-3 build tile k
+ * into histogram k & 1 while waves 4-7 finish tile k - 1 from the other, so a tile's finish
+ * runs under the next tile's loads instead of holding the tile's slot.  Every wave passes
+ * the same three barriers per step (the build's start barriers, then the step's end).
+ * Tiles: XCD x (workgroups b with b % 8 == x, dealt round robin) owns the contiguous eighth
+ * x of the tile range and its workgroups interleave over it, so the tiles in flight on an
+ * XCD are neighbours (their shifted rows share 128-B lines in that XCD's L2).
+ * ------------------------------------------------------------------------------------ */
+#define SGH_WS_BW 4		/* builder waves (one per SIMD) */
+#ifndef SGH_WS_NB
+#define SGH_WS_NB 2		/* 16-frame blocks in flight per builder wave */
+#endif
+struct SghWsLds {
+	SghLds<2> L[2];
+};
+
+template <int NORM>
+__global__ void __launch_bounds__(512)
+k_stack_hist_ws(SgStackParams p, const int *__restrict__ tab, const int4 *__restrict__ norm,
+		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
+	constexpr int NI = 2, COLS = 256, FW = 8 - SGH_WS_BW;
+	SghRo ro;
+	ro.tab = tab;
+	ro.norm = norm;
+	ro.npad = p.hist_npad;
+	__shared__ SghWsLds S;
+	const int tid = threadIdx.x, lane = tid & 63;
+	const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+	const int ntx = (p.W + COLS - 1) / COLS, nrows = p.row_end - p.row_begin;
+	const int ntiles = ntx * nrows * p.C;
+	const int G8 = (int)gridDim.x >> 3, xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
+	const int t0 = (int)((long long)xcd * ntiles / 8), t1 = (int)((long long)(xcd + 1) * ntiles / 8);
+	const int K = slot < t1 - t0 ? (t1 - t0 - slot + G8 - 1) / G8 : 0;
+	struct Tile {
+		int R, c, x0;
+		bool interior;
+	};
+	auto tile = [&](int k) {
+		int bid = t0 + slot + k * G8;
+		Tile t;
+		const int xt = bid % ntx;
+		bid /= ntx;
+		t.R = p.row_begin + bid % nrows;
+		t.c = bid / nrows;
+		t.x0 = xt * COLS;
+		t.interior = t.x0 >= p.hist_maxsx && t.x0 + COLS + p.hist_maxsx <= p.W;
+		return t;
+	};
+	const bool builder = wave < SGH_WS_BW;
+	if (builder)	/* the loads issue ahead of the finishers on the same SIMD */
+		__builtin_amdgcn_s_setprio(1);
+	for (int k = 0; k <= K; k++) {
+		SghLds<NI> &Lb = S.L[k & 1], &Lf = S.L[(k & 1) ^ 1];
+		if (builder) {
+			if (k < K) {
+				const Tile t = tile(k);
+				SghFrame F;
+				F.plane0 = (const char *)(p.frames + (int64_t)t.c * p.plane_stride);
+				F.fstride2 = p.frame_stride * 2;
+				F.plane_bytes = (uint32_t)p.H * (uint32_t)p.W * 2u;
+				F.w2 = p.W * 2;
+				F.rw2 = t.R * p.W * 2;
+				F.xa2 = (uint32_t)(t.x0 + 2 * lane) * 2u;
+				F.x02 = (uint32_t)t.x0 * 2u;
+				uint32_t nonzero[NI], nsat[NI], lo2[NI];
+#pragma unroll
+				for (int i = 0; i < NI; i++)
+					nonzero[i] = nsat[i] = 0;
+				int counted = 0;
+				/* two barriers inside: centre sample published, band starts published */
+				if (t.interior)
+					sgh_build_half<false, NORM, NI, SGH_WS_NB, SGH_WS_BW>(p, ro, Lb, F, wave, lane, lo2, nonzero, nsat,
+							counted, false);
+				else
+					sgh_build_half<true, NORM, NI, SGH_WS_NB, SGH_WS_BW>(p, ro, Lb, F, wave, lane, lo2, nonzero, nsat,
+							counted, false);
+				if (counted) {
+#pragma unroll
+					for (int i = 0; i < NI; i++) {
+						atomicAdd(&Lb.nz[128 * i + lane], (uint32_t)counted - (nonzero[i] & 0xFFFFu));
+						atomicAdd(&Lb.nz[128 * i + 64 + lane], (uint32_t)counted - (nonzero[i] >> 16));
+						atomicAdd(&Lb.ns[128 * i + lane], nsat[i] & 0xFFFFu);
+						atomicAdd(&Lb.ns[128 * i + 64 + lane], nsat[i] >> 16);
+					}
+				}
+			} else {
+				__syncthreads();
+				__syncthreads();
+			}
+		} else {
+			__syncthreads();
+			__syncthreads();
+			if (k > 0) {
+				const Tile t = tile(k - 1);
+				auto col_x = [&](int col) { return t.x0 + 128 * (col >> 7) + 2 * (col & 63) + ((col >> 6) & 1); };
+				auto col_lo = [&](int col) {
+					return (int)((Lf.lo2[col >> 7][col & 63] >> (16 * ((col >> 6) & 1))) & 0xFFFFu);
+				};
+				const int half = lane & 1;
+				for (int col = 32 * (wave - SGH_WS_BW) + (lane >> 1); col < COLS; col += 32 * FW)
+					sgh_finish2<2, true, NI, NORM == 1 || NORM == 3>(p, Lf, col, half, col_lo(col), t.R, t.c, col_x(col),
+							redo_count, redo_list, t.interior);
+			}
+		}
+		__syncthreads();	/* tile k built, tile k - 1 finished: the histograms swap roles */
+	}
+}
+template __global__ void k_stack_hist_ws<0>(SgStackParams, const int *, const int4 *, unsigned int *, unsigned int *);
+
+/* LDS bytes of the wave-specialised kernel (the host checks the device can hold them) */
+size_t sgh_ws_lds_bytes() {
+	return sizeof(SghWsLds);
 }
