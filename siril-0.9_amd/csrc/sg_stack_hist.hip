@@ -1313,10 +1313,14 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 /* clear the tile's histogram and counters with 16-byte stores (called after the first frame
  * loads are issued, so their latency covers it; the build's start barrier orders it before
  * the first atomic) */
-template <int NI, int BW = SghCfg<NI>::WAVES>
-__device__ __forceinline__ void sgh_clear(SghLds<NI> &L, bool wait_prev) {
+struct SghWgBarrier {
+	__device__ __forceinline__ void operator()() const { __syncthreads(); }
+	__device__ __forceinline__ void wait_prev() const { __syncthreads(); }
+};
+template <int NI, int BW = SghCfg<NI>::WAVES, class BAR = SghWgBarrier>
+__device__ __forceinline__ void sgh_clear(SghLds<NI> &L, bool wait_prev, const BAR &bar = BAR()) {
 	if (wait_prev)
-		__syncthreads();	/* the previous tile's finish is done with L */
+		bar.wait_prev();	/* the previous tile's finish is done with L */
 	constexpr int NH = 2 * NI * SGH_HROWS * 64 / 4, NC = 128 * NI / 4, T = 64 * BW;
 	uint4 *h = (uint4 *)&L.h[0][0][0];
 	const uint4 z = make_uint4(0u, 0u, 0u, 0u);
@@ -1468,10 +1472,10 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, const SghRo &r
 #define SGH_WINS_ORDER 1	/* WINSORIZED finish: columns with zeros / 65535s first (sgh_tile) */
 #endif
 
-template <bool EDGE, int NORM, int NI, int NB, int BW = SghCfg<NI>::WAVES>
+template <bool EDGE, int NORM, int NI, int NB, int BW = SghCfg<NI>::WAVES, class BAR = SghWgBarrier>
 __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const SghRo &ro, SghLds<NI> &L, const SghFrame &F,
 		int wave, int lane, uint32_t (&lo2)[NI], uint32_t (&nonzero)[NI], uint32_t (&nsat)[NI], int &counted,
-		bool wait_prev) {
+		bool wait_prev, const BAR &bar = BAR()) {
 	constexpr int MB = 8;
 	constexpr int WAVES = BW;	/* the waves building the tile */
 	constexpr int STEP = 16 * WAVES;	/* frames between a wave's consecutive blocks */
@@ -1508,7 +1512,7 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
 			loadh(fb, 1, buf[b][1], fix[b][1]);
 		}
 	}
-	sgh_clear<NI, BW>(L, wait_prev);
+	sgh_clear<NI, BW>(L, wait_prev, bar);
 	const bool nocentre = p.dbg == 15;	/* A/B: loads only, no centre and no start barrier */
 	static_assert(!SGH_CENTER2W || SGH_CENTER == 2 * MB, "two half blocks make the centre sample");
 	if (SGH_CENTER2W && !nocentre) {
@@ -1529,7 +1533,7 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
 					L.cs[i][m][lane] = v;
 				}
 		}
-		__syncthreads();
+		bar();
 		if (wave == 0) {
 #pragma unroll
 			for (int i = 0; i < NI; i++) {
@@ -1569,7 +1573,7 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
 		}
 	}
 	if (!nocentre)
-		__syncthreads();	/* histogram cleared, band starts published */
+		bar();	/* histogram cleared, band starts published */
 #pragma unroll
 	for (int i = 0; i < NI; i++)
 		lo2[i] = nocentre ? 0u : L.lo2[i][lane];
@@ -1975,3 +1979,131 @@ template __global__ void k_stack_hist_ws<0>(SgStackParams, const int *, const in
 size_t sgh_ws_lds_bytes() {
 	return sizeof(SghWsLds);
 }
+
+/* ------------------------------------------------------------------------------------
+ * The same walk with the two roles decoupled (SG_HIST_WS=2): no workgroup barrier after the
+ * start.  LDS counters, monotone within the launch: `built` (+1 per builder wave and tile),
+ * `freed` (+1 per finisher wave and tile) and the builders' own group barrier.  A builder
+ * issues tile k's first loads, then waits for tile k - 2's finish before clearing its
+ * histogram; a finisher waits for tile k's build.  A signal is this wave's LDS work made
+ * visible (workgroup release) and one lane's atomic add; a wait polls with s_sleep.
+ * ------------------------------------------------------------------------------------ */
+struct SghWs2Lds {
+	SghLds<2> L[2];
+	uint32_t bar_ctr, built, freed;
+};
+__device__ __forceinline__ void sgh_wait_ge(uint32_t *a, uint32_t target) {
+	while (__hip_atomic_load(a, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+		__builtin_amdgcn_s_sleep(1);
+}
+__device__ __forceinline__ void sgh_signal(uint32_t *a, int lane) {
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+	if (lane == 0)
+		__hip_atomic_fetch_add(a, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+struct SghGroupBarrier {
+	uint32_t *ctr, *freed;
+	int lane;
+	uint32_t *gen;		/* this wave's barrier target (in registers: the struct is a local) */
+	uint32_t prev_target;	/* freed count that makes the histogram free again */
+	__device__ __forceinline__ void operator()() const {
+		sgh_signal(ctr, lane);
+		*gen += SGH_WS_BW;
+		sgh_wait_ge(ctr, *gen);
+	}
+	__device__ __forceinline__ void wait_prev() const { sgh_wait_ge(freed, prev_target); }
+};
+
+template <int NORM>
+__global__ void __launch_bounds__(512)
+k_stack_hist_ws2(SgStackParams p, const int *__restrict__ tab, const int4 *__restrict__ norm,
+		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
+	constexpr int NI = 2, COLS = 256, FW = 8 - SGH_WS_BW;
+	SghRo ro;
+	ro.tab = tab;
+	ro.norm = norm;
+	ro.npad = p.hist_npad;
+	__shared__ SghWs2Lds S;
+	const int tid = threadIdx.x, lane = tid & 63;
+	const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+	const int ntx = (p.W + COLS - 1) / COLS, nrows = p.row_end - p.row_begin;
+	const int ntiles = ntx * nrows * p.C;
+	const int G8 = (int)gridDim.x >> 3, xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
+	const int t0 = (int)((long long)xcd * ntiles / 8), t1 = (int)((long long)(xcd + 1) * ntiles / 8);
+	const int K = slot < t1 - t0 ? (t1 - t0 - slot + G8 - 1) / G8 : 0;
+	struct Tile {
+		int R, c, x0;
+		bool interior;
+	};
+	auto tile = [&](int k) {
+		int bid = t0 + slot + k * G8;
+		Tile t;
+		const int xt = bid % ntx;
+		bid /= ntx;
+		t.R = p.row_begin + bid % nrows;
+		t.c = bid / nrows;
+		t.x0 = xt * COLS;
+		t.interior = t.x0 >= p.hist_maxsx && t.x0 + COLS + p.hist_maxsx <= p.W;
+		return t;
+	};
+	if (tid == 0) {
+		S.bar_ctr = 0;
+		S.built = 0;
+		S.freed = 0;
+	}
+	__syncthreads();
+	if (wave < SGH_WS_BW) {
+		__builtin_amdgcn_s_setprio(1);	/* the loads issue ahead of the finishers on the same SIMD */
+		uint32_t gen = 0;
+		for (int k = 0; k < K; k++) {
+			SghLds<NI> &Lb = S.L[k & 1];
+			const Tile t = tile(k);
+			SghFrame F;
+			F.plane0 = (const char *)(p.frames + (int64_t)t.c * p.plane_stride);
+			F.fstride2 = p.frame_stride * 2;
+			F.plane_bytes = (uint32_t)p.H * (uint32_t)p.W * 2u;
+			F.w2 = p.W * 2;
+			F.rw2 = t.R * p.W * 2;
+			F.xa2 = (uint32_t)(t.x0 + 2 * lane) * 2u;
+			F.x02 = (uint32_t)t.x0 * 2u;
+			uint32_t nonzero[NI], nsat[NI], lo2[NI];
+#pragma unroll
+			for (int i = 0; i < NI; i++)
+				nonzero[i] = nsat[i] = 0;
+			int counted = 0;
+			const SghGroupBarrier bar{&S.bar_ctr, &S.freed, lane, &gen, (uint32_t)FW * (uint32_t)(k > 1 ? k - 1 : 0)};
+			if (t.interior)
+				sgh_build_half<false, NORM, NI, SGH_WS_NB, SGH_WS_BW>(p, ro, Lb, F, wave, lane, lo2, nonzero, nsat,
+						counted, k > 1, bar);
+			else
+				sgh_build_half<true, NORM, NI, SGH_WS_NB, SGH_WS_BW>(p, ro, Lb, F, wave, lane, lo2, nonzero, nsat,
+						counted, k > 1, bar);
+			if (counted) {
+#pragma unroll
+				for (int i = 0; i < NI; i++) {
+					atomicAdd(&Lb.nz[128 * i + lane], (uint32_t)counted - (nonzero[i] & 0xFFFFu));
+					atomicAdd(&Lb.nz[128 * i + 64 + lane], (uint32_t)counted - (nonzero[i] >> 16));
+					atomicAdd(&Lb.ns[128 * i + lane], nsat[i] & 0xFFFFu);
+					atomicAdd(&Lb.ns[128 * i + 64 + lane], nsat[i] >> 16);
+				}
+			}
+			sgh_signal(&S.built, lane);
+		}
+	} else {
+		for (int k = 0; k < K; k++) {
+			sgh_wait_ge(&S.built, (uint32_t)SGH_WS_BW * (uint32_t)(k + 1));
+			SghLds<NI> &Lf = S.L[k & 1];
+			const Tile t = tile(k);
+			auto col_x = [&](int col) { return t.x0 + 128 * (col >> 7) + 2 * (col & 63) + ((col >> 6) & 1); };
+			auto col_lo = [&](int col) {
+				return (int)((Lf.lo2[col >> 7][col & 63] >> (16 * ((col >> 6) & 1))) & 0xFFFFu);
+			};
+			const int half = lane & 1;
+			for (int col = 32 * (wave - SGH_WS_BW) + (lane >> 1); col < COLS; col += 32 * FW)
+				sgh_finish2<2, true, NI, NORM == 1 || NORM == 3>(p, Lf, col, half, col_lo(col), t.R, t.c, col_x(col),
+						redo_count, redo_list, t.interior);
+			sgh_signal(&S.freed, lane);
+		}
+	}
+}
+template __global__ void k_stack_hist_ws2<0>(SgStackParams, const int *, const int4 *, unsigned int *, unsigned int *);

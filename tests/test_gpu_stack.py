@@ -378,16 +378,18 @@ def test_hist_winsorized_iteration_cap(gpu_ctx, cap):
         assert st.chain_pixels > 0.2 * H * W, st.chain_pixels   # the cap did send pixels away
 
 
+@pytest.mark.parametrize("ws", ["1", "2"])
 @pytest.mark.parametrize("H,W,N", [(96, 1024, 40), (8, 700, 24), (300, 1536, 64)])
-def test_hist_wave_specialised_sigma(H, W, N):
-    """SG_HIST_WS=1: the persistent wave-specialised SIGMA kernel (builders / finishers on two
-    LDS histograms) gives the oracle's image and counters; the shapes hold more tiles than
-    workgroups (several steps per workgroup), image-edge tiles and a partial last tile"""
+def test_hist_wave_specialised_sigma(H, W, N, ws):
+    """SG_HIST_WS=1 / 2: the persistent wave-specialised SIGMA kernels (builders / finishers on
+    two LDS histograms; workgroup barriers per step, or LDS counters) give the oracle's image
+    and counters; the shapes hold more tiles than workgroups (several steps per workgroup),
+    image-edge tiles and a partial last tile"""
     import os
     frames = orc.synth(N, 1, H, W, seed=700 + W + N, maxshift=9)
     sx, sy = orc.synth_shifts(N, seed=700 + W + N, maxshift=9)
     old = os.environ.get("SG_HIST_WS")
-    os.environ["SG_HIST_WS"] = "1"
+    os.environ["SG_HIST_WS"] = ws
     try:
         with sg.Context() as c:
             out, rej, st = _stack_path(c, frames, sg.SIGMA, (4.0, 3.0), sx, sy, max_thread=1)
