@@ -40,7 +40,8 @@ for step in "$@"; do
     test|testall)
       k=(); [ -n "$spec" ] && k=(-k "$spec")
       x=-x; [ "$kind" = testall ] && x=--maxfail=8
-      timeout -k 10 900 python -u -m pytest tests -m gpu $x -v --timeout 200 --timeout-method thread "${k[@]}" \
+      lim=900; [ -n "$spec" ] && lim=300     # a selection runs under a shorter limit
+      timeout -k 10 $lim python -u -m pytest tests -m gpu $x -v --timeout 200 --timeout-method thread "${k[@]}" \
         > "$O/pytest_gpu.log" 2>&1; rc=$?
       # testall goes on after plain test failures (pytest exit 1), never after a crash or a timeout
       if [ $rc -ne 0 ] && { [ "$kind" = test ] || [ $rc -ne 1 ]; }; then fail test "$O/pytest_gpu.log"; fi

@@ -2107,3 +2107,227 @@ k_stack_hist_ws2(SgStackParams p, const int *__restrict__ tab, const int4 *__res
 	}
 }
 template __global__ void k_stack_hist_ws2<0>(SgStackParams, const int *, const int4 *, unsigned int *, unsigned int *);
+
+/* ------------------------------------------------------------------------------------
+ * WS3 (SG_HIST_WS=3): WS2 with the builders' frame stream running across tiles.  A builder
+ * wave's refills after its last block of tile k load the first blocks of tile k + 1, so the
+ * next tile's centre sample is in registers when its histogram is cleared and no tile
+ * starts on an empty load queue (in WS2 every tile opened with a full memory latency, its
+ * CU's only loads being its own builders').  N % 64 == 0 (every block whole; the host checks).
+ * ------------------------------------------------------------------------------------ */
+struct SghWsTile {
+	int R, c, x0;
+	bool interior;
+};
+__device__ __forceinline__ SghFrame sgh_ws_frame(const SgStackParams &p, const SghWsTile &t, int lane) {
+	SghFrame F;
+	F.plane0 = (const char *)(p.frames + (int64_t)t.c * p.plane_stride);
+	F.fstride2 = p.frame_stride * 2;
+	F.plane_bytes = (uint32_t)p.H * (uint32_t)p.W * 2u;
+	F.w2 = p.W * 2;
+	F.rw2 = t.R * p.W * 2;
+	F.xa2 = (uint32_t)(t.x0 + 2 * lane) * 2u;
+	F.x02 = (uint32_t)t.x0 * 2u;
+	return F;
+}
+
+template <int NB, class TILE>
+__device__ __forceinline__ void sgh_ws3_builder(const SgStackParams &p, const SghRo &ro, SghWs2Lds &S, int K,
+		const TILE &tile, int wave, int lane) {
+	constexpr int NI = 2, MB = 8, BW = SGH_WS_BW, STEP = 16 * BW, FW = 8 - BW;
+	const int N = p.N, J = N / STEP;	/* blocks of 16 frames per wave and tile */
+	const uint32_t l4 = (uint32_t)lane * 4u;
+	const uint32_t k1 = sgh_opaque(0x00010001u), ksat = sgh_opaque(0xFFFEFFFEu);
+	uint32_t buf[NB][2][MB][NI], fix[NB][2][NI];
+	SghTab16 T;
+	uint32_t gen = 0;
+	const SghGroupBarrier bar{&S.bar_ctr, &S.freed, lane, &gen, 0u};
+	/* block j (frames 16 wave + j STEP ..) of a tile into buffer b (both halves) */
+	auto load = [&](const SghFrame &F, bool interior, int j, uint32_t (&d)[2][MB][NI], uint32_t (&fx)[2][NI]) {
+		const int f16 = 16 * wave + j * STEP;
+		sgh_tab16(ro, f16, T);
+		if (interior) {
+			sgh_loadblk<true, false, NI, MB, 0>(F, T, N, f16, d[0], fx[0]);
+			sgh_loadblk<true, false, NI, MB, 8>(F, T, N, f16 + 8, d[1], fx[1]);
+		} else {
+			sgh_loadblk<true, true, NI, MB, 0>(F, T, N, f16, d[0], fx[0]);
+			sgh_loadblk<true, true, NI, MB, 8>(F, T, N, f16 + 8, d[1], fx[1]);
+		}
+	};
+	SghWsTile tc = tile(0);
+	SghFrame Fc = sgh_ws_frame(p, tc, lane);
+#pragma unroll
+	for (int b = 0; b < NB; b++) {
+#pragma unroll
+		for (int i = 0; i < NI; i++)
+			fix[b][0][i] = fix[b][1][i] = 0;
+		if (b < J && K > 0)
+			load(Fc, tc.interior, b, buf[b], fix[b]);
+	}
+	for (int k = 0; k < K; k++) {
+		SghLds<NI> &L = S.L[k & 1];
+		const bool has_next = k + 1 < K;
+		const SghWsTile tn = has_next ? tile(k + 1) : tc;
+		const SghFrame Fn = sgh_ws_frame(p, tn, lane);
+		if (k > 1)
+			sgh_wait_ge(&S.freed, (uint32_t)FW * (uint32_t)(k - 1));	/* tile k - 2 finished */
+		sgh_clear<NI, BW>(L, false);
+		/* centre sample: the first half blocks of waves 0 and 1 (frames 0..7, 16..23) */
+		if (wave == 1) {
+#pragma unroll
+			for (int i = 0; i < NI; i++)
+#pragma unroll
+				for (int m = 0; m < MB; m++)
+					L.cs[i][m][lane] = tc.interior ? buf[0][0][m][i] : sgh_fixup<true>(buf[0][0][m][i], fix[0][0][i], m);
+		}
+		bar();
+		if (wave == 0) {
+#pragma unroll
+			for (int i = 0; i < NI; i++) {
+				uint32_t p16[SGH_CENTER];
+#pragma unroll
+				for (int m = 0; m < MB; m++) {
+					p16[m] = tc.interior ? buf[0][0][m][i] : sgh_fixup<true>(buf[0][0][m][i], fix[0][0][i], m);
+					p16[MB + m] = L.cs[i][m][lane];
+				}
+				int la, lb;
+				sgh_centre2(p16, la, lb);
+				L.lo2[i][lane] = (uint32_t)la | ((uint32_t)lb << 16);
+			}
+		}
+		bar();	/* histogram cleared, band starts published */
+		uint32_t lo2[NI], nonzero[NI], nsat[NI];
+#pragma unroll
+		for (int i = 0; i < NI; i++) {
+			lo2[i] = L.lo2[i][lane];
+			nonzero[i] = nsat[i] = 0;
+		}
+		uint32_t *const h = &L.h[0][0][0];
+		auto binh = [&](const uint32_t (&raw)[MB][NI], const uint32_t (&fx)[NI]) {
+			if (tc.interior) {
+#pragma unroll
+				for (int m = 0; m < MB; m += 2)
+#pragma unroll
+					for (int i = 0; i < NI; i++)
+						sgh_bin_pair2(h + i * (2 * SGH_HROWS * 64), l4, lo2[i], raw[m][i], raw[m + 1][i], nonzero[i],
+								nsat[i], k1, ksat);
+			} else {
+#pragma unroll
+				for (int m = 0; m < MB; m++)
+#pragma unroll
+					for (int i = 0; i < NI; i++)
+						sgh_bin_pair(h + i * (2 * SGH_HROWS * 64), l4, lo2[i], sgh_fixup<true>(raw[m][i], fx[i], m),
+								nonzero[i], nsat[i], k1, ksat);
+			}
+		};
+		for (int j0 = 0; j0 < J; j0 += NB) {
+#pragma unroll
+			for (int b = 0; b < NB; b++) {
+				const int j = j0 + b;
+				if (j < J) {
+					/* the refill: block j + NB of this tile, else the next tile's block j + NB - J */
+					const int jn = j + NB;
+					const bool mine = jn < J, nxt = !mine && has_next;
+					const int jt = mine ? jn : jn - J;
+					const SghFrame &Ft = mine ? Fc : Fn;
+					const bool it = mine ? tc.interior : tn.interior;
+					uint32_t (&d)[2][MB][NI] = buf[b];
+					uint32_t (&fx)[2][NI] = fix[b];
+					binh(d[0], fx[0]);
+					__builtin_amdgcn_sched_barrier(0);
+					if (mine || nxt) {
+						const int f16 = 16 * wave + jt * STEP;
+						sgh_tab16(ro, f16, T);
+						if (it)
+							sgh_loadblk<true, false, NI, MB, 0>(Ft, T, N, f16, d[0], fx[0]);
+						else
+							sgh_loadblk<true, true, NI, MB, 0>(Ft, T, N, f16, d[0], fx[0]);
+					}
+					__builtin_amdgcn_sched_barrier(0);
+					binh(d[1], fx[1]);
+					__builtin_amdgcn_sched_barrier(0);
+					if (mine || nxt) {
+						const int f16 = 16 * wave + jt * STEP;
+						if (it)
+							sgh_loadblk<true, false, NI, MB, 8>(Ft, T, N, f16 + 8, d[1], fx[1]);
+						else
+							sgh_loadblk<true, true, NI, MB, 8>(Ft, T, N, f16 + 8, d[1], fx[1]);
+					}
+					__builtin_amdgcn_sched_barrier(0);
+				}
+			}
+		}
+		const uint32_t counted = (uint32_t)(J * 16);
+#pragma unroll
+		for (int i = 0; i < NI; i++) {
+			atomicAdd(&L.nz[128 * i + lane], counted - (nonzero[i] & 0xFFFFu));
+			atomicAdd(&L.nz[128 * i + 64 + lane], counted - (nonzero[i] >> 16));
+			atomicAdd(&L.ns[128 * i + lane], nsat[i] & 0xFFFFu);
+			atomicAdd(&L.ns[128 * i + 64 + lane], nsat[i] >> 16);
+		}
+		sgh_signal(&S.built, lane);
+		tc = tn;
+		Fc = Fn;
+	}
+}
+
+template <int NORM>
+__global__ void __launch_bounds__(512)
+k_stack_hist_ws3(SgStackParams p, const int *__restrict__ tab, const int4 *__restrict__ norm,
+		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
+	static_assert(NORM == 0, "WS3: no normalisation");
+	constexpr int NI = 2, COLS = 256, FW = 8 - SGH_WS_BW;
+	SghRo ro;
+	ro.tab = tab;
+	ro.norm = norm;
+	ro.npad = p.hist_npad;
+	__shared__ SghWs2Lds S;
+	const int tid = threadIdx.x, lane = tid & 63;
+	const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+	const int ntx = (p.W + COLS - 1) / COLS, nrows = p.row_end - p.row_begin;
+	const int ntiles = ntx * nrows * p.C;
+	const int G8 = (int)gridDim.x >> 3, xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
+	const int t0 = (int)((long long)xcd * ntiles / 8), t1 = (int)((long long)(xcd + 1) * ntiles / 8);
+	const int K = slot < t1 - t0 ? (t1 - t0 - slot + G8 - 1) / G8 : 0;
+	auto tile = [&](int k) {
+		int bid = t0 + slot + k * G8;
+		SghWsTile t;
+		const int xt = bid % ntx;
+		bid /= ntx;
+		t.R = p.row_begin + bid % nrows;
+		t.c = bid / nrows;
+		t.x0 = xt * COLS;
+		t.interior = t.x0 >= p.hist_maxsx && t.x0 + COLS + p.hist_maxsx <= p.W;
+		return t;
+	};
+	if (tid == 0) {
+		S.bar_ctr = 0;
+		S.built = 0;
+		S.freed = 0;
+	}
+	__syncthreads();
+	if (wave < SGH_WS_BW) {
+		__builtin_amdgcn_s_setprio(1);
+		sgh_ws3_builder<SGH_WS_NB>(p, ro, S, K, tile, wave, lane);
+	} else {
+		for (int k = 0; k < K; k++) {
+			sgh_wait_ge(&S.built, (uint32_t)SGH_WS_BW * (uint32_t)(k + 1));
+			SghLds<NI> &Lf = S.L[k & 1];
+			const SghWsTile t = tile(k);
+			auto col_x = [&](int col) { return t.x0 + 128 * (col >> 7) + 2 * (col & 63) + ((col >> 6) & 1); };
+			auto col_lo = [&](int col) {
+				return (int)((Lf.lo2[col >> 7][col & 63] >> (16 * ((col >> 6) & 1))) & 0xFFFFu);
+			};
+			const int half = lane & 1;
+			for (int col = 32 * (wave - SGH_WS_BW) + (lane >> 1); col < COLS; col += 32 * FW)
+				sgh_finish2<2, true, NI, false>(p, Lf, col, half, col_lo(col), t.R, t.c, col_x(col), redo_count,
+						redo_list, t.interior);
+			sgh_signal(&S.freed, lane);
+		}
+	}
+}
+template __global__ void k_stack_hist_ws3<0>(SgStackParams, const int *, const int4 *, unsigned int *, unsigned int *);
+/* frames per WS3 cross-tile refill period: N must be a multiple (the host checks) */
+int sgh_ws3_frame_quantum() {
+	return 16 * SGH_WS_BW * SGH_WS_NB;
+}

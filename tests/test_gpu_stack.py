@@ -378,16 +378,18 @@ def test_hist_winsorized_iteration_cap(gpu_ctx, cap):
         assert st.chain_pixels > 0.2 * H * W, st.chain_pixels   # the cap did send pixels away
 
 
-@pytest.mark.parametrize("ws", ["1", "2"])
-@pytest.mark.parametrize("H,W,N", [(96, 1024, 40), (8, 700, 24), (300, 1536, 64)])
+@pytest.mark.parametrize("ws", ["1", "2", "3"])
+@pytest.mark.parametrize("H,W,N", [(96, 1024, 40), (8, 700, 24), (300, 1536, 128), (64, 2048, 256)])
 def test_hist_wave_specialised_sigma(H, W, N, ws):
-    """SG_HIST_WS=1 / 2: the persistent wave-specialised SIGMA kernels (builders / finishers on
-    two LDS histograms; workgroup barriers per step, or LDS counters) give the oracle's image
-    and counters; the shapes hold more tiles than workgroups (several steps per workgroup),
-    image-edge tiles and a partial last tile"""
+    """SG_HIST_WS=1 / 2 / 3: the persistent wave-specialised SIGMA kernels (builders / finishers
+    on two LDS histograms; workgroup barriers per step, LDS counters, LDS counters with the
+    builders' frame stream running across tiles: N = 128 and 256 take that path, 24 / 40 fall
+    back to 2) give the oracle's image and counters; the shapes hold more tiles than
+    workgroups (several steps per workgroup), image-edge tiles and a partial last tile"""
     import os
-    frames = orc.synth(N, 1, H, W, seed=700 + W + N, maxshift=9)
-    sx, sy = orc.synth_shifts(N, seed=700 + W + N, maxshift=9)
+    ms = min(9, H // 3)                 # |shifty| below the image height (the oracle's -4 guard)
+    frames = orc.synth(N, 1, H, W, seed=700 + W + N, maxshift=ms)
+    sx, sy = orc.synth_shifts(N, seed=700 + W + N, maxshift=ms)
     old = os.environ.get("SG_HIST_WS")
     os.environ["SG_HIST_WS"] = ws
     try:
