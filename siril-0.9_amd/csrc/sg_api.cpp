@@ -32,17 +32,6 @@ __global__ void k_stack_hist(SgStackParams p, const int *tab, const int4 *norm, 
 void sg_dbg_why_dump(hipStream_t s);
 int sgh_block_threads(int ni);
 __global__ void k_stack_replay(SgStackParams p);
-template <int NORM>
-__global__ void k_stack_hist_ws(SgStackParams p, const int *tab, const int4 *norm, unsigned int *redo_count,
-		unsigned int *redo_list);
-template <int NORM>
-__global__ void k_stack_hist_ws2(SgStackParams p, const int *tab, const int4 *norm, unsigned int *redo_count,
-		unsigned int *redo_list);
-template <int NORM>
-__global__ void k_stack_hist_ws3(SgStackParams p, const int *tab, const int4 *norm, unsigned int *redo_count,
-		unsigned int *redo_list);
-size_t sgh_ws_lds_bytes();
-int sgh_ws3_frame_quantum();
 __global__ void k_redo_to_literal(SgStackParams p, const unsigned int *list, const unsigned int *count,
 		unsigned int maxn);
 __global__ void k_stack_reduce(SgStackParams p);
@@ -568,29 +557,7 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			}
 			const size_t lds_pad = (size_t)ctx->knobs.hist_ldspad;
 			const dim3 hg((unsigned)nblk_h), hb((unsigned)sgh_block_threads(ni));
-			int ncu = 0;
-			if (ctx->knobs.hist_ws)
-				(void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dv.id);
-			/* A/B SG_HIST_WS=1: the wave-specialised persistent SIGMA kernel (one workgroup per CU,
-			 * a multiple of 8 so every XCD holds the same number) */
-			const bool ws = ctx->knobs.hist_ws && p.rejection == SG_SIGMA && norm == 0 && p.dbg == 0 && ncu >= 8;
-			int wsv = ws ? ctx->knobs.hist_ws : 0;
-			if (wsv == 3 && N % sgh_ws3_frame_quantum() != 0)
-				wsv = 2;	/* the cross-tile frame stream needs whole refill periods */
-			const int wscase = 1000 * wsv;
-			switch (wscase + (p.rejection == SG_WINSORIZED ? 10 : 0) + norm + 100 * ni) {
-			case 1100: case 1200:
-				hipLaunchKernelGGL(k_stack_hist_ws<0>, dim3((unsigned)(ncu & ~7)), dim3(512), 0, s, p, p.hist_tab,
-						(const int4 *)p.hist_norm, redo_count, redo_list);
-				break;
-			case 2100: case 2200:
-				hipLaunchKernelGGL(k_stack_hist_ws2<0>, dim3((unsigned)(ncu & ~7)), dim3(512), 0, s, p, p.hist_tab,
-						(const int4 *)p.hist_norm, redo_count, redo_list);
-				break;
-			case 3100: case 3200:
-				hipLaunchKernelGGL(k_stack_hist_ws3<0>, dim3((unsigned)(ncu & ~7)), dim3(512), 0, s, p, p.hist_tab,
-						(const int4 *)p.hist_norm, redo_count, redo_list);
-				break;
+			switch ((p.rejection == SG_WINSORIZED ? 10 : 0) + norm + 100 * ni) {
 			case 100: hipLaunchKernelGGL((k_stack_hist<2, 0, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 101: hipLaunchKernelGGL((k_stack_hist<2, 1, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 102: hipLaunchKernelGGL((k_stack_hist<2, 2, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;

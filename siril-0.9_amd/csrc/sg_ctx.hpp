@@ -65,7 +65,6 @@ struct SgKnobs {
 	int hist_dbg = 0;		/* SG_HIST_DBG: k_stack_hist phase / timing A/B (0 = production) */
 	int hist_prio = 1;		/* SG_HIST_PRIO: build-phase wave priority (1 measured best, scripts/gpu_prio.sh) */
 	int hist_ldspad = 0;		/* SG_HIST_LDSPAD: extra LDS bytes per histogram workgroup (occupancy A/B) */
-	int hist_ws = 0;		/* SG_HIST_WS: wave-specialised persistent SIGMA kernel (A/B): 1 barrier steps, 2 LDS flags, 3 + cross-tile frame stream */
 	int hist_ni = 1;		/* SG_HIST_NI: pixel pairs per lane of the histogram tiles (2: 256-px tiles) */
 	int wins_cap = 64;		/* SG_WINS_CAP: histogram Winsorize inner iterations per pass before the redo list */
 	int redo_replay = 1;		/* SG_REDO_REPLAY: 0 = redo list always through the sorted kernel */
@@ -86,7 +85,6 @@ struct SgKnobs {
 		hist_prio = sg_env_int("SG_HIST_PRIO", 0, 3, 1);
 		hist_ldspad = sg_env_int("SG_HIST_LDSPAD", 0, 160 * 1024, 0);
 		hist_ni = sg_env_int("SG_HIST_NI", 1, 2, 1);
-		hist_ws = sg_env_int("SG_HIST_WS", 0, 3, 0);
 		wins_cap = sg_env_int("SG_WINS_CAP", 4, 100000, 64);
 		redo_replay = sg_env_int("SG_REDO_REPLAY", 0, 1, 1);
 		reduce1 = sg_env_int("SG_REDUCE1", 0, 1, 0);

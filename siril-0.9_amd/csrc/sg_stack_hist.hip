@@ -1862,472 +1862,3 @@ template __global__ void k_stack_hist<4, 0, 2>(SgStackParams, const int *, const
 int sgh_block_threads(int ni) {
 	return ni == 2 ? 64 * SghCfg<2>::WAVES : 64 * SghCfg<1>::WAVES;
 }
-
-/* ------------------------------------------------------------------------------------
- * Wave-specialised persistent SIGMA kernel (SG_HIST_WS=1, no normalisation).  One 8-wave
- * workgroup per CU walks its tiles of 256 pixels (512-byte row segments, the faster stream
- * floor, tools/bw_probe4.hip) with TWO histograms in LDS: in step k waves 0-3 build tile k
- * into histogram k & 1 while waves 4-7 finish tile k - 1 from the other, so a tile's finish
- * runs under the next tile's loads instead of holding the tile's slot.  Every wave passes
- * the same three barriers per step (the build's start barriers, then the step's end).
- * Tiles: XCD x (workgroups b with b % 8 == x, dealt round robin) owns the contiguous eighth
- * x of the tile range and its workgroups interleave over it, so the tiles in flight on an
- * XCD are neighbours (their shifted rows share 128-B lines in that XCD's L2).
- * ------------------------------------------------------------------------------------ */
-#define SGH_WS_BW 4		/* builder waves (one per SIMD) */
-#ifndef SGH_WS_NB
-#define SGH_WS_NB 2		/* 16-frame blocks in flight per builder wave */
-#endif
-struct SghWsLds {
-	SghLds<2> L[2];
-};
-
-template <int NORM>
-__global__ void __launch_bounds__(512)
-k_stack_hist_ws(SgStackParams p, const int *__restrict__ tab, const int4 *__restrict__ norm,
-		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
-	constexpr int NI = 2, COLS = 256, FW = 8 - SGH_WS_BW;
-	SghRo ro;
-	ro.tab = tab;
-	ro.norm = norm;
-	ro.npad = p.hist_npad;
-	__shared__ SghWsLds S;
-	const int tid = threadIdx.x, lane = tid & 63;
-	const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-	const int ntx = (p.W + COLS - 1) / COLS, nrows = p.row_end - p.row_begin;
-	const int ntiles = ntx * nrows * p.C;
-	const int G8 = (int)gridDim.x >> 3, xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
-	const int t0 = (int)((long long)xcd * ntiles / 8), t1 = (int)((long long)(xcd + 1) * ntiles / 8);
-	const int K = slot < t1 - t0 ? (t1 - t0 - slot + G8 - 1) / G8 : 0;
-	struct Tile {
-		int R, c, x0;
-		bool interior;
-	};
-	auto tile = [&](int k) {
-		int bid = t0 + slot + k * G8;
-		Tile t;
-		const int xt = bid % ntx;
-		bid /= ntx;
-		t.R = p.row_begin + bid % nrows;
-		t.c = bid / nrows;
-		t.x0 = xt * COLS;
-		t.interior = t.x0 >= p.hist_maxsx && t.x0 + COLS + p.hist_maxsx <= p.W;
-		return t;
-	};
-	const bool builder = wave < SGH_WS_BW;
-	if (builder)	/* the loads issue ahead of the finishers on the same SIMD */
-		__builtin_amdgcn_s_setprio(1);
-	for (int k = 0; k <= K; k++) {
-		SghLds<NI> &Lb = S.L[k & 1], &Lf = S.L[(k & 1) ^ 1];
-		if (builder) {
-			if (k < K) {
-				const Tile t = tile(k);
-				SghFrame F;
-				F.plane0 = (const char *)(p.frames + (int64_t)t.c * p.plane_stride);
-				F.fstride2 = p.frame_stride * 2;
-				F.plane_bytes = (uint32_t)p.H * (uint32_t)p.W * 2u;
-				F.w2 = p.W * 2;
-				F.rw2 = t.R * p.W * 2;
-				F.xa2 = (uint32_t)(t.x0 + 2 * lane) * 2u;
-				F.x02 = (uint32_t)t.x0 * 2u;
-				uint32_t nonzero[NI], nsat[NI], lo2[NI];
-#pragma unroll
-				for (int i = 0; i < NI; i++)
-					nonzero[i] = nsat[i] = 0;
-				int counted = 0;
-				/* two barriers inside: centre sample published, band starts published */
-				if (t.interior)
-					sgh_build_half<false, NORM, NI, SGH_WS_NB, SGH_WS_BW>(p, ro, Lb, F, wave, lane, lo2, nonzero, nsat,
-							counted, false);
-				else
-					sgh_build_half<true, NORM, NI, SGH_WS_NB, SGH_WS_BW>(p, ro, Lb, F, wave, lane, lo2, nonzero, nsat,
-							counted, false);
-				if (counted) {
-#pragma unroll
-					for (int i = 0; i < NI; i++) {
-						atomicAdd(&Lb.nz[128 * i + lane], (uint32_t)counted - (nonzero[i] & 0xFFFFu));
-						atomicAdd(&Lb.nz[128 * i + 64 + lane], (uint32_t)counted - (nonzero[i] >> 16));
-						atomicAdd(&Lb.ns[128 * i + lane], nsat[i] & 0xFFFFu);
-						atomicAdd(&Lb.ns[128 * i + 64 + lane], nsat[i] >> 16);
-					}
-				}
-			} else {
-				__syncthreads();
-				__syncthreads();
-			}
-		} else {
-			__syncthreads();
-			__syncthreads();
-			if (k > 0) {
-				const Tile t = tile(k - 1);
-				auto col_x = [&](int col) { return t.x0 + 128 * (col >> 7) + 2 * (col & 63) + ((col >> 6) & 1); };
-				auto col_lo = [&](int col) {
-					return (int)((Lf.lo2[col >> 7][col & 63] >> (16 * ((col >> 6) & 1))) & 0xFFFFu);
-				};
-				const int half = lane & 1;
-				for (int col = 32 * (wave - SGH_WS_BW) + (lane >> 1); col < COLS; col += 32 * FW)
-					sgh_finish2<2, true, NI, NORM == 1 || NORM == 3>(p, Lf, col, half, col_lo(col), t.R, t.c, col_x(col),
-							redo_count, redo_list, t.interior);
-			}
-		}
-		__syncthreads();	/* tile k built, tile k - 1 finished: the histograms swap roles */
-	}
-}
-template __global__ void k_stack_hist_ws<0>(SgStackParams, const int *, const int4 *, unsigned int *, unsigned int *);
-
-/* LDS bytes of the wave-specialised kernel (the host checks the device can hold them) */
-size_t sgh_ws_lds_bytes() {
-	return sizeof(SghWsLds);
-}
-
-/* ------------------------------------------------------------------------------------
- * The same walk with the two roles decoupled (SG_HIST_WS=2): no workgroup barrier after the
- * start.  LDS counters, monotone within the launch: `built` (+1 per builder wave and tile),
- * `freed` (+1 per finisher wave and tile) and the builders' own group barrier.  A builder
- * issues tile k's first loads, then waits for tile k - 2's finish before clearing its
- * histogram; a finisher waits for tile k's build.  A signal is this wave's LDS work made
- * visible (workgroup release) and one lane's atomic add; a wait polls with s_sleep.
- * ------------------------------------------------------------------------------------ */
-struct SghWs2Lds {
-	SghLds<2> L[2];
-	uint32_t bar_ctr, built, freed;
-};
-__device__ __forceinline__ void sgh_wait_ge(uint32_t *a, uint32_t target) {
-	while (__hip_atomic_load(a, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
-		__builtin_amdgcn_s_sleep(1);
-}
-__device__ __forceinline__ void sgh_signal(uint32_t *a, int lane) {
-	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-	if (lane == 0)
-		__hip_atomic_fetch_add(a, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-struct SghGroupBarrier {
-	uint32_t *ctr, *freed;
-	int lane;
-	uint32_t *gen;		/* this wave's barrier target (in registers: the struct is a local) */
-	uint32_t prev_target;	/* freed count that makes the histogram free again */
-	__device__ __forceinline__ void operator()() const {
-		sgh_signal(ctr, lane);
-		*gen += SGH_WS_BW;
-		sgh_wait_ge(ctr, *gen);
-	}
-	__device__ __forceinline__ void wait_prev() const { sgh_wait_ge(freed, prev_target); }
-};
-
-template <int NORM>
-__global__ void __launch_bounds__(512)
-k_stack_hist_ws2(SgStackParams p, const int *__restrict__ tab, const int4 *__restrict__ norm,
-		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
-	constexpr int NI = 2, COLS = 256, FW = 8 - SGH_WS_BW;
-	SghRo ro;
-	ro.tab = tab;
-	ro.norm = norm;
-	ro.npad = p.hist_npad;
-	__shared__ SghWs2Lds S;
-	const int tid = threadIdx.x, lane = tid & 63;
-	const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-	const int ntx = (p.W + COLS - 1) / COLS, nrows = p.row_end - p.row_begin;
-	const int ntiles = ntx * nrows * p.C;
-	const int G8 = (int)gridDim.x >> 3, xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
-	const int t0 = (int)((long long)xcd * ntiles / 8), t1 = (int)((long long)(xcd + 1) * ntiles / 8);
-	const int K = slot < t1 - t0 ? (t1 - t0 - slot + G8 - 1) / G8 : 0;
-	struct Tile {
-		int R, c, x0;
-		bool interior;
-	};
-	auto tile = [&](int k) {
-		int bid = t0 + slot + k * G8;
-		Tile t;
-		const int xt = bid % ntx;
-		bid /= ntx;
-		t.R = p.row_begin + bid % nrows;
-		t.c = bid / nrows;
-		t.x0 = xt * COLS;
-		t.interior = t.x0 >= p.hist_maxsx && t.x0 + COLS + p.hist_maxsx <= p.W;
-		return t;
-	};
-	if (tid == 0) {
-		S.bar_ctr = 0;
-		S.built = 0;
-		S.freed = 0;
-	}
-	__syncthreads();
-	if (wave < SGH_WS_BW) {
-		__builtin_amdgcn_s_setprio(1);	/* the loads issue ahead of the finishers on the same SIMD */
-		uint32_t gen = 0;
-		for (int k = 0; k < K; k++) {
-			SghLds<NI> &Lb = S.L[k & 1];
-			const Tile t = tile(k);
-			SghFrame F;
-			F.plane0 = (const char *)(p.frames + (int64_t)t.c * p.plane_stride);
-			F.fstride2 = p.frame_stride * 2;
-			F.plane_bytes = (uint32_t)p.H * (uint32_t)p.W * 2u;
-			F.w2 = p.W * 2;
-			F.rw2 = t.R * p.W * 2;
-			F.xa2 = (uint32_t)(t.x0 + 2 * lane) * 2u;
-			F.x02 = (uint32_t)t.x0 * 2u;
-			uint32_t nonzero[NI], nsat[NI], lo2[NI];
-#pragma unroll
-			for (int i = 0; i < NI; i++)
-				nonzero[i] = nsat[i] = 0;
-			int counted = 0;
-			const SghGroupBarrier bar{&S.bar_ctr, &S.freed, lane, &gen, (uint32_t)FW * (uint32_t)(k > 1 ? k - 1 : 0)};
-			if (t.interior)
-				sgh_build_half<false, NORM, NI, SGH_WS_NB, SGH_WS_BW>(p, ro, Lb, F, wave, lane, lo2, nonzero, nsat,
-						counted, k > 1, bar);
-			else
-				sgh_build_half<true, NORM, NI, SGH_WS_NB, SGH_WS_BW>(p, ro, Lb, F, wave, lane, lo2, nonzero, nsat,
-						counted, k > 1, bar);
-			if (counted) {
-#pragma unroll
-				for (int i = 0; i < NI; i++) {
-					atomicAdd(&Lb.nz[128 * i + lane], (uint32_t)counted - (nonzero[i] & 0xFFFFu));
-					atomicAdd(&Lb.nz[128 * i + 64 + lane], (uint32_t)counted - (nonzero[i] >> 16));
-					atomicAdd(&Lb.ns[128 * i + lane], nsat[i] & 0xFFFFu);
-					atomicAdd(&Lb.ns[128 * i + 64 + lane], nsat[i] >> 16);
-				}
-			}
-			sgh_signal(&S.built, lane);
-		}
-	} else {
-		for (int k = 0; k < K; k++) {
-			sgh_wait_ge(&S.built, (uint32_t)SGH_WS_BW * (uint32_t)(k + 1));
-			SghLds<NI> &Lf = S.L[k & 1];
-			const Tile t = tile(k);
-			auto col_x = [&](int col) { return t.x0 + 128 * (col >> 7) + 2 * (col & 63) + ((col >> 6) & 1); };
-			auto col_lo = [&](int col) {
-				return (int)((Lf.lo2[col >> 7][col & 63] >> (16 * ((col >> 6) & 1))) & 0xFFFFu);
-			};
-			const int half = lane & 1;
-			for (int col = 32 * (wave - SGH_WS_BW) + (lane >> 1); col < COLS; col += 32 * FW)
-				sgh_finish2<2, true, NI, NORM == 1 || NORM == 3>(p, Lf, col, half, col_lo(col), t.R, t.c, col_x(col),
-						redo_count, redo_list, t.interior);
-			sgh_signal(&S.freed, lane);
-		}
-	}
-}
-template __global__ void k_stack_hist_ws2<0>(SgStackParams, const int *, const int4 *, unsigned int *, unsigned int *);
-
-/* ------------------------------------------------------------------------------------
- * WS3 (SG_HIST_WS=3): WS2 with the builders' frame stream running across tiles.  A builder
- * wave's refills after its last block of tile k load the first blocks of tile k + 1, so the
- * next tile's centre sample is in registers when its histogram is cleared and no tile
- * starts on an empty load queue (in WS2 every tile opened with a full memory latency, its
- * CU's only loads being its own builders').  N % 64 == 0 (every block whole; the host checks).
- * ------------------------------------------------------------------------------------ */
-struct SghWsTile {
-	int R, c, x0;
-	bool interior;
-};
-__device__ __forceinline__ SghFrame sgh_ws_frame(const SgStackParams &p, const SghWsTile &t, int lane) {
-	SghFrame F;
-	F.plane0 = (const char *)(p.frames + (int64_t)t.c * p.plane_stride);
-	F.fstride2 = p.frame_stride * 2;
-	F.plane_bytes = (uint32_t)p.H * (uint32_t)p.W * 2u;
-	F.w2 = p.W * 2;
-	F.rw2 = t.R * p.W * 2;
-	F.xa2 = (uint32_t)(t.x0 + 2 * lane) * 2u;
-	F.x02 = (uint32_t)t.x0 * 2u;
-	return F;
-}
-
-template <int NB, class TILE>
-__device__ __forceinline__ void sgh_ws3_builder(const SgStackParams &p, const SghRo &ro, SghWs2Lds &S, int K,
-		const TILE &tile, int wave, int lane) {
-	constexpr int NI = 2, MB = 8, BW = SGH_WS_BW, STEP = 16 * BW, FW = 8 - BW;
-	const int N = p.N, J = N / STEP;	/* blocks of 16 frames per wave and tile */
-	const uint32_t l4 = (uint32_t)lane * 4u;
-	const uint32_t k1 = sgh_opaque(0x00010001u), ksat = sgh_opaque(0xFFFEFFFEu);
-	uint32_t buf[NB][2][MB][NI], fix[NB][2][NI];
-	SghTab16 T;
-	uint32_t gen = 0;
-	const SghGroupBarrier bar{&S.bar_ctr, &S.freed, lane, &gen, 0u};
-	/* block j (frames 16 wave + j STEP ..) of a tile into buffer b (both halves) */
-	auto load = [&](const SghFrame &F, bool interior, int j, uint32_t (&d)[2][MB][NI], uint32_t (&fx)[2][NI]) {
-		const int f16 = 16 * wave + j * STEP;
-		sgh_tab16(ro, f16, T);
-		if (interior) {
-			sgh_loadblk<true, false, NI, MB, 0>(F, T, N, f16, d[0], fx[0]);
-			sgh_loadblk<true, false, NI, MB, 8>(F, T, N, f16 + 8, d[1], fx[1]);
-		} else {
-			sgh_loadblk<true, true, NI, MB, 0>(F, T, N, f16, d[0], fx[0]);
-			sgh_loadblk<true, true, NI, MB, 8>(F, T, N, f16 + 8, d[1], fx[1]);
-		}
-	};
-	SghWsTile tc = tile(0);
-	SghFrame Fc = sgh_ws_frame(p, tc, lane);
-#pragma unroll
-	for (int b = 0; b < NB; b++) {
-#pragma unroll
-		for (int i = 0; i < NI; i++)
-			fix[b][0][i] = fix[b][1][i] = 0;
-		if (b < J && K > 0)
-			load(Fc, tc.interior, b, buf[b], fix[b]);
-	}
-	for (int k = 0; k < K; k++) {
-		SghLds<NI> &L = S.L[k & 1];
-		const bool has_next = k + 1 < K;
-		const SghWsTile tn = has_next ? tile(k + 1) : tc;
-		const SghFrame Fn = sgh_ws_frame(p, tn, lane);
-		if (k > 1)
-			sgh_wait_ge(&S.freed, (uint32_t)FW * (uint32_t)(k - 1));	/* tile k - 2 finished */
-		sgh_clear<NI, BW>(L, false);
-		/* centre sample: the first half blocks of waves 0 and 1 (frames 0..7, 16..23) */
-		if (wave == 1) {
-#pragma unroll
-			for (int i = 0; i < NI; i++)
-#pragma unroll
-				for (int m = 0; m < MB; m++)
-					L.cs[i][m][lane] = tc.interior ? buf[0][0][m][i] : sgh_fixup<true>(buf[0][0][m][i], fix[0][0][i], m);
-		}
-		bar();
-		if (wave == 0) {
-#pragma unroll
-			for (int i = 0; i < NI; i++) {
-				uint32_t p16[SGH_CENTER];
-#pragma unroll
-				for (int m = 0; m < MB; m++) {
-					p16[m] = tc.interior ? buf[0][0][m][i] : sgh_fixup<true>(buf[0][0][m][i], fix[0][0][i], m);
-					p16[MB + m] = L.cs[i][m][lane];
-				}
-				int la, lb;
-				sgh_centre2(p16, la, lb);
-				L.lo2[i][lane] = (uint32_t)la | ((uint32_t)lb << 16);
-			}
-		}
-		bar();	/* histogram cleared, band starts published */
-		uint32_t lo2[NI], nonzero[NI], nsat[NI];
-#pragma unroll
-		for (int i = 0; i < NI; i++) {
-			lo2[i] = L.lo2[i][lane];
-			nonzero[i] = nsat[i] = 0;
-		}
-		uint32_t *const h = &L.h[0][0][0];
-		auto binh = [&](const uint32_t (&raw)[MB][NI], const uint32_t (&fx)[NI]) {
-			if (tc.interior) {
-#pragma unroll
-				for (int m = 0; m < MB; m += 2)
-#pragma unroll
-					for (int i = 0; i < NI; i++)
-						sgh_bin_pair2(h + i * (2 * SGH_HROWS * 64), l4, lo2[i], raw[m][i], raw[m + 1][i], nonzero[i],
-								nsat[i], k1, ksat);
-			} else {
-#pragma unroll
-				for (int m = 0; m < MB; m++)
-#pragma unroll
-					for (int i = 0; i < NI; i++)
-						sgh_bin_pair(h + i * (2 * SGH_HROWS * 64), l4, lo2[i], sgh_fixup<true>(raw[m][i], fx[i], m),
-								nonzero[i], nsat[i], k1, ksat);
-			}
-		};
-		for (int j0 = 0; j0 < J; j0 += NB) {
-#pragma unroll
-			for (int b = 0; b < NB; b++) {
-				const int j = j0 + b;
-				if (j < J) {
-					/* the refill: block j + NB of this tile, else the next tile's block j + NB - J */
-					const int jn = j + NB;
-					const bool mine = jn < J, nxt = !mine && has_next;
-					const int jt = mine ? jn : jn - J;
-					const SghFrame &Ft = mine ? Fc : Fn;
-					const bool it = mine ? tc.interior : tn.interior;
-					uint32_t (&d)[2][MB][NI] = buf[b];
-					uint32_t (&fx)[2][NI] = fix[b];
-					binh(d[0], fx[0]);
-					__builtin_amdgcn_sched_barrier(0);
-					if (mine || nxt) {
-						const int f16 = 16 * wave + jt * STEP;
-						sgh_tab16(ro, f16, T);
-						if (it)
-							sgh_loadblk<true, false, NI, MB, 0>(Ft, T, N, f16, d[0], fx[0]);
-						else
-							sgh_loadblk<true, true, NI, MB, 0>(Ft, T, N, f16, d[0], fx[0]);
-					}
-					__builtin_amdgcn_sched_barrier(0);
-					binh(d[1], fx[1]);
-					__builtin_amdgcn_sched_barrier(0);
-					if (mine || nxt) {
-						const int f16 = 16 * wave + jt * STEP;
-						if (it)
-							sgh_loadblk<true, false, NI, MB, 8>(Ft, T, N, f16 + 8, d[1], fx[1]);
-						else
-							sgh_loadblk<true, true, NI, MB, 8>(Ft, T, N, f16 + 8, d[1], fx[1]);
-					}
-					__builtin_amdgcn_sched_barrier(0);
-				}
-			}
-		}
-		const uint32_t counted = (uint32_t)(J * 16);
-#pragma unroll
-		for (int i = 0; i < NI; i++) {
-			atomicAdd(&L.nz[128 * i + lane], counted - (nonzero[i] & 0xFFFFu));
-			atomicAdd(&L.nz[128 * i + 64 + lane], counted - (nonzero[i] >> 16));
-			atomicAdd(&L.ns[128 * i + lane], nsat[i] & 0xFFFFu);
-			atomicAdd(&L.ns[128 * i + 64 + lane], nsat[i] >> 16);
-		}
-		sgh_signal(&S.built, lane);
-		tc = tn;
-		Fc = Fn;
-	}
-}
-
-template <int NORM>
-__global__ void __launch_bounds__(512)
-k_stack_hist_ws3(SgStackParams p, const int *__restrict__ tab, const int4 *__restrict__ norm,
-		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
-	static_assert(NORM == 0, "WS3: no normalisation");
-	constexpr int NI = 2, COLS = 256, FW = 8 - SGH_WS_BW;
-	SghRo ro;
-	ro.tab = tab;
-	ro.norm = norm;
-	ro.npad = p.hist_npad;
-	__shared__ SghWs2Lds S;
-	const int tid = threadIdx.x, lane = tid & 63;
-	const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-	const int ntx = (p.W + COLS - 1) / COLS, nrows = p.row_end - p.row_begin;
-	const int ntiles = ntx * nrows * p.C;
-	const int G8 = (int)gridDim.x >> 3, xcd = (int)blockIdx.x & 7, slot = (int)blockIdx.x >> 3;
-	const int t0 = (int)((long long)xcd * ntiles / 8), t1 = (int)((long long)(xcd + 1) * ntiles / 8);
-	const int K = slot < t1 - t0 ? (t1 - t0 - slot + G8 - 1) / G8 : 0;
-	auto tile = [&](int k) {
-		int bid = t0 + slot + k * G8;
-		SghWsTile t;
-		const int xt = bid % ntx;
-		bid /= ntx;
-		t.R = p.row_begin + bid % nrows;
-		t.c = bid / nrows;
-		t.x0 = xt * COLS;
-		t.interior = t.x0 >= p.hist_maxsx && t.x0 + COLS + p.hist_maxsx <= p.W;
-		return t;
-	};
-	if (tid == 0) {
-		S.bar_ctr = 0;
-		S.built = 0;
-		S.freed = 0;
-	}
-	__syncthreads();
-	if (wave < SGH_WS_BW) {
-		__builtin_amdgcn_s_setprio(1);
-		sgh_ws3_builder<SGH_WS_NB>(p, ro, S, K, tile, wave, lane);
-	} else {
-		for (int k = 0; k < K; k++) {
-			sgh_wait_ge(&S.built, (uint32_t)SGH_WS_BW * (uint32_t)(k + 1));
-			SghLds<NI> &Lf = S.L[k & 1];
-			const SghWsTile t = tile(k);
-			auto col_x = [&](int col) { return t.x0 + 128 * (col >> 7) + 2 * (col & 63) + ((col >> 6) & 1); };
-			auto col_lo = [&](int col) {
-				return (int)((Lf.lo2[col >> 7][col & 63] >> (16 * ((col >> 6) & 1))) & 0xFFFFu);
-			};
-			const int half = lane & 1;
-			for (int col = 32 * (wave - SGH_WS_BW) + (lane >> 1); col < COLS; col += 32 * FW)
-				sgh_finish2<2, true, NI, false>(p, Lf, col, half, col_lo(col), t.R, t.c, col_x(col), redo_count,
-						redo_list, t.interior);
-			sgh_signal(&S.freed, lane);
-		}
-	}
-}
-template __global__ void k_stack_hist_ws3<0>(SgStackParams, const int *, const int4 *, unsigned int *, unsigned int *);
-/* frames per WS3 cross-tile refill period: N must be a multiple (the host checks) */
-int sgh_ws3_frame_quantum() {
-	return 16 * SGH_WS_BW * SGH_WS_NB;
-}

@@ -376,32 +376,3 @@ def test_hist_winsorized_iteration_cap(gpu_ctx, cap):
     assert np.array_equal(rej_h, rej_ref), (rej_h, rej_ref)
     if cap == "4":
         assert st.chain_pixels > 0.2 * H * W, st.chain_pixels   # the cap did send pixels away
-
-
-@pytest.mark.parametrize("ws", ["1", "2", "3"])
-@pytest.mark.parametrize("H,W,N", [(96, 1024, 40), (8, 700, 24), (300, 1536, 128), (64, 2048, 256)])
-def test_hist_wave_specialised_sigma(H, W, N, ws):
-    """SG_HIST_WS=1 / 2 / 3: the persistent wave-specialised SIGMA kernels (builders / finishers
-    on two LDS histograms; workgroup barriers per step, LDS counters, LDS counters with the
-    builders' frame stream running across tiles: N = 128 and 256 take that path, 24 / 40 fall
-    back to 2) give the oracle's image and counters; the shapes hold more tiles than
-    workgroups (several steps per workgroup), image-edge tiles and a partial last tile"""
-    import os
-    ms = min(9, H // 3)                 # |shifty| below the image height (the oracle's -4 guard)
-    frames = orc.synth(N, 1, H, W, seed=700 + W + N, maxshift=ms)
-    sx, sy = orc.synth_shifts(N, seed=700 + W + N, maxshift=ms)
-    old = os.environ.get("SG_HIST_WS")
-    os.environ["SG_HIST_WS"] = ws
-    try:
-        with sg.Context() as c:
-            out, rej, st = _stack_path(c, frames, sg.SIGMA, (4.0, 3.0), sx, sy, max_thread=1)
-    finally:
-        if old is None:
-            os.environ.pop("SG_HIST_WS", None)
-        else:
-            os.environ["SG_HIST_WS"] = old
-    rc, ref, rej_ref = orc.stack_rejection(frames, sg.SIGMA, sig=(4.0, 3.0), shiftx=sx, shifty=sy, max_thread=1)
-    assert rc == 0
-    assert st.path == 1
-    assert_same(out, ref, f"ws H={H} W={W} N={N}")
-    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
