@@ -90,6 +90,9 @@ struct alignas(16) SghLds {
 	uint32_t lo2[NI][64];			/* band starts of the lane pixel pairs (u16 halves) */
 	uint32_t cs[NI][8][64];			/* wave 1's first 8 frames for the band centre (SGH_CENTER2W) */
 	uint8_t perm[128];			/* WINSORIZED finish order of the columns (SGH_WINS_ORDER) */
+#ifdef SGH_WPROF
+	uint64_t wp[SghCfg<NI>::WAVES][16];	/* probe build: per-wave region cycles and events (sgh_wp) */
+#endif
 };
 
 /* Finish-phase queries.  The band is cut into SGH_NGRP groups of SGH_GRP dwords (32 bins);
@@ -116,10 +119,14 @@ struct SghPix {
 	 * the halves' prefixes needs no reordering */
 	uint32_t pc[SGH_NGRP], ps[SGH_NGRP], pss[SGH_NGRP];
 	int hx;
+#ifdef SGH_WPROF
+	uint64_t *wp;		/* probe build: this wave's region accumulators in LDS */
+#endif
 	SghM Z;			/* moments of the zeros (and of the border row's normalised zeros, ztab) */
 	int zmax;		/* > 0: the below-band samples include normalised zeros up to this value;
 				 * a count query at v in [0, zmax) or a rank among them is not decided here */
 	SghM T;			/* moments of all samples */
+	double zs, zss;		/* Z.s, Z.ss as doubles (exact: below 2^53) for the Winsorized queries */
 };
 
 /* t[k] for a lane-varying k in [0, 8): a 3-level select tree on the bits of k */
@@ -874,6 +881,110 @@ __device__ __forceinline__ SghM sgh_M_le(const SghPix &P, int v) {
 	return sgh_q_moments(P, q);
 }
 
+/* One threshold query of the Winsorized loop: the samples <= v (count, and their moments
+ * relative to lo as exact doubles) and the neighbouring sample value on one side, dir 0 the
+ * smallest sample > v, dir 1 the largest sample <= v, from ONE read of the group holding v's
+ * bin.  A clamp growth needs all three (the count decides the clamp, the moments leave the
+ * inner part, the neighbour is the inner part's new end), which the round-2 loop formed with
+ * three separate queries (sgh_cnt_le, sgh_M_le, sgh_value_at1: three group reads).  A
+ * neighbour outside the group (or outside the band) comes from a rank query. */
+struct SghX {
+	int c;		/* samples <= v */
+	double s, ss;	/* their sum and sum of squares of (value - lo) */
+	int nb;		/* the neighbouring sample value, or a bound on it (sgh_qx) */
+};
+__device__ __forceinline__ SghX sgh_qx(const SghPix &P, int v, int dir) {
+	int t = v - P.lo;
+	t = t < -1 ? -1 : (t > SGH_BINS - 1 ? SGH_BINS - 1 : t);
+	const int tc = t < 0 ? 0 : t;
+	const int g = tc >> 5;
+	uint32_t d[SGH_GRP];
+	sgh_grp(P, g, d);
+	const int kb = (t >> 2) - g * SGH_GRP;	/* -1 for t = -1: nothing at or below v in the band */
+	const uint32_t mt = 0xFFFFFFFFu >> (24 - 8 * (t & 3));
+	/* the group's dwords masked to the bins <= t (d is then the dwords of the bins > t: d ^ le) */
+	uint32_t le[SGH_GRP];
+#pragma unroll
+	for (int k = 0; k < SGH_GRP; k++)
+		le[k] = d[k] & (k < kb ? 0xFFFFFFFFu : (k == kb ? mt : 0u));
+	uint32_t c = 0, s = 0, ss = 0;
+	sgh_grp_moments(le, c, s, ss);
+	const uint32_t b0 = (uint32_t)g * (4u * SGH_GRP);
+	const uint32_t bc = sgh_pre(P, P.pc, g) + c;
+	const uint32_t bs = sgh_pre(P, P.ps, g) + s + __umul24(b0, c);
+	const uint32_t bss = sgh_pre(P, P.pss, g) + ss + __umul24(2u * b0, s) + __umul24(__umul24(b0, b0), c);
+	SghX x;
+	x.c = P.nz + (int)bc;
+	x.s = P.zs + (double)bs;
+	x.ss = P.zss + (double)bss;
+	if (v < 0) {
+		x.c = 0;
+		x.s = x.ss = 0.0;
+	}
+	if (v >= 65535) {
+		x.c = P.T.c;
+		x.s = (double)P.T.s;
+		x.ss = (double)P.T.ss;
+	}
+	/* neighbour inside the group: the first non-empty bin above t, the last one at or below t */
+	int kf = -1, kl = -1;
+	uint32_t wf = 0, wl = 0;
+#pragma unroll
+	for (int k = SGH_GRP - 1; k >= 0; k--) {
+		const uint32_t gt = d[k] ^ le[k];
+		const bool nzf = gt != 0u;
+		kf = nzf ? k : kf;
+		wf = nzf ? gt : wf;
+	}
+#pragma unroll
+	for (int k = 0; k < SGH_GRP; k++) {
+		const bool nzl = le[k] != 0u;
+		kl = nzl ? k : kl;
+		wl = nzl ? le[k] : wl;
+	}
+	const int base = P.lo + 4 * g * SGH_GRP;
+	const int vf = base + 4 * kf + (int)(__builtin_ctz(wf | 0x80000000u) >> 3);
+	const int vl = base + 4 * kl + (int)((31 - __builtin_clz(wl | 1u)) >> 3);
+	/* a neighbour outside the group is not searched for (on a wave of 64 pixels some lane nearly
+	 * always misses its group, and a rank query for it cost every query its price): the
+	 * answer is then a bound, dir 0 a lower bound on the smallest sample > v (the next group's
+	 * first bin, or v + 1), dir 1 an upper bound on the largest sample <= v (the group's first
+	 * bin - 1, or v) - all the Winsorized loop asks of its inner-part ends (sgh_winsorized) */
+	const int up_lb = t < 0 ? v + 1 : (base + 4 * SGH_GRP > v + 1 ? base + 4 * SGH_GRP : v + 1);
+	const int dn_ub = t < 0 ? v : (base - 1 < v ? base - 1 : v);
+	const bool okf = kf >= 0 && v >= 0, okl = kl >= 0 && v < 65535;
+	x.nb = dir ? (okl ? vl : dn_ub) : (okf ? vf : up_lb);
+	return x;
+}
+
+/* A/B probe build (-DSGH_WPROF): wave time per region of the Winsorized finish.  One active
+ * lane (the first in EXEC) adds the cycles since the wave's previous checkpoint to the region
+ * that ends here, so divergent control flow is counted once per wave; slot 0 = last stamp,
+ * 1..7 regions, 8 inner iterations, 9 passes */
+#ifdef SGH_WPROF
+__device__ __forceinline__ void sgh_wp(uint64_t *w, int region, int cnt = 0) {
+	const uint64_t now = __builtin_readcyclecounter();
+	const uint64_t ex = __builtin_amdgcn_read_exec();
+	if ((int)(threadIdx.x & 63) == __builtin_ctzll(ex)) {
+		if (region >= 0)
+			w[1 + region] += now - w[0];
+		w[0] = now;
+		if (cnt)
+			w[7 + cnt]++;
+	}
+}
+#define SGH_WP(r, c) sgh_wp(P.wp, r, c)
+__device__ __forceinline__ void sgh_wpev(uint64_t *w, int k) {
+	const uint64_t ex = __builtin_amdgcn_read_exec();
+	if ((int)(threadIdx.x & 63) == __builtin_ctzll(ex))
+		w[10 + k]++;
+}
+#define SGH_WPEV(k) sgh_wpev(P.wp, k)
+#else
+#define SGH_WP(r, c)
+#define SGH_WPEV(k)
+#endif
+
 __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int cap, uint16_t *value, uint32_t *rlo_out,
 		uint32_t *rhi_out) {
 	int A = 0, B = 65535, n = N, r = 0, nrem;
@@ -882,18 +993,10 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 #ifdef SGH_WINS_ITERS
 	*rlo_out = 0;
 #endif
-	/* # samples <= v of the low- and high-side threshold queries, cached per side: once sigma
-	 * settles the integer thresholds repeat from one inner iteration to the next, and a wave
-	 * skips the histogram read when none of its lanes misses */
-	int cv0 = -2, ck0 = 0, cv1 = -2, ck1 = 0;
-	auto cnt_cached = [&](int v, int side) -> int {
-		int &cv = side ? cv1 : cv0, &ck = side ? ck1 : ck0;
-		if (v != cv) {
-			ck = sgh_cnt_le(P, v);
-			cv = v;
-		}
-		return ck;
-	};
+	/* smallest / largest kept sample at the start of a pass (a lower / an upper bound from the
+	 * second pass on: the clip queries' neighbours, sgh_qx); the first pass's from two rank
+	 * queries */
+	int klo = sgh_value_at1(P, 0), khi = sgh_value_at1(P, N - 1);
 	do {
 		const long long S = MB.s - MA.s;
 		const long long SS = (long long)(MB.ss - MA.ss);
@@ -903,19 +1006,23 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 		int km1, km2;	/* kept values at the median ranks: fixed for the whole pass */
 		sgh_value_at2(P, g1, g2, km1, km2);
 		double median = (g1 == g2) ? (double)km1 : (double)(km1 + km2) / 2.0;
-		/* inner loop.  The inner part of w is the kept ranks [Lw, n - Hw); its smallest and
-		 * largest values (ulo, uhi) change only when a clamp grows, so a threshold outside
-		 * [ulo, uhi] - the common case once the clamps have settled - is counted without a
-		 * histogram query, and the median of w is vlo, vhi or km1 / km2 */
-		int Lw = 0, Hw = 0, vlo = 0, vhi = 0, IA = A, IB = B;
+		SGH_WP(1, 2);
+		/* inner loop.  The inner part of w is the kept ranks [Lw, n - Hw); ulo <= its smallest
+		 * value and uhi >= its largest (bounds: sgh_qx does not leave a histogram group to find
+		 * them), so a threshold outside [ulo, uhi) - the common case once the clamps have
+		 * settled - needs no histogram query, and one inside it is counted by one sgh_qx, which
+		 * also gives the moments that leave the inner part and its new end.  The median of w is
+		 * vlo, vhi or km1 / km2 */
+		int Lw = 0, Hw = 0, vlo = 0, vhi = 0;
 		/* inner-part bounds: counts as int, moments as doubles (exact: |S| <= N 65535 and
 		 * SS <= N 65535^2 stay below 2^53) */
 		int ciA = MA.c, ciB = MB.c;
 		double sA = (double)MA.s, ssA = (double)MA.ss, sB = (double)MB.s, ssB = (double)MB.ss;
-		int ulo = sgh_value_at1(P, MA.c), uhi = sgh_value_at1(P, MA.c + n - 1);
+		int ulo = klo, uhi = khi;
 		const double inn = 1.0 / ((double)n * (double)(n - 1));
 		bool sig_e0 = e0;
 		for (int guard = 0;; guard++) {
+			SGH_WP(4, 1);
 			if (guard >= cap)
 				return 1;	/* a long Winsorize (hundreds of iterations with several 0 / 65535
 					 * samples) goes to the replay rather than holding its wave */
@@ -925,24 +1032,6 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 			const double m0 = median - 1.5 * sigma, m1d = median + 1.5 * sigma;
 			const double tol = sig_e0 ? 0.0 : SGH_BAND * (fabs(median) + 1.5 * sigma + 1.0);
 			const int nin = n - Lw - Hw;
-			/* # w elements <= v (integer v in [-1, 65535]); "< thr" is "<= ceil(thr) - 1" and
-			 * "<= thr" is "<= floor(thr)", so both sides of a rounding band usually name the
-			 * same v and one count serves both */
-			auto w_le = [&](int v, int side) {
-				int c = (Lw && vlo <= v) ? Lw : 0;
-				if (nin > 0 && v >= ulo) {
-					if (v >= uhi) {
-						c += nin;
-					} else {
-						int k = cnt_cached(v, side);
-						k = k < ciA ? ciA : (k > ciB ? ciB : k);
-						c += k - ciA;
-					}
-				}
-				if (Hw && vhi <= v)
-					c += Hw;
-				return c;
-			};
 			auto v_lt = [](double thr) {
 				const double c = ceil(thr) - 1.0;
 				return c < -1.0 ? -1 : (c > 65535.0 ? 65535 : (int)c);
@@ -954,7 +1043,9 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 			/* the common case as one floor per side: when m lies more than 2 t (t = the
 			 * rounding check's band, >= tol) from every integer and from every half-integer,
 			 * ceil(m - tol) - 1 = floor(m + tol) = floor(m), round_to_WORD(m) is decided and
-			 * not ambiguous; otherwise the thresholds come from the general formulas */
+			 * not ambiguous; otherwise the thresholds come from the general formulas.  Either
+			 * way a1 = ceil(m0 - tol) - 1 and b1 = floor(m1 + tol): the clamp bounds IA - 1
+			 * and IB of the round-2 loop, so a growth's moments are the query's own */
 			const double t2 = 2.0 * (tol + 1e-9 * tol);
 			const double fl0 = floor(m0), fr0 = m0 - fl0, fl1 = floor(m1d), fr1 = m1d - fl1;
 			const bool fast0 = fr0 > t2 && fr0 < 1.0 - t2 && fabs(fr0 - 0.5) > t2;
@@ -963,17 +1054,58 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 			auto round_fast = [](double m, double fl, double fr) -> int {
 				return m <= 0.0 ? 0 : (m > 65535.0 ? 65535 : (int)fl + (fr > 0.5 ? 1 : 0));
 			};
+			if (!fast0 || !fast1)
+				SGH_WPEV(2);
 			const int a1 = fast0 ? clampv(fl0) : v_lt(m0 - tol), a2 = fast0 ? a1 : v_le(m0 + tol);
 			const int b1 = fast1 ? clampv(fl1) : v_le(m1d + tol), b2 = fast1 ? b1 : v_lt(m1d - tol);
-			const int clo = w_le(a1, 0);
-			if (!sig_e0 && a2 != a1 && clo != w_le(a2, 0))
+			/* the growth queries of both sides through ONE query site: a lane runs its low query,
+			 * then its high one, so a wave executes the query body max(queries per lane) times
+			 * (the round-2 loop had six query sites, each run when any lane needed it) */
+			const bool needL = nin > 0 && a1 >= ulo && a1 < uhi;
+			const bool needH = nin > 0 && b1 >= ulo && b1 < uhi;
+			SghX xL = {0, 0.0, 0.0, -1}, xH = {0, 0.0, 0.0, -1};
+			int pend = (needL ? 1 : 0) | (needH ? 2 : 0);
+			SGH_WP(2, 0);
+#pragma clang loop unroll(disable)
+			while (pend != 0) {
+				SGH_WPEV(0);
+				const int side = (pend & 1) ? 0 : 1;
+				const SghX x = sgh_qx(P, side ? b1 : a1, side);
+				if (side)
+					xH = x;
+				else
+					xL = x;
+				pend &= pend - 1;
+			}
+			SGH_WP(3, 0);
+			/* # w elements <= v: the clamped copies plus the inner ones (v's count, when v lies
+			 * in [ulo, uhi), is the query's; in the rare ambiguous cases a second threshold's
+			 * count comes from a plain count query) */
+			auto w_le = [&](int v, bool have, int cq) {
+				int c = (Lw && vlo <= v) ? Lw : 0;
+				if (nin > 0 && v >= ulo) {
+					if (v >= uhi) {
+						c += nin;
+					} else {
+						if (!have)
+							SGH_WPEV(1);
+						int k = have ? cq : sgh_cnt_le(P, v);
+						k = k < ciA ? ciA : (k > ciB ? ciB : k);
+						c += k - ciA;
+					}
+				}
+				if (Hw && vhi <= v)
+					c += Hw;
+				return c;
+			};
+			const int clo = w_le(a1, true, xL.c);
+			if (!sig_e0 && a2 != a1 && clo != w_le(a2, false, 0))
 				return 1;
-			const int chi = n - w_le(b1, 1);
-			if (!sig_e0 && b2 != b1 && chi != n - w_le(b2, 1))
+			const int chi = n - w_le(b1, true, xH.c);
+			if (!sig_e0 && b2 != b1 && chi != n - w_le(b2, false, 0))
 				return 1;
 			if (clo + chi > n)
 				return 1;
-			bool grew_lo = false, grew_hi = false;
 			if (clo > 0) {
 				if (!fast0 && sgh_round_ambiguous(m0, tol + 1e-9 * tol))
 					return 1;
@@ -981,13 +1113,12 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 					return 1;
 				if (clo > Lw) {
 					/* the inner samples below m0 join the clamped copies */
-					double c = ceil(m0 - tol);
-					IA = c < 0.0 ? 0 : (c > 65536.0 ? 65536 : (int)c);
-					const SghM m = sgh_M_le(P, IA - 1);
-					ciA = m.c;
-					sA = (double)m.s;
-					ssA = (double)m.ss;
-					grew_lo = true;
+					if (!needL)
+						return 1;	/* every inner sample clamped at once: the sorted path decides */
+					SGH_WPEV(3);
+					ciA = xL.c;
+					sA = xL.s;
+					ssA = xL.ss;
 				}
 				Lw = clo;
 				vlo = fast0 ? round_fast(m0, fl0, fr0) : sg_round_to_WORD(m0);
@@ -998,24 +1129,25 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 				if (chi < Hw || chi > n - Lw)
 					return 1;
 				if (chi > Hw) {
-					double c = floor(m1d + tol);
-					IB = c < -1.0 ? -1 : (c > 65535.0 ? 65535 : (int)c);
-					const SghM m = sgh_M_le(P, IB);
-					ciB = m.c;
-					sB = (double)m.s;
-					ssB = (double)m.ss;
-					grew_hi = true;
+					if (!needH)
+						return 1;
+					SGH_WPEV(4);
+					ciB = xH.c;
+					sB = xH.s;
+					ssB = xH.ss;
 				}
 				Hw = chi;
 				vhi = fast1 ? round_fast(m1d, fl1, fr1) : sg_round_to_WORD(m1d);
 			}
 			if (ciB - ciA != n - Lw - Hw)
 				return 1;	/* inner part and clamp counts disagree: leave it to the sorted path */
+			/* the inner part's new ends (bounds): the smallest sample above a1, the largest at or
+			 * below b1; a query that found no growth still tightens its side's bound */
 			if (n - Lw - Hw > 0) {
-				if (grew_lo)
-					ulo = sgh_value_at1(P, MA.c + Lw);
-				if (grew_hi)
-					uhi = sgh_value_at1(P, MA.c + n - Hw - 1);
+				if (needL)
+					ulo = xL.nb;
+				if (needH)
+					uhi = xH.nb;
 			}
 			/* median of w: the kept values at the median ranks unless clamped */
 			{
@@ -1047,6 +1179,7 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 			sigma = 1.134 * (num > 0.0 ? sgh_sqrt_fast(num * inn) : 0.0);
 			sig_e0 = we0;
 			if (e00) {
+				SGH_WPEV(5);
 				if (we0)
 					break;	/* 0/0 = NaN: the loop exits */
 				continue;	/* x/0 = inf > 0.0005 */
@@ -1060,6 +1193,7 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 			if (!(d > 0.0))
 				break;
 		}
+		SGH_WP(4, 0);
 		/* clip pass on the kept set with the Winsorized sigma / median (:1731-1747) */
 		const double tl = sl * sigma, th = sh * sigma;
 		const double blo = median - tl, bhi = median + th;
@@ -1070,10 +1204,10 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 		int bt = sgh_floor_clamp(bhi + tol);
 		if (bt > B)
 			bt = B;
-		SghQ qa, qb;
-		sgh_q_load(P, a - 1, qa);
-		sgh_q_load(P, bt, qb);
-		const int cnt_a = sgh_q_count(P, qa), cnt_bt = sgh_q_count(P, qb);
+		/* the clip counts, moments and the next pass's kept ends (exact doubles: relative to lo,
+		 * SS <= 65535^3 < 2^53) */
+		const SghX xa = sgh_qx(P, a - 1, 0), xb = sgh_qx(P, bt, 1);
+		const int cnt_a = xa.c, cnt_bt = xb.c;
 		if (!sig_e0) {
 			int amb1 = sgh_floor_clamp(blo + tol);
 			if (amb1 > B)
@@ -1101,17 +1235,24 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 			return 1;
 		if (L) {
 			A = a;
-			MA = sgh_q_moments(P, qa);
+			MA.c = xa.c;
+			MA.s = (long long)xa.s;
+			MA.ss = (unsigned long long)xa.ss;
+			klo = xa.nb;
 		}
 		if (H) {
 			B = bt;
-			MB = sgh_q_moments(P, qb);
+			MB.c = xb.c;
+			MB.s = (long long)xb.s;
+			MB.ss = (unsigned long long)xb.ss;
+			khi = xb.nb;
 		}
 		rlo += L;
 		rhi += H;
 		r += L + H;
 		nrem = L + H;
 		n -= nrem;
+		SGH_WP(5, 0);
 	} while (nrem > 0 && n > 3);
 	const long long tot = (MB.s - MA.s) + (long long)n * P.lo;
 	*value = sg_round_to_WORD((double)tot / (double)n);
@@ -1137,6 +1278,14 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 	}
 	/* A/B timeline (dbg 11): cycles of the prefix and of the pass loop, passes per wave */
 	const uint64_t c0 = p.dbg == 11 ? __builtin_readcyclecounter() : 0;
+#ifdef SGH_WPROF
+	if (REJ == 4 && lane == 0) {
+		uint64_t *w = L.wp[threadIdx.x >> 6];
+		for (int k = 1; k < 16; k++)
+			w[k] = 0;
+		w[0] = __builtin_readcyclecounter();
+	}
+#endif
 	int passes = 0;
 	/* prefix: this lane's 4 groups, then the partner's 4 (PAIR), or all 8 */
 	constexpr int NG = PAIR ? SGH_NGRP / 2 : SGH_NGRP;
@@ -1225,6 +1374,10 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 	P.nb = (int)cum;
 	P.col = col;
 	P.hb = &L.h[0][0][0];
+#ifdef SGH_WPROF
+	P.wp = L.wp[threadIdx.x >> 6];
+	SGH_WP(0, 0);
+#endif
 	int cls = SG_CLS_OK;
 	uint16_t value = 0;
 	uint32_t rlo = 0, rhi = 0;
@@ -1252,6 +1405,9 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 			P.T.s = (long long)s32 + P.Z.s + ds * P.ns;
 			P.T.ss = (unsigned long long)ss32 + P.Z.ss + (unsigned long long)(ds * ds) * (unsigned long long)P.ns;
 			if (REJ == 4 || !PAIR) {
+				/* zeros: nz copies of -lo, exact as doubles (dz = -lo, dz^2 nz < 2^53) */
+				P.zs = -(double)lo * (double)P.nz;
+				P.zss = (double)lo * (double)lo * (double)P.nz;
 				cls = sgh_winsorized(P, N, p.sig0, p.sig1, p.wins_cap, &value, &rlo, &rhi);
 #ifdef SGH_WINS_ITERS
 				value = (uint16_t)rlo;	/* A/B probe build: the image holds the inner iteration counts */
@@ -1275,11 +1431,15 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 		const int64_t pix = ((int64_t)c * p.H + R) * p.W + x;
 		if (!half) {
 			if (cls == SG_CLS_OK) {
+#ifndef SGH_WPROF
 				if (p.dbg != 11)	/* the timeline A/B keeps its stamps in the output buffer */
 					p.out[pix] = value;
+#endif
 			} else {
+#ifndef SGH_WPROF
 				const unsigned int slot = atomicAdd(redo_count, 1u);
 				redo_list[slot] = (unsigned int)pix;
+#endif
 			}
 		}
 		if (cls != SG_CLS_OK || half)
@@ -1302,6 +1462,18 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 	/* wave sums of the rejection counts (each lane's count <= N, so a wave's sum of 32 pixel
 	 * counts fits 32 bits for any N the kernel takes): DPP row sums + 4 readlanes instead of
 	 * six dependent ds_bpermute rounds */
+#ifdef SGH_WPROF
+	if (REJ == 4) {
+		sgh_wp(L.wp[threadIdx.x >> 6], 6);
+		if (lane == 0) {
+			const uint64_t *w = L.wp[threadIdx.x >> 6];
+			unsigned long long *g = (unsigned long long *)p.out;
+			for (int k = 1; k < 16; k++)
+				atomicAdd(g + k, (unsigned long long)w[k]);
+			atomicAdd(g, 1ull);	/* finishing waves */
+		}
+	}
+#endif
 	const unsigned long long a = sgh_wave_sum(rlo), b = sgh_wave_sum(rhi);
 	if (lane == 0 && (a | b)) {
 		unsigned long long *sh = p.rej + ((size_t)((blockIdx.x * 8 + (col >> 5)) % SG_REJ_SHARDS) * 6 + c * 2);
@@ -1470,6 +1642,9 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, const SghRo &r
 #endif
 #ifndef SGH_WINS_ORDER
 #define SGH_WINS_ORDER 1	/* WINSORIZED finish: columns with zeros / 65535s first (sgh_tile) */
+#ifndef SGH_WINS_SPLIT
+#define SGH_WINS_SPLIT 0	/* WINSORIZED finish waves (A/B): 0 waves 0 / 1, 1 alternating pairs, 2 all four */
+#endif
 #endif
 
 template <bool EDGE, int NORM, int NI, int NB, int BW = SghCfg<NI>::WAVES, class BAR = SghWgBarrier>
@@ -1786,9 +1961,20 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 				L.perm[sb ? na + rb : ns + (64 - na) + (lane - rb)] = (uint8_t)cb;
 			}
 			__syncthreads();
+#if SGH_WINS_SPLIT == 1	/* A/B: tiles alternate between waves 0 / 1 and waves 2 / 3 */
+			const int fw = wave - (int)((blockIdx.x & 1u) << 1);
+			if (fw < 0 || fw >= 2)
+				return;
+			const int col = L.perm[64 * fw + lane];
+#elif SGH_WINS_SPLIT == 2	/* A/B: all four waves, 32 columns each */
+			if (lane >= 32)
+				return;
+			const int col = L.perm[32 * wave + lane];
+#else
 			if (wave >= 2)
 				return;
 			const int col = L.perm[64 * wave + lane];
+#endif
 			sgh_finish2<REJ, false, NI>(p, L, col, 0, col_lo(col), R, c, col_x(col), redo_count, redo_list);
 			return;
 		}
@@ -1814,8 +2000,11 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
  * folded + 0.5; NI pixel pairs per lane (tile of 128 NI pixels, 4 NI waves).  Two 8-wave
  * workgroups (69 KB of LDS each) or four 4-wave ones (36 KB) per CU: 16 waves, at most 128
  * VGPRs. */
+#ifndef SGH_WINS_WPE
+#define SGH_WINS_WPE 3	/* WINSORIZED: waves per SIMD the register budget is sized for (4: 128 VGPRs, spills) */
+#endif
 template <int REJ, int NORM, int NI>
-__global__ void __launch_bounds__(64 * SghCfg<NI>::WAVES, SghCfg<NI>::WPE)
+__global__ void __launch_bounds__(64 * SghCfg<NI>::WAVES, (REJ == 4 && NI == 1) ? SGH_WINS_WPE : SghCfg<NI>::WPE)
 k_stack_hist(SgStackParams p, const int *__restrict__ tab, const int4 *__restrict__ norm,
 		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
 	SghRo ro;
