@@ -194,6 +194,9 @@ __device__ __forceinline__ void sg_lds_fft(C *buf, int n, int logn, int nb, int 
  * the first pass loads everything before anyone stores.  A st that writes element i back
  * to its own slot is race-free as is: the last pass's thread reads exactly the slots it
  * writes. */
+template <int EPT, class C, class ST>
+__device__ __forceinline__ void sg_fft_io_regs(C *buf, int n, int nb, int bstride, const C *__restrict__ tw,
+		bool inv, C (&v)[EPT / 8][8], ST st);
 template <bool LDS_IN = false, int EPT = 8, class C, class LD, class ST>
 __device__ __forceinline__ void sg_fft_io(C *buf, int n, int nb, int bstride, const C *__restrict__ tw,
 		bool inv, LD ld, ST st) {
@@ -207,10 +210,10 @@ __device__ __forceinline__ void sg_fft_io(C *buf, int n, int nb, int bstride, co
 	}
 	/* first pass: radix 8, Ns = 1 (no twiddles); EPT / 8 items per thread, all loaded before
 	 * any is stored */
+	constexpr int FI = EPT / 8;
+	C v[FI][8];
 	{
-		constexpr int FI = EPT / 8;
 		const int per = n >> 3, items = nb * per;
-		C v[FI][8];
 #pragma unroll
 		for (int it = 0; it < FI; it++) {
 			const int t = threadIdx.x + it * blockDim.x;
@@ -221,8 +224,22 @@ __device__ __forceinline__ void sg_fft_io(C *buf, int n, int nb, int bstride, co
 					v[it][r] = ld(b, j + r * per);
 			}
 		}
-		if (LDS_IN)
-			__syncthreads();
+	}
+	if (LDS_IN)
+		__syncthreads();
+	sg_fft_io_regs<EPT>(buf, n, nb, bstride, tw, inv, v, st);
+}
+
+/* sg_fft_io from its first pass's inputs already in registers (n >= 16): v[it][r] = element
+ * j + r n / 8 of transform b, item t = threadIdx.x + it blockDim, b = t % nb, j = t / nb; a
+ * caller that loads them ahead (the next row's, during this row's transform) hides the load
+ * latency */
+template <int EPT, class C, class ST>
+__device__ __forceinline__ void sg_fft_io_regs(C *buf, int n, int nb, int bstride, const C *__restrict__ tw,
+		bool inv, C (&v)[EPT / 8][8], ST st) {
+	{
+		constexpr int FI = EPT / 8;
+		const int per = n >> 3, items = nb * per;
 #pragma unroll
 		for (int it = 0; it < FI; it++) {
 			const int t = threadIdx.x + it * blockDim.x;

@@ -233,39 +233,64 @@ k_reg_cols_inv_argmax(const sg_c64 *__restrict__ work, int S, int logS, int CW, 
 template <class C>
 __global__ void __launch_bounds__(512)
 k_reg_rows_fwd_half(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const int *__restrict__ fb,
-		int S, const C *__restrict__ tw, C *__restrict__ work, unsigned long long *__restrict__ energy) {
+		int S, const C *__restrict__ tw, C *__restrict__ work, unsigned long long *__restrict__ energy, int rpb) {
 	typedef typename SgReal<C>::T T;
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 	C *buf = (C *)smem;
-	const int row = blockIdx.x, pair = blockIdx.y, H = S >> 1;
+	const int pair = blockIdx.y, H = S >> 1, per = S >> 3;
 	const size_t plane = (size_t)S * S;
-	const uint16_t *pa = sel + (size_t)fa[pair] * plane + (size_t)row * S;
+	const uint16_t *pa = sel + (size_t)fa[pair] * plane;
 	const int b = fb[pair];
-	const uint16_t *pb = b >= 0 ? sel + (size_t)b * plane + (size_t)row * S : nullptr;
-	C *out = work + (size_t)pair * plane + (size_t)row * S;
-	unsigned long long ea = 0, eb = 0;
-	sg_fft_io(buf, S, 1, S, tw, false,
-			[&](int, int i) {
-				const unsigned int va = pa[i], vb = pb ? pb[i] : 0u;
-				ea += (unsigned long long)(va * va);
-				eb += (unsigned long long)(vb * vb);
-				return sg_mk<C>((T)va, (T)vb);
-			},
-			[&](int, int i, C v) { buf[sg_pad(i)] = v; });
-	sg_energy_add(ea, eb, fa[pair], b, energy);	/* its __syncthreads also orders the LDS writes */
-	for (int k = threadIdx.x; k < H; k += blockDim.x) {
-		const C zk = buf[sg_pad(k)], zm = buf[sg_pad(k ? S - k : H)];
-		C A, B;
-		if (k == 0) {
-			A = sg_mk<C>(zk.x, zm.x);	/* A(0) + i A(S/2) */
-			B = sg_mk<C>(zk.y, zm.y);
-		} else {
-			A = sg_mk<C>((T)0.5 * (zk.x + zm.x), (T)0.5 * (zk.y - zm.y));
-			B = sg_mk<C>((T)0.5 * (zk.y + zm.y), (T)-0.5 * (zk.x - zm.x));
+	const uint16_t *pb = b >= 0 ? sel + (size_t)b * plane : nullptr;
+	/* rpb rows per workgroup; the next row's samples are loaded into registers before this
+	 * row's transform (the first pass's inputs: thread t takes elements t + r S / 8), so its
+	 * load latency hides behind the LDS passes instead of opening every row (round 2: one row
+	 * per workgroup, 1.75 ms per 64 pairs of 2048^2 at 1.8 TB/s) */
+	const int t = threadIdx.x;
+	const bool act = t < per;
+	uint32_t ra[8], rb[8];
+	auto fetch = [&](int row) {
+#pragma unroll
+		for (int r = 0; r < 8; r++) {
+			const size_t i = (size_t)row * S + (size_t)(t + r * per);
+			ra[r] = act ? (uint32_t)pa[i] : 0u;
+			rb[r] = (act && pb) ? (uint32_t)pb[i] : 0u;
 		}
-		out[k] = A;
-		out[H + k] = B;
+	};
+	unsigned long long ea = 0, eb = 0;
+	const int row0 = blockIdx.x * rpb;
+	fetch(row0);
+	for (int k = 0; k < rpb; k++) {
+		const int row = row0 + k;
+		C v[1][8];
+#pragma unroll
+		for (int r = 0; r < 8; r++) {
+			v[0][r] = sg_mk<C>((T)ra[r], (T)rb[r]);
+			ea += (unsigned long long)(ra[r] * ra[r]);
+			eb += (unsigned long long)(rb[r] * rb[r]);
+		}
+		if (k + 1 < rpb)
+			fetch(row + 1);
+		if (k > 0)
+			__syncthreads();	/* the previous row's separation has read buf */
+		sg_fft_io_regs<8>(buf, S, 1, S, tw, false, v, [&](int, int i, C val) { buf[sg_pad(i)] = val; });
+		__syncthreads();
+		C *out = work + (size_t)pair * plane + (size_t)row * S;
+		for (int kx = threadIdx.x; kx < H; kx += blockDim.x) {
+			const C zk = buf[sg_pad(kx)], zm = buf[sg_pad(kx ? S - kx : H)];
+			C A, B;
+			if (kx == 0) {
+				A = sg_mk<C>(zk.x, zm.x);	/* A(0) + i A(S/2) */
+				B = sg_mk<C>(zk.y, zm.y);
+			} else {
+				A = sg_mk<C>((T)0.5 * (zk.x + zm.x), (T)0.5 * (zk.y - zm.y));
+				B = sg_mk<C>((T)0.5 * (zk.y + zm.y), (T)-0.5 * (zk.x - zm.x));
+			}
+			out[kx] = A;
+			out[H + kx] = B;
+		}
 	}
+	sg_energy_add(ea, eb, fa[pair], b, energy);
 }
 
 /* R conj F */
@@ -413,16 +438,12 @@ k_reg_final(const SgBest *__restrict__ best, int S, int count, const int *__rest
 template <class C, bool CAND>
 __global__ void __launch_bounds__(512)
 k_reg_rows_inv_half_argmax(const C *__restrict__ work, int S, const C *__restrict__ tw,
-		SgBest *__restrict__ best, const SgRegOut *__restrict__ res, SgCand *__restrict__ cand) {
+		SgBest *__restrict__ best, const SgRegOut *__restrict__ res, SgCand *__restrict__ cand, int rpb) {
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 	C *buf = (C *)smem;
 	__shared__ SgBest red[8];
-	const int row = blockIdx.x, pair = blockIdx.y, H = S >> 1;
-	const C *in = work + (size_t)pair * S * S + (size_t)row * S;
+	const int pair = blockIdx.y, H = S >> 1, per = S >> 3;
 	typedef typename SgReal<C>::T T;
-	SgTop2 ta, tb;
-	sg_top2_init(ta);
-	sg_top2_init(tb);
 	double thr[2] = {INFINITY, INFINITY};
 	if (CAND) {
 		const SgRegOut r = res[pair];
@@ -431,39 +452,69 @@ k_reg_rows_inv_half_argmax(const C *__restrict__ work, int S, const C *__restric
 		thr[0] = r.amb[0] ? r.thr[0] : INFINITY;
 		thr[1] = r.amb[1] ? r.thr[1] : INFINITY;
 	}
-	sg_fft_io(buf, S, 1, S, tw, true,
-			[&](int, int i) {
-				C qa, qb;
-				if ((i & (H - 1)) == 0) {	/* kx = 0 or S/2: the packed real pair */
-					const C a = in[0], b = in[H];
-					qa = sg_mk<C>(i ? a.y : a.x, (T)0);
-					qb = sg_mk<C>(i ? b.y : b.x, (T)0);
-				} else if (i < H) {
-					qa = in[i];
-					qb = in[H + i];
-				} else {
-					const C a = in[S - i], b = in[H + S - i];
-					qa = sg_mk<C>(a.x, -a.y);
-					qb = sg_mk<C>(b.x, -b.y);
-				}
-				return sg_mk<C>(qa.x - qb.y, qa.y + qb.x);
-			},
-			[&](int, int j, C c) {
-				const int idx = row * S + j;
-				if (CAND) {
-					sg_cand_push(cand + 2 * pair, c.x, thr[0], idx);
-					sg_cand_push(cand + 2 * pair + 1, c.y, thr[1], idx);
-					return;
-				}
-				sg_top2_add(ta, c.x, idx);
-				sg_top2_add(tb, c.y, idx);
-			});
-	if (CAND)
-		return;
-	sg_best_block(ta, tb, red);
-	if (threadIdx.x == 0) {
-		best[(size_t)pair * S + row].a = ta;
-		best[(size_t)pair * S + row].b = tb;
+	/* rpb rows per workgroup, the next row's two spectra (a, b: 16 values per thread) loaded
+	 * into registers during this row's transform, as in k_reg_rows_fwd_half.  Element i of the
+	 * full row spectrum: kx = i <= S/2 from the stored half, kx > S/2 the conjugate of S - i,
+	 * kx = 0 and S/2 the packed real pair in column 0 */
+	const int t = threadIdx.x;
+	const bool act = t < per;
+	C ra[8], rb[8];
+	auto fetch = [&](int row) {
+		const C *in = work + (size_t)pair * S * S + (size_t)row * S;
+#pragma unroll
+		for (int r = 0; r < 8; r++) {
+			const int i = t + r * per;
+			const int src = (i & (H - 1)) == 0 ? 0 : (i < H ? i : S - i);
+			ra[r] = act ? in[src] : sg_mk<C>((T)0, (T)0);
+			rb[r] = act ? in[H + src] : sg_mk<C>((T)0, (T)0);
+		}
+	};
+	const int row0 = blockIdx.x * rpb;
+	fetch(row0);
+	for (int k = 0; k < rpb; k++) {
+		const int row = row0 + k;
+		C v[1][8];
+#pragma unroll
+		for (int r = 0; r < 8; r++) {
+			const int i = t + r * per;
+			const C a = ra[r], b = rb[r];
+			C qa, qb;
+			if ((i & (H - 1)) == 0) {	/* kx = 0 or S/2: the packed real pair */
+				qa = sg_mk<C>(i ? a.y : a.x, (T)0);
+				qb = sg_mk<C>(i ? b.y : b.x, (T)0);
+			} else if (i < H) {
+				qa = a;
+				qb = b;
+			} else {
+				qa = sg_mk<C>(a.x, -a.y);
+				qb = sg_mk<C>(b.x, -b.y);
+			}
+			v[0][r] = sg_mk<C>(qa.x - qb.y, qa.y + qb.x);
+		}
+		if (k + 1 < rpb)
+			fetch(row + 1);
+		if (k > 0)
+			__syncthreads();	/* the previous row's last pass has read buf */
+		SgTop2 ta, tb;
+		sg_top2_init(ta);
+		sg_top2_init(tb);
+		sg_fft_io_regs<8>(buf, S, 1, S, tw, true, v, [&](int, int j, C c) {
+			const int idx = row * S + j;
+			if (CAND) {
+				sg_cand_push(cand + 2 * pair, c.x, thr[0], idx);
+				sg_cand_push(cand + 2 * pair + 1, c.y, thr[1], idx);
+				return;
+			}
+			sg_top2_add(ta, c.x, idx);
+			sg_top2_add(tb, c.y, idx);
+		});
+		if (CAND)
+			continue;
+		sg_best_block(ta, tb, red);
+		if (threadIdx.x == 0) {
+			best[(size_t)pair * S + row].a = ta;
+			best[(size_t)pair * S + row].b = tb;
+		}
 	}
 }
 
@@ -1266,6 +1317,13 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	const int colh_thr32 = std::max(64, CW32 * S / ept32);
 	const size_t colh_lds32 = (size_t)CW32 * (SG_PADN(S) + 1) * sizeof(float2);
 	const int colocc = ctx->knobs.reg_colocc;
+	/* rows per forward-row workgroup (the next row prefetched during this one's transform) */
+	int rpb = ctx->knobs.reg_rpb;
+	while (rpb > 1 && S % rpb != 0)
+		rpb >>= 1;
+	int rpbi = ctx->knobs.reg_rpbi;	/* the same for the inverse rows + arg-max */
+	while (rpbi > 1 && S % rpbi != 0)
+		rpbi >>= 1;
 	const int xcdmap = ctx->knobs.reg_xcd;	/* A/B knob SG_REG_XCD: 0 = strips in dispatch order */
 	/* generic rows: Bluestein needs m/8 threads (sg_lds_fft), the mixed passes take 256 */
 	const int gen_thr = pl.bluestein ? (pl.m / 8 < 64 ? 64 : pl.m / 8) : 256;
@@ -1381,8 +1439,8 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	/* half-spectrum passes of the pairs (fa, fb)[0, np): the reference spectrum (spec) of the
 	 * precision (fp64 or fp32), `mode` 0 = top-2 arg-max into best, 1 = near-tie candidates */
 	auto half_spec64 = [&]() -> int {
-		hipLaunchKernelGGL(k_reg_rows_fwd_half<sg_c64>, dim3(S, 1), dim3(row_thr), row_lds, s, d_sel, d_fa + NP,
-				d_fb + NP, S, tw, spec, energy2);
+		hipLaunchKernelGGL(k_reg_rows_fwd_half<sg_c64>, dim3(S / rpb, 1), dim3(row_thr), row_lds, s, d_sel, d_fa + NP,
+				d_fb + NP, S, tw, spec, energy2, rpb);
 		HIPCHK(hipGetLastError());
 		hipLaunchKernelGGL((k_reg_cols<sg_c64, 8>), dim3(S / 2 / CWh, 1), dim3(colh_thr), colh_lds, s, spec, S, logS,
 				CWh, tw, 0, xcdmap);
@@ -1391,37 +1449,37 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	};
 	auto half64 = [&](const int *fa, const int *fb, int np, unsigned long long *en, int mode, const SgRegOut *res)
 			-> int {
-		hipLaunchKernelGGL(k_reg_rows_fwd_half<sg_c64>, dim3(S, np), dim3(row_thr), row_lds, s, d_sel, fa, fb, S, tw,
-				work, en);
+		hipLaunchKernelGGL(k_reg_rows_fwd_half<sg_c64>, dim3(S / rpb, np), dim3(row_thr), row_lds, s, d_sel, fa, fb, S, tw,
+				work, en, rpb);
 		HIPCHK(hipGetLastError());
 		hipLaunchKernelGGL((k_reg_cols_xpower<sg_c64, 8>), dim3(S / CWh, np), dim3(colh_thr), colh_lds, s, work,
 				(const sg_c64 *)spec, S, CWh, tw, xcdmap, ctx->knobs.reg_pb);
 		HIPCHK(hipGetLastError());
 		if (mode)
-			hipLaunchKernelGGL((k_reg_rows_inv_half_argmax<sg_c64, true>), dim3(S, np), dim3(row_thr), row_lds, s,
-					(const sg_c64 *)work, S, tw, best, res, cand);
+			hipLaunchKernelGGL((k_reg_rows_inv_half_argmax<sg_c64, true>), dim3(S / rpbi, np), dim3(row_thr), row_lds, s,
+					(const sg_c64 *)work, S, tw, best, res, cand, rpbi);
 		else
-			hipLaunchKernelGGL((k_reg_rows_inv_half_argmax<sg_c64, false>), dim3(S, np), dim3(row_thr), row_lds, s,
-					(const sg_c64 *)work, S, tw, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
+			hipLaunchKernelGGL((k_reg_rows_inv_half_argmax<sg_c64, false>), dim3(S / rpbi, np), dim3(row_thr), row_lds, s,
+					(const sg_c64 *)work, S, tw, best, (const SgRegOut *)nullptr, (SgCand *)nullptr, rpbi);
 		HIPCHK(hipGetLastError());
 		return SG_OK;
 	};
 	auto half32 = [&](const int *fa, const int *fb, int np, unsigned long long *en) -> int {
-		hipLaunchKernelGGL(k_reg_rows_fwd_half<float2>, dim3(S, np), dim3(row_thr), row_lds32, s, d_sel, fa, fb, S,
-				tw32, work32, en);
+		hipLaunchKernelGGL(k_reg_rows_fwd_half<float2>, dim3(S / rpb, np), dim3(row_thr), row_lds32, s, d_sel, fa, fb, S,
+				tw32, work32, en, rpb);
 		HIPCHK(hipGetLastError());
 		if (ept32 == 16)
 			hipLaunchKernelGGL((k_reg_cols_xpower<float2, 16>), dim3(S / CW32, np), dim3(colh_thr32), colh_lds32, s,
 					work32, (const float2 *)spec32, S, CW32, tw32, xcdmap, 1);
-		else if (colocc)	/* A/B SG_REG_COLOCC=1: 64 VGPRs (8 waves / SIMD, two 1024-thread workgroups per CU) */
+		else if (colocc)	/* default (SG_REG_COLOCC=1): 64 VGPRs (8 waves / SIMD, two 1024-thread workgroups per CU) */
 			hipLaunchKernelGGL((k_reg_cols_xpower<float2, 8, 8>), dim3(S / CW32, np), dim3(colh_thr32), colh_lds32, s,
 					work32, (const float2 *)spec32, S, CW32, tw32, xcdmap, 1);
 		else
 			hipLaunchKernelGGL((k_reg_cols_xpower<float2, 8>), dim3(S / CW32, np), dim3(colh_thr32), colh_lds32, s,
 					work32, (const float2 *)spec32, S, CW32, tw32, xcdmap, 1);
 		HIPCHK(hipGetLastError());
-		hipLaunchKernelGGL((k_reg_rows_inv_half_argmax<float2, false>), dim3(S, np), dim3(row_thr), row_lds32, s,
-				(const float2 *)work32, S, tw32, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
+		hipLaunchKernelGGL((k_reg_rows_inv_half_argmax<float2, false>), dim3(S / rpbi, np), dim3(row_thr), row_lds32, s,
+				(const float2 *)work32, S, tw32, best, (const SgRegOut *)nullptr, (SgCand *)nullptr, rpbi);
 		HIPCHK(hipGetLastError());
 		return SG_OK;
 	};
@@ -1436,8 +1494,8 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		hipLaunchKernelGGL(k_gen_rows, dim3(S, 1), dim3(gen_thr), gen_lds, s, d_sel, d_fa + NP, d_fb + NP, spec, S, pl,
 				tbl, (int)SG_GEN_C2C, 0, energy, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
 	} else if (fp32) {
-		hipLaunchKernelGGL(k_reg_rows_fwd_half<float2>, dim3(S, 1), dim3(row_thr), row_lds32, s, d_sel, d_fa + NP,
-				d_fb + NP, S, tw32, spec32, energy);
+		hipLaunchKernelGGL(k_reg_rows_fwd_half<float2>, dim3(S / rpb, 1), dim3(row_thr), row_lds32, s, d_sel, d_fa + NP,
+				d_fb + NP, S, tw32, spec32, energy, rpb);
 		HIPCHK(hipGetLastError());
 		if (ept32 == 16)
 			hipLaunchKernelGGL((k_reg_cols<float2, 16>), dim3(S / 2 / CW32, 1), dim3(colh_thr32), colh_lds32, s, spec32,
@@ -1446,8 +1504,8 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 			hipLaunchKernelGGL((k_reg_cols<float2, 8>), dim3(S / 2 / CW32, 1), dim3(colh_thr32), colh_lds32, s, spec32,
 					S, logS, CW32, tw32, 0, xcdmap);
 	} else if (half) {
-		hipLaunchKernelGGL(k_reg_rows_fwd_half<sg_c64>, dim3(S, 1), dim3(row_thr), row_lds, s, d_sel, d_fa + NP,
-				d_fb + NP, S, tw, spec, energy);
+		hipLaunchKernelGGL(k_reg_rows_fwd_half<sg_c64>, dim3(S / rpb, 1), dim3(row_thr), row_lds, s, d_sel, d_fa + NP,
+				d_fb + NP, S, tw, spec, energy, rpb);
 		HIPCHK(hipGetLastError());
 		hipLaunchKernelGGL((k_reg_cols<sg_c64, 8>), dim3(S / 2 / CWh, 1), dim3(colh_thr), colh_lds, s, spec, S, logS,
 				CWh, tw, 0, xcdmap);
