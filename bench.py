@@ -385,6 +385,23 @@ def main_sigma(args):
     D.close()
 
 
+def stack_roofline(achieved, algo_bytes, rej, N, C, H, W, world):
+    """roofline of main_config's stack kernel; traffic = the PMC FETCH/WRITE bytes per launch
+    of the whole configs[4] image (profiles/traffic_winsorized_<N>x<C>x<H>x<W>.json, 1 GPU)"""
+    import sirilgpu as sg
+    r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "stack"}
+    path = os.path.join(ROOT, "profiles", f"traffic_winsorized_{N}x{C}x{H}x{W}.json")
+    if rej == sg.WINSORIZED and world == 1 and os.path.exists(path):
+        with open(path) as f:
+            t = json.load(f)
+        r["traffic"] = int(t["traffic_bytes"])
+        r["traffic_unit"] = "B/launch"
+        r["traffic_over_algorithmic"] = round(t["traffic_bytes"] / algo_bytes, 4)
+        r["traffic_src"] = os.path.relpath(path, ROOT)
+    return r
+
+
 def main_config(args):
     """configs[1] (register-mean) and configs[4] (winsorized-rgb): one step = registration +
     stack; at N GPUs the registration is sharded over frames and the stack over row bands"""
@@ -493,8 +510,7 @@ def main_config(args):
                        "rejection": "none" if rej == sg.NO_REJEC else "winsorized",
                        "parallelism": "1 GPU" if world == 1 else
                        f"registration frame-sharded x{world} + stack row-band x{world}, RCCL gather"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "stack"},
+            "roofline": stack_roofline(achieved, stack_bytes, rej, N, C, H, W, world),
             "stage_ms": {"selection": round(stage[0] * 1e3, 3), "register": round(stage[1] * 1e3, 3),
                          "stack": round(stage[2] * 1e3, 3), "stack_kernel": round(kavg, 3)},
             "register_GBps_model": round(reg_bytes / stage[1] / 1e9, 1),
