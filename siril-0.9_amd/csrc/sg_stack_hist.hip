@@ -898,25 +898,36 @@ __device__ __forceinline__ SghX sgh_qx(const SghPix &P, int v, int dir) {
 	t = t < -1 ? -1 : (t > SGH_BINS - 1 ? SGH_BINS - 1 : t);
 	const int tc = t < 0 ? 0 : t;
 	const int g = tc >> 5;
+	/* the group's 8 dwords and the boundary dword (the one holding bin tc) read once more
+	 * instead of selected (SghQ's trick).  The group prefixes stay in registers: kept in LDS
+	 * (25 dwords per column) they grew a tile to 49.5 KB of LDS and cost 3.5 ms on configs[4] -
+	 * at 36.7 KB a fourth tile fits a CU while other tiles' waves 2 / 3 have left after their
+	 * build (profiles/r03_wins_ab.log) */
 	uint32_t d[SGH_GRP];
 	sgh_grp(P, g, d);
+	const uint32_t bw = P.hb[((P.col >> 6) * SGH_HROWS + (tc >> 2)) * 64 + (P.col & 63)];
+	const uint32_t pc = sgh_pre(P, P.pc, g), ps = sgh_pre(P, P.ps, g), pss = sgh_pre(P, P.pss, g);
 	const int kb = (t >> 2) - g * SGH_GRP;	/* -1 for t = -1: nothing at or below v in the band */
-	const uint32_t mt = 0xFFFFFFFFu >> (24 - 8 * (t & 3));
-	/* the group's dwords masked to the bins <= t (d is then the dwords of the bins > t: d ^ le) */
-	uint32_t le[SGH_GRP];
+	const uint32_t mt = t >= 0 ? 0xFFFFFFFFu >> (24 - 8 * (t & 3)) : 0u;	/* bins <= t of the boundary dword */
 #pragma unroll
 	for (int k = 0; k < SGH_GRP; k++)
-		le[k] = d[k] & (k < kb ? 0xFFFFFFFFu : (k == kb ? mt : 0u));
-	uint32_t c = 0, s = 0, ss = 0;
-	sgh_grp_moments(le, c, s, ss);
+		d[k] = k < kb ? d[k] : 0u;
+	const uint32_t bd = bw & mt;
+	uint32_t c = __builtin_amdgcn_sad_u8(bd, 0u, 0u), s = 0, ss = 0;
+	sgh_grp_moments(d, c, s, ss);
+	/* the boundary dword: bins j = 4 kq + b, j^2 = (4 kq)^2 + 2 (4 kq) b + b^2 */
+	const uint32_t kq = (uint32_t)((tc >> 2) - g * SGH_GRP);
+	const uint32_t cb = __builtin_amdgcn_sad_u8(bd, 0u, 0u);
+	const uint32_t sb = __builtin_amdgcn_udot4(bd, 0x03020100u, 0u, false);
+	const uint32_t qb = __builtin_amdgcn_udot4(bd, 0x09040100u, 0u, false);
+	const uint32_t k4 = 4u * kq;
+	ss += qb + __umul24(2u * k4, sb) + __umul24(__umul24(k4, k4), cb);
+	s += sb + __umul24(k4, cb);
 	const uint32_t b0 = (uint32_t)g * (4u * SGH_GRP);
-	const uint32_t bc = sgh_pre(P, P.pc, g) + c;
-	const uint32_t bs = sgh_pre(P, P.ps, g) + s + __umul24(b0, c);
-	const uint32_t bss = sgh_pre(P, P.pss, g) + ss + __umul24(2u * b0, s) + __umul24(__umul24(b0, b0), c);
 	SghX x;
-	x.c = P.nz + (int)bc;
-	x.s = P.zs + (double)bs;
-	x.ss = P.zss + (double)bss;
+	x.c = P.nz + (int)(pc + c);
+	x.s = P.zs + (double)(ps + s + __umul24(b0, c));
+	x.ss = P.zss + (double)(pss + ss + __umul24(2u * b0, s) + __umul24(__umul24(b0, b0), c));
 	if (v < 0) {
 		x.c = 0;
 		x.s = x.ss = 0.0;
@@ -926,34 +937,17 @@ __device__ __forceinline__ SghX sgh_qx(const SghPix &P, int v, int dir) {
 		x.s = (double)P.T.s;
 		x.ss = (double)P.T.ss;
 	}
-	/* neighbour inside the group: the first non-empty bin above t, the last one at or below t */
-	int kf = -1, kl = -1;
-	uint32_t wf = 0, wl = 0;
-#pragma unroll
-	for (int k = SGH_GRP - 1; k >= 0; k--) {
-		const uint32_t gt = d[k] ^ le[k];
-		const bool nzf = gt != 0u;
-		kf = nzf ? k : kf;
-		wf = nzf ? gt : wf;
-	}
-#pragma unroll
-	for (int k = 0; k < SGH_GRP; k++) {
-		const bool nzl = le[k] != 0u;
-		kl = nzl ? k : kl;
-		wl = nzl ? le[k] : wl;
-	}
-	const int base = P.lo + 4 * g * SGH_GRP;
-	const int vf = base + 4 * kf + (int)(__builtin_ctz(wf | 0x80000000u) >> 3);
-	const int vl = base + 4 * kl + (int)((31 - __builtin_clz(wl | 1u)) >> 3);
-	/* a neighbour outside the group is not searched for (on a wave of 64 pixels some lane nearly
-	 * always misses its group, and a rank query for it cost every query its price): the
-	 * answer is then a bound, dir 0 a lower bound on the smallest sample > v (the next group's
-	 * first bin, or v + 1), dir 1 an upper bound on the largest sample <= v (the group's first
-	 * bin - 1, or v) - all the Winsorized loop asks of its inner-part ends (sgh_winsorized) */
-	const int up_lb = t < 0 ? v + 1 : (base + 4 * SGH_GRP > v + 1 ? base + 4 * SGH_GRP : v + 1);
-	const int dn_ub = t < 0 ? v : (base - 1 < v ? base - 1 : v);
-	const bool okf = kf >= 0 && v >= 0, okl = kl >= 0 && v < 65535;
-	x.nb = dir ? (okl ? vl : dn_ub) : (okf ? vf : up_lb);
+	/* neighbour from the boundary dword only: up, the first non-empty bin above t in it (else
+	 * a lower bound: the next dword's first bin, or v + 1); down, the last non-empty bin at or
+	 * below t in it (else an upper bound: the dword's first bin - 1, or v).  Bounds are all
+	 * the Winsorized loop asks of its inner-part ends (sgh_winsorized) */
+	const int base = P.lo + 4 * (tc >> 2);
+	const uint32_t wu = bw & ~mt, wd = bd;
+	const int up = t < 0 ? v + 1 : base + 4;
+	const int dn = t < 0 ? v : base - 1;
+	const int vf = wu && v >= 0 ? base + (int)(__builtin_ctz(wu) >> 3) : (up > v + 1 ? up : v + 1);
+	const int vl = wd && v < 65535 ? base + (int)((31 - __builtin_clz(wd)) >> 3) : (dn < v ? dn : v);
+	x.nb = dir ? vl : vf;
 	return x;
 }
 
