@@ -503,9 +503,10 @@ __device__ __forceinline__ uint32_t sgh_norm_pair(uint32_t v, double a, double b
 		const double y = NORM == 3 ? t - b : (NORM == 1 ? t - b : t * b) + 0.5;
 		uint32_t r;
 		asm("v_cvt_u32_f64 %0, %1" : "=v"(r) : "v"(y));
-		return r < 65535u ? r : 65535u;
+		return r;
 	};
-	uint32_t r = g(v & 0xFFFFu) | (g(v >> 16) << 16);
+	/* the two u32 results clamped to 65535 and packed by one v_cvt_pk_u16_u32 (saturating) */
+	uint32_t r = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pk_u16((int)g(v & 0xFFFFu), (int)g(v >> 16)));
 	if (EDGE) {
 		const uint32_t f = (fix >> (2 * m)) & 3u;
 		r &= f == 0u ? 0xFFFFFFFFu : (f == 1u ? 0xFFFF0000u : (f == 2u ? 0x0000FFFFu : 0u));

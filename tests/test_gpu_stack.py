@@ -212,6 +212,40 @@ def test_hist_path_normalization(gpu_ctx, normalize, rejection):
 
 
 @pytest.mark.parametrize("rejection", [sg.SIGMA, sg.WINSORIZED])
+@pytest.mark.parametrize("normalize", [sg.ADDITIVE, sg.MULTIPLICATIVE, sg.ADDITIVE_SCALING,
+                                       sg.MULTIPLICATIVE_SCALING])
+def test_hist_path_normalised_saturation(gpu_ctx, normalize, rejection):
+    """normalised samples above 65535 saturate (round_to_WORD, :1635-1652): a bright block near
+    65000 with offsets below the reference's (additive) or multipliers above 1
+    (multiplicative) sends part of it past 65535 in the histogram path's normalising load"""
+    N, H, W = 40, 48, 300
+    frames = orc.synth(N, 1, H, W, seed=520 + normalize, maxshift=6)
+    rng = np.random.default_rng(520 + normalize)
+    frames[:, :, 8:36, 90:170] = (64800 + rng.integers(0, 736, (N, 1, 28, 80))).astype(np.uint16)
+    sx, sy = orc.synth_shifts(N, seed=520 + normalize, maxshift=6)
+    loc = 1000 - rng.random(N) * 300
+    loc[0] = 1000.0
+    scl = 30 + rng.random(N) * 0.9
+    off, mul, scale = orc.compute_normalization(normalize, loc, scl, ref_image=0)
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=rejection, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                              normalize=normalize, offset=off, mul=mul, scale=scale, max_thread=2,
+                              max_number_of_rows=H)
+    rc, out, rej, _ = gpu_ctx.stack_host(desc, np.ascontiguousarray(frames))
+    assert rc == 0, gpu_ctx.error()
+    assert gpu_ctx.stats().path == 1
+    rc, ref, rej_ref = orc.stack_rejection(frames, rejection, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                                           normalize=normalize, offset=off, mul=mul, scale=scale, max_thread=2)
+    assert rc == 0
+    assert_same(out, ref, f"saturation norm={normalize} rej={rejection}")
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+    # some normalised samples of the block do exceed 65535 (before round_to_WORD's clamp)
+    blk = frames[:, 0, 8:36, 90:170].astype(np.float64)
+    nv = blk * scale[:, None, None] - off[:, None, None] if normalize in (sg.ADDITIVE, sg.ADDITIVE_SCALING) \
+        else blk * scale[:, None, None] * mul[:, None, None]
+    assert (nv > 65535.5).any()
+
+
+@pytest.mark.parametrize("rejection", [sg.SIGMA, sg.WINSORIZED])
 @pytest.mark.parametrize("tiny", [False, True])
 def test_hist_path_additive_fold(gpu_ctx, rejection, tiny):
     """additive normalisation with every offset - 0.5 exact takes the folded kernel (NORM 3);
