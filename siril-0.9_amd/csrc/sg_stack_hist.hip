@@ -1058,7 +1058,12 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 			 * (the round-2 loop had six query sites, each run when any lane needed it) */
 			const bool needL = nin > 0 && a1 >= ulo && a1 < uhi;
 			const bool needH = nin > 0 && b1 >= ulo && b1 < uhi;
-			SghX xL = {0, 0.0, 0.0, -1}, xH = {0, 0.0, 0.0, -1};
+			/* a query writes its side's inner-part bound and moments straight into the state
+			 * (a query that finds no growth returns the moments the state already holds: no
+			 * sample lies between the last growth's threshold and this one, since a1 >= ulo); the
+			 * count checks below use the values from before the queries */
+			const int ciA0 = ciA, ciB0 = ciB, ulo0 = ulo, uhi0 = uhi;
+			int cL = 0, cH = 0;
 			int pend = (needL ? 1 : 0) | (needH ? 2 : 0);
 			SGH_WP(2, 0);
 #pragma clang loop unroll(disable)
@@ -1066,10 +1071,17 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 				SGH_WPEV(0);
 				const int side = (pend & 1) ? 0 : 1;
 				const SghX x = sgh_qx(P, side ? b1 : a1, side);
-				if (side)
-					xH = x;
-				else
-					xL = x;
+				if (side) {
+					cH = x.c;
+					sB = x.s;
+					ssB = x.ss;
+					uhi = x.nb;
+				} else {
+					cL = x.c;
+					sA = x.s;
+					ssA = x.ss;
+					ulo = x.nb;
+				}
 				pend &= pend - 1;
 			}
 			SGH_WP(3, 0);
@@ -1078,25 +1090,25 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 			 * count comes from a plain count query) */
 			auto w_le = [&](int v, bool have, int cq) {
 				int c = (Lw && vlo <= v) ? Lw : 0;
-				if (nin > 0 && v >= ulo) {
-					if (v >= uhi) {
+				if (nin > 0 && v >= ulo0) {
+					if (v >= uhi0) {
 						c += nin;
 					} else {
 						if (!have)
 							SGH_WPEV(1);
 						int k = have ? cq : sgh_cnt_le(P, v);
-						k = k < ciA ? ciA : (k > ciB ? ciB : k);
-						c += k - ciA;
+						k = k < ciA0 ? ciA0 : (k > ciB0 ? ciB0 : k);
+						c += k - ciA0;
 					}
 				}
 				if (Hw && vhi <= v)
 					c += Hw;
 				return c;
 			};
-			const int clo = w_le(a1, true, xL.c);
+			const int clo = w_le(a1, true, cL);
 			if (!sig_e0 && a2 != a1 && clo != w_le(a2, false, 0))
 				return 1;
-			const int chi = n - w_le(b1, true, xH.c);
+			const int chi = n - w_le(b1, true, cH);
 			if (!sig_e0 && b2 != b1 && chi != n - w_le(b2, false, 0))
 				return 1;
 			if (clo + chi > n)
@@ -1111,9 +1123,7 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 					if (!needL)
 						return 1;	/* every inner sample clamped at once: the sorted path decides */
 					SGH_WPEV(3);
-					ciA = xL.c;
-					sA = xL.s;
-					ssA = xL.ss;
+					ciA = cL;
 				}
 				Lw = clo;
 				vlo = fast0 ? round_fast(m0, fl0, fr0) : sg_round_to_WORD(m0);
@@ -1127,23 +1137,13 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 					if (!needH)
 						return 1;
 					SGH_WPEV(4);
-					ciB = xH.c;
-					sB = xH.s;
-					ssB = xH.ss;
+					ciB = cH;
 				}
 				Hw = chi;
 				vhi = fast1 ? round_fast(m1d, fl1, fr1) : sg_round_to_WORD(m1d);
 			}
 			if (ciB - ciA != n - Lw - Hw)
 				return 1;	/* inner part and clamp counts disagree: leave it to the sorted path */
-			/* the inner part's new ends (bounds): the smallest sample above a1, the largest at or
-			 * below b1; a query that found no growth still tightens its side's bound */
-			if (n - Lw - Hw > 0) {
-				if (needL)
-					ulo = xL.nb;
-				if (needH)
-					uhi = xH.nb;
-			}
 			/* median of w: the kept values at the median ranks unless clamped */
 			{
 				const int lhs = (n - 1) / 2, rhs = n / 2;
