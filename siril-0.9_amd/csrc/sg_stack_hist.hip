@@ -1911,27 +1911,6 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 		__builtin_amdgcn_s_setprio(1);	/* A/B: the finish raised instead */
 	else if (p.prio)
 		__builtin_amdgcn_s_setprio(0);
-#if defined(SGH_PROBE_VALU) || defined(SGH_PROBE_SLEEP)
-	{	/* sensitivity probes (A/B builds only): extra finish VALU, or extra finish latency */
-#ifdef SGH_PROBE_VALU
-		float z0 = (float)lane, z1 = z0 + 1.f, z2 = z0 + 2.f, z3 = z0 + 3.f;
-#pragma unroll 1
-		for (int k = 0; k < SGH_PROBE_VALU / 16; k++) {
-#pragma unroll
-			for (int u = 0; u < 4; u++) {
-				z0 = z0 * 1.0001f + 0.5f;
-				z1 = z1 * 1.0001f + 0.5f;
-				z2 = z2 * 1.0001f + 0.5f;
-				z3 = z3 * 1.0001f + 0.5f;
-			}
-		}
-		if (z0 + z1 + z2 + z3 == 1.2345f)
-			p.out[0] = 1;
-#else
-		__builtin_amdgcn_s_sleep(SGH_PROBE_SLEEP);
-#endif
-	}
-#endif
 	/* column col = 64 g + l of the tile: pixel pair i = g >> 1 of lane l, half g & 1, i.e.
 	 * image column x0 + 128 i + 2 l + (g & 1); its band start is the half of lo2[i][l] */
 	auto col_x = [&](int col) { return x0 + 128 * (col >> 7) + 2 * (col & 63) + ((col >> 6) & 1); };

@@ -379,6 +379,42 @@ def test_hist_path_border_normalised_zeros(gpu_ctx, normalize, dark):
         assert st.chain_pixels < border * W, st.chain_pixels
 
 
+@pytest.mark.parametrize("rejection", [sg.SIGMA, sg.WINSORIZED])
+@pytest.mark.parametrize("normalize", [sg.ADDITIVE, sg.ADDITIVE_SCALING])
+def test_hist_path_edge_corners_stars(gpu_ctx, normalize, rejection):
+    """additive normalisation at the image corners: frames shifted out in BOTH directions (x
+    and y, shifts up to 12 in every sign) give the x shift's raw 0 where the y shift alone
+    gives the normalised zero (:1628-1632 vs :1550-1577, :1635-1652), image-edge tiles hold
+    both kinds in their border rows, and stars (bright Gaussian blobs) sit on the corners and
+    the edges so those pixels also carry out-of-band samples of their own"""
+    N, H, W = 48, 56, 400
+    rng = np.random.default_rng(900 + normalize + 3 * rejection)
+    loc = 1000.0 + rng.random(N) * 90
+    loc[0] = loc.max() + 5
+    scl = 30 + rng.random(N) * 0.9
+    yy, xx = np.mgrid[0:H, 0:W]
+    scene = np.zeros((H, W))
+    for cy, cx in [(2, 3), (H - 3, W - 4), (4, W - 6), (H - 5, 5), (H // 2, 1), (1, W // 2), (H - 2, W // 3)]:
+        scene += 20000.0 * np.exp(-((yy - cy) ** 2 + (xx - cx) ** 2) / (2 * 2.0 ** 2))
+    frames = np.clip(loc[:, None, None, None] + scene[None, None] + rng.normal(0, 20.0, (N, 1, H, W)), 0,
+                     65535).astype(np.uint16)
+    sx = rng.integers(-12, 13, N).astype(np.int32)
+    sy = rng.integers(-12, 13, N).astype(np.int32)
+    sx[0] = sy[0] = 0
+    off, mul, scale = orc.compute_normalization(normalize, loc, scl, ref_image=0)
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=rejection, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                              normalize=normalize, offset=off, mul=mul, scale=scale, max_thread=2,
+                              max_number_of_rows=H)
+    rc, out, rej, _ = gpu_ctx.stack_host(desc, np.ascontiguousarray(frames))
+    assert rc == 0, gpu_ctx.error()
+    assert gpu_ctx.stats().path == 1
+    rc, ref, rej_ref = orc.stack_rejection(frames, rejection, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                                           normalize=normalize, offset=off, mul=mul, scale=scale, max_thread=2)
+    assert rc == 0
+    assert_same(out, ref, f"corners norm={normalize} rej={rejection}")
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+
+
 @pytest.mark.parametrize("cap", [None, "4", "12"])
 def test_hist_winsorized_iteration_cap(gpu_ctx, cap):
     """pixels whose Winsorize pass needs more inner iterations than SG_WINS_CAP leave the
