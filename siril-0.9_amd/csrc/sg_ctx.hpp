@@ -81,7 +81,6 @@ struct SgKnobs {
 	int reg_cw32 = 4;		/* SG_REG_CW32: columns per strip of the fp32 column pass (4: 32-B row segments, no spill; 8: 64-B segments, 16 elements per thread) */
 	int reg_colocc = 1;		/* SG_REG_COLOCC: 1 = fp32 column pass held to 64 VGPRs (two 1024-thread workgroups per CU: registration 6.86 -> 6.21 ms on configs[1], profiles/r03t_ab_reg_cols.log), 0 = 76 VGPRs, one workgroup */
 	int reg_rpb = 4;		/* SG_REG_RPB: rows per forward-row workgroup of the half-spectrum path (1 -> 4: 6.46 -> 5.92 ms registration on configs[1], profiles/r03u_ab_reg_rows.log) */
-	int reg_rpbi = 1;		/* SG_REG_RPBI: rows per inverse-row (arg-max) workgroup (2-8 measured equal, profiles/r03v_ab_reg_rows_inv.log) */
 	void read() {
 		hist_dbg = sg_env_int("SG_HIST_DBG", 0, 1000, 0);
 		hist_prio = sg_env_int("SG_HIST_PRIO", 0, 3, 1);
@@ -105,7 +104,6 @@ struct SgKnobs {
 		reg_cw32 = sg_env_int("SG_REG_CW32", 1, 16, 4);
 		reg_colocc = sg_env_int("SG_REG_COLOCC", 0, 1, 1);
 		reg_rpb = sg_env_int("SG_REG_RPB", 1, 64, 4);
-		reg_rpbi = sg_env_int("SG_REG_RPBI", 1, 64, 1);
 	}
 };
 

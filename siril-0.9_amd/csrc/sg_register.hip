@@ -230,8 +230,11 @@ k_reg_cols_inv_argmax(const sg_c64 *__restrict__ work, int S, int logS, int CW, 
  * Same unnormalised FFTW_BACKWARD result as the full complex transforms; plane traffic per
  * pair 84 B per pixel instead of 116.
  * ------------------------------------------------------------------------------------- */
+#ifndef SG_REG_FWD_WPE
+#define SG_REG_FWD_WPE 4	/* forward row pass: waves per SIMD its register budget is sized for (4: 127 VGPRs, 28 B of scratch, registration 5.93 -> 5.82 ms on configs[1]; 1: 134 VGPRs; 6: 208 B of scratch, 6.97 ms) */
+#endif
 template <class C>
-__global__ void __launch_bounds__(512)
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(SG_REG_FWD_WPE)))
 k_reg_rows_fwd_half(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const int *__restrict__ fb,
 		int S, const C *__restrict__ tw, C *__restrict__ work, unsigned long long *__restrict__ energy, int rpb) {
 	typedef typename SgReal<C>::T T;
@@ -438,12 +441,16 @@ k_reg_final(const SgBest *__restrict__ best, int S, int count, const int *__rest
 template <class C, bool CAND>
 __global__ void __launch_bounds__(512)
 k_reg_rows_inv_half_argmax(const C *__restrict__ work, int S, const C *__restrict__ tw,
-		SgBest *__restrict__ best, const SgRegOut *__restrict__ res, SgCand *__restrict__ cand, int rpb) {
+		SgBest *__restrict__ best, const SgRegOut *__restrict__ res, SgCand *__restrict__ cand) {
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 	C *buf = (C *)smem;
 	__shared__ SgBest red[8];
-	const int pair = blockIdx.y, H = S >> 1, per = S >> 3;
+	const int row = blockIdx.x, pair = blockIdx.y, H = S >> 1;
+	const C *in = work + (size_t)pair * S * S + (size_t)row * S;
 	typedef typename SgReal<C>::T T;
+	SgTop2 ta, tb;
+	sg_top2_init(ta);
+	sg_top2_init(tb);
 	double thr[2] = {INFINITY, INFINITY};
 	if (CAND) {
 		const SgRegOut r = res[pair];
@@ -452,69 +459,39 @@ k_reg_rows_inv_half_argmax(const C *__restrict__ work, int S, const C *__restric
 		thr[0] = r.amb[0] ? r.thr[0] : INFINITY;
 		thr[1] = r.amb[1] ? r.thr[1] : INFINITY;
 	}
-	/* rpb rows per workgroup, the next row's two spectra (a, b: 16 values per thread) loaded
-	 * into registers during this row's transform, as in k_reg_rows_fwd_half.  Element i of the
-	 * full row spectrum: kx = i <= S/2 from the stored half, kx > S/2 the conjugate of S - i,
-	 * kx = 0 and S/2 the packed real pair in column 0 */
-	const int t = threadIdx.x;
-	const bool act = t < per;
-	C ra[8], rb[8];
-	auto fetch = [&](int row) {
-		const C *in = work + (size_t)pair * S * S + (size_t)row * S;
-#pragma unroll
-		for (int r = 0; r < 8; r++) {
-			const int i = t + r * per;
-			const int src = (i & (H - 1)) == 0 ? 0 : (i < H ? i : S - i);
-			ra[r] = act ? in[src] : sg_mk<C>((T)0, (T)0);
-			rb[r] = act ? in[H + src] : sg_mk<C>((T)0, (T)0);
-		}
-	};
-	const int row0 = blockIdx.x * rpb;
-	fetch(row0);
-	for (int k = 0; k < rpb; k++) {
-		const int row = row0 + k;
-		C v[1][8];
-#pragma unroll
-		for (int r = 0; r < 8; r++) {
-			const int i = t + r * per;
-			const C a = ra[r], b = rb[r];
-			C qa, qb;
-			if ((i & (H - 1)) == 0) {	/* kx = 0 or S/2: the packed real pair */
-				qa = sg_mk<C>(i ? a.y : a.x, (T)0);
-				qb = sg_mk<C>(i ? b.y : b.x, (T)0);
-			} else if (i < H) {
-				qa = a;
-				qb = b;
-			} else {
-				qa = sg_mk<C>(a.x, -a.y);
-				qb = sg_mk<C>(b.x, -b.y);
-			}
-			v[0][r] = sg_mk<C>(qa.x - qb.y, qa.y + qb.x);
-		}
-		if (k + 1 < rpb)
-			fetch(row + 1);
-		if (k > 0)
-			__syncthreads();	/* the previous row's last pass has read buf */
-		SgTop2 ta, tb;
-		sg_top2_init(ta);
-		sg_top2_init(tb);
-		sg_fft_io_regs<8>(buf, S, 1, S, tw, true, v, [&](int, int j, C c) {
-			const int idx = row * S + j;
-			if (CAND) {
-				sg_cand_push(cand + 2 * pair, c.x, thr[0], idx);
-				sg_cand_push(cand + 2 * pair + 1, c.y, thr[1], idx);
-				return;
-			}
-			sg_top2_add(ta, c.x, idx);
-			sg_top2_add(tb, c.y, idx);
-		});
-		if (CAND)
-			continue;
-		sg_best_block(ta, tb, red);
-		if (threadIdx.x == 0) {
-			best[(size_t)pair * S + row].a = ta;
-			best[(size_t)pair * S + row].b = tb;
-		}
+	sg_fft_io(buf, S, 1, S, tw, true,
+			[&](int, int i) {
+				C qa, qb;
+				if ((i & (H - 1)) == 0) {	/* kx = 0 or S/2: the packed real pair */
+					const C a = in[0], b = in[H];
+					qa = sg_mk<C>(i ? a.y : a.x, (T)0);
+					qb = sg_mk<C>(i ? b.y : b.x, (T)0);
+				} else if (i < H) {
+					qa = in[i];
+					qb = in[H + i];
+				} else {
+					const C a = in[S - i], b = in[H + S - i];
+					qa = sg_mk<C>(a.x, -a.y);
+					qb = sg_mk<C>(b.x, -b.y);
+				}
+				return sg_mk<C>(qa.x - qb.y, qa.y + qb.x);
+			},
+			[&](int, int j, C c) {
+				const int idx = row * S + j;
+				if (CAND) {
+					sg_cand_push(cand + 2 * pair, c.x, thr[0], idx);
+					sg_cand_push(cand + 2 * pair + 1, c.y, thr[1], idx);
+					return;
+				}
+				sg_top2_add(ta, c.x, idx);
+				sg_top2_add(tb, c.y, idx);
+			});
+	if (CAND)
+		return;
+	sg_best_block(ta, tb, red);
+	if (threadIdx.x == 0) {
+		best[(size_t)pair * S + row].a = ta;
+		best[(size_t)pair * S + row].b = tb;
 	}
 }
 
@@ -1321,9 +1298,6 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	int rpb = ctx->knobs.reg_rpb;
 	while (rpb > 1 && S % rpb != 0)
 		rpb >>= 1;
-	int rpbi = ctx->knobs.reg_rpbi;	/* the same for the inverse rows + arg-max */
-	while (rpbi > 1 && S % rpbi != 0)
-		rpbi >>= 1;
 	const int xcdmap = ctx->knobs.reg_xcd;	/* A/B knob SG_REG_XCD: 0 = strips in dispatch order */
 	/* generic rows: Bluestein needs m/8 threads (sg_lds_fft), the mixed passes take 256 */
 	const int gen_thr = pl.bluestein ? (pl.m / 8 < 64 ? 64 : pl.m / 8) : 256;
@@ -1456,11 +1430,11 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 				(const sg_c64 *)spec, S, CWh, tw, xcdmap, ctx->knobs.reg_pb);
 		HIPCHK(hipGetLastError());
 		if (mode)
-			hipLaunchKernelGGL((k_reg_rows_inv_half_argmax<sg_c64, true>), dim3(S / rpbi, np), dim3(row_thr), row_lds, s,
-					(const sg_c64 *)work, S, tw, best, res, cand, rpbi);
+			hipLaunchKernelGGL((k_reg_rows_inv_half_argmax<sg_c64, true>), dim3(S, np), dim3(row_thr), row_lds, s,
+					(const sg_c64 *)work, S, tw, best, res, cand);
 		else
-			hipLaunchKernelGGL((k_reg_rows_inv_half_argmax<sg_c64, false>), dim3(S / rpbi, np), dim3(row_thr), row_lds, s,
-					(const sg_c64 *)work, S, tw, best, (const SgRegOut *)nullptr, (SgCand *)nullptr, rpbi);
+			hipLaunchKernelGGL((k_reg_rows_inv_half_argmax<sg_c64, false>), dim3(S, np), dim3(row_thr), row_lds, s,
+					(const sg_c64 *)work, S, tw, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
 		HIPCHK(hipGetLastError());
 		return SG_OK;
 	};
@@ -1478,8 +1452,8 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 			hipLaunchKernelGGL((k_reg_cols_xpower<float2, 8>), dim3(S / CW32, np), dim3(colh_thr32), colh_lds32, s,
 					work32, (const float2 *)spec32, S, CW32, tw32, xcdmap, 1);
 		HIPCHK(hipGetLastError());
-		hipLaunchKernelGGL((k_reg_rows_inv_half_argmax<float2, false>), dim3(S / rpbi, np), dim3(row_thr), row_lds32, s,
-				(const float2 *)work32, S, tw32, best, (const SgRegOut *)nullptr, (SgCand *)nullptr, rpbi);
+		hipLaunchKernelGGL((k_reg_rows_inv_half_argmax<float2, false>), dim3(S, np), dim3(row_thr), row_lds32, s,
+				(const float2 *)work32, S, tw32, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
 		HIPCHK(hipGetLastError());
 		return SG_OK;
 	};
