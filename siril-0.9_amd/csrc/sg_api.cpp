@@ -31,6 +31,7 @@ __global__ void k_stack_hist(SgStackParams p, const int *tab, const int4 *norm, 
 		unsigned int *redo_list);
 void sg_dbg_why_dump(hipStream_t s);
 int sgh_block_threads(int ni);
+template <int NM>
 __global__ void k_stack_replay(SgStackParams p);
 __global__ void k_redo_to_literal(SgStackParams p, const unsigned int *list, const unsigned int *count,
 		unsigned int maxn);
@@ -615,7 +616,10 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		HIPCHK(ensure(dv.scratch, (size_t)SG_LIT_THREADS * (((size_t)N * 5 + 15) & ~(size_t)15)));
 		auto launch_tail = [&]() -> int {
 			if ((p.rejection == SG_SIGMA || p.rejection == SG_WINSORIZED) && N <= SG_REPLAY_MAXN) {
-				hipLaunchKernelGGL(k_stack_replay, dim3(2048), dim3(64 * SG_REPLAY_WAVES), 0, s, p);
+				if (N <= 512)	/* the per-wave LDS sized for 512 frames (k_stack_replay<SG_REPLAY_FASTN>) */
+					hipLaunchKernelGGL(k_stack_replay<512>, dim3(2048), dim3(64 * SG_REPLAY_WAVES), 0, s, p);
+				else
+					hipLaunchKernelGGL(k_stack_replay<SG_REPLAY_MAXN>, dim3(2048), dim3(64 * SG_REPLAY_WAVES), 0, s, p);
 				HIPCHK(hipGetLastError());
 				ctx->stats.launches++;
 			}

@@ -1104,12 +1104,16 @@ __device__ __forceinline__ void gather_stack(const SgStackParams &p, int64_t pix
 #ifndef SG_REPLAY_WFAST
 #define SG_REPLAY_WFAST 1	/* WINSORIZED passes on the same fast path (replay_winsor_inner) */
 #endif
-struct SgReplayLds {
-	uint16_t stack[SG_REPLAY_MAXN];
-	uint16_t w[SG_REPLAY_MAXN];
-	uint16_t wprev[SG_REPLAY_MAXN];	/* w before the current clamp (exact-mode recomputation) */
-	uint16_t orig[SG_REPLAY_MAXN];	/* the first pass's stack in frame order */
-	int8_t rej[SG_REPLAY_MAXN];
+/* per-wave LDS of the replay, sized for up to NM frames: k_stack_replay<SG_REPLAY_FASTN> for
+ * N <= 512 holds 10.6 KB per wave instead of 24.8 KB, so 7 two-wave workgroups fit a CU
+ * instead of 3 (the replay is latency-bound: one wave per pixel) */
+template <int NM>
+struct SgReplayLdsT {
+	uint16_t stack[NM];
+	uint16_t w[NM];
+	uint16_t wprev[NM];	/* w before the current clamp (exact-mode recomputation) */
+	uint16_t orig[NM];	/* the first pass's stack in frame order */
+	int8_t rej[NM];
 	uint32_t p1[SG_REPLAY_FASTN + 1];	/* prefix sums of the sorted stack (SIGMA fast passes) */
 	unsigned long long p2[SG_REPLAY_FASTN + 1];
 	int nsd, npass, handover;	/* fp80 recomputations, passes, fast-path handovers (SG_HIST_DBG=12 timing) */
@@ -1266,7 +1270,8 @@ __device__ __forceinline__ double replay_gsl_sd(const uint16_t *a, int n, int la
 		v = lit_sd(a, n);
 	return __shfl(v, 0, 64);
 }
-__device__ __forceinline__ double replay_gsl_sd(SgReplayLds &L, const uint16_t *a, int n, int lane) {
+template <class LDS>
+__device__ __forceinline__ double replay_gsl_sd(LDS &L, const uint16_t *a, int n, int lane) {
 	SG_RPROF(if (lane == 0) L.nsd++;)
 	return replay_gsl_sd(a, n, lane);
 }
@@ -1336,7 +1341,8 @@ __device__ __forceinline__ unsigned long long wave_excl_scan_u64(unsigned long l
  * a sigma the reference's way (ambiguous clamp or convergence decision) or give up (guard):
  * the pass then goes to the general loop.  On 1, median / sigma / e0 are the pass's
  * Winsorized values. */
-__device__ int replay_winsor_inner(SgReplayLds &L, const uint32_t (&xs)[SG_REPLAY_FASTN / 64], int lo, int hi,
+template <class LDS>
+__device__ int replay_winsor_inner(LDS &L, const uint32_t (&xs)[SG_REPLAY_FASTN / 64], int lo, int hi,
 		int lane, double &median, double &sigma, bool &e0) {
 	constexpr int KM = SG_REPLAY_FASTN / 64;
 	const int n = hi - lo;
@@ -1417,7 +1423,8 @@ __device__ int replay_winsor_inner(SgReplayLds &L, const uint32_t (&xs)[SG_REPLA
 	return 1;
 }
 
-__device__ int replay_sigma_fast(SgReplayLds &L, int &N, int &r, int &iter, double sl, double sh, int lane,
+template <class LDS>
+__device__ int replay_sigma_fast(LDS &L, int &N, int &r, int &iter, double sl, double sh, int lane,
 		uint32_t &clo, uint32_t &chi, uint16_t *value, int type = 2) {
 	constexpr int KM = SG_REPLAY_FASTN / 64;
 	{	/* prefix sums over the sorted stack, 8 consecutive samples per lane */
@@ -1561,8 +1568,8 @@ __device__ int replay_sigma_fast(SgReplayLds &L, int &N, int &r, int &iter, doub
 /* PMAX: positions per lane of the general loop's per-lane chunks (8 for N <= 512, so the chunk
  * arrays d[] / kv[] are indexed statically and stay in registers; 32 up to SG_REPLAY_MAXN,
  * where they live in scratch) */
-template <int PMAX>
-__device__ int replay_pixel(SgReplayLds &L, int N0, int type, double sl, double sh, int lane, uint16_t *value,
+template <int PMAX, class LDS>
+__device__ int replay_pixel(LDS &L, int N0, int type, double sl, double sh, int lane, uint16_t *value,
 		uint32_t *rlo, uint32_t *rhi) {
 	int N = N0, r = 0, n, iter = 0;
 	uint32_t clo = 0, chi = 0;
@@ -1801,15 +1808,16 @@ k_redo_to_literal(SgStackParams p, const unsigned int *__restrict__ list, const 
 	}
 }
 
+template <int NM>
 __global__ void __launch_bounds__(64 * SG_REPLAY_WAVES)
 k_stack_replay(SgStackParams p) {
-	__shared__ SgReplayLds Ls[SG_REPLAY_WAVES];
+	__shared__ SgReplayLdsT<NM> Ls[SG_REPLAY_WAVES];
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-	SgReplayLds &L = Ls[wv];
+	SgReplayLdsT<NM> &L = Ls[wv];
 	unsigned int count = *p.flag_count;
 	if (count > p.flag_cap)
 		count = p.flag_cap;
-	if ((p.rejection != 2 && p.rejection != 4) || p.N > SG_REPLAY_MAXN)
+	if ((p.rejection != 2 && p.rejection != 4) || p.N > NM)
 		return;
 	const unsigned int nw = gridDim.x * SG_REPLAY_WAVES;
 	for (unsigned int i = blockIdx.x * SG_REPLAY_WAVES + wv; i < count; i += nw) {
@@ -1838,7 +1846,7 @@ k_stack_replay(SgStackParams p) {
 		uint32_t rl, rh;
 		const int ok = p.N <= SG_REPLAY_FASTN ? replay_pixel<SG_REPLAY_FASTN / 64>(L, p.N, p.rejection, p.sig0, p.sig1,
 									     lane, &v, &rl, &rh)
-						     : replay_pixel<SG_REPLAY_MAXN / 64>(L, p.N, p.rejection, p.sig0, p.sig1,
+						     : replay_pixel<NM / 64>(L, p.N, p.rejection, p.sig0, p.sig1,
 									     lane, &v, &rl, &rh);
 #ifdef SG_REPLAY_PROF
 		if (p.dbg == 12 && lane == 0) {
@@ -1874,6 +1882,8 @@ k_stack_replay(SgStackParams p) {
 		}
 	}
 }
+template __global__ void k_stack_replay<SG_REPLAY_FASTN>(SgStackParams);
+template __global__ void k_stack_replay<SG_REPLAY_MAXN>(SgStackParams);
 
 /* phase 1: queued pixels (class LITERAL) replayed with an all-zero incoming rejected[];
  * a pixel whose first pass breaks early with N > 4 read its predecessor's stale entries
