@@ -30,7 +30,7 @@ template <int REJ, int NORM, int NI>
 __global__ void k_stack_hist(SgStackParams p, const int *tab, const int4 *norm, unsigned int *redo_count,
 		unsigned int *redo_list);
 void sg_dbg_why_dump(hipStream_t s);
-int sgh_block_threads(int ni);
+int sgh_block_threads(int ni, int rej);
 template <int NM>
 __global__ void k_stack_replay(SgStackParams p);
 __global__ void k_redo_to_literal(SgStackParams p, const unsigned int *list, const unsigned int *count,
@@ -550,14 +550,14 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			if (p.dbg == 14) {	/* A/B: report the resident workgroups per CU */
 				int per_cu = -1;
 				(void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ni == 2 ? (const void *)k_stack_hist<2, 0, 2>
-						: (const void *)k_stack_hist<2, 0, 1>, sgh_block_threads(ni), (size_t)ctx->knobs.hist_ldspad);
+						: (const void *)k_stack_hist<2, 0, 1>, sgh_block_threads(ni, 2), (size_t)ctx->knobs.hist_ldspad);
 				hipDeviceProp_t prop;
 				(void)hipGetDeviceProperties(&prop, dv.id);
 				fprintf(stderr, "k_stack_hist: %d workgroups/CU (lds/CU %zu, lds/block max %zu, pad %d)\n", per_cu,
 						(size_t)prop.maxSharedMemoryPerMultiProcessor, (size_t)prop.sharedMemPerBlock, ctx->knobs.hist_ldspad);
 			}
 			const size_t lds_pad = (size_t)ctx->knobs.hist_ldspad;
-			const dim3 hg((unsigned)nblk_h), hb((unsigned)sgh_block_threads(ni));
+			const dim3 hg((unsigned)nblk_h), hb((unsigned)sgh_block_threads(ni, p.rejection == SG_WINSORIZED ? 4 : 2));
 			switch ((p.rejection == SG_WINSORIZED ? 10 : 0) + norm + 100 * ni) {
 			case 100: hipLaunchKernelGGL((k_stack_hist<2, 0, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 101: hipLaunchKernelGGL((k_stack_hist<2, 1, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;

@@ -63,6 +63,14 @@ struct SghCfg {
 	static constexpr int WAVES = NI == 1 ? SGH_WAVES_PER_NI : SGH_WAVES_NI2;
 	static constexpr int WPE = NI == 1 ? 4 : (SGH_WAVES_NI2 == 4 ? 2 : 4);	/* waves per SIMD (launch bound) */
 };
+#ifndef SGH_WINS_WAVES
+#define SGH_WINS_WAVES 2	/* waves per 128-pixel WINSORIZED tile: 2, each building twice the frames, so 4 tiles fit a CU at 2 waves per SIMD (26.5 -> 25.7 ms on configs[4], profiles/r03_wins_ab.log); 4: the SIGMA shape */
+#endif
+/* waves of a tile of kernel k_stack_hist<REJ, ., NI> */
+template <int REJ, int NI>
+struct SghW {
+	static constexpr int WAVES = (REJ == 4 && NI == 1) ? SGH_WINS_WAVES : SghCfg<NI>::WAVES;
+};
 #ifndef SGH_CENTER
 #define SGH_CENTER 16		/* frames used for the centre estimate */
 #endif
@@ -1832,7 +1840,7 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
 template <int REJ, int NORM, int NI>
 __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro, SghLds<NI> &L, int bid, bool wait_prev,
 		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
-	constexpr int WAVES = SghCfg<NI>::WAVES, COLS = 128 * NI;
+	constexpr int WAVES = SghW<REJ, NI>::WAVES, COLS = 128 * NI;
 	const int tid = threadIdx.x, lane = tid & 63;
 	const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 	const int ntx = (p.W + COLS - 1) / COLS;
@@ -1889,11 +1897,11 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 			sgh_build<true, SGH_NBUF, NORM, NI>(p, ro, L, F, wave, lane, lo2, nonzero, nsat, counted, wait_prev);
 	} else {
 		if (interior)
-			sgh_build_half<false, NORM, NI, NI == 1 ? SGH_NB : SGH_NB2>(p, ro, L, F, wave, lane, lo2, nonzero, nsat,
-					counted, wait_prev);
+			sgh_build_half<false, NORM, NI, NI == 1 ? SGH_NB : SGH_NB2, WAVES>(p, ro, L, F, wave, lane, lo2, nonzero,
+					nsat, counted, wait_prev);
 		else
-			sgh_build_half<true, NORM, NI, NI == 1 ? SGH_NB : SGH_NB2>(p, ro, L, F, wave, lane, lo2, nonzero, nsat,
-					counted, wait_prev);
+			sgh_build_half<true, NORM, NI, NI == 1 ? SGH_NB : SGH_NB2, WAVES>(p, ro, L, F, wave, lane, lo2, nonzero,
+					nsat, counted, wait_prev);
 	}
 	if (counted) {
 #pragma unroll
@@ -1975,10 +1983,10 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
  * workgroups (69 KB of LDS each) or four 4-wave ones (36 KB) per CU: 16 waves, at most 128
  * VGPRs. */
 #ifndef SGH_WINS_WPE
-#define SGH_WINS_WPE 3	/* WINSORIZED: waves per SIMD the register budget is sized for (4: 128 VGPRs, spills) */
+#define SGH_WINS_WPE 2	/* WINSORIZED: waves per SIMD the register budget is sized for (2-wave tiles: 4 tiles per CU, the LDS limit; 4 waves per SIMD = 128 VGPRs spill) */
 #endif
 template <int REJ, int NORM, int NI>
-__global__ void __launch_bounds__(64 * SghCfg<NI>::WAVES, (REJ == 4 && NI == 1) ? SGH_WINS_WPE : SghCfg<NI>::WPE)
+__global__ void __launch_bounds__((64 * SghW<REJ, NI>::WAVES), ((REJ == 4 && NI == 1) ? SGH_WINS_WPE : SghCfg<NI>::WPE))
 k_stack_hist(SgStackParams p, const int *__restrict__ tab, const int4 *__restrict__ norm,
 		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
 	SghRo ro;
@@ -2022,6 +2030,8 @@ template __global__ void k_stack_hist<4, 0, 2>(SgStackParams, const int *, const
 		unsigned int *);
 
 /* threads per histogram workgroup (the host's launch shape) */
-int sgh_block_threads(int ni) {
+int sgh_block_threads(int ni, int rej) {
+	if (rej == 4)
+		return ni == 2 ? 64 * SghW<4, 2>::WAVES : 64 * SghW<4, 1>::WAVES;
 	return ni == 2 ? 64 * SghCfg<2>::WAVES : 64 * SghCfg<1>::WAVES;
 }
