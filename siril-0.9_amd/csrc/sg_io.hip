@@ -90,15 +90,23 @@ static int rd_parallel(const std::vector<SgRead> &segs) {
 				return -1;
 		return 0;
 	}
-	/* slice t covers bytes [t total / nt, (t + 1) total / nt) of the concatenated reads */
+	/* slice t covers bytes [b(t), b(t + 1)) of the concatenated reads, b(t) = t total / nt; the
+	 * slice of byte x is the largest t with b(t) <= x (x nt / total alone can name the slice
+	 * before it when total is not a multiple of nt, and the read would then never advance) */
+	auto bound = [&](int t) { return (size_t)t * total / (size_t)nt; };
 	std::vector<std::vector<SgRead>> part((size_t)nt);
 	size_t pos = 0;
 	for (const SgRead &r : segs) {
 		size_t done = 0;
 		while (done < r.len) {
-			const int t = (int)std::min<size_t>((size_t)nt - 1, (pos + done) * (size_t)nt / total);
-			const size_t end_t = (size_t)(t + 1) * total / (size_t)nt;
-			const size_t take = std::min(r.len - done, end_t - (pos + done));
+			const size_t x = pos + done;
+			int t = (int)std::min<size_t>((size_t)nt - 1, x * (size_t)nt / total);
+			while (t + 1 < nt && bound(t + 1) <= x)
+				t++;
+			while (t > 0 && bound(t) > x)
+				t--;
+			const size_t end_t = bound(t + 1);
+			const size_t take = std::min(r.len - done, end_t - x);
 			part[(size_t)t].push_back({r.fd, r.dst + done, take, r.off + (int64_t)done});
 			done += take;
 		}

@@ -1344,7 +1344,9 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	 * re-runs) and the near-tie candidates of one batch */
 	const int NP = npairs_total > 0 ? npairs_total : 1;
 	HIPCHK(ensure(dv.reg_spec, plane * sizeof(sg_c64) + (fp32 ? plane * sizeof(float2) : 0)));
-	HIPCHK(ensure(dv.reg_work, (size_t)Bc * pair_bytes));
+	/* the fp64 near-tie re-runs use the same buffer: at least one fp64 plane (B64 >= 1 even
+	 * when the fp32 batch is a single pair, whose plane is half that size) */
+	HIPCHK(ensure(dv.reg_work, std::max((size_t)Bc * pair_bytes, (size_t)B64 * plane * sizeof(sg_c64))));
 	const size_t o_out = ((size_t)std::max(Bc, B64) * S * sizeof(SgBest) + 255) & ~(size_t)255;
 	const size_t o_fab = o_out + (((size_t)(NP + 1) * sizeof(SgRegOut) + 255) & ~(size_t)255);
 	const size_t o_en = o_fab + (((size_t)(NP + 1) * 4 * sizeof(int) + 255) & ~(size_t)255);

@@ -1645,9 +1645,6 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, const SghRo &r
 #endif
 #ifndef SGH_WINS_ORDER
 #define SGH_WINS_ORDER 1	/* WINSORIZED finish: columns with zeros / 65535s first (sgh_tile) */
-#ifndef SGH_WINS_SPLIT
-#define SGH_WINS_SPLIT 0	/* WINSORIZED finish waves (A/B): 0 waves 0 / 1, 1 alternating pairs, 2 all four */
-#endif
 #endif
 
 template <bool EDGE, int NORM, int NI, int NB, int BW = SghCfg<NI>::WAVES, class BAR = SghWgBarrier>
@@ -1943,20 +1940,9 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 				L.perm[sb ? na + rb : ns + (64 - na) + (lane - rb)] = (uint8_t)cb;
 			}
 			__syncthreads();
-#if SGH_WINS_SPLIT == 1	/* A/B: tiles alternate between waves 0 / 1 and waves 2 / 3 */
-			const int fw = wave - (int)((blockIdx.x & 1u) << 1);
-			if (fw < 0 || fw >= 2)
-				return;
-			const int col = L.perm[64 * fw + lane];
-#elif SGH_WINS_SPLIT == 2	/* A/B: all four waves, 32 columns each */
-			if (lane >= 32)
-				return;
-			const int col = L.perm[32 * wave + lane];
-#else
 			if (wave >= 2)
 				return;
 			const int col = L.perm[64 * wave + lane];
-#endif
 			sgh_finish2<REJ, false, NI>(p, L, col, 0, col_lo(col), R, c, col_x(col), redo_count, redo_list);
 			return;
 		}

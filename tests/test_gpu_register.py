@@ -185,6 +185,27 @@ def test_register_exact_tie_takes_lowest_index(gpu_ctx, S):
         assert st.reg_fp64_reruns >= 1          # the fp32 passes handed the pair to fp64 first
 
 
+@pytest.mark.gpu
+def test_register_tie_rerun_on_fresh_context_large_side():
+    """a single fp32 pair re-run in fp64 on a FRESH context at S = 1024: the fp64 plane is twice
+    the fp32 pair plane, and the work buffer is sized for it (no other test's larger buffer to
+    hide an overflow)"""
+    S = 1024
+    ref, img = _periodic_pair(S, 3, 5, seed=S)
+    sel = np.stack([ref, img]).astype(np.uint16)
+    with sg.Context() as c:
+        gx, gy, _ = c.register_dft(sel)
+        st = c.stats()
+    k1 = ((-5) % S, (-3) % S)
+    k2 = (k1[0], (k1[1] + S // 2) % S)
+    lo = min(k1[0] * S + k1[1], k2[0] * S + k2[1])
+    y, x = divmod(lo, S)
+    assert (gx[1], gy[1]) == (x - S if x > S // 2 else x, y - S if y > S // 2 else y)
+    assert st.reg_ties_resolved >= 1
+    if os.environ.get("SG_REG_FP", "32") == "32":
+        assert st.reg_fp64_reruns >= 1
+
+
 def test_register_near_tie_takes_exact_maximum(gpu_ctx):
     """two maxima differing by exactly 1 in the integer correlation (a cross term of two
     single-pixel +1 perturbations, one in each frame, lands on the later one): flagged and

@@ -142,6 +142,25 @@ def test_load_device(tmp_path, gpu_ctx, name, kw, C):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(5, 1000, 1000, 16), (7, 999, 1001, 8)])
+def test_load_device_ragged_read_slices(tmp_path, gpu_ctx, shape):
+    """a batch whose byte count is not a multiple of the reader thread count (5 x 1000^2 u16 =
+    10 MB over 3 threads; an odd 8-bit frame): every slice boundary advances (sg_io.hip
+    rd_parallel), the frames load whole"""
+    import torch
+    N, H, W, depth = shape
+    frames = _frames(N, 1, H, W, depth, seed=H)
+    p = str(tmp_path / "ragged.ser")
+    write_ser(p, frames, depth=depth)
+    with sg.Seq.open_ser(p) as seq:
+        d = torch.zeros(N * H * W, dtype=torch.int16, device="cuda")
+        torch.cuda.synchronize()
+        gpu_ctx.load_seq_device(seq, d.data_ptr())
+        got = d.cpu().numpy().view(np.uint16).reshape(N, 1, H, W)
+        assert np.array_equal(got, frames)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("fmt", ["ser", "fits"])
 def test_stack_from_files(tmp_path, gpu_ctx, fmt):
     """stack_mean_with_rejection fed by the library's own region reader (the reference's
