@@ -33,6 +33,8 @@ typedef char gchar;
 #endif
 
 #define USHORT_IMG 20	/* cfitsio bitpix codes */
+#define TSTRING 16	/* cfitsio datatype codes */
+#define TDOUBLE 82
 #define BYTE_IMG 8
 #define FLEN_VALUE 71	/* cfitsio fitsio.h */
 #define PREVIEW_NB 2	/* src/core/siril.h:171 */
@@ -210,6 +212,9 @@ int seq_opened_read_region(sequence *seq, int layer, int index, WORD *buffer, co
 int seq_read_frame_part(sequence *seq, int layer, int index, fits *dest, const rectangle *area,
 		gboolean do_photometry);
 int get_thread_run(void);
+/* cfitsio (Siril links the real one; here siril_env.c reads the header cards of the
+ * sequence's opened files): TDOUBLE and TSTRING values */
+int fits_read_key(fitsfile *fptr, int datatype, const char *keyname, void *value, char *comm, int *status);
 int get_registration_layer(void);
 int compute_normalization(struct stacking_args *args, norm_coeff *coeff, normalization mode);
 void clearfits(fits *fit);

@@ -32,6 +32,43 @@ struct harness_com com = { 16 };
 static int reglayer = -1;
 static int cancel_after = -1;	/* tests: get_thread_run() turns false after this many calls */
 
+/* the opened file of a FITS frame: what seq->fptr[i] points to (seq_open_image) */
+struct fitsfile {
+	sg_seq *gs;
+	int index;
+};
+
+/* cfitsio fits_read_key for the two datatypes the glue reads: the value text of the key
+ * (sg_seq_read_key), converted as ffc2d does (numbers; logical T / F = 1 / 0).  Status codes
+ * are cfitsio's: KEY_NO_EXIST 202, BAD_C2D 409 */
+int fits_read_key(fitsfile *fptr, int datatype, const char *keyname, void *value, char *comm, int *status) {
+	char v[80];
+	(void)comm;
+	if (*status > 0)
+		return *status;
+	if (!fptr || sg_seq_read_key(fptr->gs, fptr->index, keyname, v, sizeof v))
+		return *status = 202;
+	if (datatype == TSTRING) {
+		memcpy(value, v, 70);
+		((char *)value)[70] = 0;
+		return 0;
+	}
+	if (datatype != TDOUBLE)
+		return *status = 410;	/* BAD_DATATYPE */
+	if (!strcmp(v, "T") || !strcmp(v, "F")) {
+		*(double *)value = v[0] == 'T' ? 1.0 : 0.0;
+		return 0;
+	}
+	char *end = NULL;
+	const double d = strtod(v, &end);
+	while (end && *end == ' ')
+		end++;
+	if (!end || end == v || *end)
+		return *status = 409;
+	*(double *)value = d;
+	return 0;
+}
+
 /* sequence -> opened frame source */
 #define MAX_SEQS 64
 static struct { sequence *seq; sg_seq *gs; } seqs[MAX_SEQS];
@@ -218,6 +255,14 @@ static sequence *new_sequence(sg_seq *gs, const char *name, sequence_type type) 
 		seq->imgparam[i].incl = TRUE;
 	}
 	seq->regparam = calloc(info.nb_layers, sizeof(regdata *));
+	if (type == SEQ_REGULAR) {	/* the opened files (seq_open_image leaves them in fptr[]) */
+		seq->fptr = calloc(info.nb_frames, sizeof(fitsfile *));
+		for (int i = 0; i < info.nb_frames; i++) {
+			seq->fptr[i] = malloc(sizeof(struct fitsfile));
+			seq->fptr[i]->gs = gs;
+			seq->fptr[i]->index = i;
+		}
+	}
 	seqs[slot].seq = seq;
 	seqs[slot].gs = gs;
 	return seq;
@@ -256,6 +301,10 @@ void harness_close(sequence *seq) {
 		free(seq->imgparam[i].stats);
 	for (int l = 0; l < seq->nb_layers; l++)
 		free(seq->regparam[l]);
+	if (seq->fptr)
+		for (int i = 0; i < seq->number; i++)
+			free(seq->fptr[i]);
+	free(seq->fptr);
 	free(seq->regparam);
 	free(seq->imgparam);
 	free(seq->seqname);
@@ -263,6 +312,11 @@ void harness_close(sequence *seq) {
 }
 
 void harness_set_registration_layer(int layer) { reglayer = layer; }
+static int run_in_thread = 0;	/* registration launched from the GUI thread handler (start_in_new_thread) */
+void harness_set_run_in_thread(int on) { run_in_thread = on; }
+double harness_gfit_exposure(void) { return gfit.exposure; }
+int siril_gpu_set_devices(int n, const int *devs);
+int harness_set_devices(int n, const int *devs) { return siril_gpu_set_devices(n, devs); }
 void harness_set_max_thread(int n) { com.max_thread = n; }
 void harness_set_cancel_after(int n) { cancel_after = n; }
 void harness_set_reference_image(sequence *seq, int ref) { seq->reference_image = ref; }
@@ -335,7 +389,7 @@ int harness_register(sequence *seq, int layer, int x, int y, int size, int proce
 	args.selection.y = y;
 	args.selection.w = args.selection.h = size;
 	args.layer = layer;
-	args.run_in_thread = FALSE;
+	args.run_in_thread = run_in_thread;
 	args.retval = args.func(&args);
 	return args.retval;
 }

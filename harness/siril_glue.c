@@ -18,13 +18,31 @@
 #define _(s) (s)
 #endif
 
-/* one context for the process (in Siril: created in initialize_stacking_methods()) */
+/* one context for the process (in Siril: created in initialize_stacking_methods()), driving
+ * every visible GPU: sg_stack_u16 gives each device a share of the output rows and its own
+ * host thread (the reference's OpenMP team over row blocks, stacking.c:1513-1516) */
 static sg_ctx *gpu_ctx;
+static int gpu_ndev = -1;	/* -1: all visible devices */
+static int gpu_devs[16];
 
 sg_ctx *siril_gpu_context(void) {
-	if (!gpu_ctx && sg_init(&gpu_ctx, 0, NULL) != SG_OK)
+	if (!gpu_ctx && sg_init(&gpu_ctx, gpu_ndev, gpu_ndev > 0 ? gpu_devs : NULL) != SG_OK)
 		gpu_ctx = NULL;
 	return gpu_ctx;
+}
+
+/* choose the devices of the context (a setcpu-like setting, src/core/command.c:1460-1484):
+ * n = -1 all visible devices; devs may repeat an id (several slots sharing one card) */
+int siril_gpu_set_devices(int n, const int *devs) {
+	if (n > 16 || (n > 0 && !devs))
+		return -1;
+	if (gpu_ctx)
+		sg_shutdown(gpu_ctx);
+	gpu_ctx = NULL;
+	gpu_ndev = n > 0 ? n : -1;
+	for (int i = 0; i < n; i++)
+		gpu_devs[i] = devs[i];
+	return siril_gpu_context() ? 0 : -1;
 }
 
 void siril_gpu_release(void) {
@@ -51,9 +69,55 @@ static int keep_going(void *u) {
 	return get_thread_run();
 }
 
+/*
+ * the summed exposure the stackers hand to gfit.exposure:
+ *  - stack_mean_with_rejection / stack_median (:1284-1294, :457-467): for FITS sequences, per
+ *    stacked image EXPTIME, or EXPOSURE when EXPTIME is absent or <= 0, read from the opened
+ *    file; SER sequences sum nothing;
+ *  - stack_summing / addmax / addmin (:294-295, :912-913, :1068-1069): fit->exposure of every
+ *    frame seq_read_frame loaded, i.e. readfits' __tryToFindKeywords(EXPTIME, EXPOSURE)
+ *    (image_format_fits.c:41-52,135), which leaves the previous frame's value when neither
+ *    key is present (wfit[0] is reused and not cleared; 0 before the first); SER frames carry
+ *    no exposure (ser_read_frame never sets it).
+ */
+static double summed_exposure(sequence *seq, const int *indices, int nb, int per_frame_read) {
+	double exposure = 0.0, last = 0.0, tmp;
+	int i, status;
+	if (seq->type != SEQ_REGULAR || !seq->fptr)
+		return 0.0;
+	for (i = 0; i < nb; i++) {
+		fitsfile *fptr = seq->fptr[indices[i]];
+		if (per_frame_read) {
+			status = 0;
+			fits_read_key(fptr, TDOUBLE, "EXPTIME", &tmp, NULL, &status);
+			if (status > 0) {
+				status = 0;
+				fits_read_key(fptr, TDOUBLE, "EXPOSURE", &tmp, NULL, &status);
+			}
+			if (!status)
+				last = tmp;
+			exposure += last;
+			continue;
+		}
+		status = 0;
+		fits_read_key(fptr, TDOUBLE, "EXPTIME", &tmp, NULL, &status);
+		if (status || tmp <= 0.0) {
+			status = 0;
+			fits_read_key(fptr, TDOUBLE, "EXPOSURE", &tmp, NULL, &status);
+		}
+		if (!status)
+			exposure += tmp;
+	}
+	return exposure;
+}
+
 /* gfit takes ownership of the planar bottom-up result, as the reference's
- * copyfits(fit, &gfit, CP_FORMAT) + data hand-over does (stacking.c:1820-1827, :778-785) */
-static void hand_over_to_gfit(WORD *out, const sequence *seq) {
+ * copyfits(fit, &gfit, CP_FORMAT) + data hand-over does (stacking.c:1820-1827, :778-785).
+ * CP_FORMAT copies the geometry, bitpix and lo / hi of the stacker's working fits
+ * (image_format_fits.c:996-1006): geometry and bitpix are set here; lo / hi are the stale
+ * values of the reused wfit[0] in the reference (never set by the rejection / median
+ * stackers, the last frame's for the sum stackers), so only SUM's hi (:324) is carried. */
+static void hand_over_to_gfit(WORD *out, const sequence *seq, double exposure) {
 	const unsigned int W = seq->rx, H = seq->ry;
 	const int C = seq->nb_layers;
 	if (gfit.data)
@@ -69,7 +133,7 @@ static void hand_over_to_gfit(WORD *out, const sequence *seq) {
 	gfit.pdata[RLAYER] = out;
 	gfit.pdata[GLAYER] = C == 3 ? out + (size_t)W * H : out;
 	gfit.pdata[BLAYER] = C == 3 ? out + (size_t)W * H * 2 : out;
-	gfit.exposure = 0.0;	/* the EXPTIME sum of FITS headers is not carried by this path */
+	gfit.exposure = exposure;	/* :326, :781, :1823 */
 }
 
 /*
@@ -150,7 +214,8 @@ static int gpu_stack(struct stacking_args *args, int method, const int *indices,
 				siril_log_message(_("Pixel rejection in channel #%d: %.3lf%% - %.3lf%%\n"), i,
 						rej[i][0] / nb_tot * 100.0, rej[i][1] / nb_tot * 100.0);
 		}
-		hand_over_to_gfit(out, seq);
+		hand_over_to_gfit(out, seq, summed_exposure(seq, indices, nb,
+					method != SG_STACK_MEAN && method != SG_STACK_MEDIAN));
 	}
 end:
 	free(sx);
@@ -221,7 +286,7 @@ int stack_addmin(struct stacking_args *args) {
 int register_shift_dft(struct registration_args *args) {
 	sequence *seq = args->seq;
 	const int n = seq->number, S = args->selection.w;
-	int f, rc;
+	int f, rc, cancelled = 0, best_frame = -1;
 	sg_ctx *ctx = siril_gpu_context();
 	if (!ctx || args->selection.w != args->selection.h)
 		return -1;
@@ -237,22 +302,39 @@ int register_shift_dft(struct registration_args *args) {
 		rc = -2;
 		goto end;
 	}
-	for (f = 0; f < n; f++) {
+	/* the reference frame first (:236-244), then the frames in index order: with run_in_thread
+	 * the loop polls get_thread_run() before each frame and, when it turns false, registers no
+	 * further frame (:281-285).  The reference then still returns 0, keeps what it registered
+	 * (abort does not set ret) and normalizeQualityData stops at once on the same poll
+	 * (:166-168), leaving the qualities raw.  This is the outcome of the reference's OpenMP
+	 * loop run by one thread. */
+	for (f = 0; f < n; f++)
 		inc[f] = args->process_all_frames || seq->imgparam[f].incl;
-		if (!inc[f] && f != ref)
-			continue;
+	for (f = -1; f < n; f++) {
+		const int idx = f < 0 ? ref : f;
+		if (f >= 0) {
+			if (f == ref || !inc[f])
+				continue;
+			if (!cancelled && args->run_in_thread && !get_thread_run())
+				cancelled = 1;
+			if (cancelled) {
+				inc[f] = 0;	/* not registered: keeps its regdata */
+				continue;
+			}
+		}
 		fits fit;
 		memset(&fit, 0, sizeof fit);
-		if (seq_read_frame_part(seq, args->layer, f, &fit, &args->selection, FALSE)) {
-			siril_log_message(_("Could not load partial image %d\n"), f);
+		if (seq_read_frame_part(seq, args->layer, idx, &fit, &args->selection, FALSE)) {
+			siril_log_message(_("Could not load partial image %d\n"), idx);
 			clearfits(&fit);
 			rc = 1;	/* :373-381 (the reference frame: :238-244 returns its status) */
 			goto end;
 		}
-		memcpy(sel + (size_t)f * S * S, fit.data, (size_t)S * S * sizeof(WORD));
+		memcpy(sel + (size_t)idx * S * S, fit.data, (size_t)S * S * sizeof(WORD));
 		clearfits(&fit);
 	}
-	rc = sg_register_dft_u16(ctx, sel, n, S, ref, inc, sx, sy, q);
+	/* shifts and RAW qualities from the GPU (every device of the context shares the frames) */
+	rc = sg_register_dft_u16_raw(ctx, sel, n, S, ref, inc, sx, sy, q);
 	if (rc) {
 		siril_log_message("%s\n", sg_last_error(ctx));
 		goto end;
@@ -263,15 +345,37 @@ int register_shift_dft(struct registration_args *args) {
 			rc = -2;
 			goto end;
 		}
-		for (f = 0; f < n; f++)
-			if (inc[f] || f == ref) {
-				rd[f].shiftx = sx[f];
-				rd[f].shifty = sy[f];
-				rd[f].quality = q[f];
+		/* q_min / q_max / q_index (:270-271, :315-324): seeded by the reference frame, then the
+		 * registered frames in processing order with the reference's min() macro */
+		double q_min = q[ref], q_max = q[ref];
+		int q_index = ref;
+		rd[ref].shiftx = 0;
+		rd[ref].shifty = 0;
+		rd[ref].quality = q[ref];
+		for (f = 0; f < n; f++) {
+			if (f == ref || !inc[f])
+				continue;
+			rd[f].shiftx = sx[f];
+			rd[f].shifty = sy[f];
+			rd[f].quality = q[f];
+			if (q[f] > q_max) {
+				q_max = q[f];
+				q_index = f;
 			}
+			q_min = q_min < q[f] ? q_min : q[f];
+		}
 		seq->regparam[args->layer] = rd;
+		/* normalizeQualityData (:163-176) over the included frames, unless cancelled */
+		for (f = 0; f < n && !cancelled; f++) {
+			if (!args->process_all_frames && !seq->imgparam[f].incl)
+				continue;
+			rd[f].quality -= q_min;
+			rd[f].quality /= (q_max - q_min);
+		}
+		best_frame = q_index;
 	}
 	siril_log_message(_("Registration finished.\n"));
+	siril_log_message(_("Best frame: #%d.\n"), best_frame);	/* :397 (siril_log_color_message, bold) */
 end:
 	free(sel);
 	free(inc);

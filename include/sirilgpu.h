@@ -88,7 +88,10 @@ typedef struct {
 
 typedef struct sg_ctx sg_ctx;
 
-/* Open the devices this context drives (ndev = 0: device 0).  One HIP stream per device. */
+/* Open the devices this context drives: devs[0..ndev) (NULL: 0..ndev-1), ndev = 0 device 0,
+ * ndev < 0 every visible device.  An id may repeat (context slots sharing one card).  One HIP
+ * stream per slot; the host-pull calls (sg_stack_u16, sg_register_dft_u16) drive every slot
+ * from its own host thread. */
 int sg_init(sg_ctx **ctx, int ndev, const int *devs);
 void sg_shutdown(sg_ctx *ctx);
 const char *sg_last_error(const sg_ctx *ctx);
@@ -96,10 +99,17 @@ const char *sg_last_error(const sg_ctx *ctx);
 /*
  * Host-pull stack: replaces the bodies of stack_summing / stack_mean_with_rejection /
  * stack_median / stack_addmax / stack_addmin (src/stacking/stacking.c:196,1189,362,824,979).
- * Pixels are pulled through `pull` (seq_opened_read_region shape) into pinned staging and
- * uploaded to HBM; the result is written bottom-up into `out` (nb_layers*H*W WORDs, the
- * buffer the reference hands to gfit.data).  rej receives the per-channel low/high rejection
- * counters of :1796-1817 (MEAN only), maxim the sum maximum of :311-313 (SUM only).
+ * Every device of the context takes a contiguous share of the output rows (the reference's
+ * row blocks, :1397-1476, are the natural shard) and is driven by its own host thread, whose
+ * readers (the reference's team size max_thread shared between the devices, at most 8 per
+ * device) pull that share's frame rows through `pull` (seq_opened_read_region shape, called
+ * concurrently as the reference's OpenMP team does) into pinned staging and upload them
+ * directly to that device; a share larger than the device's HBM budget is stacked in row bands.
+ * The result is written bottom-up into `out` (nb_layers*H*W WORDs, the buffer the reference
+ * hands to gfit.data).  rej receives the per-channel low/high rejection counters of
+ * :1796-1817 (MEAN only, summed over the devices), maxim the sum maximum of :311-313 (SUM only,
+ * over the whole image; the 65535/max scaling uses it on every device).  `cont` is polled once
+ * per frame read (get_thread_run, :1539); a cancellation returns SG_ERR_GENERIC.
  */
 int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *desc, sg_read_region_fn pull, void *user,
 		sg_should_continue_fn cont, void *cont_user, uint16_t *out, uint64_t rej[3][2],
@@ -172,6 +182,13 @@ int sg_compute_normalization(int mode, int nframes, int ref_image, const double 
  */
 int sg_register_dft_u16(sg_ctx *ctx, const uint16_t *sel, int nframes, int S, int ref_image,
 		const int *included, int *shiftx, int *shifty, double *quality);
+/* the same with the qualities left RAW (QualityEstimate of the reference and of every
+ * registered frame): the glue replays the reference's q_min / q_max / q_index bookkeeping and
+ * normalizeQualityData itself, which a cancelled registration skips (registration.c:166-168).
+ * Host selections: with several devices in the context the frames are split into contiguous
+ * shards, one host thread per device. */
+int sg_register_dft_u16_raw(sg_ctx *ctx, const uint16_t *sel, int nframes, int S, int ref_image,
+		const int *included, int *shiftx, int *shifty, double *quality_raw);
 int sg_register_dft_u16_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int nframes,
 		int S, int ref_image, const int *included, int *shiftx, int *shifty,
 		double *quality, void *stream);

@@ -32,6 +32,12 @@ int sg_seq_open_fits(const char *const *paths, int nframes, sg_seq **out);
 void sg_seq_close(sg_seq *seq);
 int sg_seq_get_info(const sg_seq *seq, sg_seq_info *info);
 
+/* FITS header keyword `key` of frame `index` (what fits_read_key reads from seq->fptr[index]
+ * for the EXPTIME / EXPOSURE sums of the stackers, src/stacking/stacking.c:1284-1294, and
+ * readfits' header, src/io/image_format_fits.c:72-140): the value text (a string without its
+ * quotes) into value[len]; 0, or SG_ERR_GENERIC when the key is absent / the sequence is SER */
+int sg_seq_read_key(const sg_seq *seq, int index, const char *key, char *value, int len);
+
 /* seq_opened_read_region (src/io/sequence.c:690-700): top-down band `area` of channel
  * `layer` of frame `index` (ser_read_opened_partial src/io/ser.c:772-971,
  * read_opened_fits_partial src/io/image_format_fits.c:581-635); 0 ok, -1 failure */

@@ -15,6 +15,10 @@
 #include <vector>
 #include <string>
 #include <algorithm>
+#include <array>
+#include <atomic>
+#include <mutex>
+#include <thread>
 #include "sg_common.hpp"
 #include "../../include/sirilgpu.h"
 
@@ -44,6 +48,14 @@ __global__ void k_synth_fill(uint16_t *frames, int first_frame, int nframes, int
 
 #include "sg_ctx.hpp"
 
+__global__ void k_flip_rows(const uint16_t *src, uint16_t *dst, int W, int rows);
+/* host-pull readers per device and the bytes of one region read (two pinned + two device
+ * staging buffers of this size per reader) */
+#define SG_PULL_READERS 8
+#define SG_PULL_CHUNK_BYTES ((size_t)4 << 20)
+/* rejection counter shards at the start of the counter block (SgDevice::ctr) */
+static const size_t SG_CTR_REJB = sizeof(unsigned long long) * SG_REJ_SHARDS * 6;
+
 extern "C" int sg_init(sg_ctx **out, int ndev, const int *devs) {
 	if (!out)
 		return SG_ERR_GENERIC;
@@ -54,7 +66,11 @@ extern "C" int sg_init(sg_ctx **out, int ndev, const int *devs) {
 	sg_ctx *ctx = new sg_ctx();
 	memset(&ctx->stats, 0, sizeof ctx->stats);
 	ctx->knobs.read();
-	if (ndev <= 0)
+	if (ndev < 0) {	/* every visible device */
+		ndev = count;
+		devs = nullptr;
+	}
+	if (ndev == 0)
 		ndev = 1;
 	for (int i = 0; i < ndev; i++) {
 		SgDevice d;
@@ -73,6 +89,9 @@ extern "C" int sg_init(sg_ctx **out, int ndev, const int *devs) {
 			(void)hipEventCreateWithFlags(&d.io_ev[k], hipEventDisableTiming);
 		ctx->dev.push_back(d);
 	}
+	for (auto &a : ctx->dev)
+		for (auto &b : ctx->dev)
+			a.shared += (&a != &b && a.id == b.id) ? 1 : 0;
 	*out = ctx;
 	return SG_OK;
 }
@@ -105,6 +124,20 @@ extern "C" void sg_shutdown(sg_ctx *ctx) {
 		for (int k = 0; k < 4; k++)
 			if (d.ev[k])
 				(void)hipEventDestroy(d.ev[k]);
+		for (SgReader &rd : d.readers) {
+			if (rd.stream)
+				(void)hipStreamSynchronize(rd.stream);
+			for (int k = 0; k < 2; k++) {
+				if (rd.pin[k])
+					(void)hipHostFree(rd.pin[k]);
+				if (rd.dstage[k])
+					(void)hipFree(rd.dstage[k]);
+				if (rd.ev[k])
+					(void)hipEventDestroy(rd.ev[k]);
+			}
+			if (rd.stream)
+				(void)hipStreamDestroy(rd.stream);
+		}
 		(void)hipStreamDestroy(d.stream);
 	}
 	delete ctx;
@@ -117,6 +150,7 @@ extern "C" const char *sg_last_error(const sg_ctx *ctx) {
 extern "C" int sg_get_last_stats(const sg_ctx *ctx, sg_stack_stats *st) {
 	if (!ctx || !st)
 		return SG_ERR_GENERIC;
+	std::lock_guard<std::mutex> lk(((sg_ctx *)ctx)->mu);
 	*st = ctx->stats;
 	return SG_OK;
 }
@@ -246,7 +280,18 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 	hipStream_t s = stream ? (hipStream_t)stream : dv.stream;
 	const int nrows = row_end - row_begin;
 	const size_t npix_img = (size_t)C * H * W;
-	memset(&ctx->stats, 0, sizeof ctx->stats);
+	/* this call's statistics: the device's own record (one thread per device), published to the
+	 * context when the call returns, whatever the outcome */
+	sg_stack_stats &st = dv.stats;
+	memset(&st, 0, sizeof st);
+	struct Publish {
+		sg_ctx *c;
+		const sg_stack_stats &s;
+		~Publish() {
+			std::lock_guard<std::mutex> lk(c->mu);
+			c->stats = s;
+		}
+	} publish{ctx, st};
 
 	SgStackParams p;
 	memset(&p, 0, sizeof p);
@@ -460,7 +505,7 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 	};
 	/* counters: rejection shards, then {flag count, walk fault, redo count} and the sum maximum
 	 * 64 bytes further (kept across the bands of a streamed SUM); one memset, one read-back */
-	const size_t REJB = sizeof(unsigned long long) * SG_REJ_SHARDS * 6, CTRB = REJB + 128;
+	const size_t REJB = SG_CTR_REJB, CTRB = REJB + 128;
 	HIPCHK(ensure(dv.ctr, CTRB));
 	if (!dv.ctr_h)
 		HIPCHK(hipHostMalloc(&dv.ctr_h, CTRB));
@@ -485,8 +530,17 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 	if (sorted) {
 		const int nreg = pick_nreg(N);
 		unsigned int *late_redo = nullptr, *late_list = nullptr;	/* redo list routed on the device */
-		if (!nreg)
-			return set_err(ctx, SG_ERR_SIZE, "rejection/median stacking supports up to 1024 frames%s (%ld)", "", N);
+		/* histogram fast path (sg_stack_hist.hip): SIGMA / WINSORIZED / PERCENTILE rejection and
+		 * stack_median, any normalisation, 16 <= N <= 65535 (per-lane zero / 65535 counters are
+		 * 16-bit halves) */
+		const bool hist = d->kernel_path != SG_PATH_SORTED && N >= 16 && N <= 65535 && hist_addr_ok &&
+			(d->method == SG_STACK_MEDIAN || (d->method == SG_STACK_MEAN && (d->rejection == SG_SIGMA ||
+					d->rejection == SG_WINSORIZED || d->rejection == SG_PERCENTILE)));
+		/* beyond the sorted kernel's 1024 frames only the histogram path runs; its redo pixels
+		 * all go to the replay / literal kernels (they take any N) */
+		if (!nreg && !hist)
+			return set_err(ctx, SG_ERR_SIZE, "this rejection supports up to 1024 frames%s (%ld); SIGMA, "
+					"WINSORIZED, PERCENTILE and median stacks take up to 65535", "", N);
 		const size_t npix_launch = (size_t)C * nrows * W;
 		HIPCHK(ensure(dv.flag_list, sizeof(unsigned int) * npix_launch));
 		HIPCHK(ensure(dv.flag_map, npix_img));
@@ -527,12 +581,6 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		const int ntx = (W + SG_TILE_W - 1) / SG_TILE_W;
 		const size_t nblk = (size_t)ntx * nrows * C;
 		const size_t lds = (size_t)N * SG_STAGE_STRIDE * 2;
-		/* histogram fast path (sg_stack_hist.hip): SIGMA / WINSORIZED, any normalisation,
-		 * 16 <= N <= 65535 (per-lane zero / 65535 counters are 16-bit halves) */
-		const int path = d->kernel_path;
-		const bool hist = path != SG_PATH_SORTED && d->method == SG_STACK_MEAN &&
-			(d->rejection == SG_SIGMA || d->rejection == SG_WINSORIZED) &&
-			N >= 16 && N <= 65535 && hist_addr_ok;
 		if (hist) {
 			HIPCHK(ensure(dv.redo, sizeof(unsigned int) * (npix_launch + 16)));
 			unsigned int *redo_count = p.flag_count + 2;	/* cleared with the counters */
@@ -545,9 +593,10 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			/* tile = 128 NI pixels of a row, 4 NI waves: NI = 1 by default (sg_stack_hist.hip);
 			 * the A/B NI = 2 (SG_HIST_NI=2) exists without normalisation only (it spills there:
 			 * the per-sample double arithmetic of two pixel pairs) */
-			const int ni = (norm == 0 && ctx->knobs.hist_ni == 2) ? 2 : 1;
+			const int ni = (norm == 0 && ctx->knobs.hist_ni == 2 && (d->method == SG_STACK_MEAN &&
+						(p.rejection == SG_SIGMA || p.rejection == SG_WINSORIZED))) ? 2 : 1;
 			const size_t nblk_h = (size_t)((W + 128 * ni - 1) / (128 * ni)) * nrows * C;
-			if (p.dbg == 14) {	/* A/B: report the resident workgroups per CU */
+			if (SG_DBG(p) == 14) {	/* A/B: report the resident workgroups per CU */
 				int per_cu = -1;
 				(void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ni == 2 ? (const void *)k_stack_hist<2, 0, 2>
 						: (const void *)k_stack_hist<2, 0, 1>, sgh_block_threads(ni, 2), (size_t)ctx->knobs.hist_ldspad);
@@ -557,8 +606,11 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 						(size_t)prop.maxSharedMemoryPerMultiProcessor, (size_t)prop.sharedMemPerBlock, ctx->knobs.hist_ldspad);
 			}
 			const size_t lds_pad = (size_t)ctx->knobs.hist_ldspad;
-			const dim3 hg((unsigned)nblk_h), hb((unsigned)sgh_block_threads(ni, p.rejection == SG_WINSORIZED ? 4 : 2));
-			switch ((p.rejection == SG_WINSORIZED ? 10 : 0) + norm + 100 * ni) {
+			/* REJ: 2 SIGMA, 4 WINSORIZED, 1 PERCENTILE, 8 stack_median */
+			const int rj = d->method == SG_STACK_MEDIAN ? 8 : p.rejection == SG_WINSORIZED ? 4 :
+				p.rejection == SG_PERCENTILE ? 1 : 2;
+			const dim3 hg((unsigned)nblk_h), hb((unsigned)sgh_block_threads(ni, rj));
+			switch ((rj == 4 ? 10 : rj == 1 ? 20 : rj == 8 ? 30 : 0) + norm + 100 * (rj == 1 || rj == 8 ? 1 : ni)) {
 			case 100: hipLaunchKernelGGL((k_stack_hist<2, 0, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 101: hipLaunchKernelGGL((k_stack_hist<2, 1, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 102: hipLaunchKernelGGL((k_stack_hist<2, 2, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
@@ -567,6 +619,14 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			case 111: hipLaunchKernelGGL((k_stack_hist<4, 1, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 112: hipLaunchKernelGGL((k_stack_hist<4, 2, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 113: hipLaunchKernelGGL((k_stack_hist<4, 3, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			case 120: hipLaunchKernelGGL((k_stack_hist<1, 0, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			case 121: hipLaunchKernelGGL((k_stack_hist<1, 1, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			case 122: hipLaunchKernelGGL((k_stack_hist<1, 2, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			case 123: hipLaunchKernelGGL((k_stack_hist<1, 3, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			case 130: hipLaunchKernelGGL((k_stack_hist<8, 0, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			case 131: hipLaunchKernelGGL((k_stack_hist<8, 1, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			case 132: hipLaunchKernelGGL((k_stack_hist<8, 2, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			case 133: hipLaunchKernelGGL((k_stack_hist<8, 3, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 200: hipLaunchKernelGGL((k_stack_hist<2, 0, 2>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 210: hipLaunchKernelGGL((k_stack_hist<4, 0, 2>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			default: return set_err(ctx, SG_ERR_GENERIC, "no histogram kernel for this case%s%.0ld", "", 0);
@@ -574,32 +634,33 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			HIPCHK(hipGetLastError());
 			HIPCHK(hipEventRecord(dv.ev[1], s));
 			HIPCHK(hipMemsetAsync(dv.flag_map.p, 0, npix_img, s));
-			ctx->stats.path = 1;
-			ctx->stats.main_kernel_blocks = (int)nblk;
-			ctx->stats.launches = 1;
+			st.path = 1;
+			st.main_kernel_blocks = (int)nblk;
+			st.launches = 1;
 			/* the redo pixels: up to SG_REDO_REPLAY_MAX go straight to the wave-per-pixel replay
 			 * (every sample of a pixel gathered by one wave at once), decided on the device so
 			 * the step needs no host round trip; a longer list (rare: e.g. the normalised zeros
 			 * of rows near the frame border) goes through the sorted kernel, 64 pixels per
 			 * workgroup, once the count is back (measured: 22 k pixels faster in the replay,
 			 * 113 k slower) */
-			const bool dev_route = N <= SG_REPLAY_MAXN && ctx->knobs.redo_replay;
+			/* N > 1024 (no sorted kernel): every redo pixel goes to the replay / literal kernels */
+			const bool dev_route = (N <= SG_REPLAY_MAXN && ctx->knobs.redo_replay) || !nreg;
 			if (dev_route) {
 				hipLaunchKernelGGL(k_redo_to_literal, dim3(64), dim3(256), 0, s, p, (const unsigned int *)redo_list,
-						(const unsigned int *)redo_count, (unsigned int)SG_REDO_REPLAY_MAX);
+						(const unsigned int *)redo_count, nreg ? (unsigned int)SG_REDO_REPLAY_MAX : 0xFFFFFFFFu);
 				HIPCHK(hipGetLastError());
-				ctx->stats.launches++;
+				st.launches++;
 				late_redo = redo_count;
 				late_list = redo_list;
 			} else {
 				unsigned int nredo = 0;
 				HIPCHK(hipMemcpyAsync(&nredo, redo_count, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
 				HIPCHK(hipStreamSynchronize(s));
-				ctx->stats.chain_pixels = nredo;
+				st.chain_pixels = nredo;
 				if (nredo) {
 					HIPCHK(launch_sorted(nreg, true, dim3((nredo + SG_TILE_W - 1) / SG_TILE_W), lds, s, p,
 							redo_list, redo_count));
-					ctx->stats.launches++;
+					st.launches++;
 				}
 			}
 		} else {
@@ -607,28 +668,34 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			HIPCHK(hipEventRecord(dv.ev[0], s));
 			HIPCHK(launch_sorted(nreg, false, dim3((unsigned)nblk), lds, s, p, nullptr, nullptr));
 			HIPCHK(hipEventRecord(dv.ev[1], s));
-			ctx->stats.main_kernel_blocks = (int)nblk;
-			ctx->stats.launches = 1;
+			st.main_kernel_blocks = (int)nblk;
+			st.launches = 1;
 		}
 		/* exact wave-per-pixel replay of queued SIGMA / WINSORIZED pixels (early breaks with
 		 * this pixel's own stale rejected[]), then the literal path for what remains: two
 		 * phases, grids read the count on the device */
-		HIPCHK(ensure(dv.scratch, (size_t)SG_LIT_THREADS * (((size_t)N * 5 + 15) & ~(size_t)15)));
+		/* literal kernel: one thread per queued pixel with N * 5 bytes of scratch each; 65536
+		 * threads up to 2048 frames, then as many as 1 GiB of scratch holds */
+		const size_t lit_bytes = ((size_t)N * 5 + 15) & ~(size_t)15;
+		const unsigned lit_threads = (unsigned)std::max<size_t>(4096,
+				std::min<size_t>(SG_LIT_THREADS, ((size_t)1 << 30) / lit_bytes) & ~(size_t)63);
+		HIPCHK(ensure(dv.scratch, (size_t)lit_threads * lit_bytes));
 		auto launch_tail = [&]() -> int {
-			if ((p.rejection == SG_SIGMA || p.rejection == SG_WINSORIZED) && N <= SG_REPLAY_MAXN) {
+			if (d->method == SG_STACK_MEAN && (p.rejection == SG_SIGMA || p.rejection == SG_WINSORIZED) &&
+					N <= SG_REPLAY_MAXN) {
 				if (N <= 512)	/* the per-wave LDS sized for 512 frames (k_stack_replay<SG_REPLAY_FASTN>) */
 					hipLaunchKernelGGL(k_stack_replay<512>, dim3(2048), dim3(64 * SG_REPLAY_WAVES), 0, s, p);
 				else
 					hipLaunchKernelGGL(k_stack_replay<SG_REPLAY_MAXN>, dim3(2048), dim3(64 * SG_REPLAY_WAVES), 0, s, p);
 				HIPCHK(hipGetLastError());
-				ctx->stats.launches++;
+				st.launches++;
 			}
 			for (int phase = 1; phase <= 2; phase++) {
-				hipLaunchKernelGGL(k_stack_literal, dim3(SG_LIT_THREADS / 64), dim3(64), 0, s, p, ct,
+				hipLaunchKernelGGL(k_stack_literal, dim3(lit_threads / 64), dim3(64), 0, s, p, ct,
 						0u, (uint8_t *)dv.scratch.p, phase);
 				HIPCHK(hipGetLastError());
 			}
-			ctx->stats.launches += 2;
+			st.launches += 2;
 			return SG_OK;
 		};
 		if (int rc = launch_tail())
@@ -640,12 +707,12 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			if (int rc = readback())
 				return rc;
 			const unsigned int nredo = ctr_flags[2];
-			ctx->stats.chain_pixels = nredo;
-			if (nredo > SG_REDO_REPLAY_MAX) {
+			st.chain_pixels = nredo;
+			if (nredo > SG_REDO_REPLAY_MAX && nreg) {
 				have_counts = false;
 				HIPCHK(launch_sorted(nreg, true, dim3((nredo + SG_TILE_W - 1) / SG_TILE_W), lds, s, p, late_list,
 						late_redo));
-				ctx->stats.launches++;
+				st.launches++;
 				if (int rc = launch_tail())
 					return rc;
 			}
@@ -668,8 +735,8 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			hipLaunchKernelGGL(k_stack_reduce, grid, dim3(256), 0, s, p);
 		HIPCHK(hipGetLastError());
 		HIPCHK(hipEventRecord(dv.ev[1], s));
-		ctx->stats.main_kernel_blocks = pairs ? (int)(grid2.x * grid2.y * grid2.z) : (int)(grid.x * grid.y * grid.z);
-		ctx->stats.launches = 1;
+		st.main_kernel_blocks = pairs ? (int)(grid2.x * grid2.y * grid2.z) : (int)(grid.x * grid.y * grid.z);
+		st.launches = 1;
 		if (d->method == SG_STACK_SUM && (sum_mode == SUM_WHOLE || sum_mode == SUM_LAST_BAND)) {
 			/* the 65535/max scaling (:328-342) needs the maximum over the whole image: a
 			 * streamed sequence finalises every row once its last band is summed */
@@ -682,7 +749,7 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			}
 			hipLaunchKernelGGL(k_sum_finalize, gf, dim3(256), 0, s, pf);
 			HIPCHK(hipGetLastError());
-			ctx->stats.launches++;
+			st.launches++;
 		}
 	}
 	if (!have_counts) {
@@ -695,14 +762,14 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 	if (cnt[1])
 		return set_err(ctx, SG_ERR_WALK, "a first-pass early break needs the stale rejected[] of a pixel "
 				"whose frame rows are not resident; make the full frames resident%s%.0ld", "", 0);
-	if (p.dbg == 12)
+	if (SG_DBG(p) == 12)
 		sg_dbg_why_dump(s);
 	float ms = 0.f, ms2 = 0.f;
 	HIPCHK(hipEventElapsedTime(&ms, dv.ev[0], dv.ev[1]));
 	HIPCHK(hipEventElapsedTime(&ms2, dv.ev[0], dv.ev[2]));
-	ctx->stats.kernel_ms = ms;
-	ctx->stats.total_ms = ms2;
-	ctx->stats.slow_pixels = cnt[0];
+	st.kernel_ms = ms;
+	st.total_ms = ms2;
+	st.slow_pixels = cnt[0];
 	if (rej) {
 		for (int c = 0; c < 3; c++)
 			rej[c][0] = rej[c][1] = 0;
@@ -727,148 +794,364 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 
 /* device bytes a stack call holds besides the frames: the output image (2 B per sample),
  * flag list and redo list (4 + 4 B), flag map (1 B), SUM's u32 sums (4 B), the literal
- * kernel's scratch and the small tables */
+ * kernel's scratch, the readers' staging and the small tables */
 static size_t fixed_device_bytes(int N, int W, int H, int C) {
 	const size_t npix = (size_t)C * H * W;
-	return npix * 15 + (size_t)SG_LIT_THREADS * (((size_t)N * 5 + 15) & ~(size_t)15) + ((size_t)4 << 20);
+	const size_t lit = (size_t)SG_LIT_THREADS * (((size_t)N * 5 + 15) & ~(size_t)15);
+	return npix * 15 + std::min(lit, ((size_t)1 << 30) + ((size_t)1 << 20)) + ((size_t)4 << 20) +
+		(size_t)SG_PULL_READERS * 2 * SG_PULL_CHUNK_BYTES;
 }
 
-/* HBM the host-pull path may fill with frames: SG_HOST_BUDGET_BYTES (tests: the frame budget
- * itself), else 85 % of the free device memory (plus what the context already holds for
- * frames) less the call's other buffers */
+/* HBM the host-pull path may fill with frames on one device: SG_HOST_BUDGET_BYTES (tests: the
+ * frame budget itself), else 85 % of the free device memory (plus what the context already holds
+ * for frames) less the call's other buffers, split between the context slots that share the card */
 static size_t host_budget(const sg_ctx *ctx, SgDevice &dv, int N, int W, int H, int C) {
 	if (ctx->knobs.host_budget > 0)
 		return (size_t)ctx->knobs.host_budget;
 	size_t fr = 0, tot = 0;
 	if (hipMemGetInfo(&fr, &tot) != hipSuccess)
 		return 0;
-	const size_t b = (size_t)((double)(fr + dv.frames.size + dv.out.size) * 0.85);
+	const size_t b = (size_t)((double)(fr + dv.frames.size + dv.out.size) * 0.85) / (size_t)std::max(1, dv.shared);
 	const size_t fixed = fixed_device_bytes(N, W, H, C);
 	return b > fixed ? b - fixed : 0;
 }
 
-/*
- * host-pull path: frames come through seq_opened_read_region-shaped callbacks.  Like the
- * reference's row blocks (stacking.c:1397-1476, sized from the memory budget :1903-1915),
- * a sequence larger than the HBM budget is stacked in row bands: for each band the rows
- * its shifts reach are pulled for every frame (the reference's area.y += shifty reads,
- * :1544-1577), uploaded through two pinned buffers, and stacked with those rows resident.
- */
-extern "C" int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *d, sg_read_region_fn pull, void *user,
-		sg_should_continue_fn cont, void *cont_user, uint16_t *out, uint64_t rej[3][2],
-		uint64_t *maxim) {
-	if (!ctx || !d || !pull || !out || ctx->dev.empty())
-		return SG_ERR_GENERIC;
-	SgDevice &dv = ctx->dev[0];
-	const int N = d->nb_frames, W = d->width, H = d->height, C = d->nb_layers;
-	if (N < 2)
-		return set_err(ctx, SG_ERR_GENERIC, "select at least two frames%s (%ld)", "", N);
-	if (W <= 0 || H <= 0 || C < 1 || C > 3)
-		return SG_ERR_SIZE;
-	HIPCHK(hipSetDevice(dv.id));
-	/* frame rows a band reads: [b - sy_max, e - 1 - sy_min] */
-	const bool use_shift = d->method != SG_STACK_MEDIAN && d->shiftx && d->shifty;
-	int sy_min = 0, sy_max = 0;
-	for (int i = 0; use_shift && i < N; i++) {
-		sy_min = i ? std::min(sy_min, d->shifty[i]) : d->shifty[i];
-		sy_max = i ? std::max(sy_max, d->shifty[i]) : d->shifty[i];
+/* state shared by the device threads and their readers of one sg_stack_u16 call */
+struct PullCall {
+	const sg_stack_desc *d;
+	sg_read_region_fn pull;
+	void *user;
+	sg_should_continue_fn cont;
+	void *cont_user;
+	int sy_min, sy_max;
+	bool multi;			/* more than one device: SUM scales after every device's band */
+	std::mutex cont_mu;		/* the caller's get_thread_run is asked from one thread at a time */
+	std::atomic<int> stop{0};	/* a reader failed or the caller cancelled: every thread winds down */
+	bool keep_going() {
+		if (stop.load())
+			return false;
+		if (!cont)
+			return true;
+		std::lock_guard<std::mutex> lk(cont_mu);
+		if (stop.load())
+			return false;
+		if (!cont(cont_user)) {
+			stop = 1;
+			return false;
+		}
+		return true;
 	}
-	const int64_t halo = std::min<int64_t>((int64_t)sy_max - sy_min, H);
+};
+
+static int ensure_readers(sg_ctx *ctx, SgDevice &dv, int nreaders, size_t elems) {
+	if ((int)dv.readers.size() < nreaders)
+		dv.readers.resize((size_t)nreaders);
+	for (int r = 0; r < nreaders; r++) {
+		SgReader &rd = dv.readers[(size_t)r];
+		if (!rd.stream) {
+			HIPCHK(hipStreamCreateWithFlags(&rd.stream, hipStreamNonBlocking));
+			for (int k = 0; k < 2; k++)
+				HIPCHK(hipEventCreateWithFlags(&rd.ev[k], hipEventDisableTiming));
+		}
+		if (rd.cap < elems) {
+			for (int k = 0; k < 2; k++) {
+				if (rd.used[k])
+					HIPCHK(hipEventSynchronize(rd.ev[k]));
+				rd.used[k] = false;
+				if (rd.pin[k])
+					(void)hipHostFree(rd.pin[k]);
+				if (rd.dstage[k])
+					(void)hipFree(rd.dstage[k]);
+				rd.pin[k] = rd.dstage[k] = nullptr;
+			}
+			rd.cap = 0;
+			for (int k = 0; k < 2; k++) {
+				HIPCHK(hipHostMalloc((void **)&rd.pin[k], elems * sizeof(uint16_t)));
+				HIPCHK(hipMalloc((void **)&rd.dstage[k], elems * sizeof(uint16_t)));
+			}
+			rd.cap = elems;
+		}
+	}
+	return SG_OK;
+}
+
+/*
+ * One band of frame rows onto one device: memory rows [lo, lo + nres) of every frame and
+ * channel into `frames` (plane (i C + c) at (i C + c) nres W).  Like the reference's OpenMP
+ * team reading its blocks (stacking.c:1513-1591, seq_opened_read_region under per-file locks),
+ * `nreaders` host threads pull frames i = r, r + R, ... in top-down row chunks of at most
+ * SG_PULL_CHUNK_BYTES into their two pinned buffers (the reader refills one while the other is
+ * in flight), copy each chunk on their own stream and flip it into place on the device.  The
+ * caller's cancellation is polled once per frame, as get_thread_run() is per frame read
+ * (:1539).  Returns once every chunk has landed.
+ */
+static int pull_band(sg_ctx *ctx, SgDevice &dv, PullCall &pc, int nreaders, uint16_t *frames, int lo, int nres) {
+	const sg_stack_desc *d = pc.d;
+	const int N = d->nb_frames, W = d->width, H = d->height, C = d->nb_layers;
+	const int chunk = (int)std::max<size_t>(1, SG_PULL_CHUNK_BYTES / ((size_t)W * sizeof(uint16_t)));
+	const size_t bplane = (size_t)nres * W;
+	std::atomic<int> rc{SG_OK};
+	auto fail = [&](int code) {
+		int expect = SG_OK;
+		rc.compare_exchange_strong(expect, code);
+		pc.stop = 1;
+	};
+	auto work = [&](int r) {
+		SgReader &rd = dv.readers[(size_t)r];
+		if (hipSetDevice(dv.id) != hipSuccess)
+			return fail(set_err(ctx, SG_ERR_DEVICE, "hipSetDevice failed in a reader%s%ld", "", dv.id));
+		int k = 0;
+		for (int i = r; i < N; i += nreaders) {
+			if (!pc.keep_going())
+				return fail(SG_ERR_GENERIC);	/* cancelled, or another thread failed */
+			for (int c = 0; c < C; c++) {
+				uint16_t *plane = frames + ((size_t)i * C + c) * bplane;
+				for (int m0 = 0; m0 < nres; m0 += chunk) {
+					const int h = std::min(chunk, nres - m0);
+					if (rd.used[k] && hipEventSynchronize(rd.ev[k]) != hipSuccess)
+						return fail(set_err(ctx, SG_ERR_DEVICE, "staging event failed%s%ld", "", i));
+					/* memory rows lo + m0 .. lo + m0 + h - 1 as the top-down area the
+					 * region reader takes (y = H - 1 - the highest memory row) */
+					const sg_rect area = {0, H - lo - m0 - h, W, h};
+					if (pc.pull(pc.user, c, i, rd.pin[k], &area) < 0)
+						return fail(set_err(ctx, SG_ERR_READ, "could not read frame%s %ld", "", i));
+					if (hipMemcpyAsync(rd.dstage[k], rd.pin[k], (size_t)h * W * sizeof(uint16_t), hipMemcpyHostToDevice,
+							rd.stream) != hipSuccess)
+						return fail(set_err(ctx, SG_ERR_DEVICE, "upload failed for frame%s %ld", "", i));
+					hipLaunchKernelGGL(k_flip_rows, dim3((unsigned)std::min(64, (W + 255) / 256), (unsigned)h), dim3(256), 0,
+							rd.stream, (const uint16_t *)rd.dstage[k], plane + (size_t)m0 * W, W, h);
+					if (hipGetLastError() != hipSuccess || hipEventRecord(rd.ev[k], rd.stream) != hipSuccess)
+						return fail(set_err(ctx, SG_ERR_DEVICE, "flip launch failed for frame%s %ld", "", i));
+					rd.used[k] = true;
+					k ^= 1;
+				}
+			}
+		}
+	};
+	std::vector<std::thread> th;
+	for (int r = 1; r < nreaders; r++)
+		th.emplace_back(work, r);
+	work(0);
+	for (std::thread &t : th)
+		t.join();
+	for (int r = 0; r < nreaders; r++)
+		if (hipStreamSynchronize(dv.readers[(size_t)r].stream) != hipSuccess && rc.load() == SG_OK)
+			fail(set_err(ctx, SG_ERR_DEVICE, "upload stream failed%s%ld", "", r));
+	return rc.load();
+}
+
+/*
+ * The rows [B, E) of the output on device g: banded under the device's HBM budget like the
+ * reference's row blocks (stacking.c:1397-1476, sized from the memory budget :1903-1915); each
+ * band's frame rows (the rows its shifts reach, :1544-1577) are pulled by the device's readers
+ * and stacked with only those rows resident.  The output rows stay in the device's dv.out
+ * (SUM of several devices: raw sums, scaled once the maximum over every device is known).
+ */
+static int pull_device(sg_ctx *ctx, int g, PullCall &pc, int B, int E, int nreaders, uint64_t rej[3][2],
+		uint64_t *maxim) {
+	SgDevice &dv = ctx->dev[(size_t)g];
+	const sg_stack_desc *d = pc.d;
+	const int N = d->nb_frames, W = d->width, H = d->height, C = d->nb_layers;
+	HIPCHK(hipSetDevice(dv.id));
+	const int64_t halo = std::min<int64_t>((int64_t)pc.sy_max - pc.sy_min, H);
 	const size_t row_bytes = (size_t)N * C * W * sizeof(uint16_t);	/* one row of every frame */
-	int band = H;
+	int band = E - B;
 	const size_t budget = host_budget(ctx, dv, N, W, H, C);
-	if ((size_t)H * row_bytes > budget) {
+	if ((size_t)band * row_bytes > budget) {
 		const int64_t fit = (int64_t)(budget / row_bytes) - halo;
 		if (fit < 1)
 			return set_err(ctx, SG_ERR_SIZE, "the sequence does not fit the device even one row at a "
 					"time%s%.0ld", "", 0);
-		band = (int)std::min<int64_t>(fit, H);
+		band = (int)std::min<int64_t>(fit, band);
 	}
 	const int64_t rows_cap = std::min<int64_t>(band + halo, H);
-	const size_t plane = (size_t)rows_cap * W;
-	HIPCHK(ensure(dv.frames, plane * C * N * sizeof(uint16_t)));
+	HIPCHK(ensure(dv.frames, (size_t)rows_cap * W * C * N * sizeof(uint16_t)));
 	HIPCHK(ensure(dv.out, (size_t)W * H * C * sizeof(uint16_t)));
-	if (dv.pinned_size < plane) {
-		for (int k = 0; k < 2; k++) {
-			if (dv.pinned[k])
-				(void)hipHostFree(dv.pinned[k]);
-			dv.pinned[k] = nullptr;
-			dv.pinned_size = 0;
-			HIPCHK(hipHostMalloc((void **)&dv.pinned[k], plane * sizeof(uint16_t) * 2));
-		}
-		dv.pinned_size = plane;
-	}
-	if (rej)
-		for (int c = 0; c < 3; c++)
-			rej[c][0] = rej[c][1] = 0;
-	const bool banded = band < H;
-	int k = 0;
-	bool used[2] = {false, false};
+	const size_t chunk_elems = std::min<size_t>((size_t)rows_cap * W,
+			std::max<size_t>(1, SG_PULL_CHUNK_BYTES / ((size_t)W * sizeof(uint16_t))) * W);
+	if (int rc = ensure_readers(ctx, dv, nreaders, chunk_elems))
+		return rc;
+	for (int c = 0; c < 3; c++)
+		rej[c][0] = rej[c][1] = 0;
+	const bool banded = band < E - B || pc.multi;
 	/* extra: rows above the band kept resident besides the halo.  A first-pass early break
 	 * inherits the stale rejected[] of the previous pixel of the reference's OpenMP thread
 	 * (stacking.c:1684), i.e. of the pixel one memory row up (rows run top-down inside a
 	 * block); when that pixel lies above the band the core reports it (SG_ERR_WALK) and the
 	 * band is retried narrower with more rows above it resident (same total rows) */
 	int extra = 0;
-	for (int b = 0; b < H;) {
-		const int e = std::min(H, b + std::max(1, band - extra));
-		int lo = (int)std::max<int64_t>(0, (int64_t)b - sy_max);
-		int hi = (int)std::min<int64_t>(H - 1, (int64_t)e - 1 - sy_min + extra);
+	for (int b = B; b < E;) {
+		const int e = std::min(E, b + std::max(1, band - extra));
+		int lo = (int)std::max<int64_t>(0, (int64_t)b - pc.sy_max);
+		int hi = (int)std::min<int64_t>(H - 1, (int64_t)e - 1 - pc.sy_min + extra);
 		if (lo > hi)	/* every row of the band is shifted out of the frames: nothing is read */
 			lo = hi = std::min(b, H - 1);
 		const int nres = hi - lo + 1;
 		const size_t bplane = (size_t)nres * W;
-		/* top-down area of memory rows lo..hi (the reference's region convention) */
-		const sg_rect area = {0, H - 1 - hi, W, nres};
-		/* two pinned buffers: the reader fills and flips one while the other's upload is
-		 * in flight; a buffer is reused once the event recorded after its upload fired */
-		for (int i = 0; i < N; i++) {
-			if (cont && !cont(cont_user)) {
-				(void)hipStreamSynchronize(dv.stream);
-				return SG_ERR_GENERIC;	/* cancelled, like get_thread_run() */
-			}
-			for (int c = 0; c < C; c++) {
-				uint16_t *flip = dv.pinned[k];
-				if (used[k])
-					HIPCHK(hipEventSynchronize(dv.io_ev[k]));	/* buffer k free again */
-				uint16_t *tb = flip + plane;	/* top-down band as returned by the reader */
-				if (pull(user, c, i, tb, &area) < 0) {
-					(void)hipStreamSynchronize(dv.stream);
-					return set_err(ctx, SG_ERR_READ, "could not read frame%s %ld", "", i);
-				}
-				for (int t = 0; t < nres; t++)
-					memcpy(flip + (size_t)(nres - 1 - t) * W, tb + (size_t)t * W, W * sizeof(uint16_t));
-				HIPCHK(hipMemcpyAsync((uint16_t *)dv.frames.p + ((size_t)i * C + c) * bplane, flip,
-						bplane * sizeof(uint16_t), hipMemcpyHostToDevice, dv.stream));
-				HIPCHK(hipEventRecord(dv.io_ev[k], dv.stream));
-				used[k] = true;
-				k ^= 1;
-			}
-		}
+		if (int rc = pull_band(ctx, dv, pc, nreaders, (uint16_t *)dv.frames.p, lo, nres))
+			return rc;
 		sg_stack_desc bd = *d;
 		bd.resident_rows[0] = lo;
 		bd.resident_rows[1] = hi + 1;
 		const int sum_mode = d->method != SG_STACK_SUM || !banded ? SUM_WHOLE
-			: b == 0 ? SUM_FIRST_BAND : e == H ? SUM_LAST_BAND : SUM_MID_BAND;
+			: b == B ? SUM_FIRST_BAND : (!pc.multi && e == H) ? SUM_LAST_BAND : SUM_MID_BAND;
 		uint64_t brej[3][2];
 		/* base pointer biased so that memory row r of a frame plane sits at r*W */
 		const uint16_t *base = (const uint16_t *)dv.frames.p - (ptrdiff_t)lo * W;
-		int rc = stack_device_core(ctx, 0, &bd, base, (int64_t)bplane * C, (int64_t)bplane,
-				(uint16_t *)dv.out.p, b, e, brej, maxim, nullptr, sum_mode);
-		if (rc == SG_ERR_WALK && banded && hi < H - 1 && band - extra > 1) {
+		int rc = stack_device_core(ctx, g, &bd, base, (int64_t)bplane * C, (int64_t)bplane, (uint16_t *)dv.out.p, b,
+				e, brej, maxim, dv.stream, sum_mode);
+		if (rc == SG_ERR_WALK && hi < H - 1 && band - extra > 1) {
 			extra = std::min(band - 1, extra ? 2 * extra : 4);
 			continue;	/* same band start, narrower band, more rows above resident */
 		}
 		if (rc)
 			return rc == SG_ERR_WALK ? SG_ERR_GENERIC : rc;
-		if (rej)
-			for (int c = 0; c < 3; c++) {
-				rej[c][0] += brej[c][0];
-				rej[c][1] += brej[c][1];
-			}
+		for (int c = 0; c < 3; c++) {
+			rej[c][0] += brej[c][0];
+			rej[c][1] += brej[c][1];
+		}
 		b = e;
 	}
-	HIPCHK(hipMemcpy(out, dv.out.p, (size_t)W * H * C * sizeof(uint16_t), hipMemcpyDeviceToHost));
+	return SG_OK;
+}
+
+/* SUM over several devices: the 65535/max scaling of stack_summing (:328-342) with the maximum
+ * over the whole image, applied to device g's rows [B, E) of raw sums */
+static int sum_finalize_rows(sg_ctx *ctx, int g, int W, int H, int C, int B, int E, unsigned int gmax) {
+	SgDevice &dv = ctx->dev[(size_t)g];
+	HIPCHK(hipSetDevice(dv.id));
+	SgStackParams p;
+	memset(&p, 0, sizeof p);
+	p.W = W;
+	p.H = H;
+	p.C = C;
+	p.out = (uint16_t *)dv.out.p;
+	p.sum_buf = (uint32_t *)dv.sum_buf.p;
+	p.row_begin = B;
+	p.row_end = E;
+	p.maxim = (unsigned int *)((char *)dv.ctr.p + SG_CTR_REJB + 64);
+	HIPCHK(hipMemcpyAsync(p.maxim, &gmax, sizeof gmax, hipMemcpyHostToDevice, dv.stream));
+	hipLaunchKernelGGL(k_sum_finalize, dim3((unsigned)((W + 255) / 256), (unsigned)(E - B), (unsigned)C), dim3(256), 0,
+			dv.stream, p);
+	HIPCHK(hipGetLastError());
+	HIPCHK(hipStreamSynchronize(dv.stream));
+	return SG_OK;
+}
+
+/*
+ * host-pull path: frames come through seq_opened_read_region-shaped callbacks.  Every device of
+ * the context takes a contiguous share of the output rows (the reference's row blocks are the
+ * natural shard) and is driven by its own host thread, whose readers pull and upload
+ * that share's frame rows directly (no device relays another's data); each device's band is
+ * copied back into `out`, the rejection counters are summed.
+ */
+extern "C" int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *d, sg_read_region_fn pull, void *user,
+		sg_should_continue_fn cont, void *cont_user, uint16_t *out, uint64_t rej[3][2],
+		uint64_t *maxim) {
+	if (!ctx || !d || !pull || !out || ctx->dev.empty())
+		return SG_ERR_GENERIC;
+	const int N = d->nb_frames, W = d->width, H = d->height, C = d->nb_layers;
+	if (N < 2)
+		return set_err(ctx, SG_ERR_GENERIC, "select at least two frames%s (%ld)", "", N);
+	if (W <= 0 || H <= 0 || C < 1 || C > 3)
+		return SG_ERR_SIZE;
+	PullCall pc;
+	pc.d = d;
+	pc.pull = pull;
+	pc.user = user;
+	pc.cont = cont;
+	pc.cont_user = cont_user;
+	/* frame rows a band reads: [b - sy_max, e - 1 - sy_min] */
+	const bool use_shift = d->method != SG_STACK_MEDIAN && d->shiftx && d->shifty;
+	pc.sy_min = pc.sy_max = 0;
+	for (int i = 0; use_shift && i < N; i++) {
+		pc.sy_min = i ? std::min(pc.sy_min, d->shifty[i]) : d->shifty[i];
+		pc.sy_max = i ? std::max(pc.sy_max, d->shifty[i]) : d->shifty[i];
+	}
+	const int G = (int)std::min<size_t>(ctx->dev.size(), (size_t)H);
+	pc.multi = G > 1;
+	/* readers per device: the reference's team size (com.max_thread) shared between the
+	 * devices, at least one, at most SG_PULL_READERS */
+	const int team = d->max_thread > 0 ? d->max_thread : default_threads();
+	const int nreaders = std::max(1, std::min(SG_PULL_READERS, team / G));
+	std::vector<int> rb((size_t)G + 1);
+	for (int g = 0; g <= G; g++)
+		rb[(size_t)g] = (int)((int64_t)g * H / G);
+	std::vector<int> rcs((size_t)G, SG_OK);
+	std::vector<std::array<uint64_t, 6>> rj((size_t)G);
+	std::vector<uint64_t> mx((size_t)G, 0);
+	auto run = [&](int g) {
+		uint64_t r6[3][2];
+		rcs[(size_t)g] = pull_device(ctx, g, pc, rb[(size_t)g], rb[(size_t)g + 1], nreaders, r6, &mx[(size_t)g]);
+		if (rcs[(size_t)g])
+			pc.stop = 1;
+		memcpy(rj[(size_t)g].data(), r6, sizeof r6);
+	};
+	{
+		std::vector<std::thread> th;
+		for (int g = 1; g < G; g++)
+			th.emplace_back(run, g);
+		run(0);
+		for (std::thread &t : th)
+			t.join();
+	}
+	/* a device's own failure wins over the stop (SG_ERR_GENERIC) it caused in the others;
+	 * a cancellation alone is SG_ERR_GENERIC, as get_thread_run() going false is (-1) */
+	int rc = SG_OK;
+	for (int g = 0; g < G && rc == SG_OK; g++)
+		if (rcs[(size_t)g] != SG_ERR_GENERIC)
+			rc = rcs[(size_t)g];
+	for (int g = 0; g < G && rc == SG_OK; g++)
+		rc = rcs[(size_t)g];
+	if (rc) {
+		for (int g = 0; g < G; g++) {
+			(void)hipSetDevice(ctx->dev[(size_t)g].id);
+			(void)hipStreamSynchronize(ctx->dev[(size_t)g].stream);
+		}
+		return rc;
+	}
+	uint64_t gmax = 0;
+	for (int g = 0; g < G; g++)
+		gmax = std::max(gmax, mx[(size_t)g]);
+	for (int g = 0; g < G; g++) {
+		SgDevice &dv = ctx->dev[(size_t)g];
+		const int B = rb[(size_t)g], E = rb[(size_t)g + 1];
+		if (d->method == SG_STACK_SUM && pc.multi)
+			if (int r = sum_finalize_rows(ctx, g, W, H, C, B, E, (unsigned int)gmax))
+				return r;
+		HIPCHK(hipSetDevice(dv.id));
+		for (int c = 0; c < C; c++) {
+			const size_t o = ((size_t)c * H + B) * W;
+			HIPCHK(hipMemcpy(out + o, (const uint16_t *)dv.out.p + o, (size_t)(E - B) * W * sizeof(uint16_t),
+					hipMemcpyDeviceToHost));
+		}
+	}
+	if (rej)
+		for (int c = 0; c < 3; c++) {
+			rej[c][0] = rej[c][1] = 0;
+			for (int g = 0; g < G; g++) {
+				rej[c][0] += rj[(size_t)g][(size_t)c * 2];
+				rej[c][1] += rj[(size_t)g][(size_t)c * 2 + 1];
+			}
+		}
+	if (maxim)
+		*maxim = gmax;
+	if (pc.multi) {	/* the call's statistics over every device */
+		sg_stack_stats agg;
+		memset(&agg, 0, sizeof agg);
+		for (int g = 0; g < G; g++) {
+			const sg_stack_stats &s = ctx->dev[(size_t)g].stats;
+			agg.kernel_ms = std::max(agg.kernel_ms, s.kernel_ms);
+			agg.total_ms = std::max(agg.total_ms, s.total_ms);
+			agg.slow_pixels += s.slow_pixels;
+			agg.chain_pixels += s.chain_pixels;
+			agg.launches += s.launches;
+			agg.main_kernel_blocks += s.main_kernel_blocks;
+			agg.path = s.path;
+		}
+		std::lock_guard<std::mutex> lk(ctx->mu);
+		ctx->stats = agg;
+	}
 	return SG_OK;
 }
 

@@ -9,6 +9,13 @@
 #define SG_STAGE_STRIDE 66	/* u16 per staged frame row: 64 px + 2 pad -> 33 dwords, bank-conflict free */
 #define SG_SORT_THREADS 256
 #define SG_REJ_SHARDS 1024
+/* A/B probe modes of the stacking kernels (SG_HIST_DBG: phase timings, loads only, timelines,
+ * occupancy reports): compiled in only by a probe build (make EXTRA=-DSG_DBG_MODES=1 BUILD=...);
+ * the product kernels carry no branch on them */
+#ifndef SG_DBG_MODES
+#define SG_DBG_MODES 0
+#endif
+#define SG_DBG(p) (SG_DBG_MODES ? (p).dbg : 0)
 
 enum { SG_CLS_OK = 0, SG_CLS_LITERAL = 1, SG_CLS_CHAIN = 2, SG_CLS_DONE = 3 };
 /* k_stack_replay: waves per block (one pixel per wave, ~18 KB of LDS each), max frames */

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <mutex>
 #include <string>
 #include <vector>
 #include "../../include/sirilgpu.h"
@@ -17,8 +18,23 @@ struct SgBuf {
 	size_t size = 0;
 };
 
+/* one host reader of the host-pull path (sg_stack_u16): it pulls top-down row chunks through the
+ * region callback into its pinned buffers, copies them on its own stream to a device staging
+ * buffer and flips them into the frame planes; ev[k] marks buffer k (host and device) free */
+struct SgReader {
+	hipStream_t stream = nullptr;
+	uint16_t *pin[2] = {nullptr, nullptr};
+	uint16_t *dstage[2] = {nullptr, nullptr};
+	hipEvent_t ev[2] = {nullptr, nullptr};
+	bool used[2] = {false, false};
+	size_t cap = 0;		/* elements per buffer */
+};
+
 struct SgDevice {
 	int id = 0;
+	int shared = 1;		/* context slots on this physical device (sg_init(devs = {0, 0}) shares one card) */
+	sg_stack_stats stats;	/* last stack call on this device (published to sg_ctx::stats) */
+	std::vector<SgReader> readers;
 	hipStream_t stream = nullptr;
 	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 	SgBuf flag_list, flag_map, sum_buf, scratch, frames, out, stats_buf;
@@ -74,7 +90,7 @@ struct SgKnobs {
 	int qgrad_threads = 128;	/* SG_QGRAD_THREADS: 128 measured best (scripts/gpu_qgrad.sh) */
 	int reg_batch = 0;		/* SG_REG_BATCH: pairs per launch (0 = up to 2 GB of pair planes) */
 	int reg_cw = 0;			/* SG_REG_CW: columns per column-pass workgroup (0 = 8192 / S) */
-	int reg_path = 2;		/* SG_REG_PATH: registration pass order 0 / 1 / 2, 3 = the generic passes */
+	int reg_path = 2;		/* SG_REG_PATH: 2 = half-spectrum passes (power-of-two sides), 3 = the generic passes */
 	int reg_xcd = 1;		/* SG_REG_XCD: 0 = column strips in dispatch order */
 	int reg_pb = 1;			/* SG_REG_PB: pairs per strip block of the fused column pass (1 = pair-major) */
 	int reg_fp = 32;		/* SG_REG_FP: 32 = fp32 half-spectrum passes, near ties re-run in fp64; 64 = fp64 only */
@@ -97,7 +113,7 @@ struct SgKnobs {
 		qgrad_threads = (qg == 64 || qg == 128 || qg == 256) ? qg : 128;
 		reg_batch = sg_env_int("SG_REG_BATCH", 1, 1024, 0);
 		reg_cw = sg_env_int("SG_REG_CW", 1, 64, 0);
-		reg_path = sg_env_int("SG_REG_PATH", 0, 3, 2);
+		reg_path = sg_env_int("SG_REG_PATH", 2, 3, 2);
 		reg_xcd = sg_env_int("SG_REG_XCD", 0, 1, 1);
 		reg_pb = sg_env_int("SG_REG_PB", 1, 64, 1);
 		reg_fp = sg_env_int("SG_REG_FP", 32, 64, 32) == 64 ? 64 : 32;
@@ -109,6 +125,7 @@ struct SgKnobs {
 
 struct sg_ctx {
 	std::vector<SgDevice> dev;
+	std::mutex mu;		/* err / stats: the host-pull path drives every device from its own thread */
 	std::string err;
 	sg_stack_stats stats;
 	SgKnobs knobs;
@@ -121,8 +138,10 @@ struct sg_ctx {
 static inline int set_err(sg_ctx *ctx, int code, const char *fmt, const char *a = "", long b = 0) {
 	char buf[512];
 	snprintf(buf, sizeof buf, fmt, a, b);
-	if (ctx)
+	if (ctx) {
+		std::lock_guard<std::mutex> lk(ctx->mu);
 		ctx->err = buf;
+	}
 	return code;
 }
 

@@ -48,6 +48,7 @@ struct sg_seq {
 	int debayer;		/* -1, or the SG_BAYER_* pattern of a demosaiced CFA SER */
 	std::vector<int> fd;	/* SER: one; FITS: one per frame */
 	std::vector<int64_t> data_off;	/* byte offset of the pixel data (per file) */
+	std::vector<std::string> cards;	/* FITS: the value cards of each file's primary header (80 B each) */
 	int64_t frame_bytes;	/* raw bytes of one frame */
 };
 
@@ -206,7 +207,7 @@ extern "C" int sg_seq_open_ser(const char *path, sg_seq **out) {
 
 /* FITS primary header: 80-byte cards in 2880-byte blocks */
 static int fits_header(int fd, int *bitpix, int *naxis, long naxes[3], double *bzero, double *bscale,
-		int64_t *data_off) {
+		int64_t *data_off, std::string *cards) {
 	char card[81];
 	card[80] = 0;
 	*bitpix = 0;
@@ -223,6 +224,7 @@ static int fits_header(int fd, int *bitpix, int *naxis, long naxes[3], double *b
 		}
 		if (card[8] != '=')
 			continue;
+		cards->append(card, 80);
 		char key[9];
 		memcpy(key, card, 8);
 		key[8] = 0;
@@ -268,7 +270,8 @@ static int sg_seq_open_fits_impl(const char *const *paths, int nframes, sg_seq *
 		long naxes[3];
 		double bzero, bscale;
 		int64_t doff;
-		if (fits_header(fd, &bitpix, &naxis, naxes, &bzero, &bscale, &doff)) {
+		s->cards.emplace_back();
+		if (fits_header(fd, &bitpix, &naxis, naxes, &bzero, &bscale, &doff, &s->cards.back())) {
 			sg_seq_close(s);
 			return SG_ERR_READ;
 		}
@@ -322,6 +325,54 @@ extern "C" void sg_seq_close(sg_seq *s) {
 		if (fd >= 0)
 			close(fd);
 	delete s;
+}
+
+/* the value of keyword `key` in the primary header of FITS frame `index`, as fits_read_key
+ * finds it (cfitsio ffgkey + ffc2s): a quoted string without its quotes ('' -> ', trailing
+ * blanks dropped), any other value as its token before the comment */
+extern "C" int sg_seq_read_key(const sg_seq *s, int index, const char *key, char *value, int len) {
+	if (!s || !key || !value || len < 1 || s->kind != SG_SRC_FITS || index < 0 || index >= s->frames ||
+			(size_t)index >= s->cards.size())
+		return SG_ERR_GENERIC;
+	const std::string &c = s->cards[(size_t)index];
+	const size_t kl = strlen(key);
+	if (kl == 0 || kl > 8)
+		return SG_ERR_GENERIC;
+	for (size_t o = 0; o + 80 <= c.size(); o += 80) {
+		const char *card = c.data() + o;
+		size_t n = 8;
+		while (n > 0 && card[n - 1] == ' ')
+			n--;
+		if (n != kl || strncmp(card, key, kl))
+			continue;
+		std::string v;
+		int i = 10;
+		while (i < 80 && card[i] == ' ')
+			i++;
+		if (i < 80 && card[i] == '\'') {
+			for (i++; i < 80; i++) {
+				if (card[i] == '\'') {
+					if (i + 1 < 80 && card[i + 1] == '\'') {
+						v.push_back('\'');
+						i++;
+						continue;
+					}
+					break;
+				}
+				v.push_back(card[i]);
+			}
+			while (!v.empty() && v.back() == ' ')
+				v.pop_back();
+		} else {
+			while (i < 80 && card[i] != '/' && card[i] != ' ')
+				v.push_back(card[i++]);
+			if (v.empty())
+				return SG_ERR_GENERIC;	/* VALUE_UNDEFINED */
+		}
+		snprintf(value, (size_t)len, "%s", v.c_str());
+		return SG_OK;
+	}
+	return SG_ERR_GENERIC;	/* KEY_NO_EXIST */
 }
 
 extern "C" int sg_seq_get_info(const sg_seq *s, sg_seq_info *info) {
@@ -659,6 +710,19 @@ __global__ void __launch_bounds__(256) k_debayer_frames(SgDecode d, int pattern)
 		out[(int64_t)k * plane + o] = (uint16_t)rgb[k];
 	if (bad)
 		atomicOr(d.bad, 1u);
+}
+
+/* host-pull path (sg_stack_u16): a top-down chunk of `rows` rows as the region callback
+ * returned it (seq_opened_read_region, src/io/sequence.c:690-700) -> memory rows (bottom-up,
+ * the stacking layout) of a frame plane: src row t lands at dst row rows - 1 - t.  The flip
+ * runs on the device (HBM-trivial) instead of as a second host pass over every byte. */
+__global__ void __launch_bounds__(256) k_flip_rows(const uint16_t *__restrict__ src, uint16_t *__restrict__ dst, int W,
+		int rows) {
+	const int t = blockIdx.y;
+	const uint16_t *s = src + (size_t)t * W;
+	uint16_t *o = dst + (size_t)(rows - 1 - t) * W;
+	for (int x = blockIdx.x * 256 + threadIdx.x; x < W; x += gridDim.x * 256)
+		o[x] = s[x];
 }
 
 extern "C" int sg_seq_load_device(sg_ctx *ctx, int dev_index, const sg_seq *s, int first, int count,

@@ -32,34 +32,10 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
+#include <thread>
 #include <type_traits>
 #include <vector>
-
-/* row pass of the forward transform of a + i b (b = -1: zero imaginary part) */
-__global__ void __launch_bounds__(512)
-k_reg_rows_fwd(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const int *__restrict__ fb,
-		int S, int logS, const sg_c64 *__restrict__ tw, sg_c64 *__restrict__ work,
-		unsigned long long *__restrict__ energy) {
-	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-	sg_c64 *buf = (sg_c64 *)smem;
-	const int row = blockIdx.x, pair = blockIdx.y;
-	const size_t plane = (size_t)S * S;
-	const uint16_t *pa = sel + (size_t)fa[pair] * plane + (size_t)row * S;
-	const int b = fb[pair];
-	const uint16_t *pb = b >= 0 ? sel + (size_t)b * plane + (size_t)row * S : nullptr;
-	sg_c64 *out = work + (size_t)pair * plane + (size_t)row * S;
-	unsigned long long ea = 0, eb = 0;
-	(void)logS;
-	sg_fft_io(buf, S, 1, S, tw, false,
-			[&](int, int i) {
-				const unsigned int va = pa[i], vb = pb ? pb[i] : 0u;
-				ea += (unsigned long long)(va * va);
-				eb += (unsigned long long)(vb * vb);
-				return make_double2((double)va, (double)vb);
-			},
-			[&](int, int i, sg_c64 v) { out[i] = v; });
-	sg_energy_add(ea, eb, fa[pair], b, energy);
-}
 
 /* strip of workgroup `id` out of n: the dispatcher deals workgroups round-robin over the 8
  * XCDs, so neighbouring strips (which share 128-B lines: a strip row is 64 B) would be
@@ -96,121 +72,6 @@ __device__ __forceinline__ sg_c64 sg_xpower_at(sg_c64 zk, sg_c64 zm, sg_c64 rk) 
 	const double pr = rk.x * ar + rk.y * ai, pi = rk.y * ar - rk.x * ai;
 	const double qr = rk.x * br + rk.y * bi, qi = rk.y * br - rk.x * bi;
 	return make_double2(pr - qi, pi + qr);
-}
-
-/* separate the packed spectra and form the packed cross-power spectrum, in place:
- * each (k, -k) pair is handled by the thread of the smaller linear index */
-__global__ void __launch_bounds__(256)
-k_reg_xpower(sg_c64 *__restrict__ work, const sg_c64 *__restrict__ spec, int S) {
-	const size_t plane = (size_t)S * S;
-	sg_c64 *Z = work + (size_t)blockIdx.y * plane;
-	for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < plane; i += (size_t)gridDim.x * blockDim.x) {
-		const int ky = (int)(i / S), kx = (int)(i - (size_t)ky * S);
-		const int my = (S - ky) & (S - 1), mx = (S - kx) & (S - 1);
-		const size_t m = (size_t)my * S + mx;
-		if (m < i)
-			continue;
-		const sg_c64 zk = Z[i], zm = Z[m];
-		/* F_a(k) = (Z(k) + conj Z(-k))/2, F_b(k) = (Z(k) - conj Z(-k))/(2i) */
-		const double ar = 0.5 * (zk.x + zm.x), ai = 0.5 * (zk.y - zm.y);
-		const double br = 0.5 * (zk.y + zm.y), bi = -0.5 * (zk.x - zm.x);
-		const sg_c64 rk = spec[i], rm = spec[m];
-		/* P(k) = R(k) conj F_a(k) + i R(k) conj F_b(k) */
-		{
-			const double pr = rk.x * ar + rk.y * ai, pi = rk.y * ar - rk.x * ai;	/* R conj(Fa) */
-			const double qr = rk.x * br + rk.y * bi, qi = rk.y * br - rk.x * bi;	/* R conj(Fb) */
-			Z[i] = make_double2(pr - qi, pi + qr);
-		}
-		if (m != i) {
-			/* F_a(-k) = conj F_a(k), F_b(-k) = conj F_b(k): P(-k) = R(-k) F_a + i R(-k) F_b */
-			const double pr = rm.x * ar - rm.y * ai, pi = rm.x * ai + rm.y * ar;
-			const double qr = rm.x * br - rm.y * bi, qi = rm.x * bi + rm.y * br;
-			Z[m] = make_double2(pr - qi, pi + qr);
-		}
-	}
-}
-
-/* cross-power fused into the inverse ROW pass: workgroup (ky, pair) transforms rows ky
- * and -ky (mod S) together (the rows whose cross-power terms need each other): the first
- * FFT pass forms each term from the forward spectrum and the reference spectrum as it
- * reads them (sg_xpower_at), the last writes the inverse rows back in place.  The
- * inverse column pass then only reads (k_reg_cols_inv_argmax). */
-__global__ void __launch_bounds__(1024)
-k_reg_xpower_rows_inv(sg_c64 *__restrict__ work, const sg_c64 *__restrict__ spec, int S, int logS,
-		const sg_c64 *__restrict__ tw) {
-	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-	sg_c64 *buf = (sg_c64 *)smem;
-	const int ky = blockIdx.x, pair = blockIdx.y;
-	const int my = (S - ky) & (S - 1);
-	const bool self = my == ky;
-	sg_c64 *Z = work + (size_t)pair * S * S;
-	const sg_c64 *Rs = spec;
-	(void)logS;
-	/* element i of row `row` (its mirror row `mrow`): the cross-power term as
-	 * sg_xpower_at forms it, read straight from memory by the first FFT pass */
-	sg_fft_io(buf, S, self ? 1 : 2, SG_PADN(S), tw, true,
-			[&](int b, int i) {
-				const int rw = b ? my : ky, mr = b ? ky : my;
-				return sg_xpower_at(Z[(size_t)rw * S + i], Z[(size_t)mr * S + ((S - i) & (S - 1))],
-						Rs[(size_t)rw * S + i]);
-			},
-			[&](int b, int i, sg_c64 v) { Z[(size_t)(b ? my : ky) * S + i] = v; });
-}
-
-/* inverse row pass fused with the per-row top-2 arg-max of the real (frame a) and imaginary
- * (frame b) parts */
-__global__ void __launch_bounds__(512)
-k_reg_rows_inv_argmax(const sg_c64 *__restrict__ work, int S, int logS, const sg_c64 *__restrict__ tw,
-		SgBest *__restrict__ best) {
-	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-	sg_c64 *buf = (sg_c64 *)smem;
-	__shared__ SgBest red[8];
-	const int row = blockIdx.x, pair = blockIdx.y;
-	const sg_c64 *in = work + (size_t)pair * S * S + (size_t)row * S;
-	SgTop2 ta, tb;
-	sg_top2_init(ta);
-	sg_top2_init(tb);
-	(void)logS;
-	sg_fft_io(buf, S, 1, S, tw, true, [&](int, int j) { return in[j]; },
-			[&](int, int j, sg_c64 c) {
-				const int idx = row * S + j;
-				sg_top2_add(ta, c.x, idx);
-				sg_top2_add(tb, c.y, idx);
-			});
-	sg_best_block(ta, tb, red);
-	if (threadIdx.x == 0) {
-		best[(size_t)pair * S + row].a = ta;
-		best[(size_t)pair * S + row].b = tb;
-	}
-}
-
-/* inverse column pass fused with the top-2 arg-max of the real (frame a) and imaginary
- * (frame b) parts over the strip: nothing is written back */
-__global__ void __launch_bounds__(1024)
-k_reg_cols_inv_argmax(const sg_c64 *__restrict__ work, int S, int logS, int CW, const sg_c64 *__restrict__ tw,
-		SgBest *__restrict__ best, int xcdmap) {
-	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-	sg_c64 *buf = (sg_c64 *)smem;
-	__shared__ SgBest red[16];
-	const int strip = sg_xcd_strip(blockIdx.x, gridDim.x, xcdmap);
-	const int x0 = strip * CW, pair = blockIdx.y;
-	const int bstride = SG_PADN(S) + 1;
-	const sg_c64 *base = work + (size_t)pair * S * S + x0;
-	SgTop2 ta, tb;
-	sg_top2_init(ta);
-	sg_top2_init(tb);
-	(void)logS;
-	sg_fft_io(buf, S, CW, bstride, tw, true, [&](int c, int r) { return base[(size_t)r * S + c]; },
-			[&](int c, int r, sg_c64 v) {
-				const int lin = r * S + x0 + c;
-				sg_top2_add(ta, v.x, lin);
-				sg_top2_add(tb, v.y, lin);
-			});
-	sg_best_block(ta, tb, red);
-	if (threadIdx.x == 0) {
-		best[(size_t)pair * gridDim.x + strip].a = ta;
-		best[(size_t)pair * gridDim.x + strip].b = tb;
-	}
 }
 
 /* ---------------------------------------------------------------------------------------
@@ -1164,14 +1025,25 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	hipStream_t s = stream ? (hipStream_t)stream : dv.stream;
 	const int logS = ilog2(S);
 	const size_t plane = (size_t)S * S;
-	/* power-of-two sides take the fused half-spectrum passes; any other side the generic
-	 * mixed-radix / Bluestein passes (SG_REG_PATH=3 forces those for a power of two, A/B) */
+	/* power-of-two sides take the half-spectrum passes; any other side the generic mixed-radix /
+	 * Bluestein passes (SG_REG_PATH=3 forces those for a power of two, A/B; the round-1/2 full-
+	 * spectrum pass orders 0 / 1 were removed in round 4) */
 	const int path = ctx->knobs.reg_path;	/* A/B knob SG_REG_PATH */
 	const bool generic = (S & (S - 1)) != 0 || S < 8 || path == 3;
-	const bool fused = !generic && path == 1;
-	const bool half = !generic && path == 2;
-	const bool resolvable = generic || half;	/* paths with a candidate pass */
-	ctx->stats.reg_ties_resolved = ctx->stats.reg_ties_unresolved = ctx->stats.reg_fp64_reruns = 0;
+	const bool half = !generic;	/* power of two: the half-spectrum passes */
+	/* the call's tie statistics: the device's record (one host thread per device), published to
+	 * the context when the call returns */
+	dv.stats.reg_ties_resolved = dv.stats.reg_ties_unresolved = dv.stats.reg_fp64_reruns = 0;
+	struct Publish {
+		sg_ctx *c;
+		const sg_stack_stats &s;
+		~Publish() {
+			std::lock_guard<std::mutex> lk(c->mu);
+			c->stats.reg_ties_resolved = s.reg_ties_resolved;
+			c->stats.reg_ties_unresolved = s.reg_ties_unresolved;
+			c->stats.reg_fp64_reruns = s.reg_fp64_reruns;
+		}
+	} publish{ctx, dv.stats};
 
 	/* frames to register, in index order (the reference skips ref and excluded frames) */
 	std::vector<int> todo;
@@ -1277,11 +1149,10 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		CW = 8;
 	if (ctx->knobs.reg_cw > 0)	/* A/B knob SG_REG_CW: columns per column-pass workgroup */
 		CW = ctx->knobs.reg_cw;
-	const size_t col_lds = (size_t)CW * (SG_PADN(S) + 1) * sizeof(sg_c64);
 	/* threads: 8 elements per thread in every fp64 LDS FFT (sg_stockham_pass's register
 	 * budget), 16 in the fp32 column pass; at least one wave, at most 1024 */
 	auto thr_for = [](int elems) { return elems / 8 < 64 ? 64 : elems / 8; };
-	const int row_thr = thr_for(S), col_thr = thr_for(CW * S), xri_thr = thr_for(2 * S);
+	const int row_thr = thr_for(S);
 	/* half-spectrum columns: a strip stays inside one half (CW divides S/2) */
 	const int CWh = CW < S / 2 ? CW : S / 2;
 	const size_t colh_lds = (size_t)CWh * (SG_PADN(S) + 1) * sizeof(sg_c64);
@@ -1303,15 +1174,8 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	const int gen_thr = pl.bluestein ? (pl.m / 8 < 64 ? 64 : pl.m / 8) : 256;
 	const size_t gen_lds = pl.bluestein ? (size_t)SG_PADN(pl.m) * sizeof(sg_c64) : 2 * row_lds;
 	if (!generic) {
-		(void)hipFuncSetAttribute((const void *)k_reg_rows_fwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)row_lds);
-		(void)hipFuncSetAttribute((const void *)k_reg_rows_inv_argmax, hipFuncAttributeMaxDynamicSharedMemorySize,
-				(int)row_lds);
 		(void)hipFuncSetAttribute((const void *)k_reg_cols<sg_c64, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-				(int)col_lds);
-		(void)hipFuncSetAttribute((const void *)k_reg_cols_inv_argmax, hipFuncAttributeMaxDynamicSharedMemorySize,
-				(int)col_lds);
-		(void)hipFuncSetAttribute((const void *)k_reg_xpower_rows_inv, hipFuncAttributeMaxDynamicSharedMemorySize,
-				(int)(2 * row_lds));
+				(int)colh_lds);
 		(void)hipFuncSetAttribute((const void *)k_reg_rows_fwd_half<sg_c64>, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)row_lds);
 		(void)hipFuncSetAttribute((const void *)k_reg_rows_inv_half_argmax<sg_c64, false>,
@@ -1479,18 +1343,12 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		else
 			hipLaunchKernelGGL((k_reg_cols<float2, 8>), dim3(S / 2 / CW32, 1), dim3(colh_thr32), colh_lds32, s, spec32,
 					S, logS, CW32, tw32, 0, xcdmap);
-	} else if (half) {
+	} else {
 		hipLaunchKernelGGL(k_reg_rows_fwd_half<sg_c64>, dim3(S / rpb, 1), dim3(row_thr), row_lds, s, d_sel, d_fa + NP,
 				d_fb + NP, S, tw, spec, energy, rpb);
 		HIPCHK(hipGetLastError());
 		hipLaunchKernelGGL((k_reg_cols<sg_c64, 8>), dim3(S / 2 / CWh, 1), dim3(colh_thr), colh_lds, s, spec, S, logS,
 				CWh, tw, 0, xcdmap);
-	} else {
-		hipLaunchKernelGGL(k_reg_rows_fwd, dim3(S, 1), dim3(row_thr), row_lds, s, d_sel, d_fa + NP, d_fb + NP, S,
-				logS, tw, spec, energy);
-		HIPCHK(hipGetLastError());
-		hipLaunchKernelGGL((k_reg_cols<sg_c64, 8>), dim3(S / CW, 1), dim3(col_thr), col_lds, s, spec, S, logS, CW, tw, 0,
-				xcdmap);
 	}
 	HIPCHK(hipGetLastError());
 	shiftx[ref_image] = 0;
@@ -1508,34 +1366,9 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		} else if (fp32) {
 			if (int r = half32(d_fa + p0, d_fb + p0, np, energy))
 				return r;
-		} else if (half) {
+		} else {
 			if (int r = half64(d_fa + p0, d_fb + p0, np, energy, 0, nullptr))
 				return r;
-		} else {
-			hipLaunchKernelGGL(k_reg_rows_fwd, dim3(S, np), dim3(row_thr), row_lds, s, d_sel, d_fa + p0, d_fb + p0, S,
-					logS, tw, work, energy);
-			HIPCHK(hipGetLastError());
-			hipLaunchKernelGGL((k_reg_cols<sg_c64, 8>), dim3(S / CW, np), dim3(col_thr), col_lds, s, work, S, logS, CW,
-					tw, 0, xcdmap);
-			HIPCHK(hipGetLastError());
-			if (fused) {
-				/* cross-power + inverse rows (row pairs ky, -ky), then inverse columns with the
-				 * arg-max: two plane round trips fewer than the unfused order */
-				hipLaunchKernelGGL(k_reg_xpower_rows_inv, dim3(S / 2 + 1, np), dim3(xri_thr), 2 * row_lds, s, work,
-						(const sg_c64 *)spec, S, logS, tw);
-				HIPCHK(hipGetLastError());
-				hipLaunchKernelGGL(k_reg_cols_inv_argmax, dim3(S / CW, np), dim3(col_thr), col_lds, s,
-						(const sg_c64 *)work, S, logS, CW, tw, best, xcdmap);
-				count = S / CW;
-			} else {
-				hipLaunchKernelGGL(k_reg_xpower, dim3(1024, np), dim3(256), 0, s, work, (const sg_c64 *)spec, S);
-				HIPCHK(hipGetLastError());
-				hipLaunchKernelGGL((k_reg_cols<sg_c64, 8>), dim3(S / CW, np), dim3(col_thr), col_lds, s, work, S, logS,
-						CW, tw, 1, xcdmap);
-				HIPCHK(hipGetLastError());
-				hipLaunchKernelGGL(k_reg_rows_inv_argmax, dim3(S, np), dim3(row_thr), row_lds, s,
-						(const sg_c64 *)work, S, logS, tw, best);
-			}
 		}
 		HIPCHK(hipGetLastError());
 		hipLaunchKernelGGL(k_reg_final, dim3(np), dim3(256), 0, s, (const SgBest *)best, S, count,
@@ -1595,10 +1428,10 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		HIPCHK(hipStreamSynchronize(s));
 		for (int i = 0; i < na; i++)
 			hout[amb[i]] = ares[i];
-		ctx->stats.reg_fp64_reruns += (uint64_t)na;
+		dv.stats.reg_fp64_reruns += (uint64_t)na;
 		ambiguous(amb);
 	}
-	if (!amb.empty() && resolvable) {
+	if (!amb.empty()) {
 		if (int r = upload_subset(amb, ares))
 			return r;
 		const int na = (int)amb.size();
@@ -1637,9 +1470,9 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 			shiftx[fr[h]] = hout[k].sx[h];
 			shifty[fr[h]] = hout[k].sy[h];
 			if (hout[k].amb[h] == 2)
-				ctx->stats.reg_ties_resolved++;
+				dv.stats.reg_ties_resolved++;
 			else if (hout[k].amb[h])
-				ctx->stats.reg_ties_unresolved++;
+				dv.stats.reg_ties_unresolved++;
 		}
 	}
 
@@ -1669,17 +1502,134 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	return SG_OK;
 }
 
-extern "C" int sg_register_dft_u16(sg_ctx *ctx, const uint16_t *sel, int nframes, int S, int ref_image,
-		const int *included, int *shiftx, int *shifty, double *quality) {
-	if (!ctx || ctx->dev.empty() || !sel)
+/*
+ * host selections: one device registers everything; several devices split the frames to
+ * register into contiguous shards (frames are independent), each device driven by
+ * its own host thread with the reference selection and its shard uploaded, the reference
+ * spectrum and quality computed on every device.  The raw shard results are reassembled and
+ * the quality bookkeeping of the reference (q_min / q_max seeded by the reference frame, the
+ * frames in index order, the min() macro, normalizeQualityData :163-176) replayed over all of
+ * them, so the result is the one-device result (test_register_raw_shards_reassemble).
+ */
+static int reg_host(sg_ctx *ctx, const uint16_t *sel, int nframes, int S, int ref_image, const int *included,
+		int *shiftx, int *shifty, double *quality, bool normalize_q) {
+	if (!ctx || ctx->dev.empty() || !sel || !shiftx || !shifty || !quality)
 		return SG_ERR_GENERIC;
 	if (nframes < 1 || S < 1)
 		return SG_ERR_GENERIC;
-	SgDevice &dv = ctx->dev[0];
-	HIPCHK(hipSetDevice(dv.id));
-	const size_t bytes = (size_t)nframes * S * S * sizeof(uint16_t);
-	HIPCHK(ensure(dv.reg_sel, bytes));
-	HIPCHK(hipMemcpyAsync(dv.reg_sel.p, sel, bytes, hipMemcpyHostToDevice, dv.stream));
-	return sg_register_dft_u16_device(ctx, 0, (const uint16_t *)dv.reg_sel.p, nframes, S, ref_image, included,
-			shiftx, shifty, quality, nullptr);
+	if (ref_image < 0)
+		ref_image = 0;
+	if (ref_image >= nframes)
+		return set_err(ctx, SG_ERR_GENERIC, "reference image out of range%s %ld", "", ref_image);
+	const size_t plane = (size_t)S * S;
+	std::vector<int> todo;
+	for (int f = 0; f < nframes; f++)
+		if (f != ref_image && (!included || included[f]))
+			todo.push_back(f);
+	const int G = (int)std::max<size_t>(1, std::min(ctx->dev.size(), todo.size()));
+	if (G == 1) {
+		SgDevice &dv = ctx->dev[0];
+		HIPCHK(hipSetDevice(dv.id));
+		const size_t bytes = (size_t)nframes * plane * sizeof(uint16_t);
+		HIPCHK(ensure(dv.reg_sel, bytes));
+		HIPCHK(hipMemcpyAsync(dv.reg_sel.p, sel, bytes, hipMemcpyHostToDevice, dv.stream));
+		return reg_dft_device(ctx, 0, (const uint16_t *)dv.reg_sel.p, nframes, S, ref_image, included, shiftx, shifty,
+				quality, nullptr, normalize_q);
+	}
+	/* shard g: local frame 0 = the reference, 1..k = todo[t0 .. t1) */
+	std::vector<int> rcs((size_t)G, SG_OK);
+	std::vector<double> qraw((size_t)nframes, 0.0);
+	std::vector<double> qref((size_t)G, 0.0);
+	auto run = [&](int g) {
+		const size_t t0 = todo.size() * (size_t)g / (size_t)G, t1 = todo.size() * (size_t)(g + 1) / (size_t)G;
+		const int k = (int)(t1 - t0);
+		SgDevice &dv = ctx->dev[(size_t)g];
+		int &rc = rcs[(size_t)g];
+		if (hipSetDevice(dv.id) != hipSuccess) {
+			rc = set_err(ctx, SG_ERR_DEVICE, "hipSetDevice failed%s %ld", "", dv.id);
+			return;
+		}
+		const size_t bytes = (size_t)(k + 1) * plane * sizeof(uint16_t);
+		if (ensure(dv.reg_sel, bytes) != hipSuccess) {
+			rc = set_err(ctx, SG_ERR_DEVICE, "no device memory for the selections%s (%ld frames)", "", k + 1);
+			return;
+		}
+		uint16_t *d = (uint16_t *)dv.reg_sel.p;
+		hipError_t e = hipMemcpyAsync(d, sel + (size_t)ref_image * plane, plane * sizeof(uint16_t),
+				hipMemcpyHostToDevice, dv.stream);
+		for (int j = 0; j < k && e == hipSuccess; j++)
+			e = hipMemcpyAsync(d + (size_t)(j + 1) * plane, sel + (size_t)todo[t0 + (size_t)j] * plane,
+					plane * sizeof(uint16_t), hipMemcpyHostToDevice, dv.stream);
+		if (e != hipSuccess) {
+			rc = set_err(ctx, SG_ERR_DEVICE, "selection upload failed%s %ld", "", g);
+			return;
+		}
+		std::vector<int> lx((size_t)k + 1), ly((size_t)k + 1);
+		std::vector<double> lq((size_t)k + 1);
+		rc = reg_dft_device(ctx, g, d, k + 1, S, 0, nullptr, lx.data(), ly.data(), lq.data(), nullptr, false);
+		if (rc)
+			return;
+		qref[(size_t)g] = lq[0];
+		for (int j = 0; j < k; j++) {
+			const int f = todo[t0 + (size_t)j];
+			shiftx[f] = lx[(size_t)j + 1];
+			shifty[f] = ly[(size_t)j + 1];
+			qraw[(size_t)f] = lq[(size_t)j + 1];
+		}
+	};
+	{
+		std::vector<std::thread> th;
+		for (int g = 1; g < G; g++)
+			th.emplace_back(run, g);
+		run(0);
+		for (std::thread &t : th)
+			t.join();
+	}
+	sg_stack_stats agg;
+	memset(&agg, 0, sizeof agg);
+	for (int g = 0; g < G; g++) {
+		const sg_stack_stats &st = ctx->dev[(size_t)g].stats;
+		agg.reg_ties_resolved += st.reg_ties_resolved;
+		agg.reg_ties_unresolved += st.reg_ties_unresolved;
+		agg.reg_fp64_reruns += st.reg_fp64_reruns;
+	}
+	{
+		std::lock_guard<std::mutex> lk(ctx->mu);
+		ctx->stats.reg_ties_resolved = agg.reg_ties_resolved;
+		ctx->stats.reg_ties_unresolved = agg.reg_ties_unresolved;
+		ctx->stats.reg_fp64_reruns = agg.reg_fp64_reruns;
+	}
+	for (int g = 0; g < G; g++)
+		if (rcs[(size_t)g])
+			return rcs[(size_t)g];
+	shiftx[ref_image] = shifty[ref_image] = 0;
+	quality[ref_image] = qref[0];
+	for (int f : todo)
+		quality[f] = qraw[(size_t)f];
+	if (!normalize_q)
+		return SG_OK;
+	double q_min = qref[0], q_max = qref[0];
+	for (int f : todo) {
+		const double qv = qraw[(size_t)f];
+		if (qv > q_max)
+			q_max = qv;
+		q_min = (q_min < qv) ? q_min : qv;
+	}
+	for (int f = 0; f < nframes; f++) {
+		if (included && !included[f])
+			continue;
+		quality[f] -= q_min;
+		quality[f] /= (q_max - q_min);
+	}
+	return SG_OK;
+}
+
+extern "C" int sg_register_dft_u16(sg_ctx *ctx, const uint16_t *sel, int nframes, int S, int ref_image,
+		const int *included, int *shiftx, int *shifty, double *quality) {
+	return reg_host(ctx, sel, nframes, S, ref_image, included, shiftx, shifty, quality, true);
+}
+
+extern "C" int sg_register_dft_u16_raw(sg_ctx *ctx, const uint16_t *sel, int nframes, int S, int ref_image,
+		const int *included, int *shiftx, int *shifty, double *quality_raw) {
+	return reg_host(ctx, sel, nframes, S, ref_image, included, shiftx, shifty, quality_raw, false);
 }

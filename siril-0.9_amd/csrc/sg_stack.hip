@@ -1849,7 +1849,7 @@ k_stack_replay(SgStackParams p) {
 						     : replay_pixel<NM / 64>(L, p.N, p.rejection, p.sig0, p.sig1,
 									     lane, &v, &rl, &rh);
 #ifdef SG_REPLAY_PROF
-		if (p.dbg == 12 && lane == 0) {
+		if (SG_DBG(p) == 12 && lane == 0) {
 			const unsigned long long t2 = __builtin_readcyclecounter();
 			atomicMax(&g_sg_rprof[0], t2 - t0);
 			atomicMax(&g_sg_rprof[1], t1 - t0);
@@ -1912,6 +1912,12 @@ k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *s
 			continue;	/* SG_CLS_DONE: finished by k_stack_replay */
 		uint32_t crej[2] = {0, 0};
 		int fbrk;
+		if (p.method == 2) {	/* stack_median's pixel (:746-767): redo list of the histogram path */
+			gather_stack(p, pix, stack);
+			shellsort_u16(stack, p.N);
+			p.out[pix] = (uint16_t)lit_median(stack, p.N);
+			continue;
+		}
 		if (phase == 1) {
 			for (int k = 0; k < p.N; k++)
 				rejected[k] = 0;

@@ -1268,19 +1268,85 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 
 /* pixel column `col` of the tile (x its image column); PAIR: lane pair half `half`, else one
  * lane per column (half = 0) */
+/*
+ * stack_median's pixel (src/stacking/stacking.c:746-767, REJ 8) and PERCENTILE rejection
+ * (:1660-1673 + percentile_clipping :1130-1143, REJ 1) from the column histogram.  Both are
+ * rank queries on the sorted column: the median is gsl_stats_ushort_median_from_sorted_data
+ * (odd N: a[N/2]; even: (a[(N-1)/2] + a[N/2]) / 2.0), which stack_median truncates to WORD
+ * (:766-767).  PERCENTILE rejects a sample p as low when (median - p) / median > sig[0], else
+ * as high when (p - median) / median > sig[1], both evaluated in the reference's double
+ * arithmetic (median is a half-integer, median - p is exact, the division correctly rounded
+ * and monotone in p): the low set is {p <= L}, the high set {p >= Uh}, found at the bound
+ * estimate and stepped to the exact predicate edge, so no rounding band is needed.  The kept
+ * samples are the values in (L, Uh); their exact sum / count is round_to_WORD'ed (:1790-1794).
+ * The removal loop keeps its last sample when every one is rejected (`N > 1`, :1667-1672):
+ * the largest.  With this row's normalised zeros among the below-band samples (ZT) a rank or
+ * a count landing among them is not decided here (redo).
+ */
+template <int REJ, bool ZT>
+__device__ __forceinline__ int sgh_median_pct(const SghPix &P, int N, double sl, double sh, uint16_t *value,
+		uint32_t *rlo, uint32_t *rhi) {
+	const int g1 = (N - 1) / 2, g2 = N / 2;
+	if (ZT && P.zmax > 0 && g1 < P.nz)
+		return SG_CLS_LITERAL;
+	int m1, m2;
+	sgh_value_at2(P, g1, g2, m1, m2);
+	if (REJ == 8) {
+		*value = (uint16_t)((m1 + m2) >> 1);	/* (WORD)((a + b) / 2.0): truncation of a half-integer */
+		return SG_CLS_OK;
+	}
+	const double median = g1 == g2 ? (double)m1 : ((double)m1 + (double)m2) / 2.0;
+	auto plo = [&](int v) { return (median - (double)v) / median > sl; };
+	auto phi = [&](int v) { return ((double)v - median) / median > sh; };
+	/* L: the largest sample value rejected low (-1: none); Uh: the smallest rejected high
+	 * (65536: none) and not low (the reference tests low first) */
+	int L = sgh_ceil_clamp(median - sl * median) - 1;	/* NaN -> -1 */
+	L = L > 65535 ? 65535 : L;
+	while (L < 65535 && plo(L + 1))
+		L++;
+	while (L >= 0 && !plo(L))
+		L--;
+	int U = sgh_floor_clamp(median + sh * median) + 1;	/* NaN -> 65536 */
+	U = U < 0 ? 0 : U;
+	while (U > 0 && phi(U - 1))
+		U--;
+	while (U <= 65535 && !phi(U))
+		U++;
+	const int Uh = U > L + 1 ? U : L + 1;
+	if (ZT && P.zmax > 0 && ((L >= 0 && L < P.zmax) || (Uh - 1 >= 0 && Uh - 1 < P.zmax)))
+		return SG_CLS_LITERAL;
+	SghQ qa, qb;
+	sgh_q_load(P, L, qa);
+	sgh_q_load(P, Uh - 1, qb);
+	const int nlow = sgh_q_count(P, qa), nle = sgh_q_count(P, qb);
+	const int nhigh = N - nle, kept = nle - nlow;
+	*rlo = (uint32_t)nlow;
+	*rhi = (uint32_t)nhigh;
+	if (kept == 0) {	/* every sample rejected: the removal stops at the last one */
+		int mx, mx2;
+		sgh_value_at2(P, N - 1, N - 1, mx, mx2);
+		*value = (uint16_t)mx;
+		return SG_CLS_OK;
+	}
+	const SghM ma = sgh_q_moments(P, qa), mb = sgh_q_moments(P, qb);
+	const long long sum = (mb.s - ma.s) + (long long)kept * P.lo;	/* exact: below 2^32 */
+	*value = sg_round_to_WORD((double)sum / (double)kept);
+	return SG_CLS_OK;
+}
+
 template <int REJ, bool PAIR, int NI, bool ZT = false>
 __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int half, int lo, int R, int c, int x,
 		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list, bool zrow = false) {
 	const int lane = threadIdx.x & 63;
 	const int N = p.N;
 	const uint32_t *hc = &L.h[col >> 6][0][col & 63];	/* dword j at hc[64 j] */
-	if (p.dbg == 2 || p.dbg == 3) {
+	if (SG_DBG(p) == 2 || SG_DBG(p) == 3) {
 		if (x < p.W && !half)
 			p.out[((int64_t)c * p.H + R) * p.W + x] = (uint16_t)(hc[0] + L.nz[col]);
 		return;
 	}
 	/* A/B timeline (dbg 11): cycles of the prefix and of the pass loop, passes per wave */
-	const uint64_t c0 = p.dbg == 11 ? __builtin_readcyclecounter() : 0;
+	const uint64_t c0 = SG_DBG(p) == 11 ? __builtin_readcyclecounter() : 0;
 #ifdef SGH_WPROF
 	if (REJ == 4 && lane == 0) {
 		uint64_t *w = L.wp[threadIdx.x >> 6];
@@ -1384,9 +1450,9 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 	int cls = SG_CLS_OK;
 	uint16_t value = 0;
 	uint32_t rlo = 0, rhi = 0;
-	const uint64_t c1 = p.dbg == 11 ? __builtin_readcyclecounter() : 0;
+	const uint64_t c1 = SG_DBG(p) == 11 ? __builtin_readcyclecounter() : 0;
 	if (x < p.W) {
-		if (p.dbg == 1) {
+		if (SG_DBG(p) == 1) {
 			value = (uint16_t)(s32 + ss32);
 		} else if (P.nb + oob != N || oob != P.nz + P.ns + zc || (zc && zmax >= lo)) {
 			cls = 1;	/* out-of-band sample other than 0 / 65535 (or than this row's normalised
@@ -1407,7 +1473,9 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 			P.T.c = N;
 			P.T.s = (long long)s32 + P.Z.s + ds * P.ns;
 			P.T.ss = (unsigned long long)ss32 + P.Z.ss + (unsigned long long)(ds * ds) * (unsigned long long)P.ns;
-			if (REJ == 4 || !PAIR) {
+			if (REJ == 1 || REJ == 8) {
+				cls = sgh_median_pct<REJ, ZT>(P, N, p.sig0, p.sig1, &value, &rlo, &rhi);
+			} else if (REJ == 4 || !PAIR) {
 				/* zeros: nz copies of -lo, exact as doubles (dz = -lo, dz^2 nz < 2^53) */
 				P.zs = -(double)lo * (double)P.nz;
 				P.zss = (double)lo * (double)lo * (double)P.nz;
@@ -1435,7 +1503,7 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 		if (!half) {
 			if (cls == SG_CLS_OK) {
 #ifndef SGH_WPROF
-				if (p.dbg != 11)	/* the timeline A/B keeps its stamps in the output buffer */
+				if (SG_DBG(p) != 11)	/* the timeline A/B keeps its stamps in the output buffer */
 					p.out[pix] = value;
 #endif
 			} else {
@@ -1448,7 +1516,7 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 		if (cls != SG_CLS_OK || half)
 			rlo = rhi = 0;
 	}
-	if (p.dbg == 11 && NI == 2) {
+	if (SG_DBG(p) == 11 && NI == 2) {
 		const uint64_t c2 = __builtin_readcyclecounter();
 		int pmax = passes, psum = passes;
 		for (int o = 32; o > 0; o >>= 1) {
@@ -1572,7 +1640,7 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, const SghRo &r
 #pragma unroll
 	for (int i = 0; i < NI; i++)
 		lo2[i] = L.lo2[i][lane];
-	const bool loads_only = p.dbg == 3;
+	const bool loads_only = SG_DBG(p) == 3;
 	auto binblk = [&](int f0, const uint32_t (&raw)[M][NI], const uint32_t (&fx)[NI]) {
 		if (loads_only) {
 #pragma unroll
@@ -1688,7 +1756,7 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
 		}
 	}
 	sgh_clear<NI, BW>(L, wait_prev, bar);
-	const bool nocentre = p.dbg == 15;	/* A/B: loads only, no centre and no start barrier */
+	const bool nocentre = SG_DBG(p) == 15;	/* A/B: loads only, no centre and no start barrier */
 	static_assert(!SGH_CENTER2W || SGH_CENTER == 2 * MB, "two half blocks make the centre sample");
 	if (SGH_CENTER2W && !nocentre) {
 		/* the centre sample is the first half block of wave 0 (frames 0..7) and of wave 1
@@ -1752,7 +1820,7 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
 #pragma unroll
 	for (int i = 0; i < NI; i++)
 		lo2[i] = nocentre ? 0u : L.lo2[i][lane];
-	const bool loads_only = p.dbg == 3 || nocentre;
+	const bool loads_only = SG_DBG(p) == 3 || nocentre;
 	/* bin one half (frames f0 .. f0 + 7), per-frame bounds when it is not whole */
 	auto binh = [&](int f0, const uint32_t (&raw)[MB][NI], const uint32_t (&fx)[NI], bool whole) {
 		if (loads_only) {
@@ -1849,9 +1917,9 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 	const int c = bid / nrows;
 	const int x0 = xt * COLS;
 	bool interior = x0 >= p.hist_maxsx && x0 + COLS + p.hist_maxsx <= p.W;
-	if (p.dbg == 4)		/* A/B: every full tile on the dword path (wrong edges) */
+	if (SG_DBG(p) == 4)		/* A/B: every full tile on the dword path (wrong edges) */
 		interior = x0 + COLS <= p.W;
-	if (p.dbg == 5 && !interior)	/* A/B: skip the edge tiles */
+	if (SG_DBG(p) == 5 && !interior)	/* A/B: skip the edge tiles */
 		return;
 	SghFrame F;
 	F.plane0 = (const char *)(p.frames + (int64_t)c * p.plane_stride);
@@ -1868,7 +1936,7 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 	 * after the build barrier and at the end of every wave's finish, written into the
 	 * output buffer as u64 [tile][4] (the image is garbage in this mode) */
 	uint64_t *const tl = (uint64_t *)p.out + (size_t)blockIdx.x * 32;
-	const bool timeline = NI == 2 && p.dbg == 11;
+	const bool timeline = NI == 2 && SG_DBG(p) == 11;
 	if (timeline && tid == 0) {
 		tl[0] = __builtin_amdgcn_s_memrealtime();
 		tl[3] = 0;
@@ -2009,6 +2077,22 @@ template __global__ void k_stack_hist<4, 0, 1>(SgStackParams, const int *, const
 template __global__ void k_stack_hist<4, 1, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
 		unsigned int *);
 template __global__ void k_stack_hist<4, 2, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);
+template __global__ void k_stack_hist<1, 0, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);
+template __global__ void k_stack_hist<1, 1, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);
+template __global__ void k_stack_hist<1, 2, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);
+template __global__ void k_stack_hist<1, 3, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);
+template __global__ void k_stack_hist<8, 0, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);
+template __global__ void k_stack_hist<8, 1, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);
+template __global__ void k_stack_hist<8, 2, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);
+template __global__ void k_stack_hist<8, 3, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
 		unsigned int *);
 template __global__ void k_stack_hist<2, 0, 2>(SgStackParams, const int *, const int4 *, unsigned int *,
 		unsigned int *);

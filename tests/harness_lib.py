@@ -42,6 +42,9 @@ def load():
     lib.harness_gfit_hi.restype = ctypes.c_ushort
     lib.harness_save_gfit.argtypes = [ctypes.c_char_p]
     lib.siril_gpu_release.restype = None
+    lib.harness_set_run_in_thread.argtypes = [ctypes.c_int]
+    lib.harness_gfit_exposure.restype = ctypes.c_double
+    lib.harness_set_devices.argtypes = [ctypes.c_int, P]
     _lib = lib
     return lib
 
@@ -93,6 +96,15 @@ class Sequence:
                 return None
             sx[i], sy[i], q[i] = a.value, b.value, c.value
         return sx, sy, q
+
+
+def set_devices(devs):
+    """the glue's context on these device ids (None: every visible device)"""
+    lib = load()
+    if devs is None:
+        return lib.harness_set_devices(-1, None)
+    arr = (ctypes.c_int * len(devs))(*devs)
+    return lib.harness_set_devices(len(devs), ctypes.cast(arr, P))
 
 
 def gfit():

@@ -47,7 +47,8 @@ def _card(key, value, comment=""):
     return s.ljust(80)[:80].encode("ascii")
 
 
-def write_fits(path, frame, bitpix=16, bzero=None):
+def write_fits(path, frame, bitpix=16, bzero=None, keys=None):
+    """savefits restated; keys: extra (keyword, value text) cards, e.g. ("EXPTIME", "30.")"""
     frame = np.asarray(frame)
     C, H, W = frame.shape
     if bzero is None:
@@ -58,6 +59,8 @@ def write_fits(path, frame, bitpix=16, bzero=None):
         cards.append(_card("NAXIS3", str(C)))
     if bitpix == 16:
         cards += [_card("BZERO", str(bzero)), _card("BSCALE", "1")]
+    for k, v in (keys or []):
+        cards.append(_card(k, v))
     cards.append(b"END".ljust(80))
     hdr = b"".join(cards)
     hdr += b" " * ((-len(hdr)) % 2880)

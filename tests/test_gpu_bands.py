@@ -159,12 +159,12 @@ def test_band_rows_not_resident_rejected(gpu_ctx):
         gpu_ctx.stack_device(desc, band.data_ptr() - b * W * 2, (e - b) * W, (e - b) * W, d_out.data_ptr(), b, e)
 
 
-def _with_budget(nbytes, fn):
+def _with_budget(nbytes, fn, devices=None):
     """fn(ctx) on a context created under the budget knob (knobs are read at sg_init)"""
     old = os.environ.get("SG_HOST_BUDGET_BYTES")
     os.environ["SG_HOST_BUDGET_BYTES"] = str(nbytes)
     try:
-        with sg.Context() as ctx:
+        with sg.Context(devices) as ctx:
             return fn(ctx)
     finally:
         if old is None:
@@ -226,3 +226,51 @@ def test_host_pull_band_inherits_stale_state(gpu_ctx, max_thread):
     assert rc == 0, err
     assert_same(out, ref, f"host bands with stale state, thr={max_thread}")
     assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+
+
+@pytest.mark.parametrize("method,rejection", CASES + [(sg.SUM, sg.NO_REJEC)])
+@pytest.mark.parametrize("devs,band_rows", [([0, 0], 0), ([0, 0, 0], 4), ([0, 0, 0, 0, 0], 0)])
+def test_host_pull_device_slots(gpu_ctx, method, rejection, devs, band_rows):
+    """sg_stack_u16 on a context of several device slots (here all on one card): each slot takes
+    a contiguous share of the output rows, pulls its frame rows with its own readers and stacks
+    them (banded under a budget when band_rows > 0); SUM scales by the maximum over every slot.
+    Equal to the one-image oracle, counters summed"""
+    N, C, H, W = 20, 2, 31, 90
+    frames = orc.synth(N, C, H, W, seed=52, maxshift=5)
+    sx, sy = orc.synth_shifts(N, seed=52, maxshift=5)
+    sig = REJ[rejection]
+    if method == sg.SUM:
+        rc, ref, mref = orc.stack_sum(frames, sx, sy)
+        assert rc == 0 and mref > 65535
+        rej_ref = np.zeros((3, 2), np.uint64)
+    else:
+        ref, rej_ref = _oracle(frames, method, rejection, sig, sx, sy, 4)
+    desc, keep = sg.make_desc(method, N, W, H, C, rejection=rejection, sig=sig, shiftx=sx, shifty=sy,
+                              max_thread=4, max_number_of_rows=H)
+    if band_rows:
+        halo = 0 if method == sg.MEDIAN else int(sy.max() - sy.min())
+        budget = N * C * W * 2 * (band_rows + halo)
+        rc, out, rej, maxim, err = _with_budget(budget, lambda c: c.stack_host(desc, frames) + (c.error(),), devs)
+    else:
+        with sg.Context(devs) as c:
+            rc, out, rej, maxim = c.stack_host(desc, frames)
+            err = c.error()
+    assert rc == 0, err
+    assert_same(out, ref, f"slots={len(devs)} method={method} rej={rejection} rows={band_rows}")
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+    if method == sg.SUM:
+        assert maxim == mref
+
+
+@pytest.mark.parametrize("devs", [None, [0, 0]])
+def test_host_pull_cancel(gpu_ctx, devs):
+    """the caller's get_thread_run() turning false mid-read: the call stops and returns -1
+    (stacking.c:1539), whichever slot's reader polls it"""
+    N, C, H, W = 12, 1, 24, 64
+    frames = orc.synth(N, C, H, W, seed=3, maxshift=3)
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, C, rejection=sg.SIGMA)
+    with sg.Context(devs) as c:
+        rc, out, rej, _ = c.stack_host(desc, frames, cancel_after=5)
+        assert rc == -1
+        rc, out, rej, _ = c.stack_host(desc, frames)       # the context stays usable
+        assert rc == 0, c.error()

@@ -9,7 +9,8 @@ the oracle and with the one-pixel-per-lane kernel (SG_REDUCE1=1), bit for bit.
 
 Registration: the smallest sides (S = 8, 16: the staged small-FFT path and strips that
 span a whole half spectrum), odd frame counts (a pair with an empty imaginary part), the
-three pass orders (SG_REG_PATH 0/1/2) agreeing exactly, and at full size (S = 2048, where
+the pass families (fp32 half spectra, fp64 half spectra SG_REG_FP=64, the generic mixed-radix
+passes SG_REG_PATH=3) agreeing exactly, and at full size (S = 2048, where
 the plain-DFT oracle is too slow) circular shifts recovered exactly with the sign
 convention the oracle shows at S = 64.
 """
@@ -100,13 +101,13 @@ def test_register_small_sides(gpu_ctx, S, n):
 @pytest.mark.parametrize("S,n", [(64, 5), (512, 9)])
 def test_register_pass_orders_agree(gpu_ctx, S, n):
     sel = orc.synth(n, 1, S, S, seed=S + 3 * n, maxshift=12)[:, 0].copy()
-    res = {}
-    for path in ("0", "1", "2"):
-        res[path] = _with_env("SG_REG_PATH", path, lambda c: c.register_dft(sel))
-    for path in ("0", "1"):
+    res = {"fp32": gpu_ctx.register_dft(sel)}
+    res["fp64"] = _with_env("SG_REG_FP", "64", lambda c: c.register_dft(sel))
+    res["generic"] = _with_env("SG_REG_PATH", "3", lambda c: c.register_dft(sel))
+    for name in ("fp64", "generic"):
         for k in range(3):
-            assert np.array_equal(np.nan_to_num(res[path][k], nan=-7.0),
-                                  np.nan_to_num(res["2"][k], nan=-7.0)), (path, k)
+            assert np.array_equal(np.nan_to_num(res[name][k], nan=-7.0),
+                                  np.nan_to_num(res["fp32"][k], nan=-7.0)), (name, k)
 
 
 def _scene(S, seed):

@@ -1,0 +1,130 @@
+"""stack_median and PERCENTILE rejection on the histogram path (k_stack_hist<8> / <1>,
+siril-0.9_amd/csrc/sg_stack_hist.hip sgh_median_pct) against the C oracle, and frame counts
+beyond the sorted kernel's 1024 on the histogram path.
+
+stack_median (src/stacking/stacking.c:746-767): normalise at load, sort, GSL median, truncate to
+WORD.  PERCENTILE (:1660-1673 + percentile_clipping :1130-1143): the reference's double
+predicates on the GSL median, the kept samples' mean round_to_WORD'ed, the last sample kept
+when every one is rejected.  Bit-exact; the main kernel must be the histogram one
+(sg_stack_stats.path == 1) and pixels it cannot decide (out-of-band samples other than 0 /
+65535, u8 bin overflow, ranks among normalised border zeros) go through the redo list.
+"""
+import numpy as np
+import pytest
+
+import oracle_lib as orc
+import sirilgpu as sg
+from test_gpu_stack import assert_same, gpu_stack
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames(N, C, H, W, seed, maxshift=6):
+    f = orc.synth(N, C, H, W, seed=seed, maxshift=maxshift)
+    rng = np.random.default_rng(seed)
+    f[:, :, 1, :7] = 0                                  # zero columns: median 0 (PERCENTILE / 0)
+    f[:, :, 2, 3:9] = 65535                             # saturated columns
+    f[: N // 2, :, 3, 10:14] = 0                        # half the stack at 0
+    f[:, :, 4, 20:30] = 1500                            # constant: u8 bins overflow for N >= 256
+    m = rng.random(f.shape) < 0.01
+    f[m] = rng.integers(20000, 60000, size=int(m.sum()))    # far outliers: out-of-band redo pixels
+    return f
+
+
+def _coeffs(normalize, N, seed):
+    rng = np.random.default_rng(seed)
+    loc = 1000 + rng.random(N) * 80
+    scl = 30 + rng.random(N) * 6
+    return orc.compute_normalization(normalize, loc, scl, ref_image=0)
+
+
+@pytest.mark.parametrize("N", [16, 17, 64, 300])
+@pytest.mark.parametrize("C", [1, 3])
+def test_median_hist(gpu_ctx, N, C):
+    H, W = 9, 300
+    frames = _frames(N, C, H, W, seed=N + C)
+    rc, ref = orc.stack_median(frames, max_thread=3)
+    assert rc == 0
+    out, _, _ = gpu_stack(gpu_ctx, frames, sg.MEDIAN, max_thread=3)
+    assert gpu_ctx.stats().path == 1
+    assert_same(out, ref, f"median N={N} C={C}")
+
+
+@pytest.mark.parametrize("normalize", [sg.ADDITIVE, sg.MULTIPLICATIVE, sg.ADDITIVE_SCALING,
+                                       sg.MULTIPLICATIVE_SCALING])
+def test_median_hist_normalised(gpu_ctx, normalize):
+    N, C, H, W = 33, 1, 12, 260
+    frames = _frames(N, C, H, W, seed=7)
+    off, mul, sc = _coeffs(normalize, N, seed=normalize)
+    rc, ref = orc.stack_median(frames, normalize, off, mul, sc, max_thread=2)
+    assert rc == 0
+    out, _, _ = gpu_stack(gpu_ctx, frames, sg.MEDIAN, normalize=normalize, offset=off, mul=mul, scale=sc,
+                          max_thread=2)
+    assert gpu_ctx.stats().path == 1
+    assert_same(out, ref, f"median norm={normalize}")
+
+
+@pytest.mark.parametrize("sig", [(0.2, 0.1), (0.0, 0.0), (0.05, 0.5), (1e9, 1e9), (-0.01, -0.02),
+                                 (float("nan"), 0.1)])
+@pytest.mark.parametrize("N", [16, 40, 129])
+def test_percentile_hist(gpu_ctx, sig, N):
+    """shifts (edge tiles, zero fill), median 0 columns, every-sample-rejected pixels (sig < 0
+    with an even N), NaN thresholds: result and counters == the oracle"""
+    C, H, W = 2, 28, 280      # blocks of 7 rows (4 threads): |shifty| below the block height (:1560)
+    frames = _frames(N, C, H, W, seed=3 * N)
+    sx, sy = orc.synth_shifts(N, seed=N, maxshift=6)
+    rc, ref, rej_ref = orc.stack_rejection(frames, sg.PERCENTILE, sig=sig, shiftx=sx, shifty=sy, max_thread=4)
+    assert rc == 0
+    out, rej, _ = gpu_stack(gpu_ctx, frames, sg.MEAN, sg.PERCENTILE, sig, sx, sy, max_thread=4)
+    assert gpu_ctx.stats().path == 1
+    assert_same(out, ref, f"percentile sig={sig} N={N}")
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+
+
+@pytest.mark.parametrize("normalize", [sg.ADDITIVE, sg.MULTIPLICATIVE, sg.ADDITIVE_SCALING,
+                                       sg.MULTIPLICATIVE_SCALING])
+def test_percentile_hist_normalised(gpu_ctx, normalize):
+    """normalised loads, including the border rows' normalised zeros (additive, ztab)"""
+    N, C, H, W = 24, 1, 20, 270
+    frames = _frames(N, C, H, W, seed=11)
+    sx, sy = orc.synth_shifts(N, seed=12, maxshift=5)
+    off, mul, sc = _coeffs(normalize, N, seed=20 + normalize)
+    sig = (0.1, 0.08)
+    rc, ref, rej_ref = orc.stack_rejection(frames, sg.PERCENTILE, sig=sig, shiftx=sx, shifty=sy,
+                                           normalize=normalize, offset=off, mul=mul, scale=sc, max_thread=2)
+    assert rc == 0
+    out, rej, _ = gpu_stack(gpu_ctx, frames, sg.MEAN, sg.PERCENTILE, sig, sx, sy, normalize=normalize, offset=off,
+                            mul=mul, scale=sc, max_thread=2)
+    assert_same(out, ref, f"percentile norm={normalize}")
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+
+
+@pytest.mark.parametrize("method,rejection", [(sg.MEAN, sg.SIGMA), (sg.MEAN, sg.WINSORIZED),
+                                              (sg.MEAN, sg.PERCENTILE), (sg.MEDIAN, sg.NO_REJEC)])
+def test_more_than_1024_frames(gpu_ctx, method, rejection):
+    """N = 2048 (beyond the sorted kernel's 1024): the histogram path runs and its redo pixels
+    (here: constant columns whose u8 bins overflow, far outliers) go to the replay / literal
+    kernels.  The reference sizes its buffers from N with no cap (:1486-1507)"""
+    N, C, H, W = 2048, 1, 16, 140
+    frames = _frames(N, C, H, W, seed=5, maxshift=3)
+    sx, sy = orc.synth_shifts(N, seed=5, maxshift=3)
+    sig = {sg.SIGMA: (3.0, 3.0), sg.WINSORIZED: (3.0, 3.0), sg.PERCENTILE: (0.2, 0.1), sg.NO_REJEC: (0, 0)}[rejection]
+    if method == sg.MEDIAN:
+        rc, ref = orc.stack_median(frames, max_thread=2)
+        rej_ref = np.zeros((3, 2), np.uint64)
+    else:
+        rc, ref, rej_ref = orc.stack_rejection(frames, rejection, sig=sig, shiftx=sx, shifty=sy, max_thread=2)
+    assert rc == 0
+    out, rej, _ = gpu_stack(gpu_ctx, frames, method, rejection, sig, sx, sy, max_thread=2)
+    assert gpu_ctx.stats().path == 1
+    assert_same(out, ref, f"N=2048 method={method} rej={rejection}")
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+
+
+def test_more_than_1024_frames_sorted_only_rejection_refused(gpu_ctx):
+    """SIGMEDIAN / LINEARFIT have no histogram path: beyond 1024 frames the call fails loudly"""
+    N, C, H, W = 1100, 1, 2, 64
+    frames = orc.synth(N, C, H, W, seed=1, maxshift=2)
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, C, rejection=sg.SIGMEDIAN)
+    rc, out, rej, _ = gpu_ctx.stack_host(desc, frames)
+    assert rc == -2 and "1024" in gpu_ctx.error()

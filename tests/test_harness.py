@@ -190,3 +190,136 @@ def test_cli_register_and_stack(tmp_path):
         got = s.read_frame(0)
     bad = np.argwhere(got != ref)
     assert len(bad) == 0, (len(bad), bad[:8].tolist(), r.stdout, rx.tolist(), ry.tolist())
+
+
+def _rej_logged(text, C):
+    """the per-channel rejection percentages the glue logs (:1811-1817 format)"""
+    import re
+    got = re.findall(r"Pixel rejection in channel #(\d+): ([0-9.]+)% - ([0-9.]+)%", text)
+    return [(float(a), float(b)) for _, a, b in got[-C:]]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devs", [[0, 0], [0, 0, 0]])
+def test_multi_device_slots_from_c(tmp_path, capfd, devs):
+    """the glue's context on several device slots (sg_init(ndev, {0, 0, ...}) on one card): every
+    slot stacks its share of the rows from its own host thread with its own readers.  SIGMA and
+    WINSORIZED rejection (result + logged rejection %), SUM with the 65535/max scaling over the
+    whole image (gfit.hi), MEDIAN with normalisation == the oracle; gfit.exposure = the EXPTIME
+    sum (EXPOSURE where EXPTIME is missing or <= 0, :1284-1294) for the rejection / median
+    stackers and readfits' carried value for the sum stackers"""
+    lib = hl.load()
+    N, C, H, W = 14, 3, 37, 70
+    frames = orc.synth(N, C, H, W, seed=33, maxshift=4)
+    sx, sy = orc.synth_shifts(N, seed=33, maxshift=4)
+    exptime = [("EXPTIME", f"{1.5 * (i + 1)}") if i % 4 else ("EXPOSURE", f"{2.0 + i}") for i in range(N)]
+    exptime[5] = ("EXPTIME", "0.")          # <= 0: the rejection stackers fall back to EXPOSURE
+    paths = []
+    for i in range(N):
+        p = str(tmp_path / f"m_{i + 1:05d}.fit")
+        keys = [exptime[i]] + ([("EXPOSURE", "7.25")] if i == 5 else [])
+        write_fits(p, frames[i], keys=keys)
+        paths.append(p)
+    exp_rej = sum(float(v) if not (k == "EXPTIME" and float(v) <= 0) else 7.25 for k, v in exptime)
+    exp_sum = sum(float(v) for k, v in exptime)      # readfits takes EXPTIME even at 0
+    try:
+        assert hl.set_devices(devs) == 0
+        lib.harness_set_max_thread(4)
+        with hl.Sequence.fits(paths) as seq:
+            seq.set_regdata(0, sx, sy)
+            lib.harness_set_registration_layer(0)
+            for rejection, sig in [(SIGMA, (3.0, 3.0)), (WINSORIZED, (2.5, 2.5))]:
+                capfd.readouterr()
+                assert lib.harness_stack(seq.h, MEAN, rejection, 0, sig[0], sig[1], 0, 0) == 0
+                out = capfd.readouterr().out
+                rc, ref, rej = orc.stack_rejection(frames, rejection, sig=sig, shiftx=sx, shifty=sy, max_thread=4)
+                assert np.array_equal(hl.gfit(), ref), rejection
+                nb_tot = float(W * H * N)
+                want = [(round(rej[c][0] / nb_tot * 100.0, 3), round(rej[c][1] / nb_tot * 100.0, 3)) for c in range(C)]
+                assert _rej_logged(out, C) == want, (out, want)
+                assert lib.harness_gfit_exposure() == pytest.approx(exp_rej, rel=0, abs=1e-9)
+            assert lib.harness_stack(seq.h, SUM, 0, 0, 0.0, 0.0, 0, 0) == 0
+            rc, ref, mref = orc.stack_sum(frames, sx, sy)
+            assert mref > 65535
+            assert np.array_equal(hl.gfit(), ref) and lib.harness_gfit_hi() == 65535
+            assert lib.harness_gfit_exposure() == pytest.approx(exp_sum, rel=0, abs=1e-9)
+            lib.harness_set_registration_layer(-1)
+            loc, scl = np.zeros(N), np.zeros(N)
+            for i in range(N):
+                _, loc[i], scl[i] = orc.statistics_ikss(frames[i])
+            off, mul, sc = orc.compute_normalization(2, loc, scl)
+            rc, ref = orc.stack_median(frames, normalize=2, offset=off, mul=mul, scale=sc, max_thread=4)
+            assert lib.harness_stack(seq.h, MEDIAN, 0, 2, 0.0, 0.0, 0, 0) == 0
+            assert np.array_equal(hl.gfit(), ref)
+    finally:
+        lib.harness_set_registration_layer(-1)
+        hl.set_devices(None)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devs", [None, [0, 0]])
+def test_register_cancel_from_c(tmp_path, devs):
+    """register_shift_dft with run_in_thread and get_thread_run() turning false after 3 polls:
+    the reference registers the frames polled before that (:281-285), still returns 0, keeps
+    the rest's regdata and skips normalizeQualityData (:166-168), so the registered frames keep
+    RAW qualities; the best frame is logged"""
+    lib = hl.load()
+    N, H, W, S = 9, 96, 128, 64
+    frames = _star_field(N, H, W, seed=17, maxshift=4)
+    x, y = (W - S) // 2, (H - S) // 2
+    m0 = H - y - S
+    sel = frames[:, 0, m0:m0 + S, x:x + S]
+    ref = 2
+    done = [0, 1, 3]                       # the first three frames polled (ref skipped, not polled)
+    inc = np.zeros(N, np.int32)
+    inc[done] = 1
+    rx, ry, _ = orc.register_dft(sel, ref_image=ref, included=inc)
+    p = str(tmp_path / "c.ser")
+    write_ser(p, frames, depth=16)
+    try:
+        if devs:
+            assert hl.set_devices(devs) == 0
+        with hl.Sequence.ser(p) as seq:
+            lib.harness_set_reference_image(seq.h, ref)
+            seq.set_regdata(0, np.full(N, 7), np.full(N, -7))     # earlier registration data
+            lib.harness_set_run_in_thread(1)
+            lib.harness_set_cancel_after(3)
+            rc = lib.harness_register(seq.h, 0, x, y, S, 1)
+            lib.harness_set_cancel_after(-1)
+            lib.harness_set_run_in_thread(0)
+            assert rc == 0
+            gx, gy, gq = seq.regdata(0, N)
+        for f in range(N):
+            if f in done or f == ref:
+                assert (gx[f], gy[f]) == ((rx[f], ry[f]) if f != ref else (0, 0)), f
+                assert gq[f] == orc.quality(sel[f]), f      # raw QualityEstimate
+            else:
+                assert (gx[f], gy[f]) == (7, -7), f         # kept
+    finally:
+        lib.harness_set_cancel_after(-1)
+        lib.harness_set_run_in_thread(0)
+        if devs:
+            hl.set_devices(None)
+
+
+@pytest.mark.gpu
+def test_register_best_frame_logged(tmp_path, capfd):
+    """the best frame (q_index, :315-324, logged :397) is the frame of highest quality"""
+    lib = hl.load()
+    N, H, W, S = 6, 96, 128, 64
+    frames = _star_field(N, H, W, seed=29, maxshift=3)
+    x, y = (W - S) // 2, (H - S) // 2
+    m0 = H - y - S
+    sel = frames[:, 0, m0:m0 + S, x:x + S]
+    q = [orc.quality(sel[f]) for f in range(N)]
+    want = 0
+    for f in range(1, N):
+        if q[f] > q[want]:
+            want = f
+    p = str(tmp_path / "b.ser")
+    write_ser(p, frames, depth=16)
+    with hl.Sequence.ser(p) as seq:
+        capfd.readouterr()
+        assert lib.harness_register(seq.h, 0, x, y, S, 1) == 0
+        out = capfd.readouterr().out
+    assert f"Best frame: #{want}." in out, out
