@@ -15,6 +15,8 @@ BASELINE.json metric.  Workloads (frames synthetic, include/sg_synth.h, generate
                    selection + WINSORIZED (4, 3).  At N GPUs: registration sharded over frames (each
                    rank its block + the reference, shifts all-gathered, normalizeQualityData over all
                    frames), the stack over row bands, output gathered to rank 0.
+  median           stack_median of the configs[2] frames (512 x 4096 x 4096 u16, registration ignored as
+                   the reference's :703-722 does): the histogram rank path (k_stack_hist<8>).
   sum-fits         configs[0]: stack_summing of 16 x 1024 x 1024 u16 FITS files, end to end from the
                    files (host-pull path: reads + PCIe + kernels), the CPU reference configuration.
 
@@ -36,7 +38,8 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", choices=["sigma", "register-mean", "winsorized-rgb", "sum-fits", "register-mean-file"],
+    ap.add_argument("--workload", choices=["sigma", "median", "register-mean", "winsorized-rgb", "sum-fits",
+                                           "register-mean-file"],
                     default="sigma",
                     help="sigma = BASELINE configs[2] (1 GPU) / configs[3] (N GPUs, default); register-mean = "
                          "configs[1]; winsorized-rgb = configs[4]; sum-fits = configs[0]")
@@ -108,9 +111,10 @@ def _omp_threads(n):
         pass
 
 
-def cpu_baseline(args, N, W):
-    """configs[2]: the oracle (C restatement of stack_mean_with_rejection, -O2 -fopenmp, the
-    reference's block partition and OpenMP schedule) on a bounded sample of the same workload"""
+def cpu_baseline(args, N, W, median=False):
+    """configs[2]: the oracle (C restatement of stack_mean_with_rejection / stack_median, -O2
+    -fopenmp, the reference's block partition and OpenMP schedule) on a bounded sample of the
+    same workload"""
     import oracle_lib as orc
     rows = min(args.cpu_rows, args.height)
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
@@ -119,15 +123,21 @@ def cpu_baseline(args, N, W):
     frames = orc.synth(N, 1, rows, W, seed=0x5151, maxshift=16)
     sx, sy = orc.synth_shifts(N, seed=0x5151, maxshift=16)
     t0 = time.perf_counter()
-    rc, out, rej = orc.stack_rejection(frames, 2, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
-                                       max_thread=threads, max_number_of_rows=rows)
+    if median:
+        rc, out = orc.stack_median(frames, max_thread=threads, max_number_of_rows=rows)
+        what = "stack_median"
+    else:
+        rej_mode = {"sigma": 2, "winsorized": 4, "none": 0, "percentile": 1}[args.rejection]
+        rc, out, rej = orc.stack_rejection(frames, rej_mode, sig=(4.0, 3.0) if rej_mode != 1 else (0.2, 0.1),
+                                           shiftx=sx, shifty=sy, max_thread=threads, max_number_of_rows=rows)
+        what = f"stack_mean_with_rejection {args.rejection}"
     dt = time.perf_counter() - t0
     del frames
     frac = rows / args.height
     return {"value": round(N * frac / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(),
-            "sample": f"oracle stack_mean_with_rejection SIGMA(4,3), {N} frames x {rows} rows x {W} "
-                      f"cols ({threads} OpenMP threads); frames/s scaled by {rows}/{args.height} rows",
+            "sample": f"oracle {what}, {N} frames x {rows} rows x {W} cols ({threads} OpenMP threads), "
+                      f"timed on {rows} of {args.height} rows; frames/s = {N} x {rows}/{args.height} / seconds",
             "seconds": round(dt, 3), "rc": rc}
 
 
@@ -277,6 +287,9 @@ def main_sigma(args):
     N, W, H = args.frames, args.width, args.height
     rej_mode = {"sigma": sg.SIGMA, "winsorized": sg.WINSORIZED, "none": sg.NO_REJEC,
                 "percentile": sg.PERCENTILE}[args.rejection]
+    median = args.workload == "median"
+    method = sg.MEDIAN if median else sg.MEAN
+    sig = (0.2, 0.1) if rej_mode == sg.PERCENTILE else (4.0, 3.0)
     ctx = sg.Context([dev])
     strong = args.scaling == "strong" or world == 1
     # strong: one sequence of N frames of H x W in `world` row bands; weak: one sequence of
@@ -289,7 +302,10 @@ def main_sigma(args):
     if args.zero_shift:
         (shx if args.zero_shift == "x" else shy)[:] = 0
     b, e = sd.row_band(rank, world, H) if strong else (rank * H, (rank + 1) * H)
-    lo, hi = max(0, b - int(shy.max())), min(Htot - 1, e - 1 - int(shy.min()))
+    if median:      # stack_median ignores the registration shifts (:703-722): the band's own rows
+        lo, hi = b, e - 1
+    else:
+        lo, hi = max(0, b - int(shy.max())), min(Htot - 1, e - 1 - int(shy.min()))
     nres = hi - lo + 1
     fstride = nres * W + args.frame_pad
     frames = torch.empty(N * fstride, dtype=torch.int16, device="cuda")
@@ -315,7 +331,7 @@ def main_sigma(args):
         else:
             norm_mode = sg.MULTIPLICATIVE_SCALING
             mul = loc[0] / loc
-    desc, keep = sg.make_desc(sg.MEAN, N, W, Htot, 1, rejection=rej_mode, sig=(4.0, 3.0),
+    desc, keep = sg.make_desc(method, N, W, Htot, 1, rejection=rej_mode if not median else sg.NO_REJEC, sig=sig,
                               shiftx=shx, shifty=shy, normalize=norm_mode, offset=off, mul=mul, scale=scale,
                               max_thread=8, max_number_of_rows=Htot, resident_rows=(lo, hi + 1))
     torch.cuda.synchronize()
@@ -343,15 +359,17 @@ def main_sigma(args):
     algo_bytes = N * (e - b) * W * 2 + (e - b) * W * 2     # this rank's launch: its band's samples + output
     achieved = algo_bytes / (kavg * 1e-3) / 1e9
     if rank == 0:
+        kind = "median stack" if median else f"{args.rejection} rejection stack"
         if world == 1:
-            workload = f"sigma-clip stack {N}x{H}x{W} u16 mono (BASELINE configs[2])"
+            workload = (f"{kind} {N}x{H}x{W} u16 mono (BASELINE configs[2] frames)" if median or args.rejection != "sigma"
+                        else f"sigma-clip stack {N}x{H}x{W} u16 mono (BASELINE configs[2])")
             par = "1 GPU"
         elif strong:
-            workload = (f"sigma-clip stack {N}x{H}x{W} u16 mono in {world} row bands of {hband} rows, output "
+            workload = (f"{kind} {N}x{H}x{W} u16 mono in {world} row bands of {hband} rows, output "
                         f"gathered to rank 0 (BASELINE configs[3])")
             par = f"row-band x{world}, RCCL gather"
         else:
-            workload = f"sigma-clip stack {N}x{H}x{W} u16 mono per GPU, one {N}x{Htot}x{W} sequence in {world} bands"
+            workload = f"{kind} {N}x{H}x{W} u16 mono per GPU, one {N}x{Htot}x{W} sequence in {world} bands"
             par = f"row-band x{world} (weak)"
         res = {
             "metric": "frames/sec stacked (4096x4096 u16, sigma-clip) + achieved HBM GB/s",
@@ -366,10 +384,11 @@ def main_sigma(args):
             "vs_baseline": None,
             "dtype": "u16",
             "data": "synthetic (include/sg_synth.h, generated in HBM)",
-            "config": {"workload": workload, "frames": N, "height": H, "width": W, "rejection": args.rejection,
-                       "sig": [4.0, 3.0], "normalize": args.normalize, "parallelism": par},
-            "roofline": roofline(achieved, algo_bytes, N, H, W, args.rejection
-                                 if args.normalize == "none" else f"{args.rejection}_{args.normalize}",
+            "config": {"workload": workload, "frames": N, "height": H, "width": W,
+                       "method": "median" if median else "mean", "rejection": "none" if median else args.rejection,
+                       "sig": list(sig), "normalize": args.normalize, "parallelism": par},
+            "roofline": roofline(achieved, algo_bytes, N, H, W, ("median" if median else args.rejection)
+                                 if args.normalize == "none" else f"{'median' if median else args.rejection}_{args.normalize}",
                                  with_traffic=world == 1),
             "kernel_ms": round(kavg, 3),
             "slow_pixels": int(st.slow_pixels),
@@ -380,7 +399,7 @@ def main_sigma(args):
             res["per_rank_kernel_ms"] = [round(x, 3) for x in per_rank_kms]
             res["rows_per_rank"] = e - b
         if not args.no_cpu_baseline and world == 1:
-            res["cpu_baseline"] = cpu_baseline(args, N, W)
+            res["cpu_baseline"] = cpu_baseline(args, N, W, median)
         print(json.dumps(res), flush=True)
     ctx.close()
     D.close()
@@ -655,7 +674,7 @@ def main_register_file(args):
 
 def main():
     args = parse()
-    if args.workload == "sigma":
+    if args.workload in ("sigma", "median"):
         return main_sigma(args)
     if args.workload == "sum-fits":
         return main_sum(args)

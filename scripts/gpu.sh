@@ -38,7 +38,7 @@ for step in "$@"; do
   [ "$kind" = "$step" ] && spec=""
   case $kind in
     test|testall)
-      k=(); [ -n "$spec" ] && k=(-k "$spec")
+      k=(); [ -n "$spec" ] && k=(-k "${spec//,/ }")   # commas between the words of a -k expression
       x=-x; [ "$kind" = testall ] && x=--maxfail=8
       lim=900; [ -n "$spec" ] && lim=300     # a selection runs under a shorter limit
       timeout -k 10 $lim python -u -m pytest tests -m gpu $x -v --timeout 200 --timeout-method thread "${k[@]}" \

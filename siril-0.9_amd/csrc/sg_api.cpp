@@ -41,6 +41,8 @@ __global__ void k_redo_to_literal(SgStackParams p, const unsigned int *list, con
 		unsigned int maxn);
 __global__ void k_stack_reduce(SgStackParams p);
 __global__ void k_stack_reduce2(SgStackParams p);
+template <int M>
+__global__ void k_stack_reduce3(SgStackParams p, const int *tab, const int *shifty);
 __global__ void k_sum_finalize(SgStackParams p);
 __global__ void k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *scratch, int phase);
 __global__ void k_synth_fill(uint16_t *frames, int first_frame, int nframes, int C, int H, int W, int row_begin,
@@ -643,9 +645,18 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			 * of rows near the frame border) goes through the sorted kernel, 64 pixels per
 			 * workgroup, once the count is back (measured: 22 k pixels faster in the replay,
 			 * 113 k slower) */
-			/* N > 1024 (no sorted kernel): every redo pixel goes to the replay / literal kernels */
+			/* N > 1024 (no sorted kernel): every redo pixel goes to the replay / literal kernels.
+			 * stack_median / PERCENTILE: the sorted kernel takes up to SG_REDO_REPLAY_MAX listed
+			 * pixels straight away (its grid idles past the device-side count; the literal
+			 * kernel's one thread per pixel sorts slowly: 740 pixels took 8 ms) */
+			const bool sorted_redo = nreg && (d->method == SG_STACK_MEDIAN || p.rejection == SG_PERCENTILE);
 			const bool dev_route = (N <= SG_REPLAY_MAXN && ctx->knobs.redo_replay) || !nreg;
-			if (dev_route) {
+			if (sorted_redo) {
+				HIPCHK(launch_sorted(nreg, true, dim3(SG_REDO_REPLAY_MAX / SG_TILE_W), lds, s, p, redo_list, redo_count));
+				st.launches++;
+				late_redo = redo_count;
+				late_list = redo_list;
+			} else if (dev_route) {
 				hipLaunchKernelGGL(k_redo_to_literal, dim3(64), dim3(256), 0, s, p, (const unsigned int *)redo_list,
 						(const unsigned int *)redo_count, nreg ? (unsigned int)SG_REDO_REPLAY_MAX : 0xFFFFFFFFu);
 				HIPCHK(hipGetLastError());
@@ -726,16 +737,28 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		}
 		dim3 grid((W + 255) / 256, nrows, C);
 		/* pixel pairs per lane (dword loads) unless a plane is too large for a 31-bit offset */
-		const bool pairs = W >= 2 && (uint64_t)W * (uint64_t)H * 2u < (1ull << 31) && !ctx->knobs.reduce1;
+		const bool pairs = W >= 2 && (uint64_t)W * (uint64_t)H * 2u < (1ull << 31) && ctx->knobs.reduce1 != 1;
 		const dim3 grid2(((W + 1) / 2 + 255) / 256, nrows, C);
+		/* XCD-aware SGPR-offset loads (k_stack_reduce3) when the shifted row offsets fit 32 bits,
+		 * the per-lane pair kernel (SG_REDUCE1=2, A/B) otherwise */
+		const bool r3 = pairs && hist_addr_ok && ctx->knobs.reduce1 == 0;
+		const unsigned nb3 = (unsigned)(((W + 511) / 512) * (size_t)nrows * C);
 		HIPCHK(hipEventRecord(dv.ev[0], s));
-		if (pairs)
+		if (r3) {
+			switch (d->method) {
+			case SG_STACK_SUM: hipLaunchKernelGGL(k_stack_reduce3<0>, dim3(nb3), dim3(256), 0, s, p, p.hist_tab, p.shifty); break;
+			case SG_STACK_MEAN: hipLaunchKernelGGL(k_stack_reduce3<1>, dim3(nb3), dim3(256), 0, s, p, p.hist_tab, p.shifty); break;
+			case SG_STACK_MAX: hipLaunchKernelGGL(k_stack_reduce3<3>, dim3(nb3), dim3(256), 0, s, p, p.hist_tab, p.shifty); break;
+			default: hipLaunchKernelGGL(k_stack_reduce3<4>, dim3(nb3), dim3(256), 0, s, p, p.hist_tab, p.shifty); break;
+			}
+		} else if (pairs) {
 			hipLaunchKernelGGL(k_stack_reduce2, grid2, dim3(256), 0, s, p);
-		else
+		} else {
 			hipLaunchKernelGGL(k_stack_reduce, grid, dim3(256), 0, s, p);
+		}
 		HIPCHK(hipGetLastError());
 		HIPCHK(hipEventRecord(dv.ev[1], s));
-		st.main_kernel_blocks = pairs ? (int)(grid2.x * grid2.y * grid2.z) : (int)(grid.x * grid.y * grid.z);
+		st.main_kernel_blocks = r3 ? (int)nb3 : pairs ? (int)(grid2.x * grid2.y * grid2.z) : (int)(grid.x * grid.y * grid.z);
 		st.launches = 1;
 		if (d->method == SG_STACK_SUM && (sum_mode == SUM_WHOLE || sum_mode == SUM_LAST_BAND)) {
 			/* the 65535/max scaling (:328-342) needs the maximum over the whole image: a

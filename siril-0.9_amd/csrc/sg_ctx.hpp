@@ -84,7 +84,7 @@ struct SgKnobs {
 	int hist_ni = 1;		/* SG_HIST_NI: pixel pairs per lane of the histogram tiles (2: 256-px tiles) */
 	int wins_cap = 64;		/* SG_WINS_CAP: histogram Winsorize inner iterations per pass before the redo list */
 	int redo_replay = 1;		/* SG_REDO_REPLAY: 0 = redo list always through the sorted kernel */
-	int reduce1 = 0;		/* SG_REDUCE1: 1 = one pixel per lane in the SUM/MAX/MIN/MEAN reduce */
+	int reduce1 = 0;		/* SG_REDUCE1: 1 = one pixel per lane, 2 = the per-lane pixel-pair kernel, in the SUM/MAX/MIN/MEAN reduce (A/B) */
 	long long host_budget = 0;	/* SG_HOST_BUDGET_BYTES: host-pull HBM budget (0 = 85 % of free HBM) */
 	int qsub_threads = 64;		/* SG_QSUB_THREADS: 64 measured best (scripts/gpu_qsub.sh) */
 	int qgrad_threads = 128;	/* SG_QGRAD_THREADS: 128 measured best (scripts/gpu_qgrad.sh) */
@@ -104,7 +104,7 @@ struct SgKnobs {
 		hist_ni = sg_env_int("SG_HIST_NI", 1, 2, 1);
 		wins_cap = sg_env_int("SG_WINS_CAP", 4, 100000, 64);
 		redo_replay = sg_env_int("SG_REDO_REPLAY", 0, 1, 1);
-		reduce1 = sg_env_int("SG_REDUCE1", 0, 1, 0);
+		reduce1 = sg_env_int("SG_REDUCE1", 0, 2, 0);
 		if (const char *e = getenv("SG_HOST_BUDGET_BYTES"))
 			host_budget = atoll(e) > 0 ? atoll(e) : 0;
 		const int qs = sg_env_int("SG_QSUB_THREADS", 64, 1024, 64);

@@ -458,8 +458,11 @@ k_stack_sorted(SgStackParams p, const unsigned int *__restrict__ list, const uns
 	const int N = p.N;
 	int c0 = 0;
 	if (LISTED) {
-		/* redo list of the histogram path: slot i = pixel list[64 * block + i] */
+		/* redo list of the histogram path: slot i = pixel list[64 * block + i]; a grid sized
+		 * for the longest list the device routes itself leaves its blocks past the count idle */
 		const unsigned int count = *list_count;
+		if ((unsigned int)blockIdx.x * SG_TILE_W >= count)
+			return;
 		if (tid < SG_TILE_W) {
 			const unsigned int k = blockIdx.x * SG_TILE_W + tid;
 			if (k < count) {
@@ -700,16 +703,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t sg_plane_rsrc(const uint16_t *
 	return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)nrec, 0x00020000);
 }
 
-__global__ void __launch_bounds__(256)
-k_stack_reduce2(SgStackParams p) {
-	const int x = 2 * (blockIdx.x * 256 + threadIdx.x);
-	const int R = p.row_begin + blockIdx.y;
-	const int c = blockIdx.z;
+/* the per-lane pixel-pair loop of the general path: any shift, the image edges, the masks of
+ * every method */
+__device__ __forceinline__ void sg_reduce_pairs(const SgStackParams &p, int x, int R, int c, uint32_t &acc_a,
+		uint32_t &acc_b) {
 	const bool live_a = x < p.W, live_b = x + 1 < p.W;
 	const uint16_t *plane = p.frames + (int64_t)c * p.plane_stride;
 	const uint32_t nrec = (uint32_t)p.H * (uint32_t)p.W * 2u;
 	const int N = p.N;
-	uint32_t acc_a = (p.method == 4) ? 65535u : 0u, acc_b = acc_a;
 	/* shifts of 64 frames at a time: one vector load per wave (lane l = frame f0 + l), read
 	 * back per frame with readlane, so a batch's sample loads do not wait on 32 scalar loads */
 	int vsx = 0, vsy = 0;
@@ -779,6 +780,13 @@ k_stack_reduce2(SgStackParams p) {
 			}
 		}
 	}
+}
+
+/* the pair's results: MEAN round_to_WORD(sum / N) (:1790-1794), SUM raw sums + the maximum
+ * (scaled by k_sum_finalize, :328-342), MAX / MIN the extremum */
+__device__ __forceinline__ void sg_reduce_store(const SgStackParams &p, int x, int R, int c, uint32_t acc_a,
+		uint32_t acc_b) {
+	const bool live_a = x < p.W, live_b = x + 1 < p.W;
 	unsigned int blockmax = 0;
 	const int64_t pix = ((int64_t)c * p.H + R) * p.W + x;
 	for (int k = 0; k < 2; k++) {
@@ -786,7 +794,7 @@ k_stack_reduce2(SgStackParams p) {
 			continue;
 		const uint32_t acc = k ? acc_b : acc_a;
 		if (p.method == 1) {
-			p.out[pix + k] = sg_round_to_WORD((double)acc / (double)N);
+			p.out[pix + k] = sg_round_to_WORD((double)acc / (double)p.N);
 		} else if (p.method == 0) {
 			p.sum_buf[pix + k] = acc;
 			blockmax = acc > blockmax ? acc : blockmax;
@@ -803,6 +811,147 @@ k_stack_reduce2(SgStackParams p) {
 			atomicMax(p.maxim, blockmax);
 	}
 }
+
+__global__ void __launch_bounds__(256)
+k_stack_reduce2(SgStackParams p) {
+	const int x = 2 * (blockIdx.x * 256 + threadIdx.x);
+	const int R = p.row_begin + blockIdx.y;
+	const int c = blockIdx.z;
+	uint32_t acc_a = (p.method == 4) ? 65535u : 0u, acc_b = acc_a;
+	sg_reduce_pairs(p, x, R, c, acc_a, acc_b);
+	sg_reduce_store(p, x, R, c, acc_a, acc_b);
+}
+
+/*
+ * k_stack_reduce3: the same reductions with the loads of k_stack_hist.  A workgroup of 4 waves
+ * takes a 512-pixel segment of one row (a lane a pixel pair, a wave 128 pixels); workgroups are dealt XCD-aware
+ * (each XCD gets contiguous whole rows, so the 128-B lines a shifted row segment straddles are
+ * fetched once into that XCD's L2 and shared by the neighbouring segment).  In an interior
+ * segment (no shifted column can leave the image, and none reaches source pixel 0) a frame's
+ * shifted row segment start is one SGPR offset, (R W + x0) 2 - c1[f] with c1 = shifty W 2 +
+ * 2 shiftx from the call's shift table (scalar loads), so a load costs no VALU; a row shifted
+ * out of the frame reads 0 from the buffer bounds check (gfx950 checks voffset + soffset
+ * unsigned, so a negative start is out of range too).  SUM and MEAN add 0 for such rows (the
+ * reference's zero fill, normalised for MEAN), MAX ignores them, MIN skips them (a uniform
+ * test of the frame's shifty).  Two 16-frame register buffers per lane.  Other segments take the
+ * general per-lane loop (sg_reduce_pairs).  M: 0 SUM, 1 MEAN, 3 MAX, 4 MIN.
+ */
+template <int M>
+__global__ void __launch_bounds__(256)
+k_stack_reduce3(SgStackParams p, const int *__restrict__ tab, const int *__restrict__ shifty) {
+	const int nblk = (int)gridDim.x, xcd = (int)blockIdx.x & 7, q = nblk >> 3, rem = nblk & 7;
+	const int vb = xcd * q + (xcd < rem ? xcd : rem) + ((int)blockIdx.x >> 3);
+	const int bpr = (p.W + 511) >> 9;
+	const int nrows = p.row_end - p.row_begin;
+	const int xt = vb % bpr, rr = vb / bpr;
+	const int R = p.row_begin + rr % nrows, c = rr / nrows;
+	/* each wave its own 128-pixel segment: only the segments at the image edges take the
+	 * general loop */
+	const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+	const int x0 = xt * 512 + 128 * wave;
+	const int x = xt * 512 + 2 * (int)threadIdx.x;
+	const bool interior = x0 > p.hist_maxsx && x0 + 128 + p.hist_maxsx <= p.W;
+	uint32_t acc_a = M == 4 ? 65535u : 0u, acc_b = acc_a;
+	if (!interior) {
+		sg_reduce_pairs(p, x, R, c, acc_a, acc_b);
+		sg_reduce_store(p, x, R, c, acc_a, acc_b);
+		return;
+	}
+	const int N = p.N;
+	const char *plane = (const char *)(p.frames + (int64_t)c * p.plane_stride);
+	const uint32_t nrec = (uint32_t)p.H * (uint32_t)p.W * 2u;
+	const int rowb = (R * p.W + x0) * 2;
+	const int vofs = ((int)threadIdx.x & 63) * 4;
+	uint32_t mm = M == 4 ? 0xFFFFFFFFu : 0u;	/* MAX / MIN: both pixels packed */
+	const int64_t fstride2 = p.frame_stride * 2;
+	const int lane = threadIdx.x & 63;
+	int vsy = 0;	/* MIN: shifty of frames f0 + lane (64 at a time), read back with readlane */
+	/* 16 frames: their c1 (scalar loads; the table is zero padded to a multiple of 16 frames),
+	 * then one load per frame; frames past N read nothing */
+	auto load16 = [&](int f0, uint32_t (&v)[16]) {
+		int c1[16];
+		const int *t = tab + __builtin_amdgcn_readfirstlane(f0);
+#pragma unroll
+		for (int i = 0; i < 16; i++)
+			c1[i] = t[i];
+		const char *fb = plane + (int64_t)f0 * fstride2;
+#pragma unroll
+		for (int m = 0; m < 16; m++) {
+			const uint32_t n = f0 + m < N ? nrec : 0u;
+			v[m] = __builtin_amdgcn_raw_buffer_load_b32(sg_plane_rsrc((const uint16_t *)(fb + (int64_t)m * fstride2), n),
+					vofs, rowb - c1[m], 0);
+		}
+	};
+	auto acc16 = [&](int f0, const uint32_t (&v)[16], bool full) {
+		if (M == 4 && p.use_shift && (f0 & 63) == 0)
+			vsy = shifty[f0 + lane < N ? f0 + lane : N - 1];
+#pragma unroll
+		for (int m = 0; m < 16; m++) {
+			const int f = f0 + m;
+			if (!full && f >= N)
+				continue;
+			const uint32_t a = v[m] & 0xFFFFu, b = v[m] >> 16;
+			if (M == 0) {
+				acc_a += a;
+				acc_b += b;
+			} else if (M == 1) {
+				if (p.normalize) {	/* the zero fill of a row shifted out is normalised too */
+					acc_a += sg_normalize(p, f, (uint16_t)a);
+					acc_b += sg_normalize(p, f, (uint16_t)b);
+				} else {
+					acc_a += a;
+					acc_b += b;
+				}
+			} else if (M == 3) {
+				mm = __builtin_bit_cast(uint32_t,
+						__builtin_elementwise_max(__builtin_bit_cast(sg_u16x2, mm), __builtin_bit_cast(sg_u16x2, v[m])));
+			} else {
+				const int sy = p.use_shift ? __builtin_amdgcn_readlane(vsy, (f0 & 63) + m) : 0;
+				if ((unsigned)(R - sy) < (unsigned)p.H)
+					mm = __builtin_bit_cast(uint32_t,
+							__builtin_elementwise_min(__builtin_bit_cast(sg_u16x2, mm), __builtin_bit_cast(sg_u16x2, v[m])));
+			}
+		}
+	};
+	/* two 16-frame register buffers: the next block's loads are issued before this block is
+	 * accumulated; the steady loop is straight-line code with sched_barriers (the compiler
+	 * otherwise interleaves the accumulation with the loads, and conditional loads make its
+	 * vmcnt waits drain the block in flight) */
+	uint32_t bufa[16], bufb[16];
+	load16(0, bufa);
+	int f0 = 0;
+	while (f0 + 48 <= N) {
+		load16(f0 + 16, bufb);
+		__builtin_amdgcn_sched_barrier(0);
+		acc16(f0, bufa, true);
+		__builtin_amdgcn_sched_barrier(0);
+		load16(f0 + 32, bufa);
+		__builtin_amdgcn_sched_barrier(0);
+		acc16(f0 + 16, bufb, true);
+		__builtin_amdgcn_sched_barrier(0);
+		f0 += 32;
+	}
+	/* the last one to three blocks, with bounds */
+	if (f0 + 16 < N)
+		load16(f0 + 16, bufb);
+	acc16(f0, bufa, f0 + 16 <= N);
+	if (f0 + 16 < N) {
+		if (f0 + 32 < N)
+			load16(f0 + 32, bufa);
+		acc16(f0 + 16, bufb, f0 + 32 <= N);
+		if (f0 + 32 < N)
+			acc16(f0 + 32, bufa, f0 + 48 <= N);
+	}
+	if (M == 3 || M == 4) {
+		acc_a = mm & 0xFFFFu;
+		acc_b = mm >> 16;
+	}
+	sg_reduce_store(p, x, R, c, acc_a, acc_b);
+}
+template __global__ void k_stack_reduce3<0>(SgStackParams, const int *, const int *);
+template __global__ void k_stack_reduce3<1>(SgStackParams, const int *, const int *);
+template __global__ void k_stack_reduce3<3>(SgStackParams, const int *, const int *);
+template __global__ void k_stack_reduce3<4>(SgStackParams, const int *, const int *);
 
 /* SUM finalisation: out = round_to_WORD(sum) or round_to_WORD(sum * 65535/maxim) (:328-342) */
 __global__ void __launch_bounds__(256)

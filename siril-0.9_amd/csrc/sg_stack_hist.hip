@@ -95,6 +95,7 @@ template <int NI>
 struct alignas(16) SghLds {
 	uint32_t h[2 * NI][SGH_HROWS][64];
 	uint32_t nz[128 * NI], ns[128 * NI];	/* zeros / 65535s (all of them lie outside the band) */
+	uint32_t na[128 * NI];			/* samples above the band (stack_median / PERCENTILE kernels only) */
 	uint32_t lo2[NI][64];			/* band starts of the lane pixel pairs (u16 halves) */
 	uint32_t cs[NI][8][64];			/* wave 1's first 8 frames for the band centre (SGH_CENTER2W) */
 	uint8_t perm[128];			/* WINSORIZED finish order of the columns (SGH_WINS_ORDER) */
@@ -300,6 +301,26 @@ __device__ __forceinline__ int sgh_locate(const SghPix &P, int g, const uint32_t
  * in the same band group */
 __device__ __forceinline__ void sgh_value_at2(const SghPix &P, int g1, int g2, int &m1, int &m2) {
 	const int r1 = g1 - P.nz, r2 = g2 - P.nz;
+	const bool in1 = r1 >= 0 && r1 < P.nb, in2 = r2 >= 0 && r2 < P.nb;
+	const int grp1 = sgh_grp_of(P, r1), grp2 = sgh_grp_of(P, r2);
+	uint32_t d[SGH_GRP];
+	sgh_grp(P, grp1, d);
+	const uint32_t base1 = sgh_pre(P, P.pc, grp1);
+	m1 = in1 ? sgh_locate(P, grp1, d, base1, (uint32_t)r1) : (r1 < 0 ? 0 : 65535);
+	if (in2 && grp2 == grp1) {
+		m2 = sgh_locate(P, grp1, d, base1, (uint32_t)r2);
+	} else if (in2) {
+		sgh_grp(P, grp2, d);
+		m2 = sgh_locate(P, grp2, d, sgh_pre(P, P.pc, grp2), (uint32_t)r2);
+	} else {
+		m2 = r2 < 0 ? 0 : 65535;
+	}
+}
+
+/* sgh_value_at2 with nbl samples below the band (a rank below them reads 0, one past the band
+ * 65535: the caller has checked those samples are zeros / 65535s) */
+__device__ __forceinline__ void sgh_value_at2n(const SghPix &P, int nbl, int g1, int g2, int &m1, int &m2) {
+	const int r1 = g1 - nbl, r2 = g2 - nbl;
 	const bool in1 = r1 >= 0 && r1 < P.nb, in2 = r2 >= 0 && r2 < P.nb;
 	const int grp1 = sgh_grp_of(P, r1), grp2 = sgh_grp_of(P, r2);
 	uint32_t d[SGH_GRP];
@@ -581,10 +602,18 @@ __device__ __forceinline__ uint32_t sgh_opaque(uint32_t k) {
 	asm volatile("s_mov_b32 %0, %1" : "=s"(r) : "i"(k));
 	return r;
 }
+/* AB (stack_median / PERCENTILE kernels): also count the samples above the band, min(sat(v - hi), 1)
+ * per half with hi = lo + 255, so the finish can place ranks and counts beside out-of-band samples
+ * other than 0 / 65535 (unregistered stars in a median stack) */
+template <bool AB = false>
 __device__ __forceinline__ void sgh_bin_pair(uint32_t *h, uint32_t l4, uint32_t lo2, uint32_t vv,
-		uint32_t &nonzero, uint32_t &nsat, uint32_t k1 = 0x00010001u, uint32_t ksat = 0xFFFEFFFEu) {
+		uint32_t &nonzero, uint32_t &nsat, uint32_t k1 = 0x00010001u, uint32_t ksat = 0xFFFEFFFEu,
+		uint32_t *nab = nullptr, uint32_t hi2 = 0u) {
 #if !SGH_BIN_ASM
 	const sgh_u16x2 v16 = __builtin_bit_cast(sgh_u16x2, vv);
+	if (AB)
+		*nab += __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_elementwise_sub_sat(v16,
+				__builtin_bit_cast(sgh_u16x2, hi2)), __builtin_bit_cast(sgh_u16x2, k1)));
 	const sgh_u16x2 tt = __builtin_elementwise_min(v16 - __builtin_bit_cast(sgh_u16x2, lo2), (sgh_u16x2){256, 256});
 	const uint32_t t64 = __builtin_bit_cast(uint32_t, (sgh_u16x2)(tt << (sgh_u16x2){6, 6}));
 	const uint32_t t8 = __builtin_bit_cast(uint32_t, (sgh_u16x2)(tt << (sgh_u16x2){3, 3}));
@@ -613,8 +642,9 @@ __device__ __forceinline__ void sgh_bin_pair(uint32_t *h, uint32_t l4, uint32_t 
 /* two frames of one pixel pair, their independent packed ops interleaved: a packed op that
  * reads the previous op's result needs a wait state (s_nop) on gfx950, the other frame's op
  * fills it */
+template <bool AB = false>
 __device__ __forceinline__ void sgh_bin_pair2(uint32_t *h, uint32_t l4, uint32_t lo2, uint32_t va, uint32_t vb,
-		uint32_t &nonzero, uint32_t &nsat, uint32_t k1, uint32_t ksat) {
+		uint32_t &nonzero, uint32_t &nsat, uint32_t k1, uint32_t ksat, uint32_t *nab = nullptr, uint32_t hi2 = 0u) {
 	const sgh_u16x2 a16 = __builtin_bit_cast(sgh_u16x2, va), b16 = __builtin_bit_cast(sgh_u16x2, vb);
 	const sgh_u16x2 l16 = __builtin_bit_cast(sgh_u16x2, lo2), c256 = {256, 256};
 	/* sched_barriers between the stages: the scheduler otherwise serialises the two frames again
@@ -638,6 +668,11 @@ __device__ __forceinline__ void sgh_bin_pair2(uint32_t *h, uint32_t l4, uint32_t
 		__builtin_bit_cast(uint32_t, __builtin_elementwise_min(b16, k1v));
 	nsat += __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(a16, ksv)) +
 		__builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(b16, ksv));
+	if (AB) {
+		const sgh_u16x2 hv = __builtin_bit_cast(sgh_u16x2, hi2);
+		*nab += __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_elementwise_sub_sat(a16, hv), k1v)) +
+			__builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_elementwise_sub_sat(b16, hv), k1v));
+	}
 }
 
 /* ------------------------------------------------------------------------------------
@@ -1284,13 +1319,24 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
  * a count landing among them is not decided here (redo).
  */
 template <int REJ, bool ZT>
-__device__ __forceinline__ int sgh_median_pct(const SghPix &P, int N, double sl, double sh, uint16_t *value,
-		uint32_t *rlo, uint32_t *rhi) {
+__device__ __forceinline__ int sgh_median_pct(const SghPix &P, int N, double sl, double sh, int nbl, bool cleanB,
+		bool cleanA, uint16_t *value, uint32_t *rlo, uint32_t *rhi) {
+	/* nbl samples lie below the band (cleanB: all of them zeros, or this row's normalised
+	 * zeros under ZT), N - nbl - nb above it (cleanA: all 65535).  A rank among the below- or
+	 * above-band samples is decided here only when they are clean (a normalised-zero rank
+	 * never: those values are not in the histogram) */
+	auto rank_ok = [&](int g) {
+		return g >= nbl ? (g < nbl + P.nb || cleanA) : (cleanB && !(ZT && P.zmax > 0));
+	};
+	auto value_at = [&](int g, int &v1) {	/* single rank, the band group read once */
+		int x2;
+		sgh_value_at2n(P, nbl, g, g, v1, x2);
+	};
 	const int g1 = (N - 1) / 2, g2 = N / 2;
-	if (ZT && P.zmax > 0 && g1 < P.nz)
+	if (!rank_ok(g1) || !rank_ok(g2))
 		return SG_CLS_LITERAL;
 	int m1, m2;
-	sgh_value_at2(P, g1, g2, m1, m2);
+	sgh_value_at2n(P, nbl, g1, g2, m1, m2);
 	if (REJ == 8) {
 		*value = (uint16_t)((m1 + m2) >> 1);	/* (WORD)((a + b) / 2.0): truncation of a half-integer */
 		return SG_CLS_OK;
@@ -1313,21 +1359,33 @@ __device__ __forceinline__ int sgh_median_pct(const SghPix &P, int N, double sl,
 	while (U <= 65535 && !phi(U))
 		U++;
 	const int Uh = U > L + 1 ? U : L + 1;
+	/* the counts at L and Uh - 1 and the kept samples' sum are exact when no below-band sample
+	 * of unknown value can be kept or counted apart (L >= lo - 1, or the below-band samples are
+	 * clean) and likewise above the band; normalised zeros straddling a threshold are not */
+	if ((!cleanB && L < P.lo - 1) || (!cleanA && Uh - 1 > P.lo + 255))
+		return SG_CLS_LITERAL;
 	if (ZT && P.zmax > 0 && ((L >= 0 && L < P.zmax) || (Uh - 1 >= 0 && Uh - 1 < P.zmax)))
 		return SG_CLS_LITERAL;
 	SghQ qa, qb;
 	sgh_q_load(P, L, qa);
 	sgh_q_load(P, Uh - 1, qb);
-	const int nlow = sgh_q_count(P, qa), nle = sgh_q_count(P, qb);
+	auto count = [&](const SghQ &q) {
+		return q.v < 0 ? 0 : (q.v >= 65535 ? N : nbl + (int)(sgh_pre(P, P.pc, q.g) + q.cp));
+	};
+	const int nlow = count(qa), nle = count(qb);
 	const int nhigh = N - nle, kept = nle - nlow;
 	*rlo = (uint32_t)nlow;
 	*rhi = (uint32_t)nhigh;
 	if (kept == 0) {	/* every sample rejected: the removal stops at the last one */
-		int mx, mx2;
-		sgh_value_at2(P, N - 1, N - 1, mx, mx2);
+		if (!rank_ok(N - 1))
+			return SG_CLS_LITERAL;
+		int mx;
+		value_at(N - 1, mx);
 		*value = (uint16_t)mx;
 		return SG_CLS_OK;
 	}
+	/* the moments at L and Uh - 1 both hold the below-band samples (their difference cancels
+	 * them unless L = -1, where they are kept and clean) */
 	const SghM ma = sgh_q_moments(P, qa), mb = sgh_q_moments(P, qb);
 	const long long sum = (mb.s - ma.s) + (long long)kept * P.lo;	/* exact: below 2^32 */
 	*value = sg_round_to_WORD((double)sum / (double)kept);
@@ -1454,7 +1512,7 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 	if (x < p.W) {
 		if (SG_DBG(p) == 1) {
 			value = (uint16_t)(s32 + ss32);
-		} else if (P.nb + oob != N || oob != P.nz + P.ns + zc || (zc && zmax >= lo)) {
+		} else if (P.nb + oob != N || (zc && zmax >= lo) || (REJ != 1 && REJ != 8 && oob != P.nz + P.ns + zc)) {
 			cls = 1;	/* out-of-band sample other than 0 / 65535 (or than this row's normalised
 				 * zeros), or a wrapped u8 counter */
 		} else {
@@ -1474,7 +1532,9 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 			P.T.s = (long long)s32 + P.Z.s + ds * P.ns;
 			P.T.ss = (unsigned long long)ss32 + P.Z.ss + (unsigned long long)(ds * ds) * (unsigned long long)P.ns;
 			if (REJ == 1 || REJ == 8) {
-				cls = sgh_median_pct<REJ, ZT>(P, N, p.sig0, p.sig1, &value, &rlo, &rhi);
+				/* out-of-band samples of any value: below the band nbl of them, above na */
+				const int na = (int)L.na[col], nbl = oob - na;
+				cls = sgh_median_pct<REJ, ZT>(P, N, p.sig0, p.sig1, nbl, nbl == P.nz, na == P.ns, &value, &rlo, &rhi);
 			} else if (REJ == 4 || !PAIR) {
 				/* zeros: nz copies of -lo, exact as doubles (dz = -lo, dz^2 nz < 2^53) */
 				P.zs = -(double)lo * (double)P.nz;
@@ -1576,6 +1636,7 @@ __device__ __forceinline__ void sgh_clear(SghLds<NI> &L, bool wait_prev, const B
 	if ((int)threadIdx.x < NC) {
 		((uint4 *)L.nz)[threadIdx.x] = z;
 		((uint4 *)L.ns)[threadIdx.x] = z;
+		((uint4 *)L.na)[threadIdx.x] = z;
 	}
 }
 
@@ -1715,10 +1776,10 @@ __device__ __forceinline__ void sgh_build(const SgStackParams &p, const SghRo &r
 #define SGH_WINS_ORDER 1	/* WINSORIZED finish: columns with zeros / 65535s first (sgh_tile) */
 #endif
 
-template <bool EDGE, int NORM, int NI, int NB, int BW = SghCfg<NI>::WAVES, class BAR = SghWgBarrier>
+template <bool EDGE, int NORM, int NI, int NB, int BW = SghCfg<NI>::WAVES, class BAR = SghWgBarrier, bool AB = false>
 __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const SghRo &ro, SghLds<NI> &L, const SghFrame &F,
 		int wave, int lane, uint32_t (&lo2)[NI], uint32_t (&nonzero)[NI], uint32_t (&nsat)[NI], int &counted,
-		bool wait_prev, const BAR &bar = BAR()) {
+		bool wait_prev, const BAR &bar = BAR(), uint32_t *nab = nullptr) {
 	constexpr int MB = 8;
 	constexpr int WAVES = BW;	/* the waves building the tile */
 	constexpr int STEP = 16 * WAVES;	/* frames between a wave's consecutive blocks */
@@ -1820,6 +1881,10 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
 #pragma unroll
 	for (int i = 0; i < NI; i++)
 		lo2[i] = nocentre ? 0u : L.lo2[i][lane];
+	uint32_t hi2[NI];	/* AB: lo + 255 per half (lo <= 65279: no carry between the halves) */
+#pragma unroll
+	for (int i = 0; i < NI; i++)
+		hi2[i] = lo2[i] + 0x00FF00FFu;
 	const bool loads_only = SG_DBG(p) == 3 || nocentre;
 	/* bin one half (frames f0 .. f0 + 7), per-frame bounds when it is not whole */
 	auto binh = [&](int f0, const uint32_t (&raw)[MB][NI], const uint32_t (&fx)[NI], bool whole) {
@@ -1834,8 +1899,8 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
 			for (int m = 0; m < MB; m += 2)
 #pragma unroll
 				for (int i = 0; i < NI; i++)
-					sgh_bin_pair2(h + i * (2 * SGH_HROWS * 64), l4, lo2[i], raw[m][i], raw[m + 1][i], nonzero[i],
-							nsat[i], k1, ksat);
+					sgh_bin_pair2<AB>(h + i * (2 * SGH_HROWS * 64), l4, lo2[i], raw[m][i], raw[m + 1][i], nonzero[i],
+							nsat[i], k1, ksat, AB ? nab + i : nullptr, hi2[i]);
 		} else {
 #pragma unroll
 			for (int m = 0; m < MB; m++) {
@@ -1848,7 +1913,8 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
 						uint32_t v = sgh_fixup<EDGE>(raw[m][i], fx[i], m);
 						if (NORM)
 							v = sgh_norm_pair<NORM, EDGE>(v, a, b, fx[i], m);
-						sgh_bin_pair(h + i * (2 * SGH_HROWS * 64), l4, lo2[i], v, nonzero[i], nsat[i], k1, ksat);
+						sgh_bin_pair<AB>(h + i * (2 * SGH_HROWS * 64), l4, lo2[i], v, nonzero[i], nsat[i], k1, ksat,
+								AB ? nab + i : nullptr, hi2[i]);
 					}
 				}
 			}
@@ -1942,10 +2008,11 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 		tl[3] = 0;
 	}
 
-	uint32_t nonzero[NI], nsat[NI], lo2[NI];
+	uint32_t nonzero[NI], nsat[NI], lo2[NI], nab[NI];
+	constexpr bool AB = REJ == 1 || REJ == 8;	/* stack_median / PERCENTILE: count the samples above the band */
 #pragma unroll
 	for (int i = 0; i < NI; i++)
-		nonzero[i] = nsat[i] = 0;
+		nonzero[i] = nsat[i] = nab[i] = 0;
 	int counted = 0;
 	/* the loading phase at a raised wave priority (SgStackParams::prio, default 1), so the
 	 * waves that keep loads in flight issue ahead of other tiles' finish phases on the same
@@ -1955,18 +2022,18 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 		__builtin_amdgcn_s_setprio(1);
 	else if (p.prio == 2)
 		__builtin_amdgcn_s_setprio(3);
-	if (NI == 1 && !SGH_HALF1) {
+	if (NI == 1 && !SGH_HALF1 && !AB) {
 		if (interior)
 			sgh_build<false, SGH_NBUF, NORM, NI>(p, ro, L, F, wave, lane, lo2, nonzero, nsat, counted, wait_prev);
 		else
 			sgh_build<true, SGH_NBUF, NORM, NI>(p, ro, L, F, wave, lane, lo2, nonzero, nsat, counted, wait_prev);
 	} else {
 		if (interior)
-			sgh_build_half<false, NORM, NI, NI == 1 ? SGH_NB : SGH_NB2, WAVES>(p, ro, L, F, wave, lane, lo2, nonzero,
-					nsat, counted, wait_prev);
+			sgh_build_half<false, NORM, NI, NI == 1 ? SGH_NB : SGH_NB2, WAVES, SghWgBarrier, AB>(p, ro, L, F, wave, lane,
+					lo2, nonzero, nsat, counted, wait_prev, SghWgBarrier(), nab);
 		else
-			sgh_build_half<true, NORM, NI, NI == 1 ? SGH_NB : SGH_NB2, WAVES>(p, ro, L, F, wave, lane, lo2, nonzero,
-					nsat, counted, wait_prev);
+			sgh_build_half<true, NORM, NI, NI == 1 ? SGH_NB : SGH_NB2, WAVES, SghWgBarrier, AB>(p, ro, L, F, wave, lane,
+					lo2, nonzero, nsat, counted, wait_prev, SghWgBarrier(), nab);
 	}
 	if (counted) {
 #pragma unroll
@@ -1975,6 +2042,10 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 			atomicAdd(&L.nz[128 * i + 64 + lane], (uint32_t)counted - (nonzero[i] >> 16));
 			atomicAdd(&L.ns[128 * i + lane], nsat[i] & 0xFFFFu);
 			atomicAdd(&L.ns[128 * i + 64 + lane], nsat[i] >> 16);
+			if (AB) {
+				atomicAdd(&L.na[128 * i + lane], nab[i] & 0xFFFFu);
+				atomicAdd(&L.na[128 * i + 64 + lane], nab[i] >> 16);
+			}
 		}
 	}
 	__syncthreads();
