@@ -75,8 +75,10 @@ static void dft_rec(const double *xr, const double *xi, int is, double *yr, doub
 }
 
 /* in-place 1-D complex DFT of length n with stride 1 (radix-2 if n is a power of two,
- * otherwise the recursive mixed radix above) */
-static void dft1d(double *re, double *im, int n, int sign, double *wre, double *wim) {
+ * otherwise the recursive mixed radix above).  tw: the radix-2 stages' twiddles, stage len at
+ * tw + 2 (len / 2 - 1) as (cos, sin)(sign 2 pi k / len), k < len / 2 - the values the plain
+ * loop computes per stage, tabulated once per 2-D transform */
+static void dft1d(double *re, double *im, int n, int sign, const double *tw) {
 	if ((n & (n - 1)) == 0) {
 		/* bit reversal */
 		for (int i = 1, j = 0; i < n; i++) {
@@ -90,17 +92,13 @@ static void dft1d(double *re, double *im, int n, int sign, double *wre, double *
 			}
 		}
 		for (int len = 2; len <= n; len <<= 1) {
-			double ang = sign * 2.0 * M_PI / len;
-			for (int k = 0; k < len / 2; k++) {
-				wre[k] = cos(ang * k);
-				wim[k] = sin(ang * k);
-			}
+			const double *w = tw + 2 * (len / 2 - 1);
 			for (int i = 0; i < n; i += len) {
 				for (int k = 0; k < len / 2; k++) {
 					double ur = re[i + k], ui = im[i + k];
 					double xr = re[i + k + len / 2], xi = im[i + k + len / 2];
-					double vr = xr * wre[k] - xi * wim[k];
-					double vi = xr * wim[k] + xi * wre[k];
+					double vr = xr * w[2 * k] - xi * w[2 * k + 1];
+					double vi = xr * w[2 * k + 1] + xi * w[2 * k];
 					re[i + k] = ur + vr;
 					im[i + k] = ui + vi;
 					re[i + k + len / 2] = ur - vr;
@@ -119,22 +117,32 @@ static void dft1d(double *re, double *im, int n, int sign, double *wre, double *
 }
 
 void or_dft2d(double *re, double *im, int S, int sign) {
-	double *wre = malloc(S * sizeof(double)), *wim = malloc(S * sizeof(double));
+	/* stage tables: sum over stages of len / 2 = S - 1 (cos, sin) pairs */
+	double *tw = malloc(2 * (size_t)(S > 1 ? S : 2) * sizeof(double));
+	if ((S & (S - 1)) == 0)
+		for (int len = 2; len <= S; len <<= 1) {
+			const double ang = sign * 2.0 * M_PI / len;
+			double *w = tw + 2 * (len / 2 - 1);
+			for (int k = 0; k < len / 2; k++) {
+				w[2 * k] = cos(ang * k);
+				w[2 * k + 1] = sin(ang * k);
+			}
+		}
 	double *cr = malloc(S * sizeof(double)), *ci = malloc(S * sizeof(double));
 	for (int y = 0; y < S; y++)
-		dft1d(re + (size_t)y * S, im + (size_t)y * S, S, sign, wre, wim);
+		dft1d(re + (size_t)y * S, im + (size_t)y * S, S, sign, tw);
 	for (int x = 0; x < S; x++) {
 		for (int y = 0; y < S; y++) {
 			cr[y] = re[(size_t)y * S + x];
 			ci[y] = im[(size_t)y * S + x];
 		}
-		dft1d(cr, ci, S, sign, wre, wim);
+		dft1d(cr, ci, S, sign, tw);
 		for (int y = 0; y < S; y++) {
 			re[(size_t)y * S + x] = cr[y];
 			im[(size_t)y * S + x] = ci[y];
 		}
 	}
-	free(wre); free(wim); free(cr); free(ci);
+	free(tw); free(cr); free(ci);
 }
 
 /* quality.h constants */
@@ -296,7 +304,6 @@ int or_register_shift_dft(const uint16_t *sel, int nframes, int S, int ref_image
 		const int *included, int *shiftx, int *shifty, double *quality) {
 	size_t sq = (size_t)S * S;
 	double *inr = malloc(sq * sizeof(double)), *ini = malloc(sq * sizeof(double));
-	double *ar = malloc(sq * sizeof(double)), *ai = malloc(sq * sizeof(double));
 	double q_max, q_min;
 	if (ref_image < 0)
 		ref_image = 0;
@@ -309,45 +316,58 @@ int or_register_shift_dft(const uint16_t *sel, int nframes, int S, int ref_image
 	or_dft2d(inr, ini, S, -1);
 	shiftx[ref_image] = 0;
 	shifty[ref_image] = 0;
+	/* the frames in an OpenMP loop with per-thread buffers, as the reference's
+	 * `omp parallel for ... firstprivate(fit) schedule(static)` (:276-279); q_min / q_max are
+	 * formed afterwards in index order (the reference's omp critical takes them in completion
+	 * order, which only matters for NaN qualities through the min() macro) */
+#pragma omp parallel
+	{
+		double *ar = malloc(sq * sizeof(double)), *ai = malloc(sq * sizeof(double));
+#pragma omp for schedule(static)
+		for (int frame = 0; frame < nframes; ++frame) {
+			if (frame == ref_image)
+				continue;
+			if (included && !included[frame])
+				continue;
+			const uint16_t *img = sel + (size_t)frame * sq;
+			for (size_t x = 0; x < sq; x++) {
+				ar[x] = (double)img[x];
+				ai[x] = 0.0;
+			}
+			quality[frame] = or_quality_estimate(img, S, S);
+			or_dft2d(ar, ai, S, -1);
+			/* convol2 = in * conj(out2) */
+			for (size_t x = 0; x < sq; x++) {
+				double br = ar[x], bi = -ai[x];
+				double cr = inr[x] * br - ini[x] * bi;
+				double ci = inr[x] * bi + ini[x] * br;
+				ar[x] = cr;
+				ai[x] = ci;
+			}
+			or_dft2d(ar, ai, S, +1);
+			size_t shift = 0;
+			for (size_t x = 1; x < sq; ++x)
+				if (ar[x] > ar[shift])
+					shift = x;
+			int sy = (int)(shift / S), sx = (int)(shift % S);
+			if (sy > S / 2)
+				sy -= S;
+			if (sx > S / 2)
+				sx -= S;
+			shiftx[frame] = sx;
+			shifty[frame] = sy;
+		}
+		free(ar);
+		free(ai);
+	}
 	q_min = q_max = quality[ref_image];
 	for (int frame = 0; frame < nframes; ++frame) {
-		if (frame == ref_image)
+		if (frame == ref_image || (included && !included[frame]))
 			continue;
-		if (included && !included[frame])
-			continue;
-		const uint16_t *img = sel + (size_t)frame * sq;
-		for (size_t x = 0; x < sq; x++) {
-			ar[x] = (double)img[x];
-			ai[x] = 0.0;
-		}
-		quality[frame] = or_quality_estimate(img, S, S);
-		{
-			double qual = quality[frame];
-			if (qual > q_max)
-				q_max = qual;
-			q_min = (q_min < qual) ? q_min : qual;	/* siril.h:30-33 min() */
-		}
-		or_dft2d(ar, ai, S, -1);
-		/* convol2 = in * conj(out2) */
-		for (size_t x = 0; x < sq; x++) {
-			double br = ar[x], bi = -ai[x];
-			double cr = inr[x] * br - ini[x] * bi;
-			double ci = inr[x] * bi + ini[x] * br;
-			ar[x] = cr;
-			ai[x] = ci;
-		}
-		or_dft2d(ar, ai, S, +1);
-		size_t shift = 0;
-		for (size_t x = 1; x < sq; ++x)
-			if (ar[x] > ar[shift])
-				shift = x;
-		int sy = (int)(shift / S), sx = (int)(shift % S);
-		if (sy > S / 2)
-			sy -= S;
-		if (sx > S / 2)
-			sx -= S;
-		shiftx[frame] = sx;
-		shifty[frame] = sy;
+		const double qual = quality[frame];
+		if (qual > q_max)
+			q_max = qual;
+		q_min = (q_min < qual) ? q_min : qual;	/* siril.h:30-33 min() */
 	}
 	/* normalizeQualityData */
 	for (int frame = 0; frame < nframes; ++frame) {
@@ -356,7 +376,7 @@ int or_register_shift_dft(const uint16_t *sel, int nframes, int S, int ref_image
 		quality[frame] -= q_min;
 		quality[frame] /= (q_max - q_min);
 	}
-	free(inr); free(ini); free(ar); free(ai);
+	free(inr); free(ini);
 	return 0;
 }
 

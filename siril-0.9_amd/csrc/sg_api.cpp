@@ -527,6 +527,34 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		return SG_OK;
 	};
 
+	/* stack_mean_with_rejection reads a block's rows with area.y += shifty; when a block that
+	 * does not start at the top (area.y > 0) is shifted partly above the frame (area.y + shifty
+	 * < 0 <= area.y + h - 1 + shifty) it places the rows it reads at offset W (area.y - shifty)
+	 * instead of W (-area.y - shifty) (src/stacking/stacking.c:1555-1561): the rows land 2 area.y
+	 * too low and run 2 area.y + h - largest_block_h rows past its block buffer, always a heap
+	 * overflow (the neighbouring buffer or the allocator's data).  No defined result exists to
+	 * reproduce, so the call refuses the shifts instead of zero filling silently */
+	if (d->method == SG_STACK_MEAN && p.use_shift && p.sy_min < 0) {
+		const int nthr = d->max_thread > 0 ? d->max_thread : default_threads();
+		const int maxrows = d->max_number_of_rows > 0 ? d->max_number_of_rows : H;
+		std::vector<Block> blocks;
+		if (make_blocks(H, C, maxrows, nthr, blocks) == 0)
+			for (const Block &b : blocks) {
+				const long ay = b.start_row, ah = b.end_row - b.start_row + 1;
+				if (ay > 0 && ay + p.sy_min < 0 && ay + ah - 1 + p.sy_max >= 0) {
+					bool hit = false;
+					for (int i = 0; i < N && !hit; i++)
+						hit = ay + d->shifty[i] < 0 && ay + ah - 1 + d->shifty[i] >= 0;
+					if (hit) {
+						char m[320];
+						snprintf(m, sizeof m, "a registration shift of %d rows reaches above the block starting at "
+								"row %ld: the reference overflows its block buffer there (stacking.c:1555-1561); "
+								"use more rows per block (max_number_of_rows / fewer threads)", p.sy_min, ay);
+						return set_err(ctx, SG_ERR_GENERIC, "%s%.0ld", m, 0);
+					}
+				}
+			}
+	}
 	const bool sorted = (d->method == SG_STACK_MEDIAN) ||
 		(d->method == SG_STACK_MEAN && d->rejection != SG_NO_REJEC);
 	if (sorted) {

@@ -446,3 +446,27 @@ def test_hist_winsorized_iteration_cap(gpu_ctx, cap):
     assert np.array_equal(rej_h, rej_ref), (rej_h, rej_ref)
     if cap == "4":
         assert st.chain_pixels > 0.2 * H * W, st.chain_pixels   # the cap did send pixels away
+
+
+def test_block_overflow_shift_refused(gpu_ctx):
+    """a shift reaching above a block that does not start at the top of the image: the reference
+    reads the block's rows 2 start_row too low and past its buffer (stacking.c:1555-1561, the
+    oracle returns -4); the library refuses instead of silently zero filling"""
+    N, C, H, W = 8, 1, 24, 64
+    frames = orc.synth(N, C, H, W, seed=4, maxshift=2)
+    sx = np.zeros(N, np.int32)
+    sy = np.zeros(N, np.int32)
+    sy[3] = -9                          # 4 threads, 24 rows: blocks of 6 rows; -9 < -6
+    rc, ref, _ = orc.stack_rejection(frames, sg.SIGMA, shiftx=sx, shifty=sy, max_thread=4)
+    assert rc == -4
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, C, rejection=sg.SIGMA, shiftx=sx, shifty=sy, max_thread=4,
+                              max_number_of_rows=H)
+    rc, out, rej, _ = gpu_ctx.stack_host(desc, frames)
+    assert rc == -1 and "overflows" in gpu_ctx.error()
+    # one thread: 4 blocks of 6 rows too (H / rows < 4); with max_number_of_rows 24 and a shift
+    # that stays below the first block start it stacks
+    sy[3] = -5
+    rc, ref, rr = orc.stack_rejection(frames, sg.SIGMA, shiftx=sx, shifty=sy, max_thread=4)
+    assert rc == 0
+    out, rej, _ = gpu_stack(gpu_ctx, frames, sg.MEAN, sg.SIGMA, shiftx=sx, shifty=sy, max_thread=4)
+    assert_same(out, ref, "shift below the block height")
