@@ -37,9 +37,6 @@ void sg_dbg_why_dump(hipStream_t s);
 int sgh_block_threads(int ni, int rej);
 template <int NM>
 __global__ void k_stack_replay(SgStackParams p);
-__global__ void k_stack_wins_tail(SgStackParams p, unsigned int *redo_count, unsigned int *redo_list);
-#define SGH_STRAG_DW 96			/* u32 per WINSORIZED straggler record (sg_stack_hist.hip) */
-#define SG_STRAG_MAX (4u << 20)		/* straggler records per call (1.5 GiB); beyond it a tile finishes its own */
 __global__ void k_redo_to_literal(SgStackParams p, const unsigned int *list, const unsigned int *count,
 		unsigned int maxn);
 __global__ void k_stack_reduce(SgStackParams p);
@@ -109,7 +106,7 @@ extern "C" void sg_shutdown(sg_ctx *ctx) {
 		(void)hipStreamSynchronize(d.stream);
 		SgBuf *bufs[] = {&d.flag_list, &d.flag_map, &d.sum_buf, &d.scratch, &d.frames, &d.out, &d.reg_sel, &d.reg_spec,
 			&d.reg_work, &d.reg_tw, &d.reg_tw32, &d.reg_best, &d.reg_qbuf, &d.reg_qacc, &d.redo, &d.zeros,
-			&d.io_raw, &d.io_bad, &d.warp_tab, &d.stats_buf, &d.inb, &d.ctr, &d.strag};
+			&d.io_raw, &d.io_bad, &d.warp_tab, &d.stats_buf, &d.inb, &d.ctr};
 		for (SgBuf *b : bufs)
 			if (b->p)
 				(void)hipFree(b->p);
@@ -346,7 +343,6 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 	p.dbg = ctx->knobs.hist_dbg;
 	p.prio = ctx->knobs.hist_prio;	/* 1 measured best: 4.73 -> 4.58 ms (scripts/gpu_prio.sh) */
 	p.wins_cap = ctx->knobs.wins_cap;
-	p.wins_budget = ctx->knobs.wins_budget;
 
 	/* per-frame constants: shifts + normalisation coefficients */
 	const int Npad = (N + 15) & ~15;	/* histogram-path table: 64-byte aligned, padded */
@@ -521,7 +517,6 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 	p.flag_count = (unsigned int *)((char *)dv.ctr.p + REJB);
 	p.walk_fault = p.flag_count + 1;
 	p.maxim = (unsigned int *)((char *)dv.ctr.p + REJB + 64);
-	p.strag_count = p.flag_count + 3;	/* cleared with the counters */
 	const unsigned int *ctr_flags = (const unsigned int *)((const char *)dv.ctr_h + REJB);
 	bool have_counts = false;
 	auto readback = [&]() -> int {
@@ -645,12 +640,6 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			const int rj = d->method == SG_STACK_MEDIAN ? 8 : p.rejection == SG_WINSORIZED ? 4 :
 				p.rejection == SG_PERCENTILE ? 1 : 2;
 			const dim3 hg((unsigned)nblk_h), hb((unsigned)sgh_block_threads(ni, rj));
-			if (rj == 4 && p.wins_budget > 0) {
-				const size_t cap = std::min<size_t>(npix_launch, SG_STRAG_MAX);
-				HIPCHK(ensure(dv.strag, cap * SGH_STRAG_DW * sizeof(uint32_t)));
-				p.strag = (uint32_t *)dv.strag.p;
-				p.strag_cap = (unsigned int)cap;
-			}
 			switch ((rj == 4 ? 10 : rj == 1 ? 20 : rj == 8 ? 30 : 0) + norm + 100 * (rj == 1 || rj == 8 ? 1 : ni)) {
 			case 100: hipLaunchKernelGGL((k_stack_hist<2, 0, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 101: hipLaunchKernelGGL((k_stack_hist<2, 1, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
@@ -673,12 +662,6 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			default: return set_err(ctx, SG_ERR_GENERIC, "no histogram kernel for this case%s%.0ld", "", 0);
 			}
 			HIPCHK(hipGetLastError());
-			if (rj == 4 && p.wins_budget > 0) {
-				/* the WINSORIZED stragglers, resumed from their pass-start state */
-				hipLaunchKernelGGL(k_stack_wins_tail, dim3(1024), dim3(128), 0, s, p, redo_count, redo_list);
-				HIPCHK(hipGetLastError());
-				st.launches++;
-			}
 			HIPCHK(hipEventRecord(dv.ev[1], s));
 			HIPCHK(hipMemsetAsync(dv.flag_map.p, 0, npix_img, s));
 			st.path = 1;

@@ -61,12 +61,6 @@ struct SgStackParams {
 	uint8_t *flag_map;			/* [C][H][W] class per pixel (chain walk) */
 	uint32_t *sum_buf;			/* SUM: raw sums [C][H][W] */
 	unsigned int *maxim;			/* SUM: global max of sums */
-	/* histogram WINSORIZED: a pixel whose inner iterations exceed wins_budget (0: never) leaves its
-	 * tile as a straggler record (its pass-start state and histogram) for k_stack_wins_tail */
-	int wins_budget;
-	unsigned int strag_cap;
-	unsigned int *strag_count;
-	uint32_t *strag;			/* [strag_cap][SGH_STRAG_DW] */
 };
 
 /* round_to_WORD, src/core/utils.c:68-74 */

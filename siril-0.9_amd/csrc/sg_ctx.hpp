@@ -41,7 +41,6 @@ struct SgDevice {
 	/* registration workspaces (sg_register.hip) */
 	SgBuf reg_sel, reg_spec, reg_work, reg_tw, reg_tw32, reg_best, reg_qbuf, reg_qacc;
 	SgBuf redo;	/* redo list of the histogram stacking path */
-	SgBuf strag;	/* WINSORIZED straggler records (k_stack_hist<4> -> k_stack_wins_tail) */
 	SgBuf zeros;	/* zero page for out-of-frame sample loads */
 	/* stacking call inputs (shift table, normalisation coefficients, chain tables) packed into
 	 * one pinned host block and one device block: one H2D copy per call; ev[3] marks the copy
@@ -84,7 +83,6 @@ struct SgKnobs {
 	int hist_ldspad = 0;		/* SG_HIST_LDSPAD: extra LDS bytes per histogram workgroup (occupancy A/B) */
 	int hist_ni = 1;		/* SG_HIST_NI: pixel pairs per lane of the histogram tiles (2: 256-px tiles) */
 	int wins_cap = 64;		/* SG_WINS_CAP: histogram Winsorize inner iterations per pass before the redo list */
-	int wins_budget = 8;		/* SG_WINS_BUDGET: inner iterations before a WINSORIZED pixel leaves its tile as a straggler (0: never) */
 	int redo_replay = 1;		/* SG_REDO_REPLAY: 0 = redo list always through the sorted kernel */
 	int reduce1 = 0;		/* SG_REDUCE1: 1 = one pixel per lane, 2 = the per-lane pixel-pair kernel, in the SUM/MAX/MIN/MEAN reduce (A/B) */
 	long long host_budget = 0;	/* SG_HOST_BUDGET_BYTES: host-pull HBM budget (0 = 85 % of free HBM) */
@@ -105,7 +103,6 @@ struct SgKnobs {
 		hist_ldspad = sg_env_int("SG_HIST_LDSPAD", 0, 160 * 1024, 0);
 		hist_ni = sg_env_int("SG_HIST_NI", 1, 2, 1);
 		wins_cap = sg_env_int("SG_WINS_CAP", 4, 100000, 64);
-		wins_budget = sg_env_int("SG_WINS_BUDGET", 0, 100000, 8);
 		redo_replay = sg_env_int("SG_REDO_REPLAY", 0, 1, 1);
 		reduce1 = sg_env_int("SG_REDUCE1", 0, 2, 0);
 		if (const char *e = getenv("SG_HOST_BUDGET_BYTES"))

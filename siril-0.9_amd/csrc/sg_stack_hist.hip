@@ -138,24 +138,6 @@ struct SghPix {
 	double zs, zss;		/* Z.s, Z.ss as doubles (exact: below 2^53) for the Winsorized queries */
 };
 
-/* the WINSORIZED loop's state at the start of a pass (sgh_winsorized): what a straggler carries
- * out of its tile to k_stack_wins_tail, which resumes the pass from it */
-struct SghWState {
-	int A, B, n, r, klo, khi;
-	uint32_t rlo, rhi;
-	SghM MA, MB;
-};
-/* straggler record in HBM: pixel, band start, zero / 65535 counts, pass-start state, the 65
- * histogram dwords of the column (sgh_finish2 -> k_stack_wins_tail) */
-struct SghStrag {
-	uint32_t pix;
-	int lo, nz, ns;
-	SghWState st;
-	uint32_t h[SGH_HROWS];
-};
-#define SGH_STRAG_DW 96
-static_assert(sizeof(SghStrag) <= SGH_STRAG_DW * 4, "straggler record size");
-
 /* t[k] for a lane-varying k in [0, 8): a 3-level select tree on the bits of k */
 __device__ __forceinline__ uint32_t sgh_sel(const uint32_t (&t)[SGH_NGRP], int k) {
 	static_assert(SGH_NGRP == 8, "3-level tree");
@@ -1041,12 +1023,8 @@ __device__ __forceinline__ void sgh_wpev(uint64_t *w, int k) {
 #define SGH_WPEV(k)
 #endif
 
-/* returns SG_CLS_OK, 1 (redo list) or 2 (budget: more than `budget` inner iterations in all, 0 =
- * no limit; *ws holds the current pass's starting state and the pixel is resumed from it by
- * k_stack_wins_tail).  resume: start from *ws instead of the first pass */
-#define SGH_WINS_HANDOFF 2
 __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int cap, uint16_t *value, uint32_t *rlo_out,
-		uint32_t *rhi_out, SghWState *ws = nullptr, int budget = 0, bool resume = false) {
+		uint32_t *rhi_out) {
 	int A = 0, B = 65535, n = N, r = 0, nrem;
 	SghM MA = {0, 0, 0}, MB = P.T;
 	uint32_t rlo = 0, rhi = 0;
@@ -1056,23 +1034,7 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 	/* smallest / largest kept sample at the start of a pass (a lower / an upper bound from the
 	 * second pass on: the clip queries' neighbours, sgh_qx); the first pass's from two rank
 	 * queries */
-	int klo, khi;
-	if (resume) {
-		A = ws->A;
-		B = ws->B;
-		n = ws->n;
-		r = ws->r;
-		klo = ws->klo;
-		khi = ws->khi;
-		rlo = ws->rlo;
-		rhi = ws->rhi;
-		MA = ws->MA;
-		MB = ws->MB;
-	} else {
-		klo = sgh_value_at1(P, 0);
-		khi = sgh_value_at1(P, N - 1);
-	}
-	int iters = 0;
+	int klo = sgh_value_at1(P, 0), khi = sgh_value_at1(P, N - 1);
 	do {
 		const long long S = MB.s - MA.s;
 		const long long SS = (long long)(MB.ss - MA.ss);
@@ -1102,21 +1064,6 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 			if (guard >= cap)
 				return 1;	/* a long Winsorize (hundreds of iterations with several 0 / 65535
 					 * samples) goes to the replay rather than holding its wave */
-			if (budget && ++iters > budget) {
-				/* a straggler: the pass-start state (nothing of it changes inside the
-				 * inner loop) leaves the tile, the pass is redone by k_stack_wins_tail */
-				ws->A = A;
-				ws->B = B;
-				ws->n = n;
-				ws->r = r;
-				ws->klo = klo;
-				ws->khi = khi;
-				ws->rlo = rlo;
-				ws->rhi = rhi;
-				ws->MA = MA;
-				ws->MB = MB;
-				return SGH_WINS_HANDOFF;
-			}
 #ifdef SGH_WINS_ITERS	/* A/B probe build: inner iterations (low 16 bits) and outer passes (high) */
 			(*rlo_out)++;
 #endif
@@ -1447,8 +1394,7 @@ __device__ __forceinline__ int sgh_median_pct(const SghPix &P, int N, double sl,
 
 template <int REJ, bool PAIR, int NI, bool ZT = false>
 __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int half, int lo, int R, int c, int x,
-		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list, bool zrow = false,
-		const SghWState *resume = nullptr) {
+		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list, bool zrow = false) {
 	const int lane = threadIdx.x & 63;
 	const int N = p.N;
 	const uint32_t *hc = &L.h[col >> 6][0][col & 63];	/* dword j at hc[64 j] */
@@ -1593,31 +1539,7 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 				/* zeros: nz copies of -lo, exact as doubles (dz = -lo, dz^2 nz < 2^53) */
 				P.zs = -(double)lo * (double)P.nz;
 				P.zss = (double)lo * (double)lo * (double)P.nz;
-				/* a pixel still iterating after wins_budget inner iterations leaves the tile as a
-				 * straggler (k_stack_wins_tail finishes it with the other stragglers, so the
-				 * tile's waves and LDS go to the next tile instead of waiting on their slowest
-				 * lane); resume: such a pixel in k_stack_wins_tail */
-				SghWState ws;
-				if (resume)
-					ws = *resume;
-				cls = sgh_winsorized(P, N, p.sig0, p.sig1, p.wins_cap, &value, &rlo, &rhi, &ws,
-						resume ? 0 : p.wins_budget, resume != nullptr);
-				if (cls == SGH_WINS_HANDOFF) {
-					const unsigned int slot = atomicAdd(p.strag_count, 1u);
-					if (slot < p.strag_cap) {
-						SghStrag *g = (SghStrag *)(p.strag + (size_t)slot * SGH_STRAG_DW);
-						g->pix = (uint32_t)(((int64_t)c * p.H + R) * p.W + x);
-						g->lo = lo;
-						g->nz = P.nz;
-						g->ns = P.ns;
-						g->st = ws;
-#pragma unroll 5
-						for (int j = 0; j < SGH_HROWS; j++)
-							g->h[j] = hc[64 * j];
-					} else {	/* no room: finish it here */
-						cls = sgh_winsorized(P, N, p.sig0, p.sig1, p.wins_cap, &value, &rlo, &rhi, &ws, 0, true);
-					}
-				}
+				cls = sgh_winsorized(P, N, p.sig0, p.sig1, p.wins_cap, &value, &rlo, &rhi);
 #ifdef SGH_WINS_ITERS
 				value = (uint16_t)rlo;	/* A/B probe build: the image holds the inner iteration counts */
 				cls = SG_CLS_OK;
@@ -1638,7 +1560,7 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 			}
 		}
 		const int64_t pix = ((int64_t)c * p.H + R) * p.W + x;
-		if (!half && cls != SGH_WINS_HANDOFF) {
+		if (!half) {
 			if (cls == SG_CLS_OK) {
 #ifndef SGH_WPROF
 				if (SG_DBG(p) != 11)	/* the timeline A/B keeps its stamps in the output buffer */
@@ -2209,43 +2131,6 @@ k_stack_hist(SgStackParams p, const int *__restrict__ tab, const int4 *__restric
 	 * (scripts/gpu_r3p.sh; the tile loop also costs registers: 128 VGPRs + scratch) */
 	if (vb < ntiles)
 		sgh_tile<REJ, NORM, NI>(p, ro, L, vb, false, redo_count, redo_list);
-}
-
-/*
- * k_stack_wins_tail: the WINSORIZED stragglers of k_stack_hist<4> (pixels still iterating after
- * wins_budget inner iterations), 128 per 2-wave workgroup, one lane each: the record's histogram
- * goes back into the tile layout and the pixel resumes its pass from the saved state through
- * the same finish (sgh_finish2) - only stragglers share a wave here, so no lane waits on a
- * pixel that finished in two iterations.  The count is read on the device (no host round trip).
- */
-__global__ void __launch_bounds__(128, 2)
-k_stack_wins_tail(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
-	__shared__ SghLds<1> L;
-	unsigned int count = *p.strag_count;
-	if (count > p.strag_cap)
-		count = p.strag_cap;
-	const int col = (int)threadIdx.x;
-	for (unsigned int base = blockIdx.x * 128u; base < count; base += gridDim.x * 128u) {
-		__syncthreads();	/* the previous round's finish is done with L */
-		const unsigned int k = base + (unsigned int)col;
-		const bool live = k < count;
-		const SghStrag *g = (const SghStrag *)(p.strag + (size_t)(live ? k : base) * SGH_STRAG_DW);
-		uint32_t *hc = &L.h[col >> 6][0][col & 63];
-#pragma unroll 5
-		for (int j = 0; j < SGH_HROWS; j++)
-			hc[64 * j] = live ? g->h[j] : 0u;
-		L.nz[col] = live ? (uint32_t)g->nz : 0u;
-		L.ns[col] = live ? (uint32_t)g->ns : 0u;
-		const SghWState st = g->st;
-		const uint32_t pix = g->pix;
-		const int lo = g->lo;
-		__syncthreads();
-		/* a dead lane finishes a copy of the round's first record with x = W (nothing written) */
-		const int x = live ? (int)(pix % (uint32_t)p.W) : p.W;
-		const uint32_t cr = pix / (uint32_t)p.W;
-		sgh_finish2<4, false, 1>(p, L, col, 0, lo, (int)(cr % (uint32_t)p.H), (int)(cr / (uint32_t)p.H), x, redo_count,
-				redo_list, false, &st);
-	}
 }
 
 template __global__ void k_stack_hist<2, 0, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
