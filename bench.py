@@ -63,6 +63,9 @@ def parse():
                     help="A/B only: drop the x or y registration shifts")
     ap.add_argument("--frame-pad", type=int, default=0,
                     help="extra elements between frames in HBM (breaks power-of-two frame strides)")
+    ap.add_argument("--selection", type=int, default=0,
+                    help="register-mean / winsorized-rgb: side of the registration selection (default 2048; "
+                         "e.g. 4000 = configs[4]'s full height, a non-power-of-two side)")
     ap.add_argument("--cpu-rows", type=int, default=1024, help="rows of the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="OpenMP threads of the CPU baseline (the GPU box's CPU share is 16)")
@@ -409,12 +412,13 @@ def main_sigma(args):
 
 def stack_roofline(achieved, algo_bytes, rej, N, C, H, W, world):
     """roofline of main_config's stack kernel; traffic = the PMC FETCH/WRITE bytes per launch
-    of the whole configs[4] image (profiles/traffic_winsorized_<N>x<C>x<H>x<W>.json, 1 GPU)"""
+    of the whole image (profiles/traffic_{winsorized|mean}_<N>x<C>x<H>x<W>.json, 1 GPU)"""
     import sirilgpu as sg
     r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "stack"}
-    path = os.path.join(ROOT, "profiles", f"traffic_winsorized_{N}x{C}x{H}x{W}.json")
-    if rej == sg.WINSORIZED and world == 1 and os.path.exists(path):
+    name = "winsorized" if rej == sg.WINSORIZED else "mean"
+    path = os.path.join(ROOT, "profiles", f"traffic_{name}_{N}x{C}x{H}x{W}.json")
+    if world == 1 and os.path.exists(path):
         with open(path) as f:
             t = json.load(f)
         r["traffic"] = int(t["traffic_bytes"])
@@ -439,6 +443,10 @@ def main_config(args):
         N, C, H, W, S, layer, rej, cfg = 128, 1, 2048, 2048, 2048, 0, sg.NO_REJEC, "BASELINE configs[1]"
     else:
         N, C, H, W, S, layer, rej, cfg = 256, 3, 4000, 6000, 2048, 1, sg.WINSORIZED, "BASELINE configs[4]"
+    if args.selection:
+        S = args.selection
+        if not 2 <= S <= min(H, W):
+            raise SystemExit(f"--selection {S} does not fit a {H}x{W} frame")
     seed, M = 0x5EED, 16
     y0, x0 = (H - S) // 2, (W - S) // 2
     ex, ey = synth_shifts_np(N, seed, M)
@@ -520,6 +528,11 @@ def main_config(args):
     stack_bytes = N * C * (e - b) * W * 2 + C * (e - b) * W * 2
     achieved = stack_bytes / (kavg * 1e-3) / 1e9
     reg_bytes = nsel * S * S * 58          # stated 2-pass c64 FFT model, SURVEY.md section 8(d)
+    reg_traffic = None
+    tpath = os.path.join(ROOT, "profiles", f"traffic_register_{N}x{S}.json")
+    if world == 1 and os.path.exists(tpath):
+        with open(tpath) as f:
+            reg_traffic = json.load(f)
     if rank == 0:
         res = {
             "metric": "frames/sec stacked (registration + stack) + achieved HBM GB/s",
@@ -527,7 +540,8 @@ def main_config(args):
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u16",
             "data": "synthetic (include/sg_synth.h, generated in HBM)",
-            "config": {"workload": f"{args.workload} {N}x{C}x{H}x{W} ({cfg})", "frames": N, "layers": C,
+            "config": {"workload": f"{args.workload} {N}x{C}x{H}x{W} ({cfg})" +
+                       (f", {S}^2 selection" if args.selection else ""), "frames": N, "layers": C,
                        "height": H, "width": W, "selection": S, "register_layer": layer,
                        "rejection": "none" if rej == sg.NO_REJEC else "winsorized",
                        "parallelism": "1 GPU" if world == 1 else
@@ -538,7 +552,15 @@ def main_config(args):
             "register_GBps_model": round(reg_bytes / stage[1] / 1e9, 1),
             "register_shifts_exact": reg_ok,
         }
-        if not args.no_cpu_baseline and world == 1:
+        if reg_traffic is not None:
+            # PMC FETCH/WRITE bytes of the registration kernels per step (scripts/pmc_traffic.py)
+            tb = reg_traffic["traffic_bytes_per_step"]
+            res["register_traffic"] = {"bytes_per_step": int(tb), "GBps": round(tb / stage[1] / 1e9, 1),
+                                       "frac": round(tb / stage[1] / 1e9 / HBM_PEAK_GBS, 4),
+                                       "src": os.path.relpath(tpath, ROOT)}
+        if S & (S - 1):
+            res["cpu_baseline_note"] = "none: the oracle's radix-2 DFT takes power-of-two sides only"
+        if not args.no_cpu_baseline and world == 1 and (S & (S - 1)) == 0:
             res["cpu_baseline"] = cpu_baseline_config(args, args.workload, N, C, H, W, S, layer)
         print(json.dumps(res), flush=True)
     ctx.close()

@@ -10,7 +10,8 @@
 #   bench=NAME[:ARGS]           python bench.py ARGS -> NAME.log + one summary line
 #   env=NAME:VAR=V[;VAR=V]:ARGS the same with an environment (A/B: SG_* knobs, SG_LIB_PATH)
 #   prof=NAME[:ARGS]            rocprofv3 --kernel-trace --stats of bench.py ARGS -> NAME/
-#   pmc=NAME[:ARGS]             FETCH_SIZE and WRITE_SIZE passes (own runs) -> NAME_traffic.json
+#   pmc=NAME[@K1,K2][:ARGS]     FETCH_SIZE and WRITE_SIZE passes (own runs) -> NAME_traffic.json
+#                               (kernels K: default $PMC_KERNEL or k_stack_hist; several = per-step totals)
 #   sq=NAME:CTRS[:ARGS]         one rocprofv3 --pmc pass with counters CTRS ('+' between them,
 #                               within the per-block slot limits) -> NAME.txt (pmc_sum.py)
 #   py=NAME:SCRIPT[:ARGS]       python SCRIPT ARGS -> NAME.log
@@ -64,13 +65,14 @@ for step in "$@"; do
       echo "$name: $(summary "$O/$name.log")" ;;
     pmc)
       name=${spec%%:*}; args=""; [ "$name" != "$spec" ] && args=${spec#*:}
+      kern=${PMC_KERNEL:-k_stack_hist}; [ "${name#*@}" != "$name" ] && { kern=${name#*@}; name=${name%%@*}; }
       for grp in FETCH_SIZE WRITE_SIZE; do
         timeout -s KILL 180 rocprofv3 --pmc $grp --output-format csv -d "$O/${name}_$grp" -o run -- \
           python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ${args//,/ } > "$O/${name}_$grp.log" 2>&1 \
           || fail "pmc $grp" "$O/${name}_$grp.log"
       done
-      python3 scripts/pmc_traffic.py "$O/${name}_FETCH_SIZE" "$O/${name}_WRITE_SIZE" "${PMC_KERNEL:-k_stack_hist}" \
-        "$O/${name}_traffic.json" || fail "pmc parse" ;;
+      python3 scripts/pmc_traffic.py "$O/${name}_FETCH_SIZE" "$O/${name}_WRITE_SIZE" "$kern" \
+        "$O/${name}_traffic.json" ${PMC_STEPS:-1} || fail "pmc parse" ;;
     sq)
       name=${spec%%:*}; rest=${spec#*:}; ctrs=${rest%%:*}; args=""; [ "$ctrs" != "$rest" ] && args=${rest#*:}
       timeout -s KILL 180 rocprofv3 --pmc ${ctrs//+/ } --output-format csv -d "$O/$name" -o run -- \

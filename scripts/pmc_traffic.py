@@ -1,6 +1,8 @@
 """Per-launch HBM traffic of a kernel from rocprofv3 FETCH_SIZE / WRITE_SIZE passes.
 
-usage: pmc_traffic.py <fetch_run_dir> <write_run_dir> <kernel_substring> <out.json>
+usage: pmc_traffic.py <fetch_run_dir> <write_run_dir> <kernel_substring>[,<kernel_substring>...] <out.json> [steps]
+
+With several kernels: totals over all their dispatches divided by the number of steps run.
 
 Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE / WRITE_SIZE are in KiB;
 on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced streaming read
@@ -24,20 +26,49 @@ def per_dispatch(path, kernel, counter):
     return sum(vals) / len(vals), len(vals)
 
 
+def totals(path, kernel, counter):
+    """sum and dispatch count of `counter` over every dispatch whose name contains `kernel`"""
+    tot, n = 0.0, 0
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if kernel in row["Kernel_Name"] and row["Counter_Name"] == counter:
+                tot += float(row["Counter_Value"])
+                n += 1
+    return tot, n
+
+
 def main():
     fdir, wdir, kernel, out = sys.argv[1:5]
-    fetch_kib, nf = per_dispatch(f"{fdir}/run_counter_collection.csv", kernel, "FETCH_SIZE")
-    write_kib, nw = per_dispatch(f"{wdir}/run_counter_collection.csv", kernel, "WRITE_SIZE")
-    res = {
-        "kernel": kernel,
-        "fetch_size_kib_raw": fetch_kib,
-        "write_size_kib_raw": write_kib,
-        "dispatches": [nf, nw],
-        "read_bytes": fetch_kib * 1024 * 2,
-        "write_bytes": write_kib * 1024,
-        "correction": "FETCH_SIZE x 2 (gfx950, 128-B requests tallied at 64 B), KiB -> B",
-    }
-    res["traffic_bytes"] = res["read_bytes"] + res["write_bytes"]
+    if "," in kernel:
+        # several kernels of one step (registration): totals per step over `runs` executed steps
+        runs = int(sys.argv[5]) if len(sys.argv) > 5 else 1
+        res = {"kernels": {}, "steps_profiled": runs,
+               "correction": "FETCH_SIZE x 2 (gfx950, 128-B requests tallied at 64 B), KiB -> B; calibrated for "
+                             "16-B-per-lane streaming reads only (MI355X_MICROARCH.md): the raw KiB are kept"}
+        rb = wb = 0.0
+        for k in kernel.split(","):
+            fk, nf = totals(f"{fdir}/run_counter_collection.csv", k, "FETCH_SIZE")
+            wk, nw = totals(f"{wdir}/run_counter_collection.csv", k, "WRITE_SIZE")
+            res["kernels"][k] = {"fetch_size_kib_raw_per_step": fk / runs, "write_size_kib_raw_per_step": wk / runs,
+                                 "dispatches": [nf, nw],
+                                 "read_bytes_per_step": fk * 1024 * 2 / runs, "write_bytes_per_step": wk * 1024 / runs}
+            rb += fk * 1024 * 2 / runs
+            wb += wk * 1024 / runs
+        res["read_bytes_per_step"], res["write_bytes_per_step"] = rb, wb
+        res["traffic_bytes_per_step"] = rb + wb
+    else:
+        fetch_kib, nf = per_dispatch(f"{fdir}/run_counter_collection.csv", kernel, "FETCH_SIZE")
+        write_kib, nw = per_dispatch(f"{wdir}/run_counter_collection.csv", kernel, "WRITE_SIZE")
+        res = {
+            "kernel": kernel,
+            "fetch_size_kib_raw": fetch_kib,
+            "write_size_kib_raw": write_kib,
+            "dispatches": [nf, nw],
+            "read_bytes": fetch_kib * 1024 * 2,
+            "write_bytes": write_kib * 1024,
+            "correction": "FETCH_SIZE x 2 (gfx950, 128-B requests tallied at 64 B), KiB -> B",
+        }
+        res["traffic_bytes"] = res["read_bytes"] + res["write_bytes"]
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))

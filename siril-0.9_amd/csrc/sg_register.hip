@@ -580,79 +580,134 @@ __device__ __forceinline__ void sg_unit(int m, double &c, double &s) {
 	s *= sg;
 }
 
-/* in-register DFT of an odd prime R: y_k = sum_j v_j w^{jk}, w = exp(-+2 pi i / R) */
+/* in-register DFT of an odd prime R: y_k = sum_j v_j w^{jk}, w = exp(-+2 pi i / R), from the
+ * symmetric sums t_j = v_j + v_{R-j} and differences u_j = v_j - v_{R-j} (j <= R/2): y_k and
+ * y_{R-k} share a = v_0 + sum_j t_j cos(2 pi jk / R) and b = sum_j u_j sin(2 pi jk / R),
+ * y_k = a -+ i b, y_{R-k} = a +- i b (half the multiplies of the direct sum and ~half its live
+ * registers: the radix-7 pass spilled at 128 VGPRs with the direct form).  Its rounding is far
+ * below the fp64 tie tolerance (sg_reg_tol). */
 template <int R>
 __device__ __forceinline__ void sg_dft_odd(sg_c64 (&v)[R], bool inv) {
-	sg_c64 y[R];
+	constexpr int H = R / 2;
+	sg_c64 t[H + 1], u[H + 1];
+	double y0x = v[0].x, y0y = v[0].y;
 #pragma unroll
-	for (int k = 0; k < R; k++) {
-		double re = 0.0, im = 0.0;
+	for (int j = 1; j <= H; j++) {
+		t[j] = make_double2(v[j].x + v[R - j].x, v[j].y + v[R - j].y);
+		u[j] = make_double2(v[j].x - v[R - j].x, v[j].y - v[R - j].y);
+		y0x += t[j].x;
+		y0y += t[j].y;
+	}
 #pragma unroll
-		for (int j = 0; j < R; j++) {
+	for (int k = 1; k <= H; k++) {
+		double ax = v[0].x, ay = v[0].y, bx = 0.0, by = 0.0;
+#pragma unroll
+		for (int j = 1; j <= H; j++) {
 			double c, sn;
 			sg_unit<R>((j * k) % R, c, sn);
-			if (inv)
-				sn = -sn;
-			/* v_j (c - i sn) */
-			re += v[j].x * c + v[j].y * sn;
-			im += v[j].y * c - v[j].x * sn;
+			ax += t[j].x * c;
+			ay += t[j].y * c;
+			bx += u[j].x * sn;
+			by += u[j].y * sn;
 		}
-		y[k] = make_double2(re, im);
+		/* forward: y_k = a - i b = (ax + by, ay - bx); inverse: a + i b */
+		if (!inv) {
+			v[k] = make_double2(ax + by, ay - bx);
+			v[R - k] = make_double2(ax - by, ay + bx);
+		} else {
+			v[k] = make_double2(ax - by, ay + bx);
+			v[R - k] = make_double2(ax + by, ay - bx);
+		}
 	}
-#pragma unroll
-	for (int k = 0; k < R; k++)
-		v[k] = y[k];
+	v[0] = make_double2(y0x, y0y);
 }
 
-/* one Stockham pass of radix R, src -> dst (padded LDS indices), items strided over the block */
-template <int R>
-__device__ __forceinline__ void sg_gen_pass(const sg_c64 *src, sg_c64 *dst, int n, int Ns, const sg_c64 *__restrict__ tw,
-		bool inv) {
+/* Mixed-radix Stockham passes on one line, in place in ONE LDS buffer (72 KB at S = 4000, so
+ * two workgroups share a CU; the round-3 ping-pong between two buffers held one workgroup of 4
+ * waves per CU).  Work item j of a radix-R pass (j < n / R, k = j mod Ns) reads elements
+ * j + r n / R, twiddles them by w^(r k n / (Ns R)), and writes (j - k) R + k + r Ns: every item's
+ * inputs are loaded into registers before the barrier and stored after it.  The first pass reads
+ * the line straight from memory (ld(i)), the last pass hands its outputs to st(i, v): two LDS
+ * round trips fewer.  Items per thread: blockDim >= n / 8, and >= n / 7 when 7 divides n (host-
+ * sized), so a radix-R pass has at most 4 (R = 2), 3 (3), 2 (4, 5) or 1 (7, 8) items per thread
+ * (two radix-7 items per thread spilled at the 128 VGPRs of two workgroups per CU). */
+template <int R> struct SgGenItems { static constexpr int v = R == 2 ? 4 : (R == 3 ? 3 : (R == 8 || R == 7 ? 1 : 2)); };
+
+template <int R, bool IN_MEM, bool OUT_MEM, class LD, class ST>
+__device__ __forceinline__ void sg_gen_pass_ip(sg_c64 *buf, int n, int Ns, const sg_c64 *__restrict__ tw, bool inv,
+		LD &ld, ST &st) {
+	constexpr int MAXI = SgGenItems<R>::v;
 	const int per = n / R, tstep = n / (Ns * R);
-	for (int j = threadIdx.x; j < per; j += blockDim.x) {
-		const int k = j % Ns;
-		sg_c64 v[R];
+	sg_c64 v[MAXI][R];
 #pragma unroll
-		for (int r = 0; r < R; r++)
-			v[r] = src[sg_pad(j + r * per)];
-		if (Ns > 1) {
+	for (int it = 0; it < MAXI; it++) {
+		const int j = threadIdx.x + it * blockDim.x;
+		if (j < per) {
+			const int k = j % Ns;
 #pragma unroll
-			for (int r = 1; r < R; r++)
-				v[r] = sg_cmul(v[r], sg_twiddle(tw, n, r * k * tstep, inv));
+			for (int r = 0; r < R; r++)
+				v[it][r] = IN_MEM ? ld(j + r * per) : buf[sg_pad(j + r * per)];
+			if (Ns > 1) {
+#pragma unroll
+				for (int r = 1; r < R; r++)
+					v[it][r] = sg_cmul(v[it][r], sg_twiddle(tw, n, r * k * tstep, inv));
+			}
 		}
-		if constexpr (R == 2 || R == 4 || R == 8)
-			sg_dft_small<R, R>(v, inv);
-		else
-			sg_dft_odd<R>(v, inv);
-		const int base = (j - k) * R + k;
-#pragma unroll
-		for (int r = 0; r < R; r++)
-			dst[sg_pad(base + r * Ns)] = v[r];
 	}
-	__syncthreads();
+	if (!IN_MEM && !OUT_MEM)
+		__syncthreads();	/* in place: every input read before any output lands */
+#pragma unroll
+	for (int it = 0; it < MAXI; it++) {
+		const int j = threadIdx.x + it * blockDim.x;
+		if (j < per) {
+			const int k = j % Ns;
+			if constexpr (R == 2 || R == 4 || R == 8)
+				sg_dft_small<R, R>(v[it], inv);
+			else
+				sg_dft_odd<R>(v[it], inv);
+			const int base = (j - k) * R + k;
+#pragma unroll
+			for (int r = 0; r < R; r++) {
+				if (OUT_MEM)
+					st(base + r * Ns, v[it][r]);
+				else
+					buf[sg_pad(base + r * Ns)] = v[it][r];
+			}
+		}
+	}
+	if (!OUT_MEM)
+		__syncthreads();
 }
 
-/* the line in b0 (written and synchronised by the caller) transformed; returns the buffer
- * holding the result (b0 or b1) */
-__device__ sg_c64 *sg_gen_fft_mixed(sg_c64 *b0, sg_c64 *b1, const SgGenPlan &pl, const sg_c64 *__restrict__ tw, bool inv) {
-	sg_c64 *src = b0, *dst = b1;
-	int Ns = 1;
-	for (int q = 0; q < pl.npass; q++) {
-		const int R = pl.radix[q];
-		switch (R) {
-		case 8: sg_gen_pass<8>(src, dst, pl.n, Ns, tw, inv); break;
-		case 4: sg_gen_pass<4>(src, dst, pl.n, Ns, tw, inv); break;
-		case 2: sg_gen_pass<2>(src, dst, pl.n, Ns, tw, inv); break;
-		case 3: sg_gen_pass<3>(src, dst, pl.n, Ns, tw, inv); break;
-		case 5: sg_gen_pass<5>(src, dst, pl.n, Ns, tw, inv); break;
-		default: sg_gen_pass<7>(src, dst, pl.n, Ns, tw, inv); break;
-		}
-		Ns *= R;
-		sg_c64 *t = src;
-		src = dst;
-		dst = t;
+template <bool IN_MEM, bool OUT_MEM, class LD, class ST>
+__device__ __forceinline__ void sg_gen_pass_r(int R, sg_c64 *buf, int n, int Ns, const sg_c64 *__restrict__ tw, bool inv,
+		LD &ld, ST &st) {
+	switch (R) {
+	case 8: sg_gen_pass_ip<8, IN_MEM, OUT_MEM>(buf, n, Ns, tw, inv, ld, st); break;
+	case 4: sg_gen_pass_ip<4, IN_MEM, OUT_MEM>(buf, n, Ns, tw, inv, ld, st); break;
+	case 2: sg_gen_pass_ip<2, IN_MEM, OUT_MEM>(buf, n, Ns, tw, inv, ld, st); break;
+	case 3: sg_gen_pass_ip<3, IN_MEM, OUT_MEM>(buf, n, Ns, tw, inv, ld, st); break;
+	case 5: sg_gen_pass_ip<5, IN_MEM, OUT_MEM>(buf, n, Ns, tw, inv, ld, st); break;
+	default: sg_gen_pass_ip<7, IN_MEM, OUT_MEM>(buf, n, Ns, tw, inv, ld, st); break;
 	}
-	return src;
+}
+
+/* the n-point transform of the line ld(0..n) into st(0..n), natural order in and out */
+template <class LD, class ST>
+__device__ __forceinline__ void sg_gen_fft_mixed(sg_c64 *buf, const SgGenPlan &pl, const sg_c64 *__restrict__ tw, bool inv, LD &ld,
+		ST &st) {
+	const int n = pl.n;
+	if (pl.npass == 1) {
+		sg_gen_pass_r<true, true>(pl.radix[0], buf, n, 1, tw, inv, ld, st);
+		return;
+	}
+	sg_gen_pass_r<true, false>(pl.radix[0], buf, n, 1, tw, inv, ld, st);
+	int Ns = pl.radix[0];
+	for (int q = 1; q + 1 < pl.npass; q++) {
+		sg_gen_pass_r<false, false>(pl.radix[q], buf, n, Ns, tw, inv, ld, st);
+		Ns *= pl.radix[q];
+	}
+	sg_gen_pass_r<false, true>(pl.radix[pl.npass - 1], buf, n, Ns, tw, inv, ld, st);
 }
 
 /* Bluestein: x (n values at buf[pad(0..n)], written and synchronised by the caller) -> X in
@@ -696,14 +751,15 @@ enum { SG_GEN_FWD_U16 = 0, SG_GEN_C2C = 1, SG_GEN_INV_ARGMAX = 2, SG_GEN_INV_CAN
 /* one row of pair blockIdx.y: mode FWD_U16 (u16 rows of frames fa / fb packed a + i b, forward,
  * energies), C2C (in place, forward or inverse), INV_ARGMAX (inverse, top-2 arg-max over the
  * row), INV_CAND (inverse, candidates of a near tie) */
-__global__ void __launch_bounds__(1024)
+template <bool BLUE>
+__global__ void __launch_bounds__(BLUE ? 1024 : 640) __attribute__((amdgpu_waves_per_eu(BLUE ? 1 : 4)))
 k_gen_rows(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const int *__restrict__ fb,
 		sg_c64 *__restrict__ data, int S, SgGenPlan pl, SgGenTables tb, int mode, int inverse,
 		unsigned long long *__restrict__ energy, SgBest *__restrict__ best, const SgRegOut *__restrict__ res,
 		SgCand *__restrict__ cand) {
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 	__shared__ SgBest red[16];
-	sg_c64 *b0 = (sg_c64 *)smem, *b1 = b0 + SG_PADN(S);
+	sg_c64 *b0 = (sg_c64 *)smem;
 	const int row = blockIdx.x, pair = blockIdx.y;
 	sg_c64 *line = data + ((size_t)pair * S + row) * S;
 	const bool inv = mode >= SG_GEN_INV_ARGMAX || (mode == SG_GEN_C2C && inverse);
@@ -715,49 +771,54 @@ k_gen_rows(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const i
 		thr[0] = r.amb[0] ? r.thr[0] : INFINITY;
 		thr[1] = r.amb[1] ? r.thr[1] : INFINITY;
 	}
+	const uint16_t *pa = nullptr, *pb = nullptr;
+	const int b = mode == SG_GEN_FWD_U16 ? fb[pair] : -1;
 	if (mode == SG_GEN_FWD_U16) {
 		const size_t plane = (size_t)S * S;
-		const uint16_t *pa = sel + (size_t)fa[pair] * plane + (size_t)row * S;
-		const int b = fb[pair];
-		const uint16_t *pb = b >= 0 ? sel + (size_t)b * plane + (size_t)row * S : nullptr;
+		pa = sel + (size_t)fa[pair] * plane + (size_t)row * S;
+		pb = b >= 0 ? sel + (size_t)b * plane + (size_t)row * S : nullptr;
+	}
+	if (mode == SG_GEN_FWD_U16) {	/* the frames' energies (the rows are read again by the transform, from cache) */
 		unsigned long long ea = 0, eb = 0;
 		for (int i = threadIdx.x; i < S; i += blockDim.x) {
 			const unsigned int va = pa[i], vb = pb ? pb[i] : 0u;
 			ea += (unsigned long long)(va * va);
 			eb += (unsigned long long)(vb * vb);
-			b0[sg_pad(i)] = make_double2((double)va, (double)vb);
 		}
-		sg_energy_add(ea, eb, fa[pair], b, energy);	/* synchronises */
-	} else {
-		for (int i = threadIdx.x; i < S; i += blockDim.x)
-			b0[sg_pad(i)] = line[i];
-		__syncthreads();
-	}
-	sg_c64 *out = b0;
-	if (pl.bluestein)
-		sg_gen_fft_bluestein(b0, pl, tb.twm, tb.chirp, tb.bhat, inv);
-	else
-		out = sg_gen_fft_mixed(b0, b1, pl, tb.tw, inv);
-	if (mode <= SG_GEN_C2C) {
-		for (int i = threadIdx.x; i < S; i += blockDim.x)
-			line[i] = out[sg_pad(i)];
-		return;
+		sg_energy_add(ea, eb, fa[pair], b, energy);
 	}
 	SgTop2 ta, tbv;
 	sg_top2_init(ta);
 	sg_top2_init(tbv);
-	for (int j = threadIdx.x; j < S; j += blockDim.x) {
-		const sg_c64 c = out[sg_pad(j)];
-		const int idx = row * S + j;
-		if (mode == SG_GEN_INV_CAND) {
-			sg_cand_push(cand + 2 * pair, c.x, thr[0], idx);
-			sg_cand_push(cand + 2 * pair + 1, c.y, thr[1], idx);
+	/* element i of the input line (FWD_U16: frames a + i b) */
+	auto ld = [&](int i) -> sg_c64 {
+		if (mode == SG_GEN_FWD_U16)
+			return make_double2((double)pa[i], pb ? (double)pb[i] : 0.0);
+		return line[i];
+	};
+	/* element i of the transformed line */
+	auto st = [&](int i, sg_c64 c) {
+		if (mode <= SG_GEN_C2C) {
+			line[i] = c;
+		} else if (mode == SG_GEN_INV_CAND) {
+			sg_cand_push(cand + 2 * pair, c.x, thr[0], row * S + i);
+			sg_cand_push(cand + 2 * pair + 1, c.y, thr[1], row * S + i);
 		} else {
-			sg_top2_add(ta, c.x, idx);
-			sg_top2_add(tbv, c.y, idx);
+			sg_top2_add(ta, c.x, row * S + i);
+			sg_top2_add(tbv, c.y, row * S + i);
 		}
+	};
+	if constexpr (BLUE) {
+		for (int i = threadIdx.x; i < S; i += blockDim.x)
+			b0[sg_pad(i)] = ld(i);
+		__syncthreads();
+		sg_gen_fft_bluestein(b0, pl, tb.twm, tb.chirp, tb.bhat, inv);
+		for (int i = threadIdx.x; i < S; i += blockDim.x)
+			st(i, b0[sg_pad(i)]);
+	} else {
+		sg_gen_fft_mixed(b0, pl, tb.tw, inv, ld, st);
 	}
-	if (mode == SG_GEN_INV_CAND)
+	if (mode <= SG_GEN_C2C || mode == SG_GEN_INV_CAND)
 		return;
 	sg_best_block(ta, tbv, red);
 	if (threadIdx.x == 0) {
@@ -1170,9 +1231,22 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	while (rpb > 1 && S % rpb != 0)
 		rpb >>= 1;
 	const int xcdmap = ctx->knobs.reg_xcd;	/* A/B knob SG_REG_XCD: 0 = strips in dispatch order */
-	/* generic rows: Bluestein needs m/8 threads (sg_lds_fft), the mixed passes take 256 */
-	const int gen_thr = pl.bluestein ? (pl.m / 8 < 64 ? 64 : pl.m / 8) : 256;
-	const size_t gen_lds = pl.bluestein ? (size_t)SG_PADN(pl.m) * sizeof(sg_c64) : 2 * row_lds;
+	/* generic rows: Bluestein needs m/8 threads (sg_lds_fft), the mixed passes ceil(S / 8) (ceil(S / 7)
+	 * with a radix-7 pass) rounded to whole waves (sg_gen_pass_ip's items per thread) */
+	bool has7 = false;
+	for (int q = 0; q < pl.npass; q++)
+		has7 |= pl.radix[q] == 7;
+	const int gen_thr = pl.bluestein ? (pl.m / 8 < 64 ? 64 : pl.m / 8)
+					 : std::max(64, ((has7 ? (S + 6) / 7 : (S + 7) / 8) + 63) / 64 * 64);
+	const size_t gen_lds = pl.bluestein ? (size_t)SG_PADN(pl.m) * sizeof(sg_c64) : row_lds;
+	/* one instantiation per transform kind (register allocation is per kernel) */
+	const void *k_rows = pl.bluestein ? (const void *)k_gen_rows<true> : (const void *)k_gen_rows<false>;
+	auto gen_rows = [&](dim3 grid, auto... a) {
+		if (pl.bluestein)
+			hipLaunchKernelGGL(k_gen_rows<true>, grid, dim3(gen_thr), gen_lds, s, a...);
+		else
+			hipLaunchKernelGGL(k_gen_rows<false>, grid, dim3(gen_thr), gen_lds, s, a...);
+	};
 	if (!generic) {
 		(void)hipFuncSetAttribute((const void *)k_reg_cols<sg_c64, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)colh_lds);
@@ -1199,7 +1273,7 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower<float2, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)colh_lds32);
 	} else {
-		(void)hipFuncSetAttribute((const void *)k_gen_rows, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gen_lds);
+		(void)hipFuncSetAttribute(k_rows, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gen_lds);
 	}
 
 	/* device workspace: reference spectrum (fp64, and fp32 behind it), pair planes, per-row
@@ -1259,17 +1333,17 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	/* generic passes up to the cross power's inverse: transposed spectrum of the rows of `fa`
 	 * / `fb` pairs -> `work` holds the pairs' inverse column transforms in row layout */
 	auto gen_forward = [&](const int *fa, const int *fb, int np, unsigned long long *en) -> int {
-		hipLaunchKernelGGL(k_gen_rows, dim3(S, np), dim3(gen_thr), gen_lds, s, d_sel, fa, fb, work, S, pl, tbl,
+		gen_rows(dim3(S, np), d_sel, fa, fb, work, S, pl, tbl,
 				(int)SG_GEN_FWD_U16, 0, en, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
 		HIPCHK(hipGetLastError());
 		hipLaunchKernelGGL(k_gen_transpose, dim3(tgrid.x, tgrid.y, np), dim3(32, 8), 0, s, (const sg_c64 *)work, work2, S);
 		HIPCHK(hipGetLastError());
-		hipLaunchKernelGGL(k_gen_rows, dim3(S, np), dim3(gen_thr), gen_lds, s, d_sel, fa, fb, work2, S, pl, tbl,
+		gen_rows(dim3(S, np), d_sel, fa, fb, work2, S, pl, tbl,
 				(int)SG_GEN_C2C, 0, en, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
 		HIPCHK(hipGetLastError());
 		hipLaunchKernelGGL(k_gen_xpower, dim3(1024, np), dim3(256), 0, s, work2, (const sg_c64 *)spec, S);
 		HIPCHK(hipGetLastError());
-		hipLaunchKernelGGL(k_gen_rows, dim3(S, np), dim3(gen_thr), gen_lds, s, d_sel, fa, fb, work2, S, pl, tbl,
+		gen_rows(dim3(S, np), d_sel, fa, fb, work2, S, pl, tbl,
 				(int)SG_GEN_C2C, 1, en, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
 		HIPCHK(hipGetLastError());
 		hipLaunchKernelGGL(k_gen_transpose, dim3(tgrid.x, tgrid.y, np), dim3(32, 8), 0, s, (const sg_c64 *)work2, work, S);
@@ -1326,12 +1400,12 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 
 	/* reference spectrum R = FFT2(ref) (half layout: the A' half only; generic: transposed) */
 	if (generic) {
-		hipLaunchKernelGGL(k_gen_rows, dim3(S, 1), dim3(gen_thr), gen_lds, s, d_sel, d_fa + NP, d_fb + NP, work, S, pl,
+		gen_rows(dim3(S, 1), d_sel, d_fa + NP, d_fb + NP, work, S, pl,
 				tbl, (int)SG_GEN_FWD_U16, 0, energy, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
 		HIPCHK(hipGetLastError());
 		hipLaunchKernelGGL(k_gen_transpose, dim3(tgrid.x, tgrid.y, 1), dim3(32, 8), 0, s, (const sg_c64 *)work, spec, S);
 		HIPCHK(hipGetLastError());
-		hipLaunchKernelGGL(k_gen_rows, dim3(S, 1), dim3(gen_thr), gen_lds, s, d_sel, d_fa + NP, d_fb + NP, spec, S, pl,
+		gen_rows(dim3(S, 1), d_sel, d_fa + NP, d_fb + NP, spec, S, pl,
 				tbl, (int)SG_GEN_C2C, 0, energy, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
 	} else if (fp32) {
 		hipLaunchKernelGGL(k_reg_rows_fwd_half<float2>, dim3(S / rpb, 1), dim3(row_thr), row_lds32, s, d_sel, d_fa + NP,
@@ -1360,7 +1434,7 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		if (generic) {
 			if (int r = gen_forward(d_fa + p0, d_fb + p0, np, energy))
 				return r;
-			hipLaunchKernelGGL(k_gen_rows, dim3(S, np), dim3(gen_thr), gen_lds, s, d_sel, d_fa + p0, d_fb + p0, work, S,
+			gen_rows(dim3(S, np), d_sel, d_fa + p0, d_fb + p0, work, S,
 					pl, tbl, (int)SG_GEN_INV_ARGMAX, 1, energy, best, (const SgRegOut *)nullptr,
 					(SgCand *)nullptr);
 		} else if (fp32) {
@@ -1441,7 +1515,7 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 			if (generic) {
 				if (int r = gen_forward(d_fa2 + p0, d_fb2 + p0, np, energy2))
 					return r;
-				hipLaunchKernelGGL(k_gen_rows, dim3(S, np), dim3(gen_thr), gen_lds, s, d_sel, d_fa2 + p0, d_fb2 + p0,
+				gen_rows(dim3(S, np), d_sel, d_fa2 + p0, d_fb2 + p0,
 						work, S, pl, tbl, (int)SG_GEN_INV_CAND, 1, energy2, best, (const SgRegOut *)(d_res2 + p0),
 						cand);
 			} else {

@@ -1301,8 +1301,6 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 	return SG_CLS_OK;
 }
 
-/* pixel column `col` of the tile (x its image column); PAIR: lane pair half `half`, else one
- * lane per column (half = 0) */
 /*
  * stack_median's pixel (src/stacking/stacking.c:746-767, REJ 8) and PERCENTILE rejection
  * (:1660-1673 + percentile_clipping :1130-1143, REJ 1) from the column histogram.  Both are
@@ -1392,6 +1390,8 @@ __device__ __forceinline__ int sgh_median_pct(const SghPix &P, int N, double sl,
 	return SG_CLS_OK;
 }
 
+/* pixel column `col` of the tile (x its image column); PAIR: lane pair half `half`, else one
+ * lane per column (half = 0) */
 template <int REJ, bool PAIR, int NI, bool ZT = false>
 __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int half, int lo, int R, int c, int x,
 		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list, bool zrow = false) {

@@ -4,7 +4,8 @@ oracle and against golden registration results (tests/golden/make_golden_fullsiz
   configs[0]  stack_summing of 16 x 1024 x 1024 u16 mono FITS files, from the files
   configs[1]  128 x 2048 x 2048 u16 mono SER file: device load, full-frame DFT registration,
               NO_REJEC mean stack with the found shifts (device and host-pull paths)
-  configs[2]  SIGMA (4, 3) stack of 512 x 4096 x 4096, the WHOLE image against the oracle
+  configs[2]  SIGMA (4, 3) stack of 512 x 4096 x 4096, the WHOLE image against the oracle; the
+              same frames' whole stack_median and PERCENTILE images (histogram rank path)
   configs[3]  the same stack as 8 row bands (the multi-GPU partition, band-only residency
               windows) equal to the one-call image
   configs[4]  256 x 3 x 4000 x 6000: DFT registration of layer 1's centred 2048 selection,
@@ -176,6 +177,39 @@ def test_cfg2_sigma_whole_image_and_cfg3_bands(gpu_ctx):
     assert rc == 0
     bad = np.argwhere(img != ref[0])
     assert bad.size == 0, f"{len(bad)} pixels differ from the oracle, first {bad[:3].tolist()}"
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+
+
+def test_cfg2_median_and_percentile_whole_image(gpu_ctx):
+    """configs[2]'s frames through the histogram rank path of stack_median
+    (src/stacking/stacking.c:746-767) and PERCENTILE (0.2, 0.1) rejection (:1660-1673), the whole
+    512 x 4096^2 image (and the counters) against the oracle"""
+    import torch
+    frames, sx, sy, (N, H, W, M) = _sigma_cfg2(gpu_ctx)
+    out = torch.zeros(H * W, dtype=torch.int16, device="cuda")
+    dmed, km = sg.make_desc(sg.MEDIAN, N, W, H, 1, max_thread=16, max_number_of_rows=H)
+    torch.cuda.synchronize()
+    gpu_ctx.stack_device(dmed, frames.data_ptr(), H * W, H * W, out.data_ptr(), 0, H)
+    assert gpu_ctx.stats().path == 1
+    med = out.cpu().numpy().view(np.uint16).reshape(H, W).copy()
+    dpct, kp = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=sg.PERCENTILE, sig=(0.2, 0.1), shiftx=sx, shifty=sy,
+                            max_thread=16, max_number_of_rows=H)
+    rej, _ = gpu_ctx.stack_device(dpct, frames.data_ptr(), H * W, H * W, out.data_ptr(), 0, H)
+    assert gpu_ctx.stats().path == 1
+    pct = out.cpu().numpy().view(np.uint16).reshape(H, W)
+    host = frames.cpu().numpy().view(np.uint16).reshape(N, 1, H, W)
+    del frames, out
+    _free()
+    rc, ref = orc.stack_median(host, max_thread=16, max_number_of_rows=H)
+    assert rc == 0
+    bad = np.argwhere(med != ref[0])
+    assert bad.size == 0, f"median: {len(bad)} pixels differ from the oracle, first {bad[:3].tolist()}"
+    del ref
+    rc, ref, rej_ref = orc.stack_rejection(host, sg.PERCENTILE, sig=(0.2, 0.1), shiftx=sx, shifty=sy,
+                                           max_thread=16, max_number_of_rows=H)
+    assert rc == 0
+    bad = np.argwhere(pct != ref[0])
+    assert bad.size == 0, f"percentile: {len(bad)} pixels differ from the oracle, first {bad[:3].tolist()}"
     assert np.array_equal(rej, rej_ref), (rej, rej_ref)
 
 

@@ -84,7 +84,7 @@ def _numpy_shifts(sel, ref=0):
     return sx, sy
 
 
-@pytest.mark.parametrize("S", [6, 12, 48, 97, 100, 105, 120])
+@pytest.mark.parametrize("S", [6, 7, 12, 35, 48, 97, 100, 105, 120])
 def test_register_any_side_matches_oracle(gpu_ctx, S):
     """mixed radix (2, 3, 5, 7 factors) and Bluestein (97: prime) against the oracle's
     mixed-radix DFT, shifts and qualities exactly"""
@@ -97,9 +97,10 @@ def test_register_any_side_matches_oracle(gpu_ctx, S):
     assert _same_q(gq, rq), (gq, rq)
 
 
-@pytest.mark.parametrize("S", [1500, 1009, 1234])
+@pytest.mark.parametrize("S", [1500, 2940, 1009, 1234])
 def test_register_large_non_power_of_two(gpu_ctx, S):
-    """1500 = 2^2 3 5^3 (mixed radix), 1009 (prime) and 1234 = 2 x 617 (Bluestein, m = 4096):
+    """1500 = 2^2 3 5^3 and 2940 = 2^2 3 5 7^2 (mixed radix, in-place LDS passes), 1009 (prime)
+    and 1234 = 2 x 617 (Bluestein, m = 4096):
     the arg-max equals an independent numpy FFT's (translations recovered to a pixel);
     qualities equal the oracle's QualityEstimate"""
     n, M = 6, 12
