@@ -131,6 +131,13 @@ int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *desc, sg_read_region_fn pull,
  * outside the band, and is then recomputed from the frames.  If its rows are not resident
  * the call fails with SG_ERR_GENERIC instead of guessing: for such stacks (in practice
  * small N with strong rejection) make the full frames resident.
+ *
+ * Refused regime (both entry points): a MEAN stack (stack_mean_with_rejection, any rejection;
+ * stack_median ignores shifts) whose shifts make a row block
+ * of the reference's partition (max_thread, max_number_of_rows; :1397-1476) with start_row > 0
+ * read above the frame.  The reference then writes offset = W*(area.y - shifty) past its block
+ * buffer (stacking.c:1555-1561, a heap overflow with an undefined result); the call fails with
+ * SG_ERR_GENERIC and a message instead of zero-filling.  Keep |shifty| below the block height.
  */
 int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_desc *desc,
 		const uint16_t *d_frames, int64_t frame_stride, int64_t plane_stride,

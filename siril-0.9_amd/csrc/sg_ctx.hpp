@@ -113,11 +113,15 @@ struct SgKnobs {
 		qgrad_threads = (qg == 64 || qg == 128 || qg == 256) ? qg : 128;
 		reg_batch = sg_env_int("SG_REG_BATCH", 1, 1024, 0);
 		reg_cw = sg_env_int("SG_REG_CW", 1, 64, 0);
+		while (reg_cw & (reg_cw - 1))	/* strips of a power of two columns (the FFT helpers split indices by shifts) */
+			reg_cw &= reg_cw - 1;
 		reg_path = sg_env_int("SG_REG_PATH", 2, 3, 2);
 		reg_xcd = sg_env_int("SG_REG_XCD", 0, 1, 1);
 		reg_pb = sg_env_int("SG_REG_PB", 1, 64, 1);
 		reg_fp = sg_env_int("SG_REG_FP", 32, 64, 32) == 64 ? 64 : 32;
 		reg_cw32 = sg_env_int("SG_REG_CW32", 1, 16, 4);
+		while (reg_cw32 & (reg_cw32 - 1))
+			reg_cw32 &= reg_cw32 - 1;
 		reg_colocc = sg_env_int("SG_REG_COLOCC", 0, 1, 1);
 		reg_rpb = sg_env_int("SG_REG_RPB", 1, 64, 4);
 	}

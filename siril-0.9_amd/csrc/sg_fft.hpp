@@ -29,6 +29,17 @@ __device__ __forceinline__ int sg_pad(int i) {
 	return i + (i >> 3);
 }
 #define SG_PADN(n) ((n) + ((n) >> 3))
+/* element stride between the columns of a column-strip kernel (k_reg_cols, k_reg_cols_xpower):
+ * float2 strips +4 so that the batch-minor passes (4 columns x 8 consecutive elements per 32-lane
+ * group: the last FFT pass, the cross power, the inverse's first pass) and the first pass's
+ * stores fall on distinct banks -- a bank model of the S = 2048 pass (64 banks for ds_read_b64,
+ * 32 for ds_write_b64, MI355X_MICROARCH.md LDS) gives 1.54x the conflict-free LDS cycles against
+ * 2.62x at +1, and SQ_LDS_BANK_CONFLICT of the pass was 2.05x its active LDS cycles
+ * (profiles/r04r_sq_register_1.txt); double2 strips keep +1 */
+template <class C>
+__host__ __device__ constexpr int sg_col_stride(int S) {
+	return SG_PADN(S) + (sizeof(C) == 8 ? 4 : 1);
+}
 
 /* complex arithmetic for C = double2 (the default, every path) or float2 (the fp32 power-of-two
  * passes, whose near ties are re-run in fp64) */
@@ -112,11 +123,18 @@ __device__ __forceinline__ C sg_twiddle(const C *__restrict__ tw, int n, int k, 
 	return (inv ? tw + n : tw)[k];
 }
 
+/* log2 of a power of two (a uniform value: scalar code); the batched transforms of this file
+ * have power-of-two n, batch counts nb and strides, so item indices split with shifts and masks
+ * instead of the integer divisions (v_rcp / v_mul_hi sequences) a runtime divisor costs */
+__device__ __forceinline__ int sg_log2(int x) {
+	return __builtin_ctz((unsigned)x);
+}
+
 template <int R, int EPT = 8, class C>
 __device__ __forceinline__ void sg_stockham_pass(C *buf, int n, int nb, int bstride, int Ns,
 		const C *__restrict__ tw, bool inv) {
 	constexpr int MAXI = EPT / R;	/* work items per thread: nb * n <= EPT * blockDim (host-sized launches) */
-	const int per = n / R, items = nb * per;
+	const int per = n / R, items = nb * per, lper = sg_log2(per), lks = sg_log2(n / (Ns * R));
 	C v[MAXI][R], w[MAXI][R];
 	const bool twiddled = Ns > 1;	/* the first pass (Ns = 1) multiplies by w^0 = 1 only */
 	/* load every item's R inputs before anyone stores (in-place pass); the twiddles are
@@ -125,14 +143,14 @@ __device__ __forceinline__ void sg_stockham_pass(C *buf, int n, int nb, int bstr
 	for (int it = 0; it < MAXI; it++) {
 		const int t = threadIdx.x + it * blockDim.x;
 		if (t < items) {
-			const int b = t / per, j = t - b * per;
-			const C *x = buf + (size_t)b * bstride;
+			const int b = t >> lper, j = t & (per - 1);
+			const C *x = buf + b * bstride;
 #pragma unroll
 			for (int r = 0; r < R; r++)
 				v[it][r] = x[sg_pad(j + r * per)];
 			if (twiddled) {
 				const int jm = j & (Ns - 1);
-				const int kstep = jm * (n / (Ns * R));
+				const int kstep = jm << lks;
 #pragma unroll
 				for (int r = 1; r < R; r++)
 					w[it][r] = sg_twiddle(tw, n, r * kstep, inv);
@@ -144,7 +162,7 @@ __device__ __forceinline__ void sg_stockham_pass(C *buf, int n, int nb, int bstr
 	for (int it = 0; it < MAXI; it++) {
 		const int t = threadIdx.x + it * blockDim.x;
 		if (t < items) {
-			const int b = t / per, j = t - b * per;
+			const int b = t >> lper, j = t & (per - 1);
 			const int jm = j & (Ns - 1);
 			if (twiddled) {
 #pragma unroll
@@ -152,7 +170,7 @@ __device__ __forceinline__ void sg_stockham_pass(C *buf, int n, int nb, int bstr
 					v[it][r] = sg_cmul(v[it][r], w[it][r]);
 			}
 			sg_dft_small<R, R>(v[it], inv);
-			C *y = buf + (size_t)b * bstride;
+			C *y = buf + b * bstride;
 			const int base = (j - jm) * R + jm;
 #pragma unroll
 			for (int r = 0; r < R; r++)
@@ -213,12 +231,12 @@ __device__ __forceinline__ void sg_fft_io(C *buf, int n, int nb, int bstride, co
 	constexpr int FI = EPT / 8;
 	C v[FI][8];
 	{
-		const int per = n >> 3, items = nb * per;
+		const int per = n >> 3, items = nb * per, lnb = sg_log2(nb);
 #pragma unroll
 		for (int it = 0; it < FI; it++) {
 			const int t = threadIdx.x + it * blockDim.x;
 			if (t < items) {
-				const int b = t % nb, j = t / nb;
+				const int b = t & (nb - 1), j = t >> lnb;
 #pragma unroll
 				for (int r = 0; r < 8; r++)
 					v[it][r] = ld(b, j + r * per);
@@ -239,14 +257,14 @@ __device__ __forceinline__ void sg_fft_io_regs(C *buf, int n, int nb, int bstrid
 		bool inv, C (&v)[EPT / 8][8], ST st) {
 	{
 		constexpr int FI = EPT / 8;
-		const int per = n >> 3, items = nb * per;
+		const int per = n >> 3, items = nb * per, lnb = sg_log2(nb);
 #pragma unroll
 		for (int it = 0; it < FI; it++) {
 			const int t = threadIdx.x + it * blockDim.x;
 			if (t < items) {
-				const int b = t % nb, j = t / nb;
+				const int b = t & (nb - 1), j = t >> lnb;
 				sg_dft_small<8, 8>(v[it], inv);
-				C *y = buf + (size_t)b * bstride;
+				C *y = buf + b * bstride;
 #pragma unroll
 				for (int r = 0; r < 8; r++)
 					y[sg_pad(j * 8 + r)] = v[it][r];
@@ -265,13 +283,13 @@ __device__ __forceinline__ void sg_fft_io_regs(C *buf, int n, int nb, int bstrid
 	auto last = [&](auto RC) {
 		constexpr int R = decltype(RC)::value;
 		constexpr int MAXI = EPT / R;
-		const int per = n / R, items = nb * per;
+		const int per = n / R, items = nb * per, lnb = sg_log2(nb);
 #pragma unroll
 		for (int it = 0; it < MAXI; it++) {
 			const int t = threadIdx.x + it * blockDim.x;
 			if (t < items) {
-				const int b = t % nb, j = t / nb;
-				const C *x = buf + (size_t)b * bstride;
+				const int b = t & (nb - 1), j = t >> lnb;
+				const C *x = buf + b * bstride;
 				C v[R];
 #pragma unroll
 				for (int r = 0; r < R; r++)
@@ -332,6 +350,37 @@ __device__ __forceinline__ void sg_top2_wave(SgTop2 &a) {
 		const int i = __shfl_down(a.i, o, 64);
 		sg_top2_merge(a, v, v2, i);
 	}
+}
+
+/* a thread's own top-2 in the precision of its transform (float for the fp32 passes: the
+ * comparisons are those of the exactly converted doubles), branch-free: the update of
+ * sg_top2_add as selects instead of a divergent branch per element; widened to SgTop2 for the
+ * block reduction */
+template <class T> struct SgTop2T {
+	T v, v2;
+	int i;
+};
+template <class T>
+__device__ __forceinline__ void sg_top2t_init(SgTop2T<T> &t) {
+	t.v = -INFINITY;
+	t.v2 = -INFINITY;
+	t.i = 0x7fffffff;
+}
+template <class T>
+__device__ __forceinline__ void sg_top2t_add(SgTop2T<T> &a, T v, int i) {
+	const bool nb = v > a.v || (v == a.v && i < a.i);
+	a.v2 = nb ? a.v : fmax(a.v2, v);
+	a.v = nb ? v : a.v;
+	a.i = nb ? i : a.i;
+}
+template <class T>
+__device__ __forceinline__ SgTop2 sg_top2t_wide(const SgTop2T<T> &a) {
+	SgTop2 t;
+	t.v = (double)a.v;
+	t.v2 = (double)a.v2;
+	t.i = a.i;
+	t.pad = 0;
+	return t;
 }
 
 /* per-pair arg-max partial of the two frames a (real part) and b (imaginary part) */

@@ -54,7 +54,7 @@ k_reg_cols(C *__restrict__ work, int S, int logS, int CW, const C *__restrict__ 
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 	C *buf = (C *)smem;
 	const int x0 = sg_xcd_strip(blockIdx.x, gridDim.x, xcdmap) * CW, pair = blockIdx.y;
-	const int bstride = SG_PADN(S) + 1;
+	const int bstride = sg_col_stride<C>(S);
 	C *base = work + (size_t)pair * S * S + x0;
 	(void)logS;
 	sg_fft_io<false, EPT>(buf, S, CW, bstride, tw, inverse != 0, [&](int c, int r) { return base[(size_t)r * S + c]; },
@@ -185,11 +185,11 @@ k_reg_cols_xpower(C *__restrict__ work, const C *__restrict__ spec, int S, int C
 		x0 = strip * CW;
 	}
 	typedef typename SgReal<C>::T T;
-	const int bstride = SG_PADN(S) + 1, H = S >> 1;
+	const int bstride = sg_col_stride<C>(S), H = S >> 1;
 	C *base = work + (size_t)pair * S * S + x0;
 	auto slot = [&](int c, int r) -> C & { return buf[(size_t)c * bstride + sg_pad(r)]; };
 	constexpr int NI = EPT;
-	const int items = CW * S;
+	const int items = CW * S, lcw = sg_log2(CW);	/* CW: a power of two */
 	/* the reference's packed column 0 (a strip starting at kx = 0 of either half) also needs
 	 * R(-ky): read where it is used, so the other strips keep no second register array */
 	C rk[NI];
@@ -199,7 +199,7 @@ k_reg_cols_xpower(C *__restrict__ work, const C *__restrict__ spec, int S, int C
 			const int t = threadIdx.x + it * blockDim.x;
 			rk[it] = sg_mk<C>((T)0, (T)0);
 			if (t < items) {
-				const int c = t % CW, ky = t / CW, kx = (x0 + c) & (H - 1);
+				const int c = t & (CW - 1), ky = t >> lcw, kx = (x0 + c) & (H - 1);
 				rk[it] = spec[(size_t)ky * S + kx];
 			}
 		}
@@ -213,7 +213,7 @@ k_reg_cols_xpower(C *__restrict__ work, const C *__restrict__ spec, int S, int C
 		const int t = threadIdx.x + it * blockDim.x;
 		if (t >= items)
 			continue;
-		const int c = t % CW, ky = t / CW, kx = (x0 + c) & (H - 1);
+		const int c = t & (CW - 1), ky = t >> lcw, kx = (x0 + c) & (H - 1);
 		if (kx) {
 			slot(c, ky) = sg_rconj(rk[it], slot(c, ky));
 			continue;
@@ -309,9 +309,9 @@ k_reg_rows_inv_half_argmax(const C *__restrict__ work, int S, const C *__restric
 	const int row = blockIdx.x, pair = blockIdx.y, H = S >> 1;
 	const C *in = work + (size_t)pair * S * S + (size_t)row * S;
 	typedef typename SgReal<C>::T T;
-	SgTop2 ta, tb;
-	sg_top2_init(ta);
-	sg_top2_init(tb);
+	SgTop2T<T> ta, tb;
+	sg_top2t_init(ta);
+	sg_top2t_init(tb);
 	double thr[2] = {INFINITY, INFINITY};
 	if (CAND) {
 		const SgRegOut r = res[pair];
@@ -344,15 +344,16 @@ k_reg_rows_inv_half_argmax(const C *__restrict__ work, int S, const C *__restric
 					sg_cand_push(cand + 2 * pair + 1, c.y, thr[1], idx);
 					return;
 				}
-				sg_top2_add(ta, c.x, idx);
-				sg_top2_add(tb, c.y, idx);
+				sg_top2t_add(ta, c.x, idx);
+				sg_top2t_add(tb, c.y, idx);
 			});
 	if (CAND)
 		return;
-	sg_best_block(ta, tb, red);
+	SgTop2 wa = sg_top2t_wide(ta), wb = sg_top2t_wide(tb);
+	sg_best_block(wa, wb, red);
 	if (threadIdx.x == 0) {
-		best[(size_t)pair * S + row].a = ta;
-		best[(size_t)pair * S + row].b = tb;
+		best[(size_t)pair * S + row].a = wa;
+		best[(size_t)pair * S + row].b = wb;
 	}
 }
 
@@ -1216,7 +1217,7 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	const int row_thr = thr_for(S);
 	/* half-spectrum columns: a strip stays inside one half (CW divides S/2) */
 	const int CWh = CW < S / 2 ? CW : S / 2;
-	const size_t colh_lds = (size_t)CWh * (SG_PADN(S) + 1) * sizeof(sg_c64);
+	const size_t colh_lds = (size_t)CWh * sg_col_stride<sg_c64>(S) * sizeof(sg_c64);
 	const int colh_thr = thr_for(CWh * S);
 	/* fp32 columns: CW32 columns per strip (8: 64-B row segments), 16 elements per thread */
 	int CW32 = ctx->knobs.reg_cw32;
@@ -1224,7 +1225,7 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		CW32 >>= 1;
 	const int ept32 = CW32 * S / 1024 > 8 ? 16 : 8;
 	const int colh_thr32 = std::max(64, CW32 * S / ept32);
-	const size_t colh_lds32 = (size_t)CW32 * (SG_PADN(S) + 1) * sizeof(float2);
+	const size_t colh_lds32 = (size_t)CW32 * sg_col_stride<float2>(S) * sizeof(float2);
 	const int colocc = ctx->knobs.reg_colocc;
 	/* rows per forward-row workgroup (the next row prefetched during this one's transform) */
 	int rpb = ctx->knobs.reg_rpb;
