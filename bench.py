@@ -387,7 +387,7 @@ def main_sigma(args):
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
-            "scaling": "strong" if strong else "weak",
+            "scaling": args.scaling,          # at N = 1 both forms are the same workload
             "vs_baseline": None,
             "dtype": "u16",
             "data": "synthetic (include/sg_synth.h, generated in HBM)",

@@ -980,9 +980,18 @@ static int pull_band(sg_ctx *ctx, SgDevice &dv, PullCall &pc, int nreaders, uint
 		}
 	};
 	std::vector<std::thread> th;
-	for (int r = 1; r < nreaders; r++)
-		th.emplace_back(work, r);
-	work(0);
+	int started = 1;
+	for (int r = 1; r < nreaders; r++) {
+		try {
+			th.emplace_back(work, r);
+			started++;
+		} catch (...) {	/* no thread: the frames of the readers not started go unread -> fail */
+			fail(set_err(ctx, SG_ERR_GENERIC, "could not start reader thread%s %ld", "", r));
+			break;
+		}
+	}
+	if (started == nreaders)
+		work(0);
 	for (std::thread &t : th)
 		t.join();
 	for (int r = 0; r < nreaders; r++)
@@ -1131,18 +1140,47 @@ extern "C" int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *d, sg_read_region_
 	std::vector<int> rcs((size_t)G, SG_OK);
 	std::vector<std::array<uint64_t, 6>> rj((size_t)G);
 	std::vector<uint64_t> mx((size_t)G, 0);
+	/* SUM over several devices scales with the maximum over all of them (after the join);
+	 * every other result leaves its device from the device's own thread */
+	const bool late_copy = d->method == SG_STACK_SUM && pc.multi;
+	auto copy_out = [&](int g) -> int {
+		SgDevice &dv = ctx->dev[(size_t)g];
+		const int B = rb[(size_t)g], E = rb[(size_t)g + 1];
+		HIPCHK(hipSetDevice(dv.id));
+		for (int c = 0; c < C; c++) {
+			const size_t o = ((size_t)c * H + B) * W;
+			HIPCHK(hipMemcpy(out + o, (const uint16_t *)dv.out.p + o, (size_t)(E - B) * W * sizeof(uint16_t),
+					hipMemcpyDeviceToHost));
+		}
+		return SG_OK;
+	};
 	auto run = [&](int g) {
 		uint64_t r6[3][2];
-		rcs[(size_t)g] = pull_device(ctx, g, pc, rb[(size_t)g], rb[(size_t)g + 1], nreaders, r6, &mx[(size_t)g]);
-		if (rcs[(size_t)g])
+		int r = pull_device(ctx, g, pc, rb[(size_t)g], rb[(size_t)g + 1], nreaders, r6, &mx[(size_t)g]);
+		if (r == SG_OK && !late_copy)
+			r = copy_out(g);
+		rcs[(size_t)g] = r;
+		if (r)
 			pc.stop = 1;
 		memcpy(rj[(size_t)g].data(), r6, sizeof r6);
 	};
 	{
 		std::vector<std::thread> th;
-		for (int g = 1; g < G; g++)
-			th.emplace_back(run, g);
-		run(0);
+		bool started = true;
+		for (int g = 1; g < G; g++) {
+			try {
+				th.emplace_back(run, g);
+			} catch (...) {
+				rcs[(size_t)g] = set_err(ctx, SG_ERR_GENERIC, "could not start the thread of device slot%s %ld", "", g);
+				pc.stop = 1;
+				started = false;
+				break;
+			}
+		}
+		if (started)
+			run(0);
+		else
+			rcs[0] = SG_ERR_GENERIC;
 		for (std::thread &t : th)
 			t.join();
 	}
@@ -1164,18 +1202,11 @@ extern "C" int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *d, sg_read_region_
 	uint64_t gmax = 0;
 	for (int g = 0; g < G; g++)
 		gmax = std::max(gmax, mx[(size_t)g]);
-	for (int g = 0; g < G; g++) {
-		SgDevice &dv = ctx->dev[(size_t)g];
-		const int B = rb[(size_t)g], E = rb[(size_t)g + 1];
-		if (d->method == SG_STACK_SUM && pc.multi)
-			if (int r = sum_finalize_rows(ctx, g, W, H, C, B, E, (unsigned int)gmax))
-				return r;
-		HIPCHK(hipSetDevice(dv.id));
-		for (int c = 0; c < C; c++) {
-			const size_t o = ((size_t)c * H + B) * W;
-			HIPCHK(hipMemcpy(out + o, (const uint16_t *)dv.out.p + o, (size_t)(E - B) * W * sizeof(uint16_t),
-					hipMemcpyDeviceToHost));
-		}
+	for (int g = 0; g < G && late_copy; g++) {
+		if (int r = sum_finalize_rows(ctx, g, W, H, C, rb[(size_t)g], rb[(size_t)g + 1], (unsigned int)gmax))
+			return r;
+		if (int r = copy_out(g))
+			return r;
 	}
 	if (rej)
 		for (int c = 0; c < 3; c++) {

@@ -636,13 +636,13 @@ template <int R> struct SgGenItems { static constexpr int v = R == 2 ? 4 : (R ==
 
 template <int R, bool IN_MEM, bool OUT_MEM, class LD, class ST>
 __device__ __forceinline__ void sg_gen_pass_ip(sg_c64 *buf, int n, int Ns, const sg_c64 *__restrict__ tw, bool inv,
-		LD &ld, ST &st) {
+		LD &ld, ST &st, int tid, int nt) {
 	constexpr int MAXI = SgGenItems<R>::v;
 	const int per = n / R, tstep = n / (Ns * R);
 	sg_c64 v[MAXI][R];
 #pragma unroll
 	for (int it = 0; it < MAXI; it++) {
-		const int j = threadIdx.x + it * blockDim.x;
+		const int j = tid + it * nt;
 		if (j < per) {
 			const int k = j % Ns;
 #pragma unroll
@@ -659,7 +659,7 @@ __device__ __forceinline__ void sg_gen_pass_ip(sg_c64 *buf, int n, int Ns, const
 		__syncthreads();	/* in place: every input read before any output lands */
 #pragma unroll
 	for (int it = 0; it < MAXI; it++) {
-		const int j = threadIdx.x + it * blockDim.x;
+		const int j = tid + it * nt;
 		if (j < per) {
 			const int k = j % Ns;
 			if constexpr (R == 2 || R == 4 || R == 8)
@@ -682,33 +682,40 @@ __device__ __forceinline__ void sg_gen_pass_ip(sg_c64 *buf, int n, int Ns, const
 
 template <bool IN_MEM, bool OUT_MEM, class LD, class ST>
 __device__ __forceinline__ void sg_gen_pass_r(int R, sg_c64 *buf, int n, int Ns, const sg_c64 *__restrict__ tw, bool inv,
-		LD &ld, ST &st) {
+		LD &ld, ST &st, int tid, int nt) {
 	switch (R) {
-	case 8: sg_gen_pass_ip<8, IN_MEM, OUT_MEM>(buf, n, Ns, tw, inv, ld, st); break;
-	case 4: sg_gen_pass_ip<4, IN_MEM, OUT_MEM>(buf, n, Ns, tw, inv, ld, st); break;
-	case 2: sg_gen_pass_ip<2, IN_MEM, OUT_MEM>(buf, n, Ns, tw, inv, ld, st); break;
-	case 3: sg_gen_pass_ip<3, IN_MEM, OUT_MEM>(buf, n, Ns, tw, inv, ld, st); break;
-	case 5: sg_gen_pass_ip<5, IN_MEM, OUT_MEM>(buf, n, Ns, tw, inv, ld, st); break;
-	default: sg_gen_pass_ip<7, IN_MEM, OUT_MEM>(buf, n, Ns, tw, inv, ld, st); break;
+	case 8: sg_gen_pass_ip<8, IN_MEM, OUT_MEM>(buf, n, Ns, tw, inv, ld, st, tid, nt); break;
+	case 4: sg_gen_pass_ip<4, IN_MEM, OUT_MEM>(buf, n, Ns, tw, inv, ld, st, tid, nt); break;
+	case 2: sg_gen_pass_ip<2, IN_MEM, OUT_MEM>(buf, n, Ns, tw, inv, ld, st, tid, nt); break;
+	case 3: sg_gen_pass_ip<3, IN_MEM, OUT_MEM>(buf, n, Ns, tw, inv, ld, st, tid, nt); break;
+	case 5: sg_gen_pass_ip<5, IN_MEM, OUT_MEM>(buf, n, Ns, tw, inv, ld, st, tid, nt); break;
+	default: sg_gen_pass_ip<7, IN_MEM, OUT_MEM>(buf, n, Ns, tw, inv, ld, st, tid, nt); break;
 	}
 }
 
-/* the n-point transform of the line ld(0..n) into st(0..n), natural order in and out */
-template <class LD, class ST>
+/* the n-point transform of the line, natural order in and out: FROM_MEM reads it through
+ * ld(0..n) (else it is in buf, written and synchronised by the caller), TO_MEM hands the result
+ * to st(0..n) (else it is left in buf, synchronised).  Threads tid < nt of the block take part
+ * (a block may run one line per part, all parts through the same passes and barriers). */
+template <bool FROM_MEM, bool TO_MEM, class LD, class ST>
 __device__ __forceinline__ void sg_gen_fft_mixed(sg_c64 *buf, const SgGenPlan &pl, const sg_c64 *__restrict__ tw, bool inv, LD &ld,
-		ST &st) {
+		ST &st, int tid, int nt) {
 	const int n = pl.n;
 	if (pl.npass == 1) {
-		sg_gen_pass_r<true, true>(pl.radix[0], buf, n, 1, tw, inv, ld, st);
+		if (FROM_MEM || TO_MEM) {
+			sg_gen_pass_r<FROM_MEM, TO_MEM>(pl.radix[0], buf, n, 1, tw, inv, ld, st, tid, nt);
+		} else {
+			sg_gen_pass_r<false, false>(pl.radix[0], buf, n, 1, tw, inv, ld, st, tid, nt);
+		}
 		return;
 	}
-	sg_gen_pass_r<true, false>(pl.radix[0], buf, n, 1, tw, inv, ld, st);
+	sg_gen_pass_r<FROM_MEM, false>(pl.radix[0], buf, n, 1, tw, inv, ld, st, tid, nt);
 	int Ns = pl.radix[0];
 	for (int q = 1; q + 1 < pl.npass; q++) {
-		sg_gen_pass_r<false, false>(pl.radix[q], buf, n, Ns, tw, inv, ld, st);
+		sg_gen_pass_r<false, false>(pl.radix[q], buf, n, Ns, tw, inv, ld, st, tid, nt);
 		Ns *= pl.radix[q];
 	}
-	sg_gen_pass_r<false, true>(pl.radix[pl.npass - 1], buf, n, Ns, tw, inv, ld, st);
+	sg_gen_pass_r<false, TO_MEM>(pl.radix[pl.npass - 1], buf, n, Ns, tw, inv, ld, st, tid, nt);
 }
 
 /* Bluestein: x (n values at buf[pad(0..n)], written and synchronised by the caller) -> X in
@@ -817,7 +824,7 @@ k_gen_rows(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const i
 		for (int i = threadIdx.x; i < S; i += blockDim.x)
 			st(i, b0[sg_pad(i)]);
 	} else {
-		sg_gen_fft_mixed(b0, pl, tb.tw, inv, ld, st);
+		sg_gen_fft_mixed<true, true>(b0, pl, tb.tw, inv, ld, st, (int)threadIdx.x, (int)blockDim.x);
 	}
 	if (mode <= SG_GEN_C2C || mode == SG_GEN_INV_CAND)
 		return;
@@ -865,6 +872,50 @@ k_gen_xpower(sg_c64 *__restrict__ work, const sg_c64 *__restrict__ spec, int S) 
 		if (m != i)
 			Z[m] = sg_xpower_at(zm, zk, spec[m]);
 	}
+}
+
+/* The generic column passes fused (mixed-radix plans): rows kx and (S - kx) mod S of the
+ * transposed spectrum planes (spectrum columns) in one workgroup, each half of the block one
+ * row through the same passes and barriers.  Forward transform in LDS, the packed cross power
+ * (the mirror of (kx, ky) is ((S - kx) mod S, (S - ky) mod S): the other row), inverse
+ * transform stored back: 3 plane passes instead of the 7 of rows + k_gen_xpower + rows.  Rows
+ * 0 and S/2 are their own mirror (the second half idles through the barriers).  blockDim =
+ * 2 x the row kernel's thread count (<= 1024), LDS two padded rows. */
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4)))
+k_gen_cols_xpower(sg_c64 *__restrict__ data, const sg_c64 *__restrict__ spec, int S, SgGenPlan pl,
+		const sg_c64 *__restrict__ tw) {
+	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+	const int T = (int)blockDim.x >> 1, half = (int)threadIdx.x >= T ? 1 : 0, tid = (int)threadIdx.x - half * T;
+	const int kx = blockIdx.x, pair = blockIdx.y, kxm = kx ? S - kx : 0;
+	const bool single = kxm == kx, active = !(single && half);
+	const int row = half ? kxm : kx;
+	sg_c64 *buf = (sg_c64 *)smem + half * SG_PADN(S);
+	const sg_c64 *oth = (const sg_c64 *)smem + (single ? 0 : 1 - half) * SG_PADN(S);
+	sg_c64 *line = data + ((size_t)pair * S + row) * S;
+	auto ld = [&](int i) -> sg_c64 { return active ? line[i] : make_double2(0.0, 0.0); };
+	auto st = [&](int i, sg_c64 v) {
+		if (active)
+			line[i] = v;
+	};
+	sg_gen_fft_mixed<true, false>(buf, pl, tw, false, ld, st, tid, T);
+	/* cross power: every element read (this row and the mirror row) before any is written */
+	constexpr int MX = 8;	/* S <= 8 T (T >= ceil(S / 8)) */
+	sg_c64 pv[MX];
+#pragma unroll
+	for (int it = 0; it < MX; it++) {
+		const int ky = tid + it * T;
+		if (ky < S && active)
+			pv[it] = sg_xpower_at(buf[sg_pad(ky)], oth[sg_pad(ky ? S - ky : 0)], spec[(size_t)row * S + ky]);
+	}
+	__syncthreads();
+#pragma unroll
+	for (int it = 0; it < MX; it++) {
+		const int ky = tid + it * T;
+		if (ky < S && active)
+			buf[sg_pad(ky)] = pv[it];
+	}
+	__syncthreads();
+	sg_gen_fft_mixed<false, true>(buf, pl, tw, true, ld, st, tid, T);
 }
 
 /* exact sum_n ref(n + k) img(n) (circular) at every candidate k of a near tie (below 2^56) */
@@ -1242,6 +1293,13 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	const size_t gen_lds = pl.bluestein ? (size_t)SG_PADN(pl.m) * sizeof(sg_c64) : row_lds;
 	/* one instantiation per transform kind (register allocation is per kernel) */
 	const void *k_rows = pl.bluestein ? (const void *)k_gen_rows<true> : (const void *)k_gen_rows<false>;
+	/* the fused generic column pass: mixed-radix plans whose two rows fit a block and the LDS
+	 * (SG_REG_GENFUSE=0: the three-kernel sequence, A/B) */
+	const bool gen_fuse = generic && !pl.bluestein && 2 * gen_thr <= 1024 && 2 * gen_lds <= 160 * 1024 &&
+			ctx->knobs.reg_genfuse;
+	if (gen_fuse)
+		(void)hipFuncSetAttribute((const void *)k_gen_cols_xpower, hipFuncAttributeMaxDynamicSharedMemorySize,
+				(int)(2 * gen_lds));
 	auto gen_rows = [&](dim3 grid, auto... a) {
 		if (pl.bluestein)
 			hipLaunchKernelGGL(k_gen_rows<true>, grid, dim3(gen_thr), gen_lds, s, a...);
@@ -1339,14 +1397,20 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		HIPCHK(hipGetLastError());
 		hipLaunchKernelGGL(k_gen_transpose, dim3(tgrid.x, tgrid.y, np), dim3(32, 8), 0, s, (const sg_c64 *)work, work2, S);
 		HIPCHK(hipGetLastError());
-		gen_rows(dim3(S, np), d_sel, fa, fb, work2, S, pl, tbl,
-				(int)SG_GEN_C2C, 0, en, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
-		HIPCHK(hipGetLastError());
-		hipLaunchKernelGGL(k_gen_xpower, dim3(1024, np), dim3(256), 0, s, work2, (const sg_c64 *)spec, S);
-		HIPCHK(hipGetLastError());
-		gen_rows(dim3(S, np), d_sel, fa, fb, work2, S, pl, tbl,
-				(int)SG_GEN_C2C, 1, en, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
-		HIPCHK(hipGetLastError());
+		if (gen_fuse) {	/* forward columns + cross power + inverse columns in one pass */
+			hipLaunchKernelGGL(k_gen_cols_xpower, dim3(S / 2 + 1, np), dim3(2 * gen_thr), 2 * gen_lds, s, work2,
+					(const sg_c64 *)spec, S, pl, tw);
+			HIPCHK(hipGetLastError());
+		} else {
+			gen_rows(dim3(S, np), d_sel, fa, fb, work2, S, pl, tbl,
+					(int)SG_GEN_C2C, 0, en, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
+			HIPCHK(hipGetLastError());
+			hipLaunchKernelGGL(k_gen_xpower, dim3(1024, np), dim3(256), 0, s, work2, (const sg_c64 *)spec, S);
+			HIPCHK(hipGetLastError());
+			gen_rows(dim3(S, np), d_sel, fa, fb, work2, S, pl, tbl,
+					(int)SG_GEN_C2C, 1, en, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
+			HIPCHK(hipGetLastError());
+		}
 		hipLaunchKernelGGL(k_gen_transpose, dim3(tgrid.x, tgrid.y, np), dim3(32, 8), 0, s, (const sg_c64 *)work2, work, S);
 		HIPCHK(hipGetLastError());
 		return SG_OK;

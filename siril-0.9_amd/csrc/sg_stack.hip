@@ -495,14 +495,38 @@ k_stack_sorted(SgStackParams p, const unsigned int *__restrict__ list, const uns
 	}
 	__syncthreads();
 
-	/* 1. stage the tile: frame f, slot -> stage[f][slot] */
-	for (int idx = tid; idx < N * SG_TILE_W; idx += SG_SORT_THREADS) {
-		const int f = idx >> 6, px = idx & 63;
-		const int xx = slot_x[px];
-		uint16_t v = 0;
-		if (xx >= 0)
-			v = sg_gather(p, f, slot_c[px], slot_R[px], xx);
-		stage[f * SG_STAGE_STRIDE + px] = v;
+	/* 1. stage the tile: frame f, slot -> stage[f][slot].  Lane = slot (its pixel fixed), wave w
+	 * takes frames w, w + 4, ...: a frame's shift and normalisation coefficients are wave-uniform
+	 * (scalar loads), where the flat idx loop loaded them per sample (the redo lists of
+	 * normalised stacks, ~200 k pixels, spent most of their time here) */
+	{
+		const int xx = slot_x[lane], cc = slot_c[lane], RR = slot_R[lane];
+		constexpr int NW = SG_SORT_THREADS / 64, NB = 8;
+		const uint16_t *plane = p.frames + (int64_t)cc * p.plane_stride;
+		/* NB frames per wave in flight: every lane loads from a clamped (always valid) address,
+		 * the sample is then selected (sg_gather's rules: an x-shifted sample is 0 and not
+		 * normalised, a y-shifted row reads 0 and is normalised) */
+		for (int f0 = __builtin_amdgcn_readfirstlane(wave); f0 < N; f0 += NW * NB) {
+			uint16_t raw[NB];
+			bool xin[NB];
+#pragma unroll
+			for (int k = 0; k < NB; k++) {
+				const int f = f0 + k * NW < N ? f0 + k * NW : N - 1;
+				const int sx = p.use_shift ? p.shiftx[f] : 0, sy = p.use_shift ? p.shifty[f] : 0;
+				const int sr = RR - sy, sc = xx - sx;
+				const bool yin = (unsigned)sr < (unsigned)p.H;
+				xin[k] = xx >= 0 && (unsigned)sc < (unsigned)p.W;
+				const int r = yin ? sr : 0, c = xin[k] ? sc : 0;
+				const uint16_t v = plane[(int64_t)f * p.frame_stride + (int64_t)r * p.W + c];
+				raw[k] = yin ? v : (uint16_t)0;
+			}
+#pragma unroll
+			for (int k = 0; k < NB; k++) {
+				const int f = f0 + k * NW;
+				if (f < N)
+					stage[f * SG_STAGE_STRIDE + lane] = xin[k] ? sg_normalize(p, f, raw[k]) : (uint16_t)0;
+			}
+		}
 	}
 	__syncthreads();
 

@@ -135,6 +135,23 @@ def test_register_generic_path_on_power_of_two(gpu_ctx):
     assert np.array_equal(gx, hx) and np.array_equal(gy, hy) and _same_q(gq, hq)
 
 
+@pytest.mark.parametrize("S", [105, 1500])
+def test_register_generic_fused_columns_match_unfused(gpu_ctx, S):
+    """the fused generic column pass (k_gen_cols_xpower: rows kx and S - kx of the transposed
+    spectrum in one workgroup) gives the three-kernel sequence's shifts and qualities
+    (SG_REG_GENFUSE=0)"""
+    n = 5
+    sel = orc.synth(n, 1, S, S, seed=S + 5, maxshift=min(9, S // 4))[:, 0].copy()
+    gx, gy, gq = gpu_ctx.register_dft(sel)
+    os.environ["SG_REG_GENFUSE"] = "0"
+    try:
+        with sg.Context() as c0:
+            hx, hy, hq = c0.register_dft(sel)
+    finally:
+        del os.environ["SG_REG_GENFUSE"]
+    assert np.array_equal(gx, hx) and np.array_equal(gy, hy) and _same_q(gq, hq)
+
+
 @pytest.mark.parametrize("S", [256, 2048])
 def test_register_fp32_passes_match_fp64(gpu_ctx, S):
     """the fp32 half-spectrum passes (default, SG_REG_FP=32) give the fp64 passes' shifts and
