@@ -1025,8 +1025,10 @@ __device__ __forceinline__ double lit_median(const uint16_t *s, int n) {
 }
 
 __device__ __forceinline__ double lit_sd(const uint16_t *s, int n) {
-	const double mean = f80_gsl_mean_u16(s, n);
-	const double var = f80_gsl_variance_m_u16(s, n, mean);
+	/* the double-double evaluation of the x87 recurrences (sg_f80.h; soft sg_f80 steps only near
+	 * a rounding midpoint) */
+	const double mean = f80dd_gsl_mean_u16(s, n);
+	const double var = f80dd_gsl_variance_m_u16(s, n, mean);
 	return sqrt(var * ((double)n / (double)(n - 1)));
 }
 

@@ -184,7 +184,8 @@ def test_product_never_links_oracle():
 
 
 def test_f80_soft_float_matches_x87(tmp_path):
-    """sg_f80.h (the literal path's x87 emulation) against native long double on the host"""
+    """sg_f80.h (the literal path's x87 emulation: the soft sg_f80 and the double-double
+    evaluation the device runs) against native long double on the host"""
     src = tmp_path / "t.c"
     src.write_text(r'''
 #include <stdio.h>
@@ -212,6 +213,10 @@ int main(void) {
         double gm = f80_gsl_mean_u16(d, n);
         double gv = f80_gsl_variance_m_u16(d, n, gm);
         if (gm != m || gv != v) { bad++; if (bad < 5) printf("n=%d mean %.17g %.17g var %.17g %.17g\n", n, m, gm, v, gv); }
+        /* the double-double evaluation the device uses (lit_sd) */
+        double hm = f80dd_gsl_mean_u16(d, n);
+        double hv = f80dd_gsl_variance_m_u16(d, n, hm);
+        if (hm != m || hv != v) { bad++; if (bad < 5) printf("dd n=%d mean %.17g %.17g var %.17g %.17g\n", n, m, hm, v, hv); }
         free(d);
     }
     /* the small-integer divider against the general one and native long double */
@@ -225,6 +230,24 @@ int main(void) {
         if (x.m != y.m || x.e != y.e || x.s != y.s || lx != lq) {
             bad++;
             if (bad < 5) printf("div %llx e%d / %u\n", (unsigned long long)a.m, a.e, d);
+        }
+    }
+    /* double-double x87 add / divide-by-count (with their soft fallbacks) against long double:
+     * exponent gaps up to 80, near cancellation */
+    for (int t = 0; t < 300000; t++) {
+        sg_f80 a = {rnd() | (1ull << 63), (int32_t)(rnd() % 40) - 20, (int32_t)(rnd() & 1)};
+        sg_f80 b = {rnd() | (1ull << 63), a.e - (int32_t)(rnd() % 80), (int32_t)(rnd() & 1)};
+        if (t % 3 == 0) b.m = (a.m & ~0xFFFull) | (rnd() & 0xFFF);
+        long double la = ldexpl((long double)a.m, a.e - 63) * (a.s ? -1 : 1);
+        long double lb = ldexpl((long double)b.m, b.e - 63) * (b.s ? -1 : 1);
+        sg_f80 xf = dd_to_f80(dd80_add(f80_to_dd(a), f80_to_dd(b)));
+        long double lx = xf.m ? ldexpl((long double)xf.m, xf.e - 63) * (xf.s ? -1 : 1) : 0;
+        uint32_t dv = t % 4 == 0 ? (uint32_t)(rnd() % ((1u << 20) - 1)) + 1 : (uint32_t)(rnd() % 4096) + 1;
+        sg_f80 qf = dd_to_f80(dd80_div_count(f80_to_dd(a), dv));
+        long double lq = ldexpl((long double)qf.m, qf.e - 63) * (qf.s ? -1 : 1);
+        if (lx != la + lb || lq != la / (long double)dv) {
+            bad++;
+            if (bad < 5) printf("dd op %d add %d div %d\n", t, lx != la + lb, lq != la / (long double)dv);
         }
     }
     printf("bad=%d\n", bad);
