@@ -140,6 +140,15 @@ extern "C" void sg_shutdown(sg_ctx *ctx) {
 			if (rd.stream)
 				(void)hipStreamDestroy(rd.stream);
 		}
+		if (d.aux) {
+			(void)hipStreamSynchronize(d.aux);
+			(void)hipStreamDestroy(d.aux);
+		}
+		for (int k = 0; k < 2; k++)
+			if (d.aux_ev[k])
+				(void)hipEventDestroy(d.aux_ev[k]);
+		if (d.qacc_h)
+			(void)hipHostFree(d.qacc_h);
 		(void)hipStreamDestroy(d.stream);
 	}
 	delete ctx;

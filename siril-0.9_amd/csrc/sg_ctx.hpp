@@ -41,6 +41,12 @@ struct SgDevice {
 	/* registration workspaces (sg_register.hip) */
 	SgBuf reg_sel, reg_spec, reg_work, reg_tw, reg_tw32, reg_best, reg_qbuf, reg_qacc;
 	SgBuf redo;	/* redo list of the histogram stacking path */
+	/* registration: the quality estimate runs on its own stream beside the FFT passes; its
+	 * sums come back into a pinned block, aux_ev marks them landed */
+	hipStream_t aux = nullptr;
+	hipEvent_t aux_ev[2] = {nullptr, nullptr};
+	unsigned long long *qacc_h = nullptr;
+	size_t qacc_h_n = 0;
 	SgBuf zeros;	/* zero page for out-of-frame sample loads */
 	/* stacking call inputs (shift table, normalisation coefficients, chain tables) packed into
 	 * one pinned host block and one device block: one H2D copy per call; ev[3] marks the copy

@@ -988,38 +988,66 @@ k_reg_resolve(const SgCand *__restrict__ cand, int S, int np, SgRegOut *__restri
 	out[pair] = o;
 }
 
-static int reg_quality(sg_ctx *ctx, SgDevice &dv, hipStream_t s, const uint16_t *d_sel, int S,
-		const std::vector<int> &frames, std::vector<double> &qual) {
+/* The quality estimate of `frames`, enqueued on the device's auxiliary stream (after the work
+ * already on `s`, which produced d_sel) so that it runs beside the FFT passes: its kernels are
+ * short and the passes leave the chip latency-bound.  reg_quality_finish waits for the sums and
+ * forms the values; *launched = false when the subsample loop never runs (dval = 0, :95-98). */
+static int reg_quality_launch(sg_ctx *ctx, SgDevice &dv, hipStream_t s, const uint16_t *d_sel, int S,
+		const std::vector<int> &frames, bool *launched) {
+	*launched = false;
 	const int nq = (int)frames.size();
-	qual.assign(nq, 0.0);
-	if (!nq)
-		return SG_OK;
 	const int xs = (S - 1) / 3, ys = (S - 1) / 3;
-	if (xs < 2 || ys < 2)	/* the subsample loop never runs: dval = 0 (:95-98) */
+	if (!nq || xs < 2 || ys < 2)
 		return SG_OK;
+	if (!dv.aux) {
+		HIPCHK(hipStreamCreateWithFlags(&dv.aux, hipStreamNonBlocking));
+		for (int k = 0; k < 2; k++)
+			HIPCHK(hipEventCreateWithFlags(&dv.aux_ev[k], hipEventDisableTiming));
+	}
+	if (dv.qacc_h_n < 3 * (size_t)nq) {
+		HIPCHK(hipStreamSynchronize(dv.aux));
+		if (dv.qacc_h)
+			(void)hipHostFree(dv.qacc_h);
+		dv.qacc_h = nullptr;
+		dv.qacc_h_n = 0;
+		HIPCHK(hipHostMalloc((void **)&dv.qacc_h, sizeof(unsigned long long) * 3 * nq));
+		dv.qacc_h_n = 3 * (size_t)nq;
+	}
+	HIPCHK(hipStreamSynchronize(dv.aux));	/* the previous call's buffers are free */
 	HIPCHK(ensure(dv.reg_qbuf, (size_t)nq * xs * ys * sizeof(uint16_t) + sizeof(int) * nq + 64));
 	HIPCHK(ensure(dv.reg_qacc, (size_t)nq * (3 * sizeof(unsigned long long) + sizeof(unsigned int))));
 	uint16_t *qbuf = (uint16_t *)dv.reg_qbuf.p;
 	int *d_frames = (int *)((char *)dv.reg_qbuf.p + (((size_t)nq * xs * ys * sizeof(uint16_t) + 15) & ~(size_t)15));
 	unsigned long long *acc = (unsigned long long *)dv.reg_qacc.p;
 	unsigned int *qmax = (unsigned int *)(acc + 3 * nq);
-	HIPCHK(hipMemcpyAsync(d_frames, frames.data(), sizeof(int) * nq, hipMemcpyHostToDevice, s));
-	HIPCHK(hipMemsetAsync(dv.reg_qacc.p, 0, (size_t)nq * (3 * sizeof(unsigned long long) + sizeof(unsigned int)), s));
+	HIPCHK(hipEventRecord(dv.aux_ev[1], s));
+	HIPCHK(hipStreamWaitEvent(dv.aux, dv.aux_ev[1], 0));
+	HIPCHK(hipMemcpyAsync(d_frames, frames.data(), sizeof(int) * nq, hipMemcpyHostToDevice, dv.aux));
+	HIPCHK(hipMemsetAsync(dv.reg_qacc.p, 0, (size_t)nq * (3 * sizeof(unsigned long long) + sizeof(unsigned int)), dv.aux));
 	/* one wave per workgroup, walking the row pairs: 283 us per 129 frames of 2048^2 against
 	 * 332 / 348 / 403 / 618 us with 128 / 192 / 256 / 384 threads (scripts/gpu_qsub.sh) */
 	const int qthr = ctx->knobs.qsub_threads;	/* A/B knob SG_QSUB_THREADS */
-	hipLaunchKernelGGL(k_quality_sub, dim3((ys + SG_QROWS - 1) / SG_QROWS, nq), dim3(qthr), 0, s, d_sel, d_frames, S,
+	hipLaunchKernelGGL(k_quality_sub, dim3((ys + SG_QROWS - 1) / SG_QROWS, nq), dim3(qthr), 0, dv.aux, d_sel, d_frames, S,
 			xs, ys, qbuf, qmax);
 	HIPCHK(hipGetLastError());
 	/* 2 waves per 64x16 tile: 214 us per 129 frames against 238 (4 waves) and 333 (1 wave),
 	 * scripts/gpu_qgrad.sh */
 	const int gthr = ctx->knobs.qgrad_threads;	/* A/B knob SG_QGRAD_THREADS */
-	hipLaunchKernelGGL(k_quality_grad, dim3((xs + 63) / 64, (ys + SG_QGT - 1) / SG_QGT, nq), dim3(gthr), 0, s, qbuf, xs, ys,
-			qmax, acc);
+	hipLaunchKernelGGL(k_quality_grad, dim3((xs + 63) / 64, (ys + SG_QGT - 1) / SG_QGT, nq), dim3(gthr), 0, dv.aux, qbuf, xs,
+			ys, qmax, acc);
 	HIPCHK(hipGetLastError());
-	std::vector<unsigned long long> h(3 * (size_t)nq);
-	HIPCHK(hipMemcpyAsync(h.data(), acc, sizeof(unsigned long long) * 3 * nq, hipMemcpyDeviceToHost, s));
-	HIPCHK(hipStreamSynchronize(s));
+	HIPCHK(hipMemcpyAsync(dv.qacc_h, acc, sizeof(unsigned long long) * 3 * nq, hipMemcpyDeviceToHost, dv.aux));
+	HIPCHK(hipEventRecord(dv.aux_ev[0], dv.aux));
+	*launched = true;
+	return SG_OK;
+}
+
+static int reg_quality_finish(sg_ctx *ctx, SgDevice &dv, int nq, bool launched, std::vector<double> &qual) {
+	qual.assign(nq, 0.0);
+	if (!launched)
+		return SG_OK;
+	HIPCHK(hipEventSynchronize(dv.aux_ev[0]));
+	const unsigned long long *h = dv.qacc_h;
 	for (int i = 0; i < nq; i++) {
 		double q;
 		if (!h[3 * i + 2]) {
@@ -1226,7 +1254,8 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	qframes.push_back(ref_image);
 	qframes.insert(qframes.end(), todo.begin(), todo.end());
 	std::vector<double> qual;
-	int rc = reg_quality(ctx, dv, s, d_sel, S, qframes, qual);
+	bool q_launched = false;
+	int rc = reg_quality_launch(ctx, dv, s, d_sel, S, qframes, &q_launched);
 	if (rc)
 		return rc;
 
@@ -1615,6 +1644,8 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		}
 	}
 
+	if (int qrc = reg_quality_finish(ctx, dv, (int)qframes.size(), q_launched, qual))
+		return qrc;
 	/* quality: q_min/q_max seeded by the reference frame, then frames in index order with
 	 * the reference's min() macro (src/core/siril.h), then normalizeQualityData */
 	if (!normalize_q) {	/* raw values of the processed frames (sharded registration) */
