@@ -9,8 +9,9 @@ oracle and against golden registration results (tests/golden/make_golden_fullsiz
   configs[3]  the same stack as 8 row bands (the multi-GPU partition, band-only residency
               windows) equal to the one-call image
   configs[4]  256 x 3 x 4000 x 6000: DFT registration of layer 1's centred 2048 selection,
-              WINSORIZED (4, 3) stack of all three channels with those shifts, sampled row bands
-              of every channel against the oracle
+              WINSORIZED (4, 3) stack of all three channels with those shifts: the whole image
+              against the independent sorted-kernel path, sampled row bands of every channel
+              against the oracle
 
 Frames are the synthetic sequence of include/sg_synth.h (generated in HBM by the library,
 and by the oracle for the golden files).  At these frame counts no first sigma pass breaks
@@ -235,7 +236,20 @@ def test_cfg4_rgb_register_and_winsorized(gpu_ctx):
     torch.cuda.synchronize()
     desc, keep = sg.make_desc(sg.MEAN, N, W, H, C, rejection=sg.WINSORIZED, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
                               max_thread=16, max_number_of_rows=H)
-    gpu_ctx.stack_device(desc, frames.data_ptr(), C * H * W, H * W, out.data_ptr(), 0, H)
+    rej, _ = gpu_ctx.stack_device(desc, frames.data_ptr(), C * H * W, H * W, out.data_ptr(), 0, H)
+    assert gpu_ctx.stats().path == 1
+    # the WHOLE image (all 3 channels) against the independent sort-based kernel path
+    # (k_stack_sorted + replay + literal, each checked against the oracle at small sizes)
+    d_s, k_s = sg.make_desc(sg.MEAN, N, W, H, C, rejection=sg.WINSORIZED, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                            max_thread=16, max_number_of_rows=H, kernel_path=sg.PATH_SORTED)
+    out_s = torch.zeros(C * H * W, dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
+    rej_s, _ = gpu_ctx.stack_device(d_s, frames.data_ptr(), C * H * W, H * W, out_s.data_ptr(), 0, H)
+    assert gpu_ctx.stats().path == 0
+    nbad = int((out_s != out).sum())
+    assert nbad == 0, f"{nbad} pixels differ between the histogram and the sorted kernel paths"
+    assert np.array_equal(rej_s, rej), (rej_s, rej)
+    del out_s
     img = out.cpu().numpy().view(np.uint16).reshape(C, H, W)
     for c in range(C):
         for b, e in [(0, 64), (H // 2 - 32, H // 2 + 32), (H - 64, H)]:
