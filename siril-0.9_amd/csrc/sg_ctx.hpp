@@ -102,6 +102,7 @@ struct SgKnobs {
 	int reg_fp = 32;		/* SG_REG_FP: 32 = fp32 half-spectrum passes, near ties re-run in fp64; 64 = fp64 only */
 	int reg_cw32 = 4;		/* SG_REG_CW32: columns per strip of the fp32 column pass (4: 32-B row segments, no spill; 8: 64-B segments, 16 elements per thread) */
 	int reg_colocc = 1;		/* SG_REG_COLOCC: 1 = fp32 column pass held to 64 VGPRs (two 1024-thread workgroups per CU: registration 6.86 -> 6.21 ms on configs[1], profiles/r03t_ab_reg_cols.log), 0 = 76 VGPRs, one workgroup */
+	int reg_wcol = 1;		/* SG_REG_WCOL: 1 = wave-level fp32 column pass at S = 2048 (k_reg_cols_xpower_w), 0 = block-level */
 	int reg_genfuse = 1;		/* SG_REG_GENFUSE: 1 = generic sides' fused column pass (k_gen_cols_xpower), 0 = rows + k_gen_xpower + rows */
 	int reg_rpb = 4;		/* SG_REG_RPB: rows per forward-row workgroup of the half-spectrum path (1 -> 4: 6.46 -> 5.92 ms registration on configs[1], profiles/r03u_ab_reg_rows.log) */
 	void read() {
@@ -127,6 +128,7 @@ struct SgKnobs {
 		reg_pb = sg_env_int("SG_REG_PB", 1, 64, 1);
 		reg_fp = sg_env_int("SG_REG_FP", 32, 64, 32) == 64 ? 64 : 32;
 		reg_genfuse = sg_env_int("SG_REG_GENFUSE", 0, 1, 1);
+		reg_wcol = sg_env_int("SG_REG_WCOL", 0, 1, 1);
 		reg_cw32 = sg_env_int("SG_REG_CW32", 1, 16, 4);
 		while (reg_cw32 & (reg_cw32 - 1))
 			reg_cw32 &= reg_cw32 - 1;

@@ -238,6 +238,210 @@ k_reg_cols_xpower(C *__restrict__ work, const C *__restrict__ spec, int S, int C
 			[&](int c, int r, C v) { base[(size_t)r * S + c] = v; });
 }
 
+/* ---------------------------------------------------------------------------------------
+ * Wave-level fused column pass, fp32, S = 2048 (configs[1] / configs[4]): one WAVE per column
+ * of a 4-column strip, the 2048-point transforms as 32 x 64 four-step FFTs held in registers
+ * (32 complex per lane), so the block synchronises only around the coalesced strip load and
+ * store.  Forward: lane l holds x[64 j + l] (j = 0..31); a 32-point DFT over j in registers,
+ * twiddles w_S^(l k1), a transpose through the wave's own LDS column (rows of 66 for banks) to
+ * lane m = (k1 = m / 2, h = m % 2) holding the odd / even lanes' values (i -> l = 2 i + h), a
+ * 32-point DFT over i, twiddles w_64^(h k2) and one radix-2 step across the lane pair (DPP):
+ * lane m, register k2 then holds X[ky], ky = m / 2 + 32 k2 + 1024 (m % 2).  The cross power is
+ * elementwise at ky (the packed column 0 also reads Z(-ky), through the wave's LDS), and the
+ * inverse runs the same steps mirrored, ending in natural order.  Same products and packing as
+ * k_reg_cols_xpower; the FFT's rounding differs and stays within the fp32 tie tolerance
+ * (sg_reg_tol).  The round-3 kernel (1024 threads, four radix-8/4 LDS passes each way) spent
+ * ~15 k wave-instructions per column, mostly index arithmetic, LDS traffic and barriers.
+ * ------------------------------------------------------------------------------------- */
+__device__ __forceinline__ float2 sg_cmulf(float2 a, float2 b) {
+	return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+/* 32-point DFT of v (natural order in and out) in registers, radix-2 decimation in frequency */
+template <bool INV>
+__device__ __forceinline__ void sg_dft32_lane(float2 (&v)[32]) {
+	constexpr float C[16] = {1.0f, 0.9807852506637573f, 0.9238795042037964f, 0.8314695954322815f,
+		0.7071067690849304f, 0.5555702447891235f, 0.3826834261417389f, 0.19509032368659973f, 0.0f,
+		-0.19509032368659973f, -0.3826834261417389f, -0.5555702447891235f, -0.7071067690849304f,
+		-0.8314695954322815f, -0.9238795042037964f, -0.9807852506637573f};
+	constexpr float SN[16] = {0.0f, 0.19509032368659973f, 0.3826834261417389f, 0.5555702447891235f,
+		0.7071067690849304f, 0.8314695954322815f, 0.9238795042037964f, 0.9807852506637573f, 1.0f,
+		0.9807852506637573f, 0.9238795042037964f, 0.8314695954322815f, 0.7071067690849304f,
+		0.5555702447891235f, 0.3826834261417389f, 0.19509032368659973f};
+#pragma unroll
+	for (int half = 16; half >= 1; half >>= 1) {
+#pragma unroll
+		for (int blk = 0; blk < 32; blk += 2 * half) {
+#pragma unroll
+			for (int i = 0; i < half; i++) {
+				const float2 a = v[blk + i], b = v[blk + i + half];
+				v[blk + i] = make_float2(a.x + b.x, a.y + b.y);
+				const float2 d = make_float2(a.x - b.x, a.y - b.y);
+				const int m = i * (16 / half);	/* w_32^m, m < 16 */
+				if (m == 0) {
+					v[blk + i + half] = d;
+				} else if (m == 8) {	/* -i (forward) / +i (inverse) */
+					v[blk + i + half] = INV ? make_float2(-d.y, d.x) : make_float2(d.y, -d.x);
+				} else {
+					const float2 w = make_float2(C[m], INV ? SN[m] : -SN[m]);
+					v[blk + i + half] = sg_cmulf(d, w);
+				}
+			}
+		}
+		__builtin_amdgcn_sched_barrier(0);	/* stage by stage: interleaved stages took 249 VGPRs */
+	}
+	float2 t[32];
+#pragma unroll
+	for (int k = 0; k < 32; k++)
+		t[k] = v[(int)(__builtin_bitreverse32((unsigned)k) >> 27)];
+#pragma unroll
+	for (int k = 0; k < 32; k++)
+		v[k] = t[k];
+}
+
+/* the lane-pair partner's value (lane ^ 1), DPP quad_perm [1, 0, 3, 2] */
+__device__ __forceinline__ float2 sg_pair_swap(float2 v) {
+	return make_float2(__int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.x), 0xB1, 0xF, 0xF, false)),
+			__int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.y), 0xB1, 0xF, 0xF, false)));
+}
+
+/* v[k1] *= w^(lane k1) (k1 >= 1; tw: the forward or inverse table of S entries).  The table is
+ * read at k1 = 1, 8, 16, 24 only (lane-scattered loads, 64 distinct lines per instruction, were
+ * the pass's bottleneck: 31 of them per transform) and the powers in between are formed by
+ * multiplying by w^lane: at most 7 products per twiddle, within the fp32 tie tolerance */
+__device__ __forceinline__ void sg_twiddle_rows(float2 (&v)[32], const float2 *__restrict__ tw, int lane) {
+	const float2 b = tw[lane];
+	float2 t8[3];
+#pragma unroll
+	for (int q = 0; q < 3; q++)
+		t8[q] = tw[lane * 8 * (q + 1)];
+	float2 t = b;
+#pragma unroll
+	for (int k1 = 1; k1 < 32; k1++) {
+		if (k1 > 1)
+			t = (k1 & 7) ? sg_cmulf(t, b) : t8[(k1 >> 3) - 1];
+		v[k1] = sg_cmulf(v[k1], t);
+	}
+}
+
+#ifndef SG_WCOL_WPE
+#define SG_WCOL_WPE 2
+#endif
+#define SG_WCOL_CS 2120	/* LDS float2 per column: 2048 (strip) / 32 x 66 (transposes), +8 for the strip's banks */
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SG_WCOL_WPE)))
+k_reg_cols_xpower_w(float2 *__restrict__ work, const float2 *__restrict__ spec, const float2 *__restrict__ tw, int xcdmap) {
+	constexpr int S = 2048, H = 1024, P = 32, CS = SG_WCOL_CS, TR = 66;
+	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+	float2 *lds = (float2 *)smem;
+	const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+	const int x0 = sg_xcd_strip(blockIdx.x, gridDim.x, xcdmap) * 4, pair = blockIdx.y;
+	float2 *base = work + (size_t)pair * S * S + x0;
+	float2 *col = lds + wave * CS;
+	auto wsync = [] { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); };
+	/* strip -> LDS: rows of 4 columns (32 B), column c at lds + c CS */
+#pragma unroll 4
+	for (int it = 0; it < P; it++) {
+		const int r = (threadIdx.x >> 2) + 64 * it, c = threadIdx.x & 3;
+		lds[c * CS + r] = base[(size_t)r * S + c];
+	}
+	__syncthreads();
+	float2 v[P];
+#pragma unroll
+	for (int j = 0; j < P; j++)
+		v[j] = col[64 * j + lane];
+	/* ---- forward ---- */
+	sg_dft32_lane<false>(v);
+	sg_twiddle_rows(v, tw, lane);
+	wsync();
+#pragma unroll
+	for (int k1 = 0; k1 < P; k1++)
+		col[k1 * TR + lane] = v[k1];
+	wsync();
+	const int km = lane >> 1, hm = lane & 1;
+#pragma unroll
+	for (int i = 0; i < P; i++)
+		v[i] = col[km * TR + 2 * i + hm];
+	sg_dft32_lane<false>(v);
+#pragma unroll
+	for (int k = 1; k < P; k++) {
+		const float2 t = tw[32 * k];
+		v[k] = sg_cmulf(v[k], hm ? t : make_float2(1.0f, 0.0f));
+	}
+#pragma unroll
+	for (int k = 0; k < P; k++) {
+		const float2 o = sg_pair_swap(v[k]);
+		v[k] = hm ? make_float2(o.x - v[k].x, o.y - v[k].y) : make_float2(v[k].x + o.x, v[k].y + o.y);
+	}
+	/* ---- cross power at ky = km + 32 k + 1024 hm ---- */
+	const int kx = (x0 + wave) & (H - 1);
+	/* the reference spectrum's strip through LDS (coalesced 32-B rows, as the work strip; read
+	 * per lane at its ky it touched 64 rows per instruction), except a packed column 0, whose
+	 * wave keeps its LDS column for Z(-ky) and reads its reference column directly */
+	__syncthreads();	/* every wave is done with its transposes */
+	const int kx0 = x0 & (H - 1);	/* a strip lies inside one half */
+#pragma unroll 4
+	for (int it = 0; it < P; it++) {
+		const int r = (threadIdx.x >> 2) + 64 * it, c = threadIdx.x & 3;
+		if (kx0 + c)
+			lds[c * CS + r] = spec[(size_t)r * S + kx0 + c];
+	}
+	__syncthreads();
+	if (kx) {
+#pragma unroll
+		for (int k = 0; k < P; k++)
+			v[k] = sg_rconj(col[km + 32 * k + 1024 * hm], v[k]);
+	} else {	/* packed column: Z = F0 + i FN, the reference likewise; needs Z(-ky) */
+		wsync();
+#pragma unroll
+		for (int k = 0; k < P; k++)
+			col[km + 32 * k + 1024 * hm] = v[k];
+		wsync();
+#pragma unroll
+		for (int k = 0; k < P; k++) {
+			const int ky = km + 32 * k + 1024 * hm, m = (S - ky) & (S - 1);
+			const float2 zk = v[k], zm = col[m], r1 = spec[(size_t)ky * S], r2 = spec[(size_t)m * S];
+			const float2 f0 = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
+			const float2 fn = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
+			const float2 r0 = make_float2(0.5f * (r1.x + r2.x), 0.5f * (r1.y - r2.y));
+			const float2 rn = make_float2(0.5f * (r1.y + r2.y), -0.5f * (r1.x - r2.x));
+			const float2 p0 = sg_rconj(r0, f0), pn = sg_rconj(rn, fn);
+			v[k] = make_float2(p0.x - pn.y, p0.y + pn.x);
+		}
+	}
+	/* ---- inverse (unnormalised, FFTW_BACKWARD) ---- */
+#pragma unroll
+	for (int k = 0; k < P; k++) {
+		const float2 o = sg_pair_swap(v[k]);
+		v[k] = hm ? make_float2(o.x - v[k].x, o.y - v[k].y) : make_float2(v[k].x + o.x, v[k].y + o.y);
+	}
+#pragma unroll
+	for (int k = 1; k < P; k++) {
+		const float2 t = tw[S + 32 * k];
+		v[k] = sg_cmulf(v[k], hm ? t : make_float2(1.0f, 0.0f));
+	}
+	sg_dft32_lane<true>(v);
+	wsync();
+#pragma unroll
+	for (int i = 0; i < P; i++)
+		col[km * TR + 2 * i + hm] = v[i];
+	wsync();
+#pragma unroll
+	for (int k1 = 0; k1 < P; k1++)
+		v[k1] = col[k1 * TR + lane];
+	sg_twiddle_rows(v, tw + S, lane);
+	sg_dft32_lane<true>(v);
+	wsync();
+#pragma unroll
+	for (int j = 0; j < P; j++)
+		col[64 * j + lane] = v[j];
+	__syncthreads();
+#pragma unroll 4
+	for (int it = 0; it < P; it++) {
+		const int r = (threadIdx.x >> 2) + 64 * it, c = threadIdx.x & 3;
+		base[(size_t)r * S + c] = lds[c * CS + r];
+	}
+}
+
 /* per-pair result of a registration batch (frame a = the real part, frame b = the imaginary) */
 struct SgRegOut {
 	int sx[2], sy[2];	/* the shifts (:344-351) */
@@ -1307,6 +1511,9 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	const int colh_thr32 = std::max(64, CW32 * S / ept32);
 	const size_t colh_lds32 = (size_t)CW32 * sg_col_stride<float2>(S) * sizeof(float2);
 	const int colocc = ctx->knobs.reg_colocc;
+	/* the wave-level fp32 column pass: S = 2048 only (32 x 64 four-step transforms) */
+	const bool wcol = S == 2048 && ctx->knobs.reg_wcol;
+	const size_t wcol_lds = (size_t)4 * SG_WCOL_CS * sizeof(float2);
 	/* rows per forward-row workgroup (the next row prefetched during this one's transform) */
 	int rpb = ctx->knobs.reg_rpb;
 	while (rpb > 1 && S % rpb != 0)
@@ -1360,6 +1567,8 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 				(int)colh_lds32);
 		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower<float2, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)colh_lds32);
+		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower_w, hipFuncAttributeMaxDynamicSharedMemorySize,
+				(int)wcol_lds);
 	} else {
 		(void)hipFuncSetAttribute(k_rows, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gen_lds);
 	}
@@ -1476,7 +1685,10 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		hipLaunchKernelGGL(k_reg_rows_fwd_half<float2>, dim3(S / rpb, np), dim3(row_thr), row_lds32, s, d_sel, fa, fb, S,
 				tw32, work32, en, rpb);
 		HIPCHK(hipGetLastError());
-		if (ept32 == 16)
+		if (wcol)	/* S = 2048: the wave-level column pass (SG_REG_WCOL=0: the block-level one, A/B) */
+			hipLaunchKernelGGL(k_reg_cols_xpower_w, dim3(S / 4, np), dim3(256), wcol_lds, s, work32,
+					(const float2 *)spec32, tw32, xcdmap);
+		else if (ept32 == 16)
 			hipLaunchKernelGGL((k_reg_cols_xpower<float2, 16>), dim3(S / CW32, np), dim3(colh_thr32), colh_lds32, s,
 					work32, (const float2 *)spec32, S, CW32, tw32, xcdmap, 1);
 		else if (colocc)	/* default (SG_REG_COLOCC=1): 64 VGPRs (8 waves / SIMD, two 1024-thread workgroups per CU) */

@@ -152,6 +152,24 @@ def test_register_generic_fused_columns_match_unfused(gpu_ctx, S):
     assert np.array_equal(gx, hx) and np.array_equal(gy, hy) and _same_q(gq, hq)
 
 
+def test_register_wave_columns_match_block_columns(gpu_ctx):
+    """S = 2048: the wave-level fp32 column pass (k_reg_cols_xpower_w, 32 x 64 four-step
+    transforms in registers) gives the block-level pass's shifts and qualities (SG_REG_WCOL=0),
+    and the numpy arg-max; an odd frame count exercises the pair with an empty imaginary frame"""
+    S, n = 2048, 7
+    sel = orc.synth(n, 1, S, S, seed=91, maxshift=14)[:, 0].copy()
+    gx, gy, gq = gpu_ctx.register_dft(sel)
+    os.environ["SG_REG_WCOL"] = "0"
+    try:
+        with sg.Context() as c0:
+            hx, hy, hq = c0.register_dft(sel)
+    finally:
+        del os.environ["SG_REG_WCOL"]
+    assert np.array_equal(gx, hx) and np.array_equal(gy, hy) and _same_q(gq, hq)
+    nx, ny = _numpy_shifts(sel)
+    assert np.array_equal(gx, nx) and np.array_equal(gy, ny), (gx, nx, gy, ny)
+
+
 @pytest.mark.parametrize("S", [256, 2048])
 def test_register_fp32_passes_match_fp64(gpu_ctx, S):
     """the fp32 half-spectrum passes (default, SG_REG_FP=32) give the fp64 passes' shifts and
