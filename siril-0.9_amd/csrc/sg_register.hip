@@ -324,6 +324,38 @@ __device__ __forceinline__ void sg_twiddle_rows(float2 (&v)[32], const float2 *_
 	}
 }
 
+/* 2048-point DFT of the wave's line, four-step 32 x 64: lane l holds x[64 j + l] in v[j]; on
+ * return lane m holds X[m / 2 + 32 k + 1024 (m % 2)] in v[k] (INV: conjugate roots, the
+ * unnormalised inverse).  col: the wave's LDS (32 rows of 66 float2).  tw: the forward table
+ * (tw + 2048 is the inverse one). */
+template <bool INV>
+__device__ __forceinline__ void sg_fft2048_wave(float2 (&v)[32], float2 *col, const float2 *__restrict__ tw, int lane) {
+	constexpr int S = 2048, P = 32, TR = 66;
+	const float2 *twd = INV ? tw + S : tw;
+	sg_dft32_lane<INV>(v);
+	sg_twiddle_rows(v, twd, lane);
+	__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+	for (int k1 = 0; k1 < P; k1++)
+		col[k1 * TR + lane] = v[k1];
+	__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+	const int km = lane >> 1, hm = lane & 1;
+#pragma unroll
+	for (int i = 0; i < P; i++)
+		v[i] = col[km * TR + 2 * i + hm];
+	sg_dft32_lane<INV>(v);
+#pragma unroll
+	for (int k = 1; k < P; k++) {
+		const float2 t = twd[32 * k];
+		v[k] = sg_cmulf(v[k], hm ? t : make_float2(1.0f, 0.0f));
+	}
+#pragma unroll
+	for (int k = 0; k < P; k++) {
+		const float2 o = sg_pair_swap(v[k]);
+		v[k] = hm ? make_float2(o.x - v[k].x, o.y - v[k].y) : make_float2(v[k].x + o.x, v[k].y + o.y);
+	}
+}
+
 #ifndef SG_WCOL_WPE
 #define SG_WCOL_WPE 2
 #endif
@@ -350,28 +382,8 @@ k_reg_cols_xpower_w(float2 *__restrict__ work, const float2 *__restrict__ spec, 
 	for (int j = 0; j < P; j++)
 		v[j] = col[64 * j + lane];
 	/* ---- forward ---- */
-	sg_dft32_lane<false>(v);
-	sg_twiddle_rows(v, tw, lane);
-	wsync();
-#pragma unroll
-	for (int k1 = 0; k1 < P; k1++)
-		col[k1 * TR + lane] = v[k1];
-	wsync();
+	sg_fft2048_wave<false>(v, col, tw, lane);
 	const int km = lane >> 1, hm = lane & 1;
-#pragma unroll
-	for (int i = 0; i < P; i++)
-		v[i] = col[km * TR + 2 * i + hm];
-	sg_dft32_lane<false>(v);
-#pragma unroll
-	for (int k = 1; k < P; k++) {
-		const float2 t = tw[32 * k];
-		v[k] = sg_cmulf(v[k], hm ? t : make_float2(1.0f, 0.0f));
-	}
-#pragma unroll
-	for (int k = 0; k < P; k++) {
-		const float2 o = sg_pair_swap(v[k]);
-		v[k] = hm ? make_float2(o.x - v[k].x, o.y - v[k].y) : make_float2(v[k].x + o.x, v[k].y + o.y);
-	}
 	/* ---- cross power at ky = km + 32 k + 1024 hm ---- */
 	const int kx = (x0 + wave) & (H - 1);
 	/* the reference spectrum's strip through LDS (coalesced 32-B rows, as the work strip; read
@@ -439,6 +451,138 @@ k_reg_cols_xpower_w(float2 *__restrict__ work, const float2 *__restrict__ spec, 
 	for (int it = 0; it < P; it++) {
 		const int r = (threadIdx.x >> 2) + 64 * it, c = threadIdx.x & 3;
 		base[(size_t)r * S + c] = lds[c * CS + r];
+	}
+}
+
+/* Wave-level fp32 forward row pass at S = 2048: one wave per row (4 rows per workgroup, no
+ * block barrier), the row of a + i b through sg_fft2048_wave, then staged in natural order in
+ * the wave's LDS for the separation into the half spectra A, B (k_reg_rows_fwd_half's
+ * arithmetic); the frames' energies summed per wave */
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SG_WCOL_WPE)))
+k_reg_rows_fwd_half_w(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const int *__restrict__ fb,
+		const float2 *__restrict__ tw, float2 *__restrict__ work, unsigned long long *__restrict__ energy) {
+	constexpr int S = 2048, H = 1024, P = 32;
+	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+	const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+	const int row = blockIdx.x * 4 + wave, pair = blockIdx.y;
+	float2 *col = (float2 *)smem + wave * SG_WCOL_CS;
+	const size_t plane = (size_t)S * S;
+	const uint16_t *pa = sel + (size_t)fa[pair] * plane + (size_t)row * S;
+	const int b = fb[pair];
+	const uint16_t *pb = b >= 0 ? sel + (size_t)b * plane + (size_t)row * S : nullptr;
+	float2 v[P];
+	unsigned long long ea = 0, eb = 0;
+	/* frame a, then frame b, 8 samples in flight at a time (all 64 at once spilled) */
+#pragma unroll
+	for (int j0 = 0; j0 < P; j0 += 8) {
+		uint32_t u[8];
+#pragma unroll
+		for (int j = 0; j < 8; j++)
+			u[j] = pa[64 * (j0 + j) + lane];
+#pragma unroll
+		for (int j = 0; j < 8; j++) {
+			ea += (unsigned long long)(u[j] * u[j]);
+			v[j0 + j] = make_float2((float)u[j], 0.0f);
+		}
+		__builtin_amdgcn_sched_barrier(0);
+	}
+	if (pb) {
+#pragma unroll
+		for (int j0 = 0; j0 < P; j0 += 8) {
+			uint32_t u[8];
+#pragma unroll
+			for (int j = 0; j < 8; j++)
+				u[j] = pb[64 * (j0 + j) + lane];
+#pragma unroll
+			for (int j = 0; j < 8; j++) {
+				eb += (unsigned long long)(u[j] * u[j]);
+				v[j0 + j].y = (float)u[j];
+			}
+			__builtin_amdgcn_sched_barrier(0);
+		}
+	}
+	sg_fft2048_wave<false>(v, col, tw, lane);
+	const int km = lane >> 1, hm = lane & 1;
+	__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+	for (int k = 0; k < P; k++)
+		col[km + 32 * k + 1024 * hm] = v[k];
+	__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+	float2 *out = work + (size_t)pair * plane + (size_t)row * S;
+#pragma unroll 4
+	for (int q = 0; q < H / 64; q++) {
+		const int kx = 64 * q + lane;
+		const float2 zk = col[kx], zm = col[kx ? S - kx : H];
+		float2 A, B;
+		if (kx == 0) {
+			A = make_float2(zk.x, zm.x);	/* A(0) + i A(S/2) */
+			B = make_float2(zk.y, zm.y);
+		} else {
+			A = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
+			B = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
+		}
+		out[kx] = A;
+		out[H + kx] = B;
+	}
+	for (int o = 32; o > 0; o >>= 1) {
+		ea += __shfl_xor(ea, o, 64);
+		eb += __shfl_xor(eb, o, 64);
+	}
+	if (lane == 0) {
+		atomicAdd(energy + fa[pair], ea);
+		if (b >= 0)
+			atomicAdd(energy + b, eb);
+	}
+}
+
+/* Wave-level fp32 inverse row pass + arg-max at S = 2048: one wave per row; the packed
+ * spectrum Qa + i Qb rebuilt per element as k_reg_rows_inv_half_argmax does, the inverse
+ * transform by sg_fft2048_wave<true> (its permuted output order only changes which index a
+ * value carries), the row's top-2 reduced in the wave */
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SG_WCOL_WPE)))
+k_reg_rows_inv_half_w(const float2 *__restrict__ work, const float2 *__restrict__ tw, SgBest *__restrict__ best) {
+	constexpr int S = 2048, H = 1024, P = 32;
+	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+	const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+	const int row = blockIdx.x * 4 + wave, pair = blockIdx.y;
+	float2 *col = (float2 *)smem + wave * SG_WCOL_CS;
+	const float2 *in = work + (size_t)pair * S * S + (size_t)row * S;
+	float2 v[P];
+#pragma unroll
+	for (int j = 0; j < P; j++) {
+		const int i = 64 * j + lane;
+		float2 qa, qb;
+		if ((i & (H - 1)) == 0) {	/* kx = 0 or S/2: the packed real pair */
+			const float2 a = in[0], bb = in[H];
+			qa = make_float2(i ? a.y : a.x, 0.0f);
+			qb = make_float2(i ? bb.y : bb.x, 0.0f);
+		} else if (i < H) {
+			qa = in[i];
+			qb = in[H + i];
+		} else {
+			const float2 a = in[S - i], bb = in[H + S - i];
+			qa = make_float2(a.x, -a.y);
+			qb = make_float2(bb.x, -bb.y);
+		}
+		v[j] = make_float2(qa.x - qb.y, qa.y + qb.x);
+	}
+	sg_fft2048_wave<true>(v, col, tw, lane);
+	const int km = lane >> 1, hm = lane & 1;
+	SgTop2T<float> ta, tb;
+	sg_top2t_init(ta);
+	sg_top2t_init(tb);
+#pragma unroll
+	for (int k = 0; k < P; k++) {
+		const int idx = row * S + km + 32 * k + 1024 * hm;
+		sg_top2t_add(ta, v[k].x, idx);
+		sg_top2t_add(tb, v[k].y, idx);
+	}
+	SgTop2 wa = sg_top2t_wide(ta), wb = sg_top2t_wide(tb);
+	sg_top2_wave(wa);
+	sg_top2_wave(wb);
+	if (lane == 0) {
+		best[(size_t)pair * S + row].a = wa;
+		best[(size_t)pair * S + row].b = wb;
 	}
 }
 
@@ -1569,6 +1713,10 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 				(int)colh_lds32);
 		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower_w, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)wcol_lds);
+		(void)hipFuncSetAttribute((const void *)k_reg_rows_fwd_half_w, hipFuncAttributeMaxDynamicSharedMemorySize,
+				(int)wcol_lds);
+		(void)hipFuncSetAttribute((const void *)k_reg_rows_inv_half_w, hipFuncAttributeMaxDynamicSharedMemorySize,
+				(int)wcol_lds);
 	} else {
 		(void)hipFuncSetAttribute(k_rows, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gen_lds);
 	}
@@ -1682,8 +1830,12 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		return SG_OK;
 	};
 	auto half32 = [&](const int *fa, const int *fb, int np, unsigned long long *en) -> int {
-		hipLaunchKernelGGL(k_reg_rows_fwd_half<float2>, dim3(S / rpb, np), dim3(row_thr), row_lds32, s, d_sel, fa, fb, S,
-				tw32, work32, en, rpb);
+		if (wcol)
+			hipLaunchKernelGGL(k_reg_rows_fwd_half_w, dim3(S / 4, np), dim3(256), wcol_lds, s, d_sel, fa, fb, tw32,
+					work32, en);
+		else
+			hipLaunchKernelGGL(k_reg_rows_fwd_half<float2>, dim3(S / rpb, np), dim3(row_thr), row_lds32, s, d_sel, fa,
+					fb, S, tw32, work32, en, rpb);
 		HIPCHK(hipGetLastError());
 		if (wcol)	/* S = 2048: the wave-level column pass (SG_REG_WCOL=0: the block-level one, A/B) */
 			hipLaunchKernelGGL(k_reg_cols_xpower_w, dim3(S / 4, np), dim3(256), wcol_lds, s, work32,
@@ -1698,8 +1850,12 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 			hipLaunchKernelGGL((k_reg_cols_xpower<float2, 8>), dim3(S / CW32, np), dim3(colh_thr32), colh_lds32, s,
 					work32, (const float2 *)spec32, S, CW32, tw32, xcdmap, 1);
 		HIPCHK(hipGetLastError());
-		hipLaunchKernelGGL((k_reg_rows_inv_half_argmax<float2, false>), dim3(S, np), dim3(row_thr), row_lds32, s,
-				(const float2 *)work32, S, tw32, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
+		if (wcol)
+			hipLaunchKernelGGL(k_reg_rows_inv_half_w, dim3(S / 4, np), dim3(256), wcol_lds, s, (const float2 *)work32,
+					tw32, best);
+		else
+			hipLaunchKernelGGL((k_reg_rows_inv_half_argmax<float2, false>), dim3(S, np), dim3(row_thr), row_lds32, s,
+					(const float2 *)work32, S, tw32, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
 		HIPCHK(hipGetLastError());
 		return SG_OK;
 	};
