@@ -784,7 +784,12 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		if (r3) {
 			switch (d->method) {
 			case SG_STACK_SUM: hipLaunchKernelGGL(k_stack_reduce3<0>, dim3(nb3), dim3(256), 0, s, p, p.hist_tab, p.shifty); break;
-			case SG_STACK_MEAN: hipLaunchKernelGGL(k_stack_reduce3<1>, dim3(nb3), dim3(256), 0, s, p, p.hist_tab, p.shifty); break;
+			case SG_STACK_MEAN:	/* the normalising instance's fp64 path costs registers: its own kernel */
+				if (p.normalize)
+					hipLaunchKernelGGL(k_stack_reduce3<2>, dim3(nb3), dim3(256), 0, s, p, p.hist_tab, p.shifty);
+				else
+					hipLaunchKernelGGL(k_stack_reduce3<1>, dim3(nb3), dim3(256), 0, s, p, p.hist_tab, p.shifty);
+				break;
 			case SG_STACK_MAX: hipLaunchKernelGGL(k_stack_reduce3<3>, dim3(nb3), dim3(256), 0, s, p, p.hist_tab, p.shifty); break;
 			default: hipLaunchKernelGGL(k_stack_reduce3<4>, dim3(nb3), dim3(256), 0, s, p, p.hist_tab, p.shifty); break;
 			}

@@ -858,7 +858,7 @@ k_stack_reduce2(SgStackParams p) {
  * unsigned, so a negative start is out of range too).  SUM and MEAN add 0 for such rows (the
  * reference's zero fill, normalised for MEAN), MAX ignores them, MIN skips them (a uniform
  * test of the frame's shifty).  Two 16-frame register buffers per lane.  Other segments take the
- * general per-lane loop (sg_reduce_pairs).  M: 0 SUM, 1 MEAN, 3 MAX, 4 MIN.
+ * general per-lane loop (sg_reduce_pairs).  M: 0 SUM, 1 MEAN, 2 normalised MEAN, 3 MAX, 4 MIN.
  */
 template <int M>
 __global__ void __launch_bounds__(256)
@@ -918,14 +918,12 @@ k_stack_reduce3(SgStackParams p, const int *__restrict__ tab, const int *__restr
 			if (M == 0) {
 				acc_a += a;
 				acc_b += b;
-			} else if (M == 1) {
-				if (p.normalize) {	/* the zero fill of a row shifted out is normalised too */
-					acc_a += sg_normalize(p, f, (uint16_t)a);
-					acc_b += sg_normalize(p, f, (uint16_t)b);
-				} else {
-					acc_a += a;
-					acc_b += b;
-				}
+			} else if (M == 1) {	/* MEAN without normalisation: the sum (the divisor is N) */
+				acc_a += a;
+				acc_b += b;
+			} else if (M == 2) {	/* normalised MEAN: the zero fill of a row shifted out is normalised too */
+				acc_a += sg_normalize(p, f, (uint16_t)a);
+				acc_b += sg_normalize(p, f, (uint16_t)b);
 			} else if (M == 3) {
 				mm = __builtin_bit_cast(uint32_t,
 						__builtin_elementwise_max(__builtin_bit_cast(sg_u16x2, mm), __builtin_bit_cast(sg_u16x2, v[m])));
@@ -974,6 +972,7 @@ k_stack_reduce3(SgStackParams p, const int *__restrict__ tab, const int *__restr
 }
 template __global__ void k_stack_reduce3<0>(SgStackParams, const int *, const int *);
 template __global__ void k_stack_reduce3<1>(SgStackParams, const int *, const int *);
+template __global__ void k_stack_reduce3<2>(SgStackParams, const int *, const int *);
 template __global__ void k_stack_reduce3<3>(SgStackParams, const int *, const int *);
 template __global__ void k_stack_reduce3<4>(SgStackParams, const int *, const int *);
 
