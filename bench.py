@@ -400,6 +400,7 @@ def main_sigma(args):
             "kernel_ms": round(kavg, 3),
             "slow_pixels": int(st.slow_pixels),
             "redo_pixels": int(st.chain_pixels),
+            "compact_pixels": int(st.compact_pixels),
             "rejected": [int(x) for x in np.asarray(rej_tot).reshape(-1)[:2]],
         }
         if world > 1:

@@ -157,6 +157,8 @@ typedef struct {
 	 * integer correlations / left to the FFT arg-max (more candidates than the cap) */
 	uint64_t reg_ties_resolved, reg_ties_unresolved;
 	uint64_t reg_fp64_reruns;	/* pairs of the fp32 passes re-run in fp64 (near ties at fp32 tolerance) */
+	uint64_t compact_pixels;	/* normalised histogram stacks: redo pixels whose sorted columns the
+					 * histogram kernel wrote out (no gather in the sorted kernel) */
 } sg_stack_stats;
 int sg_get_last_stats(const sg_ctx *ctx, sg_stack_stats *st);
 

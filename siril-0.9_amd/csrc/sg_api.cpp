@@ -106,7 +106,7 @@ extern "C" void sg_shutdown(sg_ctx *ctx) {
 		(void)hipStreamSynchronize(d.stream);
 		SgBuf *bufs[] = {&d.flag_list, &d.flag_map, &d.sum_buf, &d.scratch, &d.frames, &d.out, &d.reg_sel, &d.reg_spec,
 			&d.reg_work, &d.reg_tw, &d.reg_tw32, &d.reg_best, &d.reg_qbuf, &d.reg_qacc, &d.redo, &d.zeros,
-			&d.io_raw, &d.io_bad, &d.warp_tab, &d.stats_buf, &d.inb, &d.ctr};
+			&d.cmp_cols, &d.cmp_list, &d.io_raw, &d.io_bad, &d.warp_tab, &d.stats_buf, &d.inb, &d.ctr};
 		for (SgBuf *b : bufs)
 			if (b->p)
 				(void)hipFree(b->p);
@@ -648,6 +648,19 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			/* REJ: 2 SIGMA, 4 WINSORIZED, 1 PERCENTILE, 8 stack_median */
 			const int rj = d->method == SG_STACK_MEDIAN ? 8 : p.rejection == SG_WINSORIZED ? 4 :
 				p.rejection == SG_PERCENTILE ? 1 : 2;
+			/* normalised SIGMA / WINSORIZED: redo pixels whose samples the tile fully knows leave
+			 * their sorted columns for the sorted kernel (sgh_compact), up to a 384 MiB buffer */
+			const bool compact = norm != 0 && (rj == 2 || rj == 4) && nreg && ctx->knobs.hist_compact;
+			if (compact) {
+				const size_t cap = std::min<size_t>(npix_launch, ctx->knobs.hist_compact >= 2 ?
+						(size_t)ctx->knobs.hist_compact : ((size_t)384 << 20) / ((size_t)N * 2));
+				HIPCHK(ensure(dv.cmp_cols, cap * (size_t)N * 2));
+				HIPCHK(ensure(dv.cmp_list, cap * sizeof(unsigned int)));
+				p.cmp_cols = (uint16_t *)dv.cmp_cols.p;
+				p.cmp_list = (unsigned int *)dv.cmp_list.p;
+				p.cmp_count = p.flag_count + 3;	/* cleared with the counters */
+				p.cmp_cap = (unsigned int)cap;
+			}
 			const dim3 hg((unsigned)nblk_h), hb((unsigned)sgh_block_threads(ni, rj));
 			switch ((rj == 4 ? 10 : rj == 1 ? 20 : rj == 8 ? 30 : 0) + norm + 100 * (rj == 1 || rj == 8 ? 1 : ni)) {
 			case 100: hipLaunchKernelGGL((k_stack_hist<2, 0, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
@@ -676,6 +689,14 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			st.path = 1;
 			st.main_kernel_blocks = (int)nblk;
 			st.launches = 1;
+			if (compact) {
+				/* the grid covers the capacity; blocks past the device-side count return at once */
+				SgStackParams q = p;
+				q.cmp_src = p.cmp_cols;
+				HIPCHK(launch_sorted(nreg, true, dim3((p.cmp_cap + SG_TILE_W - 1) / SG_TILE_W), lds, s, q, p.cmp_list,
+						p.cmp_count));
+				st.launches++;
+			}
 			/* the redo pixels: up to SG_REDO_REPLAY_MAX go straight to the wave-per-pixel replay
 			 * (every sample of a pixel gathered by one wave at once), decided on the device so
 			 * the step needs no host round trip; a longer list (rare: e.g. the normalised zeros
@@ -835,6 +856,7 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 	st.kernel_ms = ms;
 	st.total_ms = ms2;
 	st.slow_pixels = cnt[0];
+	st.compact_pixels = std::min(ctr_flags[3], p.cmp_cap);
 	if (rej) {
 		for (int c = 0; c < 3; c++)
 			rej[c][0] = rej[c][1] = 0;
@@ -1241,6 +1263,7 @@ extern "C" int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *d, sg_read_region_
 			agg.total_ms = std::max(agg.total_ms, s.total_ms);
 			agg.slow_pixels += s.slow_pixels;
 			agg.chain_pixels += s.chain_pixels;
+			agg.compact_pixels += s.compact_pixels;
 			agg.launches += s.launches;
 			agg.main_kernel_blocks += s.main_kernel_blocks;
 			agg.path = s.path;

@@ -59,6 +59,14 @@ struct SgStackParams {
 	unsigned int *flag_list;		/* encoded (c*H + R)*W + x */
 	unsigned int flag_cap;
 	uint8_t *flag_map;			/* [C][H][W] class per pixel (chain walk) */
+	/* histogram path, normalised SIGMA / WINSORIZED: a redo pixel whose only out-of-band
+	 * samples besides 0 / 65535 are the few the build captured (SGH_OVK) leaves its whole sorted
+	 * column at cmp_cols[slot][N] and its pixel at cmp_list[slot] (slot < cmp_cap), so the
+	 * sorted kernel reads N contiguous values instead of gathering N scattered lines */
+	uint16_t *cmp_cols;
+	unsigned int *cmp_list, *cmp_count;
+	unsigned int cmp_cap;
+	const uint16_t *cmp_src;		/* k_stack_sorted<., true>: stage the listed columns from here (sorted) */
 	uint32_t *sum_buf;			/* SUM: raw sums [C][H][W] */
 	unsigned int *maxim;			/* SUM: global max of sums */
 };

@@ -41,6 +41,7 @@ struct SgDevice {
 	/* registration workspaces (sg_register.hip) */
 	SgBuf reg_sel, reg_spec, reg_work, reg_tw, reg_tw32, reg_best, reg_qbuf, reg_qacc;
 	SgBuf redo;	/* redo list of the histogram stacking path */
+	SgBuf cmp_cols, cmp_list;	/* compact redo columns / pixels of normalised histogram stacks */
 	/* registration: the quality estimate runs on its own stream beside the FFT passes; its
 	 * sums come back into a pinned block, aux_ev marks them landed */
 	hipStream_t aux = nullptr;
@@ -90,6 +91,8 @@ struct SgKnobs {
 	int hist_ni = 1;		/* SG_HIST_NI: pixel pairs per lane of the histogram tiles (2: 256-px tiles) */
 	int wins_cap = 64;		/* SG_WINS_CAP: histogram Winsorize inner iterations per pass before the redo list */
 	int redo_replay = 1;		/* SG_REDO_REPLAY: 0 = redo list always through the sorted kernel */
+	int hist_compact = 1;		/* SG_HIST_COMPACT: 0 = normalised redo pixels gather their columns again,
+					 * >= 2: the compact list's capacity in pixels (tests of the overflow) */
 	int reduce1 = 0;		/* SG_REDUCE1: 1 = one pixel per lane, 2 = the per-lane pixel-pair kernel, in the SUM/MAX/MIN/MEAN reduce (A/B) */
 	long long host_budget = 0;	/* SG_HOST_BUDGET_BYTES: host-pull HBM budget (0 = 85 % of free HBM) */
 	int qsub_threads = 64;		/* SG_QSUB_THREADS: 64 measured best (scripts/gpu_qsub.sh) */
@@ -112,6 +115,7 @@ struct SgKnobs {
 		hist_ni = sg_env_int("SG_HIST_NI", 1, 2, 1);
 		wins_cap = sg_env_int("SG_WINS_CAP", 4, 100000, 64);
 		redo_replay = sg_env_int("SG_REDO_REPLAY", 0, 1, 1);
+		hist_compact = sg_env_int("SG_HIST_COMPACT", 0, 1 << 30, 1);
 		reduce1 = sg_env_int("SG_REDUCE1", 0, 2, 0);
 		if (const char *e = getenv("SG_HOST_BUDGET_BYTES"))
 			host_budget = atoll(e) > 0 ? atoll(e) : 0;

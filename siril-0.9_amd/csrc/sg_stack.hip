@@ -460,7 +460,9 @@ k_stack_sorted(SgStackParams p, const unsigned int *__restrict__ list, const uns
 	if (LISTED) {
 		/* redo list of the histogram path: slot i = pixel list[64 * block + i]; a grid sized
 		 * for the longest list the device routes itself leaves its blocks past the count idle */
-		const unsigned int count = *list_count;
+		unsigned int count = *list_count;
+		if (p.cmp_src && count > p.cmp_cap)	/* the compact list: slots past the capacity went to the redo list */
+			count = p.cmp_cap;
 		if ((unsigned int)blockIdx.x * SG_TILE_W >= count)
 			return;
 		if (tid < SG_TILE_W) {
@@ -495,59 +497,73 @@ k_stack_sorted(SgStackParams p, const unsigned int *__restrict__ list, const uns
 	}
 	__syncthreads();
 
-	/* 1. stage the tile: frame f, slot -> stage[f][slot].  Lane = slot (its pixel fixed), wave w
-	 * takes frames w, w + 4, ...: a frame's shift and normalisation coefficients are wave-uniform
-	 * (scalar loads), where the flat idx loop loaded them per sample (the redo lists of
-	 * normalised stacks, ~200 k pixels, spent most of their time here) */
-	{
-		const int xx = slot_x[lane], cc = slot_c[lane], RR = slot_R[lane];
-		constexpr int NW = SG_SORT_THREADS / 64, NB = 8;
-		const uint16_t *plane = p.frames + (int64_t)cc * p.plane_stride;
-		/* NB frames per wave in flight: every lane loads from a clamped (always valid) address,
-		 * the sample is then selected (sg_gather's rules: an x-shifted sample is 0 and not
-		 * normalised, a y-shifted row reads 0 and is normalised) */
-		for (int f0 = __builtin_amdgcn_readfirstlane(wave); f0 < N; f0 += NW * NB) {
-			uint16_t raw[NB];
-			bool xin[NB];
+	if (LISTED && p.cmp_src) {
+		/* the compact redo list (sg_stack_hist.hip sgh_compact): slot k's sorted column is
+		 * cmp_src[k][0 .. N), read by a wave per slot with coalesced loads; no gather, no sort */
+		const unsigned int k0 = blockIdx.x * SG_TILE_W;
+		for (int sl = wave; sl < SG_TILE_W; sl += SG_SORT_THREADS / 64) {
+			if (slot_x[sl] < 0)
+				continue;
+			const uint16_t *col = p.cmp_src + (size_t)(k0 + sl) * (size_t)N;
+			for (int e = lane; e < N; e += 64)
+				stage[e * SG_STAGE_STRIDE + sl] = col[e];
+		}
+		__syncthreads();
+	} else {
+		/* 1. stage the tile: frame f, slot -> stage[f][slot].  Lane = slot (its pixel fixed), wave w
+		 * takes frames w, w + 4, ...: a frame's shift and normalisation coefficients are wave-uniform
+		 * (scalar loads), where the flat idx loop loaded them per sample (the redo lists of
+		 * normalised stacks, ~200 k pixels, spent most of their time here) */
+		{
+			const int xx = slot_x[lane], cc = slot_c[lane], RR = slot_R[lane];
+			constexpr int NW = SG_SORT_THREADS / 64, NB = 8;
+			const uint16_t *plane = p.frames + (int64_t)cc * p.plane_stride;
+			/* NB frames per wave in flight: every lane loads from a clamped (always valid) address,
+			 * the sample is then selected (sg_gather's rules: an x-shifted sample is 0 and not
+			 * normalised, a y-shifted row reads 0 and is normalised) */
+			for (int f0 = __builtin_amdgcn_readfirstlane(wave); f0 < N; f0 += NW * NB) {
+				uint16_t raw[NB];
+				bool xin[NB];
 #pragma unroll
-			for (int k = 0; k < NB; k++) {
-				const int f = f0 + k * NW < N ? f0 + k * NW : N - 1;
-				const int sx = p.use_shift ? p.shiftx[f] : 0, sy = p.use_shift ? p.shifty[f] : 0;
-				const int sr = RR - sy, sc = xx - sx;
-				const bool yin = (unsigned)sr < (unsigned)p.H;
-				xin[k] = xx >= 0 && (unsigned)sc < (unsigned)p.W;
-				const int r = yin ? sr : 0, c = xin[k] ? sc : 0;
-				const uint16_t v = plane[(int64_t)f * p.frame_stride + (int64_t)r * p.W + c];
-				raw[k] = yin ? v : (uint16_t)0;
-			}
+				for (int k = 0; k < NB; k++) {
+					const int f = f0 + k * NW < N ? f0 + k * NW : N - 1;
+					const int sx = p.use_shift ? p.shiftx[f] : 0, sy = p.use_shift ? p.shifty[f] : 0;
+					const int sr = RR - sy, sc = xx - sx;
+					const bool yin = (unsigned)sr < (unsigned)p.H;
+					xin[k] = xx >= 0 && (unsigned)sc < (unsigned)p.W;
+					const int r = yin ? sr : 0, c = xin[k] ? sc : 0;
+					const uint16_t v = plane[(int64_t)f * p.frame_stride + (int64_t)r * p.W + c];
+					raw[k] = yin ? v : (uint16_t)0;
+				}
 #pragma unroll
-			for (int k = 0; k < NB; k++) {
-				const int f = f0 + k * NW;
-				if (f < N)
-					stage[f * SG_STAGE_STRIDE + lane] = xin[k] ? sg_normalize(p, f, raw[k]) : (uint16_t)0;
+				for (int k = 0; k < NB; k++) {
+					const int f = f0 + k * NW;
+					if (f < N)
+						stage[f * SG_STAGE_STRIDE + lane] = xin[k] ? sg_normalize(p, f, raw[k]) : (uint16_t)0;
+				}
 			}
 		}
-	}
-	__syncthreads();
+		__syncthreads();
 
-	/* 2. sort column pairs (2q, 2q+1) */
-	for (int q = wave; q < SG_TILE_W / 2; q += SG_SORT_THREADS / 64) {
-		uint32_t v[NREG];
+		/* 2. sort column pairs (2q, 2q+1) */
+		for (int q = wave; q < SG_TILE_W / 2; q += SG_SORT_THREADS / 64) {
+			uint32_t v[NREG];
 #pragma unroll
-		for (int r = 0; r < NREG; r++) {
-			const int f = r * 64 + lane;
-			v[r] = (f < N) ? stage32[f * (SG_STAGE_STRIDE / 2) + q] : 0xFFFFFFFFu;
-		}
-		bitonic_sort_packed<NREG>(v, lane);
-		/* write back sorted element e = lane*NREG + r into row e (only e < N) */
+			for (int r = 0; r < NREG; r++) {
+				const int f = r * 64 + lane;
+				v[r] = (f < N) ? stage32[f * (SG_STAGE_STRIDE / 2) + q] : 0xFFFFFFFFu;
+			}
+			bitonic_sort_packed<NREG>(v, lane);
+			/* write back sorted element e = lane*NREG + r into row e (only e < N) */
 #pragma unroll
-		for (int r = 0; r < NREG; r++) {
-			const int e = lane * NREG + r;
-			if (e < N)
-				stage32[e * (SG_STAGE_STRIDE / 2) + q] = v[r];
+			for (int r = 0; r < NREG; r++) {
+				const int e = lane * NREG + r;
+				if (e < N)
+					stage32[e * (SG_STAGE_STRIDE / 2) + q] = v[r];
+			}
 		}
+		__syncthreads();
 	}
-	__syncthreads();
 
 	/* 3. per-pixel rejection, one lane per pixel */
 	uint32_t my_rlo = 0, my_rhi = 0;

@@ -91,6 +91,7 @@ typedef unsigned short sgh_u16x2 __attribute__((ext_vector_type(2)));
  *   h[half][64][l]               : samples outside the band (u32: zeros, 65535s; anything
  *                                  else sends the pixel to the redo list) */
 #define SGH_HROWS (SGH_DW + 1)
+#define SGH_OVK 4	/* out-of-band sample values captured per column (normalised stacks) */
 template <int NI>
 struct alignas(16) SghLds {
 	uint32_t h[2 * NI][SGH_HROWS][64];
@@ -99,6 +100,10 @@ struct alignas(16) SghLds {
 	uint32_t lo2[NI][64];			/* band starts of the lane pixel pairs (u16 halves) */
 	uint32_t cs[NI][8][64];			/* wave 1's first 8 frames for the band centre (SGH_CENTER2W) */
 	uint8_t perm[128];			/* WINSORIZED finish order of the columns (SGH_WINS_ORDER) */
+	/* normalised SIGMA / WINSORIZED builds: the first SGH_OVK out-of-band samples of a column
+	 * that are neither 0 nor 65535, and how many there were (sgh_capture, sgh_compact) */
+	uint16_t ov[SGH_OVK][128 * NI];
+	uint32_t ovn[128 * NI];
 #ifdef SGH_WPROF
 	uint64_t wp[SghCfg<NI>::WAVES][16];	/* probe build: per-wave region cycles and events (sgh_wp) */
 #endif
@@ -672,6 +677,39 @@ __device__ __forceinline__ void sgh_bin_pair2(uint32_t *h, uint32_t l4, uint32_t
 		const sgh_u16x2 hv = __builtin_bit_cast(sgh_u16x2, hi2);
 		*nab += __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_elementwise_sub_sat(a16, hv), k1v)) +
 			__builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_elementwise_sub_sat(b16, hv), k1v));
+	}
+}
+
+/* normalised SIGMA / WINSORIZED builds: keep the value of an out-of-band sample other than 0 /
+ * 65535 (a cosmic ray that the frame's scale moved off 65535, a cold pixel).  Such a sample
+ * used to send its pixel to the redo list, whose kernel gathers the whole column again, one
+ * scattered line per sample (1.2 % of the pixels under multiplicative scaling, 1.65 ms of
+ * staging for 0.2 GB of data); with the few values known the finish writes the pixel's
+ * sorted column itself (sgh_compact).  A rare branch: the test is four VALU ops per pair */
+template <int NI>
+__device__ __forceinline__ void sgh_capture(SghLds<NI> &L, int i, int lane, uint32_t lo2, uint32_t v, uint32_t k1,
+		uint32_t ksat, uint32_t k255) {
+	/* packed: sat(v - lo - 255) > 0 (outside the band) and min(v, 1) - sat(v - 65534) = 1 (not 0,
+	 * not 65535); the last two are the build's own counter terms (shared after inlining) */
+	const sgh_u16x2 v16 = __builtin_bit_cast(sgh_u16x2, v);
+	const sgh_u16x2 d = __builtin_elementwise_sub_sat(v16 - __builtin_bit_cast(sgh_u16x2, lo2),
+			__builtin_bit_cast(sgh_u16x2, k255));
+	const sgh_u16x2 nrm = __builtin_elementwise_min(v16, __builtin_bit_cast(sgh_u16x2, k1)) -
+		__builtin_elementwise_sub_sat(v16, __builtin_bit_cast(sgh_u16x2, ksat));
+	const uint32_t g = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(d, nrm));
+	if (__builtin_expect(g != 0u, 0)) {
+		if (g & 0xFFFFu) {
+			const int col = 128 * i + lane;
+			const uint32_t k = atomicAdd(&L.ovn[col], 1u);
+			if (k < SGH_OVK)
+				L.ov[k][col] = (uint16_t)(v & 0xFFFFu);
+		}
+		if (g >> 16) {
+			const int col = 128 * i + 64 + lane;
+			const uint32_t k = atomicAdd(&L.ovn[col], 1u);
+			if (k < SGH_OVK)
+				L.ov[k][col] = (uint16_t)(v >> 16);
+		}
 	}
 }
 
@@ -1390,9 +1428,90 @@ __device__ __forceinline__ int sgh_median_pct(const SghPix &P, int N, double sl,
 	return SG_CLS_OK;
 }
 
+/* the compact redo (normalised SIGMA / WINSORIZED): every lane with `want` set owns a pixel
+ * whose samples are all known to the tile, the histogram's band, its zeros and 65535s and the
+ * k <= SGH_OVK captured out-of-band values.  The whole wave writes each such pixel's sorted
+ * column to p.cmp_cols[slot] (N u16: zeros, the captured values below the band, the band
+ * expanded bin by bin, those above it, 65535s) and its pixel to p.cmp_list[slot];
+ * k_stack_sorted<., true> then stages the column with coalesced loads instead of N scattered
+ * ones.  A pixel past p.cmp_cap goes to the redo list as before.  Wave-uniform control flow */
+template <int NI>
+__device__ __forceinline__ void sgh_compact(const SgStackParams &p, const SghLds<NI> &L, bool want, int col, int lo,
+		unsigned int pix, int nzl, int nsl, int kl, unsigned int *__restrict__ redo_count,
+		unsigned int *__restrict__ redo_list) {
+	const int lane = threadIdx.x & 63;
+	const int N = p.N;
+	uint64_t m = __ballot(want);
+	if (!m)
+		return;
+	/* one slot reservation for all of the wave's pixels (a returning global atomic per pixel
+	 * serialised the loop on its latency) */
+	unsigned int base = 0;
+	if (lane == 0)
+		base = atomicAdd(p.cmp_count, (unsigned int)__popcll(m));
+	base = (unsigned int)__builtin_amdgcn_readfirstlane((int)base);
+	for (unsigned int slot = base; m; slot++) {
+		const int src = __builtin_ctzll(m);
+		m &= m - 1;
+		const int cs = __builtin_amdgcn_readlane(col, src), ls = __builtin_amdgcn_readlane(lo, src);
+		const unsigned int ps = (unsigned int)__builtin_amdgcn_readlane((int)pix, src);
+		if (slot >= p.cmp_cap) {
+			if (lane == 0)
+				redo_list[atomicAdd(redo_count, 1u)] = ps;
+			continue;
+		}
+		uint16_t *dst = p.cmp_cols + (size_t)slot * (size_t)N;
+		const int nz = __builtin_amdgcn_readlane(nzl, src), ns = __builtin_amdgcn_readlane(nsl, src);
+		const int k = __builtin_amdgcn_readlane(kl, src);	/* <= SGH_OVK: checked by the caller */
+		/* the captured values: lane t < k holds value t; below the band or above it */
+		const int ov = lane < k ? (int)L.ov[lane < SGH_OVK ? lane : 0][cs] : 0;
+		const bool below = lane < k && ov < ls;
+		const int nbelow = __popcll(__ballot(below)), nabove = k - nbelow;
+		if (lane < k) {
+			/* rank among the captured values on the same side (ties by index) */
+			int r = 0;
+#pragma unroll
+			for (int t = 0; t < SGH_OVK; t++) {
+				const int u = __shfl(ov, t, 64);
+				if (t < k && t != lane && ((u < ls) == below) && (u < ov || (u == ov && t < lane)))
+					r++;
+			}
+			dst[below ? nz + r : N - ns - nabove + r] = (uint16_t)ov;
+		}
+		/* the band: lane l expands dword l (values lo + 4 l .. lo + 4 l + 3) after the exclusive
+		 * prefix of the lanes before it */
+		const uint32_t d = L.h[cs >> 6][lane][cs & 63];
+		const int c0 = (int)(d & 0xFFu), c1 = (int)((d >> 8) & 0xFFu), c2 = (int)((d >> 16) & 0xFFu), c3 = (int)(d >> 24);
+		const int tot = c0 + c1 + c2 + c3;
+		int inc = tot;
+#pragma unroll
+		for (int o = 1; o < 64; o <<= 1) {
+			const int y = __shfl_up(inc, o, 64);
+			if (lane >= o)
+				inc += y;
+		}
+		int pos = nz + nbelow + inc - tot;
+		const int v0 = ls + 4 * lane;
+		const int cnt[4] = {c0, c1, c2, c3};
+#pragma unroll
+		for (int b = 0; b < 4; b++) {
+			for (int r = 0; r < cnt[b]; r++)
+				dst[pos + r] = (uint16_t)(v0 + b);
+			pos += cnt[b];
+		}
+		for (int r = lane; r < nz; r += 64)
+			dst[r] = 0;
+		for (int r = N - ns + lane; r < N; r += 64)
+			dst[r] = 65535;
+		if (lane == 0)
+			p.cmp_list[slot] = ps;
+	}
+}
+
 /* pixel column `col` of the tile (x its image column); PAIR: lane pair half `half`, else one
- * lane per column (half = 0) */
-template <int REJ, bool PAIR, int NI, bool ZT = false>
+ * lane per column (half = 0); CAP: normalised SIGMA / WINSORIZED kernel (captured out-of-band
+ * values, sgh_compact) */
+template <int REJ, bool PAIR, int NI, bool ZT = false, bool CAP = false>
 __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int half, int lo, int R, int c, int x,
 		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list, bool zrow = false) {
 	const int lane = threadIdx.x & 63;
@@ -1508,6 +1627,7 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 	int cls = SG_CLS_OK;
 	uint16_t value = 0;
 	uint32_t rlo = 0, rhi = 0;
+	bool cmp = false;	/* CAP: the pixel's sorted column goes out through sgh_compact */
 	const uint64_t c1 = SG_DBG(p) == 11 ? __builtin_readcyclecounter() : 0;
 	if (x < p.W) {
 		if (SG_DBG(p) == 1) {
@@ -1515,6 +1635,10 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 		} else if (P.nb + oob != N || (zc && zmax >= lo) || (REJ != 1 && REJ != 8 && oob != P.nz + P.ns + zc)) {
 			cls = 1;	/* out-of-band sample other than 0 / 65535 (or than this row's normalised
 				 * zeros), or a wrapped u8 counter */
+			if (CAP && p.cmp_cols) {	/* every sample known: no wrap, no row zeros, all captured */
+				const int k = oob - P.nz - P.ns;
+				cmp = P.nb + oob == N && zc == 0 && k > 0 && k <= SGH_OVK && (int)L.ovn[col] == k;
+			}
 		} else {
 			const long long dz = -(long long)lo, ds = 65535 - (long long)lo;
 			P.Z.c = P.nz;
@@ -1566,7 +1690,7 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 				if (SG_DBG(p) != 11)	/* the timeline A/B keeps its stamps in the output buffer */
 					p.out[pix] = value;
 #endif
-			} else {
+			} else if (!cmp) {
 #ifndef SGH_WPROF
 				const unsigned int slot = atomicAdd(redo_count, 1u);
 				redo_list[slot] = (unsigned int)pix;
@@ -1605,6 +1729,9 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 		}
 	}
 #endif
+	if (CAP)
+		sgh_compact<NI>(p, L, cmp && !half && x < p.W, col, lo, (unsigned int)(((int64_t)c * p.H + R) * p.W + x),
+				P.nz, P.ns, oob - P.nz - P.ns, redo_count, redo_list);
 	const unsigned long long a = sgh_wave_sum(rlo), b = sgh_wave_sum(rhi);
 	if (lane == 0 && (a | b)) {
 		unsigned long long *sh = p.rej + ((size_t)((blockIdx.x * 8 + (col >> 5)) % SG_REJ_SHARDS) * 6 + c * 2);
@@ -1637,6 +1764,7 @@ __device__ __forceinline__ void sgh_clear(SghLds<NI> &L, bool wait_prev, const B
 		((uint4 *)L.nz)[threadIdx.x] = z;
 		((uint4 *)L.ns)[threadIdx.x] = z;
 		((uint4 *)L.na)[threadIdx.x] = z;
+		((uint4 *)L.ovn)[threadIdx.x] = z;
 	}
 }
 
@@ -1787,6 +1915,7 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
 	uint32_t *const h = &L.h[0][0][0];
 	const uint32_t l4 = (uint32_t)lane * 4u;
 	const uint32_t k1 = sgh_opaque(0x00010001u), ksat = sgh_opaque(0xFFFEFFFEu);
+	const uint32_t k255 = NORM && !AB ? sgh_opaque(0x00FF00FFu) : 0u;
 	uint32_t buf[NB][2][MB][NI], fix[NB][2][NI];
 	SghTab16 T;
 	/* half hh (frames f16 + 8 hh ..) of the block at f16, bounds-checked unless whole */
@@ -1915,6 +2044,8 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
 							v = sgh_norm_pair<NORM, EDGE>(v, a, b, fx[i], m);
 						sgh_bin_pair<AB>(h + i * (2 * SGH_HROWS * 64), l4, lo2[i], v, nonzero[i], nsat[i], k1, ksat,
 								AB ? nab + i : nullptr, hi2[i]);
+						if (NORM && !AB)
+							sgh_capture(L, i, lane, lo2[i], v, k1, ksat, k255);
 					}
 				}
 			}
@@ -2082,19 +2213,21 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 			if (wave >= 2)
 				return;
 			const int col = L.perm[64 * wave + lane];
-			sgh_finish2<REJ, false, NI>(p, L, col, 0, col_lo(col), R, c, col_x(col), redo_count, redo_list);
+			sgh_finish2<REJ, false, NI, false, NORM != 0>(p, L, col, 0, col_lo(col), R, c, col_x(col), redo_count,
+					redo_list);
 			return;
 		}
 		for (int col = 64 * wave + lane; col < COLS; col += 64 * WAVES)
-			sgh_finish2<REJ, false, NI>(p, L, col, 0, col_lo(col), R, c, col_x(col), redo_count, redo_list);
+			sgh_finish2<REJ, false, NI, false, NORM != 0>(p, L, col, 0, col_lo(col), R, c, col_x(col), redo_count,
+					redo_list);
 		return;
 	}
 	/* every wave finishes 32 pixel columns, a lane pair per column */
 	const int half = lane & 1;
 	int col = 32 * wave + (lane >> 1);
 	for (; col < COLS; col += 32 * WAVES)
-		sgh_finish2<REJ, true, NI, NORM == 1 || NORM == 3>(p, L, col, half, col_lo(col), R, c, col_x(col), redo_count,
-				redo_list, interior);
+		sgh_finish2<REJ, true, NI, NORM == 1 || NORM == 3, NORM != 0 && REJ == 2>(p, L, col, half, col_lo(col), R, c,
+				col_x(col), redo_count, redo_list, interior);
 	if (timeline && lane == 0) {
 		const uint64_t t = __builtin_amdgcn_s_memrealtime();
 		if (wave == 0)

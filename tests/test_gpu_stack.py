@@ -245,6 +245,74 @@ def test_hist_path_normalised_saturation(gpu_ctx, normalize, rejection):
     assert (nv > 65535.5).any()
 
 
+def _outlier_frames(N, H, W, seed):
+    """synthetic frames with sparse out-of-band samples: 1..6 frames of ~4 % of the pixels hold a
+    cosmic ray (20000..65000) or a cold value (1..300), so some pixels keep all their unknown
+    values within the histogram kernel's capture (<= 4) and others overflow it"""
+    frames = orc.synth(N, 1, H, W, seed=seed, maxshift=6)
+    rng = np.random.default_rng(seed)
+    npx = int(0.04 * H * W)
+    ys, xs = rng.integers(0, H, npx), rng.integers(0, W, npx)
+    for y, x in zip(ys, xs):
+        k = int(rng.integers(1, 7))
+        fs = rng.choice(N, k, replace=False)
+        hot = rng.random(k) < 0.7
+        frames[fs, 0, y, x] = np.where(hot, rng.integers(20000, 65001, k), rng.integers(1, 301, k)).astype(np.uint16)
+    return frames
+
+
+@pytest.mark.parametrize("rejection", [sg.SIGMA, sg.WINSORIZED])
+@pytest.mark.parametrize("normalize", [sg.MULTIPLICATIVE_SCALING, sg.ADDITIVE_SCALING, sg.MULTIPLICATIVE])
+@pytest.mark.parametrize("cap", [None, 40])
+def test_hist_path_normalised_compact_redo(gpu_ctx, normalize, rejection, cap):
+    """normalised stacks: a pixel whose out-of-band samples (besides 0 / 65535) are few leaves
+    its sorted column from the histogram kernel (sgh_compact) and the sorted kernel stages it
+    without a gather; more than 4 such samples, or a full compact list (cap = 40 pixels), send
+    the pixel to the gathering redo list.  Both must equal the oracle"""
+    N, H, W = 64, 48, 300
+    seed = 900 + normalize
+    frames = _outlier_frames(N, H, W, seed)
+    sx, sy = orc.synth_shifts(N, seed=seed, maxshift=6)
+    rng = np.random.default_rng(seed + 1)
+    loc = 1000 + rng.random(N) * 40
+    loc[0] = 1000.0
+    scl = 30 + rng.random(N) * 0.9
+    off, mul, scale = orc.compute_normalization(normalize, loc, scl, ref_image=0)
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=rejection, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                              normalize=normalize, offset=off, mul=mul, scale=scale, max_thread=2,
+                              max_number_of_rows=H)
+
+    def run(ctx):
+        rc, out, rej, _ = ctx.stack_host(desc, np.ascontiguousarray(frames))
+        assert rc == 0, ctx.error()
+        return out, rej, ctx.stats()
+
+    if cap is None:
+        out, rej, st = run(gpu_ctx)
+    else:
+        import os
+        old = os.environ.get("SG_HIST_COMPACT")
+        os.environ["SG_HIST_COMPACT"] = str(cap)
+        try:
+            with sg.Context() as ctx:
+                out, rej, st = run(ctx)
+        finally:
+            if old is None:
+                del os.environ["SG_HIST_COMPACT"]
+            else:
+                os.environ["SG_HIST_COMPACT"] = old
+    assert st.path == 1
+    rc, ref, rej_ref = orc.stack_rejection(frames, rejection, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                                           normalize=normalize, offset=off, mul=mul, scale=scale, max_thread=2)
+    assert rc == 0
+    assert_same(out, ref, f"compact norm={normalize} rej={rejection} cap={cap}")
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+    if cap is None:
+        assert st.compact_pixels >= 100, st.compact_pixels
+    else:
+        assert st.compact_pixels == cap, st.compact_pixels
+
+
 @pytest.mark.parametrize("rejection", [sg.SIGMA, sg.WINSORIZED])
 @pytest.mark.parametrize("tiny", [False, True])
 def test_hist_path_additive_fold(gpu_ctx, rejection, tiny):
