@@ -399,7 +399,9 @@ F80_HD sg_dd dd_round64(double hi, double lo, int exact, int *amb) {
 	if ((hb & 0xFFFFFFFFFFFFFull) == 0 && lo != 0.0 && ((lo < 0.0) != (hi < 0.0)))
 		e--;	/* hi a power of two, the value in the binade below */
 	const double u = f80_pow2(e - 63);
-	const double x = lo / u;	/* exact: a power-of-two scale */
+	/* exact: a power-of-two scale (a multiply; a division here cost a full fp64 divide sequence
+	 * per rounding, three per recurrence step) */
+	const double x = e > -900 ? lo * f80_pow2(63 - e) : lo / u;
 	const double rx = rint(x);	/* ties to even: hi / u is a multiple of 2^10 */
 	if (!exact && fabs(fabs(x - rx) - 0.5) < 9.3e-10)
 		*amb = 1;
@@ -420,10 +422,14 @@ F80_HD sg_dd dd80_add(sg_dd a, sg_dd b) {
 /* x87 a / d for an integer count 1 <= d < 2^21 */
 F80_HD sg_dd dd80_div_count(sg_dd a, uint32_t d) {
 	const double y = (double)d;
-	const double th = a.hi / y;
+	/* one division per step: th only needs to lie within a few ulps of a.hi / y (the exact
+	 * remainder a - th y corrects it) and tl's relative error 2^-52 on a remainder of a few
+	 * ulp(th) stays far below the 2^-93 |v| the midpoint test allows */
+	const double ry = 1.0 / y;
+	const double th = a.hi * ry;
 	const sg_dd p = dd_two_prod(th, y);
 	const double dh = a.hi - p.hi, dl = a.lo - p.lo;
-	const double tl = (dh + dl) / y;
+	const double tl = (dh + dl) * ry;
 	const sg_dd z = dd_fast_two_sum(th, tl);
 	int amb = 0;
 	const sg_dd r = dd_round64(z.hi, z.lo, 0, &amb);
