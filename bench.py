@@ -132,7 +132,8 @@ def cpu_baseline(args, N, W, median=False):
         rc, out = orc.stack_median(frames, max_thread=threads, max_number_of_rows=rows)
         what = "stack_median"
     else:
-        rej_mode = {"sigma": 2, "winsorized": 4, "none": 0, "percentile": 1}[args.rejection]
+        rej_mode = {"sigma": 2, "winsorized": 4, "none": 0, "percentile": 1, "sigmedian": 3,
+                    "linearfit": 5}[args.rejection]
         rc, out, rej = orc.stack_rejection(frames, rej_mode, sig=(4.0, 3.0) if rej_mode != 1 else (0.2, 0.1),
                                            shiftx=sx, shifty=sy, max_thread=threads, max_number_of_rows=rows)
         what = f"stack_mean_with_rejection {args.rejection}"
@@ -293,7 +294,7 @@ def main_sigma(args):
     dev = torch.cuda.current_device()
     N, W, H = args.frames, args.width, args.height
     rej_mode = {"sigma": sg.SIGMA, "winsorized": sg.WINSORIZED, "none": sg.NO_REJEC,
-                "percentile": sg.PERCENTILE}[args.rejection]
+                "percentile": sg.PERCENTILE, "sigmedian": sg.SIGMEDIAN, "linearfit": sg.LINEARFIT}[args.rejection]
     median = args.workload == "median"
     method = sg.MEDIAN if median else sg.MEAN
     sig = (0.2, 0.1) if rej_mode == sg.PERCENTILE else (4.0, 3.0)

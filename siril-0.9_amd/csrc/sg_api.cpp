@@ -525,6 +525,7 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 	p.rej = (unsigned long long *)dv.ctr.p;
 	p.flag_count = (unsigned int *)((char *)dv.ctr.p + REJB);
 	p.walk_fault = p.flag_count + 1;
+	p.loop_fault = p.flag_count + 4;
 	p.maxim = (unsigned int *)((char *)dv.ctr.p + REJB + 64);
 	const unsigned int *ctr_flags = (const unsigned int *)((const char *)dv.ctr_h + REJB);
 	bool have_counts = false;
@@ -845,6 +846,9 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 	}
 	const unsigned long long *shards = (const unsigned long long *)dv.ctr_h;
 	const unsigned int cnt[3] = {ctr_flags[0], ctr_flags[1], ctr_flags[16]};	/* flag count, walk fault, sum maximum */
+	if (ctr_flags[4])
+		return set_err(ctx, SG_ERR_GENERIC, "SIGMEDIAN: the reference's clipping loop never ends for some pixel "
+				"(a pass replaces samples by the values they already hold, stacking.c:1696-1709)%s%.0ld", "", 0);
 	if (cnt[1])
 		return set_err(ctx, SG_ERR_WALK, "a first-pass early break needs the stale rejected[] of a pixel "
 				"whose frame rows are not resident; make the full frames resident%s%.0ld", "", 0);

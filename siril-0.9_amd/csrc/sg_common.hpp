@@ -17,7 +17,8 @@
 #endif
 #define SG_DBG(p) (SG_DBG_MODES ? (p).dbg : 0)
 
-enum { SG_CLS_OK = 0, SG_CLS_LITERAL = 1, SG_CLS_CHAIN = 2, SG_CLS_DONE = 3 };
+enum { SG_CLS_OK = 0, SG_CLS_LITERAL = 1, SG_CLS_CHAIN = 2, SG_CLS_DONE = 3,
+	SG_CLS_NOTERM = 4 /* SIGMEDIAN whose reference loop never ends (p.loop_fault; the call fails) */ };
 /* k_stack_replay: waves per block (one pixel per wave, ~18 KB of LDS each), max frames */
 #define SG_REPLAY_WAVES 2
 #define SG_REPLAY_MAXN 2048
@@ -54,6 +55,7 @@ struct SgStackParams {
 	int res_begin, res_end;			/* memory rows present at `frames` (desc->resident_rows) */
 	int sy_min, sy_max;			/* range of shifty (0, 0 without shifts) */
 	unsigned int *walk_fault;		/* set when a stale-state chain needs rows that are not resident */
+	unsigned int *loop_fault;		/* set when a SIGMEDIAN pixel's reference loop never ends */
 	unsigned long long *rej;		/* [SG_REJ_SHARDS][3][2] */
 	unsigned int *flag_count;
 	unsigned int *flag_list;		/* encoded (c*H + R)*W + x */

@@ -260,6 +260,131 @@ __device__ int reject_sigma(const SgCol &A, SgRejState &st, double sl, double sh
 	return SG_CLS_OK;
 }
 
+/* SIGMEDIAN (:1696-1709): a rejected sample is replaced by round_to_WORD(median) and N stays,
+ * so the pixel's multiset is the sorted window A[lo, hi) of samples never replaced plus a few
+ * groups of equal replacement values (one new group per pass at most, ascending by value).
+ * st.S / st.SS hold the whole multiset's exact moments; sigma and the decisions take the SIGMA
+ * path's rounding band, a decision inside it goes to the literal kernel. */
+#define SG_SMG 4	/* replacement groups a pixel may collect before it goes to the literal kernel */
+struct SgSmed {
+	int ng;
+	uint32_t gv[SG_SMG];
+	int gc[SG_SMG];
+};
+/* # multiset elements < t (le: <= t) */
+__device__ __forceinline__ int smed_count(const SgCol &A, const SgRejState &st, const SgSmed &g, double t, bool le) {
+	int c = le ? col_count_le(A, st.lo, st.hi, t) : col_count_lt(A, st.lo, st.hi, t);
+	for (int k = 0; k < g.ng; k++)
+		c += (le ? (double)g.gv[k] <= t : (double)g.gv[k] < t) ? g.gc[k] : 0;
+	return c;
+}
+/* the r-th smallest element (0-based) of the multiset */
+__device__ __forceinline__ uint32_t smed_at(const SgCol &A, const SgRejState &st, const SgSmed &g, int r) {
+	int before = 0;	/* group elements ranked before r */
+	for (int k = 0; k < g.ng; k++) {
+		const int start = col_count_lt(A, st.lo, st.hi, (double)g.gv[k]) + before;
+		if (r < start)
+			break;
+		if (r < start + g.gc[k])
+			return g.gv[k];
+		before += g.gc[k];
+	}
+	return A(st.lo + r - before);
+}
+__device__ int reject_sigmedian(const SgCol &A, SgRejState &st, double sl, double sh, int N0) {
+	SgSmed g;
+	g.ng = 0;
+	int n;
+	do {
+		/* the reference has no cap: a pass whose replacements hold the values they replace
+		 * repeats forever (e.g. {0, 0, 1, 1} with sig[1] < 0.87: median 0.5, both 1s clipped and
+		 * set to round_to_WORD(0.5) = 1); such a pixel, or one past 4096 passes, fails the call */
+		if (++st.iter > 4096)
+			return SG_CLS_NOTERM;
+		bool e0;
+		const double sigma = exact_sd(N0, st.S, st.SS, &e0);
+		const int g1 = (N0 - 1) / 2, g2 = N0 / 2;
+		const uint32_t m1 = smed_at(A, st, g, g1), m2 = g1 == g2 ? m1 : smed_at(A, st, g, g2);
+		const double median = g1 == g2 ? (double)m1 : (double)(m1 + m2) / 2.0;
+		const double tl = sl * sigma, th = sh * sigma;
+		const double blo = median - tl, bhi = median + th;
+		/* low: median - v > tl, else high: v - median > th (median - v is exact) */
+		double tlo = blo, thi = bhi;
+		if (!e0) {
+			const double tol = SG_BAND * (fabs(median) + fabs(tl) + fabs(th) + 1.0);
+			if (smed_count(A, st, g, blo - tol, false) != smed_count(A, st, g, blo + tol, true))
+				return SG_WHY(21);
+			if (smed_count(A, st, g, bhi - tol, false) != smed_count(A, st, g, bhi + tol, true))
+				return SG_WHY(22);
+			tlo = blo - tol;	/* no element lies within tol of either threshold */
+			thi = bhi + tol;
+		}
+		const int L = smed_count(A, st, g, tlo, false), H = N0 - smed_count(A, st, g, thi, true);
+		if (L + H > N0)
+			return SG_WHY(23);	/* negative sigma factors: the else-if order matters */
+		n = L + H;
+		st.rlo += (uint32_t)L;
+		st.rhi += (uint32_t)H;
+		if (!n)
+			break;
+		/* the window's rejected prefix and suffix, then the rejected groups */
+		const int wl = col_count_lt(A, st.lo, st.hi, tlo);
+		const int wh = (st.hi - st.lo) - col_count_le(A, st.lo, st.hi, thi);
+		uint64_t rs = 0, rss = 0;	/* moments of the replaced samples */
+		for (int i = 0; i < wl; i++) {
+			const uint64_t v = A(st.lo + i);
+			rs += v;
+			rss += v * v;
+		}
+		for (int i = 0; i < wh; i++) {
+			const uint64_t v = A(st.hi - 1 - i);
+			rs += v;
+			rss += v * v;
+		}
+		st.lo += wl;
+		st.hi -= wh;
+		int ng = 0;
+		for (int k = 0; k < g.ng; k++) {
+			const double v = (double)g.gv[k];
+			if (v < tlo || v > thi) {
+				const uint64_t u = g.gv[k];
+				rs += u * (uint64_t)g.gc[k];
+				rss += u * u * (uint64_t)g.gc[k];
+			} else {
+				g.gv[ng] = g.gv[k];
+				g.gc[ng] = g.gc[k];
+				ng++;
+			}
+		}
+		g.ng = ng;
+		/* the n replacements round_to_WORD(median), kept ascending */
+		const uint32_t mw = sg_round_to_WORD(median);
+		/* every replaced sample already equal to mw (equal sums and sums of squares): the next
+		 * pass sees the same array */
+		if (rs == (uint64_t)mw * n && rss == (uint64_t)mw * mw * n)
+			return SG_CLS_NOTERM;
+		st.S += (uint64_t)mw * (uint64_t)n - rs;
+		st.SS += (uint64_t)mw * mw * (uint64_t)n - rss;
+		int k = 0;
+		while (k < g.ng && g.gv[k] < mw)
+			k++;
+		if (k < g.ng && g.gv[k] == mw) {
+			g.gc[k] += n;
+		} else {
+			if (g.ng == SG_SMG)
+				return SG_WHY(24);
+			for (int j = g.ng; j > k; j--) {
+				g.gv[j] = g.gv[j - 1];
+				g.gc[j] = g.gc[j - 1];
+			}
+			g.gv[k] = mw;
+			g.gc[k] = n;
+			g.ng++;
+		}
+	} while (n > 0 && N0 > 3);
+	return SG_CLS_OK;
+}
+
 /* element i of the Winsorized copy w = [vlo x Lw] ++ A[lo+Lw, hi-Hw) ++ [vhi x Hw] */
 struct SgWins {
 	int Lw, Hw;
@@ -602,13 +727,21 @@ k_stack_sorted(SgStackParams p, const unsigned int *__restrict__ list, const uns
 				case 4:
 					cls = reject_winsorized(A, st, p.sig0, p.sig1, N);
 					break;
+				case 3:
+					cls = reject_sigmedian(A, st, p.sig0, p.sig1, N);
+					if (cls == SG_CLS_NOTERM) {
+						*p.loop_fault = 1u;
+						cls = SG_CLS_OK;
+					}
+					break;
 				case 0:
 					break;
-				default:	/* SIGMEDIAN, LINEARFIT: literal path */
+				default:	/* LINEARFIT: literal path */
 					cls = SG_CLS_LITERAL;
 				}
 				if (cls == SG_CLS_OK) {
-					value = sg_round_to_WORD((double)st.S / (double)(st.hi - st.lo));
+					/* SIGMEDIAN keeps all N samples (the replaced ones in st.S) */
+					value = sg_round_to_WORD((double)st.S / (double)(p.rejection == 3 ? N : st.hi - st.lo));
 					my_rlo = st.rlo;
 					my_rhi = st.rhi;
 				}
@@ -1141,19 +1274,28 @@ __device__ uint16_t literal_pixel(uint16_t *stack, int8_t *rejected, uint16_t *w
 		} while (n > 0 && N > 3);
 		break;
 	case 3: {
+		/* a pass whose replacements change nothing repeats forever in the reference (see
+		 * reject_sigmedian): *first_break = 2 reports it, as does a pixel past 4096 passes */
 		int guard = 0;
 		do {
 			sigma = lit_sd(stack, N);
 			shellsort_u16(stack, N);
 			median = lit_median(stack, N);
 			n = 0;
+			bool changed = false;
 			for (frame = 0; frame < N; frame++) {
 				if (lit_sigma_clip(stack[frame], sl, sh, sigma, median, crej)) {
-					stack[frame] = sg_round_to_WORD(median);
+					const uint16_t mw = sg_round_to_WORD(median);
+					changed |= stack[frame] != mw;
+					stack[frame] = mw;
 					n++;
 				}
 			}
-		} while (n > 0 && N > 3 && ++guard < 100000);
+			if (n > 0 && N > 3 && (!changed || ++guard >= 4096)) {
+				*first_break = 2;
+				break;
+			}
+		} while (n > 0 && N > 3);
 		break;
 	}
 	case 5:
@@ -2129,7 +2271,7 @@ k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *s
 						rejected[k] = 0;
 					gather_stack(p, q, stack);
 					literal_pixel(stack, rejected, wst, p.N, p.rejection, p.sig0, p.sig1, dummy, &fbrk);
-					if (!(fbrk && p.N > 4))
+					if (!(fbrk == 1 && p.N > 4))
 						break;
 				}
 				q = chain_pred(p, t, q);
@@ -2164,7 +2306,9 @@ k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *s
 		}
 		gather_stack(p, pix, stack);
 		const uint16_t v = literal_pixel(stack, rejected, wst, p.N, p.rejection, p.sig0, p.sig1, crej, &fbrk);
-		if (phase == 1 && fbrk && p.N > 4) {
+		if (p.rejection == 3 && fbrk == 2)
+			*p.loop_fault = 1u;
+		if (phase == 1 && fbrk == 1 && p.N > 4) {
 			p.flag_map[pix] = SG_CLS_CHAIN;
 			continue;
 		}

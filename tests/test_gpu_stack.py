@@ -48,6 +48,45 @@ def test_rejection_parity(gpu_ctx, rejection, C):
     assert np.array_equal(rej, rej_ref), (rej, rej_ref)
 
 
+@pytest.mark.parametrize("N", [2, 3, 4, 7, 16, 64, 200])
+@pytest.mark.parametrize("sig", [(4.0, 3.0), (1.0, 1.0), (2.5, 1.2)])
+def test_sigmedian_sorted_path(gpu_ctx, N, sig):
+    """SIGMEDIAN on the sorted kernel (replacement groups over the sorted window, exact moments,
+    the SIGMA band; more than 4 groups or a decision in the band go to the literal kernel): the
+    image and the counters equal the oracle, and with the default sigmas the literal kernel
+    takes few pixels"""
+    H, W = 20, 130
+    frames = _outlier_frames(N, H, W, 700 + N)
+    rng = np.random.default_rng(N)
+    frames[:, :, :, :8] = rng.integers(900, 1100, size=(N, 1, H, 8)).astype(np.uint16)  # noise-only columns
+    sx, sy = orc.synth_shifts(N, seed=700 + N, maxshift=3)
+    rc, ref, rej_ref = orc.stack_rejection(frames, sg.SIGMEDIAN, sig=sig, shiftx=sx, shifty=sy, max_thread=2)
+    assert rc == 0
+    out, rej, _ = gpu_stack(gpu_ctx, frames, sg.MEAN, sg.SIGMEDIAN, sig, sx, sy, max_thread=2)
+    assert_same(out, ref, f"sigmedian N={N} sig={sig}")
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+    if sig == (4.0, 3.0) and N >= 16:
+        assert gpu_ctx.stats().slow_pixels <= 0.02 * H * W, gpu_ctx.stats().slow_pixels
+
+
+def test_sigmedian_never_ending_loop_fails(gpu_ctx):
+    """the reference's SIGMEDIAN loop has no cap: {990, 0, 0, 1049} with sig = (2.5, 0.7) halves
+    its top pair towards {0, 0, 1, 1}, where both 1s are clipped and replaced by
+    round_to_WORD(0.5) = 1 forever (stacking.c:1696-1709; Siril hangs).  The call fails with an
+    error instead of hanging the GPU (the oracle is not run: it would not return)"""
+    N, H, W = 4, 8, 16
+    frames = np.full((N, 1, H, W), 1000, dtype=np.uint16)     # (noise of a few ADU at N = 4 can
+    frames[:, 0, 3, 5] = [990, 0, 0, 1049]                     # reach the same kind of cycle)
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=sg.SIGMEDIAN, sig=(2.5, 0.7), max_thread=1,
+                              max_number_of_rows=H)
+    rc, out, rej, _ = gpu_ctx.stack_host(desc, np.ascontiguousarray(frames))
+    assert rc != 0
+    assert "never ends" in gpu_ctx.error()
+    frames[:, 0, 3, 5] = 1000      # the same stack without that pixel succeeds
+    rc, out, rej, _ = gpu_ctx.stack_host(desc, np.ascontiguousarray(frames))
+    assert rc == 0, gpu_ctx.error()
+
+
 @pytest.mark.parametrize("N", [2, 3, 4, 5, 6, 7, 8, 9, 12])
 @pytest.mark.parametrize("rejection", [sg.SIGMA, sg.WINSORIZED, sg.LINEARFIT])
 def test_small_n_stale_state(gpu_ctx, N, rejection):
@@ -254,7 +293,7 @@ def _outlier_frames(N, H, W, seed):
     npx = int(0.04 * H * W)
     ys, xs = rng.integers(0, H, npx), rng.integers(0, W, npx)
     for y, x in zip(ys, xs):
-        k = int(rng.integers(1, 7))
+        k = min(int(rng.integers(1, 7)), N)
         fs = rng.choice(N, k, replace=False)
         hot = rng.random(k) < 0.7
         frames[fs, 0, y, x] = np.where(hot, rng.integers(20000, 65001, k), rng.integers(1, 301, k)).astype(np.uint16)
