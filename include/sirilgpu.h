@@ -138,6 +138,10 @@ int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *desc, sg_read_region_fn pull,
  * read above the frame.  The reference then writes offset = W*(area.y - shifty) past its block
  * buffer (stacking.c:1555-1561, a heap overflow with an undefined result); the call fails with
  * SG_ERR_GENERIC and a message instead of zero-filling.  Keep |shifty| below the block height.
+ * Second refused regime: a SIGMEDIAN pixel whose clipping loop (stacking.c:1696-1709, no pass
+ * cap) never ends, i.e. a pass replaces samples by the values they already hold (e.g. {0, 0,
+ * 1, 1} with sig[1] < 0.87) or the pixel needs more than 4096 passes; Siril hangs there, the
+ * call fails with SG_ERR_GENERIC.
  */
 int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_desc *desc,
 		const uint16_t *d_frames, int64_t frame_stride, int64_t plane_stride,
