@@ -620,7 +620,9 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 
 		const int ntx = (W + SG_TILE_W - 1) / SG_TILE_W;
 		const size_t nblk = (size_t)ntx * nrows * C;
-		const size_t lds = (size_t)N * SG_STAGE_STRIDE * 2;
+		/* LINEARFIT: + one rejected[] bit per frame and pixel of the tile (reject_linearfit) */
+		const size_t lds = (size_t)N * SG_STAGE_STRIDE * 2 +
+			(d->rejection == SG_LINEARFIT ? (size_t)64 * ((N + 31) / 32) * 4 : 0);
 		if (hist) {
 			HIPCHK(ensure(dv.redo, sizeof(unsigned int) * (npix_launch + 16)));
 			unsigned int *redo_count = p.flag_count + 2;	/* cleared with the counters */

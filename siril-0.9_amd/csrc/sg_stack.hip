@@ -385,6 +385,74 @@ __device__ int reject_sigmedian(const SgCol &A, SgRejState &st, double sl, doubl
 	return SG_CLS_OK;
 }
 
+/* LINEARFIT (:1750-1784) literally on the lane's sorted column in LDS (element e at
+ * col[e * SG_STAGE_STRIDE]): gsl_fit_linear's double recurrences, the mean absolute residual,
+ * line_clipping with rejected[] by position (one bit per entry in LDS, rb[(j / 32) * 64]; the
+ * entries after the `N - r <= 4` break keep this pixel's previous pass) and the order-preserving
+ * removal, compacting the column in place (a sorted array stays sorted, so quicksort_s is the
+ * identity).  The double operations and their order are k_stack_literal's, so the result is
+ * bit-identical; a first pass that breaks early needs the previous pixel's stale entries and
+ * goes to the literal kernel. */
+__device__ int reject_linearfit(uint16_t *col, uint32_t *rb, int N0, double sl, double sh, SgRejState &st) {
+	auto at = [&](int e) -> uint32_t { return col[e * SG_STAGE_STRIDE]; };
+	int N = N0, r = 0, n, pass = 0;
+	do {
+		double m_x = 0, m_y = 0, m_dx2 = 0, m_dxdy = 0;
+		for (int i = 0; i < N; i++) {
+			m_x += ((double)i - m_x) / (i + 1.0);
+			m_y += ((double)at(i) - m_y) / (i + 1.0);
+		}
+		for (int i = 0; i < N; i++) {
+			const double dx = (double)i - m_x;
+			const double dy = (double)at(i) - m_y;
+			m_dx2 += (dx * dx - m_dx2) / (i + 1.0);
+			m_dxdy += (dx * dy - m_dxdy) / (i + 1.0);
+		}
+		const double a = m_dxdy / m_dx2;
+		const double b = m_y - m_x * a;
+		double sigma = 0.0;
+		for (int f = 0; f < N; f++)
+			sigma += (fabs((double)at(f) - (a * (double)f + b)));
+		sigma /= (double)N;
+		n = 0;
+		int frame;
+		for (frame = 0; frame < N; frame++) {
+			int v = 0;
+			if (((a * (double)frame + b - (double)at(frame)) / sigma) > sl) {
+				st.rlo++;
+				v = -1;
+			} else if ((((double)at(frame) - a * (double)frame - b) / sigma) > sh) {
+				st.rhi++;
+				v = 1;
+			}
+			uint32_t &w = rb[(frame >> 5) * 64];
+			w = v ? (w | (1u << (frame & 31))) : (w & ~(1u << (frame & 31)));
+			if (v != 0)
+				r++;
+			if (N - r <= 4)
+				break;
+		}
+		if (pass++ == 0 && frame < N - 1)
+			return SG_CLS_LITERAL;
+		for (int f = 0, j = 0; f < N - n; f++, j++) {
+			if ((rb[(j >> 5) * 64] >> (j & 31)) & 1u) {
+				for (int k = f; k < N - n - 1; k++)
+					col[k * SG_STAGE_STRIDE] = col[(k + 1) * SG_STAGE_STRIDE];
+				f--;
+				n++;
+			}
+		}
+		N -= n;
+	} while (n > 0 && N > 3);
+	uint64_t S = 0;
+	for (int e = 0; e < N; e++)
+		S += at(e);
+	st.S = S;
+	st.lo = 0;
+	st.hi = N;
+	return SG_CLS_OK;
+}
+
 /* element i of the Winsorized copy w = [vlo x Lw] ++ A[lo+Lw, hi-Hw) ++ [vhi x Hw] */
 struct SgWins {
 	int Lw, Hw;
@@ -691,13 +759,14 @@ k_stack_sorted(SgStackParams p, const unsigned int *__restrict__ list, const uns
 	}
 
 	/* 3. per-pixel rejection, one lane per pixel */
+	const int sl = tid;
 	uint32_t my_rlo = 0, my_rhi = 0;
 	if (tid < SG_TILE_W) {
-		const int x = slot_x[tid];
-		const int c = slot_c[tid];
-		const int R = slot_R[tid];
+		const int x = slot_x[sl];
+		const int c = slot_c[sl];
+		const int R = slot_R[sl];
 		if (x >= 0) {
-			SgCol A = {stage + tid};
+			SgCol A = {stage + sl};
 			uint16_t value = 0;
 			int cls = SG_CLS_OK;
 			if (p.method == 2) {	/* stack_median: implicit double -> WORD truncation */
@@ -734,9 +803,13 @@ k_stack_sorted(SgStackParams p, const unsigned int *__restrict__ list, const uns
 						cls = SG_CLS_OK;
 					}
 					break;
+				case 5:
+					cls = reject_linearfit(stage + sl, (uint32_t *)(stage + (size_t)N * SG_STAGE_STRIDE) + sl, N,
+							p.sig0, p.sig1, st);
+					break;
 				case 0:
 					break;
-				default:	/* LINEARFIT: literal path */
+				default:	/* SIGMEDIAN past its groups etc. never come here: unknown codes go literal */
 					cls = SG_CLS_LITERAL;
 				}
 				if (cls == SG_CLS_OK) {
@@ -760,7 +833,7 @@ k_stack_sorted(SgStackParams p, const unsigned int *__restrict__ list, const uns
 		if (p.method != 2) {
 			if (LISTED) {
 				if (my_rlo | my_rhi) {
-					unsigned long long *sh = p.rej + ((size_t)(tid % SG_REJ_SHARDS) * 6 + c * 2);
+					unsigned long long *sh = p.rej + ((size_t)(sl % SG_REJ_SHARDS) * 6 + c * 2);
 					atomicAdd(sh, (unsigned long long)my_rlo);
 					atomicAdd(sh + 1, (unsigned long long)my_rhi);
 				}

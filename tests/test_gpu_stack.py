@@ -69,6 +69,24 @@ def test_sigmedian_sorted_path(gpu_ctx, N, sig):
         assert gpu_ctx.stats().slow_pixels <= 0.02 * H * W, gpu_ctx.stats().slow_pixels
 
 
+@pytest.mark.parametrize("N", [5, 9, 16, 64, 200])
+@pytest.mark.parametrize("sig", [(5.0, 5.0), (2.0, 2.0), (1.0, 3.0)])
+def test_linearfit_sorted_path(gpu_ctx, N, sig):
+    """LINEARFIT on the sorted kernel (the literal double recurrences on the lane's sorted LDS
+    column, rejected[] bits with the early break's stale entries, in-place removal): image and
+    counters equal the oracle; first-pass early breaks go to the literal kernel"""
+    H, W = 20, 130
+    frames = _outlier_frames(N, H, W, 800 + N)
+    sx, sy = orc.synth_shifts(N, seed=800 + N, maxshift=3)
+    rc, ref, rej_ref = orc.stack_rejection(frames, sg.LINEARFIT, sig=sig, shiftx=sx, shifty=sy, max_thread=2)
+    assert rc == 0
+    out, rej, _ = gpu_stack(gpu_ctx, frames, sg.MEAN, sg.LINEARFIT, sig, sx, sy, max_thread=2)
+    assert_same(out, ref, f"linearfit N={N} sig={sig}")
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+    if sig == (5.0, 5.0) and N >= 64:
+        assert gpu_ctx.stats().slow_pixels <= 0.05 * H * W, gpu_ctx.stats().slow_pixels
+
+
 def test_sigmedian_never_ending_loop_fails(gpu_ctx):
     """the reference's SIGMEDIAN loop has no cap: {990, 0, 0, 1049} with sig = (2.5, 0.7) halves
     its top pair towards {0, 0, 1, 1}, where both 1s are clipped and replaced by
