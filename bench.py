@@ -69,9 +69,63 @@ def parse():
                     help="register-mean / winsorized-rgb: side of the registration selection (default 2048; "
                          "e.g. 4000 = configs[4]'s full height, a non-power-of-two side)")
     ap.add_argument("--cpu-rows", type=int, default=1024, help="rows of the CPU baseline sample")
-    ap.add_argument("--cpu-threads", type=int, default=16,
-                    help="OpenMP threads of the CPU baseline (the GPU box's CPU share is 16)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="OpenMP threads of the CPU baseline (default: the CPUs this process may run on, "
+                         "sched_getaffinity, capped by the cgroup's cpu.max quota)")
     return ap.parse_args()
+
+
+def cpu_share():
+    """the CPUs this process may use: its affinity mask, capped by the cgroup v2 cpu.max quota (CPUs'
+    worth of time per period) when one is set and by OMP_NUM_THREADS when the host sets one (the
+    GPU box exports its per-GPU CPU share there); the CPU baseline runs that many OpenMP threads,
+    as the reference's team is com.max_thread = omp_get_num_procs() (src/main.c:375)"""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    raw = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            raw = f.read().strip()
+        q, per = raw.split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    use = aff if quota is None else max(1, min(aff, int(quota)))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        use = min(use, int(omp))
+    return {"affinity_cpus": aff, "cgroup_cpu_max": raw, "cgroup_quota_cpus": quota, "omp_num_threads": omp,
+            "os_cpu_count": os.cpu_count(), "threads": use}
+
+
+def cpu_threads(args):
+    return args.cpu_threads if args.cpu_threads > 0 else cpu_share()["threads"]
+
+
+def self_launch(args):
+    """--gpus N > 1 without a launcher: start N ranks as fresh child processes (torch.distributed.run,
+    one process per GPU, rendezvous on 127.0.0.1) before anything here touches a GPU, and exit with
+    their return code.  Under a launcher, WORLD_SIZE must equal --gpus."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            print(f"bench.py: WORLD_SIZE={ws} but --gpus {args.gpus}", file=sys.stderr, flush=True)
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
 
 
 def _mix64(z):
@@ -122,7 +176,7 @@ def cpu_baseline(args, N, W, median=False):
     same workload"""
     import oracle_lib as orc
     rows = min(args.cpu_rows, args.height)
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    threads = cpu_threads(args)
     orc.load()
     _omp_threads(threads)
     frames = orc.synth(N, 1, rows, W, seed=0x5151, maxshift=16)
@@ -141,7 +195,7 @@ def cpu_baseline(args, N, W, median=False):
     del frames
     frac = rows / args.height
     return {"value": round(N * frac / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(),
+            "cpu_model": cpu_model(), "cpu_share": cpu_share(),
             "sample": f"oracle {what}, {N} frames x {rows} rows x {W} cols ({threads} OpenMP threads), "
                       f"timed on {rows} of {args.height} rows; frames/s = {N} x {rows}/{args.height} / seconds",
             "seconds": round(dt, 3), "rc": rc}
@@ -149,13 +203,13 @@ def cpu_baseline(args, N, W, median=False):
 
 def cpu_baseline_config(args, workload, N, C, H, W, S, layer):
     """configs[1] / configs[4]: the oracle's register_shift_dft over 32 frames with the reference's
-    OpenMP loop over frames (registration.c:276-279) on 16 threads, timed, and its stacker
-    (NO_REJEC mean / WINSORIZED, 16 threads) on a row sample; the step estimate is
+    OpenMP loop over frames (registration.c:276-279) on the process's CPU share (cpu_share), timed,
+    and its stacker (NO_REJEC mean / WINSORIZED, same threads) on a row sample; the step estimate is
     N x (registration seconds per frame) + t_stack scaled to the full image.  The oracle's FFT is
     a plain radix-2 complex-double transform, not FFTW (FFTW_ESTIMATE plans are several times
     faster per transform), which the sample text states"""
     import oracle_lib as orc
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    threads = cpu_threads(args)
     orc.load()
     _omp_threads(threads)
     nreg = 33
@@ -175,7 +229,7 @@ def cpu_baseline_config(args, workload, N, C, H, W, S, layer):
     del frames
     step = N * t_reg + t_stack
     return {"value": round(N / step, 3), "unit": "frames/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(),
+            "cpu_model": cpu_model(), "cpu_share": cpu_share(),
             "sample": f"oracle register_shift_dft on {nreg - 1} frames of {S}^2 + the reference, {threads} OpenMP "
                       f"threads over frames as :276-279 (measured {t_reg * 1e3:.1f} ms per frame; its FFT is a plain "
                       f"radix-2 complex-double transform, not FFTW) + oracle "
@@ -702,6 +756,13 @@ def main_register_file(args):
 
 def main():
     args = parse()
+    rc = self_launch(args)
+    if rc is not None:
+        sys.exit(rc)
+    if os.environ.get("SG_BENCH_LAUNCH_PROBE") == "1":     # tests: report the rank layout, touch no GPU
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": int(os.environ.get("WORLD_SIZE", "1")),
+                          "gpus": args.gpus}), flush=True)
+        return
     if args.workload in ("sigma", "median"):
         return main_sigma(args)
     if args.workload == "sum-fits":

@@ -18,6 +18,9 @@
 #define _(s) (s)
 #endif
 
+/* register_shift_dft: frames per batch handed to the library (two batches held on the host) */
+#define REG_BATCH_MAX 256
+
 /* one context for the process (in Siril: created in initialize_stacking_methods()), driving
  * every visible GPU: sg_stack_u16 gives each device a share of the output rows and its own
  * host thread (the reference's OpenMP team over row blocks, stacking.c:1513-1516) */
@@ -282,11 +285,45 @@ int stack_addmin(struct stacking_args *args) {
  * (seq_read_frame_part of args->layer, :236-244, :301-306), the DFT + arg-max + quality on the
  * GPU, regdata written for the reference frame and every processed frame (others keep what
  * they had: zero for a new array, :210-220), quality normalised over the processed frames.
+ *
+ * The selections go to the library in batches as they are read: batch k is registered by a
+ * worker thread (sg_register_dft_u16_raw on [reference, batch k]) while this thread reads batch
+ * k + 1, as the reference's OpenMP loop transforms one frame while its team reads others
+ * (:276-351).  Host memory holds two batches, not the whole sequence.
  */
+#include <pthread.h>
+
+struct reg_batch {
+	sg_ctx *ctx;
+	uint16_t *sel;		/* [1 + n][S][S]: the reference selection, then the batch's frames */
+	int n, S;
+	int idx[REG_BATCH_MAX];	/* sequence index of batch frame j (slot j + 1) */
+	int bx[REG_BATCH_MAX + 1], by[REG_BATCH_MAX + 1];
+	double bq[REG_BATCH_MAX + 1];
+	int rc;
+};
+
+static void *reg_batch_run(void *u) {
+	struct reg_batch *b = (struct reg_batch *)u;
+	b->rc = sg_register_dft_u16_raw(b->ctx, b->sel, 1 + b->n, b->S, 0, NULL, b->bx, b->by, b->bq);
+	return NULL;
+}
+
+/* batch k's results into the per-frame arrays (and the reference's raw quality) */
+static void reg_batch_collect(const struct reg_batch *b, int ref, int *sx, int *sy, double *q) {
+	q[ref] = b->bq[0];
+	for (int j = 0; j < b->n; j++) {
+		sx[b->idx[j]] = b->bx[j + 1];
+		sy[b->idx[j]] = b->by[j + 1];
+		q[b->idx[j]] = b->bq[j + 1];
+	}
+}
+
 int register_shift_dft(struct registration_args *args) {
 	sequence *seq = args->seq;
 	const int n = seq->number, S = args->selection.w;
-	int f, rc, cancelled = 0, best_frame = -1;
+	const size_t plane = (size_t)S * S;
+	int f, rc = 0, cancelled = 0, best_frame = -1, cur = 0, inflight = -1, sent = 0;
 	sg_ctx *ctx = siril_gpu_context();
 	if (!ctx || args->selection.w != args->selection.h)
 		return -1;
@@ -295,50 +332,120 @@ int register_shift_dft(struct registration_args *args) {
 		return -1;
 	}
 	const int ref = seq->reference_image == -1 ? 0 : seq->reference_image;
-	uint16_t *sel = malloc((size_t)n * S * S * sizeof(uint16_t));
+	/* frames per batch: a few pair launches per device of the context */
+	int ndev = 1;
+	(void)sg_device_count(ctx, &ndev);
+	int per = 16 * (ndev > 0 ? ndev : 1);
+	if (per < 64)
+		per = 64;
+	if (per > REG_BATCH_MAX)
+		per = REG_BATCH_MAX;
+	struct reg_batch *bt = calloc(2, sizeof(struct reg_batch));
 	int *inc = malloc(n * sizeof(int)), *sx = calloc(n, sizeof(int)), *sy = calloc(n, sizeof(int));
 	double *q = calloc(n, sizeof(double));
-	if (!sel || !inc || !sx || !sy || !q) {
+	pthread_t worker;
+	if (!bt || !inc || !sx || !sy || !q) {
 		rc = -2;
 		goto end;
 	}
-	/* the reference frame first (:236-244), then the frames in index order: with run_in_thread
-	 * the loop polls get_thread_run() before each frame and, when it turns false, registers no
-	 * further frame (:281-285).  The reference then still returns 0, keeps what it registered
-	 * (abort does not set ret) and normalizeQualityData stops at once on the same poll
-	 * (:166-168), leaving the qualities raw.  This is the outcome of the reference's OpenMP
+	for (int k = 0; k < 2; k++) {
+		bt[k].ctx = ctx;
+		bt[k].S = S;
+		bt[k].sel = malloc((1 + (size_t)per) * plane * sizeof(uint16_t));
+		if (!bt[k].sel) {
+			rc = -2;
+			goto end;
+		}
+	}
+	/* the reference frame first (:236-244); its selection leads every batch */
+	{
+		fits fit;
+		memset(&fit, 0, sizeof fit);
+		if (seq_read_frame_part(seq, args->layer, ref, &fit, &args->selection, FALSE)) {
+			siril_log_message(_("Could not load partial image %d\n"), ref);
+			clearfits(&fit);
+			rc = 1;	/* :238-244 returns its status */
+			goto end;
+		}
+		memcpy(bt[0].sel, fit.data, plane * sizeof(WORD));
+		memcpy(bt[1].sel, fit.data, plane * sizeof(WORD));
+		clearfits(&fit);
+	}
+	/* then the frames in index order: with run_in_thread the loop polls get_thread_run() for
+	 * every frame index, before its reference / inclusion checks, and once it turns false
+	 * registers no further frame (:280-290).  The reference then still returns 0, keeps what it
+	 * registered (abort does not set ret) and normalizeQualityData stops at once on the same
+	 * poll (:166-168), leaving the qualities raw.  This is the outcome of the reference's OpenMP
 	 * loop run by one thread. */
 	for (f = 0; f < n; f++)
 		inc[f] = args->process_all_frames || seq->imgparam[f].incl;
-	for (f = -1; f < n; f++) {
-		const int idx = f < 0 ? ref : f;
-		if (f >= 0) {
-			if (f == ref || !inc[f])
-				continue;
+	for (f = 0; f <= n; f++) {
+		if (f < n) {
 			if (!cancelled && args->run_in_thread && !get_thread_run())
 				cancelled = 1;
+			if (f == ref || !inc[f])
+				continue;
 			if (cancelled) {
 				inc[f] = 0;	/* not registered: keeps its regdata */
 				continue;
 			}
-		}
-		fits fit;
-		memset(&fit, 0, sizeof fit);
-		if (seq_read_frame_part(seq, args->layer, idx, &fit, &args->selection, FALSE)) {
-			siril_log_message(_("Could not load partial image %d\n"), idx);
+			fits fit;
+			memset(&fit, 0, sizeof fit);
+			if (seq_read_frame_part(seq, args->layer, f, &fit, &args->selection, FALSE)) {
+				siril_log_message(_("Could not load partial image %d\n"), f);
+				clearfits(&fit);
+				rc = 1;	/* :373-381 */
+				break;
+			}
+			struct reg_batch *b = &bt[cur];
+			memcpy(b->sel + (1 + (size_t)b->n) * plane, fit.data, plane * sizeof(WORD));
 			clearfits(&fit);
-			rc = 1;	/* :373-381 (the reference frame: :238-244 returns its status) */
-			goto end;
+			b->idx[b->n++] = f;
+			if (b->n < per)
+				continue;
+		} else if (bt[cur].n == 0 && sent) {
+			break;	/* nothing left to send */
 		}
-		memcpy(sel + (size_t)idx * S * S, fit.data, (size_t)S * S * sizeof(WORD));
-		clearfits(&fit);
+		/* hand batch `cur` over: wait for the one in flight, collect it, start this one */
+		if (inflight >= 0) {
+			pthread_join(worker, NULL);
+			if (bt[inflight].rc) {
+				rc = bt[inflight].rc;
+				siril_log_message("%s\n", sg_last_error(ctx));
+				inflight = -1;
+				break;
+			}
+			reg_batch_collect(&bt[inflight], ref, sx, sy, q);
+			bt[inflight].n = 0;
+			inflight = -1;
+		}
+		if (pthread_create(&worker, NULL, reg_batch_run, &bt[cur])) {
+			reg_batch_run(&bt[cur]);	/* no thread: register it here */
+			if (bt[cur].rc) {
+				rc = bt[cur].rc;
+				siril_log_message("%s\n", sg_last_error(ctx));
+				break;
+			}
+			reg_batch_collect(&bt[cur], ref, sx, sy, q);
+			bt[cur].n = 0;
+		} else {
+			inflight = cur;
+			cur ^= 1;
+		}
+		sent = 1;
 	}
-	/* shifts and RAW qualities from the GPU (every device of the context shares the frames) */
-	rc = sg_register_dft_u16_raw(ctx, sel, n, S, ref, inc, sx, sy, q);
-	if (rc) {
-		siril_log_message("%s\n", sg_last_error(ctx));
+	if (inflight >= 0) {
+		pthread_join(worker, NULL);
+		if (bt[inflight].rc) {
+			siril_log_message("%s\n", sg_last_error(ctx));
+			if (!rc)
+				rc = bt[inflight].rc;
+		} else if (!rc) {
+			reg_batch_collect(&bt[inflight], ref, sx, sy, q);
+		}
+	}
+	if (rc)
 		goto end;
-	}
 	{
 		regdata *rd = seq->regparam[args->layer] ? seq->regparam[args->layer] : calloc(n, sizeof(regdata));
 		if (!rd) {
@@ -377,7 +484,11 @@ int register_shift_dft(struct registration_args *args) {
 	siril_log_message(_("Registration finished.\n"));
 	siril_log_message(_("Best frame: #%d.\n"), best_frame);	/* :397 (siril_log_color_message, bold) */
 end:
-	free(sel);
+	if (bt) {
+		free(bt[0].sel);
+		free(bt[1].sel);
+	}
+	free(bt);
 	free(inc);
 	free(sx);
 	free(sy);

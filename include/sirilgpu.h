@@ -165,6 +165,9 @@ typedef struct {
 					 * histogram kernel wrote out (no gather in the sorted kernel) */
 } sg_stack_stats;
 int sg_get_last_stats(const sg_ctx *ctx, sg_stack_stats *st);
+/* device slots of the context (sg_init's ndev): callers size their batches by it, as the
+ * reference sizes its work by com.max_thread (src/core/siril.h:596) */
+int sg_device_count(const sg_ctx *ctx, int *ndev);
 
 /*
  * Per-frame normalisation statistics: location / scale of layer 0 as

@@ -166,6 +166,13 @@ extern "C" int sg_get_last_stats(const sg_ctx *ctx, sg_stack_stats *st) {
 	return SG_OK;
 }
 
+extern "C" int sg_device_count(const sg_ctx *ctx, int *ndev) {
+	if (!ctx || !ndev)
+		return SG_ERR_GENERIC;
+	*ndev = (int)ctx->dev.size();
+	return SG_OK;
+}
+
 /* ---- reference block partition (src/stacking/stacking.c:1397-1476) and the libgomp
  *      schedule(static) assignment of blocks to OpenMP threads (:1513-1516) ---- */
 struct Block {
@@ -268,6 +275,16 @@ static hipError_t launch_sorted(int nreg, bool listed, dim3 grid, size_t lds, hi
 #undef SG_CASE
 	}
 	return hipErrorInvalidValue;
+}
+
+/* k_stack_literal: one thread per queued pixel with N * 5 bytes of scratch each; SG_LIT_THREADS
+ * threads up to 2048 frames, then as many as 1 GiB of scratch holds (at least 4096) */
+static unsigned lit_thread_count(int N) {
+	const size_t lit_bytes = ((size_t)N * 5 + 15) & ~(size_t)15;
+	return (unsigned)std::max<size_t>(4096, std::min<size_t>(SG_LIT_THREADS, ((size_t)1 << 30) / lit_bytes) & ~(size_t)63);
+}
+static size_t lit_scratch_bytes(int N) {
+	return (size_t)lit_thread_count(N) * (((size_t)N * 5 + 15) & ~(size_t)15);
 }
 
 /* SUM over row bands streamed by the host-pull path: the raw sums and the maximum carry
@@ -713,7 +730,11 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			const bool sorted_redo = nreg && (d->method == SG_STACK_MEDIAN || p.rejection == SG_PERCENTILE);
 			const bool dev_route = (N <= SG_REPLAY_MAXN && ctx->knobs.redo_replay) || !nreg;
 			if (sorted_redo) {
-				HIPCHK(launch_sorted(nreg, true, dim3(SG_REDO_REPLAY_MAX / SG_TILE_W), lds, s, p, redo_list, redo_count));
+				/* the grid covers SG_REDO_REPLAY_MAX slots: a longer list makes this launch idle and
+				 * the late launch below takes the whole list (each pixel's counters added once) */
+				SgStackParams q = p;
+				q.list_maxn = SG_REDO_REPLAY_MAX;
+				HIPCHK(launch_sorted(nreg, true, dim3(SG_REDO_REPLAY_MAX / SG_TILE_W), lds, s, q, redo_list, redo_count));
 				st.launches++;
 				late_redo = redo_count;
 				late_list = redo_list;
@@ -748,10 +769,8 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		 * phases, grids read the count on the device */
 		/* literal kernel: one thread per queued pixel with N * 5 bytes of scratch each; 65536
 		 * threads up to 2048 frames, then as many as 1 GiB of scratch holds */
-		const size_t lit_bytes = ((size_t)N * 5 + 15) & ~(size_t)15;
-		const unsigned lit_threads = (unsigned)std::max<size_t>(4096,
-				std::min<size_t>(SG_LIT_THREADS, ((size_t)1 << 30) / lit_bytes) & ~(size_t)63);
-		HIPCHK(ensure(dv.scratch, (size_t)lit_threads * lit_bytes));
+		const unsigned lit_threads = lit_thread_count(N);
+		HIPCHK(ensure(dv.scratch, lit_scratch_bytes(N)));
 		auto launch_tail = [&]() -> int {
 			if (d->method == SG_STACK_MEAN && (p.rejection == SG_SIGMA || p.rejection == SG_WINSORIZED) &&
 					N <= SG_REPLAY_MAXN) {
@@ -890,8 +909,7 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
  * kernel's scratch, the readers' staging and the small tables */
 static size_t fixed_device_bytes(int N, int W, int H, int C) {
 	const size_t npix = (size_t)C * H * W;
-	const size_t lit = (size_t)SG_LIT_THREADS * (((size_t)N * 5 + 15) & ~(size_t)15);
-	return npix * 15 + std::min(lit, ((size_t)1 << 30) + ((size_t)1 << 20)) + ((size_t)4 << 20) +
+	return npix * 15 + lit_scratch_bytes(N) + ((size_t)4 << 20) +
 		(size_t)SG_PULL_READERS * 2 * SG_PULL_CHUNK_BYTES;
 }
 

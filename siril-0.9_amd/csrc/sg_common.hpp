@@ -18,7 +18,8 @@
 #define SG_DBG(p) (SG_DBG_MODES ? (p).dbg : 0)
 
 enum { SG_CLS_OK = 0, SG_CLS_LITERAL = 1, SG_CLS_CHAIN = 2, SG_CLS_DONE = 3,
-	SG_CLS_NOTERM = 4 /* SIGMEDIAN whose reference loop never ends (p.loop_fault; the call fails) */ };
+	SG_CLS_NOTERM = 4 /* SIGMEDIAN whose reference loop never ends (p.loop_fault; the call fails) */,
+	SG_CLS_CHAIN_DONE = 5 /* a CHAIN pixel k_stack_literal's phase 2 finished (still a chain link for walks) */ };
 /* k_stack_replay: waves per block (one pixel per wave, ~18 KB of LDS each), max frames */
 #define SG_REPLAY_WAVES 2
 #define SG_REPLAY_MAXN 2048
@@ -69,6 +70,8 @@ struct SgStackParams {
 	unsigned int *cmp_list, *cmp_count;
 	unsigned int cmp_cap;
 	const uint16_t *cmp_src;		/* k_stack_sorted<., true>: stage the listed columns from here (sorted) */
+	unsigned int list_maxn;			/* k_stack_sorted<., true> on the redo list: do nothing when the device count
+						 * exceeds this (0: no limit); the host then relaunches over the whole list */
 	uint32_t *sum_buf;			/* SUM: raw sums [C][H][W] */
 	unsigned int *maxim;			/* SUM: global max of sums */
 };

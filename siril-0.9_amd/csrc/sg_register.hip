@@ -2116,10 +2116,24 @@ static int reg_host(sg_ctx *ctx, const uint16_t *sel, int nframes, int S, int re
 		}
 	};
 	{
+		/* a thread that cannot start fails its slot (and the call) instead of escaping the C ABI;
+		 * the threads that did start are always joined */
 		std::vector<std::thread> th;
-		for (int g = 1; g < G; g++)
-			th.emplace_back(run, g);
-		run(0);
+		bool started = true;
+		for (int g = 1; g < G; g++) {
+			try {
+				th.emplace_back(run, g);
+			} catch (...) {
+				for (int h = g; h < G; h++)
+					rcs[(size_t)h] = set_err(ctx, SG_ERR_GENERIC, "could not start the thread of device slot%s %ld", "", h);
+				started = false;
+				break;
+			}
+		}
+		if (started)
+			run(0);
+		else
+			rcs[0] = SG_ERR_GENERIC;
 		for (std::thread &t : th)
 			t.join();
 	}

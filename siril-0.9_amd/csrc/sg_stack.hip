@@ -656,6 +656,8 @@ k_stack_sorted(SgStackParams p, const unsigned int *__restrict__ list, const uns
 		unsigned int count = *list_count;
 		if (p.cmp_src && count > p.cmp_cap)	/* the compact list: slots past the capacity went to the redo list */
 			count = p.cmp_cap;
+		if (!p.cmp_src && p.list_maxn && count > p.list_maxn)
+			return;	/* a longer list than this launch's grid: the host's late launch takes all of it */
 		if ((unsigned int)blockIdx.x * SG_TILE_W >= count)
 			return;
 		if (tid < SG_TILE_W) {
@@ -2321,6 +2323,7 @@ k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *s
 			gather_stack(p, pix, stack);
 			shellsort_u16(stack, p.N);
 			p.out[pix] = (uint16_t)lit_median(stack, p.N);
+			p.flag_map[pix] = SG_CLS_DONE;
 			continue;
 		}
 		if (phase == 1) {
@@ -2332,7 +2335,7 @@ k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *s
 			bool fault = false;
 			while (q >= 0) {
 				if (chain_in_band(p, q)) {
-					if (p.flag_map[q] != SG_CLS_CHAIN)
+					if (p.flag_map[q] != SG_CLS_CHAIN && p.flag_map[q] != SG_CLS_CHAIN_DONE)
 						break;
 				} else {
 					if (!chain_resident(p, q)) {
@@ -2386,6 +2389,9 @@ k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *s
 			continue;
 		}
 		p.out[pix] = v;
+		/* finished: a second tail launch (after the host's late redo launch) skips it; a phase-2
+		 * pixel stays a chain link for the other walks of this phase */
+		p.flag_map[pix] = phase == 1 ? SG_CLS_DONE : SG_CLS_CHAIN_DONE;
 		const int c = (int)(pix / ((int64_t)p.W * p.H));
 		unsigned long long *sh = p.rej + ((size_t)(i % SG_REJ_SHARDS) * 6 + c * 2);
 		if (crej[0])

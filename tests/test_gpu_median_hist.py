@@ -121,6 +121,33 @@ def test_more_than_1024_frames(gpu_ctx, method, rejection):
     assert np.array_equal(rej, rej_ref), (rej, rej_ref)
 
 
+@pytest.mark.parametrize("normalize", [sg.NO_NORM, sg.ADDITIVE_SCALING])
+def test_percentile_long_redo_list_counted_once(gpu_ctx, normalize):
+    """more redo pixels than the sorted kernel's early grid (SG_REDO_REPLAY_MAX = 32768): every
+    pixel holds 300 equal samples (u8 bin overflow) plus low / high outliers outside the band, so
+    all 40 k pixels are redone; the early listed launch must stay idle and the late one count each
+    pixel's rejections once (the counters were added twice)"""
+    N, C, H, W = 400, 1, 160, 256
+    rng = np.random.default_rng(41)
+    frames = np.full((N, C, H, W), 1000, np.uint16)
+    frames[300:350] = rng.integers(500, 700, size=(50, C, H, W))      # low-rejected (p < 0.8 median)
+    frames[350:] = rng.integers(1300, 1500, size=(50, C, H, W))       # high-rejected (p > 1.1 median)
+    frames = frames[rng.permutation(N)]
+    sig = (0.2, 0.1)
+    off = mul = sc = None
+    if normalize != sg.NO_NORM:
+        off, mul, sc = _coeffs(normalize, N, seed=41)
+    rc, ref, rej_ref = orc.stack_rejection(frames, sg.PERCENTILE, sig=sig, normalize=normalize, offset=off, mul=mul,
+                                           scale=sc, max_thread=2)
+    assert rc == 0
+    out, rej, _ = gpu_stack(gpu_ctx, frames, sg.MEAN, sg.PERCENTILE, sig, normalize=normalize, offset=off, mul=mul,
+                            scale=sc, max_thread=2)
+    st = gpu_ctx.stats()
+    assert st.path == 1 and st.chain_pixels > 32768, st.chain_pixels
+    assert_same(out, ref, f"percentile long redo norm={normalize}")
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+
+
 def test_more_than_1024_frames_sorted_only_rejection_refused(gpu_ctx):
     """SIGMEDIAN / LINEARFIT have no histogram path: beyond 1024 frames the call fails loudly"""
     N, C, H, W = 1100, 1, 2, 64

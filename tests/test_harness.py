@@ -260,7 +260,8 @@ def test_multi_device_slots_from_c(tmp_path, capfd, devs):
 @pytest.mark.parametrize("devs", [None, [0, 0]])
 def test_register_cancel_from_c(tmp_path, devs):
     """register_shift_dft with run_in_thread and get_thread_run() turning false after 3 polls:
-    the reference registers the frames polled before that (:281-285), still returns 0, keeps
+    the reference polls every frame index before its reference / inclusion checks (:280-290),
+    registers the frames polled before the failing poll, still returns 0, keeps
     the rest's regdata and skips normalizeQualityData (:166-168), so the registered frames keep
     RAW qualities; the best frame is logged"""
     lib = hl.load()
@@ -270,7 +271,7 @@ def test_register_cancel_from_c(tmp_path, devs):
     m0 = H - y - S
     sel = frames[:, 0, m0:m0 + S, x:x + S]
     ref = 2
-    done = [0, 1, 3]                       # the first three frames polled (ref skipped, not polled)
+    done = [0, 1]                          # polls 1, 2 (frames 0, 1), 3 (frame 2 = ref, skipped); frame 3's fails
     inc = np.zeros(N, np.int32)
     inc[done] = 1
     rx, ry, _ = orc.register_dft(sel, ref_image=ref, included=inc)
