@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--normalize", choices=["none", "additive-scaling", "multiplicative-scaling"], default="none",
                     help="sigma workload: per-frame normalisation (synthetic location / scale, as "
                          "compute_normalization derives them)")
+    ap.add_argument("--band-of", type=int, default=0,
+                    help="A/B at 1 GPU: stack only band 0 of the configs[3] job split into this many row bands "
+                         "(one rank's call of the strong form), only that band's rows resident")
     ap.add_argument("--maxshift", type=int, default=16, help="synthetic registration shift range")
     ap.add_argument("--even-shifts", action="store_true",
                     help="A/B only: round x shifts down to even (4-byte aligned pixel-pair loads)")
@@ -322,11 +325,13 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def timed(steps, warmup, step, D):
+def timed(steps, warmup, step, D, after_warmup=None):
     import torch
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
+    if after_warmup:
+        after_warmup()
     D.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -357,13 +362,15 @@ def main_sigma(args):
     # strong: one sequence of N frames of H x W in `world` row bands; weak: one sequence of
     # N frames of (H*world) x W, a full H-row band per rank.  Each rank holds only the frame
     # rows its band reads (band + shift halo), addressed through a biased base pointer.
+    # --band-of K at 1 GPU: rank 0's band of the strong form at K ranks, alone
+    nb = world if world > 1 else max(1, args.band_of)
     Htot = H if strong else H * world
     shx, shy = synth_shifts_np(N, 0x5151, args.maxshift)
     if args.even_shifts:
         shx &= ~1
     if args.zero_shift:
         (shx if args.zero_shift == "x" else shy)[:] = 0
-    b, e = sd.row_band(rank, world, H) if strong else (rank * H, (rank + 1) * H)
+    b, e = sd.row_band(rank, nb, H) if strong else (rank * H, (rank + 1) * H)
     if median:      # stack_median ignores the registration shifts (:703-722): the band's own rows
         lo, hi = b, e - 1
     else:
@@ -373,7 +380,7 @@ def main_sigma(args):
     frames = torch.empty(N * fstride, dtype=torch.int16, device="cuda")
     base = frames.data_ptr() - lo * W * 2
     ctx.synth_fill(base, N, 1, Htot, W, lo, hi + 1, 0x5151, args.maxshift, frame_stride=fstride)
-    hband = -(-H // world) if strong else H
+    hband = -(-H // nb) if strong else H
     band_out = torch.zeros(hband * W, dtype=torch.int16, device="cuda")
     out_base = band_out.data_ptr() - b * W * 2          # the library writes rows [b, e) of the image
     gathered = None
@@ -398,31 +405,46 @@ def main_sigma(args):
                               max_thread=8, max_number_of_rows=Htot, resident_rows=(lo, hi + 1))
     torch.cuda.synchronize()
     kms = []
-    state = {}
+    stream = torch.cuda.current_stream().cuda_stream
 
+    # one step = one whole stack of the band, queued with sg_stack_u16_device_async on torch's
+    # stream (every launch decided on the device, the counters read back into a pinned slot):
+    # the host prepares the next step while the device runs this one; the strong form gathers the
+    # output bands to rank 0 behind it on the same stream (RCCL over xGMI)
     def step():
-        rej, _ = ctx.stack_device(desc, base, fstride, nres * W, out_base, b, e)
-        kms.append(ctx.stats().kernel_ms)
-        state["rej"] = rej
+        ctx.stack_device_async(desc, base, fstride, nres * W, out_base, b, e, stream=stream)
+        kms.append(ctx.stats().kernel_ms)       # the last folded call's (at most two calls behind)
         if strong and world > 1:
-            D.gather_to_root(band_out, gathered)        # output bands -> rank 0 (RCCL over xGMI)
-            state["rej_t"] = D.sum_counters(rej)        # rejection counters, :1796-1817
+            D.gather_to_root(band_out, gathered)
 
-    elapsed = timed(args.steps, args.warmup, step, D)
+    def reset_counters():
+        rc, _, _ = ctx.collect()
+        assert rc == 0, ctx.error()
+
+    elapsed = timed(args.steps, args.warmup, step, D, after_warmup=reset_counters)
+    rc, rej_steps, _ = ctx.collect()            # every timed step's counters, summed
+    assert rc == 0, ctx.error()
     st = ctx.stats()
-    kms = kms[args.warmup:]
+    kms.append(st.kernel_ms)
+    kms = kms[args.warmup + 1:]
     kavg = sum(kms) / len(kms)
     per_rank_kms = D.all_floats(kavg)
-    rej_tot = state["rej"]
+    assert not (rej_steps % args.steps).any(), "the steps' rejection counters differ"
+    rej_tot = rej_steps // args.steps           # one step's (every step stacks the same band)
     if world > 1:
-        rej_tot = (state["rej_t"].cpu().numpy() if strong else sd.sum_counters(rej_tot, D.dist, device=D.cdev))
+        rej_tot = sd.sum_counters(rej_tot, D.dist, device=D.cdev)   # rejection counters, :1796-1817
     ms_step = elapsed / args.steps * 1e3
     frames_per_s = N * (1 if strong else world) / (elapsed / args.steps)
     algo_bytes = N * (e - b) * W * 2 + (e - b) * W * 2     # this rank's launch: its band's samples + output
     achieved = algo_bytes / (kavg * 1e-3) / 1e9
     if rank == 0:
         kind = "median stack" if median else f"{args.rejection} rejection stack"
-        if world == 1:
+        if world == 1 and nb > 1:
+            workload = (f"A/B: band 0 ({e - b} rows) of the {kind} {N}x{H}x{W} u16 mono split into {nb} row bands "
+                        f"(one rank's call of BASELINE configs[3] at {nb} GPUs), only its rows resident; "
+                        f"value = frames/s of this band's work")
+            par = f"1 GPU, one of {nb} row bands"
+        elif world == 1:
             workload = (f"{kind} {N}x{H}x{W} u16 mono (BASELINE configs[2] frames)" if median or args.rejection != "sigma"
                         else f"sigma-clip stack {N}x{H}x{W} u16 mono (BASELINE configs[2])")
             par = "1 GPU"
@@ -451,7 +473,7 @@ def main_sigma(args):
                        "sig": list(sig), "normalize": args.normalize, "parallelism": par},
             "roofline": roofline(achieved, algo_bytes, N, H, W, ("median" if median else args.rejection)
                                  if args.normalize == "none" else f"{'median' if median else args.rejection}_{args.normalize}",
-                                 with_traffic=world == 1),
+                                 with_traffic=world == 1 and nb == 1),
             "kernel_ms": round(kavg, 3),
             "slow_pixels": int(st.slow_pixels),
             "redo_pixels": int(st.chain_pixels),
@@ -461,7 +483,7 @@ def main_sigma(args):
         if world > 1:
             res["per_rank_kernel_ms"] = [round(x, 3) for x in per_rank_kms]
             res["rows_per_rank"] = e - b
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and nb == 1:
             res["cpu_baseline"] = cpu_baseline(args, N, W, median)
         print(json.dumps(res), flush=True)
     ctx.close()

@@ -147,6 +147,21 @@ int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_desc *desc,
 		const uint16_t *d_frames, int64_t frame_stride, int64_t plane_stride,
 		uint16_t *d_out, int row_begin, int row_end, uint64_t rej[3][2], uint64_t *maxim,
 		void *stream);
+/*
+ * The same stack queued without waiting for it (replaces the same loop body as
+ * sg_stack_u16_device, for callers that keep several stacks in flight, e.g. a row band per call
+ * in a loop: the host prepares the next call while the device works).  Every launch decision is
+ * made on the device, so nothing here waits for the GPU except reusing a counter slot: at most
+ * two calls per device slot are pending, a third folds the oldest.  Successive async calls of a
+ * device slot must use one stream.  sg_stack_collect waits for every pending call of the slot
+ * and returns the SUM of their rejection counters, the maximum of their SUM maxima and the first
+ * error any of them met (SG_ERR_GENERIC for the refused regimes above); statistics then describe
+ * the last folded call.
+ */
+int sg_stack_u16_device_async(sg_ctx *ctx, int dev_index, const sg_stack_desc *desc,
+		const uint16_t *d_frames, int64_t frame_stride, int64_t plane_stride,
+		uint16_t *d_out, int row_begin, int row_end, void *stream);
+int sg_stack_collect(sg_ctx *ctx, int dev_index, uint64_t rej[3][2], uint64_t *maxim);
 
 /* Statistics of the last stack call on this context (for bench.py / rocprof cross-checks). */
 typedef struct {

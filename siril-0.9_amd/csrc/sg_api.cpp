@@ -88,6 +88,9 @@ extern "C" int sg_init(sg_ctx **out, int ndev, const int *devs) {
 		for (int k = 0; k < 4; k++)
 			(void)hipEventCreate(&d.ev[k]);
 		for (int k = 0; k < 2; k++)
+			for (int j = 0; j < 3; j++)
+				(void)hipEventCreate(&d.cev[k][j]);
+		for (int k = 0; k < 2; k++)
 			(void)hipEventCreateWithFlags(&d.io_ev[k], hipEventDisableTiming);
 		ctx->dev.push_back(d);
 	}
@@ -126,6 +129,10 @@ extern "C" void sg_shutdown(sg_ctx *ctx) {
 		for (int k = 0; k < 4; k++)
 			if (d.ev[k])
 				(void)hipEventDestroy(d.ev[k]);
+		for (int k = 0; k < 2; k++)
+			for (int j = 0; j < 3; j++)
+				if (d.cev[k][j])
+					(void)hipEventDestroy(d.cev[k][j]);
 		for (SgReader &rd : d.readers) {
 			if (rd.stream)
 				(void)hipStreamSynchronize(rd.stream);
@@ -291,9 +298,79 @@ static size_t lit_scratch_bytes(int N) {
  * across the band calls, the scaling runs once after the last band */
 enum { SUM_WHOLE = 0, SUM_FIRST_BAND = 1, SUM_MID_BAND = 2, SUM_LAST_BAND = 3 };
 
+/* counter block of one slot: rejection shards, then {flag count, walk fault, redo count, compact
+ * count, loop fault} and the SUM maximum 64 bytes further */
+static const size_t SG_CTRB = SG_CTR_REJB + 128;
+/* blocks of the listed k_stack_sorted launches (grid-stride over any list length) */
+#define SG_LIST_GRID 1024
+
+/*
+ * wait for the call queued in counter slot `slot` and take its results: faults, the rejection
+ * counters (rej, may be null), the SUM maximum, the call's statistics (published to the context)
+ */
+static int stack_fold(sg_ctx *ctx, SgDevice &dv, int slot, uint64_t rej[3][2], uint64_t *maxim_out, bool sync) {
+	HIPCHK(hipEventSynchronize(dv.cev[slot][2]));
+	dv.pend[slot] = false;
+	dv.stage_pending = false;	/* the input copy ran before this call's kernels */
+	const char *h = (const char *)dv.ctr_h + (size_t)slot * SG_CTRB;
+	const unsigned int *fl = (const unsigned int *)(h + SG_CTR_REJB);
+	sg_stack_stats &st = dv.pstats[slot];
+	float ms = 0.f, ms2 = 0.f;
+	HIPCHK(hipEventElapsedTime(&ms, dv.cev[slot][0], dv.cev[slot][1]));
+	HIPCHK(hipEventElapsedTime(&ms2, dv.cev[slot][0], dv.cev[slot][2]));
+	st.kernel_ms = ms;
+	st.total_ms = ms2;
+	st.slow_pixels = fl[0];
+	if (st.path == 1)
+		st.chain_pixels = fl[2];
+	st.compact_pixels = std::min<uint64_t>(fl[3], st.compact_pixels);	/* pstats holds the capacity */
+	if (sync) {	/* the calling stack_device_core publishes dv.stats when it returns */
+		dv.stats = st;
+	} else {
+		std::lock_guard<std::mutex> lk(ctx->mu);
+		ctx->stats = st;
+	}
+	if (fl[4])
+		return set_err(ctx, SG_ERR_GENERIC, "SIGMEDIAN: the reference's clipping loop never ends for some pixel "
+				"(a pass replaces samples by the values they already hold, stacking.c:1696-1709)%s%.0ld", "", 0);
+	if (fl[1])
+		return set_err(ctx, SG_ERR_WALK, "a first-pass early break needs the stale rejected[] of a pixel "
+				"whose frame rows are not resident; make the full frames resident%s%.0ld", "", 0);
+	if (rej) {
+		const unsigned long long *shards = (const unsigned long long *)h;
+		for (int c = 0; c < 3; c++)
+			rej[c][0] = rej[c][1] = 0;
+		for (int k = 0; k < SG_REJ_SHARDS; k++)
+			for (int c = 0; c < 3; c++) {
+				rej[c][0] += shards[(size_t)k * 6 + c * 2];
+				rej[c][1] += shards[(size_t)k * 6 + c * 2 + 1];
+			}
+	}
+	if (maxim_out)
+		*maxim_out = fl[16];
+	return SG_OK;
+}
+
+/* fold a pending async call into the device's accumulators (sg_stack_collect returns them) */
+static void stack_fold_acc(sg_ctx *ctx, SgDevice &dv, int slot) {
+	uint64_t r[3][2], mx = 0;
+	const int rc = stack_fold(ctx, dv, slot, r, &mx, false);
+	if (rc) {
+		if (!dv.acc_rc)
+			dv.acc_rc = rc == SG_ERR_WALK ? SG_ERR_GENERIC : rc;
+		return;
+	}
+	for (int c = 0; c < 3; c++) {
+		dv.acc_rej[c][0] += r[c][0];
+		dv.acc_rej[c][1] += r[c][1];
+	}
+	dv.acc_max = std::max<uint64_t>(dv.acc_max, mx);
+}
+
 static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		const uint16_t *d_frames, int64_t frame_stride, int64_t plane_stride, uint16_t *d_out,
-		int row_begin, int row_end, uint64_t rej[3][2], uint64_t *maxim_out, void *stream, int sum_mode) {
+		int row_begin, int row_end, uint64_t rej[3][2], uint64_t *maxim_out, void *stream, int sum_mode,
+		bool async = false) {
 	if (!ctx || !d || dev_index < 0 || dev_index >= (int)ctx->dev.size())
 		return SG_ERR_GENERIC;
 	SgDevice &dv = ctx->dev[dev_index];
@@ -531,26 +608,39 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		}
 		return SG_OK;
 	};
-	/* counters: rejection shards, then {flag count, walk fault, redo count} and the sum maximum
-	 * 64 bytes further (kept across the bands of a streamed SUM); one memset, one read-back */
-	const size_t REJB = SG_CTR_REJB, CTRB = REJB + 128;
-	HIPCHK(ensure(dv.ctr, CTRB));
+	/* counters: rejection shards, then {flag count, walk fault, redo count, compact count, loop
+	 * fault} and the sum maximum 64 bytes further (kept across the bands of a streamed SUM); one
+	 * memset, one read-back.  A synchronous call uses slot 0 (a streamed SUM keeps its maximum
+	 * there); an async call the free slot, folding the older pending call when both are taken */
+	const size_t REJB = SG_CTR_REJB, CTRB = SG_CTRB;
+	HIPCHK(ensure(dv.ctr, 2 * CTRB));
 	if (!dv.ctr_h)
-		HIPCHK(hipHostMalloc(&dv.ctr_h, CTRB));
+		HIPCHK(hipHostMalloc(&dv.ctr_h, 2 * CTRB));
+	int slot = 0;
+	if (async) {
+		if (dv.pend[0] && dv.pend[1])
+			stack_fold_acc(ctx, dv, dv.pend_seq[0] < dv.pend_seq[1] ? 0 : 1);
+		slot = dv.pend[0] ? 1 : 0;
+	} else if (dv.pend[0]) {
+		stack_fold_acc(ctx, dv, 0);
+	}
+	char *cblk = (char *)dv.ctr.p + (size_t)slot * CTRB;
+	hipEvent_t *cev = dv.cev[slot];
 	const bool clear_max = sum_mode == SUM_WHOLE || sum_mode == SUM_FIRST_BAND;
-	HIPCHK(hipMemsetAsync(dv.ctr.p, 0, clear_max ? CTRB : REJB + 64, s));
-	p.rej = (unsigned long long *)dv.ctr.p;
-	p.flag_count = (unsigned int *)((char *)dv.ctr.p + REJB);
+	HIPCHK(hipMemsetAsync(cblk, 0, clear_max ? CTRB : REJB + 64, s));
+	p.rej = (unsigned long long *)cblk;
+	p.flag_count = (unsigned int *)(cblk + REJB);
 	p.walk_fault = p.flag_count + 1;
 	p.loop_fault = p.flag_count + 4;
-	p.maxim = (unsigned int *)((char *)dv.ctr.p + REJB + 64);
-	const unsigned int *ctr_flags = (const unsigned int *)((const char *)dv.ctr_h + REJB);
-	bool have_counts = false;
-	auto readback = [&]() -> int {
-		HIPCHK(hipMemcpyAsync(dv.ctr_h, dv.ctr.p, CTRB, hipMemcpyDeviceToHost, s));
-		HIPCHK(hipStreamSynchronize(s));
-		dv.stage_pending = false;
-		have_counts = true;
+	p.maxim = (unsigned int *)(cblk + REJB + 64);
+	/* the pixel classes of the band's rows (no other row's class is read: a chain walk that
+	 * leaves the band replays its pixels, k_stack_literal) */
+	auto clear_flags = [&]() -> int {
+		char *fm = (char *)dv.flag_map.p + (size_t)row_begin * W;
+		if (C == 1)
+			HIPCHK(hipMemsetAsync(fm, 0, (size_t)nrows * W, s));
+		else
+			HIPCHK(hipMemset2DAsync(fm, (size_t)H * W, 0, (size_t)nrows * W, (size_t)C, s));
 		return SG_OK;
 	};
 
@@ -586,7 +676,6 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		(d->method == SG_STACK_MEAN && d->rejection != SG_NO_REJEC);
 	if (sorted) {
 		const int nreg = pick_nreg(N);
-		unsigned int *late_redo = nullptr, *late_list = nullptr;	/* redo list routed on the device */
 		/* histogram fast path (sg_stack_hist.hip): SIGMA / WINSORIZED / PERCENTILE rejection and
 		 * stack_median, any normalisation, 16 <= N <= 65535 (per-lane zero / 65535 counters are
 		 * 16-bit halves) */
@@ -601,8 +690,8 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		const size_t npix_launch = (size_t)C * nrows * W;
 		HIPCHK(ensure(dv.flag_list, sizeof(unsigned int) * npix_launch));
 		HIPCHK(ensure(dv.flag_map, npix_img));
-		/* flag_map is cleared right after the main kernel is queued (only the kernels after it
-		 * read it), so the clear is not ahead of the histogram kernel's launch */
+		/* flag_map (the band's rows) is cleared right after the main kernel is queued (only the
+		 * kernels after it read it), so the clear is not ahead of the histogram kernel's launch */
 		p.flag_list = (unsigned int *)dv.flag_list.p;
 		p.flag_cap = (unsigned int)npix_launch;
 		p.flag_map = (uint8_t *)dv.flag_map.p;
@@ -644,7 +733,7 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			HIPCHK(ensure(dv.redo, sizeof(unsigned int) * (npix_launch + 16)));
 			unsigned int *redo_count = p.flag_count + 2;	/* cleared with the counters */
 			unsigned int *redo_list = (unsigned int *)dv.redo.p + 16;
-			HIPCHK(hipEventRecord(dv.ev[0], s));
+			HIPCHK(hipEventRecord(cev[0], s));
 			/* NORM: 0 none, 1 additive (round(v scale - offset)), 2 multiplicative (round(v scale mul)),
 			 * 3 additive with the folded + 0.5 */
 			const int norm = p.normalize == SG_NO_NORM ? 0 :
@@ -704,110 +793,77 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			default: return set_err(ctx, SG_ERR_GENERIC, "no histogram kernel for this case%s%.0ld", "", 0);
 			}
 			HIPCHK(hipGetLastError());
-			HIPCHK(hipEventRecord(dv.ev[1], s));
-			HIPCHK(hipMemsetAsync(dv.flag_map.p, 0, npix_img, s));
+			HIPCHK(hipEventRecord(cev[1], s));
+			if (int rc = clear_flags())
+				return rc;
 			st.path = 1;
 			st.main_kernel_blocks = (int)nblk;
 			st.launches = 1;
+			st.compact_pixels = compact ? p.cmp_cap : 0;	/* the capacity; clamped to the count when folded */
+			const dim3 lgrid(SG_LIST_GRID);
 			if (compact) {
-				/* the grid covers the capacity; blocks past the device-side count return at once */
+				/* the compact columns, any count up to the capacity (grid-stride) */
 				SgStackParams q = p;
 				q.cmp_src = p.cmp_cols;
-				HIPCHK(launch_sorted(nreg, true, dim3((p.cmp_cap + SG_TILE_W - 1) / SG_TILE_W), lds, s, q, p.cmp_list,
-						p.cmp_count));
+				HIPCHK(launch_sorted(nreg, true, lgrid, lds, s, q, p.cmp_list, p.cmp_count));
 				st.launches++;
 			}
-			/* the redo pixels: up to SG_REDO_REPLAY_MAX go straight to the wave-per-pixel replay
-			 * (every sample of a pixel gathered by one wave at once), decided on the device so
-			 * the step needs no host round trip; a longer list (rare: e.g. the normalised zeros
-			 * of rows near the frame border) goes through the sorted kernel, 64 pixels per
-			 * workgroup, once the count is back (measured: 22 k pixels faster in the replay,
-			 * 113 k slower) */
-			/* N > 1024 (no sorted kernel): every redo pixel goes to the replay / literal kernels.
-			 * stack_median / PERCENTILE: the sorted kernel takes up to SG_REDO_REPLAY_MAX listed
-			 * pixels straight away (its grid idles past the device-side count; the literal
-			 * kernel's one thread per pixel sorts slowly: 740 pixels took 8 ms) */
-			const bool sorted_redo = nreg && (d->method == SG_STACK_MEDIAN || p.rejection == SG_PERCENTILE);
-			const bool dev_route = (N <= SG_REPLAY_MAXN && ctx->knobs.redo_replay) || !nreg;
-			if (sorted_redo) {
-				/* the grid covers SG_REDO_REPLAY_MAX slots: a longer list makes this launch idle and
-				 * the late launch below takes the whole list (each pixel's counters added once) */
+			/* the redo pixels, routed on the device (no host round trip in the call):
+			 * - SIGMA / WINSORIZED, N <= SG_REPLAY_MAXN: up to SG_REDO_REPLAY_MAX pixels straight to
+			 *   the wave-per-pixel replay (every sample of a pixel gathered by one wave at once), a
+			 *   longer list (rare: e.g. normalised zeros of rows near the frame border) through the
+			 *   sorted kernel (measured: 22 k pixels faster in the replay, 113 k slower);
+			 * - stack_median / PERCENTILE: the sorted kernel (the literal kernel's one thread per
+			 *   pixel sorts slowly: 740 pixels took 8 ms);
+			 * - N > 1024 (no sorted kernel): every redo pixel to the replay / literal kernels */
+			const bool replay_route = nreg && d->method == SG_STACK_MEAN && (p.rejection == SG_SIGMA ||
+					p.rejection == SG_WINSORIZED) && N <= SG_REPLAY_MAXN && ctx->knobs.redo_replay;
+			if (replay_route) {
 				SgStackParams q = p;
-				q.list_maxn = SG_REDO_REPLAY_MAX;
-				HIPCHK(launch_sorted(nreg, true, dim3(SG_REDO_REPLAY_MAX / SG_TILE_W), lds, s, q, redo_list, redo_count));
+				q.list_minn = SG_REDO_REPLAY_MAX;	/* idle unless the list is longer */
+				HIPCHK(launch_sorted(nreg, true, lgrid, lds, s, q, redo_list, redo_count));
+				p.rp_list = redo_list;
+				p.rp_count = redo_count;
+				p.rp_maxn = SG_REDO_REPLAY_MAX;
 				st.launches++;
-				late_redo = redo_count;
-				late_list = redo_list;
-			} else if (dev_route) {
+			} else if (nreg) {
+				HIPCHK(launch_sorted(nreg, true, lgrid, lds, s, p, redo_list, redo_count));
+				st.launches++;
+			} else {
 				hipLaunchKernelGGL(k_redo_to_literal, dim3(64), dim3(256), 0, s, p, (const unsigned int *)redo_list,
-						(const unsigned int *)redo_count, nreg ? (unsigned int)SG_REDO_REPLAY_MAX : 0xFFFFFFFFu);
+						(const unsigned int *)redo_count, 0xFFFFFFFFu);
 				HIPCHK(hipGetLastError());
 				st.launches++;
-				late_redo = redo_count;
-				late_list = redo_list;
-			} else {
-				unsigned int nredo = 0;
-				HIPCHK(hipMemcpyAsync(&nredo, redo_count, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
-				HIPCHK(hipStreamSynchronize(s));
-				st.chain_pixels = nredo;
-				if (nredo) {
-					HIPCHK(launch_sorted(nreg, true, dim3((nredo + SG_TILE_W - 1) / SG_TILE_W), lds, s, p,
-							redo_list, redo_count));
-					st.launches++;
-				}
 			}
 		} else {
-			HIPCHK(hipMemsetAsync(dv.flag_map.p, 0, npix_img, s));
-			HIPCHK(hipEventRecord(dv.ev[0], s));
+			if (int rc = clear_flags())
+				return rc;
+			HIPCHK(hipEventRecord(cev[0], s));
 			HIPCHK(launch_sorted(nreg, false, dim3((unsigned)nblk), lds, s, p, nullptr, nullptr));
-			HIPCHK(hipEventRecord(dv.ev[1], s));
+			HIPCHK(hipEventRecord(cev[1], s));
 			st.main_kernel_blocks = (int)nblk;
 			st.launches = 1;
 		}
-		/* exact wave-per-pixel replay of queued SIGMA / WINSORIZED pixels (early breaks with
-		 * this pixel's own stale rejected[]), then the literal path for what remains: two
-		 * phases, grids read the count on the device */
-		/* literal kernel: one thread per queued pixel with N * 5 bytes of scratch each; 65536
-		 * threads up to 2048 frames, then as many as 1 GiB of scratch holds */
+		/* exact wave-per-pixel replay of queued SIGMA / WINSORIZED pixels (the replay route's redo
+		 * list, early breaks with this pixel's own stale rejected[]), then the literal path for what
+		 * remains: two phases, grids read the count on the device */
 		const unsigned lit_threads = lit_thread_count(N);
 		HIPCHK(ensure(dv.scratch, lit_scratch_bytes(N)));
-		auto launch_tail = [&]() -> int {
-			if (d->method == SG_STACK_MEAN && (p.rejection == SG_SIGMA || p.rejection == SG_WINSORIZED) &&
-					N <= SG_REPLAY_MAXN) {
-				if (N <= 512)	/* the per-wave LDS sized for 512 frames (k_stack_replay<SG_REPLAY_FASTN>) */
-					hipLaunchKernelGGL(k_stack_replay<512>, dim3(2048), dim3(64 * SG_REPLAY_WAVES), 0, s, p);
-				else
-					hipLaunchKernelGGL(k_stack_replay<SG_REPLAY_MAXN>, dim3(2048), dim3(64 * SG_REPLAY_WAVES), 0, s, p);
-				HIPCHK(hipGetLastError());
-				st.launches++;
-			}
-			for (int phase = 1; phase <= 2; phase++) {
-				hipLaunchKernelGGL(k_stack_literal, dim3(lit_threads / 64), dim3(64), 0, s, p, ct,
-						0u, (uint8_t *)dv.scratch.p, phase);
-				HIPCHK(hipGetLastError());
-			}
-			st.launches += 2;
-			return SG_OK;
-		};
-		if (int rc = launch_tail())
-			return rc;
-		if (late_redo) {
-			/* the redo count comes back with the counters (no extra round trip); only a long
-			 * list the device left alone needs the sorted kernel, the tail and a second read */
-			HIPCHK(hipEventRecord(dv.ev[2], s));
-			if (int rc = readback())
-				return rc;
-			const unsigned int nredo = ctr_flags[2];
-			st.chain_pixels = nredo;
-			if (nredo > SG_REDO_REPLAY_MAX && nreg) {
-				have_counts = false;
-				HIPCHK(launch_sorted(nreg, true, dim3((nredo + SG_TILE_W - 1) / SG_TILE_W), lds, s, p, late_list,
-						late_redo));
-				st.launches++;
-				if (int rc = launch_tail())
-					return rc;
-			}
+		if (d->method == SG_STACK_MEAN && (p.rejection == SG_SIGMA || p.rejection == SG_WINSORIZED) &&
+				N <= SG_REPLAY_MAXN) {
+			if (N <= 512)	/* the per-wave LDS sized for 512 frames (k_stack_replay<SG_REPLAY_FASTN>) */
+				hipLaunchKernelGGL(k_stack_replay<512>, dim3(2048), dim3(64 * SG_REPLAY_WAVES), 0, s, p);
+			else
+				hipLaunchKernelGGL(k_stack_replay<SG_REPLAY_MAXN>, dim3(2048), dim3(64 * SG_REPLAY_WAVES), 0, s, p);
+			HIPCHK(hipGetLastError());
+			st.launches++;
 		}
+		for (int phase = 1; phase <= 2; phase++) {
+			hipLaunchKernelGGL(k_stack_literal, dim3(lit_threads / 64), dim3(64), 0, s, p, ct,
+					0u, (uint8_t *)dv.scratch.p, phase);
+			HIPCHK(hipGetLastError());
+		}
+		st.launches += 2;
 	} else {
 		if (int rc = flush_inputs())
 			return rc;
@@ -823,7 +879,7 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		 * the per-lane pair kernel (SG_REDUCE1=2, A/B) otherwise */
 		const bool r3 = pairs && hist_addr_ok && ctx->knobs.reduce1 == 0;
 		const unsigned nb3 = (unsigned)(((W + 511) / 512) * (size_t)nrows * C);
-		HIPCHK(hipEventRecord(dv.ev[0], s));
+		HIPCHK(hipEventRecord(cev[0], s));
 		if (r3) {
 			switch (d->method) {
 			case SG_STACK_SUM: hipLaunchKernelGGL(k_stack_reduce3<0>, dim3(nb3), dim3(256), 0, s, p, p.hist_tab, p.shifty); break;
@@ -842,7 +898,7 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			hipLaunchKernelGGL(k_stack_reduce, grid, dim3(256), 0, s, p);
 		}
 		HIPCHK(hipGetLastError());
-		HIPCHK(hipEventRecord(dv.ev[1], s));
+		HIPCHK(hipEventRecord(cev[1], s));
 		st.main_kernel_blocks = r3 ? (int)nb3 : pairs ? (int)(grid2.x * grid2.y * grid2.z) : (int)(grid.x * grid.y * grid.z);
 		st.launches = 1;
 		if (d->method == SG_STACK_SUM && (sum_mode == SUM_WHOLE || sum_mode == SUM_LAST_BAND)) {
@@ -860,40 +916,18 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			st.launches++;
 		}
 	}
-	if (!have_counts) {
-		HIPCHK(hipEventRecord(dv.ev[2], s));
-		if (int rc = readback())	/* counters back to the host */
-			return rc;
-	}
-	const unsigned long long *shards = (const unsigned long long *)dv.ctr_h;
-	const unsigned int cnt[3] = {ctr_flags[0], ctr_flags[1], ctr_flags[16]};	/* flag count, walk fault, sum maximum */
-	if (ctr_flags[4])
-		return set_err(ctx, SG_ERR_GENERIC, "SIGMEDIAN: the reference's clipping loop never ends for some pixel "
-				"(a pass replaces samples by the values they already hold, stacking.c:1696-1709)%s%.0ld", "", 0);
-	if (cnt[1])
-		return set_err(ctx, SG_ERR_WALK, "a first-pass early break needs the stale rejected[] of a pixel "
-				"whose frame rows are not resident; make the full frames resident%s%.0ld", "", 0);
 	if (SG_DBG(p) == 12)
 		sg_dbg_why_dump(s);
-	float ms = 0.f, ms2 = 0.f;
-	HIPCHK(hipEventElapsedTime(&ms, dv.ev[0], dv.ev[1]));
-	HIPCHK(hipEventElapsedTime(&ms2, dv.ev[0], dv.ev[2]));
-	st.kernel_ms = ms;
-	st.total_ms = ms2;
-	st.slow_pixels = cnt[0];
-	st.compact_pixels = std::min(ctr_flags[3], p.cmp_cap);
-	if (rej) {
-		for (int c = 0; c < 3; c++)
-			rej[c][0] = rej[c][1] = 0;
-		for (int k = 0; k < SG_REJ_SHARDS; k++)
-			for (int c = 0; c < 3; c++) {
-				rej[c][0] += shards[(size_t)k * 6 + c * 2];
-				rej[c][1] += shards[(size_t)k * 6 + c * 2 + 1];
-			}
-	}
-	if (maxim_out)
-		*maxim_out = cnt[2];
-	return SG_OK;
+	/* the counters back to the host: queued; a synchronous call folds them at once, an async one
+	 * when its slot is needed again or at sg_stack_collect */
+	HIPCHK(hipMemcpyAsync((char *)dv.ctr_h + (size_t)slot * CTRB, cblk, CTRB, hipMemcpyDeviceToHost, s));
+	HIPCHK(hipEventRecord(cev[2], s));
+	dv.pstats[slot] = st;
+	dv.pend[slot] = true;
+	dv.pend_seq[slot] = ++dv.seq;
+	if (async)
+		return SG_OK;
+	return stack_fold(ctx, dv, slot, rej, maxim_out, true);
 }
 
 extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
@@ -902,6 +936,39 @@ extern "C" int sg_stack_u16_device(sg_ctx *ctx, int dev_index, const sg_stack_de
 	const int rc = stack_device_core(ctx, dev_index, d, d_frames, frame_stride, plane_stride, d_out, row_begin,
 			row_end, rej, maxim_out, stream, SUM_WHOLE);
 	return rc == SG_ERR_WALK ? SG_ERR_GENERIC : rc;
+}
+
+/* the same call queued without waiting: its counters come back with sg_stack_collect */
+extern "C" int sg_stack_u16_device_async(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
+		const uint16_t *d_frames, int64_t frame_stride, int64_t plane_stride, uint16_t *d_out,
+		int row_begin, int row_end, void *stream) {
+	const int rc = stack_device_core(ctx, dev_index, d, d_frames, frame_stride, plane_stride, d_out, row_begin,
+			row_end, nullptr, nullptr, stream, SUM_WHOLE, true);
+	return rc == SG_ERR_WALK ? SG_ERR_GENERIC : rc;
+}
+
+extern "C" int sg_stack_collect(sg_ctx *ctx, int dev_index, uint64_t rej[3][2], uint64_t *maxim) {
+	if (!ctx || dev_index < 0 || dev_index >= (int)ctx->dev.size())
+		return SG_ERR_GENERIC;
+	SgDevice &dv = ctx->dev[(size_t)dev_index];
+	HIPCHK(hipSetDevice(dv.id));
+	while (dv.pend[0] || dv.pend[1]) {
+		const int slot = (dv.pend[0] && (!dv.pend[1] || dv.pend_seq[0] < dv.pend_seq[1])) ? 0 : 1;
+		stack_fold_acc(ctx, dv, slot);
+	}
+	const int rc = dv.acc_rc;
+	if (rej)
+		for (int c = 0; c < 3; c++) {
+			rej[c][0] = dv.acc_rej[c][0];
+			rej[c][1] = dv.acc_rej[c][1];
+		}
+	if (maxim)
+		*maxim = dv.acc_max;
+	for (int c = 0; c < 3; c++)
+		dv.acc_rej[c][0] = dv.acc_rej[c][1] = 0;
+	dv.acc_max = 0;
+	dv.acc_rc = 0;
+	return rc;
 }
 
 /* device bytes a stack call holds besides the frames: the output image (2 B per sample),

@@ -70,8 +70,12 @@ struct SgStackParams {
 	unsigned int *cmp_list, *cmp_count;
 	unsigned int cmp_cap;
 	const uint16_t *cmp_src;		/* k_stack_sorted<., true>: stage the listed columns from here (sorted) */
-	unsigned int list_maxn;			/* k_stack_sorted<., true> on the redo list: do nothing when the device count
-						 * exceeds this (0: no limit); the host then relaunches over the whole list */
+	unsigned int list_minn;			/* k_stack_sorted<., true> on the redo list: do nothing unless the device count
+						 * exceeds this (0: take any list); the replay takes the shorter lists */
+	/* k_stack_replay: the histogram path's redo list taken directly when its count is at most
+	 * rp_maxn (null: only the flag list) */
+	const unsigned int *rp_list, *rp_count;
+	unsigned int rp_maxn;
 	uint32_t *sum_buf;			/* SUM: raw sums [C][H][W] */
 	unsigned int *maxim;			/* SUM: global max of sums */
 };

@@ -60,6 +60,18 @@ struct SgDevice {
 	 * cleared by one memset and read back by one D2H copy into ctr_h (pinned) */
 	SgBuf ctr;
 	void *ctr_h = nullptr;
+	/* two counter slots (device block + pinned host copy each): sg_stack_u16_device_async queues a
+	 * call's read-back into its slot and returns; the slot is folded (event wait, fault checks,
+	 * counters added to acc_*) by the next call that needs it or by sg_stack_collect.
+	 * cev[slot] = {start, main kernel end, read-back done} */
+	hipEvent_t cev[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
+	bool pend[2] = {false, false};
+	unsigned long long pend_seq[2] = {0, 0}, seq = 0;
+	sg_stack_stats pstats[2];	/* a pending call's statistics (timings filled in when folded) */
+	int pend_sum_read[2] = {0, 0};	/* the call reports the SUM maximum */
+	uint64_t acc_rej[3][2] = {{0, 0}, {0, 0}, {0, 0}};
+	uint64_t acc_max = 0;
+	int acc_rc = 0;
 	uint16_t *pinned[2] = {nullptr, nullptr};
 	size_t pinned_size = 0;
 	/* file decode path (sg_io.hip): pinned staging of raw frames, device raw buffers */

@@ -649,19 +649,24 @@ k_stack_sorted(SgStackParams p, const unsigned int *__restrict__ list, const uns
 	uint32_t *stage32 = (uint32_t *)stage;
 	const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 	const int N = p.N;
-	int c0 = 0;
+	/* LISTED: the redo / compact list, slots of 64 pixels dealt to the blocks in a grid-stride
+	 * loop, so one fixed grid takes any list length the device produced (no host round trip);
+	 * otherwise one tile of one image row per block */
+	unsigned int count = 0;
 	if (LISTED) {
-		/* redo list of the histogram path: slot i = pixel list[64 * block + i]; a grid sized
-		 * for the longest list the device routes itself leaves its blocks past the count idle */
-		unsigned int count = *list_count;
+		count = *list_count;
 		if (p.cmp_src && count > p.cmp_cap)	/* the compact list: slots past the capacity went to the redo list */
 			count = p.cmp_cap;
-		if (!p.cmp_src && p.list_maxn && count > p.list_maxn)
-			return;	/* a longer list than this launch's grid: the host's late launch takes all of it */
-		if ((unsigned int)blockIdx.x * SG_TILE_W >= count)
-			return;
+		if (!p.cmp_src && p.list_minn && count <= p.list_minn)
+			return;	/* a short list: k_stack_replay takes it */
+	}
+	for (unsigned int vb = blockIdx.x;; vb += gridDim.x) {
+	int c0 = 0;
+	if (LISTED) {
+		if (vb * SG_TILE_W >= count)
+			break;
 		if (tid < SG_TILE_W) {
-			const unsigned int k = blockIdx.x * SG_TILE_W + tid;
+			const unsigned int k = vb * SG_TILE_W + tid;
 			if (k < count) {
 				const unsigned int pix = list[k];
 				const int xx = (int)(pix % (unsigned)p.W);
@@ -678,7 +683,7 @@ k_stack_sorted(SgStackParams p, const unsigned int *__restrict__ list, const uns
 	} else {
 		const int ntx = (p.W + SG_TILE_W - 1) / SG_TILE_W;
 		const int nrows = p.row_end - p.row_begin;
-		int b = blockIdx.x;
+		int b = (int)vb;
 		const int xt = b % ntx;
 		b /= ntx;
 		const int R = p.row_begin + (b % nrows);
@@ -695,7 +700,7 @@ k_stack_sorted(SgStackParams p, const unsigned int *__restrict__ list, const uns
 	if (LISTED && p.cmp_src) {
 		/* the compact redo list (sg_stack_hist.hip sgh_compact): slot k's sorted column is
 		 * cmp_src[k][0 .. N), read by a wave per slot with coalesced loads; no gather, no sort */
-		const unsigned int k0 = blockIdx.x * SG_TILE_W;
+		const unsigned int k0 = vb * SG_TILE_W;
 		for (int sl = wave; sl < SG_TILE_W; sl += SG_SORT_THREADS / 64) {
 			if (slot_x[sl] < 0)
 				continue;
@@ -847,12 +852,16 @@ k_stack_sorted(SgStackParams p, const unsigned int *__restrict__ list, const uns
 					hi += __shfl_down(hi, o, 64);
 				}
 				if (tid == 0 && (lo | hi)) {
-					unsigned long long *sh = p.rej + ((size_t)(blockIdx.x % SG_REJ_SHARDS) * 6 + c0 * 2);
+					unsigned long long *sh = p.rej + ((size_t)(vb % SG_REJ_SHARDS) * 6 + c0 * 2);
 					atomicAdd(sh, lo);
 					atomicAdd(sh + 1, hi);
 				}
 			}
 		}
+	}
+	if (!LISTED)
+		break;
+	__syncthreads();	/* the slot tables and the stage are rewritten by the next list tile */
 	}
 }
 
@@ -2226,10 +2235,17 @@ k_stack_replay(SgStackParams p) {
 		count = p.flag_cap;
 	if ((p.rejection != 2 && p.rejection != 4) || p.N > NM)
 		return;
+	/* items [0, nr): the histogram path's redo list (when short enough), then the flag list (the
+	 * sorted kernel's queued pixels); a redo pixel the replay cannot finish joins the flag list as
+	 * LITERAL (appended past `count`: the literal kernel's phase 1 takes it) */
+	unsigned int nr = p.rp_list ? *p.rp_count : 0;
+	if (nr > p.rp_maxn)
+		nr = 0;
 	const unsigned int nw = gridDim.x * SG_REPLAY_WAVES;
-	for (unsigned int i = blockIdx.x * SG_REPLAY_WAVES + wv; i < count; i += nw) {
-		const int64_t pix = p.flag_list[i];
-		if (p.flag_map[pix] != SG_CLS_LITERAL)
+	for (unsigned int i = blockIdx.x * SG_REPLAY_WAVES + wv; i < nr + count; i += nw) {
+		const bool direct = i < nr;
+		const int64_t pix = direct ? p.rp_list[i] : p.flag_list[i - nr];
+		if (!direct && p.flag_map[pix] != SG_CLS_LITERAL)
 			continue;
 		const int x = (int)(pix % p.W);
 		const int64_t cr = pix / p.W;
@@ -2276,8 +2292,15 @@ k_stack_replay(SgStackParams p) {
 			atomicMax(&g_sg_rprof[14], (unsigned long long)L.npass);
 		}
 #endif
-		if (!ok)
+		if (!ok) {
+			if (direct && lane == 0) {	/* to the literal kernel, as k_redo_to_literal queues */
+				p.flag_map[pix] = SG_CLS_LITERAL;
+				const unsigned int slot = atomicAdd(p.flag_count, 1u);
+				if (slot < p.flag_cap)
+					p.flag_list[slot] = (unsigned int)pix;
+			}
 			continue;
+		}
 		if (lane == 0) {
 			p.out[pix] = v;
 			p.flag_map[pix] = SG_CLS_DONE;

@@ -78,6 +78,7 @@ class SeqInfo(ctypes.Structure):
 
 # every symbol include/sirilgpu.h and include/sirilgpu_io.h declare
 EXPORTS = ["sg_init", "sg_shutdown", "sg_last_error", "sg_stack_u16", "sg_stack_u16_device",
+           "sg_stack_u16_device_async", "sg_stack_collect", "sg_device_count",
            "sg_get_last_stats", "sg_register_dft_u16", "sg_register_dft_u16_device",
            "sg_register_dft_u16_device_raw", "sg_synth_fill_device",
            "sg_seq_open_ser", "sg_seq_open_fits", "sg_seq_close", "sg_seq_get_info", "sg_seq_read_region",
@@ -114,6 +115,13 @@ def load():
                                         ctypes.c_int64, P, ctypes.c_int, ctypes.c_int,
                                         ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64), P]
     lib.sg_stack_u16_device.restype = ctypes.c_int
+    lib.sg_stack_u16_device_async.argtypes = [P, ctypes.c_int, ctypes.POINTER(StackDesc), P, ctypes.c_int64,
+                                              ctypes.c_int64, P, ctypes.c_int, ctypes.c_int, P]
+    lib.sg_stack_u16_device_async.restype = ctypes.c_int
+    lib.sg_stack_collect.argtypes = [P, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    lib.sg_stack_collect.restype = ctypes.c_int
+    lib.sg_device_count.argtypes = [P, ctypes.POINTER(ctypes.c_int)]
+    lib.sg_device_count.restype = ctypes.c_int
     lib.sg_get_last_stats.argtypes = [P, ctypes.POINTER(StackStats)]
     lib.sg_get_last_stats.restype = ctypes.c_int
     lib.sg_synth_fill_device.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -433,6 +441,26 @@ class Context:
                                           ctypes.c_void_p(stream) if stream else None)
         self.check(rc, "sg_stack_u16_device")
         return np.array(list(rej), dtype=np.uint64).reshape(3, 2), int(maxim.value)
+
+    def stack_device_async(self, desc, d_frames, frame_stride, plane_stride, d_out, row_begin, row_end,
+                           stream=None, dev_index=0):
+        """sg_stack_u16_device_async: queued, nothing waited for; results via collect()"""
+        rc = self.lib.sg_stack_u16_device_async(self.ctx, dev_index, ctypes.byref(desc), ctypes.c_void_p(d_frames),
+                                                frame_stride, plane_stride, ctypes.c_void_p(d_out), row_begin,
+                                                row_end, ctypes.c_void_p(stream) if stream else None)
+        self.check(rc, "sg_stack_u16_device_async")
+
+    def collect(self, dev_index=0):
+        """sg_stack_collect: (rc, summed rejection counters [3][2], max SUM maximum) of the pending calls"""
+        rej = (ctypes.c_uint64 * 6)()
+        maxim = ctypes.c_uint64(0)
+        rc = self.lib.sg_stack_collect(self.ctx, dev_index, rej, ctypes.byref(maxim))
+        return rc, np.array(list(rej), dtype=np.uint64).reshape(3, 2), int(maxim.value)
+
+    def device_count(self):
+        n = ctypes.c_int(0)
+        self.check(self.lib.sg_device_count(self.ctx, ctypes.byref(n)), "sg_device_count")
+        return n.value
 
     def load_seq_device(self, seq, d_frames, first=0, count=None, frame_stride=0, dev_index=0, stream=None):
         """frames of an opened Seq decoded on the device (sg_seq_load_device)"""

@@ -274,3 +274,55 @@ def test_host_pull_cancel(gpu_ctx, devs):
         assert rc == -1
         rc, out, rej, _ = c.stack_host(desc, frames)       # the context stays usable
         assert rc == 0, c.error()
+
+
+@pytest.mark.parametrize("method,rejection", [(sg.MEAN, sg.SIGMA), (sg.MEAN, sg.WINSORIZED),
+                                              (sg.MEAN, sg.PERCENTILE), (sg.MEDIAN, sg.NO_REJEC),
+                                              (sg.MEAN, sg.NO_REJEC), (sg.MEAN, sg.LINEARFIT)])
+def test_async_bands_collect(gpu_ctx, method, rejection):
+    """sg_stack_u16_device_async: every band queued without waiting (more calls than the two
+    counter slots, so earlier calls are folded on the way), then sg_stack_collect: the image and
+    the SUMMED rejection counters equal the oracle's"""
+    import torch
+    N, C, H, W = 40, 2, 48, 200
+    frames = orc.synth(N, C, H, W, seed=61, maxshift=5)
+    sx, sy = orc.synth_shifts(N, seed=61, maxshift=5)
+    sig = REJ[rejection]
+    ref, rej_ref = _oracle(frames, method, rejection, sig, sx, sy, 4)
+    d_out = torch.zeros(C * H * W, dtype=torch.int16, device="cuda")
+    full = _dev(frames)
+    desc, keep = sg.make_desc(method, N, W, H, C, rejection=rejection, sig=sig, shiftx=sx, shifty=sy, max_thread=4,
+                              max_number_of_rows=H)
+    world = 5
+    for r in range(world):
+        b, e = sd.row_band(r, world, H)
+        gpu_ctx.stack_device_async(desc, full.data_ptr(), C * H * W, H * W, d_out.data_ptr(), b, e)
+    rc, rej, _ = gpu_ctx.collect()
+    assert rc == 0, gpu_ctx.error()
+    out = d_out.cpu().numpy().view(np.uint16).reshape(C, H, W)
+    assert_same(out, ref, f"async bands method={method} rej={rejection}")
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+    rc, rej2, _ = gpu_ctx.collect()             # nothing pending: zeros
+    assert rc == 0 and not rej2.any()
+
+
+def test_async_fault_reported_by_collect(gpu_ctx):
+    """a refused regime met by a queued call (here SIGMEDIAN's never-ending loop) surfaces at
+    sg_stack_collect, and the next collect starts clean"""
+    import torch
+    N, H, W = 4, 8, 16
+    frames = np.full((N, 1, H, W), 1000, dtype=np.uint16)
+    frames[:, 0, 3, 5] = [990, 0, 0, 1049]
+    d_out = torch.zeros(H * W, dtype=torch.int16, device="cuda")
+    full = _dev(frames)
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=sg.SIGMEDIAN, sig=(2.5, 0.7), max_thread=1,
+                              max_number_of_rows=H)
+    for b, e in [(0, 3), (3, 6), (6, 8)]:
+        gpu_ctx.stack_device_async(desc, full.data_ptr(), H * W, H * W, d_out.data_ptr(), b, e)
+    rc, _, _ = gpu_ctx.collect()
+    assert rc != 0 and "never ends" in gpu_ctx.error()
+    frames[:, 0, 3, 5] = 1000
+    full = _dev(frames)
+    gpu_ctx.stack_device_async(desc, full.data_ptr(), H * W, H * W, d_out.data_ptr(), 0, H)
+    rc, _, _ = gpu_ctx.collect()
+    assert rc == 0, gpu_ctx.error()
