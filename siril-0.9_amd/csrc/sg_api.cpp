@@ -51,6 +51,8 @@ __global__ void k_synth_fill(uint16_t *frames, int first_frame, int nframes, int
 #include "sg_ctx.hpp"
 
 __global__ void k_flip_rows(const uint16_t *src, uint16_t *dst, int W, int rows);
+__global__ void k_stage_copy(uint4 *dst, const uint4 *src, unsigned int n16);
+__global__ void k_ctr_finalize(unsigned long long *ctr, unsigned long long *host);
 /* host-pull readers per device and the bytes of one region read (two pinned + two device
  * staging buffers of this size per reader) */
 #define SG_PULL_READERS 8
@@ -301,6 +303,8 @@ enum { SUM_WHOLE = 0, SUM_FIRST_BAND = 1, SUM_MID_BAND = 2, SUM_LAST_BAND = 3 };
 /* counter block of one slot: rejection shards, then {flag count, walk fault, redo count, compact
  * count, loop fault} and the SUM maximum 64 bytes further */
 static const size_t SG_CTRB = SG_CTR_REJB + 128;
+/* host-mapped slot k_ctr_finalize writes: rejection sums at 0, the flag block at 64 */
+static const size_t SG_CTR_HOSTB = 256;
 /* blocks of the listed k_stack_sorted launches (grid-stride over any list length) */
 #define SG_LIST_GRID 1024
 
@@ -312,8 +316,8 @@ static int stack_fold(sg_ctx *ctx, SgDevice &dv, int slot, uint64_t rej[3][2], u
 	HIPCHK(hipEventSynchronize(dv.cev[slot][2]));
 	dv.pend[slot] = false;
 	dv.stage_pending = false;	/* the input copy ran before this call's kernels */
-	const char *h = (const char *)dv.ctr_h + (size_t)slot * SG_CTRB;
-	const unsigned int *fl = (const unsigned int *)(h + SG_CTR_REJB);
+	const char *h = (const char *)dv.ctr_h + (size_t)slot * SG_CTR_HOSTB;
+	const unsigned int *fl = (const unsigned int *)(h + 64);
 	sg_stack_stats &st = dv.pstats[slot];
 	float ms = 0.f, ms2 = 0.f;
 	HIPCHK(hipEventElapsedTime(&ms, dv.cev[slot][0], dv.cev[slot][1]));
@@ -337,17 +341,14 @@ static int stack_fold(sg_ctx *ctx, SgDevice &dv, int slot, uint64_t rej[3][2], u
 		return set_err(ctx, SG_ERR_WALK, "a first-pass early break needs the stale rejected[] of a pixel "
 				"whose frame rows are not resident; make the full frames resident%s%.0ld", "", 0);
 	if (rej) {
-		const unsigned long long *shards = (const unsigned long long *)h;
-		for (int c = 0; c < 3; c++)
-			rej[c][0] = rej[c][1] = 0;
-		for (int k = 0; k < SG_REJ_SHARDS; k++)
-			for (int c = 0; c < 3; c++) {
-				rej[c][0] += shards[(size_t)k * 6 + c * 2];
-				rej[c][1] += shards[(size_t)k * 6 + c * 2 + 1];
-			}
+		const unsigned long long *sums = (const unsigned long long *)h;	/* k_ctr_finalize's */
+		for (int c = 0; c < 3; c++) {
+			rej[c][0] = sums[c * 2];
+			rej[c][1] = sums[c * 2 + 1];
+		}
 	}
 	if (maxim_out)
-		*maxim_out = fl[16];
+		*maxim_out = dv.pend_sum_read[slot] ? fl[16] : 0;
 	return SG_OK;
 }
 
@@ -370,7 +371,7 @@ static void stack_fold_acc(sg_ctx *ctx, SgDevice &dv, int slot) {
 static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		const uint16_t *d_frames, int64_t frame_stride, int64_t plane_stride, uint16_t *d_out,
 		int row_begin, int row_end, uint64_t rej[3][2], uint64_t *maxim_out, void *stream, int sum_mode,
-		bool async = false) {
+		bool async = false, int *slot_out = nullptr) {
 	if (!ctx || !d || dev_index < 0 || dev_index >= (int)ctx->dev.size())
 		return SG_ERR_GENERIC;
 	SgDevice &dv = ctx->dev[dev_index];
@@ -392,11 +393,14 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 	struct Publish {
 		sg_ctx *c;
 		const sg_stack_stats &s;
+		bool on;
 		~Publish() {
+			if (!on)	/* an async call's statistics are published when it is folded */
+				return;
 			std::lock_guard<std::mutex> lk(c->mu);
 			c->stats = s;
 		}
-	} publish{ctx, st};
+	} publish{ctx, st, !async};
 
 	SgStackParams p;
 	memset(&p, 0, sizeof p);
@@ -559,7 +563,7 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		const size_t b_sh = sizeof(int) * sh.size(), o_nm = (b_sh + 255) & ~(size_t)255;
 		const size_t b_nm = sizeof(double) * nm.size(), o_tb = (o_nm + b_nm + 255) & ~(size_t)255;
 		const size_t o_zt = (o_tb + sizeof(int) * tables.size() + 255) & ~(size_t)255;
-		const size_t tot = o_zt + sizeof(int) * ztab.size();
+		const size_t tot = (o_zt + sizeof(int) * ztab.size() + 15) & ~(size_t)15;
 		if (dv.stage_pending) {	/* an earlier call's copy may still read the host block */
 			HIPCHK(hipEventSynchronize(dv.ev[3]));
 			dv.stage_pending = false;
@@ -569,8 +573,10 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 				(void)hipHostFree(dv.stage_h);
 			dv.stage_h = nullptr;
 			dv.stage_h_size = 0;
-			HIPCHK(hipHostMalloc(&dv.stage_h, tot));
+			/* coherent: the device reads it uncached, so no call sees an earlier call's inputs */
+			HIPCHK(hipHostMalloc(&dv.stage_h, tot, hipHostMallocMapped | hipHostMallocCoherent));
 			dv.stage_h_size = tot;
+			HIPCHK(hipHostGetDevicePointer(&dv.stage_d, dv.stage_h, 0));
 		}
 		HIPCHK(ensure(dv.inb, tot));
 		char *hb = (char *)dv.stage_h;
@@ -581,7 +587,9 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			memcpy(hb + o_tb, tables.data(), sizeof(int) * tables.size());
 		if (!ztab.empty())
 			memcpy(hb + o_zt, ztab.data(), sizeof(int) * ztab.size());
-		HIPCHK(hipMemcpyAsync(dv.inb.p, dv.stage_h, tot, hipMemcpyHostToDevice, s));
+		hipLaunchKernelGGL(k_stage_copy, dim3((unsigned)std::min<size_t>(64, (tot / 16 + 255) / 256)), dim3(256), 0, s,
+				(uint4 *)dv.inb.p, (const uint4 *)dv.stage_d, (unsigned int)(tot / 16));
+		HIPCHK(hipGetLastError());
 		HIPCHK(hipEventRecord(dv.ev[3], s));
 		dv.stage_pending = true;
 		const char *db = (const char *)dv.inb.p;
@@ -613,9 +621,16 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 	 * memset, one read-back.  A synchronous call uses slot 0 (a streamed SUM keeps its maximum
 	 * there); an async call the free slot, folding the older pending call when both are taken */
 	const size_t REJB = SG_CTR_REJB, CTRB = SG_CTRB;
-	HIPCHK(ensure(dv.ctr, 2 * CTRB));
-	if (!dv.ctr_h)
-		HIPCHK(hipHostMalloc(&dv.ctr_h, 2 * CTRB));
+	{
+		const void *old_ctr = dv.ctr.p;
+		HIPCHK(ensure(dv.ctr, 2 * CTRB));
+		if (dv.ctr.p != old_ctr)
+			dv.ctr_clean[0] = dv.ctr_clean[1] = false;
+	}
+	if (!dv.ctr_h) {
+		HIPCHK(hipHostMalloc(&dv.ctr_h, 2 * SG_CTR_HOSTB, hipHostMallocMapped | hipHostMallocCoherent));
+		HIPCHK(hipHostGetDevicePointer((void **)&dv.ctr_hd, dv.ctr_h, 0));
+	}
 	int slot = 0;
 	if (async) {
 		if (dv.pend[0] && dv.pend[1])
@@ -626,23 +641,19 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 	}
 	char *cblk = (char *)dv.ctr.p + (size_t)slot * CTRB;
 	hipEvent_t *cev = dv.cev[slot];
+	/* the counters are zero when the slot's last call finished (k_ctr_finalize); a fresh or
+	 * failed slot is cleared here (SUM keeps its maximum across the bands of a streamed sum) */
 	const bool clear_max = sum_mode == SUM_WHOLE || sum_mode == SUM_FIRST_BAND;
-	HIPCHK(hipMemsetAsync(cblk, 0, clear_max ? CTRB : REJB + 64, s));
+	if (!dv.ctr_clean[slot])
+		HIPCHK(hipMemsetAsync(cblk, 0, clear_max ? CTRB : REJB + 64, s));
+	else if (clear_max && d->method == SG_STACK_SUM)
+		HIPCHK(hipMemsetAsync(cblk + REJB + 64, 0, sizeof(unsigned int), s));
+	dv.ctr_clean[slot] = false;
 	p.rej = (unsigned long long *)cblk;
 	p.flag_count = (unsigned int *)(cblk + REJB);
 	p.walk_fault = p.flag_count + 1;
 	p.loop_fault = p.flag_count + 4;
 	p.maxim = (unsigned int *)(cblk + REJB + 64);
-	/* the pixel classes of the band's rows (no other row's class is read: a chain walk that
-	 * leaves the band replays its pixels, k_stack_literal) */
-	auto clear_flags = [&]() -> int {
-		char *fm = (char *)dv.flag_map.p + (size_t)row_begin * W;
-		if (C == 1)
-			HIPCHK(hipMemsetAsync(fm, 0, (size_t)nrows * W, s));
-		else
-			HIPCHK(hipMemset2DAsync(fm, (size_t)H * W, 0, (size_t)nrows * W, (size_t)C, s));
-		return SG_OK;
-	};
 
 	/* stack_mean_with_rejection reads a block's rows with area.y += shifty; when a block that
 	 * does not start at the top (area.y > 0) is shifted partly above the frame (area.y + shifty
@@ -689,7 +700,17 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 					"WINSORIZED, PERCENTILE and median stacks take up to 65535", "", N);
 		const size_t npix_launch = (size_t)C * nrows * W;
 		HIPCHK(ensure(dv.flag_list, sizeof(unsigned int) * npix_launch));
-		HIPCHK(ensure(dv.flag_map, npix_img));
+		{
+			/* pixel classes carry this call's epoch (sg_flag_get): no per-call clear; the map is
+			 * cleared when it is new or the 31 epochs wrap */
+			const void *old_map = dv.flag_map.p;
+			HIPCHK(ensure(dv.flag_map, npix_img));
+			if (dv.flag_map.p != old_map || dv.flag_epoch <= 0 || dv.flag_epoch >= 31) {
+				HIPCHK(hipMemsetAsync(dv.flag_map.p, 0, dv.flag_map.size, s));
+				dv.flag_epoch = 0;
+			}
+			p.flag_epoch = (unsigned int)++dv.flag_epoch;
+		}
 		/* flag_map (the band's rows) is cleared right after the main kernel is queued (only the
 		 * kernels after it read it), so the clear is not ahead of the histogram kernel's launch */
 		p.flag_list = (unsigned int *)dv.flag_list.p;
@@ -794,8 +815,6 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			}
 			HIPCHK(hipGetLastError());
 			HIPCHK(hipEventRecord(cev[1], s));
-			if (int rc = clear_flags())
-				return rc;
 			st.path = 1;
 			st.main_kernel_blocks = (int)nblk;
 			st.launches = 1;
@@ -836,8 +855,6 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 				st.launches++;
 			}
 		} else {
-			if (int rc = clear_flags())
-				return rc;
 			HIPCHK(hipEventRecord(cev[0], s));
 			HIPCHK(launch_sorted(nreg, false, dim3((unsigned)nblk), lds, s, p, nullptr, nullptr));
 			HIPCHK(hipEventRecord(cev[1], s));
@@ -920,11 +937,17 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		sg_dbg_why_dump(s);
 	/* the counters back to the host: queued; a synchronous call folds them at once, an async one
 	 * when its slot is needed again or at sg_stack_collect */
-	HIPCHK(hipMemcpyAsync((char *)dv.ctr_h + (size_t)slot * CTRB, cblk, CTRB, hipMemcpyDeviceToHost, s));
+	hipLaunchKernelGGL(k_ctr_finalize, dim3(1), dim3(256), 0, s, (unsigned long long *)cblk,
+			dv.ctr_hd + (size_t)slot * (SG_CTR_HOSTB / sizeof(unsigned long long)));
+	HIPCHK(hipGetLastError());
+	dv.ctr_clean[slot] = true;
 	HIPCHK(hipEventRecord(cev[2], s));
+	dv.pend_sum_read[slot] = d->method == SG_STACK_SUM;
 	dv.pstats[slot] = st;
 	dv.pend[slot] = true;
 	dv.pend_seq[slot] = ++dv.seq;
+	if (slot_out)
+		*slot_out = slot;
 	if (async)
 		return SG_OK;
 	return stack_fold(ctx, dv, slot, rej, maxim_out, true);
@@ -1131,8 +1154,12 @@ static int pull_band(sg_ctx *ctx, SgDevice &dv, PullCall &pc, int nreaders, uint
  * The rows [B, E) of the output on device g: banded under the device's HBM budget like the
  * reference's row blocks (stacking.c:1397-1476, sized from the memory budget :1903-1915); each
  * band's frame rows (the rows its shifts reach, :1544-1577) are pulled by the device's readers
- * and stacked with only those rows resident.  The output rows stay in the device's dv.out
- * (SUM of several devices: raw sums, scaled once the maximum over every device is known).
+ * and stacked with only those rows resident.  With two frame buffers (every method but SUM,
+ * whose 65535/max scaling carries one maximum across the bands) band k + 1 is read while band k
+ * stacks: the stack is queued without waiting (sg_stack_u16_device_async's path) and folded
+ * once the next band has landed, as the reference's team reads blocks while other threads stack
+ * theirs (:1513-1591).  The output rows stay in the device's dv.out (SUM of several devices:
+ * raw sums, scaled once the maximum over every device is known).
  */
 static int pull_device(sg_ctx *ctx, int g, PullCall &pc, int B, int E, int nreaders, uint64_t rej[3][2],
 		uint64_t *maxim) {
@@ -1142,17 +1169,24 @@ static int pull_device(sg_ctx *ctx, int g, PullCall &pc, int B, int E, int nread
 	HIPCHK(hipSetDevice(dv.id));
 	const int64_t halo = std::min<int64_t>((int64_t)pc.sy_max - pc.sy_min, H);
 	const size_t row_bytes = (size_t)N * C * W * sizeof(uint16_t);	/* one row of every frame */
-	int band = E - B;
 	const size_t budget = host_budget(ctx, dv, N, W, H, C);
+	int band = E - B, nbuf = 1;
 	if ((size_t)band * row_bytes > budget) {
 		const int64_t fit = (int64_t)(budget / row_bytes) - halo;
 		if (fit < 1)
 			return set_err(ctx, SG_ERR_SIZE, "the sequence does not fit the device even one row at a "
 					"time%s%.0ld", "", 0);
 		band = (int)std::min<int64_t>(fit, band);
+		/* several bands: two half-size buffers when a band of each still fits */
+		const int64_t fit2 = (int64_t)(budget / 2 / row_bytes) - halo;
+		if (d->method != SG_STACK_SUM && fit2 >= 1 && ctx->knobs.pull_overlap) {
+			band = (int)std::min<int64_t>(fit2, band);
+			nbuf = 2;
+		}
 	}
 	const int64_t rows_cap = std::min<int64_t>(band + halo, H);
-	HIPCHK(ensure(dv.frames, (size_t)rows_cap * W * C * N * sizeof(uint16_t)));
+	const size_t buf_elems = (size_t)rows_cap * W * C * N;
+	HIPCHK(ensure(dv.frames, nbuf * buf_elems * sizeof(uint16_t)));
 	HIPCHK(ensure(dv.out, (size_t)W * H * C * sizeof(uint16_t)));
 	const size_t chunk_elems = std::min<size_t>((size_t)rows_cap * W,
 			std::max<size_t>(1, SG_PULL_CHUNK_BYTES / ((size_t)W * sizeof(uint16_t))) * W);
@@ -1167,6 +1201,36 @@ static int pull_device(sg_ctx *ctx, int g, PullCall &pc, int B, int E, int nread
 	 * block); when that pixel lies above the band the core reports it (SG_ERR_WALK) and the
 	 * band is retried narrower with more rows above it resident (same total rows) */
 	int extra = 0;
+	struct Pending {
+		int slot, b, e, hi;
+	} pend = {-1, 0, 0, 0};
+	/* the band in flight: its counters, or a retry of it (the band start goes back to it) */
+	auto fold = [&](int &b) -> int {
+		uint64_t brej[3][2];
+		const int rc = stack_fold(ctx, dv, pend.slot, brej, nullptr, true);
+		const Pending pd = pend;
+		pend.slot = -1;
+		if (rc == SG_ERR_WALK && pd.hi < H - 1 && pd.e - pd.b > 1) {
+			extra = std::min(pd.e - pd.b - 1 + extra, extra ? 2 * extra : 4);
+			b = pd.b;
+			return 1;
+		}
+		if (rc)
+			return rc == SG_ERR_WALK ? SG_ERR_GENERIC : rc;
+		for (int c = 0; c < 3; c++) {
+			rej[c][0] += brej[c][0];
+			rej[c][1] += brej[c][1];
+		}
+		return SG_OK;
+	};
+	auto drain = [&]() {
+		if (pend.slot >= 0) {
+			(void)hipEventSynchronize(dv.cev[pend.slot][2]);
+			dv.pend[pend.slot] = false;
+			pend.slot = -1;
+		}
+	};
+	int buf = 0;
 	for (int b = B; b < E;) {
 		const int e = std::min(E, b + std::max(1, band - extra));
 		int lo = (int)std::max<int64_t>(0, (int64_t)b - pc.sy_max);
@@ -1175,16 +1239,46 @@ static int pull_device(sg_ctx *ctx, int g, PullCall &pc, int B, int E, int nread
 			lo = hi = std::min(b, H - 1);
 		const int nres = hi - lo + 1;
 		const size_t bplane = (size_t)nres * W;
-		if (int rc = pull_band(ctx, dv, pc, nreaders, (uint16_t *)dv.frames.p, lo, nres))
+		uint16_t *fb = (uint16_t *)dv.frames.p + (size_t)buf * buf_elems;
+		if (int rc = pull_band(ctx, dv, pc, nreaders, fb, lo, nres)) {
+			drain();
 			return rc;
+		}
+		if (pend.slot >= 0) {	/* the previous band stacked while this one was read */
+			int bb = b;
+			const int rc = fold(bb);
+			if (rc < 0)
+				return rc;
+			if (rc == 1) {	/* retry it narrower: this band's rows are read again afterwards */
+				b = bb;
+				continue;
+			}
+		}
 		sg_stack_desc bd = *d;
 		bd.resident_rows[0] = lo;
 		bd.resident_rows[1] = hi + 1;
 		const int sum_mode = d->method != SG_STACK_SUM || !banded ? SUM_WHOLE
 			: b == B ? SUM_FIRST_BAND : (!pc.multi && e == H) ? SUM_LAST_BAND : SUM_MID_BAND;
-		uint64_t brej[3][2];
 		/* base pointer biased so that memory row r of a frame plane sits at r*W */
-		const uint16_t *base = (const uint16_t *)dv.frames.p - (ptrdiff_t)lo * W;
+		const uint16_t *base = fb - (ptrdiff_t)lo * W;
+		if (nbuf == 2) {
+			int slot = -1;
+			if (int rc = stack_device_core(ctx, g, &bd, base, (int64_t)bplane * C, (int64_t)bplane,
+					(uint16_t *)dv.out.p, b, e, nullptr, nullptr, dv.stream, sum_mode, true, &slot)) {
+				drain();
+				return rc == SG_ERR_WALK ? SG_ERR_GENERIC : rc;
+			}
+			pend = {slot, b, e, hi};
+			buf ^= 1;
+			b = e;
+			if (b >= E) {	/* the last band: fold it here (a retry loops back) */
+				const int rc = fold(b);
+				if (rc < 0)
+					return rc;
+			}
+			continue;
+		}
+		uint64_t brej[3][2];
 		int rc = stack_device_core(ctx, g, &bd, base, (int64_t)bplane * C, (int64_t)bplane, (uint16_t *)dv.out.p, b,
 				e, brej, maxim, dv.stream, sum_mode);
 		if (rc == SG_ERR_WALK && hi < H - 1 && band - extra > 1) {

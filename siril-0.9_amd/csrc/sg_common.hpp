@@ -61,7 +61,9 @@ struct SgStackParams {
 	unsigned int *flag_count;
 	unsigned int *flag_list;		/* encoded (c*H + R)*W + x */
 	unsigned int flag_cap;
-	uint8_t *flag_map;			/* [C][H][W] class per pixel (chain walk) */
+	uint8_t *flag_map;			/* [C][H][W] class per pixel (chain walk): (epoch << 3) | class, an entry of
+						 * another epoch reads as SG_CLS_OK (the host clears the map when epochs wrap) */
+	unsigned int flag_epoch;		/* 1 .. 31, this call's */
 	/* histogram path, normalised SIGMA / WINSORIZED: a redo pixel whose only out-of-band
 	 * samples besides 0 / 65535 are the few the build captured (SGH_OVK) leaves its whole sorted
 	 * column at cmp_cols[slot][N] and its pixel at cmp_list[slot] (slot < cmp_cap), so the
@@ -79,6 +81,15 @@ struct SgStackParams {
 	uint32_t *sum_buf;			/* SUM: raw sums [C][H][W] */
 	unsigned int *maxim;			/* SUM: global max of sums */
 };
+
+/* pixel classes of this call (entries written by earlier calls read as SG_CLS_OK) */
+__device__ __forceinline__ int sg_flag_get(const SgStackParams &p, int64_t pix) {
+	const unsigned int v = p.flag_map[pix];
+	return (v >> 3) == p.flag_epoch ? (int)(v & 7u) : (int)SG_CLS_OK;
+}
+__device__ __forceinline__ void sg_flag_set(const SgStackParams &p, int64_t pix, int cls) {
+	p.flag_map[pix] = (uint8_t)((p.flag_epoch << 3) | (unsigned int)cls);
+}
 
 /* round_to_WORD, src/core/utils.c:68-74 */
 __device__ __forceinline__ uint16_t sg_round_to_WORD(double x) {

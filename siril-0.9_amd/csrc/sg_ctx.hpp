@@ -65,6 +65,10 @@ struct SgDevice {
 	 * counters added to acc_*) by the next call that needs it or by sg_stack_collect.
 	 * cev[slot] = {start, main kernel end, read-back done} */
 	hipEvent_t cev[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
+	unsigned long long *ctr_hd = nullptr;	/* ctr_h as the device sees it (k_ctr_finalize writes it) */
+	bool ctr_clean[2] = {false, false};	/* the slot's device counters are zero (k_ctr_finalize left them so) */
+	void *stage_d = nullptr;	/* stage_h as the device sees it (k_stage_copy reads it) */
+	int flag_epoch = 0;		/* flag_map epoch of the last call (0: clear the map first) */
 	bool pend[2] = {false, false};
 	unsigned long long pend_seq[2] = {0, 0}, seq = 0;
 	sg_stack_stats pstats[2];	/* a pending call's statistics (timings filled in when folded) */
@@ -107,6 +111,7 @@ struct SgKnobs {
 					 * >= 2: the compact list's capacity in pixels (tests of the overflow) */
 	int reduce1 = 0;		/* SG_REDUCE1: 1 = one pixel per lane, 2 = the per-lane pixel-pair kernel, in the SUM/MAX/MIN/MEAN reduce (A/B) */
 	long long host_budget = 0;	/* SG_HOST_BUDGET_BYTES: host-pull HBM budget (0 = 85 % of free HBM) */
+	int pull_overlap = 1;		/* SG_PULL_OVERLAP: 0 = host-pull bands read and stacked one after the other (A/B) */
 	int qsub_threads = 64;		/* SG_QSUB_THREADS: 64 measured best (scripts/gpu_qsub.sh) */
 	int qgrad_threads = 128;	/* SG_QGRAD_THREADS: 128 measured best (scripts/gpu_qgrad.sh) */
 	int reg_batch = 0;		/* SG_REG_BATCH: pairs per launch (0 = up to 2 GB of pair planes) */
@@ -129,6 +134,7 @@ struct SgKnobs {
 		redo_replay = sg_env_int("SG_REDO_REPLAY", 0, 1, 1);
 		hist_compact = sg_env_int("SG_HIST_COMPACT", 0, 1 << 30, 1);
 		reduce1 = sg_env_int("SG_REDUCE1", 0, 2, 0);
+		pull_overlap = sg_env_int("SG_PULL_OVERLAP", 0, 1, 1);
 		if (const char *e = getenv("SG_HOST_BUDGET_BYTES"))
 			host_budget = atoll(e) > 0 ? atoll(e) : 0;
 		const int qs = sg_env_int("SG_QSUB_THREADS", 64, 1024, 64);

@@ -830,7 +830,7 @@ k_stack_sorted(SgStackParams p, const unsigned int *__restrict__ list, const uns
 			if (cls == SG_CLS_OK) {
 				p.out[pix] = value;
 			} else {
-				p.flag_map[pix] = (uint8_t)cls;
+				sg_flag_set(p, pix, cls);
 				const unsigned int slot = atomicAdd(p.flag_count, 1u);
 				if (slot < p.flag_cap)
 					p.flag_list[slot] = (unsigned int)pix;
@@ -2217,7 +2217,7 @@ k_redo_to_literal(SgStackParams p, const unsigned int *__restrict__ list, const 
 		return;
 	for (unsigned int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
 		const unsigned int pix = list[i];
-		p.flag_map[pix] = SG_CLS_LITERAL;
+		sg_flag_set(p, pix, SG_CLS_LITERAL);
 		const unsigned int slot = atomicAdd(p.flag_count, 1u);
 		if (slot < p.flag_cap)
 			p.flag_list[slot] = pix;
@@ -2245,7 +2245,7 @@ k_stack_replay(SgStackParams p) {
 	for (unsigned int i = blockIdx.x * SG_REPLAY_WAVES + wv; i < nr + count; i += nw) {
 		const bool direct = i < nr;
 		const int64_t pix = direct ? p.rp_list[i] : p.flag_list[i - nr];
-		if (!direct && p.flag_map[pix] != SG_CLS_LITERAL)
+		if (!direct && sg_flag_get(p, pix) != SG_CLS_LITERAL)
 			continue;
 		const int x = (int)(pix % p.W);
 		const int64_t cr = pix / p.W;
@@ -2294,7 +2294,7 @@ k_stack_replay(SgStackParams p) {
 #endif
 		if (!ok) {
 			if (direct && lane == 0) {	/* to the literal kernel, as k_redo_to_literal queues */
-				p.flag_map[pix] = SG_CLS_LITERAL;
+				sg_flag_set(p, pix, SG_CLS_LITERAL);
 				const unsigned int slot = atomicAdd(p.flag_count, 1u);
 				if (slot < p.flag_cap)
 					p.flag_list[slot] = (unsigned int)pix;
@@ -2303,7 +2303,7 @@ k_stack_replay(SgStackParams p) {
 		}
 		if (lane == 0) {
 			p.out[pix] = v;
-			p.flag_map[pix] = SG_CLS_DONE;
+			sg_flag_set(p, pix, SG_CLS_DONE);
 			unsigned long long *sh = p.rej + ((size_t)(i % SG_REJ_SHARDS) * 6 + c * 2);
 			if (rl)
 				atomicAdd(sh, (unsigned long long)rl);
@@ -2337,7 +2337,7 @@ k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *s
 	}
 	for (unsigned int i = gid; i < count; i += nthreads) {
 		const int64_t pix = p.flag_list[i];
-		const int cls = p.flag_map[pix];
+		const int cls = sg_flag_get(p, pix);
 		if (cls != (phase == 1 ? SG_CLS_LITERAL : SG_CLS_CHAIN))
 			continue;	/* SG_CLS_DONE: finished by k_stack_replay */
 		uint32_t crej[2] = {0, 0};
@@ -2346,7 +2346,7 @@ k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *s
 			gather_stack(p, pix, stack);
 			shellsort_u16(stack, p.N);
 			p.out[pix] = (uint16_t)lit_median(stack, p.N);
-			p.flag_map[pix] = SG_CLS_DONE;
+			sg_flag_set(p, pix, SG_CLS_DONE);
 			continue;
 		}
 		if (phase == 1) {
@@ -2358,7 +2358,7 @@ k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *s
 			bool fault = false;
 			while (q >= 0) {
 				if (chain_in_band(p, q)) {
-					if (p.flag_map[q] != SG_CLS_CHAIN && p.flag_map[q] != SG_CLS_CHAIN_DONE)
+					if (sg_flag_get(p, q) != SG_CLS_CHAIN && sg_flag_get(p, q) != SG_CLS_CHAIN_DONE)
 						break;
 				} else {
 					if (!chain_resident(p, q)) {
@@ -2408,19 +2408,67 @@ k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *s
 		if (p.rejection == 3 && fbrk == 2)
 			*p.loop_fault = 1u;
 		if (phase == 1 && fbrk == 1 && p.N > 4) {
-			p.flag_map[pix] = SG_CLS_CHAIN;
+			sg_flag_set(p, pix, SG_CLS_CHAIN);
 			continue;
 		}
 		p.out[pix] = v;
 		/* finished: a second tail launch (after the host's late redo launch) skips it; a phase-2
 		 * pixel stays a chain link for the other walks of this phase */
-		p.flag_map[pix] = phase == 1 ? SG_CLS_DONE : SG_CLS_CHAIN_DONE;
+		sg_flag_set(p, pix, phase == 1 ? SG_CLS_DONE : SG_CLS_CHAIN_DONE);
 		const int c = (int)(pix / ((int64_t)p.W * p.H));
 		unsigned long long *sh = p.rej + ((size_t)(i % SG_REJ_SHARDS) * 6 + c * 2);
 		if (crej[0])
 			atomicAdd(sh, (unsigned long long)crej[0]);
 		if (crej[1])
 			atomicAdd(sh + 1, (unsigned long long)crej[1]);
+	}
+}
+
+/* ----------------------------------------------------------------------------------
+ * call plumbing without DMA: a stack call's inputs come from its pinned (host-mapped) staging
+ * block and its counters go back into a host-mapped slot through these two kernels (an SDMA
+ * copy's start-up cost ~20 us each way per call, profiles/r05b_band8)
+ * ---------------------------------------------------------------------------------- */
+__global__ void __launch_bounds__(256)
+k_stage_copy(uint4 *__restrict__ dst, const uint4 *__restrict__ src, unsigned int n16) {
+	for (unsigned int i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256)
+		dst[i] = src[i];
+}
+
+/* host slot: rejection sums [3][2] u64 at 0, the flag block (flag / walk-fault / redo / compact
+ * counts, loop fault, the SUM maximum at word 16) at byte 64; the device shards and flag words
+ * 0..15 are zeroed for the slot's next call (the SUM maximum stays: a streamed SUM keeps it) */
+__global__ void __launch_bounds__(256)
+k_ctr_finalize(unsigned long long *__restrict__ ctr, unsigned long long *__restrict__ host) {
+	__shared__ unsigned long long part[6][256];
+	const int t = threadIdx.x;
+	unsigned long long a[6] = {0, 0, 0, 0, 0, 0};
+	for (int k = t; k < SG_REJ_SHARDS; k += 256)
+#pragma unroll
+		for (int j = 0; j < 6; j++) {
+			a[j] += ctr[(size_t)k * 6 + j];
+			ctr[(size_t)k * 6 + j] = 0ull;
+		}
+#pragma unroll
+	for (int j = 0; j < 6; j++)
+		part[j][t] = a[j];
+	__syncthreads();
+	for (int o = 128; o > 0; o >>= 1) {
+		if (t < o)
+#pragma unroll
+			for (int j = 0; j < 6; j++)
+				part[j][t] += part[j][t + o];
+		__syncthreads();
+	}
+	unsigned int *fl = (unsigned int *)(ctr + (size_t)SG_REJ_SHARDS * 6);
+	unsigned int *hf = (unsigned int *)(host + 8);
+	if (t < 6)
+		host[t] = part[t][0];
+	if (t < 32) {
+		const unsigned int v = fl[t];
+		hf[t] = v;
+		if (t < 16)
+			fl[t] = 0u;
 	}
 }
 

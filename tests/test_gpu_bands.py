@@ -200,6 +200,43 @@ def test_host_pull_streams_row_bands(gpu_ctx, method, rejection, band_rows):
         assert maxim == mref
 
 
+def _with_env(env, fn):
+    """fn(ctx) on a context created under the given knobs (read at sg_init)"""
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        with sg.Context() as ctx:
+            return fn(ctx)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("method,rejection", CASES)
+@pytest.mark.parametrize("overlap", [1, 0])
+def test_host_pull_overlapped_bands(gpu_ctx, method, rejection, overlap):
+    """a budget of two bands of 4 rows (+ halo): band k + 1 is read into the second frame buffer
+    while band k stacks (SG_PULL_OVERLAP=1, the default) over >= 3 bands; the image and the
+    counters equal the oracle's, as with the bands read and stacked one after the other"""
+    N, C, H, W = 24, 2, 40, 96
+    frames = orc.synth(N, C, H, W, seed=43, maxshift=4)
+    sx, sy = orc.synth_shifts(N, seed=43, maxshift=4)
+    sig = REJ[rejection]
+    ref, rej_ref = _oracle(frames, method, rejection, sig, sx, sy, 4)
+    halo = 0 if method == sg.MEDIAN else int(sy.max() - sy.min())
+    budget = N * C * W * 2 * 2 * (4 + halo)
+    desc, keep = sg.make_desc(method, N, W, H, C, rejection=rejection, sig=sig, shiftx=sx, shifty=sy,
+                              max_thread=4, max_number_of_rows=H)
+    rc, out, rej, _, err = _with_env({"SG_HOST_BUDGET_BYTES": budget, "SG_PULL_OVERLAP": overlap},
+                                     lambda c: c.stack_host(desc, frames) + (c.error(),))
+    assert rc == 0, err
+    assert_same(out, ref, f"overlapped host bands method={method} rej={rejection} overlap={overlap}")
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+
+
 def test_host_pull_budget_too_small(gpu_ctx):
     N, C, H, W = 8, 1, 16, 32
     frames = orc.synth(N, C, H, W, seed=2, maxshift=3)

@@ -167,6 +167,23 @@ int main(int argc, char **argv) {
 	(void)hipMemcpy(c1, h, sizeof h, hipMemcpyHostToDevice);
 	hipLaunchKernelGGL(k_fill, dim3(8192), dim3(256), 0, 0, (unsigned *)d, (size_t)NF * FRAMEB / 4);
 	(void)hipDeviceSynchronize();
+	const int mode = argc > 2 ? atoi(argv[2]) : 0;
+	if (mode == 5) {	/* round 5: 512-B segments at 3 or 4 workgroups per CU */
+		for (int rep = 0; rep < 2; rep++) {
+			run<256, 4, 2, false>(d, c1, o, 4, 4, 34560);		/* today's geometry */
+			run<512, 4, 2, false, 8>(d, c1, o, 4, 3, 50000);
+			run<512, 4, 2, false>(d, c1, o, 4, 3, 50000);
+			run<512, 4, 2, false, 8>(d, c1, o, 8, 3, 50000);
+			run<512, 4, 2, false>(d, c1, o, 8, 3, 50000);
+			run<512, 4, 2, false, 8>(d, c1, o, 4, 4, 36000);
+			run<512, 4, 2, false>(d, c1, o, 4, 4, 36000);
+			run<512, 4, 2, false, 8>(d, c1, o, 8, 2, 70000);
+			run<512, 4, 2, false, 8>(d, c1, o, 4, 2, 70000);
+			run<1024, 4, 2, false, 8>(d, c1, o, 8, 2, 70000);
+			run<1024, 4, 2, false, 8>(d, c1, o, 4, 3, 50000);
+		}
+		return 0;
+	}
 	for (int rep = 0; rep < 2; rep++) {
 		run<256, 4, 2, false>(d, c1, o, 4, 4, 34560);
 		run<512, 4, 2, false>(d, c1, o, 8, 2, 70000);
