@@ -15,6 +15,7 @@
 #   sq=NAME:CTRS[:ARGS]         one rocprofv3 --pmc pass with counters CTRS ('+' between them,
 #                               within the per-block slot limits) -> NAME.txt (pmc_sum.py)
 #   py=NAME:SCRIPT[:ARGS]       python SCRIPT ARGS -> NAME.log
+#   bin=NAME:EXE[:ARGS]         a built probe (tools/), 300 s limit -> NAME.log
 #   dist=NAME:NPROC[:ARGS]      bench.py under torchrun with NPROC ranks on this one GPU
 #                               (SG_BENCH_REHEARSE=1: gloo collectives; a rehearsal of the multi-GPU flow)
 # ARGS use ',' between words (bench=cfg1:--workload,register-mean).
@@ -90,6 +91,10 @@ for step in "$@"; do
       name=${spec%%:*}; rest=${spec#*:}; script=${rest%%:*}; args=""; [ "$script" != "$rest" ] && args=${rest#*:}
       timeout -k 10 900 python -u "$script" ${args//,/ } > "$O/$name.log" 2>&1 || fail "py $name" "$O/$name.log"
       tail -3 "$O/$name.log" ;;
+    bin)
+      name=${spec%%:*}; rest=${spec#*:}; exe=${rest%%:*}; args=""; [ "$exe" != "$rest" ] && args=${rest#*:}
+      timeout -k 10 300 "$exe" ${args//,/ } > "$O/$name.log" 2>&1 || fail "bin $name" "$O/$name.log"
+      tail -40 "$O/$name.log" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

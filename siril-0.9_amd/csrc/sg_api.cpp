@@ -52,6 +52,7 @@ __global__ void k_synth_fill(uint16_t *frames, int first_frame, int nframes, int
 
 __global__ void k_flip_rows(const uint16_t *src, uint16_t *dst, int W, int rows);
 __global__ void k_stage_copy(uint4 *dst, const uint4 *src, unsigned int n16);
+__global__ void k_linfit_tables(double *tab, int nmax);
 __global__ void k_ctr_finalize(unsigned long long *ctr, unsigned long long *host);
 /* host-pull readers per device and the bytes of one region read (two pinned + two device
  * staging buffers of this size per reader) */
@@ -111,7 +112,7 @@ extern "C" void sg_shutdown(sg_ctx *ctx) {
 		(void)hipStreamSynchronize(d.stream);
 		SgBuf *bufs[] = {&d.flag_list, &d.flag_map, &d.sum_buf, &d.scratch, &d.frames, &d.out, &d.reg_sel, &d.reg_spec,
 			&d.reg_work, &d.reg_tw, &d.reg_tw32, &d.reg_best, &d.reg_qbuf, &d.reg_qacc, &d.redo, &d.zeros,
-			&d.cmp_cols, &d.cmp_list, &d.io_raw, &d.io_bad, &d.warp_tab, &d.stats_buf, &d.inb, &d.ctr};
+			&d.cmp_cols, &d.cmp_list, &d.io_raw, &d.io_bad, &d.warp_tab, &d.stats_buf, &d.inb, &d.ctr, &d.lin_tab};
 		for (SgBuf *b : bufs)
 			if (b->p)
 				(void)hipFree(b->p);
@@ -692,12 +693,13 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		 * 16-bit halves) */
 		const bool hist = d->kernel_path != SG_PATH_SORTED && N >= 16 && N <= 65535 && hist_addr_ok &&
 			(d->method == SG_STACK_MEDIAN || (d->method == SG_STACK_MEAN && (d->rejection == SG_SIGMA ||
-					d->rejection == SG_WINSORIZED || d->rejection == SG_PERCENTILE)));
+					d->rejection == SG_WINSORIZED || d->rejection == SG_PERCENTILE ||
+					(d->rejection == SG_SIGMEDIAN && ctx->knobs.hist_sigmedian))));
 		/* beyond the sorted kernel's 1024 frames only the histogram path runs; its redo pixels
 		 * all go to the replay / literal kernels (they take any N) */
 		if (!nreg && !hist)
 			return set_err(ctx, SG_ERR_SIZE, "this rejection supports up to 1024 frames%s (%ld); SIGMA, "
-					"WINSORIZED, PERCENTILE and median stacks take up to 65535", "", N);
+					"WINSORIZED, PERCENTILE, SIGMEDIAN and median stacks take up to 65535", "", N);
 		const size_t npix_launch = (size_t)C * nrows * W;
 		HIPCHK(ensure(dv.flag_list, sizeof(unsigned int) * npix_launch));
 		{
@@ -745,6 +747,12 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		if (int rc = flush_inputs())
 			return rc;
 
+		if (d->method == SG_STACK_MEAN && p.rejection == SG_LINEARFIT) {
+			HIPCHK(ensure(dv.lin_tab, sizeof(double) * 2 * ((size_t)N + 1)));
+			hipLaunchKernelGGL(k_linfit_tables, dim3((N + 64) / 64), dim3(64), 0, s, (double *)dv.lin_tab.p, N);
+			HIPCHK(hipGetLastError());
+			p.linfit_tab = (const double *)dv.lin_tab.p;
+		}
 		const int ntx = (W + SG_TILE_W - 1) / SG_TILE_W;
 		const size_t nblk = (size_t)ntx * nrows * C;
 		/* LINEARFIT: + one rejected[] bit per frame and pixel of the tile (reject_linearfit) */
@@ -775,9 +783,9 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 						(size_t)prop.maxSharedMemoryPerMultiProcessor, (size_t)prop.sharedMemPerBlock, ctx->knobs.hist_ldspad);
 			}
 			const size_t lds_pad = (size_t)ctx->knobs.hist_ldspad;
-			/* REJ: 2 SIGMA, 4 WINSORIZED, 1 PERCENTILE, 8 stack_median */
+			/* REJ: 2 SIGMA, 4 WINSORIZED, 1 PERCENTILE, 3 SIGMEDIAN, 8 stack_median */
 			const int rj = d->method == SG_STACK_MEDIAN ? 8 : p.rejection == SG_WINSORIZED ? 4 :
-				p.rejection == SG_PERCENTILE ? 1 : 2;
+				p.rejection == SG_PERCENTILE ? 1 : p.rejection == SG_SIGMEDIAN ? 3 : 2;
 			/* normalised SIGMA / WINSORIZED: redo pixels whose samples the tile fully knows leave
 			 * their sorted columns for the sorted kernel (sgh_compact), up to a 384 MiB buffer */
 			const bool compact = norm != 0 && (rj == 2 || rj == 4) && nreg && ctx->knobs.hist_compact;
@@ -792,7 +800,8 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 				p.cmp_cap = (unsigned int)cap;
 			}
 			const dim3 hg((unsigned)nblk_h), hb((unsigned)sgh_block_threads(ni, rj));
-			switch ((rj == 4 ? 10 : rj == 1 ? 20 : rj == 8 ? 30 : 0) + norm + 100 * (rj == 1 || rj == 8 ? 1 : ni)) {
+			switch ((rj == 4 ? 10 : rj == 1 ? 20 : rj == 8 ? 30 : rj == 3 ? 40 : 0) + norm +
+					100 * (rj == 1 || rj == 8 || rj == 3 ? 1 : ni)) {
 			case 100: hipLaunchKernelGGL((k_stack_hist<2, 0, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 101: hipLaunchKernelGGL((k_stack_hist<2, 1, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 102: hipLaunchKernelGGL((k_stack_hist<2, 2, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
@@ -809,6 +818,10 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			case 131: hipLaunchKernelGGL((k_stack_hist<8, 1, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 132: hipLaunchKernelGGL((k_stack_hist<8, 2, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 133: hipLaunchKernelGGL((k_stack_hist<8, 3, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			case 140: hipLaunchKernelGGL((k_stack_hist<3, 0, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			case 141: hipLaunchKernelGGL((k_stack_hist<3, 1, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			case 142: hipLaunchKernelGGL((k_stack_hist<3, 2, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
+			case 143: hipLaunchKernelGGL((k_stack_hist<3, 3, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 200: hipLaunchKernelGGL((k_stack_hist<2, 0, 2>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			case 210: hipLaunchKernelGGL((k_stack_hist<4, 0, 2>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;
 			default: return set_err(ctx, SG_ERR_GENERIC, "no histogram kernel for this case%s%.0ld", "", 0);

@@ -78,6 +78,7 @@ struct SgStackParams {
 	 * rp_maxn (null: only the flag list) */
 	const unsigned int *rp_list, *rp_count;
 	unsigned int rp_maxn;
+	const double *linfit_tab;		/* LINEARFIT: gsl_fit_linear's m_x, m_dx2 per N (k_linfit_tables) */
 	uint32_t *sum_buf;			/* SUM: raw sums [C][H][W] */
 	unsigned int *maxim;			/* SUM: global max of sums */
 };

@@ -41,6 +41,7 @@ struct SgDevice {
 	/* registration workspaces (sg_register.hip) */
 	SgBuf reg_sel, reg_spec, reg_work, reg_tw, reg_tw32, reg_best, reg_qbuf, reg_qacc;
 	SgBuf redo;	/* redo list of the histogram stacking path */
+	SgBuf lin_tab;	/* LINEARFIT: per-N x recurrences (k_linfit_tables) */
 	SgBuf cmp_cols, cmp_list;	/* compact redo columns / pixels of normalised histogram stacks */
 	/* registration: the quality estimate runs on its own stream beside the FFT passes; its
 	 * sums come back into a pinned block, aux_ev marks them landed */
@@ -111,6 +112,7 @@ struct SgKnobs {
 					 * >= 2: the compact list's capacity in pixels (tests of the overflow) */
 	int reduce1 = 0;		/* SG_REDUCE1: 1 = one pixel per lane, 2 = the per-lane pixel-pair kernel, in the SUM/MAX/MIN/MEAN reduce (A/B) */
 	long long host_budget = 0;	/* SG_HOST_BUDGET_BYTES: host-pull HBM budget (0 = 85 % of free HBM) */
+	int hist_sigmedian = 1;		/* SG_HIST_SIGMEDIAN: 0 = SIGMEDIAN on the sorted kernel only (A/B) */
 	int pull_overlap = 1;		/* SG_PULL_OVERLAP: 0 = host-pull bands read and stacked one after the other (A/B) */
 	int qsub_threads = 64;		/* SG_QSUB_THREADS: 64 measured best (scripts/gpu_qsub.sh) */
 	int qgrad_threads = 128;	/* SG_QGRAD_THREADS: 128 measured best (scripts/gpu_qgrad.sh) */
@@ -135,6 +137,7 @@ struct SgKnobs {
 		hist_compact = sg_env_int("SG_HIST_COMPACT", 0, 1 << 30, 1);
 		reduce1 = sg_env_int("SG_REDUCE1", 0, 2, 0);
 		pull_overlap = sg_env_int("SG_PULL_OVERLAP", 0, 1, 1);
+		hist_sigmedian = sg_env_int("SG_HIST_SIGMEDIAN", 0, 1, 1);
 		if (const char *e = getenv("SG_HOST_BUDGET_BYTES"))
 			host_budget = atoll(e) > 0 ? atoll(e) : 0;
 		const int qs = sg_env_int("SG_QSUB_THREADS", 64, 1024, 64);

@@ -385,27 +385,72 @@ __device__ int reject_sigmedian(const SgCol &A, SgRejState &st, double sl, doubl
 	return SG_CLS_OK;
 }
 
-/* LINEARFIT (:1750-1784) literally on the lane's sorted column in LDS (element e at
- * col[e * SG_STAGE_STRIDE]): gsl_fit_linear's double recurrences, the mean absolute residual,
- * line_clipping with rejected[] by position (one bit per entry in LDS, rb[(j / 32) * 64]; the
- * entries after the `N - r <= 4` break keep this pixel's previous pass) and the order-preserving
- * removal, compacting the column in place (a sorted array stays sorted, so quicksort_s is the
- * identity).  The double operations and their order are k_stack_literal's, so the result is
- * bit-identical; a first pass that breaks early needs the previous pixel's stale entries and
- * goes to the literal kernel. */
-__device__ int reject_linearfit(uint16_t *col, uint32_t *rb, int N0, double sl, double sh, SgRejState &st) {
+/* gsl_fit_linear's x-only recurrences for x = 0 .. N - 1: m_x (the mean) and m_dx2 depend on N
+ * alone, so they are tabulated once per call (tab[2 N], tab[2 N + 1]) with the same double
+ * operations in the same order (GSL fit/linear.c, as k_stack_literal runs them) */
+__global__ void __launch_bounds__(64)
+k_linfit_tables(double *__restrict__ tab, int nmax) {
+	const int n = blockIdx.x * 64 + threadIdx.x;
+	if (n < 1 || n > nmax)
+		return;
+	double m_x = 0.0, m_dx2 = 0.0;
+	for (int i = 0; i < n; i++)
+		m_x += ((double)i - m_x) / (i + 1.0);
+	for (int i = 0; i < n; i++) {
+		const double dx = (double)i - m_x;
+		m_dx2 += (dx * dx - m_dx2) / (i + 1.0);
+	}
+	tab[2 * n] = m_x;
+	tab[2 * n + 1] = m_dx2;
+}
+
+/* the smallest double t with (t / sigma) > s (line_clipping's test, :1174-1181): the rounded
+ * quotient is monotone in t for sigma > 0, so the test of every frame is one compare against this
+ * threshold instead of a division.  Returns false (the caller divides) outside the tame range
+ * where the search is known to end within a few ulps. */
+__device__ __forceinline__ bool sg_div_gt_threshold(double sigma, double s, double &thr) {
+	if (!(sigma > 1e-200 && sigma < 1e200) || !(fabs(s) < 1e100) || s != s)
+		return false;
+	double c = s * sigma;
+	if (!(fabs(c) < 1e250))
+		return false;
+	int guard = 0;
+	while ((c / sigma) > s) {	/* down to a t that fails */
+		c = nextafter(c, -HUGE_VAL);
+		if (++guard > 64)
+			return false;
+	}
+	while (!((c / sigma) > s)) {	/* up to the first t that passes */
+		c = nextafter(c, HUGE_VAL);
+		if (++guard > 128)
+			return false;
+	}
+	thr = c;
+	return true;
+}
+
+/* LINEARFIT (:1750-1784) on the lane's sorted column in LDS (element e at col[e * SG_STAGE_STRIDE]),
+ * bit-identical to the literal replay: gsl_fit_linear's y recurrences (m_y, m_dxdy) in double per
+ * pixel, its x-only ones from the per-N table (tab), the mean absolute residual, line_clipping with
+ * rejected[] by position (one bit per entry in LDS, rb[(j / 32) * 64], written a word at a time;
+ * the entries after the `N - r <= 4` break keep this pixel's previous pass), its two divisions
+ * replaced by thresholds (sg_div_gt_threshold), and the order-preserving removal as one compaction
+ * (the reference's loop visits old index j = 0 .. N - 1 and drops the flagged ones, :1767-1773; a
+ * sorted array stays sorted, so quicksort_s is the identity).  A first pass that breaks early
+ * needs the previous pixel's stale entries and goes to the literal kernel. */
+__device__ int reject_linearfit(uint16_t *col, uint32_t *rb, int N0, double sl, double sh, SgRejState &st,
+		const double *__restrict__ tab) {
 	auto at = [&](int e) -> uint32_t { return col[e * SG_STAGE_STRIDE]; };
 	int N = N0, r = 0, n, pass = 0;
 	do {
-		double m_x = 0, m_y = 0, m_dx2 = 0, m_dxdy = 0;
-		for (int i = 0; i < N; i++) {
-			m_x += ((double)i - m_x) / (i + 1.0);
+		const double m_x = tab[2 * N], m_dx2 = tab[2 * N + 1];
+		double m_y = 0;
+		for (int i = 0; i < N; i++)
 			m_y += ((double)at(i) - m_y) / (i + 1.0);
-		}
+		double m_dxdy = 0;
 		for (int i = 0; i < N; i++) {
 			const double dx = (double)i - m_x;
 			const double dy = (double)at(i) - m_y;
-			m_dx2 += (dx * dx - m_dx2) / (i + 1.0);
 			m_dxdy += (dx * dy - m_dxdy) / (i + 1.0);
 		}
 		const double a = m_dxdy / m_dx2;
@@ -414,33 +459,49 @@ __device__ int reject_linearfit(uint16_t *col, uint32_t *rb, int N0, double sl, 
 		for (int f = 0; f < N; f++)
 			sigma += (fabs((double)at(f) - (a * (double)f + b)));
 		sigma /= (double)N;
+		double tlo = 0.0, thi = 0.0;
+		const bool fast = sg_div_gt_threshold(sigma, sl, tlo) && sg_div_gt_threshold(sigma, sh, thi);
 		n = 0;
 		int frame;
+		uint32_t bits = 0;
 		for (frame = 0; frame < N; frame++) {
+			const double y = (double)at(frame), af = a * (double)frame;
 			int v = 0;
-			if (((a * (double)frame + b - (double)at(frame)) / sigma) > sl) {
+			const double t1 = af + b - y, t2 = y - af - b;
+			if (fast ? t1 >= tlo : (t1 / sigma) > sl) {
 				st.rlo++;
 				v = -1;
-			} else if ((((double)at(frame) - a * (double)frame - b) / sigma) > sh) {
+			} else if (fast ? t2 >= thi : (t2 / sigma) > sh) {
 				st.rhi++;
 				v = 1;
 			}
-			uint32_t &w = rb[(frame >> 5) * 64];
-			w = v ? (w | (1u << (frame & 31))) : (w & ~(1u << (frame & 31)));
-			if (v != 0)
+			if (v != 0) {
+				bits |= 1u << (frame & 31);
 				r++;
+			}
+			if ((frame & 31) == 31) {
+				rb[(frame >> 5) * 64] = bits;
+				bits = 0;
+			}
 			if (N - r <= 4)
 				break;
 		}
+		{	/* the word holding the last entry written: its entries above it keep their old bits */
+			const int last = frame < N ? frame : N - 1;
+			if ((last & 31) != 31) {
+				const uint32_t m = (2u << (last & 31)) - 1u;
+				uint32_t &w = rb[(last >> 5) * 64];
+				w = (w & ~m) | (bits & m);
+			}
+		}
 		if (pass++ == 0 && frame < N - 1)
 			return SG_CLS_LITERAL;
-		for (int f = 0, j = 0; f < N - n; f++, j++) {
-			if ((rb[(j >> 5) * 64] >> (j & 31)) & 1u) {
-				for (int k = f; k < N - n - 1; k++)
-					col[k * SG_STAGE_STRIDE] = col[(k + 1) * SG_STAGE_STRIDE];
-				f--;
+		int w = 0;
+		for (int j = 0; j < N; j++) {
+			if ((rb[(j >> 5) * 64] >> (j & 31)) & 1u)
 				n++;
-			}
+			else
+				col[(w++) * SG_STAGE_STRIDE] = col[j * SG_STAGE_STRIDE];
 		}
 		N -= n;
 	} while (n > 0 && N > 3);
@@ -812,7 +873,7 @@ k_stack_sorted(SgStackParams p, const unsigned int *__restrict__ list, const uns
 					break;
 				case 5:
 					cls = reject_linearfit(stage + sl, (uint32_t *)(stage + (size_t)N * SG_STAGE_STRIDE) + sl, N,
-							p.sig0, p.sig1, st);
+							p.sig0, p.sig1, st, p.linfit_tab);
 					break;
 				case 0:
 					break;

@@ -963,6 +963,178 @@ __device__ __forceinline__ SghM sgh_M_le(const SghPix &P, int v) {
 	return sgh_q_moments(P, q);
 }
 
+/* ------------------------------------------------------------------------------------
+ * SIGMEDIAN (:1696-1709 + sigma_clipping :1148-1161) on the histogram, decision for decision
+ * reject_sigmedian() of the sorted path: a clipped sample is replaced by round_to_WORD(median)
+ * and N stays, so the pixel's multiset is the window of samples never replaced - the values in
+ * [A, B], moments M(A - 1), M(B) as in SIGMA - plus up to SGH_SMG groups of equal replacement
+ * values (gc = 0: a free slot; the groups are unordered, their ranks are counted).  sigma comes
+ * from the exact moments of the whole multiset, decisions keep the rounding band, a decision
+ * inside it, a fifth group, a pass that replaces samples by the values they hold (the
+ * reference's loop never ends there) or 4096 passes go to the redo list (the sorted path takes
+ * them and reports what the reference would do).  One lane per pixel.
+ * ------------------------------------------------------------------------------------ */
+#define SGH_SMG 4
+__device__ __forceinline__ double sgh_sigma_num(long long S, unsigned long long SS, int n, bool &e0) {
+	/* n SS - S^2 in 128 bits (relative moments: S^2 passes 2^63 for large N), then as sgh_sigma_fast */
+	const __int128 num = (__int128)n * (__int128)SS - (__int128)S * (__int128)S;
+	e0 = num == 0;
+	if (num <= 0)
+		return 0.0;
+	const double nd = (double)num;
+	const double x = nd * ((double)n * (double)(n - 1));
+	const double y = __builtin_amdgcn_rsq(x);
+	double h = 0.5 * y, s = x * y;
+	double r = fma(-s, h, 0.5);
+	s = fma(s, r, s);
+	h = fma(h, r, h);
+	r = fma(-s, h, 0.5);
+	h = fma(h, r, h);
+	return (nd + nd) * h;
+}
+__device__ int sgh_sigmedian(const SghPix &P, int N, double sl, double sh, uint16_t *value, uint32_t *rlo_out,
+		uint32_t *rhi_out) {
+	int A = 0, B = 65535;
+	SghM MA = {0, 0, 0}, MB = P.T;
+	uint32_t gv[SGH_SMG];
+	int gc[SGH_SMG];
+#pragma unroll
+	for (int k = 0; k < SGH_SMG; k++) {
+		gv[k] = 0u;
+		gc[k] = 0;
+	}
+	long long S = P.T.s;			/* the multiset's moments, values relative to lo */
+	unsigned long long SS = P.T.ss;
+	uint32_t rlo = 0, rhi = 0;
+	int iter = 0, n;
+	/* window samples with value <= v (v integer) */
+	auto wle = [&](int v) -> int {
+		int c = sgh_cnt_le(P, v);
+		c = c < MA.c ? MA.c : (c > MB.c ? MB.c : c);
+		return c - MA.c;
+	};
+	/* multiset elements < t / <= t (t real) */
+	auto cnt_lt = [&](double t) -> int {
+		double cv = ceil(t) - 1.0;
+		cv = cv < -1.0 ? -1.0 : (cv > 65535.0 ? 65535.0 : cv);
+		int c = wle((int)cv);
+#pragma unroll
+		for (int k = 0; k < SGH_SMG; k++)
+			c += (gc[k] && (double)gv[k] < t) ? gc[k] : 0;
+		return c;
+	};
+	auto cnt_le = [&](double t) -> int {
+		double cv = floor(t);
+		cv = cv < -1.0 ? -1.0 : (cv > 65535.0 ? 65535.0 : cv);
+		int c = wle((int)cv);
+#pragma unroll
+		for (int k = 0; k < SGH_SMG; k++)
+			c += (gc[k] && (double)gv[k] <= t) ? gc[k] : 0;
+		return c;
+	};
+	do {
+		if (++iter > 4096)
+			return SG_CLS_LITERAL;
+		bool e0;
+		const double sigma = sgh_sigma_num(S, SS, N, e0);
+		/* median ranks: group k's copies start at rank st[k] = window samples < gv_k + the group
+		 * copies of smaller values; a rank in no group's run is a window rank */
+		int st[SGH_SMG];
+#pragma unroll
+		for (int k = 0; k < SGH_SMG; k++) {
+			int b = 0;
+#pragma unroll
+			for (int j = 0; j < SGH_SMG; j++)
+				b += (j != k && gc[j] && gv[j] < gv[k]) ? gc[j] : 0;
+			st[k] = gc[k] ? wle((int)gv[k] - 1) + b : 0;
+		}
+		auto at = [&](int r) -> int {
+			int before = 0, gval = -1;
+#pragma unroll
+			for (int k = 0; k < SGH_SMG; k++) {
+				if (gc[k]) {
+					if (r >= st[k] && r < st[k] + gc[k])
+						gval = (int)gv[k];
+					before += (st[k] + gc[k] <= r) ? gc[k] : 0;
+				}
+			}
+			return gval >= 0 ? gval : sgh_value_at1(P, MA.c + (r - before));
+		};
+		const int g1 = (N - 1) / 2, g2 = N / 2;
+		const int m1 = at(g1), m2 = g1 == g2 ? m1 : at(g2);
+		const double median = g1 == g2 ? (double)m1 : (double)(m1 + m2) / 2.0;
+		const double tl = sl * sigma, th = sh * sigma;
+		const double blo = median - tl, bhi = median + th;
+		double tlo = blo, thi = bhi;
+		if (!e0) {
+			const double tol = SGH_BAND * (fabs(median) + fabs(tl) + fabs(th) + 1.0);
+			if (cnt_lt(blo - tol) != cnt_le(blo + tol) || cnt_lt(bhi - tol) != cnt_le(bhi + tol))
+				return SG_CLS_LITERAL;
+			tlo = blo - tol;	/* no element lies within tol of either threshold */
+			thi = bhi + tol;
+		}
+		const int L = cnt_lt(tlo), H = N - cnt_le(thi);
+		if (L + H > N)
+			return SG_CLS_LITERAL;	/* negative sigma factors: the else-if order matters */
+		n = L + H;
+		rlo += (uint32_t)L;
+		rhi += (uint32_t)H;
+		if (!n)
+			break;
+		/* the window's replaced ends, then the replaced groups */
+		int A2 = sgh_ceil_clamp(tlo), B2 = sgh_floor_clamp(thi);
+		A2 = A2 < A ? A : A2;
+		B2 = B2 > B ? B : B2;
+		SghM MA2 = A2 > A ? sgh_M_le(P, A2 - 1) : MA;
+		SghM MB2 = B2 < B ? sgh_M_le(P, B2) : MB;
+		if (MB2.c < MA2.c)	/* the whole window replaced */
+			MB2 = MA2;
+		long long rs = (MA2.s - MA.s) + (MB.s - MB2.s);
+		unsigned long long rss = (MA2.ss - MA.ss) + (MB.ss - MB2.ss);
+#pragma unroll
+		for (int k = 0; k < SGH_SMG; k++) {
+			if (gc[k] && ((double)gv[k] < tlo || (double)gv[k] > thi)) {
+				const long long u = (long long)gv[k] - P.lo;
+				rs += u * gc[k];
+				rss += (unsigned long long)(u * u) * (unsigned long long)gc[k];
+				gc[k] = 0;
+			}
+		}
+		const uint32_t mw = sg_round_to_WORD(median);
+		const long long um = (long long)mw - P.lo;
+		if (rs == um * n && rss == (unsigned long long)(um * um) * (unsigned long long)n)
+			return SG_CLS_LITERAL;	/* the next pass sees the same multiset: never ends */
+		S += um * n - rs;
+		SS += (unsigned long long)(um * um) * (unsigned long long)n - rss;
+		/* the n replacements join the group of value mw, or a free slot */
+		int slot = -1;
+#pragma unroll
+		for (int k = SGH_SMG - 1; k >= 0; k--)
+			slot = (gc[k] == 0) ? k : slot;
+#pragma unroll
+		for (int k = SGH_SMG - 1; k >= 0; k--)
+			slot = (gc[k] && gv[k] == mw) ? k : slot;
+		if (slot < 0)
+			return SG_CLS_LITERAL;
+#pragma unroll
+		for (int k = 0; k < SGH_SMG; k++) {
+			if (k == slot) {
+				gc[k] = (gc[k] && gv[k] == mw) ? gc[k] + n : n;
+				gv[k] = mw;
+			}
+		}
+		A = A2;
+		B = B2;
+		MA = MA2;
+		MB = MB2;
+	} while (n > 0 && N > 3);
+	const long long tot = S + (long long)N * P.lo;
+	*value = sg_round_to_WORD((double)tot / (double)N);
+	*rlo_out = rlo;
+	*rhi_out = rhi;
+	return SG_CLS_OK;
+}
+
 /* One threshold query of the Winsorized loop: the samples <= v (count, and their moments
  * relative to lo as exact doubles) and the neighbouring sample value on one side, dir 0 the
  * smallest sample > v, dir 1 the largest sample <= v, from ONE read of the group holding v's
@@ -1659,6 +1831,8 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 				/* out-of-band samples of any value: below the band nbl of them, above na */
 				const int na = (int)L.na[col], nbl = oob - na;
 				cls = sgh_median_pct<REJ, ZT>(P, N, p.sig0, p.sig1, nbl, nbl == P.nz, na == P.ns, &value, &rlo, &rhi);
+			} else if (REJ == 3) {
+				cls = sgh_sigmedian(P, N, p.sig0, p.sig1, &value, &rlo, &rhi);
 			} else if (REJ == 4 || !PAIR) {
 				/* zeros: nz copies of -lo, exact as doubles (dz = -lo, dz^2 nz < 2^53) */
 				P.zs = -(double)lo * (double)P.nz;
@@ -2222,6 +2396,11 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 					redo_list);
 		return;
 	}
+	if (REJ == 3) {	/* SIGMEDIAN: one lane per column (waves 0 and 1) */
+		for (int col = 64 * wave + lane; col < COLS; col += 64 * WAVES)
+			sgh_finish2<REJ, false, NI, false, false>(p, L, col, 0, col_lo(col), R, c, col_x(col), redo_count, redo_list);
+		return;
+	}
 	/* every wave finishes 32 pixel columns, a lane pair per column */
 	const int half = lane & 1;
 	int col = 32 * wave + (lane >> 1);
@@ -2289,6 +2468,14 @@ template __global__ void k_stack_hist<1, 1, 1>(SgStackParams, const int *, const
 template __global__ void k_stack_hist<1, 2, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
 		unsigned int *);
 template __global__ void k_stack_hist<1, 3, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);
+template __global__ void k_stack_hist<3, 0, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);
+template __global__ void k_stack_hist<3, 1, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);
+template __global__ void k_stack_hist<3, 2, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
+		unsigned int *);
+template __global__ void k_stack_hist<3, 3, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
 		unsigned int *);
 template __global__ void k_stack_hist<8, 0, 1>(SgStackParams, const int *, const int4 *, unsigned int *,
 		unsigned int *);

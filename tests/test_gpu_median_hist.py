@@ -148,10 +148,24 @@ def test_percentile_long_redo_list_counted_once(gpu_ctx, normalize):
     assert np.array_equal(rej, rej_ref), (rej, rej_ref)
 
 
-def test_more_than_1024_frames_sorted_only_rejection_refused(gpu_ctx):
-    """SIGMEDIAN / LINEARFIT have no histogram path: beyond 1024 frames the call fails loudly"""
+def test_more_than_1024_frames_sigmedian(gpu_ctx):
+    """SIGMEDIAN beyond the sorted kernel's 1024 frames: the histogram path, its redo pixels
+    through the literal kernel (the reference has no cap, :1486-1507)"""
+    N, C, H, W = 1100, 1, 6, 140
+    frames = _frames(N, C, H, W, seed=9, maxshift=3)
+    sx, sy = orc.synth_shifts(N, seed=9, maxshift=3)
+    rc, ref, rej_ref = orc.stack_rejection(frames, sg.SIGMEDIAN, sig=(3.0, 3.0), shiftx=sx, shifty=sy, max_thread=2)
+    assert rc == 0
+    out, rej, _ = gpu_stack(gpu_ctx, frames, sg.MEAN, sg.SIGMEDIAN, (3.0, 3.0), sx, sy, max_thread=2)
+    assert gpu_ctx.stats().path == 1
+    assert_same(out, ref, "sigmedian N=1100")
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+
+
+def test_more_than_1024_frames_linearfit_refused(gpu_ctx):
+    """LINEARFIT has no histogram path: beyond 1024 frames the call fails loudly"""
     N, C, H, W = 1100, 1, 2, 64
     frames = orc.synth(N, C, H, W, seed=1, maxshift=2)
-    desc, keep = sg.make_desc(sg.MEAN, N, W, H, C, rejection=sg.SIGMEDIAN)
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, C, rejection=sg.LINEARFIT)
     rc, out, rej, _ = gpu_ctx.stack_host(desc, frames)
     assert rc == -2 and "1024" in gpu_ctx.error()

@@ -62,11 +62,44 @@ def test_sigmedian_sorted_path(gpu_ctx, N, sig):
     sx, sy = orc.synth_shifts(N, seed=700 + N, maxshift=3)
     rc, ref, rej_ref = orc.stack_rejection(frames, sg.SIGMEDIAN, sig=sig, shiftx=sx, shifty=sy, max_thread=2)
     assert rc == 0
-    out, rej, _ = gpu_stack(gpu_ctx, frames, sg.MEAN, sg.SIGMEDIAN, sig, sx, sy, max_thread=2)
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=sg.SIGMEDIAN, sig=sig, shiftx=sx, shifty=sy,
+                              max_thread=2, max_number_of_rows=H, kernel_path=sg.PATH_SORTED)
+    rc, out, rej, _ = gpu_ctx.stack_host(desc, np.ascontiguousarray(frames))
+    assert rc == 0, gpu_ctx.error()
+    assert gpu_ctx.stats().path == 0
     assert_same(out, ref, f"sigmedian N={N} sig={sig}")
     assert np.array_equal(rej, rej_ref), (rej, rej_ref)
     if sig == (4.0, 3.0) and N >= 16:
         assert gpu_ctx.stats().slow_pixels <= 0.02 * H * W, gpu_ctx.stats().slow_pixels
+
+
+@pytest.mark.parametrize("N", [16, 33, 200, 512])
+@pytest.mark.parametrize("normalize", [sg.NO_NORM, sg.ADDITIVE_SCALING, sg.MULTIPLICATIVE])
+@pytest.mark.parametrize("sig", [(4.0, 3.0), (1.0, 1.0), (2.5, 1.2), (0.3, 0.2)])
+def test_sigmedian_hist_path(gpu_ctx, N, normalize, sig):
+    """SIGMEDIAN on the histogram kernel (k_stack_hist<3>: the window of never-replaced samples
+    as a value interval of the column histogram plus up to 4 replacement groups; decisions in the
+    rounding band, a fifth group or a never-ending pass go to the redo list): the image and the
+    counters equal the oracle, shifts and normalisation included, and the main kernel is the
+    histogram one"""
+    H, W = 24, 260
+    frames = _outlier_frames(N, H, W, 900 + N)
+    rng = np.random.default_rng(N + 7)
+    frames[:, :, :, :8] = rng.integers(900, 1100, size=(N, 1, H, 8)).astype(np.uint16)
+    sx, sy = orc.synth_shifts(N, seed=900 + N, maxshift=4)
+    off = mul = sc = None
+    if normalize != sg.NO_NORM:
+        loc = 1000 + rng.random(N) * 60
+        scl = 30 + rng.random(N) * 5
+        off, mul, sc = orc.compute_normalization(normalize, loc, scl, ref_image=0)
+    rc, ref, rej_ref = orc.stack_rejection(frames, sg.SIGMEDIAN, sig=sig, shiftx=sx, shifty=sy, normalize=normalize,
+                                           offset=off, mul=mul, scale=sc, max_thread=2)
+    assert rc == 0
+    out, rej, _ = gpu_stack(gpu_ctx, frames, sg.MEAN, sg.SIGMEDIAN, sig, sx, sy, normalize=normalize, offset=off,
+                            mul=mul, scale=sc, max_thread=2)
+    assert gpu_ctx.stats().path == 1
+    assert_same(out, ref, f"sigmedian hist N={N} norm={normalize} sig={sig}")
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
 
 
 @pytest.mark.parametrize("N", [5, 9, 16, 64, 200])
