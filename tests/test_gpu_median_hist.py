@@ -151,7 +151,7 @@ def test_percentile_long_redo_list_counted_once(gpu_ctx, normalize):
 def test_more_than_1024_frames_sigmedian(gpu_ctx):
     """SIGMEDIAN beyond the sorted kernel's 1024 frames: the histogram path, its redo pixels
     through the literal kernel (the reference has no cap, :1486-1507)"""
-    N, C, H, W = 1100, 1, 6, 140
+    N, C, H, W = 1100, 1, 16, 140       # blocks of 4 rows: |shifty| < 4 (:1555-1561)
     frames = _frames(N, C, H, W, seed=9, maxshift=3)
     sx, sy = orc.synth_shifts(N, seed=9, maxshift=3)
     rc, ref, rej_ref = orc.stack_rejection(frames, sg.SIGMEDIAN, sig=(3.0, 3.0), shiftx=sx, shifty=sy, max_thread=2)
