@@ -178,6 +178,8 @@ typedef struct {
 	uint64_t reg_fp64_reruns;	/* pairs of the fp32 passes re-run in fp64 (near ties at fp32 tolerance) */
 	uint64_t compact_pixels;	/* normalised histogram stacks: redo pixels whose sorted columns the
 					 * histogram kernel wrote out (no gather in the sorted kernel) */
+	double reg_ms;			/* last registration on a device: HIP-event span of its device work
+					 * (first pass to the quality estimate's end, host waits included) */
 } sg_stack_stats;
 int sg_get_last_stats(const sg_ctx *ctx, sg_stack_stats *st);
 /* device slots of the context (sg_init's ndev): callers size their batches by it, as the

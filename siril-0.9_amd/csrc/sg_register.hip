@@ -1523,6 +1523,7 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	/* the call's tie statistics: the device's record (one host thread per device), published to
 	 * the context when the call returns */
 	dv.stats.reg_ties_resolved = dv.stats.reg_ties_unresolved = dv.stats.reg_fp64_reruns = 0;
+	dv.stats.reg_ms = 0.0;
 	struct Publish {
 		sg_ctx *c;
 		const sg_stack_stats &s;
@@ -1531,6 +1532,7 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 			c->stats.reg_ties_resolved = s.reg_ties_resolved;
 			c->stats.reg_ties_unresolved = s.reg_ties_unresolved;
 			c->stats.reg_fp64_reruns = s.reg_fp64_reruns;
+			c->stats.reg_ms = s.reg_ms;
 		}
 	} publish{ctx, dv.stats};
 
@@ -1597,6 +1599,7 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	}
 	const sg_c64 *tw = tbl.tw;
 
+	HIPCHK(hipEventRecord(dv.ev[0], s));	/* the call's device span (sg_stack_stats.reg_ms) */
 	/* quality of the reference and of every registered frame */
 	std::vector<int> qframes;
 	qframes.push_back(ref_image);
@@ -2012,8 +2015,17 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		}
 	}
 
+	if (q_launched)	/* the span ends with the quality estimate's stream */
+		HIPCHK(hipStreamWaitEvent(s, dv.aux_ev[0], 0));
+	HIPCHK(hipEventRecord(dv.ev[1], s));
 	if (int qrc = reg_quality_finish(ctx, dv, (int)qframes.size(), q_launched, qual))
 		return qrc;
+	{
+		float ms = 0.f;
+		HIPCHK(hipEventSynchronize(dv.ev[1]));
+		HIPCHK(hipEventElapsedTime(&ms, dv.ev[0], dv.ev[1]));
+		dv.stats.reg_ms = ms;
+	}
 	/* quality: q_min/q_max seeded by the reference frame, then frames in index order with
 	 * the reference's min() macro (src/core/siril.h), then normalizeQualityData */
 	if (!normalize_q) {	/* raw values of the processed frames (sharded registration) */
@@ -2144,12 +2156,14 @@ static int reg_host(sg_ctx *ctx, const uint16_t *sel, int nframes, int S, int re
 		agg.reg_ties_resolved += st.reg_ties_resolved;
 		agg.reg_ties_unresolved += st.reg_ties_unresolved;
 		agg.reg_fp64_reruns += st.reg_fp64_reruns;
+		agg.reg_ms = std::max(agg.reg_ms, st.reg_ms);
 	}
 	{
 		std::lock_guard<std::mutex> lk(ctx->mu);
 		ctx->stats.reg_ties_resolved = agg.reg_ties_resolved;
 		ctx->stats.reg_ties_unresolved = agg.reg_ties_unresolved;
 		ctx->stats.reg_fp64_reruns = agg.reg_fp64_reruns;
+		ctx->stats.reg_ms = agg.reg_ms;
 	}
 	for (int g = 0; g < G; g++)
 		if (rcs[(size_t)g])

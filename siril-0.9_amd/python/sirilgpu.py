@@ -59,6 +59,7 @@ class StackStats(ctypes.Structure):
         ("reg_ties_unresolved", ctypes.c_uint64),
         ("reg_fp64_reruns", ctypes.c_uint64),
         ("compact_pixels", ctypes.c_uint64),
+        ("reg_ms", ctypes.c_double),
     ]
 
 
