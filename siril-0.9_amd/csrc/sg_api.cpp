@@ -41,7 +41,7 @@ __global__ void k_redo_to_literal(SgStackParams p, const unsigned int *list, con
 		unsigned int maxn);
 __global__ void k_stack_reduce(SgStackParams p);
 __global__ void k_stack_reduce2(SgStackParams p);
-template <int M>
+template <int M, int SEG>
 __global__ void k_stack_reduce3(SgStackParams p, const int *tab, const int *shifty);
 __global__ void k_sum_finalize(SgStackParams p);
 __global__ void k_stack_literal(SgStackParams p, SgChainTables t, unsigned int count, uint8_t *scratch, int phase);
@@ -908,19 +908,27 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		/* XCD-aware SGPR-offset loads (k_stack_reduce3) when the shifted row offsets fit 32 bits,
 		 * the per-lane pair kernel (SG_REDUCE1=2, A/B) otherwise */
 		const bool r3 = pairs && hist_addr_ok && ctx->knobs.reduce1 == 0;
-		const unsigned nb3 = (unsigned)(((W + 511) / 512) * (size_t)nrows * C);
+		/* 256-byte segments per wave: SEG = 2 by default (SG_REDUCE_SEG: 1 / 2 / 4, A/B) */
+		const int seg = ctx->knobs.reduce_seg;
+		const unsigned nb3 = (unsigned)(((W + 512 * seg - 1) / (512 * seg)) * (size_t)nrows * C);
 		HIPCHK(hipEventRecord(cev[0], s));
 		if (r3) {
-			switch (d->method) {
-			case SG_STACK_SUM: hipLaunchKernelGGL(k_stack_reduce3<0>, dim3(nb3), dim3(256), 0, s, p, p.hist_tab, p.shifty); break;
-			case SG_STACK_MEAN:	/* the normalising instance's fp64 path costs registers: its own kernel */
-				if (p.normalize)
-					hipLaunchKernelGGL(k_stack_reduce3<2>, dim3(nb3), dim3(256), 0, s, p, p.hist_tab, p.shifty);
-				else
-					hipLaunchKernelGGL(k_stack_reduce3<1>, dim3(nb3), dim3(256), 0, s, p, p.hist_tab, p.shifty);
+			/* MEAN: the normalising instance's fp64 path costs registers: its own kernel */
+			const int m = d->method == SG_STACK_SUM ? 0 : d->method == SG_STACK_MEAN ? (p.normalize ? 2 : 1) :
+				d->method == SG_STACK_MAX ? 3 : 4;
+			switch (m * 8 + seg) {
+#define SG_R3L(M, G)                                                                            \
+			case M * 8 + G:                                                                 \
+				hipLaunchKernelGGL((k_stack_reduce3<M, G>), dim3(nb3), dim3(256), 0, s, p, p.hist_tab, p.shifty); \
 				break;
-			case SG_STACK_MAX: hipLaunchKernelGGL(k_stack_reduce3<3>, dim3(nb3), dim3(256), 0, s, p, p.hist_tab, p.shifty); break;
-			default: hipLaunchKernelGGL(k_stack_reduce3<4>, dim3(nb3), dim3(256), 0, s, p, p.hist_tab, p.shifty); break;
+			SG_R3L(0, 1) SG_R3L(0, 2) SG_R3L(0, 4)
+			SG_R3L(1, 1) SG_R3L(1, 2) SG_R3L(1, 4)
+			SG_R3L(2, 1) SG_R3L(2, 2) SG_R3L(2, 4)
+			SG_R3L(3, 1) SG_R3L(3, 2) SG_R3L(3, 4)
+			SG_R3L(4, 1) SG_R3L(4, 2) SG_R3L(4, 4)
+#undef SG_R3L
+			default:
+				return set_err(ctx, SG_ERR_GENERIC, "no reduce kernel for this case%s%.0ld", "", 0);
 			}
 		} else if (pairs) {
 			hipLaunchKernelGGL(k_stack_reduce2, grid2, dim3(256), 0, s, p);

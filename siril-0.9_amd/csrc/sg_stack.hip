@@ -1154,121 +1154,147 @@ k_stack_reduce2(SgStackParams p) {
  * test of the frame's shifty).  Two 16-frame register buffers per lane.  Other segments take the
  * general per-lane loop (sg_reduce_pairs).  M: 0 SUM, 1 MEAN, 2 normalised MEAN, 3 MAX, 4 MIN.
  */
-template <int M>
+template <int M, int SEG>
 __global__ void __launch_bounds__(256)
 k_stack_reduce3(SgStackParams p, const int *__restrict__ tab, const int *__restrict__ shifty) {
+	/* SEG 256-byte segments per wave (a wave 128 SEG pixels, a workgroup 512 SEG): each frame
+	 * row is read as SEG * 256 contiguous bytes per wave (the longer the segment, the fewer DRAM
+	 * pages opened per byte: tools/bw_probe4.hip streams 512 x 4096^2 in 3.28 ms at 256 B, 3.00 at
+	 * 512 B, 2.99 at 1 KiB, profiles/r05c_probe5.log); MB = 16 / SEG frames per register buffer
+	 * keep the bytes in flight per wave */
+	constexpr int MB = 16 / SEG, PXW = 128 * SEG, PXG = 4 * PXW;
 	const int nblk = (int)gridDim.x, xcd = (int)blockIdx.x & 7, q = nblk >> 3, rem = nblk & 7;
 	const int vb = xcd * q + (xcd < rem ? xcd : rem) + ((int)blockIdx.x >> 3);
-	const int bpr = (p.W + 511) >> 9;
+	const int bpr = (p.W + PXG - 1) / PXG;
 	const int nrows = p.row_end - p.row_begin;
 	const int xt = vb % bpr, rr = vb / bpr;
 	const int R = p.row_begin + rr % nrows, c = rr / nrows;
-	/* each wave its own 128-pixel segment: only the segments at the image edges take the
-	 * general loop */
+	/* each wave its own segment: only the segments at the image edges take the general loop */
 	const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-	const int x0 = xt * 512 + 128 * wave;
-	const int x = xt * 512 + 2 * (int)threadIdx.x;
-	const bool interior = x0 > p.hist_maxsx && x0 + 128 + p.hist_maxsx <= p.W;
-	uint32_t acc_a = M == 4 ? 65535u : 0u, acc_b = acc_a;
+	const int lane = threadIdx.x & 63;
+	const int x0 = xt * PXG + PXW * wave;
+	uint32_t acc_a[SEG], acc_b[SEG];
+#pragma unroll
+	for (int k = 0; k < SEG; k++)
+		acc_a[k] = acc_b[k] = M == 4 ? 65535u : 0u;
+	const bool interior = x0 > p.hist_maxsx && x0 + PXW + p.hist_maxsx <= p.W;
 	if (!interior) {
-		sg_reduce_pairs(p, x, R, c, acc_a, acc_b);
-		sg_reduce_store(p, x, R, c, acc_a, acc_b);
+#pragma unroll
+		for (int k = 0; k < SEG; k++) {
+			const int x = x0 + 128 * k + 2 * lane;
+			sg_reduce_pairs(p, x, R, c, acc_a[k], acc_b[k]);
+			sg_reduce_store(p, x, R, c, acc_a[k], acc_b[k]);
+		}
 		return;
 	}
 	const int N = p.N;
 	const char *plane = (const char *)(p.frames + (int64_t)c * p.plane_stride);
 	const uint32_t nrec = (uint32_t)p.H * (uint32_t)p.W * 2u;
 	const int rowb = (R * p.W + x0) * 2;
-	const int vofs = ((int)threadIdx.x & 63) * 4;
-	uint32_t mm = M == 4 ? 0xFFFFFFFFu : 0u;	/* MAX / MIN: both pixels packed */
+	const int vofs = lane * 4;
+	uint32_t mm[SEG];	/* MAX / MIN: both pixels packed */
+#pragma unroll
+	for (int k = 0; k < SEG; k++)
+		mm[k] = M == 4 ? 0xFFFFFFFFu : 0u;
 	const int64_t fstride2 = p.frame_stride * 2;
-	const int lane = threadIdx.x & 63;
 	int vsy = 0;	/* MIN: shifty of frames f0 + lane (64 at a time), read back with readlane */
-	/* 16 frames: their c1 (scalar loads; the table is zero padded to a multiple of 16 frames),
-	 * then one load per frame; frames past N read nothing */
-	auto load16 = [&](int f0, uint32_t (&v)[16]) {
-		int c1[16];
+	/* MB frames: their c1 (scalar loads; the table is zero padded to a multiple of 16 frames),
+	 * then SEG loads per frame; frames past N read nothing */
+	auto loadb = [&](int f0, uint32_t (&v)[MB][SEG]) {
+		int c1[MB];
 		const int *t = tab + __builtin_amdgcn_readfirstlane(f0);
 #pragma unroll
-		for (int i = 0; i < 16; i++)
+		for (int i = 0; i < MB; i++)
 			c1[i] = t[i];
 		const char *fb = plane + (int64_t)f0 * fstride2;
 #pragma unroll
-		for (int m = 0; m < 16; m++) {
+		for (int m = 0; m < MB; m++) {
 			const uint32_t n = f0 + m < N ? nrec : 0u;
-			v[m] = __builtin_amdgcn_raw_buffer_load_b32(sg_plane_rsrc((const uint16_t *)(fb + (int64_t)m * fstride2), n),
-					vofs, rowb - c1[m], 0);
+#pragma unroll
+			for (int k = 0; k < SEG; k++)
+				v[m][k] = __builtin_amdgcn_raw_buffer_load_b32(
+						sg_plane_rsrc((const uint16_t *)(fb + (int64_t)m * fstride2), n), vofs + 256 * k,
+						rowb - c1[m], 0);
 		}
 	};
-	auto acc16 = [&](int f0, const uint32_t (&v)[16], bool full) {
+	auto accb = [&](int f0, const uint32_t (&v)[MB][SEG], bool full) {
 		if (M == 4 && p.use_shift && (f0 & 63) == 0)
 			vsy = shifty[f0 + lane < N ? f0 + lane : N - 1];
 #pragma unroll
-		for (int m = 0; m < 16; m++) {
+		for (int m = 0; m < MB; m++) {
 			const int f = f0 + m;
 			if (!full && f >= N)
 				continue;
-			const uint32_t a = v[m] & 0xFFFFu, b = v[m] >> 16;
-			if (M == 0) {
-				acc_a += a;
-				acc_b += b;
-			} else if (M == 1) {	/* MEAN without normalisation: the sum (the divisor is N) */
-				acc_a += a;
-				acc_b += b;
-			} else if (M == 2) {	/* normalised MEAN: the zero fill of a row shifted out is normalised too */
-				acc_a += sg_normalize(p, f, (uint16_t)a);
-				acc_b += sg_normalize(p, f, (uint16_t)b);
-			} else if (M == 3) {
-				mm = __builtin_bit_cast(uint32_t,
-						__builtin_elementwise_max(__builtin_bit_cast(sg_u16x2, mm), __builtin_bit_cast(sg_u16x2, v[m])));
-			} else {
-				const int sy = p.use_shift ? __builtin_amdgcn_readlane(vsy, (f0 & 63) + m) : 0;
-				if ((unsigned)(R - sy) < (unsigned)p.H)
-					mm = __builtin_bit_cast(uint32_t,
-							__builtin_elementwise_min(__builtin_bit_cast(sg_u16x2, mm), __builtin_bit_cast(sg_u16x2, v[m])));
+			int sy = 0;
+			if (M == 4)
+				sy = p.use_shift ? __builtin_amdgcn_readlane(vsy, (f0 & 63) + m) : 0;
+#pragma unroll
+			for (int k = 0; k < SEG; k++) {
+				const uint32_t a = v[m][k] & 0xFFFFu, b = v[m][k] >> 16;
+				if (M == 0 || M == 1) {	/* SUM; MEAN without normalisation: the sum (the divisor is N) */
+					acc_a[k] += a;
+					acc_b[k] += b;
+				} else if (M == 2) {	/* normalised MEAN: the zero fill of a row shifted out is normalised too */
+					acc_a[k] += sg_normalize(p, f, (uint16_t)a);
+					acc_b[k] += sg_normalize(p, f, (uint16_t)b);
+				} else if (M == 3) {
+					mm[k] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(sg_u16x2, mm[k]),
+							__builtin_bit_cast(sg_u16x2, v[m][k])));
+				} else if ((unsigned)(R - sy) < (unsigned)p.H) {
+					mm[k] = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(sg_u16x2, mm[k]),
+							__builtin_bit_cast(sg_u16x2, v[m][k])));
+				}
 			}
 		}
 	};
-	/* two 16-frame register buffers: the next block's loads are issued before this block is
-	 * accumulated; the steady loop is straight-line code with sched_barriers (the compiler
-	 * otherwise interleaves the accumulation with the loads, and conditional loads make its
-	 * vmcnt waits drain the block in flight) */
-	uint32_t bufa[16], bufb[16];
-	load16(0, bufa);
+	/* two register buffers: the next block's loads are issued before this block is accumulated;
+	 * the steady loop is straight-line code with sched_barriers (the compiler otherwise
+	 * interleaves the accumulation with the loads, and conditional loads make its vmcnt waits
+	 * drain the block in flight) */
+	uint32_t bufa[MB][SEG], bufb[MB][SEG];
+	loadb(0, bufa);
 	int f0 = 0;
-	while (f0 + 48 <= N) {
-		load16(f0 + 16, bufb);
+	while (f0 + 3 * MB <= N) {
+		loadb(f0 + MB, bufb);
 		__builtin_amdgcn_sched_barrier(0);
-		acc16(f0, bufa, true);
+		accb(f0, bufa, true);
 		__builtin_amdgcn_sched_barrier(0);
-		load16(f0 + 32, bufa);
+		loadb(f0 + 2 * MB, bufa);
 		__builtin_amdgcn_sched_barrier(0);
-		acc16(f0 + 16, bufb, true);
+		accb(f0 + MB, bufb, true);
 		__builtin_amdgcn_sched_barrier(0);
-		f0 += 32;
+		f0 += 2 * MB;
 	}
 	/* the last one to three blocks, with bounds */
-	if (f0 + 16 < N)
-		load16(f0 + 16, bufb);
-	acc16(f0, bufa, f0 + 16 <= N);
-	if (f0 + 16 < N) {
-		if (f0 + 32 < N)
-			load16(f0 + 32, bufa);
-		acc16(f0 + 16, bufb, f0 + 32 <= N);
-		if (f0 + 32 < N)
-			acc16(f0 + 32, bufa, f0 + 48 <= N);
+	if (f0 + MB < N)
+		loadb(f0 + MB, bufb);
+	accb(f0, bufa, f0 + MB <= N);
+	if (f0 + MB < N) {
+		if (f0 + 2 * MB < N)
+			loadb(f0 + 2 * MB, bufa);
+		accb(f0 + MB, bufb, f0 + 2 * MB <= N);
+		if (f0 + 2 * MB < N)
+			accb(f0 + 2 * MB, bufa, f0 + 3 * MB <= N);
 	}
-	if (M == 3 || M == 4) {
-		acc_a = mm & 0xFFFFu;
-		acc_b = mm >> 16;
+#pragma unroll
+	for (int k = 0; k < SEG; k++) {
+		if (M == 3 || M == 4) {
+			acc_a[k] = mm[k] & 0xFFFFu;
+			acc_b[k] = mm[k] >> 16;
+		}
+		sg_reduce_store(p, x0 + 128 * k + 2 * lane, R, c, acc_a[k], acc_b[k]);
 	}
-	sg_reduce_store(p, x, R, c, acc_a, acc_b);
 }
-template __global__ void k_stack_reduce3<0>(SgStackParams, const int *, const int *);
-template __global__ void k_stack_reduce3<1>(SgStackParams, const int *, const int *);
-template __global__ void k_stack_reduce3<2>(SgStackParams, const int *, const int *);
-template __global__ void k_stack_reduce3<3>(SgStackParams, const int *, const int *);
-template __global__ void k_stack_reduce3<4>(SgStackParams, const int *, const int *);
+#define SG_R3(M)                                                                               \
+	template __global__ void k_stack_reduce3<M, 1>(SgStackParams, const int *, const int *);   \
+	template __global__ void k_stack_reduce3<M, 2>(SgStackParams, const int *, const int *);   \
+	template __global__ void k_stack_reduce3<M, 4>(SgStackParams, const int *, const int *);
+SG_R3(0)
+SG_R3(1)
+SG_R3(2)
+SG_R3(3)
+SG_R3(4)
+#undef SG_R3
 
 /* SUM finalisation: out = round_to_WORD(sum) or round_to_WORD(sum * 65535/maxim) (:328-342) */
 __global__ void __launch_bounds__(256)
