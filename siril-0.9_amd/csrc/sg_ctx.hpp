@@ -112,7 +112,7 @@ struct SgKnobs {
 					 * >= 2: the compact list's capacity in pixels (tests of the overflow) */
 	int reduce1 = 0;		/* SG_REDUCE1: 1 = one pixel per lane, 2 = the per-lane pixel-pair kernel, in the SUM/MAX/MIN/MEAN reduce (A/B) */
 	long long host_budget = 0;	/* SG_HOST_BUDGET_BYTES: host-pull HBM budget (0 = 85 % of free HBM) */
-	int reduce_seg = 2;		/* SG_REDUCE_SEG: 256-byte segments per wave in k_stack_reduce3 (1, 2, 4) */
+	int reduce_seg = 1;		/* SG_REDUCE_SEG: 256-byte segments per wave in k_stack_reduce3 (1, 2, 4; 1 measured best: 512 x 4096^2 mean 3.52 / 3.59 / 4.33 ms, profiles/r05g) */
 	int hist_sigmedian = 1;		/* SG_HIST_SIGMEDIAN: 0 = SIGMEDIAN on the sorted kernel only (A/B) */
 	int pull_overlap = 1;		/* SG_PULL_OVERLAP: 0 = host-pull bands read and stacked one after the other (A/B) */
 	int qsub_threads = 64;		/* SG_QSUB_THREADS: 64 measured best (scripts/gpu_qsub.sh) */
@@ -139,7 +139,7 @@ struct SgKnobs {
 		reduce1 = sg_env_int("SG_REDUCE1", 0, 2, 0);
 		pull_overlap = sg_env_int("SG_PULL_OVERLAP", 0, 1, 1);
 		hist_sigmedian = sg_env_int("SG_HIST_SIGMEDIAN", 0, 1, 1);
-		reduce_seg = sg_env_int("SG_REDUCE_SEG", 1, 4, 2);
+		reduce_seg = sg_env_int("SG_REDUCE_SEG", 1, 4, 1);
 		if (reduce_seg == 3)
 			reduce_seg = 2;
 		if (const char *e = getenv("SG_HOST_BUDGET_BYTES"))

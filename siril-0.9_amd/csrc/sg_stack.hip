@@ -1157,11 +1157,12 @@ k_stack_reduce2(SgStackParams p) {
 template <int M, int SEG>
 __global__ void __launch_bounds__(256)
 k_stack_reduce3(SgStackParams p, const int *__restrict__ tab, const int *__restrict__ shifty) {
-	/* SEG 256-byte segments per wave (a wave 128 SEG pixels, a workgroup 512 SEG): each frame
-	 * row is read as SEG * 256 contiguous bytes per wave (the longer the segment, the fewer DRAM
-	 * pages opened per byte: tools/bw_probe4.hip streams 512 x 4096^2 in 3.28 ms at 256 B, 3.00 at
-	 * 512 B, 2.99 at 1 KiB, profiles/r05c_probe5.log); MB = 16 / SEG frames per register buffer
-	 * keep the bytes in flight per wave */
+	/* SEG 256-byte segments per wave (a wave 128 SEG pixels, a workgroup 512 SEG), MB = 16 / SEG
+	 * frames per register buffer (the bytes in flight per wave stay).  The loads-only probe reads
+	 * 512 x 4096^2 in 3.28 ms at 256 B, 3.00 at 512 B, 2.99 at 1 KiB per frame row
+	 * (tools/bw_probe4.hip, profiles/r05c_probe5.log), but this kernel measured 3.52 / 3.59 / 4.33
+	 * ms at SEG 1 / 2 / 4 (profiles/r05g: twice the edge waves on the general path, half the
+	 * frames per buffer), so SEG = 1 is the default (SG_REDUCE_SEG, A/B) */
 	constexpr int MB = 16 / SEG, PXW = 128 * SEG, PXG = 4 * PXW;
 	const int nblk = (int)gridDim.x, xcd = (int)blockIdx.x & 7, q = nblk >> 3, rem = nblk & 7;
 	const int vb = xcd * q + (xcd < rem ? xcd : rem) + ((int)blockIdx.x >> 3);
