@@ -402,15 +402,18 @@ def main_sigma(args):
             mul = loc[0] / loc
     desc, keep = sg.make_desc(method, N, W, Htot, 1, rejection=rej_mode if not median else sg.NO_REJEC, sig=sig,
                               shiftx=shx, shifty=shy, normalize=norm_mode, offset=off, mul=mul, scale=scale,
-                              max_thread=8, max_number_of_rows=Htot, resident_rows=(lo, hi + 1))
+                              max_thread=8, max_number_of_rows=Htot, resident_rows=(lo, hi + 1),
+                              flags=0 if strong and world > 1 else sg.RESULT_AT_COLLECT)
     torch.cuda.synchronize()
     kms = []
     stream = torch.cuda.current_stream().cuda_stream
 
     # one step = one whole stack of the band, queued with sg_stack_u16_device_async on torch's
     # stream (every launch decided on the device, the counters read back into a pinned slot):
-    # the host prepares the next step while the device runs this one; the strong form gathers the
-    # output bands to rank 0 behind it on the same stream (RCCL over xGMI)
+    # the host prepares the next step while the device runs this one.  The strong form gathers the
+    # output bands to rank 0 behind it on the same stream (RCCL over xGMI); otherwise the output is
+    # read after the timed region, so each step's work after its main kernel (redo list, replay,
+    # counters) runs on the library's tail stream beside the next step (SG_STACK_RESULT_AT_COLLECT)
     def step():
         ctx.stack_device_async(desc, base, fstride, nres * W, out_base, b, e, stream=stream)
         kms.append(ctx.stats().kernel_ms)       # the last folded call's (at most two calls behind)

@@ -83,8 +83,13 @@ typedef struct {
 	 * d_frames (sg_stack_u16_device); {0, 0} = all rows [0, height).  No reference
 	 * equivalent: it lets a rank hold only its row band plus the rows its shifts reach. */
 	int resident_rows[2];
-	int reserved[3];
+	int flags;		/* SG_STACK_* flags below (0 = none) */
+	int reserved[2];
 } sg_stack_desc;
+/* sg_stack_desc.flags: the output is needed only once sg_stack_collect has returned, so an
+ * async call (sg_stack_u16_device_async) may run its work after the main kernel (redo lists,
+ * replay, counters) beside the next call's main kernel instead of on `stream` */
+#define SG_STACK_RESULT_AT_COLLECT 1
 
 typedef struct sg_ctx sg_ctx;
 

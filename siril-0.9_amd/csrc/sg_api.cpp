@@ -90,9 +90,11 @@ extern "C" int sg_init(sg_ctx **out, int ndev, const int *devs) {
 		}
 		for (int k = 0; k < 4; k++)
 			(void)hipEventCreate(&d.ev[k]);
-		for (int k = 0; k < 2; k++)
+		for (int k = 0; k < 2; k++) {
 			for (int j = 0; j < 3; j++)
 				(void)hipEventCreate(&d.cev[k][j]);
+			(void)hipEventCreateWithFlags(&d.sl[k].stage_ev, hipEventDisableTiming);
+		}
 		for (int k = 0; k < 2; k++)
 			(void)hipEventCreateWithFlags(&d.io_ev[k], hipEventDisableTiming);
 		ctx->dev.push_back(d);
@@ -110,17 +112,30 @@ extern "C" void sg_shutdown(sg_ctx *ctx) {
 	for (auto &d : ctx->dev) {
 		(void)hipSetDevice(d.id);
 		(void)hipStreamSynchronize(d.stream);
-		SgBuf *bufs[] = {&d.flag_list, &d.flag_map, &d.sum_buf, &d.scratch, &d.frames, &d.out, &d.reg_sel, &d.reg_spec,
-			&d.reg_work, &d.reg_tw, &d.reg_tw32, &d.reg_best, &d.reg_qbuf, &d.reg_qacc, &d.redo, &d.zeros,
-			&d.cmp_cols, &d.cmp_list, &d.io_raw, &d.io_bad, &d.warp_tab, &d.stats_buf, &d.inb, &d.ctr, &d.lin_tab};
+		if (d.tail)
+			(void)hipStreamSynchronize(d.tail);
+		SgBuf *bufs[] = {&d.sum_buf, &d.frames, &d.out, &d.reg_sel, &d.reg_spec, &d.reg_work, &d.reg_tw, &d.reg_tw32,
+			&d.reg_best, &d.reg_qbuf, &d.reg_qacc, &d.zeros, &d.io_raw, &d.io_bad, &d.warp_tab, &d.stats_buf, &d.ctr};
 		for (SgBuf *b : bufs)
 			if (b->p)
 				(void)hipFree(b->p);
+		for (SgSlot &q : d.sl) {
+			SgBuf *sb[] = {&q.inb, &q.flag_list, &q.flag_map, &q.redo, &q.cmp_cols, &q.cmp_list, &q.scratch, &q.lin_tab};
+			for (SgBuf *b : sb)
+				if (b->p)
+					(void)hipFree(b->p);
+			if (q.stage_h)
+				(void)hipHostFree(q.stage_h);
+			if (q.stage_ev)
+				(void)hipEventDestroy(q.stage_ev);
+		}
+		if (d.tail)
+			(void)hipStreamDestroy(d.tail);
+		if (d.tail_ev)
+			(void)hipEventDestroy(d.tail_ev);
 		for (int k = 0; k < 2; k++)
 			if (d.pinned[k])
 				(void)hipHostFree(d.pinned[k]);
-		if (d.stage_h)
-			(void)hipHostFree(d.stage_h);
 		if (d.ctr_h)
 			(void)hipHostFree(d.ctr_h);
 		for (int k = 0; k < 2; k++) {
@@ -316,7 +331,7 @@ static const size_t SG_CTR_HOSTB = 256;
 static int stack_fold(sg_ctx *ctx, SgDevice &dv, int slot, uint64_t rej[3][2], uint64_t *maxim_out, bool sync) {
 	HIPCHK(hipEventSynchronize(dv.cev[slot][2]));
 	dv.pend[slot] = false;
-	dv.stage_pending = false;	/* the input copy ran before this call's kernels */
+	dv.sl[slot].stage_pending = false;	/* the input copy ran before this call's kernels */
 	const char *h = (const char *)dv.ctr_h + (size_t)slot * SG_CTR_HOSTB;
 	const unsigned int *fl = (const unsigned int *)(h + 64);
 	sg_stack_stats &st = dv.pstats[slot];
@@ -559,28 +574,39 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 	}
 	SgChainTables ct;
 	memset(&ct, 0, sizeof ct);
+	/* the counter slot (and its buffers): a synchronous call uses slot 0, an async call the free
+	 * slot, folding the older pending call when both are taken */
+	int slot = 0;
+	if (async) {
+		if (dv.pend[0] && dv.pend[1])
+			stack_fold_acc(ctx, dv, dv.pend_seq[0] < dv.pend_seq[1] ? 0 : 1);
+		slot = dv.pend[0] ? 1 : 0;
+	} else if (dv.pend[0]) {
+		stack_fold_acc(ctx, dv, 0);
+	}
+	SgSlot &sb = dv.sl[slot];
 	/* one pinned host block -> one device block; sets the kernels' pointers into it */
 	auto flush_inputs = [&]() -> int {
 		const size_t b_sh = sizeof(int) * sh.size(), o_nm = (b_sh + 255) & ~(size_t)255;
 		const size_t b_nm = sizeof(double) * nm.size(), o_tb = (o_nm + b_nm + 255) & ~(size_t)255;
 		const size_t o_zt = (o_tb + sizeof(int) * tables.size() + 255) & ~(size_t)255;
 		const size_t tot = (o_zt + sizeof(int) * ztab.size() + 15) & ~(size_t)15;
-		if (dv.stage_pending) {	/* an earlier call's copy may still read the host block */
-			HIPCHK(hipEventSynchronize(dv.ev[3]));
-			dv.stage_pending = false;
+		if (sb.stage_pending) {	/* an earlier call's copy may still read the host block */
+			HIPCHK(hipEventSynchronize(sb.stage_ev));
+			sb.stage_pending = false;
 		}
-		if (dv.stage_h_size < tot) {
-			if (dv.stage_h)
-				(void)hipHostFree(dv.stage_h);
-			dv.stage_h = nullptr;
-			dv.stage_h_size = 0;
+		if (sb.stage_h_size < tot) {
+			if (sb.stage_h)
+				(void)hipHostFree(sb.stage_h);
+			sb.stage_h = nullptr;
+			sb.stage_h_size = 0;
 			/* coherent: the device reads it uncached, so no call sees an earlier call's inputs */
-			HIPCHK(hipHostMalloc(&dv.stage_h, tot, hipHostMallocMapped | hipHostMallocCoherent));
-			dv.stage_h_size = tot;
-			HIPCHK(hipHostGetDevicePointer(&dv.stage_d, dv.stage_h, 0));
+			HIPCHK(hipHostMalloc(&sb.stage_h, tot, hipHostMallocMapped | hipHostMallocCoherent));
+			sb.stage_h_size = tot;
+			HIPCHK(hipHostGetDevicePointer(&sb.stage_d, sb.stage_h, 0));
 		}
-		HIPCHK(ensure(dv.inb, tot));
-		char *hb = (char *)dv.stage_h;
+		HIPCHK(ensure(sb.inb, tot));
+		char *hb = (char *)sb.stage_h;
 		memcpy(hb, sh.data(), b_sh);
 		if (b_nm)
 			memcpy(hb + o_nm, nm.data(), b_nm);
@@ -589,11 +615,11 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		if (!ztab.empty())
 			memcpy(hb + o_zt, ztab.data(), sizeof(int) * ztab.size());
 		hipLaunchKernelGGL(k_stage_copy, dim3((unsigned)std::min<size_t>(64, (tot / 16 + 255) / 256)), dim3(256), 0, s,
-				(uint4 *)dv.inb.p, (const uint4 *)dv.stage_d, (unsigned int)(tot / 16));
+				(uint4 *)sb.inb.p, (const uint4 *)sb.stage_d, (unsigned int)(tot / 16));
 		HIPCHK(hipGetLastError());
-		HIPCHK(hipEventRecord(dv.ev[3], s));
-		dv.stage_pending = true;
-		const char *db = (const char *)dv.inb.p;
+		HIPCHK(hipEventRecord(sb.stage_ev, s));
+		sb.stage_pending = true;
+		const char *db = (const char *)sb.inb.p;
 		p.hist_tab = (const int *)db;
 		p.hist_npad = Npad;
 		if (p.use_shift) {
@@ -631,14 +657,6 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 	if (!dv.ctr_h) {
 		HIPCHK(hipHostMalloc(&dv.ctr_h, 2 * SG_CTR_HOSTB, hipHostMallocMapped | hipHostMallocCoherent));
 		HIPCHK(hipHostGetDevicePointer((void **)&dv.ctr_hd, dv.ctr_h, 0));
-	}
-	int slot = 0;
-	if (async) {
-		if (dv.pend[0] && dv.pend[1])
-			stack_fold_acc(ctx, dv, dv.pend_seq[0] < dv.pend_seq[1] ? 0 : 1);
-		slot = dv.pend[0] ? 1 : 0;
-	} else if (dv.pend[0]) {
-		stack_fold_acc(ctx, dv, 0);
 	}
 	char *cblk = (char *)dv.ctr.p + (size_t)slot * CTRB;
 	hipEvent_t *cev = dv.cev[slot];
@@ -686,6 +704,22 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 	}
 	const bool sorted = (d->method == SG_STACK_MEDIAN) ||
 		(d->method == SG_STACK_MEAN && d->rejection != SG_NO_REJEC);
+	/* everything after the main kernel runs on ts: the call's stream, or the device's tail stream
+	 * for an async call whose result is wanted at sg_stack_collect only (it then overlaps the
+	 * next call's main kernel, which uses the other slot's buffers) */
+	hipStream_t ts = s;
+	auto to_tail = [&]() -> int {
+		if (!(async && (d->flags & SG_STACK_RESULT_AT_COLLECT)))
+			return SG_OK;
+		if (!dv.tail) {
+			HIPCHK(hipStreamCreateWithFlags(&dv.tail, hipStreamNonBlocking));
+			HIPCHK(hipEventCreateWithFlags(&dv.tail_ev, hipEventDisableTiming));
+		}
+		HIPCHK(hipEventRecord(dv.tail_ev, s));
+		HIPCHK(hipStreamWaitEvent(dv.tail, dv.tail_ev, 0));
+		ts = dv.tail;
+		return SG_OK;
+	};
 	if (sorted) {
 		const int nreg = pick_nreg(N);
 		/* histogram fast path (sg_stack_hist.hip): SIGMA / WINSORIZED / PERCENTILE rejection and
@@ -701,23 +735,23 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			return set_err(ctx, SG_ERR_SIZE, "this rejection supports up to 1024 frames%s (%ld); SIGMA, "
 					"WINSORIZED, PERCENTILE, SIGMEDIAN and median stacks take up to 65535", "", N);
 		const size_t npix_launch = (size_t)C * nrows * W;
-		HIPCHK(ensure(dv.flag_list, sizeof(unsigned int) * npix_launch));
+		HIPCHK(ensure(sb.flag_list, sizeof(unsigned int) * npix_launch));
 		{
 			/* pixel classes carry this call's epoch (sg_flag_get): no per-call clear; the map is
 			 * cleared when it is new or the 31 epochs wrap */
-			const void *old_map = dv.flag_map.p;
-			HIPCHK(ensure(dv.flag_map, npix_img));
-			if (dv.flag_map.p != old_map || dv.flag_epoch <= 0 || dv.flag_epoch >= 31) {
-				HIPCHK(hipMemsetAsync(dv.flag_map.p, 0, dv.flag_map.size, s));
-				dv.flag_epoch = 0;
+			const void *old_map = sb.flag_map.p;
+			HIPCHK(ensure(sb.flag_map, npix_img));
+			if (sb.flag_map.p != old_map || sb.flag_epoch <= 0 || sb.flag_epoch >= 31) {
+				HIPCHK(hipMemsetAsync(sb.flag_map.p, 0, sb.flag_map.size, s));
+				sb.flag_epoch = 0;
 			}
-			p.flag_epoch = (unsigned int)++dv.flag_epoch;
+			p.flag_epoch = (unsigned int)++sb.flag_epoch;
 		}
 		/* flag_map (the band's rows) is cleared right after the main kernel is queued (only the
 		 * kernels after it read it), so the clear is not ahead of the histogram kernel's launch */
-		p.flag_list = (unsigned int *)dv.flag_list.p;
+		p.flag_list = (unsigned int *)sb.flag_list.p;
 		p.flag_cap = (unsigned int)npix_launch;
-		p.flag_map = (uint8_t *)dv.flag_map.p;
+		p.flag_map = (uint8_t *)sb.flag_map.p;
 
 		/* reference thread order tables for the stale-state chains */
 		int nthr = d->max_thread > 0 ? d->max_thread : default_threads();
@@ -748,10 +782,10 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			return rc;
 
 		if (d->method == SG_STACK_MEAN && p.rejection == SG_LINEARFIT) {
-			HIPCHK(ensure(dv.lin_tab, sizeof(double) * 2 * ((size_t)N + 1)));
-			hipLaunchKernelGGL(k_linfit_tables, dim3((N + 64) / 64), dim3(64), 0, s, (double *)dv.lin_tab.p, N);
+			HIPCHK(ensure(sb.lin_tab, sizeof(double) * 2 * ((size_t)N + 1)));
+			hipLaunchKernelGGL(k_linfit_tables, dim3((N + 64) / 64), dim3(64), 0, s, (double *)sb.lin_tab.p, N);
 			HIPCHK(hipGetLastError());
-			p.linfit_tab = (const double *)dv.lin_tab.p;
+			p.linfit_tab = (const double *)sb.lin_tab.p;
 		}
 		const int ntx = (W + SG_TILE_W - 1) / SG_TILE_W;
 		const size_t nblk = (size_t)ntx * nrows * C;
@@ -759,9 +793,9 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		const size_t lds = (size_t)N * SG_STAGE_STRIDE * 2 +
 			(d->rejection == SG_LINEARFIT ? (size_t)64 * ((N + 31) / 32) * 4 : 0);
 		if (hist) {
-			HIPCHK(ensure(dv.redo, sizeof(unsigned int) * (npix_launch + 16)));
+			HIPCHK(ensure(sb.redo, sizeof(unsigned int) * (npix_launch + 16)));
 			unsigned int *redo_count = p.flag_count + 2;	/* cleared with the counters */
-			unsigned int *redo_list = (unsigned int *)dv.redo.p + 16;
+			unsigned int *redo_list = (unsigned int *)sb.redo.p + 16;
 			HIPCHK(hipEventRecord(cev[0], s));
 			/* NORM: 0 none, 1 additive (round(v scale - offset)), 2 multiplicative (round(v scale mul)),
 			 * 3 additive with the folded + 0.5 */
@@ -792,10 +826,10 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			if (compact) {
 				const size_t cap = std::min<size_t>(npix_launch, ctx->knobs.hist_compact >= 2 ?
 						(size_t)ctx->knobs.hist_compact : ((size_t)384 << 20) / ((size_t)N * 2));
-				HIPCHK(ensure(dv.cmp_cols, cap * (size_t)N * 2));
-				HIPCHK(ensure(dv.cmp_list, cap * sizeof(unsigned int)));
-				p.cmp_cols = (uint16_t *)dv.cmp_cols.p;
-				p.cmp_list = (unsigned int *)dv.cmp_list.p;
+				HIPCHK(ensure(sb.cmp_cols, cap * (size_t)N * 2));
+				HIPCHK(ensure(sb.cmp_list, cap * sizeof(unsigned int)));
+				p.cmp_cols = (uint16_t *)sb.cmp_cols.p;
+				p.cmp_list = (unsigned int *)sb.cmp_list.p;
 				p.cmp_count = p.flag_count + 3;	/* cleared with the counters */
 				p.cmp_cap = (unsigned int)cap;
 			}
@@ -828,6 +862,8 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			}
 			HIPCHK(hipGetLastError());
 			HIPCHK(hipEventRecord(cev[1], s));
+			if (int rc = to_tail())
+				return rc;
 			st.path = 1;
 			st.main_kernel_blocks = (int)nblk;
 			st.launches = 1;
@@ -837,7 +873,7 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 				/* the compact columns, any count up to the capacity (grid-stride) */
 				SgStackParams q = p;
 				q.cmp_src = p.cmp_cols;
-				HIPCHK(launch_sorted(nreg, true, lgrid, lds, s, q, p.cmp_list, p.cmp_count));
+				HIPCHK(launch_sorted(nreg, true, lgrid, lds, ts, q, p.cmp_list, p.cmp_count));
 				st.launches++;
 			}
 			/* the redo pixels, routed on the device (no host round trip in the call):
@@ -853,16 +889,16 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			if (replay_route) {
 				SgStackParams q = p;
 				q.list_minn = SG_REDO_REPLAY_MAX;	/* idle unless the list is longer */
-				HIPCHK(launch_sorted(nreg, true, lgrid, lds, s, q, redo_list, redo_count));
+				HIPCHK(launch_sorted(nreg, true, lgrid, lds, ts, q, redo_list, redo_count));
 				p.rp_list = redo_list;
 				p.rp_count = redo_count;
 				p.rp_maxn = SG_REDO_REPLAY_MAX;
 				st.launches++;
 			} else if (nreg) {
-				HIPCHK(launch_sorted(nreg, true, lgrid, lds, s, p, redo_list, redo_count));
+				HIPCHK(launch_sorted(nreg, true, lgrid, lds, ts, p, redo_list, redo_count));
 				st.launches++;
 			} else {
-				hipLaunchKernelGGL(k_redo_to_literal, dim3(64), dim3(256), 0, s, p, (const unsigned int *)redo_list,
+				hipLaunchKernelGGL(k_redo_to_literal, dim3(64), dim3(256), 0, ts, p, (const unsigned int *)redo_list,
 						(const unsigned int *)redo_count, 0xFFFFFFFFu);
 				HIPCHK(hipGetLastError());
 				st.launches++;
@@ -871,6 +907,8 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			HIPCHK(hipEventRecord(cev[0], s));
 			HIPCHK(launch_sorted(nreg, false, dim3((unsigned)nblk), lds, s, p, nullptr, nullptr));
 			HIPCHK(hipEventRecord(cev[1], s));
+			if (int rc = to_tail())
+				return rc;
 			st.main_kernel_blocks = (int)nblk;
 			st.launches = 1;
 		}
@@ -878,19 +916,19 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		 * list, early breaks with this pixel's own stale rejected[]), then the literal path for what
 		 * remains: two phases, grids read the count on the device */
 		const unsigned lit_threads = lit_thread_count(N);
-		HIPCHK(ensure(dv.scratch, lit_scratch_bytes(N)));
+		HIPCHK(ensure(sb.scratch, lit_scratch_bytes(N)));
 		if (d->method == SG_STACK_MEAN && (p.rejection == SG_SIGMA || p.rejection == SG_WINSORIZED) &&
 				N <= SG_REPLAY_MAXN) {
 			if (N <= 512)	/* the per-wave LDS sized for 512 frames (k_stack_replay<SG_REPLAY_FASTN>) */
-				hipLaunchKernelGGL(k_stack_replay<512>, dim3(2048), dim3(64 * SG_REPLAY_WAVES), 0, s, p);
+				hipLaunchKernelGGL(k_stack_replay<512>, dim3(2048), dim3(64 * SG_REPLAY_WAVES), 0, ts, p);
 			else
-				hipLaunchKernelGGL(k_stack_replay<SG_REPLAY_MAXN>, dim3(2048), dim3(64 * SG_REPLAY_WAVES), 0, s, p);
+				hipLaunchKernelGGL(k_stack_replay<SG_REPLAY_MAXN>, dim3(2048), dim3(64 * SG_REPLAY_WAVES), 0, ts, p);
 			HIPCHK(hipGetLastError());
 			st.launches++;
 		}
 		for (int phase = 1; phase <= 2; phase++) {
-			hipLaunchKernelGGL(k_stack_literal, dim3(lit_threads / 64), dim3(64), 0, s, p, ct,
-					0u, (uint8_t *)dv.scratch.p, phase);
+			hipLaunchKernelGGL(k_stack_literal, dim3(lit_threads / 64), dim3(64), 0, ts, p, ct,
+					0u, (uint8_t *)sb.scratch.p, phase);
 			HIPCHK(hipGetLastError());
 		}
 		st.launches += 2;
@@ -955,14 +993,14 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		}
 	}
 	if (SG_DBG(p) == 12)
-		sg_dbg_why_dump(s);
+		sg_dbg_why_dump(ts);
 	/* the counters back to the host: queued; a synchronous call folds them at once, an async one
 	 * when its slot is needed again or at sg_stack_collect */
-	hipLaunchKernelGGL(k_ctr_finalize, dim3(1), dim3(256), 0, s, (unsigned long long *)cblk,
+	hipLaunchKernelGGL(k_ctr_finalize, dim3(1), dim3(256), 0, ts, (unsigned long long *)cblk,
 			dv.ctr_hd + (size_t)slot * (SG_CTR_HOSTB / sizeof(unsigned long long)));
 	HIPCHK(hipGetLastError());
 	dv.ctr_clean[slot] = true;
-	HIPCHK(hipEventRecord(cev[2], s));
+	HIPCHK(hipEventRecord(cev[2], ts));
 	dv.pend_sum_read[slot] = d->method == SG_STACK_SUM;
 	dv.pstats[slot] = st;
 	dv.pend[slot] = true;

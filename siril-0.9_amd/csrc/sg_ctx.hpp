@@ -30,6 +30,22 @@ struct SgReader {
 	size_t cap = 0;		/* elements per buffer */
 };
 
+/* per-call device buffers of one stacking counter slot.  An async call flagged
+ * SG_STACK_RESULT_AT_COLLECT runs everything after its main kernel on the device's tail stream,
+ * beside the next call's main kernel, which uses the other slot's buffers (a slot is reused only
+ * once the call two back has been folded).  Synchronous calls use slot 0. */
+struct SgSlot {
+	SgBuf inb;		/* the call's inputs (shift table, normalisation pairs, chain tables) */
+	SgBuf flag_list, flag_map, redo, cmp_cols, cmp_list, scratch, lin_tab;
+	/* pinned, host-mapped staging of the inputs (k_stage_copy reads it); stage_ev marks the copy
+	 * done before the host block is rewritten */
+	void *stage_h = nullptr, *stage_d = nullptr;
+	size_t stage_h_size = 0;
+	bool stage_pending = false;
+	hipEvent_t stage_ev = nullptr;
+	int flag_epoch = 0;	/* flag_map epoch of the slot's last call (0: clear the map first) */
+};
+
 struct SgDevice {
 	int id = 0;
 	int shared = 1;		/* context slots on this physical device (sg_init(devs = {0, 0}) shares one card) */
@@ -37,12 +53,12 @@ struct SgDevice {
 	std::vector<SgReader> readers;
 	hipStream_t stream = nullptr;
 	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-	SgBuf flag_list, flag_map, sum_buf, scratch, frames, out, stats_buf;
+	SgBuf sum_buf, frames, out, stats_buf;
+	SgSlot sl[2];
+	hipStream_t tail = nullptr;	/* SG_STACK_RESULT_AT_COLLECT calls: their post-processing */
+	hipEvent_t tail_ev = nullptr;	/* the main kernel of such a call has finished */
 	/* registration workspaces (sg_register.hip) */
 	SgBuf reg_sel, reg_spec, reg_work, reg_tw, reg_tw32, reg_best, reg_qbuf, reg_qacc;
-	SgBuf redo;	/* redo list of the histogram stacking path */
-	SgBuf lin_tab;	/* LINEARFIT: per-N x recurrences (k_linfit_tables) */
-	SgBuf cmp_cols, cmp_list;	/* compact redo columns / pixels of normalised histogram stacks */
 	/* registration: the quality estimate runs on its own stream beside the FFT passes; its
 	 * sums come back into a pinned block, aux_ev marks them landed */
 	hipStream_t aux = nullptr;
@@ -50,13 +66,6 @@ struct SgDevice {
 	unsigned long long *qacc_h = nullptr;
 	size_t qacc_h_n = 0;
 	SgBuf zeros;	/* zero page for out-of-frame sample loads */
-	/* stacking call inputs (shift table, normalisation coefficients, chain tables) packed into
-	 * one pinned host block and one device block: one H2D copy per call; ev[3] marks the copy
-	 * done before the host block is rewritten */
-	SgBuf inb;
-	void *stage_h = nullptr;
-	size_t stage_h_size = 0;
-	bool stage_pending = false;
 	/* stacking counters (rejection shards, flag / redo counts, sum maximum) in one device block,
 	 * cleared by one memset and read back by one D2H copy into ctr_h (pinned) */
 	SgBuf ctr;
@@ -68,8 +77,7 @@ struct SgDevice {
 	hipEvent_t cev[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
 	unsigned long long *ctr_hd = nullptr;	/* ctr_h as the device sees it (k_ctr_finalize writes it) */
 	bool ctr_clean[2] = {false, false};	/* the slot's device counters are zero (k_ctr_finalize left them so) */
-	void *stage_d = nullptr;	/* stage_h as the device sees it (k_stage_copy reads it) */
-	int flag_epoch = 0;		/* flag_map epoch of the last call (0: clear the map first) */
+
 	bool pend[2] = {false, false};
 	unsigned long long pend_seq[2] = {0, 0}, seq = 0;
 	sg_stack_stats pstats[2];	/* a pending call's statistics (timings filled in when folded) */

@@ -18,6 +18,7 @@ SUM, MEAN, MEDIAN, MAX, MIN = range(5)
 NO_REJEC, PERCENTILE, SIGMA, SIGMEDIAN, WINSORIZED, LINEARFIT = range(6)
 NO_NORM, ADDITIVE, MULTIPLICATIVE, ADDITIVE_SCALING, MULTIPLICATIVE_SCALING = range(5)
 PATH_AUTO, PATH_SORTED = 0, 1
+RESULT_AT_COLLECT = 1        # sg_stack_desc.flags (SG_STACK_RESULT_AT_COLLECT)
 
 SG_OK = 0
 SG_ERR_GENERIC, SG_ERR_SIZE, SG_ERR_READ, SG_ERR_DEVICE = -1, -2, -3, -10
@@ -42,7 +43,8 @@ class StackDesc(ctypes.Structure):
         ("max_number_of_rows", ctypes.c_int),
         ("kernel_path", ctypes.c_int),
         ("resident_rows", ctypes.c_int * 2),
-        ("reserved", ctypes.c_int * 3),
+        ("flags", ctypes.c_int),
+        ("reserved", ctypes.c_int * 2),
     ]
 
 
@@ -370,7 +372,7 @@ def _dptr(a):
 
 def make_desc(method, N, W, H, C, rejection=NO_REJEC, normalize=NO_NORM, sig=(4.0, 3.0),
               shiftx=None, shifty=None, offset=None, mul=None, scale=None, max_thread=8,
-              max_number_of_rows=0, kernel_path=PATH_AUTO, resident_rows=None):
+              max_number_of_rows=0, kernel_path=PATH_AUTO, resident_rows=None, flags=0):
     """Build a StackDesc; returns (desc, keepalive) -- keep the arrays alive during the call.
     resident_rows = (first, end) memory rows present at the device frames (None = all)."""
     keep = []
@@ -392,6 +394,7 @@ def make_desc(method, N, W, H, C, rejection=NO_REJEC, normalize=NO_NORM, sig=(4.
     d.offset, d.mul, d.scale = _dptr(of), _dptr(mu), _dptr(sc)
     d.max_thread, d.max_number_of_rows = max_thread, max_number_of_rows
     d.kernel_path = kernel_path
+    d.flags = flags
     if resident_rows is not None:
         d.resident_rows[0], d.resident_rows[1] = int(resident_rows[0]), int(resident_rows[1])
     return d, keep

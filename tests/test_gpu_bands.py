@@ -313,13 +313,16 @@ def test_host_pull_cancel(gpu_ctx, devs):
         assert rc == 0, c.error()
 
 
+@pytest.mark.parametrize("flags", [0, sg.RESULT_AT_COLLECT])
 @pytest.mark.parametrize("method,rejection", [(sg.MEAN, sg.SIGMA), (sg.MEAN, sg.WINSORIZED),
                                               (sg.MEAN, sg.PERCENTILE), (sg.MEDIAN, sg.NO_REJEC),
-                                              (sg.MEAN, sg.NO_REJEC), (sg.MEAN, sg.LINEARFIT)])
-def test_async_bands_collect(gpu_ctx, method, rejection):
+                                              (sg.MEAN, sg.NO_REJEC), (sg.MEAN, sg.LINEARFIT),
+                                              (sg.MEAN, sg.SIGMEDIAN)])
+def test_async_bands_collect(gpu_ctx, method, rejection, flags):
     """sg_stack_u16_device_async: every band queued without waiting (more calls than the two
     counter slots, so earlier calls are folded on the way), then sg_stack_collect: the image and
-    the SUMMED rejection counters equal the oracle's"""
+    the SUMMED rejection counters equal the oracle's; with SG_STACK_RESULT_AT_COLLECT each call's
+    redo / replay / counter work runs on the tail stream beside the next band's main kernel"""
     import torch
     N, C, H, W = 40, 2, 48, 200
     frames = orc.synth(N, C, H, W, seed=61, maxshift=5)
@@ -329,7 +332,7 @@ def test_async_bands_collect(gpu_ctx, method, rejection):
     d_out = torch.zeros(C * H * W, dtype=torch.int16, device="cuda")
     full = _dev(frames)
     desc, keep = sg.make_desc(method, N, W, H, C, rejection=rejection, sig=sig, shiftx=sx, shifty=sy, max_thread=4,
-                              max_number_of_rows=H)
+                              max_number_of_rows=H, flags=flags)
     world = 5
     for r in range(world):
         b, e = sd.row_band(r, world, H)
