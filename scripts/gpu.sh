@@ -43,7 +43,7 @@ for step in "$@"; do
       k=(); [ -n "$spec" ] && k=(-k "${spec//,/ }")   # commas between the words of a -k expression
       x=-x; [ "$kind" = testall ] && x=--maxfail=8
       lim=900; [ -n "$spec" ] && lim=300     # a selection runs under a shorter limit
-      timeout -k 10 $lim python -u -m pytest tests -m gpu $x -v --timeout 200 --timeout-method thread "${k[@]}" \
+      timeout -k 10 $lim python -u -m pytest tests -m gpu $x -v --durations=15 --timeout 200 --timeout-method thread "${k[@]}" \
         > "$O/pytest_gpu.log" 2>&1; rc=$?
       # testall goes on after plain test failures (pytest exit 1), never after a crash or a timeout
       if [ $rc -ne 0 ] && { [ "$kind" = test ] || [ $rc -ne 1 ]; }; then fail test "$O/pytest_gpu.log"; fi

@@ -53,6 +53,7 @@ __global__ void k_synth_fill(uint16_t *frames, int first_frame, int nframes, int
 __global__ void k_flip_rows(const uint16_t *src, uint16_t *dst, int W, int rows);
 __global__ void k_stage_copy(uint4 *dst, const uint4 *src, unsigned int n16);
 __global__ void k_linfit_tables(double *tab, int nmax);
+__global__ void k_list_all(SgStackParams p);
 __global__ void k_ctr_finalize(unsigned long long *ctr, unsigned long long *host);
 /* host-pull readers per device and the bytes of one region read (two pinned + two device
  * staging buffers of this size per reader) */
@@ -731,9 +732,10 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 					(d->rejection == SG_SIGMEDIAN && ctx->knobs.hist_sigmedian))));
 		/* beyond the sorted kernel's 1024 frames only the histogram path runs; its redo pixels
 		 * all go to the replay / literal kernels (they take any N) */
-		if (!nreg && !hist)
-			return set_err(ctx, SG_ERR_SIZE, "this rejection supports up to 1024 frames%s (%ld); SIGMA, "
-					"WINSORIZED, PERCENTILE, SIGMEDIAN and median stacks take up to 65535", "", N);
+		/* beyond the sorted kernel's 1024 frames a stack without a histogram path (LINEARFIT, or
+		 * planes past the histogram's 32-bit offsets) goes to the literal kernel pixel by pixel: slow,
+		 * but any N as the reference (:1486-1507) */
+		const bool literal_all = !nreg && !hist;
 		const size_t npix_launch = (size_t)C * nrows * W;
 		HIPCHK(ensure(sb.flag_list, sizeof(unsigned int) * npix_launch));
 		{
@@ -903,6 +905,14 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 				HIPCHK(hipGetLastError());
 				st.launches++;
 			}
+		} else if (literal_all) {
+			HIPCHK(hipEventRecord(cev[0], s));
+			hipLaunchKernelGGL(k_list_all, dim3(1024), dim3(256), 0, s, p);
+			HIPCHK(hipGetLastError());
+			HIPCHK(hipEventRecord(cev[1], s));
+			if (int rc = to_tail())
+				return rc;
+			st.launches = 1;
 		} else {
 			HIPCHK(hipEventRecord(cev[0], s));
 			HIPCHK(launch_sorted(nreg, false, dim3((unsigned)nblk), lds, s, p, nullptr, nullptr));

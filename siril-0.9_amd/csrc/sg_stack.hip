@@ -2312,6 +2312,21 @@ k_redo_to_literal(SgStackParams p, const unsigned int *__restrict__ list, const 
 	}
 }
 
+/* every pixel of the band (all channels) queued for k_stack_literal: the route of stacks with no
+ * histogram path beyond the sorted kernel's 1024 frames */
+__global__ void __launch_bounds__(256)
+k_list_all(SgStackParams p) {
+	const int64_t nb = (int64_t)(p.row_end - p.row_begin) * p.W, total = nb * p.C;
+	for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+		const int64_t c = i / nb, r = i - c * nb;
+		const int64_t pix = (c * p.H + p.row_begin) * p.W + r;
+		sg_flag_set(p, pix, SG_CLS_LITERAL);
+		p.flag_list[i] = (unsigned int)pix;
+	}
+	if (blockIdx.x == 0 && threadIdx.x == 0)
+		*p.flag_count = (unsigned int)total;
+}
+
 template <int NM>
 __global__ void __launch_bounds__(64 * SG_REPLAY_WAVES)
 k_stack_replay(SgStackParams p) {
