@@ -217,7 +217,8 @@ def test_cfg2_median_and_percentile_whole_image(gpu_ctx):
 def test_cfg4_rgb_register_and_winsorized(gpu_ctx):
     """configs[4] on one GPU: 256 x 3 x 4000 x 6000 frames in HBM, DFT registration of layer 1's
     centred 2048 selection (golden shifts and qualities), WINSORIZED (4, 3) stack of all three
-    channels with the found shifts, 3 row bands of every channel against the oracle"""
+    channels with the found shifts, the whole image against the sort-based kernel path and 5 row
+    bands of every channel against the oracle"""
     import torch
     g = np.load(os.path.join(GOLDEN, "register_cfg4.npz"))
     N, C, H, W, layer, S, y0, x0, seed, M = (int(v) for v in g["geometry"])
@@ -232,6 +233,27 @@ def test_cfg4_rgb_register_and_winsorized(gpu_ctx):
     assert np.array_equal(qraw, g["quality_raw"])
     assert np.array_equal(q, normalize_quality(g["quality_raw"]))
     del sel
+    # 5 oracle bands of 64 rows per channel (the top and bottom ones with the zero fill of rows
+    # shifted out of the frame, 3 evenly spaced between): 8 % of the image against the oracle,
+    # run on the host in a thread while the GPU stacks the image on both kernel paths
+    starts = [0] + [int(k * (H - 64) / 4) for k in range(1, 4)] + [H - 64]
+    jobs = []
+    for c in range(C):
+        for b in starts:
+            lo, hi = max(0, b - M), min(H, b + 64 + M)
+            jobs.append((c, b, lo, fv[:, c, lo:hi, :].cpu().numpy().view(np.uint16)[:, None]))
+
+    def oracle_bands():
+        res = []
+        for c, b, lo, band in jobs:
+            rc, ref, _ = orc.stack_rejection(band, sg.WINSORIZED, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                                             max_thread=16, max_number_of_rows=16 * 24)
+            res.append((c, b, lo, rc, ref[0, b - lo:b + 64 - lo].copy()))
+        return res
+
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(1)
+    fut = pool.submit(oracle_bands)
     out = torch.zeros(C * H * W, dtype=torch.int16, device="cuda")
     torch.cuda.synchronize()
     desc, keep = sg.make_desc(sg.MEAN, N, W, H, C, rejection=sg.WINSORIZED, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
@@ -251,20 +273,11 @@ def test_cfg4_rgb_register_and_winsorized(gpu_ctx):
     assert np.array_equal(rej_s, rej), (rej_s, rej)
     del out_s
     img = out.cpu().numpy().view(np.uint16).reshape(C, H, W)
-    # 5 oracle bands of 64 rows per channel (the top and bottom ones with the zero fill of rows
-    # shifted out of the frame, 3 evenly spaced between): 8 % of the image against the oracle (the
-    # CPU oracle's time bounds it: 8 bands per channel ran past the per-test limit)
-    starts = [0] + [int(k * (H - 64) / 4) for k in range(1, 4)] + [H - 64]
-    for c in range(C):
-        for b in starts:
-            e = b + 64
-            lo, hi = max(0, b - M), min(H, e + M)
-            band = fv[:, c, lo:hi, :].cpu().numpy().view(np.uint16)[:, None]
-            rc, ref, _ = orc.stack_rejection(band, sg.WINSORIZED, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
-                                             max_thread=16, max_number_of_rows=16 * 24)
-            assert rc == 0
-            got, want = img[c, b:e], ref[0, b - lo:e - lo]
-            bad = np.argwhere(got != want)
-            assert bad.size == 0, f"channel {c} rows {b}..{e}: {len(bad)} pixels differ, first {bad[:3].tolist()}"
+    for c, b, lo, rc, want in fut.result():
+        assert rc == 0
+        got = img[c, b:b + 64]
+        bad = np.argwhere(got != want)
+        assert bad.size == 0, f"channel {c} rows {b}..{b + 64}: {len(bad)} pixels differ, first {bad[:3].tolist()}"
+    pool.shutdown()
     del frames, out, fv
     _free()
