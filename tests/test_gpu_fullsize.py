@@ -217,7 +217,7 @@ def test_cfg2_median_and_percentile_whole_image(gpu_ctx):
 def test_cfg4_rgb_register_and_winsorized(gpu_ctx):
     """configs[4] on one GPU: 256 x 3 x 4000 x 6000 frames in HBM, DFT registration of layer 1's
     centred 2048 selection (golden shifts and qualities), WINSORIZED (4, 3) stack of all three
-    channels with the found shifts, the whole image against the sort-based kernel path and 5 row
+    channels with the found shifts, the whole image against the sort-based kernel path and 3 row
     bands of every channel against the oracle"""
     import torch
     g = np.load(os.path.join(GOLDEN, "register_cfg4.npz"))
@@ -233,10 +233,10 @@ def test_cfg4_rgb_register_and_winsorized(gpu_ctx):
     assert np.array_equal(qraw, g["quality_raw"])
     assert np.array_equal(q, normalize_quality(g["quality_raw"]))
     del sel
-    # 5 oracle bands of 64 rows per channel (the top and bottom ones with the zero fill of rows
-    # shifted out of the frame, 3 evenly spaced between): 8 % of the image against the oracle,
-    # run on the host in a thread while the GPU stacks the image on both kernel paths
-    starts = [0] + [int(k * (H - 64) / 4) for k in range(1, 4)] + [H - 64]
+    # 3 oracle bands of 64 rows per channel (the top and bottom ones with the zero fill of rows
+    # shifted out of the frame, the middle one; two more per channel in the next test), run on
+    # the host in a thread while the GPU stacks the image on both kernel paths
+    starts = [0, H // 2 - 32, H - 64]
     jobs = []
     for c in range(C):
         for b in starts:
@@ -279,5 +279,36 @@ def test_cfg4_rgb_register_and_winsorized(gpu_ctx):
         bad = np.argwhere(got != want)
         assert bad.size == 0, f"channel {c} rows {b}..{b + 64}: {len(bad)} pixels differ, first {bad[:3].tolist()}"
     pool.shutdown()
+    del frames, out, fv
+    _free()
+
+
+def test_cfg4_winsorized_more_oracle_bands(gpu_ctx):
+    """configs[4]'s WINSORIZED image (golden registration shifts) at two more 64-row bands per
+    channel, at 1/4 and 3/4 of the height, against the oracle: with the previous test 5 bands per
+    channel, 8 % of the image (the oracle's CPU time bounds the coverage per test)"""
+    import torch
+    g = np.load(os.path.join(GOLDEN, "register_cfg4.npz"))
+    N, C, H, W, layer, S, y0, x0, seed, M = (int(v) for v in g["geometry"])
+    sx, sy = g["shiftx"].astype(np.int32), g["shifty"].astype(np.int32)
+    frames = torch.empty(N * C * H * W, dtype=torch.int16, device="cuda")
+    gpu_ctx.synth_fill(frames.data_ptr(), N, C, H, W, 0, H, seed, M)
+    out = torch.zeros(C * H * W, dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, C, rejection=sg.WINSORIZED, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                              max_thread=16, max_number_of_rows=H)
+    gpu_ctx.stack_device(desc, frames.data_ptr(), C * H * W, H * W, out.data_ptr(), 0, H)
+    assert gpu_ctx.stats().path == 1
+    img = out.cpu().numpy().view(np.uint16).reshape(C, H, W)
+    fv = frames.view(N, C, H, W)
+    for c in range(C):
+        for b in (H // 4 - 32, 3 * H // 4 - 32):
+            lo, hi = max(0, b - M), min(H, b + 64 + M)
+            band = fv[:, c, lo:hi, :].cpu().numpy().view(np.uint16)[:, None]
+            rc, ref, _ = orc.stack_rejection(band, sg.WINSORIZED, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                                             max_thread=16, max_number_of_rows=16 * 24)
+            assert rc == 0
+            bad = np.argwhere(img[c, b:b + 64] != ref[0, b - lo:b + 64 - lo])
+            assert bad.size == 0, f"channel {c} rows {b}..{b + 64}: {len(bad)} pixels differ, first {bad[:3].tolist()}"
     del frames, out, fv
     _free()
