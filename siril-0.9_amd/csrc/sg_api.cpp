@@ -175,6 +175,15 @@ extern "C" void sg_shutdown(sg_ctx *ctx) {
 				(void)hipEventDestroy(d.aux_ev[k]);
 		if (d.qacc_h)
 			(void)hipHostFree(d.qacc_h);
+		if (d.aux2) {
+			(void)hipStreamSynchronize(d.aux2);
+			(void)hipStreamDestroy(d.aux2);
+		}
+		for (int k = 0; k < 2; k++)
+			if (d.aux2_ev[k])
+				(void)hipEventDestroy(d.aux2_ev[k]);
+		if (d.reg_pin)
+			(void)hipHostFree(d.reg_pin);
 		(void)hipStreamDestroy(d.stream);
 	}
 	delete ctx;

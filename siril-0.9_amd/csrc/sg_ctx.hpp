@@ -65,6 +65,14 @@ struct SgDevice {
 	hipEvent_t aux_ev[2] = {nullptr, nullptr};
 	unsigned long long *qacc_h = nullptr;
 	size_t qacc_h_n = 0;
+	/* registration tables cached per side (reg_tw for reg_tab_S / reg_tab_generic, reg_tw32 for
+	 * reg_tw32_S), the pinned pair-table / result block, and aux2: the reference spectrum's
+	 * stream beside the pairs' forward rows */
+	int reg_tab_S = 0, reg_tab_generic = -1, reg_tw32_S = 0;
+	void *reg_pin = nullptr;
+	size_t reg_pin_n = 0;
+	hipStream_t aux2 = nullptr;
+	hipEvent_t aux2_ev[2] = {nullptr, nullptr};
 	SgBuf zeros;	/* zero page for out-of-frame sample loads */
 	/* stacking counters (rejection shards, flag / redo counts, sum maximum) in one device block,
 	 * cleared by one memset and read back by one D2H copy into ctr_h (pinned) */
@@ -135,6 +143,8 @@ struct SgKnobs {
 	int reg_colocc = 1;		/* SG_REG_COLOCC: 1 = fp32 column pass held to 64 VGPRs (two 1024-thread workgroups per CU: registration 6.86 -> 6.21 ms on configs[1], profiles/r03t_ab_reg_cols.log), 0 = 76 VGPRs, one workgroup */
 	int reg_wcol = 1;		/* SG_REG_WCOL: 1 = wave-level fp32 column pass at S = 2048 (k_reg_cols_xpower_w), 0 = block-level */
 	int reg_genfuse = 1;		/* SG_REG_GENFUSE: 1 = generic sides' fused column pass (k_gen_cols_xpower), 0 = rows + k_gen_xpower + rows */
+	int reg_rpw = 8;		/* SG_REG_RPW: rows per wave of the wave-level forward row pass (the next row fetched during this one's transform) */
+	int reg_refconc = 1;		/* SG_REG_REFCONC: 1 = fp32 reference spectrum on its own stream beside the first batch's forward rows */
 	int reg_rpb = 4;		/* SG_REG_RPB: rows per forward-row workgroup of the half-spectrum path (1 -> 4: 6.46 -> 5.92 ms registration on configs[1], profiles/r03u_ab_reg_rows.log) */
 	void read() {
 		hist_dbg = sg_env_int("SG_HIST_DBG", 0, 1000, 0);
@@ -171,6 +181,8 @@ struct SgKnobs {
 			reg_cw32 &= reg_cw32 - 1;
 		reg_colocc = sg_env_int("SG_REG_COLOCC", 0, 1, 1);
 		reg_rpb = sg_env_int("SG_REG_RPB", 1, 64, 4);
+		reg_refconc = sg_env_int("SG_REG_REFCONC", 0, 1, 1);
+		reg_rpw = sg_env_int("SG_REG_RPW", 1, 64, 8);
 	}
 };
 

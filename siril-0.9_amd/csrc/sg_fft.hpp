@@ -373,6 +373,15 @@ __device__ __forceinline__ void sg_top2t_add(SgTop2T<T> &a, T v, int i) {
 	a.v = nb ? v : a.v;
 	a.i = nb ? i : a.i;
 }
+/* the same for a thread that visits its indices in increasing order: an equal value never
+ * carries a lower index, so the index tie-break drops out */
+template <class T>
+__device__ __forceinline__ void sg_top2t_add_inc(SgTop2T<T> &a, T v, int i) {
+	const bool nb = v > a.v;
+	a.v2 = nb ? a.v : fmax(a.v2, v);
+	a.v = nb ? v : a.v;
+	a.i = nb ? i : a.i;
+}
 template <class T>
 __device__ __forceinline__ SgTop2 sg_top2t_wide(const SgTop2T<T> &a) {
 	SgTop2 t;

@@ -253,11 +253,59 @@ k_reg_cols_xpower(C *__restrict__ work, const C *__restrict__ spec, int S, int C
  * (sg_reg_tol).  The round-3 kernel (1024 threads, four radix-8/4 LDS passes each way) spent
  * ~15 k wave-instructions per column, mostly index arithmetic, LDS traffic and barriers.
  * ------------------------------------------------------------------------------------- */
+typedef float sg_v2f __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float2 sg_cmulf(float2 a, float2 b) {
-	return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+	const sg_v2f av = sg_v2f{a.x, a.y}, bv = sg_v2f{b.x, b.y};
+	sg_v2f r;
+	asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]\n\t"
+	    "v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
+	    : "=&v"(r) : "v"(av), "v"(bv));
+	return make_float2(r.x, r.y);
+}
+/* the same with a uniform w (a constant root: an SGPR pair, no per-use VGPR moves) */
+__device__ __forceinline__ float2 sg_cmulk(float2 a, sg_v2f w) {
+	const sg_v2f av = sg_v2f{a.x, a.y};
+	sg_v2f r;
+	asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]\n\t"
+	    "v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
+	    : "=&v"(r) : "v"(av), "s"(w));
+	return make_float2(r.x, r.y);
+}
+
+/* s v + o for a per-lane sign s = (+-1, +-1) (the lane pair's radix-2: v + o or o - v, exact) */
+__device__ __forceinline__ float2 sg_pm_add(float2 v, float2 o, sg_v2f s2) {
+	sg_v2f r;
+	asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(s2), "v"(sg_v2f{v.x, v.y}), "v"(sg_v2f{o.x, o.y}));
+	return make_float2(r.x, r.y);
+}
+/* r conj(f) (the cross power's product) */
+__device__ __forceinline__ float2 sg_rconjf(float2 r, float2 f) {
+	sg_v2f d;
+	asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]\n\t"
+	    "v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[0,0,1]"
+	    : "=&v"(d) : "v"(sg_v2f{r.x, r.y}), "v"(sg_v2f{f.x, f.y}));
+	return make_float2(d.x, d.y);
 }
 
 /* 32-point DFT of v (natural order in and out) in registers, radix-2 decimation in frequency */
+/* d times -i (forward) / +i (inverse), exact: one packed multiply by (1, -1) / (-1, 1) with the
+ * halves swapped */
+template <bool INV>
+__device__ __forceinline__ sg_v2f sg_rot_i(sg_v2f d) {
+	sg_v2f r;
+	asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(r) : "v"(d), "s"(INV ? sg_v2f{-1.0f, 1.0f} : sg_v2f{1.0f, -1.0f}));
+	return r;
+}
+__device__ __forceinline__ sg_v2f sg_cmulk2(sg_v2f a, sg_v2f w) {
+	sg_v2f r;
+	asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]\n\t"
+	    "v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
+	    : "=&v"(r) : "v"(a), "s"(w));
+	return r;
+}
+
+/* 32-point DFT of v (natural order in and out) in registers, radix-2 decimation in frequency;
+ * each complex value one packed register pair (v_pk_add / v_pk_mul + v_pk_fma per butterfly) */
 template <bool INV>
 __device__ __forceinline__ void sg_dft32_lane(float2 (&v)[32]) {
 	constexpr float C[16] = {1.0f, 0.9807852506637573f, 0.9238795042037964f, 0.8314695954322815f,
@@ -268,35 +316,35 @@ __device__ __forceinline__ void sg_dft32_lane(float2 (&v)[32]) {
 		0.7071067690849304f, 0.8314695954322815f, 0.9238795042037964f, 0.9807852506637573f, 1.0f,
 		0.9807852506637573f, 0.9238795042037964f, 0.8314695954322815f, 0.7071067690849304f,
 		0.5555702447891235f, 0.3826834261417389f, 0.19509032368659973f};
+	sg_v2f x[32];
+#pragma unroll
+	for (int k = 0; k < 32; k++)
+		x[k] = sg_v2f{v[k].x, v[k].y};
 #pragma unroll
 	for (int half = 16; half >= 1; half >>= 1) {
 #pragma unroll
 		for (int blk = 0; blk < 32; blk += 2 * half) {
 #pragma unroll
 			for (int i = 0; i < half; i++) {
-				const float2 a = v[blk + i], b = v[blk + i + half];
-				v[blk + i] = make_float2(a.x + b.x, a.y + b.y);
-				const float2 d = make_float2(a.x - b.x, a.y - b.y);
+				const sg_v2f a = x[blk + i], b = x[blk + i + half];
+				x[blk + i] = a + b;
+				const sg_v2f d = a - b;
 				const int m = i * (16 / half);	/* w_32^m, m < 16 */
-				if (m == 0) {
-					v[blk + i + half] = d;
-				} else if (m == 8) {	/* -i (forward) / +i (inverse) */
-					v[blk + i + half] = INV ? make_float2(-d.y, d.x) : make_float2(d.y, -d.x);
-				} else {
-					const float2 w = make_float2(C[m], INV ? SN[m] : -SN[m]);
-					v[blk + i + half] = sg_cmulf(d, w);
-				}
+				if (m == 0)
+					x[blk + i + half] = d;
+				else if (m == 8)
+					x[blk + i + half] = sg_rot_i<INV>(d);
+				else
+					x[blk + i + half] = sg_cmulk2(d, sg_v2f{C[m], INV ? SN[m] : -SN[m]});
 			}
 		}
 		__builtin_amdgcn_sched_barrier(0);	/* stage by stage: interleaved stages took 249 VGPRs */
 	}
-	float2 t[32];
 #pragma unroll
-	for (int k = 0; k < 32; k++)
-		t[k] = v[(int)(__builtin_bitreverse32((unsigned)k) >> 27)];
-#pragma unroll
-	for (int k = 0; k < 32; k++)
-		v[k] = t[k];
+	for (int k = 0; k < 32; k++) {
+		const sg_v2f t = x[(int)(__builtin_bitreverse32((unsigned)k) >> 27)];
+		v[k] = make_float2(t.x, t.y);
+	}
 }
 
 /* the lane-pair partner's value (lane ^ 1), DPP quad_perm [1, 0, 3, 2] */
@@ -344,16 +392,18 @@ __device__ __forceinline__ void sg_fft2048_wave(float2 (&v)[32], float2 *col, co
 	for (int i = 0; i < P; i++)
 		v[i] = col[km * TR + 2 * i + hm];
 	sg_dft32_lane<INV>(v);
+	if (hm) {	/* odd lanes: the radix-2 stage's twiddles (uniform loads, SGPR operands) */
 #pragma unroll
-	for (int k = 1; k < P; k++) {
-		const float2 t = twd[32 * k];
-		v[k] = sg_cmulf(v[k], hm ? t : make_float2(1.0f, 0.0f));
+		for (int k = 1; k < P; k++) {
+			const float2 t = twd[32 * k];
+			v[k] = sg_cmulk(v[k], sg_v2f{t.x, t.y});
+		}
 	}
+	const float sg1 = hm ? -1.0f : 1.0f;
+	const sg_v2f s2 = sg_v2f{sg1, sg1};
 #pragma unroll
-	for (int k = 0; k < P; k++) {
-		const float2 o = sg_pair_swap(v[k]);
-		v[k] = hm ? make_float2(o.x - v[k].x, o.y - v[k].y) : make_float2(v[k].x + o.x, v[k].y + o.y);
-	}
+	for (int k = 0; k < P; k++)
+		v[k] = sg_pm_add(v[k], sg_pair_swap(v[k]), s2);
 }
 
 #ifndef SG_WCOL_WPE
@@ -371,7 +421,7 @@ k_reg_cols_xpower_w(float2 *__restrict__ work, const float2 *__restrict__ spec, 
 	float2 *col = lds + wave * CS;
 	auto wsync = [] { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); };
 	/* strip -> LDS: rows of 4 columns (32 B), column c at lds + c CS */
-#pragma unroll 4
+#pragma unroll
 	for (int it = 0; it < P; it++) {
 		const int r = (threadIdx.x >> 2) + 64 * it, c = threadIdx.x & 3;
 		lds[c * CS + r] = base[(size_t)r * S + c];
@@ -391,7 +441,7 @@ k_reg_cols_xpower_w(float2 *__restrict__ work, const float2 *__restrict__ spec, 
 	 * wave keeps its LDS column for Z(-ky) and reads its reference column directly */
 	__syncthreads();	/* every wave is done with its transposes */
 	const int kx0 = x0 & (H - 1);	/* a strip lies inside one half */
-#pragma unroll 4
+#pragma unroll
 	for (int it = 0; it < P; it++) {
 		const int r = (threadIdx.x >> 2) + 64 * it, c = threadIdx.x & 3;
 		if (kx0 + c)
@@ -401,7 +451,7 @@ k_reg_cols_xpower_w(float2 *__restrict__ work, const float2 *__restrict__ spec, 
 	if (kx) {
 #pragma unroll
 		for (int k = 0; k < P; k++)
-			v[k] = sg_rconj(col[km + 32 * k + 1024 * hm], v[k]);
+			v[k] = sg_rconjf(col[km + 32 * k + 1024 * hm], v[k]);
 	} else {	/* packed column: Z = F0 + i FN, the reference likewise; needs Z(-ky) */
 		wsync();
 #pragma unroll
@@ -421,15 +471,19 @@ k_reg_cols_xpower_w(float2 *__restrict__ work, const float2 *__restrict__ spec, 
 		}
 	}
 	/* ---- inverse (unnormalised, FFTW_BACKWARD) ---- */
+	{
+		const float sg1 = hm ? -1.0f : 1.0f;
+		const sg_v2f s2 = sg_v2f{sg1, sg1};
 #pragma unroll
-	for (int k = 0; k < P; k++) {
-		const float2 o = sg_pair_swap(v[k]);
-		v[k] = hm ? make_float2(o.x - v[k].x, o.y - v[k].y) : make_float2(v[k].x + o.x, v[k].y + o.y);
+		for (int k = 0; k < P; k++)
+			v[k] = sg_pm_add(v[k], sg_pair_swap(v[k]), s2);
 	}
+	if (hm) {
 #pragma unroll
-	for (int k = 1; k < P; k++) {
-		const float2 t = tw[S + 32 * k];
-		v[k] = sg_cmulf(v[k], hm ? t : make_float2(1.0f, 0.0f));
+		for (int k = 1; k < P; k++) {
+			const float2 t = tw[S + 32 * k];
+			v[k] = sg_cmulk(v[k], sg_v2f{t.x, t.y});
+		}
 	}
 	sg_dft32_lane<true>(v);
 	wsync();
@@ -454,75 +508,80 @@ k_reg_cols_xpower_w(float2 *__restrict__ work, const float2 *__restrict__ spec, 
 	}
 }
 
-/* Wave-level fp32 forward row pass at S = 2048: one wave per row (4 rows per workgroup, no
- * block barrier), the row of a + i b through sg_fft2048_wave, then staged in natural order in
- * the wave's LDS for the separation into the half spectra A, B (k_reg_rows_fwd_half's
- * arithmetic); the frames' energies summed per wave */
+/* Wave-level fp32 forward row pass at S = 2048: one wave per row, `rpw` rows per wave (4 rows
+ * per workgroup at a time, no block barrier; the wave's next row is fetched while this one is
+ * transformed: one row at a time left every wave waiting out the full load latency, 2 waves per
+ * SIMD being all the LDS allows), the row of a + i b through sg_fft2048_wave, then staged in
+ * natural order in the wave's LDS for the separation into the half spectra A, B
+ * (k_reg_rows_fwd_half's arithmetic); the frames' energies summed per wave */
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SG_WCOL_WPE)))
 k_reg_rows_fwd_half_w(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const int *__restrict__ fb,
-		const float2 *__restrict__ tw, float2 *__restrict__ work, unsigned long long *__restrict__ energy) {
+		const float2 *__restrict__ tw, float2 *__restrict__ work, unsigned long long *__restrict__ energy, int rpw) {
 	constexpr int S = 2048, H = 1024, P = 32;
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 	const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-	const int row = blockIdx.x * 4 + wave, pair = blockIdx.y;
+	const int row0 = blockIdx.x * 4 * rpw + wave, pair = blockIdx.y;
 	float2 *col = (float2 *)smem + wave * SG_WCOL_CS;
 	const size_t plane = (size_t)S * S;
-	const uint16_t *pa = sel + (size_t)fa[pair] * plane + (size_t)row * S;
+	const uint16_t *pa = sel + (size_t)fa[pair] * plane;
 	const int b = fb[pair];
-	const uint16_t *pb = b >= 0 ? sel + (size_t)b * plane + (size_t)row * S : nullptr;
-	float2 v[P];
+	const uint16_t *pb = b >= 0 ? sel + (size_t)b * plane : nullptr;
+	uint16_t ua[P], ub[P];
+	auto fetch = [&](int row) {
+#pragma unroll
+		for (int j = 0; j < P; j++)
+			ua[j] = pa[(size_t)row * S + 64 * j + lane];
+		if (pb) {
+#pragma unroll
+			for (int j = 0; j < P; j++)
+				ub[j] = pb[(size_t)row * S + 64 * j + lane];
+		}
+	};
+	fetch(row0);
 	unsigned long long ea = 0, eb = 0;
-	/* frame a, then frame b, 8 samples in flight at a time (all 64 at once spilled) */
-#pragma unroll
-	for (int j0 = 0; j0 < P; j0 += 8) {
-		uint32_t u[8];
-#pragma unroll
-		for (int j = 0; j < 8; j++)
-			u[j] = pa[64 * (j0 + j) + lane];
-#pragma unroll
-		for (int j = 0; j < 8; j++) {
-			ea += (unsigned long long)(u[j] * u[j]);
-			v[j0 + j] = make_float2((float)u[j], 0.0f);
-		}
-		__builtin_amdgcn_sched_barrier(0);
-	}
-	if (pb) {
-#pragma unroll
-		for (int j0 = 0; j0 < P; j0 += 8) {
-			uint32_t u[8];
-#pragma unroll
-			for (int j = 0; j < 8; j++)
-				u[j] = pb[64 * (j0 + j) + lane];
-#pragma unroll
-			for (int j = 0; j < 8; j++) {
-				eb += (unsigned long long)(u[j] * u[j]);
-				v[j0 + j].y = (float)u[j];
-			}
-			__builtin_amdgcn_sched_barrier(0);
-		}
-	}
-	sg_fft2048_wave<false>(v, col, tw, lane);
 	const int km = lane >> 1, hm = lane & 1;
-	__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+	for (int rr = 0; rr < rpw; rr++) {
+		const int row = row0 + 4 * rr;
+		float2 v[P];
 #pragma unroll
-	for (int k = 0; k < P; k++)
-		col[km + 32 * k + 1024 * hm] = v[k];
-	__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-	float2 *out = work + (size_t)pair * plane + (size_t)row * S;
-#pragma unroll 4
-	for (int q = 0; q < H / 64; q++) {
-		const int kx = 64 * q + lane;
-		const float2 zk = col[kx], zm = col[kx ? S - kx : H];
-		float2 A, B;
-		if (kx == 0) {
-			A = make_float2(zk.x, zm.x);	/* A(0) + i A(S/2) */
-			B = make_float2(zk.y, zm.y);
-		} else {
-			A = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
-			B = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
+		for (int j = 0; j < P; j++) {
+			const uint32_t u = ua[j];
+			ea += (unsigned long long)(u * u);
+			v[j] = make_float2((float)u, 0.0f);
 		}
-		out[kx] = A;
-		out[H + kx] = B;
+		if (pb) {
+#pragma unroll
+			for (int j = 0; j < P; j++) {
+				const uint32_t u = ub[j];
+				eb += (unsigned long long)(u * u);
+				v[j].y = (float)u;
+			}
+		}
+		if (rr + 1 < rpw)
+			fetch(row + 4);
+		sg_fft2048_wave<false>(v, col, tw, lane);
+		__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+		for (int k = 0; k < P; k++)
+			col[km + 32 * k + 1024 * hm] = v[k];
+		__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+		float2 *out = work + (size_t)pair * plane + (size_t)row * S;
+#pragma unroll 4
+		for (int q = 0; q < H / 64; q++) {
+			const int kx = 64 * q + lane;
+			const float2 zk = col[kx], zm = col[kx ? S - kx : H];
+			float2 A, B;
+			if (kx == 0) {
+				A = make_float2(zk.x, zm.x);	/* A(0) + i A(S/2) */
+				B = make_float2(zk.y, zm.y);
+			} else {
+				A = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
+				B = make_float2(0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x));
+			}
+			out[kx] = A;
+			out[H + kx] = B;
+		}
+		__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");	/* the next row's transposes reuse col */
 	}
 	for (int o = 32; o > 0; o >>= 1) {
 		ea += __shfl_xor(ea, o, 64);
@@ -548,21 +607,26 @@ k_reg_rows_inv_half_w(const float2 *__restrict__ work, const float2 *__restrict_
 	float2 *col = (float2 *)smem + wave * SG_WCOL_CS;
 	const float2 *in = work + (size_t)pair * S * S + (size_t)row * S;
 	float2 v[P];
+	/* every load unconditional (all 64 in flight; the packed-pair lane's branch had split them
+	 * into dependent groups), the packing and conjugation applied after */
+	float2 ra[P], rb[P];
 #pragma unroll
 	for (int j = 0; j < P; j++) {
 		const int i = 64 * j + lane;
-		float2 qa, qb;
+		const int src = (i & (H - 1)) == 0 ? 0 : (i < H ? i : S - i);
+		ra[j] = in[src];
+		rb[j] = in[H + src];
+	}
+#pragma unroll
+	for (int j = 0; j < P; j++) {
+		const int i = 64 * j + lane;
+		float2 qa = ra[j], qb = rb[j];
 		if ((i & (H - 1)) == 0) {	/* kx = 0 or S/2: the packed real pair */
-			const float2 a = in[0], bb = in[H];
-			qa = make_float2(i ? a.y : a.x, 0.0f);
-			qb = make_float2(i ? bb.y : bb.x, 0.0f);
-		} else if (i < H) {
-			qa = in[i];
-			qb = in[H + i];
-		} else {
-			const float2 a = in[S - i], bb = in[H + S - i];
-			qa = make_float2(a.x, -a.y);
-			qb = make_float2(bb.x, -bb.y);
+			qa = make_float2(i ? qa.y : qa.x, 0.0f);
+			qb = make_float2(i ? qb.y : qb.x, 0.0f);
+		} else if (i >= H) {
+			qa.y = -qa.y;
+			qb.y = -qb.y;
 		}
 		v[j] = make_float2(qa.x - qb.y, qa.y + qb.x);
 	}
@@ -574,8 +638,8 @@ k_reg_rows_inv_half_w(const float2 *__restrict__ work, const float2 *__restrict_
 #pragma unroll
 	for (int k = 0; k < P; k++) {
 		const int idx = row * S + km + 32 * k + 1024 * hm;
-		sg_top2t_add(ta, v[k].x, idx);
-		sg_top2t_add(tb, v[k].y, idx);
+		sg_top2t_add_inc(ta, v[k].x, idx);	/* idx grows with k */
+		sg_top2t_add_inc(tb, v[k].y, idx);
 	}
 	SgTop2 wa = sg_top2t_wide(ta), wb = sg_top2t_wide(tb);
 	sg_top2_wave(wa);
@@ -1549,53 +1613,65 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	SgGenTables tbl;
 	memset(&tbl, 0, sizeof tbl);
 	{
-		std::vector<double> tw;
-		make_twiddles(S, tw);
-		size_t total = tw.size();
-		std::vector<double> twm, ch, bh;
-		if (generic && !make_plan(S, pl)) {
+		const bool blue = generic && !make_plan(S, pl);
+		size_t m = 1;
+		if (blue) {
 			pl.bluestein = 1;
 			pl.m = 1;
 			while (pl.m < 2 * S - 1)
 				pl.m <<= 1;
-			const int m = pl.m;
-			make_twiddles(m, twm);
-			ch.assign(2 * (size_t)S, 0.0);
-			std::vector<double> br(m, 0.0), bi(m, 0.0);
-			for (int j = 0; j < S; j++) {
-				const long long q = ((long long)j * j) % (2ll * S);	/* j^2 mod 2S keeps the angle exact */
-				const double a = -M_PI * (double)q / (double)S;
-				ch[2 * j] = cos(a);
-				ch[2 * j + 1] = sin(a);
-				br[j] = ch[2 * j];
-				bi[j] = -ch[2 * j + 1];	/* b_j = conj c_j */
-				if (j) {
-					br[m - j] = br[j];
-					bi[m - j] = bi[j];
+			m = pl.m;
+		}
+		/* table layout: tw (4 S), then for Bluestein twm (4 m), the chirp (2 S), bhat (2 m) */
+		const size_t n_tw = 4 * (size_t)S, n_twm = blue ? 4 * m : 0, n_ch = blue ? 2 * (size_t)S : 0;
+		const size_t total = n_tw + n_twm + n_ch + (blue ? 2 * m : 0);
+		/* the tables depend on S (and the path) only: uploaded when either changes */
+		if (dv.reg_tab_S != S || dv.reg_tab_generic != (int)generic) {
+			std::vector<double> tw, twm, ch, bh;
+			make_twiddles(S, tw);
+			if (blue) {
+				make_twiddles((int)m, twm);
+				ch.assign(2 * (size_t)S, 0.0);
+				std::vector<double> br(m, 0.0), bi(m, 0.0);
+				for (int j = 0; j < S; j++) {
+					const long long q = ((long long)j * j) % (2ll * S);	/* j^2 mod 2S keeps the angle exact */
+					const double a = -M_PI * (double)q / (double)S;
+					ch[2 * j] = cos(a);
+					ch[2 * j + 1] = sin(a);
+					br[j] = ch[2 * j];
+					bi[j] = -ch[2 * j + 1];	/* b_j = conj c_j */
+					if (j) {
+						br[m - j] = br[j];
+						bi[m - j] = bi[j];
+					}
+				}
+				host_fft_pow2(br, bi, (int)m);
+				bh.assign(2 * m, 0.0);
+				for (size_t k = 0; k < m; k++) {
+					bh[2 * k] = br[k];
+					bh[2 * k + 1] = bi[k];
 				}
 			}
-			host_fft_pow2(br, bi, m);
-			bh.assign(2 * (size_t)m, 0.0);
-			for (int k = 0; k < m; k++) {
-				bh[2 * k] = br[k];
-				bh[2 * k + 1] = bi[k];
+			dv.reg_tab_S = 0;
+			HIPCHK(ensure(dv.reg_tw, sizeof(double) * total));
+			double *d = (double *)dv.reg_tw.p;
+			HIPCHK(hipMemcpyAsync(d, tw.data(), sizeof(double) * n_tw, hipMemcpyHostToDevice, s));
+			if (blue) {
+				HIPCHK(hipMemcpyAsync(d + n_tw, twm.data(), sizeof(double) * n_twm, hipMemcpyHostToDevice, s));
+				HIPCHK(hipMemcpyAsync(d + n_tw + n_twm, ch.data(), sizeof(double) * n_ch, hipMemcpyHostToDevice, s));
+				HIPCHK(hipMemcpyAsync(d + n_tw + n_twm + n_ch, bh.data(), sizeof(double) * 2 * m, hipMemcpyHostToDevice, s));
 			}
-			total += twm.size() + ch.size() + bh.size();
+			HIPCHK(hipStreamSynchronize(s));	/* the host vectors die here */
+			dv.reg_tab_S = S;
+			dv.reg_tab_generic = (int)generic;
 		}
-		HIPCHK(ensure(dv.reg_tw, sizeof(double) * total));
 		double *d = (double *)dv.reg_tw.p;
-		HIPCHK(hipMemcpyAsync(d, tw.data(), sizeof(double) * tw.size(), hipMemcpyHostToDevice, s));
 		tbl.tw = (const sg_c64 *)d;
-		if (pl.bluestein) {
-			double *d2 = d + tw.size(), *d3 = d2 + twm.size(), *d4 = d3 + ch.size();
-			HIPCHK(hipMemcpyAsync(d2, twm.data(), sizeof(double) * twm.size(), hipMemcpyHostToDevice, s));
-			HIPCHK(hipMemcpyAsync(d3, ch.data(), sizeof(double) * ch.size(), hipMemcpyHostToDevice, s));
-			HIPCHK(hipMemcpyAsync(d4, bh.data(), sizeof(double) * bh.size(), hipMemcpyHostToDevice, s));
-			tbl.twm = (const sg_c64 *)d2;
-			tbl.chirp = (const sg_c64 *)d3;
-			tbl.bhat = (const sg_c64 *)d4;
+		if (blue) {
+			tbl.twm = (const sg_c64 *)(d + n_tw);
+			tbl.chirp = (const sg_c64 *)(d + n_tw + n_twm);
+			tbl.bhat = (const sg_c64 *)(d + n_tw + n_twm + n_ch);
 		}
-		HIPCHK(hipStreamSynchronize(s));	/* the host vectors die here */
 	}
 	const sg_c64 *tw = tbl.tw;
 
@@ -1606,9 +1682,7 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	qframes.insert(qframes.end(), todo.begin(), todo.end());
 	std::vector<double> qual;
 	bool q_launched = false;
-	int rc = reg_quality_launch(ctx, dv, s, d_sel, S, qframes, &q_launched);
-	if (rc)
-		return rc;
+	int rc = SG_OK;
 
 	/* precision of the main passes: the power-of-two half-spectrum passes run in fp32
 	 * (SG_REG_FP=32, default: half the plane bytes and LDS), and a pair whose correlation
@@ -1660,6 +1734,9 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	const int colocc = ctx->knobs.reg_colocc;
 	/* the wave-level fp32 column pass: S = 2048 only (32 x 64 four-step transforms) */
 	const bool wcol = S == 2048 && ctx->knobs.reg_wcol;
+	int rpw = ctx->knobs.reg_rpw;	/* A/B knob SG_REG_RPW: rows per wave of the wave-level forward rows */
+	while (rpw > 1 && (S / 4) % rpw)
+		rpw >>= 1;
 	const size_t wcol_lds = (size_t)4 * SG_WCOL_CS * sizeof(float2);
 	/* rows per forward-row workgroup (the next row prefetched during this one's transform) */
 	int rpb = ctx->knobs.reg_rpb;
@@ -1753,15 +1830,27 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	/* fp32 twiddles, rounded from the fp64 table (behind the fp64 tables in reg_tw) */
 	const float2 *tw32 = nullptr;
 	if (fp32) {
-		HIPCHK(ensure(dv.reg_tw32, 2 * (size_t)S * sizeof(float2)));
-		std::vector<double> t64;
-		make_twiddles(S, t64);
-		std::vector<float> t32(t64.size());
-		for (size_t i = 0; i < t64.size(); i++)
-			t32[i] = (float)t64[i];
-		HIPCHK(hipMemcpyAsync(dv.reg_tw32.p, t32.data(), sizeof(float) * t32.size(), hipMemcpyHostToDevice, s));
-		HIPCHK(hipStreamSynchronize(s));
+		if (dv.reg_tw32_S != S) {
+			dv.reg_tw32_S = 0;
+			HIPCHK(ensure(dv.reg_tw32, 2 * (size_t)S * sizeof(float2)));
+			std::vector<double> t64;
+			make_twiddles(S, t64);
+			std::vector<float> t32(t64.size());
+			for (size_t i = 0; i < t64.size(); i++)
+				t32[i] = (float)t64[i];
+			HIPCHK(hipMemcpyAsync(dv.reg_tw32.p, t32.data(), sizeof(float) * t32.size(), hipMemcpyHostToDevice, s));
+			HIPCHK(hipStreamSynchronize(s));
+			dv.reg_tw32_S = S;
+		}
 		tw32 = (const float2 *)dv.reg_tw32.p;
+	}
+
+	const bool ref_conc = fp32 && ctx->knobs.reg_refconc;	/* A/B knob SG_REG_REFCONC */
+	bool ref_pending = false;
+	if (ref_conc && !dv.aux2) {
+		HIPCHK(hipStreamCreateWithFlags(&dv.aux2, hipStreamNonBlocking));
+		for (int k = 0; k < 2; k++)
+			HIPCHK(hipEventCreateWithFlags(&dv.aux2_ev[k], hipEventDisableTiming));
 	}
 
 	/* pair k = frames todo[2k], todo[2k+1] (-1: odd count, imaginary part zero); slot NP is
@@ -1774,8 +1863,23 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	}
 	hfa[NP] = ref_image;
 	hfb[NP] = -1;
-	HIPCHK(hipMemcpyAsync(d_fa, hfa.data(), sizeof(int) * (NP + 1), hipMemcpyHostToDevice, s));
-	HIPCHK(hipMemcpyAsync(d_fb, hfb.data(), sizeof(int) * (NP + 1), hipMemcpyHostToDevice, s));
+	/* the pair table goes up, and the results come back, through a pinned block (the previous
+	 * call's copies are done: every call ends on a stream synchronize) */
+	const size_t pin_res = ((size_t)2 * (NP + 1) * sizeof(int) + 63) & ~(size_t)63;
+	const size_t pin_bytes = pin_res + (size_t)NP * sizeof(SgRegOut);
+	if (dv.reg_pin_n < pin_bytes) {
+		if (dv.reg_pin)
+			(void)hipHostFree(dv.reg_pin);
+		dv.reg_pin = nullptr;
+		dv.reg_pin_n = 0;
+		HIPCHK(hipHostMalloc(&dv.reg_pin, pin_bytes));
+		dv.reg_pin_n = pin_bytes;
+	}
+	int *pfab = (int *)dv.reg_pin;
+	SgRegOut *pout = (SgRegOut *)((char *)dv.reg_pin + pin_res);
+	memcpy(pfab, hfa.data(), sizeof(int) * (NP + 1));
+	memcpy(pfab + (NP + 1), hfb.data(), sizeof(int) * (NP + 1));
+	HIPCHK(hipMemcpyAsync(d_fa, pfab, sizeof(int) * 2 * (NP + 1), hipMemcpyHostToDevice, s));	/* d_fb = d_fa + NP + 1 */
 
 	const dim3 tgrid((S + 31) / 32, (S + 31) / 32);
 	/* generic passes up to the cross power's inverse: transposed spectrum of the rows of `fa`
@@ -1834,12 +1938,16 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	};
 	auto half32 = [&](const int *fa, const int *fb, int np, unsigned long long *en) -> int {
 		if (wcol)
-			hipLaunchKernelGGL(k_reg_rows_fwd_half_w, dim3(S / 4, np), dim3(256), wcol_lds, s, d_sel, fa, fb, tw32,
-					work32, en);
+			hipLaunchKernelGGL(k_reg_rows_fwd_half_w, dim3(S / 4 / rpw, np), dim3(256), wcol_lds, s, d_sel, fa, fb, tw32,
+					work32, en, rpw);
 		else
 			hipLaunchKernelGGL(k_reg_rows_fwd_half<float2>, dim3(S / rpb, np), dim3(row_thr), row_lds32, s, d_sel, fa,
 					fb, S, tw32, work32, en, rpb);
 		HIPCHK(hipGetLastError());
+		if (ref_pending) {	/* the reference spectrum, from its stream */
+			HIPCHK(hipStreamWaitEvent(s, dv.aux2_ev[1], 0));
+			ref_pending = false;
+		}
 		if (wcol)	/* S = 2048: the wave-level column pass (SG_REG_WCOL=0: the block-level one, A/B) */
 			hipLaunchKernelGGL(k_reg_cols_xpower_w, dim3(S / 4, np), dim3(256), wcol_lds, s, work32,
 					(const float2 *)spec32, tw32, xcdmap);
@@ -1863,6 +1971,13 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		return SG_OK;
 	};
 
+	/* the quality estimate on the aux stream, queued behind the main stream's table uploads and
+	 * fills (queued ahead of them, its long-running workgroups held the fills' single workgroup
+	 * back 0.2 ms, profiles/r05m_*) */
+	rc = reg_quality_launch(ctx, dv, s, d_sel, S, qframes, &q_launched);
+	if (rc)
+		return rc;
+
 	/* reference spectrum R = FFT2(ref) (half layout: the A' half only; generic: transposed) */
 	if (generic) {
 		gen_rows(dim3(S, 1), d_sel, d_fa + NP, d_fb + NP, work, S, pl,
@@ -1873,15 +1988,29 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 		gen_rows(dim3(S, 1), d_sel, d_fa + NP, d_fb + NP, spec, S, pl,
 				tbl, (int)SG_GEN_C2C, 0, energy, best, (const SgRegOut *)nullptr, (SgCand *)nullptr);
 	} else if (fp32) {
-		hipLaunchKernelGGL(k_reg_rows_fwd_half<float2>, dim3(S / rpb, 1), dim3(row_thr), row_lds32, s, d_sel, d_fa + NP,
+		/* the reference spectrum on its own stream beside the first batch's forward rows (which do
+		 * not read it; the batch's column pass waits for it).  One workgroup per CU at most: run
+		 * alone it is 0.27 ms of latency-bound passes ahead of every pair (profiles/r05l_*) */
+		hipStream_t rs = s;
+		if (ref_conc) {
+			HIPCHK(hipEventRecord(dv.aux2_ev[0], s));
+			HIPCHK(hipStreamWaitEvent(dv.aux2, dv.aux2_ev[0], 0));
+			rs = dv.aux2;
+		}
+		hipLaunchKernelGGL(k_reg_rows_fwd_half<float2>, dim3(S / rpb, 1), dim3(row_thr), row_lds32, rs, d_sel, d_fa + NP,
 				d_fb + NP, S, tw32, spec32, energy, rpb);
 		HIPCHK(hipGetLastError());
 		if (ept32 == 16)
-			hipLaunchKernelGGL((k_reg_cols<float2, 16>), dim3(S / 2 / CW32, 1), dim3(colh_thr32), colh_lds32, s, spec32,
+			hipLaunchKernelGGL((k_reg_cols<float2, 16>), dim3(S / 2 / CW32, 1), dim3(colh_thr32), colh_lds32, rs, spec32,
 					S, logS, CW32, tw32, 0, xcdmap);
 		else
-			hipLaunchKernelGGL((k_reg_cols<float2, 8>), dim3(S / 2 / CW32, 1), dim3(colh_thr32), colh_lds32, s, spec32,
+			hipLaunchKernelGGL((k_reg_cols<float2, 8>), dim3(S / 2 / CW32, 1), dim3(colh_thr32), colh_lds32, rs, spec32,
 					S, logS, CW32, tw32, 0, xcdmap);
+		if (ref_conc) {
+			HIPCHK(hipGetLastError());
+			HIPCHK(hipEventRecord(dv.aux2_ev[1], dv.aux2));
+			ref_pending = true;
+		}
 	} else {
 		hipLaunchKernelGGL(k_reg_rows_fwd_half<sg_c64>, dim3(S / rpb, 1), dim3(row_thr), row_lds, s, d_sel, d_fa + NP,
 				d_fb + NP, S, tw, spec, energy, rpb);
@@ -1915,9 +2044,15 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 				d_out + p0);
 		HIPCHK(hipGetLastError());
 	}
+	if (ref_pending) {
+		HIPCHK(hipStreamWaitEvent(s, dv.aux2_ev[1], 0));
+		ref_pending = false;
+	}
 	if (npairs_total > 0)
-		HIPCHK(hipMemcpyAsync(hout.data(), d_out, sizeof(SgRegOut) * npairs_total, hipMemcpyDeviceToHost, s));
+		HIPCHK(hipMemcpyAsync(pout, d_out, sizeof(SgRegOut) * npairs_total, hipMemcpyDeviceToHost, s));
 	HIPCHK(hipStreamSynchronize(s));
+	if (npairs_total > 0)
+		memcpy(hout.data(), pout, sizeof(SgRegOut) * npairs_total);
 
 	/* near ties (the runner-up within the tolerance of the maximum): re-run those pairs.  After
 	 * fp32 passes, first in fp64 (a fresh arg-max at the fp64 tolerance); what is still a near
