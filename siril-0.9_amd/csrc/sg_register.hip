@@ -410,8 +410,50 @@ __device__ __forceinline__ void sg_fft2048_wave(float2 (&v)[32], float2 *col, co
 #define SG_WCOL_WPE 2
 #endif
 #define SG_WCOL_CS 2120	/* LDS float2 per column: 2048 (strip) / 32 x 66 (transposes), +8 for the strip's banks */
+/* specp: the reference spectrum in the column pass's lane order, specp[(kx 32 + k) 64 + 2 km + hm]
+ * = spec[ky][kx] at ky = km + 32 k + 1024 hm (kx < S / 2), so that the pass reads its reference
+ * column with one coalesced 512-B load per k (issued before its forward transform) instead of
+ * staging a strip through LDS between two block barriers. */
+/* the reference spectrum's forward column pass at S = 2048, wave-level (k_reg_cols_xpower_w's
+ * strip staging and transform): columns [0, S/2) of the row-transformed reference plane, written
+ * straight into specp's lane order (coalesced 512-B stores), and column 0 also back in natural
+ * order (the packed column's wave reads it by ky).  Replaces k_reg_cols + k_spec_perm on the
+ * wave-level path (one workgroup per CU there, 0.39 ms beside the pairs' forward rows). */
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SG_WCOL_WPE)))
-k_reg_cols_xpower_w(float2 *__restrict__ work, const float2 *__restrict__ spec, const float2 *__restrict__ tw, int xcdmap) {
+k_reg_cols_fwd_perm_w(float2 *__restrict__ spec, float2 *__restrict__ specp, const float2 *__restrict__ tw) {
+	constexpr int S = 2048, P = 32, CS = SG_WCOL_CS;
+	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+	float2 *lds = (float2 *)smem;
+	const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+	const int x0 = blockIdx.x * 4;
+	float2 *col = lds + wave * CS;
+#pragma unroll
+	for (int it = 0; it < P; it++) {
+		const int r = (threadIdx.x >> 2) + 64 * it, c = threadIdx.x & 3;
+		lds[c * CS + r] = spec[(size_t)r * S + x0 + c];
+	}
+	__syncthreads();
+	float2 v[P];
+#pragma unroll
+	for (int j = 0; j < P; j++)
+		v[j] = col[64 * j + lane];
+	sg_fft2048_wave<false>(v, col, tw, lane);
+	const int kx = x0 + wave, km = lane >> 1, hm = lane & 1;
+	float2 *sp = specp + (size_t)kx * S;
+#pragma unroll
+	for (int k = 0; k < P; k++)
+		sp[64 * k + lane] = v[k];
+	if (kx == 0) {
+#pragma unroll
+		for (int k = 0; k < P; k++)
+			spec[(size_t)(km + 32 * k + 1024 * hm) * S] = v[k];
+	}
+}
+
+template <bool PERM>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SG_WCOL_WPE)))
+k_reg_cols_xpower_w(float2 *__restrict__ work, const float2 *__restrict__ spec, const float2 *__restrict__ specp,
+		const float2 *__restrict__ tw, int xcdmap) {
 	constexpr int S = 2048, H = 1024, P = 32, CS = SG_WCOL_CS, TR = 66;
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 	float2 *lds = (float2 *)smem;
@@ -431,27 +473,44 @@ k_reg_cols_xpower_w(float2 *__restrict__ work, const float2 *__restrict__ spec, 
 #pragma unroll
 	for (int j = 0; j < P; j++)
 		v[j] = col[64 * j + lane];
-	/* ---- forward ---- */
-	sg_fft2048_wave<false>(v, col, tw, lane);
 	const int km = lane >> 1, hm = lane & 1;
-	/* ---- cross power at ky = km + 32 k + 1024 hm ---- */
 	const int kx = (x0 + wave) & (H - 1);
-	/* the reference spectrum's strip through LDS (coalesced 32-B rows, as the work strip; read
-	 * per lane at its ky it touched 64 rows per instruction), except a packed column 0, whose
-	 * wave keeps its LDS column for Z(-ky) and reads its reference column directly */
-	__syncthreads();	/* every wave is done with its transposes */
-	const int kx0 = x0 & (H - 1);	/* a strip lies inside one half */
-#pragma unroll
-	for (int it = 0; it < P; it++) {
-		const int r = (threadIdx.x >> 2) + 64 * it, c = threadIdx.x & 3;
-		if (kx0 + c)
-			lds[c * CS + r] = spec[(size_t)r * S + kx0 + c];
-	}
-	__syncthreads();
-	if (kx) {
+	/* PERM: the reference column's loads issued now, in flight during the forward transform */
+	float2 r[P];
+	if (PERM && kx) {
+		const float2 *sp = specp + (size_t)kx * S;
 #pragma unroll
 		for (int k = 0; k < P; k++)
-			v[k] = sg_rconjf(col[km + 32 * k + 1024 * hm], v[k]);
+			r[k] = sp[64 * k + lane];
+	}
+	/* ---- forward ---- */
+	sg_fft2048_wave<false>(v, col, tw, lane);
+	/* ---- cross power at ky = km + 32 k + 1024 hm ---- */
+	/* PERM: the reference column from specp, in lane order.  Otherwise the reference spectrum's
+	 * strip through LDS (coalesced 32-B rows, as the work strip; read per lane at its ky it
+	 * touched 64 rows per instruction).  A packed column 0's wave keeps its LDS column for
+	 * Z(-ky) and reads its reference column directly. */
+	if (!PERM) {
+		__syncthreads();	/* every wave is done with its transposes */
+		const int kx0 = x0 & (H - 1);	/* a strip lies inside one half */
+#pragma unroll
+		for (int it = 0; it < P; it++) {
+			const int r = (threadIdx.x >> 2) + 64 * it, c = threadIdx.x & 3;
+			if (kx0 + c)
+				lds[c * CS + r] = spec[(size_t)r * S + kx0 + c];
+		}
+		__syncthreads();
+	}
+	if (kx) {
+		if (PERM) {
+#pragma unroll
+			for (int k = 0; k < P; k++)
+				v[k] = sg_rconjf(r[k], v[k]);
+		} else {
+#pragma unroll
+			for (int k = 0; k < P; k++)
+				v[k] = sg_rconjf(col[km + 32 * k + 1024 * hm], v[k]);
+		}
 	} else {	/* packed column: Z = F0 + i FN, the reference likewise; needs Z(-ky) */
 		wsync();
 #pragma unroll
@@ -501,10 +560,18 @@ k_reg_cols_xpower_w(float2 *__restrict__ work, const float2 *__restrict__ spec, 
 	for (int j = 0; j < P; j++)
 		col[64 * j + lane] = v[j];
 	__syncthreads();
-#pragma unroll 4
-	for (int it = 0; it < P; it++) {
-		const int r = (threadIdx.x >> 2) + 64 * it, c = threadIdx.x & 3;
-		base[(size_t)r * S + c] = lds[c * CS + r];
+	{	/* every LDS read issued before the stores (one LDS latency, not eight) */
+		float2 o[P];
+#pragma unroll
+		for (int it = 0; it < P; it++) {
+			const int r = (threadIdx.x >> 2) + 64 * it, c = threadIdx.x & 3;
+			o[it] = lds[c * CS + r];
+		}
+#pragma unroll
+		for (int it = 0; it < P; it++) {
+			const int r = (threadIdx.x >> 2) + 64 * it, c = threadIdx.x & 3;
+			base[(size_t)r * S + c] = o[it];
+		}
 	}
 }
 
@@ -641,9 +708,9 @@ k_reg_rows_inv_half_w(const float2 *__restrict__ work, const float2 *__restrict_
 		sg_top2t_add_inc(ta, v[k].x, idx);	/* idx grows with k */
 		sg_top2t_add_inc(tb, v[k].y, idx);
 	}
-	SgTop2 wa = sg_top2t_wide(ta), wb = sg_top2t_wide(tb);
-	sg_top2_wave(wa);
-	sg_top2_wave(wb);
+	sg_top2t_wave(ta);
+	sg_top2t_wave(tb);
+	const SgTop2 wa = sg_top2t_wide(ta), wb = sg_top2t_wide(tb);
 	if (lane == 0) {
 		best[(size_t)pair * S + row].a = wa;
 		best[(size_t)pair * S + row].b = wb;
@@ -1791,7 +1858,11 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 				(int)colh_lds32);
 		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower<float2, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)colh_lds32);
-		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower_w, hipFuncAttributeMaxDynamicSharedMemorySize,
+		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower_w<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+				(int)wcol_lds);
+		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower_w<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+				(int)wcol_lds);
+		(void)hipFuncSetAttribute((const void *)k_reg_cols_fwd_perm_w, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)wcol_lds);
 		(void)hipFuncSetAttribute((const void *)k_reg_rows_fwd_half_w, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)wcol_lds);
@@ -1806,7 +1877,11 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	 * the per-pair results, the frames' energies (two sets: the main passes and the near-tie
 	 * re-runs) and the near-tie candidates of one batch */
 	const int NP = npairs_total > 0 ? npairs_total : 1;
-	HIPCHK(ensure(dv.reg_spec, plane * sizeof(sg_c64) + (fp32 ? plane * sizeof(float2) : 0)));
+	/* wave-level column pass: the fp32 reference spectrum also in its lane order (k_spec_perm,
+	 * SG_REG_SPECP=0: staged through LDS, A/B) */
+	const bool specp_on = fp32 && wcol && ctx->knobs.reg_specp;
+	HIPCHK(ensure(dv.reg_spec, plane * sizeof(sg_c64) + (fp32 ? plane * sizeof(float2) : 0) +
+			(specp_on ? plane / 2 * sizeof(float2) : 0)));
 	/* the fp64 near-tie re-runs use the same buffer: at least one fp64 plane (B64 >= 1 even
 	 * when the fp32 batch is a single pair, whose plane is half that size) */
 	HIPCHK(ensure(dv.reg_work, std::max((size_t)Bc * pair_bytes, (size_t)B64 * plane * sizeof(sg_c64))));
@@ -1820,6 +1895,7 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	char *wsp = (char *)dv.reg_best.p;
 	sg_c64 *spec = (sg_c64 *)dv.reg_spec.p, *work = (sg_c64 *)dv.reg_work.p;
 	float2 *spec32 = (float2 *)((char *)dv.reg_spec.p + plane * sizeof(sg_c64)), *work32 = (float2 *)dv.reg_work.p;
+	float2 *specp32 = specp_on ? spec32 + plane : nullptr;
 	sg_c64 *work2 = work + (size_t)Bc * plane;	/* generic path: transposed planes */
 	SgBest *best = (SgBest *)wsp;
 	SgRegOut *d_out = (SgRegOut *)(wsp + o_out), *d_res2 = (SgRegOut *)(wsp + o_res2);
@@ -1948,9 +2024,12 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 			HIPCHK(hipStreamWaitEvent(s, dv.aux2_ev[1], 0));
 			ref_pending = false;
 		}
-		if (wcol)	/* S = 2048: the wave-level column pass (SG_REG_WCOL=0: the block-level one, A/B) */
-			hipLaunchKernelGGL(k_reg_cols_xpower_w, dim3(S / 4, np), dim3(256), wcol_lds, s, work32,
-					(const float2 *)spec32, tw32, xcdmap);
+		if (wcol && specp32)	/* S = 2048: the wave-level column pass (SG_REG_WCOL=0: the block-level one, A/B) */
+			hipLaunchKernelGGL(k_reg_cols_xpower_w<true>, dim3(S / 4, np), dim3(256), wcol_lds, s, work32,
+					(const float2 *)spec32, (const float2 *)specp32, tw32, xcdmap);
+		else if (wcol)
+			hipLaunchKernelGGL(k_reg_cols_xpower_w<false>, dim3(S / 4, np), dim3(256), wcol_lds, s, work32,
+					(const float2 *)spec32, (const float2 *)nullptr, tw32, xcdmap);
 		else if (ept32 == 16)
 			hipLaunchKernelGGL((k_reg_cols_xpower<float2, 16>), dim3(S / CW32, np), dim3(colh_thr32), colh_lds32, s,
 					work32, (const float2 *)spec32, S, CW32, tw32, xcdmap, 1);
@@ -1997,15 +2076,22 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 			HIPCHK(hipStreamWaitEvent(dv.aux2, dv.aux2_ev[0], 0));
 			rs = dv.aux2;
 		}
-		hipLaunchKernelGGL(k_reg_rows_fwd_half<float2>, dim3(S / rpb, 1), dim3(row_thr), row_lds32, rs, d_sel, d_fa + NP,
-				d_fb + NP, S, tw32, spec32, energy, rpb);
-		HIPCHK(hipGetLastError());
-		if (ept32 == 16)
-			hipLaunchKernelGGL((k_reg_cols<float2, 16>), dim3(S / 2 / CW32, 1), dim3(colh_thr32), colh_lds32, rs, spec32,
-					S, logS, CW32, tw32, 0, xcdmap);
-		else
-			hipLaunchKernelGGL((k_reg_cols<float2, 8>), dim3(S / 2 / CW32, 1), dim3(colh_thr32), colh_lds32, rs, spec32,
-					S, logS, CW32, tw32, 0, xcdmap);
+		if (specp32) {	/* wave-level passes: one row per wave, the columns straight into lane order */
+			hipLaunchKernelGGL(k_reg_rows_fwd_half_w, dim3(S / 4, 1), dim3(256), wcol_lds, rs, d_sel, d_fa + NP,
+					d_fb + NP, tw32, spec32, energy, 1);
+			HIPCHK(hipGetLastError());
+			hipLaunchKernelGGL(k_reg_cols_fwd_perm_w, dim3(S / 2 / 4), dim3(256), wcol_lds, rs, spec32, specp32, tw32);
+		} else {
+			hipLaunchKernelGGL(k_reg_rows_fwd_half<float2>, dim3(S / rpb, 1), dim3(row_thr), row_lds32, rs, d_sel,
+					d_fa + NP, d_fb + NP, S, tw32, spec32, energy, rpb);
+			HIPCHK(hipGetLastError());
+			if (ept32 == 16)
+				hipLaunchKernelGGL((k_reg_cols<float2, 16>), dim3(S / 2 / CW32, 1), dim3(colh_thr32), colh_lds32, rs,
+						spec32, S, logS, CW32, tw32, 0, xcdmap);
+			else
+				hipLaunchKernelGGL((k_reg_cols<float2, 8>), dim3(S / 2 / CW32, 1), dim3(colh_thr32), colh_lds32, rs,
+						spec32, S, logS, CW32, tw32, 0, xcdmap);
+		}
 		if (ref_conc) {
 			HIPCHK(hipGetLastError());
 			HIPCHK(hipEventRecord(dv.aux2_ev[1], dv.aux2));
