@@ -410,6 +410,13 @@ __device__ __forceinline__ void sg_fft2048_wave(float2 (&v)[32], float2 *col, co
 #define SG_WCOL_WPE 2
 #endif
 #define SG_WCOL_CS 2120	/* LDS float2 per column: 2048 (strip) / 32 x 66 (transposes), +8 for the strip's banks */
+/* physical LDS row of strip row r in column c: rows of columns 2, 3 XOR 4, so that the strip's
+ * 8-byte stores (32 banks, 16-lane groups: 4 rows x 4 columns) and its 8-byte reads (64 banks,
+ * 32-lane groups: 8 rows x 4 columns, CS = 8 mod 32) are both conflict-free (a 2-way conflict on
+ * the stores was 20 % of the column pass's LDS cycles) */
+__device__ __forceinline__ int sg_strip_row(int r, int c) {
+	return r ^ ((c >> 1) << 2);
+}
 /* specp: the reference spectrum in the column pass's lane order, specp[(kx 32 + k) 64 + 2 km + hm]
  * = spec[ky][kx] at ky = km + 32 k + 1024 hm (kx < S / 2), so that the pass reads its reference
  * column with one coalesced 512-B load per k (issued before its forward transform) instead of
@@ -427,16 +434,17 @@ k_reg_cols_fwd_perm_w(float2 *__restrict__ spec, float2 *__restrict__ specp, con
 	const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 	const int x0 = blockIdx.x * 4;
 	float2 *col = lds + wave * CS;
+	const int sw = (wave >> 1) << 2;	/* sg_strip_row of this wave's column */
 #pragma unroll
 	for (int it = 0; it < P; it++) {
 		const int r = (threadIdx.x >> 2) + 64 * it, c = threadIdx.x & 3;
-		lds[c * CS + r] = spec[(size_t)r * S + x0 + c];
+		lds[c * CS + sg_strip_row(r, c)] = spec[(size_t)r * S + x0 + c];
 	}
 	__syncthreads();
 	float2 v[P];
 #pragma unroll
 	for (int j = 0; j < P; j++)
-		v[j] = col[64 * j + lane];
+		v[j] = col[64 * j + (lane ^ sw)];
 	sg_fft2048_wave<false>(v, col, tw, lane);
 	const int kx = x0 + wave, km = lane >> 1, hm = lane & 1;
 	float2 *sp = specp + (size_t)kx * S;
@@ -461,18 +469,19 @@ k_reg_cols_xpower_w(float2 *__restrict__ work, const float2 *__restrict__ spec, 
 	const int x0 = sg_xcd_strip(blockIdx.x, gridDim.x, xcdmap) * 4, pair = blockIdx.y;
 	float2 *base = work + (size_t)pair * S * S + x0;
 	float2 *col = lds + wave * CS;
+	const int sw = (wave >> 1) << 2;	/* sg_strip_row of this wave's column */
 	auto wsync = [] { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); };
 	/* strip -> LDS: rows of 4 columns (32 B), column c at lds + c CS */
 #pragma unroll
 	for (int it = 0; it < P; it++) {
 		const int r = (threadIdx.x >> 2) + 64 * it, c = threadIdx.x & 3;
-		lds[c * CS + r] = base[(size_t)r * S + c];
+		lds[c * CS + sg_strip_row(r, c)] = base[(size_t)r * S + c];
 	}
 	__syncthreads();
 	float2 v[P];
 #pragma unroll
 	for (int j = 0; j < P; j++)
-		v[j] = col[64 * j + lane];
+		v[j] = col[64 * j + (lane ^ sw)];
 	const int km = lane >> 1, hm = lane & 1;
 	const int kx = (x0 + wave) & (H - 1);
 	/* PERM: the reference column's loads issued now, in flight during the forward transform */
@@ -558,14 +567,14 @@ k_reg_cols_xpower_w(float2 *__restrict__ work, const float2 *__restrict__ spec, 
 	wsync();
 #pragma unroll
 	for (int j = 0; j < P; j++)
-		col[64 * j + lane] = v[j];
+		col[64 * j + (lane ^ sw)] = v[j];
 	__syncthreads();
 	{	/* every LDS read issued before the stores (one LDS latency, not eight) */
 		float2 o[P];
 #pragma unroll
 		for (int it = 0; it < P; it++) {
 			const int r = (threadIdx.x >> 2) + 64 * it, c = threadIdx.x & 3;
-			o[it] = lds[c * CS + r];
+			o[it] = lds[c * CS + sg_strip_row(r, c)];
 		}
 #pragma unroll
 		for (int it = 0; it < P; it++) {
@@ -628,15 +637,17 @@ k_reg_rows_fwd_half_w(const uint16_t *__restrict__ sel, const int *__restrict__ 
 			fetch(row + 4);
 		sg_fft2048_wave<false>(v, col, tw, lane);
 		__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+		/* natural order, the upper half 8 entries up: lanes km and km + 8 (hm = 0 / 1) of a
+		 * 16-lane store group on different banks */
 #pragma unroll
 		for (int k = 0; k < P; k++)
-			col[km + 32 * k + 1024 * hm] = v[k];
+			col[km + 32 * k + (1024 + 8) * hm] = v[k];
 		__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 		float2 *out = work + (size_t)pair * plane + (size_t)row * S;
 #pragma unroll 4
 		for (int q = 0; q < H / 64; q++) {
 			const int kx = 64 * q + lane;
-			const float2 zk = col[kx], zm = col[kx ? S - kx : H];
+			const float2 zk = col[kx], zm = col[(kx ? S - kx : H) + 8];
 			float2 A, B;
 			if (kx == 0) {
 				A = make_float2(zk.x, zm.x);	/* A(0) + i A(S/2) */
