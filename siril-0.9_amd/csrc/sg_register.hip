@@ -410,12 +410,14 @@ __device__ __forceinline__ void sg_fft2048_wave(float2 (&v)[32], float2 *col, co
 #define SG_WCOL_WPE 2
 #endif
 #define SG_WCOL_CS 2120	/* LDS float2 per column: 2048 (strip) / 32 x 66 (transposes), +8 for the strip's banks */
-/* physical LDS row of strip row r in column c: rows of columns 2, 3 XOR 4, so that the strip's
- * 8-byte stores (32 banks, 16-lane groups: 4 rows x 4 columns) and its 8-byte reads (64 banks,
- * 32-lane groups: 8 rows x 4 columns, CS = 8 mod 32) are both conflict-free (a 2-way conflict on
- * the stores was 20 % of the column pass's LDS cycles) */
+/* physical LDS row of strip row r in column c of a CW-column strip, so that the strip's 8-byte
+ * stores (32 banks, 16-lane groups) and its 8-byte reads (64 banks, 32-lane groups, CS = 8 mod 32)
+ * are both conflict-free (a 2-way conflict on the stores was 20 % of the column pass's LDS
+ * cycles).  CW = 4: a store group is 4 rows x 4 columns, columns 2, 3 XOR the row with 4; CW = 8:
+ * 2 rows x 8 columns, column c XORs it with 2 (c / 2). */
+template <int CW = 4>
 __device__ __forceinline__ int sg_strip_row(int r, int c) {
-	return r ^ ((c >> 1) << 2);
+	return CW == 8 ? r ^ ((c >> 1) << 1) : r ^ ((c >> 1) << 2);
 }
 /* specp: the reference spectrum in the column pass's lane order, specp[(kx 32 + k) 64 + 2 km + hm]
  * = spec[ky][kx] at ky = km + 32 k + 1024 hm (kx < S / 2), so that the pass reads its reference
@@ -434,7 +436,7 @@ k_reg_cols_fwd_perm_w(float2 *__restrict__ spec, float2 *__restrict__ specp, con
 	const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 	const int x0 = blockIdx.x * 4;
 	float2 *col = lds + wave * CS;
-	const int sw = (wave >> 1) << 2;	/* sg_strip_row of this wave's column */
+	const int sw = sg_strip_row<4>(0, wave);	/* sg_strip_row of this wave's column: lane ^ sw */
 #pragma unroll
 	for (int it = 0; it < P; it++) {
 		const int r = (threadIdx.x >> 2) + 64 * it, c = threadIdx.x & 3;
@@ -458,24 +460,24 @@ k_reg_cols_fwd_perm_w(float2 *__restrict__ spec, float2 *__restrict__ specp, con
 	}
 }
 
-template <bool PERM>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SG_WCOL_WPE)))
+template <bool PERM, int CW>
+__global__ void __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(SG_WCOL_WPE)))
 k_reg_cols_xpower_w(float2 *__restrict__ work, const float2 *__restrict__ spec, const float2 *__restrict__ specp,
 		const float2 *__restrict__ tw, int xcdmap) {
 	constexpr int S = 2048, H = 1024, P = 32, CS = SG_WCOL_CS, TR = 66;
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 	float2 *lds = (float2 *)smem;
 	const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-	const int x0 = sg_xcd_strip(blockIdx.x, gridDim.x, xcdmap) * 4, pair = blockIdx.y;
+	const int x0 = sg_xcd_strip(blockIdx.x, gridDim.x, xcdmap) * CW, pair = blockIdx.y;
 	float2 *base = work + (size_t)pair * S * S + x0;
 	float2 *col = lds + wave * CS;
-	const int sw = (wave >> 1) << 2;	/* sg_strip_row of this wave's column */
+	const int sw = sg_strip_row<CW>(0, wave);	/* sg_strip_row of this wave's column: lane ^ sw */
 	auto wsync = [] { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); };
 	/* strip -> LDS: rows of 4 columns (32 B), column c at lds + c CS */
 #pragma unroll
 	for (int it = 0; it < P; it++) {
-		const int r = (threadIdx.x >> 2) + 64 * it, c = threadIdx.x & 3;
-		lds[c * CS + sg_strip_row(r, c)] = base[(size_t)r * S + c];
+		const int r = threadIdx.x / CW + 64 * it, c = threadIdx.x % CW;
+		lds[c * CS + sg_strip_row<CW>(r, c)] = base[(size_t)r * S + c];
 	}
 	__syncthreads();
 	float2 v[P];
@@ -504,7 +506,7 @@ k_reg_cols_xpower_w(float2 *__restrict__ work, const float2 *__restrict__ spec, 
 		const int kx0 = x0 & (H - 1);	/* a strip lies inside one half */
 #pragma unroll
 		for (int it = 0; it < P; it++) {
-			const int r = (threadIdx.x >> 2) + 64 * it, c = threadIdx.x & 3;
+			const int r = threadIdx.x / CW + 64 * it, c = threadIdx.x % CW;
 			if (kx0 + c)
 				lds[c * CS + r] = spec[(size_t)r * S + kx0 + c];
 		}
@@ -573,12 +575,12 @@ k_reg_cols_xpower_w(float2 *__restrict__ work, const float2 *__restrict__ spec, 
 		float2 o[P];
 #pragma unroll
 		for (int it = 0; it < P; it++) {
-			const int r = (threadIdx.x >> 2) + 64 * it, c = threadIdx.x & 3;
-			o[it] = lds[c * CS + sg_strip_row(r, c)];
+			const int r = threadIdx.x / CW + 64 * it, c = threadIdx.x % CW;
+			o[it] = lds[c * CS + sg_strip_row<CW>(r, c)];
 		}
 #pragma unroll
 		for (int it = 0; it < P; it++) {
-			const int r = (threadIdx.x >> 2) + 64 * it, c = threadIdx.x & 3;
+			const int r = threadIdx.x / CW + 64 * it, c = threadIdx.x % CW;
 			base[(size_t)r * S + c] = o[it];
 		}
 	}
@@ -1869,9 +1871,11 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 				(int)colh_lds32);
 		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower<float2, 16>, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)colh_lds32);
-		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower_w<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower_w<true, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)wcol_lds);
-		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower_w<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower_w<true, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+				(int)(2 * wcol_lds));
+		(void)hipFuncSetAttribute((const void *)k_reg_cols_xpower_w<false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)wcol_lds);
 		(void)hipFuncSetAttribute((const void *)k_reg_cols_fwd_perm_w, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)wcol_lds);
@@ -2035,11 +2039,14 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 			HIPCHK(hipStreamWaitEvent(s, dv.aux2_ev[1], 0));
 			ref_pending = false;
 		}
-		if (wcol && specp32)	/* S = 2048: the wave-level column pass (SG_REG_WCOL=0: the block-level one, A/B) */
-			hipLaunchKernelGGL(k_reg_cols_xpower_w<true>, dim3(S / 4, np), dim3(256), wcol_lds, s, work32,
+		if (wcol && specp32 && ctx->knobs.reg_wcolw == 8)	/* 8-column strips: 64-B row segments, one workgroup per CU */
+			hipLaunchKernelGGL((k_reg_cols_xpower_w<true, 8>), dim3(S / 8, np), dim3(512), 2 * wcol_lds, s, work32,
+					(const float2 *)spec32, (const float2 *)specp32, tw32, xcdmap);
+		else if (wcol && specp32)	/* S = 2048: the wave-level column pass (SG_REG_WCOL=0: the block-level one, A/B) */
+			hipLaunchKernelGGL((k_reg_cols_xpower_w<true, 4>), dim3(S / 4, np), dim3(256), wcol_lds, s, work32,
 					(const float2 *)spec32, (const float2 *)specp32, tw32, xcdmap);
 		else if (wcol)
-			hipLaunchKernelGGL(k_reg_cols_xpower_w<false>, dim3(S / 4, np), dim3(256), wcol_lds, s, work32,
+			hipLaunchKernelGGL((k_reg_cols_xpower_w<false, 4>), dim3(S / 4, np), dim3(256), wcol_lds, s, work32,
 					(const float2 *)spec32, (const float2 *)nullptr, tw32, xcdmap);
 		else if (ept32 == 16)
 			hipLaunchKernelGGL((k_reg_cols_xpower<float2, 16>), dim3(S / CW32, np), dim3(colh_thr32), colh_lds32, s,
