@@ -1031,6 +1031,107 @@ k_quality_grad(const uint16_t *__restrict__ qbuf, int xs, int ys, const unsigned
 	}
 }
 
+/* k_quality_grad streamed down a band: one wave per (60-column band, SG_QGS_ROWS output rows,
+ * frame) of the 10 % margins' interior, lane l at column x0 - 2 + l.  Each input row is loaded
+ * and stretched once (SG_QGS_PF rows in flight), its horizontal 3-sum formed with two lane
+ * shuffles, and rolling three-row windows give the smoothed row, the thresholded map and the
+ * gradient of output row y as rows y + 2 arrive.  Only the interior's neighbourhood is read (the
+ * tiled kernel read every row and column), and no LDS or barrier: 290 -> ~? us per configs[1]
+ * step with 61 k tiled workgroups before (profiles/r05x_*).  Same integer sums, so the same
+ * result bit for bit. */
+#define SG_QGS_ROWS 64
+#define SG_QGS_PF 8
+__global__ void __launch_bounds__(64)
+k_quality_grad_s(const uint16_t *__restrict__ qbuf, int xs, int ys, const unsigned int *__restrict__ qmax,
+		unsigned long long *__restrict__ acc) {
+	const int q = blockIdx.z, lane = threadIdx.x;
+	const uint16_t *b = qbuf + (size_t)q * xs * ys;
+	const unsigned int mx = qmax[q];
+	const bool stretch = mx > 0;
+	const double mult = stretch ? (double)60000 / (double)mx : 1.0;
+	const int yb = (int)((double)ys * 0.1) + 1;
+	const int xb = (int)((double)xs * 0.1) + 1;
+	const int x0 = xb + 60 * blockIdx.x, c = x0 - 2 + lane;
+	const int y0 = yb + SG_QGS_ROWS * blockIdx.y;
+	const int y1 = min(y0 + SG_QGS_ROWS, ys - yb);	/* output rows [y0, y1) */
+	const bool in_x = c >= xb && c < xs - xb;	/* the map's and the output's column range */
+	const bool out_lane = lane >= 2 && lane < 62 && in_x;
+	const bool col_ok = c >= 0 && c < xs, sm_x = c >= 1 && c <= xs - 2;
+	unsigned long long val = 0;
+	unsigned int pix = 0, cnt = 0;
+	/* rolling state: horizontal sums of the last three stretched rows, the last two smoothed
+	 * rows (value, right neighbour's) and the last two rows' horizontally OR-ed map bits */
+	unsigned int h0 = 0, h1 = 0;
+	int sm_prev = 0, smr_prev = 0;
+	bool th_prev2 = false, th_prev = false;
+	const int ya = y0 - 2, yz = y1 + 1;	/* input rows [ya, yz] */
+	for (int g = ya; g <= yz; g += SG_QGS_PF) {
+		unsigned int raw[SG_QGS_PF];
+#pragma unroll
+		for (int k = 0; k < SG_QGS_PF; k++) {
+			const int yi = g + k;
+			raw[k] = (col_ok && yi >= 0 && yi < ys && yi <= yz) ? (unsigned int)b[(size_t)yi * xs + c] : 0u;
+		}
+#pragma unroll
+		for (int k = 0; k < SG_QGS_PF; k++) {
+			const int yi = g + k;
+			if (yi > yz)
+				break;
+			unsigned int st = raw[k];
+			if (stretch && col_ok && yi >= 0 && yi < ys) {
+				st = (unsigned int)((double)st * mult);
+				if (st > 65535u)
+					st = 65535u;
+			}
+			const unsigned int h = st + (unsigned int)__shfl_up((int)st, 1, 64) + (unsigned int)__shfl_down((int)st, 1, 64);
+			if (yi >= ya + 2) {
+				/* smoothed row qy = yi - 1 from the horizontal sums of rows yi - 2 .. yi */
+				const int qy = yi - 1;
+				const int sm = (sm_x && qy >= 1 && qy <= ys - 2) ? (int)((h0 + h1 + h) / 9) : 0;
+				const bool thr = sm >= SG_Q_THRESHOLD && in_x && qy >= yb && qy < ys - yb;
+				/* both shuffles by every lane (a short-circuit || would run them under a partial
+				 * exec mask) */
+				const int thn = (int)thr, thl = __shfl_up(thn, 1, 64), thr1 = __shfl_down(thn, 1, 64);
+				const bool th = (thn | thl | thr1) != 0;
+				const int smr = __shfl_down(sm, 1, 64);
+				/* output row yo = qy - 1: its row (sm_prev), the row below (sm), the map rows
+				 * yo - 1 .. yo + 1 */
+				const int yo = qy - 1;
+				if (yo >= y0 && out_lane) {
+					if (sm_prev >= SG_Q_THRESHOLD)
+						cnt++;
+					if (th_prev2 || th_prev || th) {
+						const long long d1 = sm_prev - smr_prev;
+						const long long d2 = sm_prev - sm;
+						val += (unsigned long long)(d1 * d1 + d2 * d2);
+						pix++;
+					}
+				}
+				sm_prev = sm;
+				smr_prev = smr;
+				th_prev2 = th_prev;
+				th_prev = th;
+			}
+			h0 = h1;
+			h1 = h;
+		}
+	}
+	unsigned long long p = pix, n = cnt;
+	for (int o = 32; o > 0; o >>= 1) {
+		val += __shfl_down(val, o, 64);
+		p += __shfl_down(p, o, 64);
+		n += __shfl_down(n, o, 64);
+	}
+	if (lane == 0) {
+		if (val)
+			atomicAdd(acc + q * 3, val);
+		if (p)
+			atomicAdd(acc + q * 3 + 1, p);
+		if (n)
+			atomicAdd(acc + q * 3 + 2, n);
+	}
+}
+
 /* ---------------------------------------------------------------------------------------
  * Any selection side (FFTW plans every S, registration.c:251-257): mixed-radix Stockham
  * passes (radix 8, 4, 2, 3, 5, 7) in LDS, one line per workgroup, ping-pong between two LDS
@@ -1525,9 +1626,19 @@ static int reg_quality_launch(sg_ctx *ctx, SgDevice &dv, hipStream_t s, const ui
 	/* 2 waves per 64x16 tile: 214 us per 129 frames against 238 (4 waves) and 333 (1 wave),
 	 * scripts/gpu_qgrad.sh */
 	const int gthr = ctx->knobs.qgrad_threads;	/* A/B knob SG_QGRAD_THREADS */
-	hipLaunchKernelGGL(k_quality_grad, dim3((xs + 63) / 64, (ys + SG_QGT - 1) / SG_QGT, nq), dim3(gthr), 0, dv.aux, qbuf, xs,
-			ys, qmax, acc);
-	HIPCHK(hipGetLastError());
+	if (ctx->knobs.qgrad_stream) {	/* A/B knob SG_QGRAD_STREAM: 0 = the tiled kernel */
+		const int xb = (int)((double)xs * 0.1) + 1, yb = (int)((double)ys * 0.1) + 1;
+		const int wi = xs - 2 * xb, hi = ys - 2 * yb;
+		if (wi > 0 && hi > 0) {
+			hipLaunchKernelGGL(k_quality_grad_s, dim3((wi + 59) / 60, (hi + SG_QGS_ROWS - 1) / SG_QGS_ROWS, nq), dim3(64),
+					0, dv.aux, qbuf, xs, ys, qmax, acc);
+			HIPCHK(hipGetLastError());
+		}
+	} else {
+		hipLaunchKernelGGL(k_quality_grad, dim3((xs + 63) / 64, (ys + SG_QGT - 1) / SG_QGT, nq), dim3(gthr), 0, dv.aux, qbuf,
+				xs, ys, qmax, acc);
+		HIPCHK(hipGetLastError());
+	}
 	HIPCHK(hipMemcpyAsync(dv.qacc_h, acc, sizeof(unsigned long long) * 3 * nq, hipMemcpyDeviceToHost, dv.aux));
 	HIPCHK(hipEventRecord(dv.aux_ev[0], dv.aux));
 	*launched = true;
