@@ -1036,9 +1036,9 @@ k_quality_grad(const uint16_t *__restrict__ qbuf, int xs, int ys, const unsigned
  * and stretched once (SG_QGS_PF rows in flight), its horizontal 3-sum formed with two lane
  * shuffles, and rolling three-row windows give the smoothed row, the thresholded map and the
  * gradient of output row y as rows y + 2 arrive.  Only the interior's neighbourhood is read (the
- * tiled kernel read every row and column), and no LDS or barrier: 290 -> ~? us per configs[1]
- * step with 61 k tiled workgroups before (profiles/r05x_*).  Same integer sums, so the same
- * result bit for bit. */
+ * tiled kernel read every row and column), and no LDS or barrier: 290 -> 190 us per configs[1]
+ * step (61 k tiled workgroups before), registration 3.20 -> 3.10 ms (profiles/r05x_*).  Same
+ * integer sums, so the same result bit for bit. */
 #define SG_QGS_ROWS 64
 #define SG_QGS_PF 8
 __global__ void __launch_bounds__(64)
