@@ -33,6 +33,8 @@ __global__ void k_stack_sorted(SgStackParams p, const unsigned int *list, const 
 template <int REJ, int NORM, int NI>
 __global__ void k_stack_hist(SgStackParams p, const int *tab, const int4 *norm, unsigned int *redo_count,
 		unsigned int *redo_list);
+template <int KM>
+__global__ void k_stack_linfit(SgStackParams p, unsigned int *redo_count, unsigned int *redo_list);
 void sg_dbg_why_dump(hipStream_t s);
 int sgh_block_threads(int ni, int rej);
 template <int NM>
@@ -735,10 +737,14 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		/* histogram fast path (sg_stack_hist.hip): SIGMA / WINSORIZED / PERCENTILE rejection and
 		 * stack_median, any normalisation, 16 <= N <= 65535 (per-lane zero / 65535 counters are
 		 * 16-bit halves) */
-		const bool hist = d->kernel_path != SG_PATH_SORTED && N >= 16 && N <= 65535 && hist_addr_ok &&
+		/* LINEARFIT's decision-exact kernel (k_stack_linfit, sg_stack.hip) takes the histogram
+		 * path's place: its redo list goes to the sorted kernel's exact replay the same way */
+		const bool linfit_fast = d->kernel_path != SG_PATH_SORTED && d->method == SG_STACK_MEAN &&
+			d->rejection == SG_LINEARFIT && N >= 16 && N <= 1024 && ctx->knobs.linfit_fast;
+		const bool hist = linfit_fast || (d->kernel_path != SG_PATH_SORTED && N >= 16 && N <= 65535 && hist_addr_ok &&
 			(d->method == SG_STACK_MEDIAN || (d->method == SG_STACK_MEAN && (d->rejection == SG_SIGMA ||
 					d->rejection == SG_WINSORIZED || d->rejection == SG_PERCENTILE ||
-					(d->rejection == SG_SIGMEDIAN && ctx->knobs.hist_sigmedian))));
+					(d->rejection == SG_SIGMEDIAN && ctx->knobs.hist_sigmedian)))));
 		/* beyond the sorted kernel's 1024 frames only the histogram path runs; its redo pixels
 		 * all go to the replay / literal kernels (they take any N) */
 		/* beyond the sorted kernel's 1024 frames a stack without a histogram path (LINEARFIT, or
@@ -833,7 +839,7 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 				p.rejection == SG_PERCENTILE ? 1 : p.rejection == SG_SIGMEDIAN ? 3 : 2;
 			/* normalised SIGMA / WINSORIZED: redo pixels whose samples the tile fully knows leave
 			 * their sorted columns for the sorted kernel (sgh_compact), up to a 384 MiB buffer */
-			const bool compact = norm != 0 && (rj == 2 || rj == 4) && nreg && ctx->knobs.hist_compact;
+			const bool compact = !linfit_fast && norm != 0 && (rj == 2 || rj == 4) && nreg && ctx->knobs.hist_compact;
 			if (compact) {
 				const size_t cap = std::min<size_t>(npix_launch, ctx->knobs.hist_compact >= 2 ?
 						(size_t)ctx->knobs.hist_compact : ((size_t)384 << 20) / ((size_t)N * 2));
@@ -845,6 +851,18 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 				p.cmp_cap = (unsigned int)cap;
 			}
 			const dim3 hg((unsigned)nblk_h), hb((unsigned)sgh_block_threads(ni, rj));
+			if (linfit_fast) {
+				/* one workgroup per 64 pixels of a row, the tile's columns in LDS */
+				const int km = N <= 512 ? 8 : 16;
+				const size_t lfx_lds = (size_t)64 * (64 * km + 2) * sizeof(uint16_t);
+				const void *kf = km == 8 ? (const void *)k_stack_linfit<8> : (const void *)k_stack_linfit<16>;
+				(void)hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lfx_lds);
+				const dim3 lg((unsigned)((size_t)((W + 63) / 64) * nrows * C));
+				if (km == 8)
+					hipLaunchKernelGGL(k_stack_linfit<8>, lg, dim3(256), lfx_lds, s, p, redo_count, redo_list);
+				else
+					hipLaunchKernelGGL(k_stack_linfit<16>, lg, dim3(256), lfx_lds, s, p, redo_count, redo_list);
+			} else
 			switch ((rj == 4 ? 10 : rj == 1 ? 20 : rj == 8 ? 30 : rj == 3 ? 40 : 0) + norm +
 					100 * (rj == 1 || rj == 8 || rj == 3 ? 1 : ni)) {
 			case 100: hipLaunchKernelGGL((k_stack_hist<2, 0, 1>), hg, hb, lds_pad, s, p, p.hist_tab, (const int4 *)p.hist_norm, redo_count, redo_list); break;

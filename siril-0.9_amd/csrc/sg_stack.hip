@@ -2294,6 +2294,350 @@ __device__ int replay_pixel(LDS &L, int N0, int type, double sl, double sh, int 
 	return 1;
 }
 
+/* ---------------------------------------------------------------------------------------
+ * LINEARFIT, decision-exact (:1750-1784).  The reference fits y = a i + b to the sorted kept
+ * stack with gsl_fit_linear's double recurrences (m_x, m_y, m_dx2, m_dxdy, then b = m_dxdy /
+ * m_dx2, a = m_y - m_x b), takes sigma = mean |y_i - (a i + b)| and clips with line_clipping.
+ * Its decisions only depend on those rounded values through comparisons, so this path takes the
+ * fit from exact integer sums (S_y = sum y, S_iy = sum i y over the kept sorted ranks i, and the
+ * closed forms of x = 0 .. N-1: slope = (12 S_iy - 6 (N-1) S_y) / (N (N^2 - 1))), and decides
+ * every test against a bound on how far the reference's rounded recurrences can be from the
+ * exact fit:
+ *   |m_x err| <= 2 N^2 u, |m_y err| <= 2 N u Y, |m_dx2 err| <= 6 N^3 u, |m_dxdy err| <= 6 N^2 u Y
+ * (u = 2^-53, Y = the kept maximum; each recurrence step m += (v - m)/(k+1) adds at most
+ * 2u|v - m|/(k+1) + u|m| and damps the carried error by k/(k+1)), propagated through the slope,
+ * intercept, residuals, sigma and the division (LINEARFIT round 5), each taken 4x.
+ * A test closer to its threshold than that, a sigma within the bound of 0, a pass that would
+ * reach the `N - r <= 4` break (its rejected[] entries after the break are stale state) or any
+ * other corner sends the pixel to the redo list (the sorted kernel's reject_linearfit, which
+ * replays the recurrences bit for bit, and the literal kernel for first-pass breaks).
+ *
+ * One workgroup per 64 pixels of a row: the N frames' 128-B row segments (shifted, normalised
+ * as sg_gather) land in LDS as per-pixel columns; each wave then takes a pixel at a time with its
+ * column in registers (element 64 k + lane in x[k]), sorts it (bitonic, replay_cx_reg), and runs
+ * the passes with ballots for the ranks and wave sums for S_y, S_iy and sigma. */
+/* lane exchanges on the VALU (DPP / swizzle instead of ds_bpermute round trips): the partner
+ * lane ^ J of every lane */
+template <int J>
+__device__ __forceinline__ uint32_t lfx_xor(uint32_t v, int lane) {
+	if (J == 1)
+		return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);	/* quad_perm [1,0,3,2] */
+	if (J == 2)
+		return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);	/* quad_perm [2,3,0,1] */
+	if (J == 4 || J == 8) {	/* row_shl:J for the lower half of each 2J group, row_shr:J for the upper */
+		const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x100 + J, 0xF, 0xF, false);
+		const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x110 + J, 0xF, 0xF, false);
+		return (lane & J) ? dn : up;
+	}
+	if (J == 16)	/* swizzle bit mode within 32 lanes: and 0x1F, xor 0x10 */
+		return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);
+	return (uint32_t)__shfl_xor((int)v, J, 64);
+}
+
+/* compare-exchanges on two pixels' columns at once: element e of pixel A in the low half of
+ * x[k], of pixel B in the high half (the network does not depend on the data), by packed u16
+ * min / max */
+__device__ __forceinline__ uint32_t lfx_pk_min(uint32_t a, uint32_t b) {
+	uint32_t r;
+	asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+	return r;
+}
+__device__ __forceinline__ uint32_t lfx_pk_max(uint32_t a, uint32_t b) {
+	uint32_t r;
+	asm("v_pk_max_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+	return r;
+}
+template <int KM, int J>
+__device__ __forceinline__ void lfx_cx_lanes(uint32_t (&x)[KM], int kk, int lane) {
+	const bool lower = (lane & J) == 0;
+#pragma unroll
+	for (int k = 0; k < KM; k++) {
+		const bool up = ((64 * k + lane) & kk) == 0;
+		const uint32_t y = lfx_xor<J>(x[k], lane);
+		x[k] = (lower == up) ? lfx_pk_min(x[k], y) : lfx_pk_max(x[k], y);
+	}
+}
+template <int KM, int JR>
+__device__ __forceinline__ void lfx_cx_reg(uint32_t (&x)[KM], int kk, int lane) {
+#pragma unroll
+	for (int k = 0; k < KM; k++) {
+		if ((k & JR) == 0 && (k | JR) < KM) {
+			const bool up = ((64 * k + lane) & kk) == 0;
+			const uint32_t u = x[k], v = x[k | JR];
+			const uint32_t mn = lfx_pk_min(u, v), mx = lfx_pk_max(u, v);
+			x[k] = up ? mn : mx;
+			x[k | JR] = up ? mx : mn;
+		}
+	}
+}
+
+template <int KM>
+__device__ __forceinline__ void lfx_sort(uint32_t (&x)[KM], int lane) {
+	constexpr int P = 64 * KM;
+#pragma unroll 1
+	for (int kk = 2; kk <= P; kk <<= 1) {
+#pragma unroll 1
+		for (int j = kk >> 1; j > 0; j >>= 1) {
+			switch (j) {
+			case 1: lfx_cx_lanes<KM, 1>(x, kk, lane); break;
+			case 2: lfx_cx_lanes<KM, 2>(x, kk, lane); break;
+			case 4: lfx_cx_lanes<KM, 4>(x, kk, lane); break;
+			case 8: lfx_cx_lanes<KM, 8>(x, kk, lane); break;
+			case 16: lfx_cx_lanes<KM, 16>(x, kk, lane); break;
+			case 32: lfx_cx_lanes<KM, 32>(x, kk, lane); break;
+			case 64: lfx_cx_reg<KM, 1>(x, kk, lane); break;
+			case 128: lfx_cx_reg<KM, 2>(x, kk, lane); break;
+			case 256: lfx_cx_reg<KM, 4>(x, kk, lane); break;
+			default: lfx_cx_reg<KM, 8>(x, kk, lane); break;
+			}
+		}
+	}
+}
+
+/* wave totals by the DPP inclusive-scan sequence (row_shr 1..3, 4, 8, row_bcast 15 / 31: the
+ * last lane holds the total), read from lane 63; no LDS round trips */
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ int lfx_dpp(int v) {
+	return __builtin_amdgcn_update_dpp(0, v, CTRL, RM, BM, true);
+}
+__device__ __forceinline__ uint32_t lfx_sum_u32(uint32_t v0) {
+	const int v = (int)v0;
+	int t = v + lfx_dpp<0x111, 0xF, 0xF>(v);
+	t += lfx_dpp<0x112, 0xF, 0xF>(v);
+	t += lfx_dpp<0x113, 0xF, 0xF>(v);
+	t += lfx_dpp<0x114, 0xF, 0xE>(t);
+	t += lfx_dpp<0x118, 0xF, 0xC>(t);
+	t += lfx_dpp<0x142, 0xA, 0xF>(t);
+	t += lfx_dpp<0x143, 0xC, 0xF>(t);
+	return (uint32_t)__builtin_amdgcn_readlane(t, 63);
+}
+__device__ __forceinline__ uint32_t lfx_max_u32(uint32_t v) {
+	auto mx = [](uint32_t a, int b) { return a > (uint32_t)b ? a : (uint32_t)b; };
+	uint32_t t = mx(v, lfx_dpp<0x111, 0xF, 0xF>((int)v));
+	t = mx(t, lfx_dpp<0x112, 0xF, 0xF>((int)v));
+	t = mx(t, lfx_dpp<0x113, 0xF, 0xF>((int)v));
+	t = mx(t, lfx_dpp<0x114, 0xF, 0xE>((int)t));
+	t = mx(t, lfx_dpp<0x118, 0xF, 0xC>((int)t));
+	t = mx(t, lfx_dpp<0x142, 0xA, 0xF>((int)t));
+	t = mx(t, lfx_dpp<0x143, 0xC, 0xF>((int)t));
+	return (uint32_t)__builtin_amdgcn_readlane((int)t, 63);
+}
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ double lfx_dppd(double x) {
+	const int lo = lfx_dpp<CTRL, RM, BM>(__double2loint(x)), hi = lfx_dpp<CTRL, RM, BM>(__double2hiint(x));
+	return __hiloint2double(hi, lo);
+}
+/* exact for the integer-valued sums used here (every partial < 2^53); the residual sum's order
+ * only enters its error bound */
+__device__ __forceinline__ double lfx_sum_f64(double v) {
+	double t = v + lfx_dppd<0x111, 0xF, 0xF>(v);
+	t += lfx_dppd<0x112, 0xF, 0xF>(v);
+	t += lfx_dppd<0x113, 0xF, 0xF>(v);
+	t += lfx_dppd<0x114, 0xF, 0xE>(t);
+	t += lfx_dppd<0x118, 0xF, 0xC>(t);
+	t += lfx_dppd<0x142, 0xA, 0xF>(t);
+	t += lfx_dppd<0x143, 0xC, 0xF>(t);
+	return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(t), 63),
+			__builtin_amdgcn_readlane(__double2loint(t), 63));
+}
+
+/* one pixel's passes; x[] sorted ascending (pads 0xFFFF at elements >= N0).  Returns 1 with the
+ * value and counters, 0 when the pixel goes to the redo list. */
+template <int KM>
+__device__ int lfx_pixel(const uint32_t (&x)[KM], int N0, double sl, double sh, int lane, uint16_t &value,
+		uint32_t &rlo, uint32_t &rhi) {
+	constexpr double u = 1.1102230246251565e-16;
+	const unsigned long long lt = (1ull << lane) - 1ull;
+	uint32_t kept = 0;
+#pragma unroll
+	for (int k = 0; k < KM; k++)
+		kept |= (64 * k + lane < N0 ? 1u : 0u) << k;
+	int N = N0, r = 0;
+	uint32_t clo = 0, chi = 0;
+	double Sy = 0.0;
+	for (int pass = 0; pass < 4096; pass++) {
+		/* ranks of the kept elements in sorted order (ballots), and the exact sums */
+		double rank[KM];
+		int base = 0;
+		uint32_t sy = 0, ymax = 0;
+		double siy = 0.0;
+#pragma unroll
+		for (int k = 0; k < KM; k++) {
+			const bool kp = (kept >> k) & 1u;
+			const unsigned long long bal = __ballot(kp);
+			const int rk = base + __popcll(bal & lt);
+			base += __popcll(bal);
+			rank[k] = (double)rk;
+			if (kp) {
+				sy += x[k];
+				siy += (double)(rk * (int)x[k]);	/* < 2^26 each, a lane's sum < 2^30: exact */
+				ymax = x[k] > ymax ? x[k] : ymax;
+			}
+		}
+		if (N < 8)
+			return 0;
+		Sy = (double)lfx_sum_u32(sy);
+		const double Siy = lfx_sum_f64(siy);
+		ymax = lfx_max_u32(ymax);
+		const double n = (double)N, Y = (double)ymax;
+		const double Pn = 12.0 * Siy - 6.0 * (n - 1.0) * Sy;	/* integers < 2^53: exact */
+		const double slope = Pn / (n * (n * n - 1.0));
+		const double b0 = Sy / n - 0.5 * (n - 1.0) * slope;
+		/* residuals (line - y, kept for the tests) and their mean absolute value */
+		double dv[KM];
+		double sres = 0.0;
+#pragma unroll
+		for (int k = 0; k < KM; k++) {
+			dv[k] = fma(slope, rank[k], b0) - (double)x[k];
+			if ((kept >> k) & 1u)
+				sres += fabs(dv[k]);
+		}
+		const double sigma = lfx_sum_f64(sres) / n;
+		/* how far the reference's values can be from these (4x the bounds above) */
+		const double as = fabs(slope);
+		const double dmx = 2.0 * n * n * u, dmy = 2.0 * n * u * Y;
+		const double dmdx2 = 6.0 * n * n * n * u, dmdxdy = 6.0 * n * n * u * Y;
+		const double mdx2 = (n * n - 1.0) / 12.0;
+		if (!(mdx2 > 4.0 * dmdx2))
+			return 0;
+		const double dS = 4.0 * ((dmdxdy + as * dmdx2) / (mdx2 - dmdx2) + 4.0 * u * as);
+		const double Rm = Y + n * as + fabs(b0) + 1.0;
+		const double dB = 4.0 * (dmy + as * dmx + 0.5 * n * dS + 8.0 * u * Rm);
+		const double dline = n * dS + dB + 32.0 * u * Rm;
+		const double dsig = 4.0 * (dline + 2.0 * (n + 2.0) * u * Rm);
+		if (!(sigma > 4.0 * dsig) || !(sl == sl) || !(sh == sh))
+			return 0;
+		/* line_clipping (:1170-1183), low first (else if); the margin of element k is
+		 * e0 + e1 rank (|d| <= Rm) */
+		const double tL = sl * sigma, tH = sh * sigma;
+		const double e1 = 4.0 * dS;
+		const double eL = 4.0 * (dB + 32.0 * u * Rm + fabs(sl) * dsig + 4.0 * u * (Rm + fabs(tL)));
+		const double eH = 4.0 * (dB + 32.0 * u * Rm + fabs(sh) * dsig + 4.0 * u * (Rm + fabs(tH)));
+		uint32_t lo_bits = 0, hi_bits = 0;
+		bool amb = false;
+#pragma unroll
+		for (int k = 0; k < KM; k++) {
+			if (!((kept >> k) & 1u))
+				continue;
+			const double tl = dv[k] - tL, th = -dv[k] - tH;
+			const double el = fma(e1, rank[k], eL), eh = fma(e1, rank[k], eH);
+			const bool low = tl > el, lamb = fabs(tl) <= el;
+			const bool high = !low && !lamb && th > eh;
+			amb |= lamb || (!low && fabs(th) <= eh);
+			lo_bits |= (low ? 1u : 0u) << k;
+			hi_bits |= (high ? 1u : 0u) << k;
+		}
+		if (__ballot(amb))
+			return 0;
+		int nl = 0, nh = 0;
+#pragma unroll
+		for (int k = 0; k < KM; k++) {
+			nl += __popcll(__ballot((lo_bits >> k) & 1u));
+			nh += __popcll(__ballot((hi_bits >> k) & 1u));
+		}
+		const int nrej = nl + nh;
+		if (r + nrej >= N - 4)	/* the `N - r <= 4` break would fire inside the pass */
+			return 0;
+		clo += nl;
+		chi += nh;
+		kept &= ~(lo_bits | hi_bits);
+		r += nrej;
+		N -= nrej;
+		if (!(nrej > 0 && N > 3)) {
+			if (nrej > 0) {	/* the kept sum after this pass's removal */
+				uint32_t s2 = 0;
+#pragma unroll
+				for (int k = 0; k < KM; k++)
+					if ((kept >> k) & 1u)
+						s2 += x[k];
+				Sy = (double)lfx_sum_u32(s2);
+			}
+			value = sg_round_to_WORD(Sy / (double)N);
+			rlo = clo;
+			rhi = chi;
+			return 1;
+		}
+	}
+	return 0;
+}
+
+template <int KM>
+__global__ void __launch_bounds__(256)
+k_stack_linfit(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
+	extern __shared__ uint16_t lfx_cols[];
+	constexpr int LS = 64 * KM + 2;	/* column stride: an odd dword count (conflict-free stores) */
+	const int tid = threadIdx.x, lane = tid & 63;
+	const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+	const int N = p.N;
+	const int ntx = (p.W + 63) / 64, nrows = p.row_end - p.row_begin;
+	int bid = blockIdx.x;
+	const int xt = bid % ntx;
+	bid /= ntx;
+	const int R = p.row_begin + (bid % nrows), c = bid / nrows;
+	const int x0 = xt * 64;
+	/* the tile: frame f's row segment by wave f % 4, sample of pixel px at lfx_cols[px LS + f] */
+	{
+		const int px = lane, x = x0 + px;
+		uint16_t *dst = lfx_cols + px * LS;
+		const uint16_t *plane = p.frames + (int64_t)c * p.plane_stride;
+#pragma unroll 8
+		for (int f = wave; f < N; f += 4) {
+			int sx = 0, sy = 0;
+			if (p.use_shift) {
+				sx = p.shiftx[f];
+				sy = p.shifty[f];
+			}
+			const int sr = R - sy, sc = x - sx;
+			const bool colok = (unsigned)sc < (unsigned)p.W;
+			uint16_t v = 0;
+			if (colok && (unsigned)sr < (unsigned)p.H)
+				v = plane[(int64_t)f * p.frame_stride + (int64_t)sr * p.W + sc];
+			dst[f] = colok ? sg_normalize(p, f, v) : (uint16_t)0;
+		}
+		for (int f = N + wave; f < 64 * KM; f += 4)
+			dst[f] = 0xFFFF;
+	}
+	__syncthreads();
+	const int np = min(64, p.W - x0);
+	/* pixel pairs (q, q + 4) of wave q % 4 sorted together (packed halves) */
+	for (int q0 = wave; q0 < np; q0 += 8) {
+		uint32_t v2[KM];
+#pragma unroll
+		for (int k = 0; k < KM; k++)
+			v2[k] = (uint32_t)lfx_cols[q0 * LS + 64 * k + lane] |
+				((uint32_t)lfx_cols[(q0 + 4 < 64 ? q0 + 4 : q0) * LS + 64 * k + lane] << 16);
+		lfx_sort<KM>(v2, lane);
+#pragma unroll 1
+		for (int h = 0; h < 2; h++) {
+			const int q = q0 + 4 * h;
+			if (q >= np)
+				break;
+			uint32_t v[KM];
+#pragma unroll
+			for (int k = 0; k < KM; k++)
+				v[k] = h ? v2[k] >> 16 : v2[k] & 0xFFFFu;
+			const int64_t pix = ((int64_t)c * p.H + R) * p.W + x0 + q;
+			uint16_t value = 0;
+			uint32_t rl = 0, rh = 0;
+			const int ok = lfx_pixel<KM>(v, N, p.sig0, p.sig1, lane, value, rl, rh);
+			if (lane == 0) {
+				if (ok) {
+					p.out[pix] = value;
+					unsigned long long *sh = p.rej + ((size_t)(blockIdx.x % SG_REJ_SHARDS) * 6 + c * 2);
+					if (rl)
+						atomicAdd(sh, (unsigned long long)rl);
+					if (rh)
+						atomicAdd(sh + 1, (unsigned long long)rh);
+				} else {
+					redo_list[atomicAdd(redo_count, 1u)] = (unsigned int)pix;
+				}
+			}
+		}
+	}
+}
+template __global__ void k_stack_linfit<8>(SgStackParams, unsigned int *, unsigned int *);
+template __global__ void k_stack_linfit<16>(SgStackParams, unsigned int *, unsigned int *);
+
 /* the histogram path's redo list queued for k_stack_replay / k_stack_literal: class
  * LITERAL, appended to the flag list the sorted kernel would have appended them to.  The
  * count is read on the device; a list longer than maxn is left to the sorted kernel. */

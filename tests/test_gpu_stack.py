@@ -113,11 +113,50 @@ def test_linearfit_sorted_path(gpu_ctx, N, sig):
     sx, sy = orc.synth_shifts(N, seed=800 + N, maxshift=3)
     rc, ref, rej_ref = orc.stack_rejection(frames, sg.LINEARFIT, sig=sig, shiftx=sx, shifty=sy, max_thread=2)
     assert rc == 0
-    out, rej, _ = gpu_stack(gpu_ctx, frames, sg.MEAN, sg.LINEARFIT, sig, sx, sy, max_thread=2)
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=sg.LINEARFIT, sig=sig, shiftx=sx, shifty=sy,
+                              max_thread=2, max_number_of_rows=H, kernel_path=sg.PATH_SORTED)
+    rc, out, rej, _ = gpu_ctx.stack_host(desc, np.ascontiguousarray(frames))
+    assert rc == 0, gpu_ctx.error()
+    assert gpu_ctx.stats().path == 0
     assert_same(out, ref, f"linearfit N={N} sig={sig}")
     assert np.array_equal(rej, rej_ref), (rej, rej_ref)
     if sig == (5.0, 5.0) and N >= 64:
         assert gpu_ctx.stats().slow_pixels <= 0.05 * H * W, gpu_ctx.stats().slow_pixels
+
+
+@pytest.mark.parametrize("N", [16, 100, 512, 700])
+@pytest.mark.parametrize("normalize", [sg.NO_NORM, sg.ADDITIVE_SCALING])
+@pytest.mark.parametrize("sig", [(5.0, 5.0), (2.0, 2.0), (1.0, 3.0)])
+def test_linearfit_fast_path(gpu_ctx, N, normalize, sig):
+    """LINEARFIT on the decision-exact kernel (k_stack_linfit: the fit from exact integer sums,
+    every clip decided outside the bound on the reference's recurrence error, the rest through the
+    sorted kernel's replay): image and counters equal the oracle, with shifts, normalisation,
+    degenerate columns (constant, an exact ramp: sigma 0, the reference's rounding noise decides)
+    and heavy rejection (the early break); few pixels leave the fast kernel"""
+    H, W = 12, 200
+    frames = _outlier_frames(N, H, W, 1300 + N)
+    frames[:, 0, :, 3] = 1234                                                   # constant column
+    frames[:, 0, :, 5] = (1000 + 7 * np.arange(N))[:, None].astype(np.uint16)   # exact ramp
+    rng = np.random.default_rng(N)
+    half = rng.random(N) < 0.5
+    frames[half, 0, :, 9] = 60000                                               # half the stack hot
+    sx, sy = orc.synth_shifts(N, seed=1300 + N, maxshift=3)
+    off = mul = sc = None
+    if normalize != sg.NO_NORM:
+        loc = 1000 + rng.random(N) * 60
+        scl = 30 + rng.random(N) * 5
+        off, mul, sc = orc.compute_normalization(normalize, loc, scl, ref_image=0)
+    rc, ref, rej_ref = orc.stack_rejection(frames, sg.LINEARFIT, sig=sig, shiftx=sx, shifty=sy, normalize=normalize,
+                                           offset=off, mul=mul, scale=sc, max_thread=2)
+    assert rc == 0
+    out, rej, _ = gpu_stack(gpu_ctx, frames, sg.MEAN, sg.LINEARFIT, sig, sx, sy, normalize=normalize, offset=off,
+                            mul=mul, scale=sc, max_thread=2)
+    st = gpu_ctx.stats()
+    assert st.path == 1
+    assert_same(out, ref, f"linearfit fast N={N} norm={normalize} sig={sig}")
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+    if sig == (5.0, 5.0):
+        assert st.chain_pixels <= 0.05 * H * W, st.chain_pixels   # the redo list
 
 
 def test_sigmedian_never_ending_loop_fails(gpu_ctx):
