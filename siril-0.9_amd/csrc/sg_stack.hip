@@ -2354,7 +2354,9 @@ __device__ __forceinline__ void lfx_cx_lanes(uint32_t (&x)[KM], int kk, int lane
 	for (int k = 0; k < KM; k++) {
 		const bool up = ((64 * k + lane) & kk) == 0;
 		const uint32_t y = lfx_xor<J>(x[k], lane);
-		x[k] = (lower == up) ? lfx_pk_min(x[k], y) : lfx_pk_max(x[k], y);
+		/* both computed, then selected (an asm call inside the ?: became a divergent branch) */
+		const uint32_t mn = lfx_pk_min(x[k], y), mx = lfx_pk_max(x[k], y);
+		x[k] = (lower == up) ? mn : mx;
 	}
 }
 template <int KM, int JR>
@@ -2447,7 +2449,6 @@ template <int KM>
 __device__ int lfx_pixel(const uint32_t (&x)[KM], int N0, double sl, double sh, int lane, uint16_t &value,
 		uint32_t &rlo, uint32_t &rhi) {
 	constexpr double u = 1.1102230246251565e-16;
-	const unsigned long long lt = (1ull << lane) - 1ull;
 	uint32_t kept = 0;
 #pragma unroll
 	for (int k = 0; k < KM; k++)
@@ -2455,52 +2456,56 @@ __device__ int lfx_pixel(const uint32_t (&x)[KM], int N0, double sl, double sh, 
 	int N = N0, r = 0;
 	uint32_t clo = 0, chi = 0;
 	double Sy = 0.0;
+	double xd[KM];
+#pragma unroll
+	for (int k = 0; k < KM; k++)
+		xd[k] = (double)x[k];
 	for (int pass = 0; pass < 4096; pass++) {
-		/* ranks of the kept elements in sorted order (ballots), and the exact sums */
+		/* ranks of the kept elements in sorted order (ballots + mbcnt), and the exact sums
+		 * (selects, no divergent blocks) */
 		double rank[KM];
 		int base = 0;
-		uint32_t sy = 0, ymax = 0;
-		double siy = 0.0;
+		uint32_t sy = 0, ymax = 0, siy = 0;	/* rank y < 2^26, a lane's KM <= 16 terms < 2^30 */
 #pragma unroll
 		for (int k = 0; k < KM; k++) {
 			const bool kp = (kept >> k) & 1u;
 			const unsigned long long bal = __ballot(kp);
-			const int rk = base + __popcll(bal & lt);
+			const int rk = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+					__builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
 			base += __popcll(bal);
 			rank[k] = (double)rk;
-			if (kp) {
-				sy += x[k];
-				siy += (double)(rk * (int)x[k]);	/* < 2^26 each, a lane's sum < 2^30: exact */
-				ymax = x[k] > ymax ? x[k] : ymax;
-			}
+			const uint32_t xk = kp ? x[k] : 0u;
+			sy += xk;
+			siy += (uint32_t)rk * xk;
+			ymax = xk > ymax ? xk : ymax;
 		}
 		if (N < 8)
 			return 0;
 		Sy = (double)lfx_sum_u32(sy);
-		const double Siy = lfx_sum_f64(siy);
+		const double Siy = lfx_sum_f64((double)siy);
 		ymax = lfx_max_u32(ymax);
-		const double n = (double)N, Y = (double)ymax;
+		const double n = (double)N, Y = (double)ymax, inv_n = 1.0 / n;
 		const double Pn = 12.0 * Siy - 6.0 * (n - 1.0) * Sy;	/* integers < 2^53: exact */
 		const double slope = Pn / (n * (n * n - 1.0));
-		const double b0 = Sy / n - 0.5 * (n - 1.0) * slope;
+		const double b0 = Sy * inv_n - 0.5 * (n - 1.0) * slope;	/* 2u of Sy/n: inside dB's 8 u Rm */
 		/* residuals (line - y, kept for the tests) and their mean absolute value */
 		double dv[KM];
 		double sres = 0.0;
 #pragma unroll
 		for (int k = 0; k < KM; k++) {
-			dv[k] = fma(slope, rank[k], b0) - (double)x[k];
-			if ((kept >> k) & 1u)
-				sres += fabs(dv[k]);
+			dv[k] = fma(slope, rank[k], b0) - xd[k];
+			sres += ((kept >> k) & 1u) ? fabs(dv[k]) : 0.0;
 		}
-		const double sigma = lfx_sum_f64(sres) / n;
+		const double sigma = lfx_sum_f64(sres) * inv_n;	/* 2u: inside dsig */
 		/* how far the reference's values can be from these (4x the bounds above) */
 		const double as = fabs(slope);
 		const double dmx = 2.0 * n * n * u, dmy = 2.0 * n * u * Y;
 		const double dmdx2 = 6.0 * n * n * n * u, dmdxdy = 6.0 * n * n * u * Y;
-		const double mdx2 = (n * n - 1.0) / 12.0;
+		const double mdx2 = (n * n - 1.0) * (1.0 / 12.0);
 		if (!(mdx2 > 4.0 * dmdx2))
 			return 0;
-		const double dS = 4.0 * ((dmdxdy + as * dmdx2) / (mdx2 - dmdx2) + 4.0 * u * as);
+		/* 1 / (mdx2 - dmdx2) <= (4/3) / mdx2 <= 16.3 / n^2 (n >= 8): no division for a bound */
+		const double dS = 4.0 * ((dmdxdy + as * dmdx2) * 16.3 * inv_n * inv_n + 4.0 * u * as);
 		const double Rm = Y + n * as + fabs(b0) + 1.0;
 		const double dB = 4.0 * (dmy + as * dmx + 0.5 * n * dS + 8.0 * u * Rm);
 		const double dline = n * dS + dB + 32.0 * u * Rm;
