@@ -2048,7 +2048,7 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	}
 
 	const bool ref_conc = fp32 && ctx->knobs.reg_refconc;	/* A/B knob SG_REG_REFCONC */
-	bool ref_pending = false;
+	bool ref_pending = false, q_deferred = false;
 	if (ref_conc && !dv.aux2) {
 		HIPCHK(hipStreamCreateWithFlags(&dv.aux2, hipStreamNonBlocking));
 		for (int k = 0; k < 2; k++)
@@ -2146,6 +2146,11 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 			hipLaunchKernelGGL(k_reg_rows_fwd_half<float2>, dim3(S / rpb, np), dim3(row_thr), row_lds32, s, d_sel, fa,
 					fb, S, tw32, work32, en, rpb);
 		HIPCHK(hipGetLastError());
+		if (q_deferred) {	/* SG_REG_QAFTER: the quality estimate beside the column pass instead */
+			q_deferred = false;
+			if (int r = reg_quality_launch(ctx, dv, s, d_sel, S, qframes, &q_launched))
+				return r;
+		}
 		if (ref_pending) {	/* the reference spectrum, from its stream */
 			HIPCHK(hipStreamWaitEvent(s, dv.aux2_ev[1], 0));
 			ref_pending = false;
@@ -2182,9 +2187,13 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int
 	/* the quality estimate on the aux stream, queued behind the main stream's table uploads and
 	 * fills (queued ahead of them, its long-running workgroups held the fills' single workgroup
 	 * back 0.2 ms, profiles/r05m_*) */
-	rc = reg_quality_launch(ctx, dv, s, d_sel, S, qframes, &q_launched);
-	if (rc)
-		return rc;
+	if (fp32 && npairs_total > 0 && ctx->knobs.reg_qafter) {
+		q_deferred = true;
+	} else {
+		rc = reg_quality_launch(ctx, dv, s, d_sel, S, qframes, &q_launched);
+		if (rc)
+			return rc;
+	}
 
 	/* reference spectrum R = FFT2(ref) (half layout: the A' half only; generic: transposed) */
 	if (generic) {
