@@ -2566,6 +2566,117 @@ __device__ int lfx_pixel(const uint32_t (&x)[KM], int N0, double sl, double sh, 
 	return 0;
 }
 
+#ifndef LFX_MASKS
+#define LFX_MASKS 1
+#endif
+/* lfx_pixel with the kept set as one 64-bit lane mask per register (uniform, SGPRs): the ranks
+ * come from mbcnt on the mask, the rejection counts and the removal are mask operations, and a
+ * lane's tests are compares whose results are the masks themselves (no per-lane bit fields); one
+ * margin serves both tests (the larger of the two sides').  Same decisions as lfx_pixel. */
+template <int KM>
+__device__ int lfx_pixel_m(const uint32_t (&x)[KM], int N0, double sl, double sh, int lane, uint16_t &value,
+		uint32_t &rlo, uint32_t &rhi) {
+	constexpr double u = 1.1102230246251565e-16;
+	unsigned long long km[KM];
+#pragma unroll
+	for (int k = 0; k < KM; k++)
+		km[k] = __ballot(64 * k + lane < N0);
+	int N = N0, r = 0;
+	uint32_t clo = 0, chi = 0;
+	double Sy = 0.0;
+	double xd[KM];
+#pragma unroll
+	for (int k = 0; k < KM; k++)
+		xd[k] = (double)x[k];
+	const double asl = fabs(sl), ash = fabs(sh), amx = asl > ash ? asl : ash;
+	for (int pass = 0; pass < 4096; pass++) {
+		double rank[KM];
+		int base = 0;
+		uint32_t sy = 0, ymax = 0, siy = 0;
+#pragma unroll
+		for (int k = 0; k < KM; k++) {
+			const bool kp = (km[k] >> lane) & 1ull;
+			const int rk = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(km[k] >> 32),
+					__builtin_amdgcn_mbcnt_lo((unsigned)km[k], 0u));
+			base += __popcll(km[k]);
+			rank[k] = (double)rk;
+			const uint32_t xk = kp ? x[k] : 0u;
+			sy += xk;
+			siy += (uint32_t)rk * xk;
+			ymax = xk > ymax ? xk : ymax;
+		}
+		if (N < 8)
+			return 0;
+		Sy = (double)lfx_sum_u32(sy);
+		const double Siy = lfx_sum_f64((double)siy);
+		ymax = lfx_max_u32(ymax);
+		const double n = (double)N, Y = (double)ymax, inv_n = 1.0 / n;
+		const double Pn = 12.0 * Siy - 6.0 * (n - 1.0) * Sy;
+		const double slope = Pn / (n * (n * n - 1.0));
+		const double b0 = Sy * inv_n - 0.5 * (n - 1.0) * slope;
+		double dv[KM];
+		double sres = 0.0;
+#pragma unroll
+		for (int k = 0; k < KM; k++) {
+			dv[k] = fma(slope, rank[k], b0) - xd[k];
+			sres += ((km[k] >> lane) & 1ull) ? fabs(dv[k]) : 0.0;
+		}
+		const double sigma = lfx_sum_f64(sres) * inv_n;
+		const double as = fabs(slope);
+		const double dmx = 2.0 * n * n * u, dmy = 2.0 * n * u * Y;
+		const double dmdx2 = 6.0 * n * n * n * u, dmdxdy = 6.0 * n * n * u * Y;
+		const double mdx2 = (n * n - 1.0) * (1.0 / 12.0);
+		if (!(mdx2 > 4.0 * dmdx2))
+			return 0;
+		const double dS = 4.0 * ((dmdxdy + as * dmdx2) * 16.3 * inv_n * inv_n + 4.0 * u * as);
+		const double Rm = Y + n * as + fabs(b0) + 1.0;
+		const double dB = 4.0 * (dmy + as * dmx + 0.5 * n * dS + 8.0 * u * Rm);
+		const double dline = n * dS + dB + 32.0 * u * Rm;
+		const double dsig = 4.0 * (dline + 2.0 * (n + 2.0) * u * Rm);
+		if (!(sigma > 4.0 * dsig) || !(sl == sl) || !(sh == sh) || !(sl > 0.0) || !(sh > 0.0))
+			return 0;	/* non-positive factors: the else-if order matters, the general path decides */
+		const double tL = sl * sigma, tH = sh * sigma;
+		const double e1 = 4.0 * dS;
+		const double eM = 4.0 * (dB + 32.0 * u * Rm + amx * dsig + 4.0 * u * (Rm + amx * sigma));
+		/* with sl, sh > 0 a sample is at most one of low (line - y > tL) and high (y - line > tH) */
+		unsigned long long amb = 0;
+		int nl = 0, nh = 0;
+#pragma unroll
+		for (int k = 0; k < KM; k++) {
+			const double e = fma(e1, rank[k], eM);
+			const double a = dv[k] - tL, b = dv[k] + tH;
+			const unsigned long long lo = __ballot(a > e) & km[k], hi = __ballot(b < -e) & km[k];
+			amb |= __ballot(fabs(a) <= e || fabs(b) <= e) & km[k];
+			nl += __popcll(lo);
+			nh += __popcll(hi);
+			km[k] &= ~(lo | hi);
+		}
+		if (amb)
+			return 0;
+		const int nrej = nl + nh;
+		if (r + nrej >= N - 4)
+			return 0;
+		clo += nl;
+		chi += nh;
+		r += nrej;
+		N -= nrej;
+		if (!(nrej > 0 && N > 3)) {
+			if (nrej > 0) {
+				uint32_t s2 = 0;
+#pragma unroll
+				for (int k = 0; k < KM; k++)
+					s2 += ((km[k] >> lane) & 1ull) ? x[k] : 0u;
+				Sy = (double)lfx_sum_u32(s2);
+			}
+			value = sg_round_to_WORD(Sy / (double)N);
+			rlo = clo;
+			rhi = chi;
+			return 1;
+		}
+	}
+	return 0;
+}
+
 template <int KM>
 __global__ void __launch_bounds__(256)
 k_stack_linfit(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
@@ -2624,7 +2735,8 @@ k_stack_linfit(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned 
 			const int64_t pix = ((int64_t)c * p.H + R) * p.W + x0 + q;
 			uint16_t value = 0;
 			uint32_t rl = 0, rh = 0;
-			const int ok = lfx_pixel<KM>(v, N, p.sig0, p.sig1, lane, value, rl, rh);
+			const int ok = LFX_MASKS ? lfx_pixel_m<KM>(v, N, p.sig0, p.sig1, lane, value, rl, rh)
+						 : lfx_pixel<KM>(v, N, p.sig0, p.sig1, lane, value, rl, rh);
 			if (lane == 0) {
 				if (ok) {
 					p.out[pix] = value;
