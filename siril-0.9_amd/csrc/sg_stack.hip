@@ -2608,7 +2608,8 @@ __device__ int lfx_pixel_m(const uint32_t (&x)[KM], int N0, double sl, double sh
 		if (N < 8)
 			return 0;
 		Sy = (double)lfx_sum_u32(sy);
-		const double Siy = lfx_sum_f64((double)siy);
+		/* S_iy < 2^36: two integer wave sums of its 16-bit halves (a lane's siy < 2^30) */
+		const double Siy = (double)lfx_sum_u32(siy & 0xFFFFu) + 65536.0 * (double)lfx_sum_u32(siy >> 16);
 		ymax = lfx_max_u32(ymax);
 		const double n = (double)N, Y = (double)ymax, inv_n = 1.0 / n;
 		const double Pn = 12.0 * Siy - 6.0 * (n - 1.0) * Sy;
