@@ -2350,9 +2350,11 @@ __device__ __forceinline__ uint32_t lfx_pk_max(uint32_t a, uint32_t b) {
 template <int KM, int J>
 __device__ __forceinline__ void lfx_cx_lanes(uint32_t (&x)[KM], int kk, int lane) {
 	const bool lower = (lane & J) == 0;
+	/* ((64 k + lane) & kk) == 0 splits into a lane part (kk < 64) and a uniform k part (kk >= 64) */
+	const bool lane_up = (lane & kk) == 0;
 #pragma unroll
 	for (int k = 0; k < KM; k++) {
-		const bool up = ((64 * k + lane) & kk) == 0;
+		const bool up = ((64 * k) & kk) == 0 && lane_up;
 		const uint32_t y = lfx_xor<J>(x[k], lane);
 		/* both computed, then selected (an asm call inside the ?: became a divergent branch) */
 		const uint32_t mn = lfx_pk_min(x[k], y), mx = lfx_pk_max(x[k], y);
@@ -2361,10 +2363,11 @@ __device__ __forceinline__ void lfx_cx_lanes(uint32_t (&x)[KM], int kk, int lane
 }
 template <int KM, int JR>
 __device__ __forceinline__ void lfx_cx_reg(uint32_t (&x)[KM], int kk, int lane) {
+	(void)lane;	/* kk >= 128 here: the direction is uniform per register */
 #pragma unroll
 	for (int k = 0; k < KM; k++) {
 		if ((k & JR) == 0 && (k | JR) < KM) {
-			const bool up = ((64 * k + lane) & kk) == 0;
+			const bool up = ((64 * k) & kk) == 0;
 			const uint32_t u = x[k], v = x[k | JR];
 			const uint32_t mn = lfx_pk_min(u, v), mx = lfx_pk_max(u, v);
 			x[k] = up ? mn : mx;
@@ -2623,15 +2626,13 @@ __device__ int lfx_pixel_m(const uint32_t (&x)[KM], int N0, double sl, double sh
 			sres += ((km[k] >> lane) & 1ull) ? fabs(dv[k]) : 0.0;
 		}
 		const double sigma = lfx_sum_f64(sres) * inv_n;
-		const double as = fabs(slope);
-		const double dmx = 2.0 * n * n * u, dmy = 2.0 * n * u * Y;
-		const double dmdx2 = 6.0 * n * n * n * u, dmdxdy = 6.0 * n * n * u * Y;
-		const double mdx2 = (n * n - 1.0) * (1.0 / 12.0);
-		if (!(mdx2 > 4.0 * dmdx2))
-			return 0;
-		const double dS = 4.0 * ((dmdxdy + as * dmdx2) * 16.3 * inv_n * inv_n + 4.0 * u * as);
-		const double Rm = Y + n * as + fabs(b0) + 1.0;
-		const double dB = 4.0 * (dmy + as * dmx + 0.5 * n * dS + 8.0 * u * Rm);
+		/* lfx_pixel's bounds in closed form (8 <= n <= 1024: mdx2 - dmdx2 >= 0.75 mdx2, and
+		 * 1 / mdx2 <= 12.2 / n^2): dS = 4 ((6 n^2 u Y + |s| 6 n^3 u) 16.3 / n^2 + 4 u |s|) rounded
+		 * up to 392 u (Y + (n + 1) |s|); dB = 4 (2 n u Y + 2 n^2 u |s| + n dS / 2 + 8 u Rm) */
+		const double as = fabs(slope), nas = n * as;
+		const double dS = 392.0 * u * (Y + nas + as);
+		const double Rm = Y + nas + fabs(b0) + 1.0;
+		const double dB = 4.0 * (2.0 * u * n * (Y + nas) + 0.5 * n * dS + 8.0 * u * Rm);
 		const double dline = n * dS + dB + 32.0 * u * Rm;
 		const double dsig = 4.0 * (dline + 2.0 * (n + 2.0) * u * Rm);
 		if (!(sigma > 4.0 * dsig) || !(sl == sl) || !(sh == sh) || !(sl > 0.0) || !(sh > 0.0))
