@@ -2447,135 +2447,11 @@ __device__ __forceinline__ double lfx_sum_f64(double v) {
 }
 
 /* one pixel's passes; x[] sorted ascending (pads 0xFFFF at elements >= N0).  Returns 1 with the
- * value and counters, 0 when the pixel goes to the redo list. */
-template <int KM>
-__device__ int lfx_pixel(const uint32_t (&x)[KM], int N0, double sl, double sh, int lane, uint16_t &value,
-		uint32_t &rlo, uint32_t &rhi) {
-	constexpr double u = 1.1102230246251565e-16;
-	uint32_t kept = 0;
-#pragma unroll
-	for (int k = 0; k < KM; k++)
-		kept |= (64 * k + lane < N0 ? 1u : 0u) << k;
-	int N = N0, r = 0;
-	uint32_t clo = 0, chi = 0;
-	double Sy = 0.0;
-	double xd[KM];
-#pragma unroll
-	for (int k = 0; k < KM; k++)
-		xd[k] = (double)x[k];
-	for (int pass = 0; pass < 4096; pass++) {
-		/* ranks of the kept elements in sorted order (ballots + mbcnt), and the exact sums
-		 * (selects, no divergent blocks) */
-		double rank[KM];
-		int base = 0;
-		uint32_t sy = 0, ymax = 0, siy = 0;	/* rank y < 2^26, a lane's KM <= 16 terms < 2^30 */
-#pragma unroll
-		for (int k = 0; k < KM; k++) {
-			const bool kp = (kept >> k) & 1u;
-			const unsigned long long bal = __ballot(kp);
-			const int rk = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
-					__builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
-			base += __popcll(bal);
-			rank[k] = (double)rk;
-			const uint32_t xk = kp ? x[k] : 0u;
-			sy += xk;
-			siy += (uint32_t)rk * xk;
-			ymax = xk > ymax ? xk : ymax;
-		}
-		if (N < 8)
-			return 0;
-		Sy = (double)lfx_sum_u32(sy);
-		const double Siy = lfx_sum_f64((double)siy);
-		ymax = lfx_max_u32(ymax);
-		const double n = (double)N, Y = (double)ymax, inv_n = 1.0 / n;
-		const double Pn = 12.0 * Siy - 6.0 * (n - 1.0) * Sy;	/* integers < 2^53: exact */
-		const double slope = Pn / (n * (n * n - 1.0));
-		const double b0 = Sy * inv_n - 0.5 * (n - 1.0) * slope;	/* 2u of Sy/n: inside dB's 8 u Rm */
-		/* residuals (line - y, kept for the tests) and their mean absolute value */
-		double dv[KM];
-		double sres = 0.0;
-#pragma unroll
-		for (int k = 0; k < KM; k++) {
-			dv[k] = fma(slope, rank[k], b0) - xd[k];
-			sres += ((kept >> k) & 1u) ? fabs(dv[k]) : 0.0;
-		}
-		const double sigma = lfx_sum_f64(sres) * inv_n;	/* 2u: inside dsig */
-		/* how far the reference's values can be from these (4x the bounds above) */
-		const double as = fabs(slope);
-		const double dmx = 2.0 * n * n * u, dmy = 2.0 * n * u * Y;
-		const double dmdx2 = 6.0 * n * n * n * u, dmdxdy = 6.0 * n * n * u * Y;
-		const double mdx2 = (n * n - 1.0) * (1.0 / 12.0);
-		if (!(mdx2 > 4.0 * dmdx2))
-			return 0;
-		/* 1 / (mdx2 - dmdx2) <= (4/3) / mdx2 <= 16.3 / n^2 (n >= 8): no division for a bound */
-		const double dS = 4.0 * ((dmdxdy + as * dmdx2) * 16.3 * inv_n * inv_n + 4.0 * u * as);
-		const double Rm = Y + n * as + fabs(b0) + 1.0;
-		const double dB = 4.0 * (dmy + as * dmx + 0.5 * n * dS + 8.0 * u * Rm);
-		const double dline = n * dS + dB + 32.0 * u * Rm;
-		const double dsig = 4.0 * (dline + 2.0 * (n + 2.0) * u * Rm);
-		if (!(sigma > 4.0 * dsig) || !(sl == sl) || !(sh == sh))
-			return 0;
-		/* line_clipping (:1170-1183), low first (else if); the margin of element k is
-		 * e0 + e1 rank (|d| <= Rm) */
-		const double tL = sl * sigma, tH = sh * sigma;
-		const double e1 = 4.0 * dS;
-		const double eL = 4.0 * (dB + 32.0 * u * Rm + fabs(sl) * dsig + 4.0 * u * (Rm + fabs(tL)));
-		const double eH = 4.0 * (dB + 32.0 * u * Rm + fabs(sh) * dsig + 4.0 * u * (Rm + fabs(tH)));
-		uint32_t lo_bits = 0, hi_bits = 0;
-		bool amb = false;
-#pragma unroll
-		for (int k = 0; k < KM; k++) {
-			if (!((kept >> k) & 1u))
-				continue;
-			const double tl = dv[k] - tL, th = -dv[k] - tH;
-			const double el = fma(e1, rank[k], eL), eh = fma(e1, rank[k], eH);
-			const bool low = tl > el, lamb = fabs(tl) <= el;
-			const bool high = !low && !lamb && th > eh;
-			amb |= lamb || (!low && fabs(th) <= eh);
-			lo_bits |= (low ? 1u : 0u) << k;
-			hi_bits |= (high ? 1u : 0u) << k;
-		}
-		if (__ballot(amb))
-			return 0;
-		int nl = 0, nh = 0;
-#pragma unroll
-		for (int k = 0; k < KM; k++) {
-			nl += __popcll(__ballot((lo_bits >> k) & 1u));
-			nh += __popcll(__ballot((hi_bits >> k) & 1u));
-		}
-		const int nrej = nl + nh;
-		if (r + nrej >= N - 4)	/* the `N - r <= 4` break would fire inside the pass */
-			return 0;
-		clo += nl;
-		chi += nh;
-		kept &= ~(lo_bits | hi_bits);
-		r += nrej;
-		N -= nrej;
-		if (!(nrej > 0 && N > 3)) {
-			if (nrej > 0) {	/* the kept sum after this pass's removal */
-				uint32_t s2 = 0;
-#pragma unroll
-				for (int k = 0; k < KM; k++)
-					if ((kept >> k) & 1u)
-						s2 += x[k];
-				Sy = (double)lfx_sum_u32(s2);
-			}
-			value = sg_round_to_WORD(Sy / (double)N);
-			rlo = clo;
-			rhi = chi;
-			return 1;
-		}
-	}
-	return 0;
-}
-
-#ifndef LFX_MASKS
-#define LFX_MASKS 1
-#endif
-/* lfx_pixel with the kept set as one 64-bit lane mask per register (uniform, SGPRs): the ranks
- * come from mbcnt on the mask, the rejection counts and the removal are mask operations, and a
- * lane's tests are compares whose results are the masks themselves (no per-lane bit fields); one
- * margin serves both tests (the larger of the two sides').  Same decisions as lfx_pixel. */
+ * value and counters, 0 when the pixel goes to the redo list.  The kept set is one 64-bit lane
+ * mask per register (uniform, SGPRs): the ranks come from mbcnt on the mask, the rejection
+ * counts and the removal are mask operations, and a lane's tests are compares whose results are
+ * the masks themselves; one margin serves both tests (the larger of the two sides'; per-lane bit
+ * fields and two margins took 303 ms against 261, profiles/r05z4_*, r05ad_*). */
 template <int KM>
 __device__ int lfx_pixel_m(const uint32_t (&x)[KM], int N0, double sl, double sh, int lane, uint16_t &value,
 		uint32_t &rlo, uint32_t &rhi) {
@@ -2626,7 +2502,7 @@ __device__ int lfx_pixel_m(const uint32_t (&x)[KM], int N0, double sl, double sh
 			sres += ((km[k] >> lane) & 1ull) ? fabs(dv[k]) : 0.0;
 		}
 		const double sigma = lfx_sum_f64(sres) * inv_n;
-		/* lfx_pixel's bounds in closed form (8 <= n <= 1024: mdx2 - dmdx2 >= 0.75 mdx2, and
+		/* the bounds above (the LINEARFIT comment) in closed form (8 <= n <= 1024: mdx2 - dmdx2 >= 0.75 mdx2, and
 		 * 1 / mdx2 <= 12.2 / n^2): dS = 4 ((6 n^2 u Y + |s| 6 n^3 u) 16.3 / n^2 + 4 u |s|) rounded
 		 * up to 392 u (Y + (n + 1) |s|); dB = 4 (2 n u Y + 2 n^2 u |s| + n dS / 2 + 8 u Rm) */
 		const double as = fabs(slope), nas = n * as;
@@ -2737,8 +2613,7 @@ k_stack_linfit(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned 
 			const int64_t pix = ((int64_t)c * p.H + R) * p.W + x0 + q;
 			uint16_t value = 0;
 			uint32_t rl = 0, rh = 0;
-			const int ok = LFX_MASKS ? lfx_pixel_m<KM>(v, N, p.sig0, p.sig1, lane, value, rl, rh)
-						 : lfx_pixel<KM>(v, N, p.sig0, p.sig1, lane, value, rl, rh);
+			const int ok = lfx_pixel_m<KM>(v, N, p.sig0, p.sig1, lane, value, rl, rh);
 			if (lane == 0) {
 				if (ok) {
 					p.out[pix] = value;

@@ -1,4 +1,4 @@
-"""The error bound k_stack_linfit decides LINEARFIT's clips with (sg_stack.hip, lfx_pixel).
+"""The error bound k_stack_linfit decides LINEARFIT's clips with (sg_stack.hip, lfx_pixel_m).
 
 The kernel takes the fit from exact integer sums and decides each `line_clipping` test
 (src/stacking/stacking.c:1170-1183) only when it lies outside a bound on how far the reference's
@@ -55,7 +55,7 @@ def exact_fit(y):
 
 
 def bounds(n, Y, slope, b0):
-    """lfx_pixel's bounds without the 4x factors (the kernel multiplies each by 4)"""
+    """the bounds of lfx_pixel_m before its 4x factors and closed-form rounding up"""
     as_ = abs(slope)
     dmx, dmy = 2.0 * n * n * U, 2.0 * n * U * Y
     dmdx2, dmdxdy = 6.0 * n ** 3 * U, 6.0 * n * n * U * Y
