@@ -2502,15 +2502,17 @@ __device__ int lfx_pixel_m(const uint32_t (&x)[KM], int N0, double sl, double sh
 			sres += ((km[k] >> lane) & 1ull) ? fabs(dv[k]) : 0.0;
 		}
 		const double sigma = lfx_sum_f64(sres) * inv_n;
-		/* the bounds above (the LINEARFIT comment) in closed form (8 <= n <= 1024: mdx2 - dmdx2 >= 0.75 mdx2, and
-		 * 1 / mdx2 <= 12.2 / n^2): dS = 4 ((6 n^2 u Y + |s| 6 n^3 u) 16.3 / n^2 + 4 u |s|) rounded
-		 * up to 392 u (Y + (n + 1) |s|); dB = 4 (2 n u Y + 2 n^2 u |s| + n dS / 2 + 8 u Rm) */
+		/* the bounds above (the LINEARFIT comment) in closed form, before one 4x safety factor on
+		 * each test's margin (8 <= n <= 1024: mdx2 - dmdx2 >= 0.75 mdx2 and 1 / mdx2 <= 12.2 / n^2):
+		 * dS = (6 n^2 u Y + |s| 6 n^3 u) 16.3 / n^2 + 4 u |s| rounded up to 98 u (Y + (n + 1) |s|);
+		 * dB = 2 n u Y + 2 n^2 u |s| + n dS / 2 + 8 u Rm.  (Each level took its own 4x until round 5:
+		 * 16-64x on a test, 10.5 k redo pixels.) */
 		const double as = fabs(slope), nas = n * as;
-		const double dS = 392.0 * u * (Y + nas + as);
+		const double dS = 98.0 * u * (Y + nas + as);
 		const double Rm = Y + nas + fabs(b0) + 1.0;
-		const double dB = 4.0 * (2.0 * u * n * (Y + nas) + 0.5 * n * dS + 8.0 * u * Rm);
+		const double dB = 2.0 * u * n * (Y + nas) + 0.5 * n * dS + 8.0 * u * Rm;
 		const double dline = n * dS + dB + 32.0 * u * Rm;
-		const double dsig = 4.0 * (dline + 2.0 * (n + 2.0) * u * Rm);
+		const double dsig = dline + 2.0 * (n + 2.0) * u * Rm;
 		if (!(sigma > 4.0 * dsig) || !(sl == sl) || !(sh == sh) || !(sl > 0.0) || !(sh > 0.0))
 			return 0;	/* non-positive factors: the else-if order matters, the general path decides */
 		const double tL = sl * sigma, tH = sh * sigma;

@@ -6,8 +6,8 @@ rounded `gsl_fit_linear` recurrences (:1750-1784) can be from the exact fit.  Th
 that bound: on random and adversarial sorted stacks it runs GSL's double recurrences exactly as
 the reference does (numpy float64 scalars, the same operation order), computes the exact slope,
 intercept and mean absolute residual with rationals, and checks that every deviation stays within
-the per-quantity bounds the kernel uses before its 4x safety factor (on these stacks the largest
-observed error is 2.3e-3 of its bound: intercept; 4.3e-4 slope, 2.4e-4 sigma).
+the per-quantity bounds the kernel uses before the 4x safety factor on each test's margin (on these
+stacks the largest observed error is 2.3e-3 of its bound: intercept; 4.3e-4 slope, 2.4e-4 sigma).
 """
 from fractions import Fraction
 
@@ -55,7 +55,7 @@ def exact_fit(y):
 
 
 def bounds(n, Y, slope, b0):
-    """the bounds of lfx_pixel_m before its 4x factors and closed-form rounding up"""
+    """the bounds of lfx_pixel_m before its 4x factor and closed-form rounding up"""
     as_ = abs(slope)
     dmx, dmy = 2.0 * n * n * U, 2.0 * n * U * Y
     dmdx2, dmdxdy = 6.0 * n ** 3 * U, 6.0 * n * n * U * Y
@@ -113,3 +113,17 @@ def test_bound_is_not_vacuous():
     almost every test: at N = 512, Y = 65535 every bound is under 1e-5"""
     dS, dB, dline, dsig = bounds(512, 65535.0, 120.0, 2000.0)
     assert 4 * dline < 1e-5 and 4 * dsig < 1e-4
+
+
+def test_closed_form_covers_bound():
+    """lfx_pixel_m rounds the bounds up to closed forms; they must not fall below the derivation"""
+    for n in (8, 9, 16, 100, 512, 1024):
+        for Y in (1.0, 300.0, 65535.0):
+            for s in (0.0, 0.01, 3.0, 1.75 * Y / n):
+                for b0 in (0.0, Y, -Y):
+                    dS, dB, dline, dsig = bounds(n, Y, s, b0)
+                    as_ = abs(s)
+                    kS = 98.0 * U * (Y + n * as_ + as_)
+                    Rm = Y + n * as_ + abs(b0) + 1.0
+                    kB = 2.0 * U * n * (Y + n * as_) + 0.5 * n * kS + 8.0 * U * Rm
+                    assert kS >= dS and kB >= dB, (n, Y, s, kS, dS, kB, dB)
