@@ -124,7 +124,7 @@ def test_linearfit_sorted_path(gpu_ctx, N, sig):
         assert gpu_ctx.stats().slow_pixels <= 0.05 * H * W, gpu_ctx.stats().slow_pixels
 
 
-@pytest.mark.parametrize("N", [16, 100, 512, 700])
+@pytest.mark.parametrize("N", [16, 100, 512, 700, 1024])
 @pytest.mark.parametrize("normalize", [sg.NO_NORM, sg.ADDITIVE_SCALING])
 @pytest.mark.parametrize("sig", [(5.0, 5.0), (2.0, 2.0), (1.0, 3.0)])
 def test_linearfit_fast_path(gpu_ctx, N, normalize, sig):
