@@ -33,7 +33,7 @@ __global__ void k_stack_sorted(SgStackParams p, const unsigned int *list, const 
 template <int REJ, int NORM, int NI>
 __global__ void k_stack_hist(SgStackParams p, const int *tab, const int4 *norm, unsigned int *redo_count,
 		unsigned int *redo_list);
-template <int KM>
+template <int KM, int NW>
 __global__ void k_stack_linfit(SgStackParams p, unsigned int *redo_count, unsigned int *redo_list);
 void sg_dbg_why_dump(hipStream_t s);
 int sgh_block_threads(int ni, int rej);
@@ -855,13 +855,16 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 				/* one workgroup per 64 pixels of a row, the tile's columns in LDS */
 				const int km = N <= 512 ? 8 : 16;
 				const size_t lfx_lds = (size_t)64 * (64 * km + 2) * sizeof(uint16_t);
-				const void *kf = km == 8 ? (const void *)k_stack_linfit<8> : (const void *)k_stack_linfit<16>;
+				/* waves per tile: 4, 8 or (KM = 8 only: 187 VGPRs at KM = 16) 16 */
+				const int lw = ctx->knobs.linfit_waves;
+				const int nw = lw == 4 ? 4 : (lw == 16 && km == 8) ? 16 : 8;
+				const void *kf = km == 8 ? (nw == 4 ? (const void *)k_stack_linfit<8, 4> :
+						nw == 8 ? (const void *)k_stack_linfit<8, 8> : (const void *)k_stack_linfit<8, 16>) :
+					(nw == 4 ? (const void *)k_stack_linfit<16, 4> : (const void *)k_stack_linfit<16, 8>);
 				(void)hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lfx_lds);
 				const dim3 lg((unsigned)((size_t)((W + 63) / 64) * nrows * C));
-				if (km == 8)
-					hipLaunchKernelGGL(k_stack_linfit<8>, lg, dim3(256), lfx_lds, s, p, redo_count, redo_list);
-				else
-					hipLaunchKernelGGL(k_stack_linfit<16>, lg, dim3(256), lfx_lds, s, p, redo_count, redo_list);
+				void *lfx_args[] = {&p, &redo_count, &redo_list};
+				(void)hipLaunchKernel(kf, lg, dim3(64 * nw), lfx_args, lfx_lds, s);
 			} else
 			switch ((rj == 4 ? 10 : rj == 1 ? 20 : rj == 8 ? 30 : rj == 3 ? 40 : 0) + norm +
 					100 * (rj == 1 || rj == 8 || rj == 3 ? 1 : ni)) {

@@ -2557,8 +2557,8 @@ __device__ int lfx_pixel_m(const uint32_t (&x)[KM], int N0, double sl, double sh
 	return 0;
 }
 
-template <int KM>
-__global__ void __launch_bounds__(256)
+template <int KM, int NW>
+__global__ void __launch_bounds__(64 * NW)
 k_stack_linfit(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
 	extern __shared__ uint16_t lfx_cols[];
 	constexpr int LS = 64 * KM + 2;	/* column stride: an odd dword count (conflict-free stores) */
@@ -2571,13 +2571,13 @@ k_stack_linfit(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned 
 	bid /= ntx;
 	const int R = p.row_begin + (bid % nrows), c = bid / nrows;
 	const int x0 = xt * 64;
-	/* the tile: frame f's row segment by wave f % 4, sample of pixel px at lfx_cols[px LS + f] */
+	/* the tile: frame f's row segment by wave f % NW, sample of pixel px at lfx_cols[px LS + f] */
 	{
 		const int px = lane, x = x0 + px;
 		uint16_t *dst = lfx_cols + px * LS;
 		const uint16_t *plane = p.frames + (int64_t)c * p.plane_stride;
 #pragma unroll 8
-		for (int f = wave; f < N; f += 4) {
+		for (int f = wave; f < N; f += NW) {
 			int sx = 0, sy = 0;
 			if (p.use_shift) {
 				sx = p.shiftx[f];
@@ -2590,22 +2590,23 @@ k_stack_linfit(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned 
 				v = plane[(int64_t)f * p.frame_stride + (int64_t)sr * p.W + sc];
 			dst[f] = colok ? sg_normalize(p, f, v) : (uint16_t)0;
 		}
-		for (int f = N + wave; f < 64 * KM; f += 4)
+		for (int f = N + wave; f < 64 * KM; f += NW)
 			dst[f] = 0xFFFF;
 	}
 	__syncthreads();
 	const int np = min(64, p.W - x0);
-	/* pixel pairs (q, q + 4) of wave q % 4 sorted together (packed halves) */
-	for (int q0 = wave; q0 < np; q0 += 8) {
+	/* pixel pairs (q, q + NW) of wave q % NW sorted together (packed halves).  The fit passes are
+	 * a serial chain of wave reductions: NW waves per tile (8: four per SIMD at KM = 8) hide it */
+	for (int q0 = wave; q0 < np; q0 += 2 * NW) {
 		uint32_t v2[KM];
 #pragma unroll
 		for (int k = 0; k < KM; k++)
 			v2[k] = (uint32_t)lfx_cols[q0 * LS + 64 * k + lane] |
-				((uint32_t)lfx_cols[(q0 + 4 < 64 ? q0 + 4 : q0) * LS + 64 * k + lane] << 16);
+				((uint32_t)lfx_cols[(q0 + NW < 64 ? q0 + NW : q0) * LS + 64 * k + lane] << 16);
 		lfx_sort<KM>(v2, lane);
 #pragma unroll 1
 		for (int h = 0; h < 2; h++) {
-			const int q = q0 + 4 * h;
+			const int q = q0 + NW * h;
 			if (q >= np)
 				break;
 			uint32_t v[KM];
@@ -2631,8 +2632,11 @@ k_stack_linfit(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned 
 		}
 	}
 }
-template __global__ void k_stack_linfit<8>(SgStackParams, unsigned int *, unsigned int *);
-template __global__ void k_stack_linfit<16>(SgStackParams, unsigned int *, unsigned int *);
+template __global__ void k_stack_linfit<8, 4>(SgStackParams, unsigned int *, unsigned int *);
+template __global__ void k_stack_linfit<8, 8>(SgStackParams, unsigned int *, unsigned int *);
+template __global__ void k_stack_linfit<8, 16>(SgStackParams, unsigned int *, unsigned int *);
+template __global__ void k_stack_linfit<16, 4>(SgStackParams, unsigned int *, unsigned int *);
+template __global__ void k_stack_linfit<16, 8>(SgStackParams, unsigned int *, unsigned int *);
 
 /* the histogram path's redo list queued for k_stack_replay / k_stack_literal: class
  * LITERAL, appended to the flag list the sorted kernel would have appended them to.  The
