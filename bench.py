@@ -241,21 +241,43 @@ def cpu_baseline_config(args, workload, N, C, H, W, S, layer):
             "seconds_register_per_frame": round(t_reg, 4), "seconds_stack_scaled": round(t_stack, 3)}
 
 
-def roofline(achieved, algo_bytes, N, H, W, rejection, with_traffic=True):
+def load_traffic(path, r, key="traffic_bytes"):
+    """the PMC capture at `path` (scripts/pmc_traffic.py) when it describes the kernel sources
+    being run: its src_id must equal the digest of the current sources (sg_srcid); a capture of
+    an older build (or one without an id) is reported as traffic_stale and its bytes dropped"""
+    import sg_srcid
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        t = json.load(f)
+    kern = ",".join(t["kernels"]) if "kernels" in t else t["kernel"]
+    try:
+        now = sg_srcid.source_id(kern)
+    except (KeyError, OSError):
+        now = None
+    if t.get("src_id") is None or t.get("src_id") != now:
+        r["traffic_stale"] = {"src": os.path.relpath(path, ROOT), "capture_src_id": t.get("src_id"),
+                              "built_src_id": now}
+        return None
+    r["traffic_src"] = os.path.relpath(path, ROOT)
+    r["traffic_src_id"] = now
+    return t
+
+
+def roofline(achieved, algo_bytes, N, H, W, rejection, with_traffic=True, profiles=None):
     """roofline object of the dominant kernel (k_stack_hist for sigma): achieved = algorithmic
     bytes per launch / HIP-event kernel time; traffic = HBM bytes per launch from the
     rocprofv3 FETCH_SIZE / WRITE_SIZE passes of the same workload (scripts/gpu.sh pmc ->
-    profiles/traffic_<workload>.json, corrected per MI355X_MICROARCH.md), when present"""
+    profiles/traffic_<workload>.json, corrected per MI355X_MICROARCH.md), when present and
+    captured from the sources being run (load_traffic)"""
     r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None}
-    path = os.path.join(ROOT, "profiles", f"traffic_{rejection}_{N}x{H}x{W}.json")
-    if with_traffic and os.path.exists(path):
-        with open(path) as f:
-            t = json.load(f)
+    path = os.path.join(profiles or os.path.join(ROOT, "profiles"), f"traffic_{rejection}_{N}x{H}x{W}.json")
+    t = load_traffic(path, r) if with_traffic else None
+    if t is not None:
         r["traffic"] = int(t["traffic_bytes"])
         r["traffic_unit"] = "B/launch"
         r["traffic_over_algorithmic"] = round(t["traffic_bytes"] / algo_bytes, 4)
-        r["traffic_src"] = os.path.relpath(path, ROOT)
     return r
 
 
@@ -501,13 +523,11 @@ def stack_roofline(achieved, algo_bytes, rej, N, C, H, W, world):
          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "stack"}
     name = "winsorized" if rej == sg.WINSORIZED else "mean"
     path = os.path.join(ROOT, "profiles", f"traffic_{name}_{N}x{C}x{H}x{W}.json")
-    if world == 1 and os.path.exists(path):
-        with open(path) as f:
-            t = json.load(f)
+    t = load_traffic(path, r) if world == 1 else None
+    if t is not None:
         r["traffic"] = int(t["traffic_bytes"])
         r["traffic_unit"] = "B/launch"
         r["traffic_over_algorithmic"] = round(t["traffic_bytes"] / algo_bytes, 4)
-        r["traffic_src"] = os.path.relpath(path, ROOT)
     return r
 
 
@@ -621,11 +641,9 @@ def main_config(args):
     # the traffic
     reg_algo = nsel * S * S * 22
     reg_ms = sum(reg_spans) / len(reg_spans) if reg_spans else stage[1] * 1e3
-    reg_traffic = None
     tpath = os.path.join(ROOT, "profiles", f"traffic_register_{N}x{S}.json")
-    if world == 1 and os.path.exists(tpath):
-        with open(tpath) as f:
-            reg_traffic = json.load(f)
+    reg_tinfo = {}
+    reg_traffic = load_traffic(tpath, reg_tinfo) if world == 1 else None
     if rank == 0:
         res = {
             "metric": "frames/sec stacked (registration + stack) + achieved HBM GB/s",
@@ -660,7 +678,7 @@ def main_config(args):
             rr["traffic_unit"] = "B/step"
             rr["traffic_over_algorithmic"] = round(tb / reg_algo, 4)
             rr["traffic_GBps"] = round(tb / (reg_ms * 1e-3) / 1e9, 1)
-            rr["traffic_src"] = os.path.relpath(tpath, ROOT)
+        rr.update(reg_tinfo)
         sr = stack_roofline(achieved, stack_bytes, rej, N, C, H, W, world)
         if reg_ms >= kavg:
             res["roofline"], res["stack_roofline"] = rr, sr

@@ -31,6 +31,7 @@ fits gfit;
 struct harness_com com = { 16 };
 static int reglayer = -1;
 static int cancel_after = -1;	/* tests: get_thread_run() turns false after this many calls */
+static int fail_read_index = -1;	/* tests: seq_read_frame_part fails for this frame (an unreadable file) */
 
 /* the opened file of a FITS frame: what seq->fptr[i] points to (seq_open_image) */
 struct fitsfile {
@@ -139,6 +140,10 @@ int seq_read_frame_part(sequence *seq, int layer, int index, fits *dest, const r
 	const sg_rect r = { area->x, area->y, area->w, area->h };
 	if (!gs || area->w < 1 || area->h < 1)
 		return 1;
+	if (index == fail_read_index) {	/* readfits_partial / ser_read_frame failing (:571-586) */
+		siril_log_message("Could not load partial image %d from sequence %s\n", index, seq->seqname);
+		return 1;
+	}
 	clearfits(dest);
 	dest->data = malloc((size_t)area->w * area->h * sizeof(WORD));
 	if (!dest->data || sg_seq_read_selection(gs, layer, index, &r, dest->data)) {
@@ -319,6 +324,7 @@ int siril_gpu_set_devices(int n, const int *devs);
 int harness_set_devices(int n, const int *devs) { return siril_gpu_set_devices(n, devs); }
 void harness_set_max_thread(int n) { com.max_thread = n; }
 void harness_set_cancel_after(int n) { cancel_after = n; }
+void harness_set_fail_read(int index) { fail_read_index = index; }
 void harness_set_reference_image(sequence *seq, int ref) { seq->reference_image = ref; }
 void harness_set_included(sequence *seq, int index, int incl) {
 	if (seq->imgparam[index].incl != !!incl)

@@ -331,6 +331,10 @@ int register_shift_dft(struct registration_args *args) {
 		siril_log_message("regparam should have been created before\n");
 		return -1;
 	}
+	/* :213-216: an existing array of this layer is reused (frames not processed keep their
+	 * regdata) and the reuse is logged */
+	if (seq->regparam[args->layer])
+		siril_log_message(_("Recomputing already existing registration for this layer\n"));
 	const int ref = seq->reference_image == -1 ? 0 : seq->reference_image;
 	/* frames per batch: a few pair launches per device of the context */
 	int ndev = 1;
@@ -361,10 +365,15 @@ int register_shift_dft(struct registration_args *args) {
 	{
 		fits fit;
 		memset(&fit, 0, sizeof fit);
-		if (seq_read_frame_part(seq, args->layer, ref, &fit, &args->selection, FALSE)) {
-			siril_log_message(_("Could not load partial image %d\n"), ref);
+		rc = seq_read_frame_part(seq, args->layer, ref, &fit, &args->selection, FALSE);
+		if (rc) {
+			/* :238-244: logged, current_regdata freed, the read's status returned.  The reference
+			 * frees an EXISTING array there without clearing seq->regparam[layer] (a dangling
+			 * pointer); the defined equivalent frees it and clears the pointer */
+			siril_log_message(_("Register: could not load first image to register, aborting.\n"));
 			clearfits(&fit);
-			rc = 1;	/* :238-244 returns its status */
+			free(seq->regparam[args->layer]);
+			seq->regparam[args->layer] = NULL;
 			goto end;
 		}
 		memcpy(bt[0].sel, fit.data, plane * sizeof(WORD));
@@ -392,9 +401,13 @@ int register_shift_dft(struct registration_args *args) {
 			fits fit;
 			memset(&fit, 0, sizeof fit);
 			if (seq_read_frame_part(seq, args->layer, f, &fit, &args->selection, FALSE)) {
-				siril_log_message(_("Could not load partial image %d\n"), f);
+				/* :375-381: the frame's read failed (seq_read_frame_part logged it): the layer's
+				 * registration array is freed, and cleared when it was the sequence's existing
+				 * one (a new array is never published), registration stops, 1 is returned */
 				clearfits(&fit);
-				rc = 1;	/* :373-381 */
+				free(seq->regparam[args->layer]);
+				seq->regparam[args->layer] = NULL;
+				rc = 1;
 				break;
 			}
 			struct reg_batch *b = &bt[cur];

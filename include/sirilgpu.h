@@ -88,7 +88,10 @@ typedef struct {
 } sg_stack_desc;
 /* sg_stack_desc.flags: the output is needed only once sg_stack_collect has returned, so an
  * async call (sg_stack_u16_device_async) may run its work after the main kernel (redo lists,
- * replay, counters) beside the next call's main kernel instead of on `stream` */
+ * replay, counters) beside the next call's main kernel instead of on `stream`.  That work still
+ * READS d_frames and WRITES d_out after `stream` has moved on: both must stay unchanged (the
+ * frames) and unread (the output) until sg_stack_collect returns, or until work queued on a
+ * stream after sg_stack_wait_tail(ctx, dev, stream) */
 #define SG_STACK_RESULT_AT_COLLECT 1
 
 typedef struct sg_ctx sg_ctx;
@@ -167,6 +170,11 @@ int sg_stack_u16_device_async(sg_ctx *ctx, int dev_index, const sg_stack_desc *d
 		const uint16_t *d_frames, int64_t frame_stride, int64_t plane_stride,
 		uint16_t *d_out, int row_begin, int row_end, void *stream);
 int sg_stack_collect(sg_ctx *ctx, int dev_index, uint64_t rej[3][2], uint64_t *maxim);
+/* device-side ordering for SG_STACK_RESULT_AT_COLLECT calls (no reference equivalent: the
+ * reference's blocks are synchronous): work queued on `stream` (NULL = the slot's own stream)
+ * after this returns waits for every tail kernel the slot's async calls have queued so far, so
+ * a band loop may refill d_frames, or read / send d_out, on its stream without a host wait */
+int sg_stack_wait_tail(sg_ctx *ctx, int dev_index, void *stream);
 
 /* Statistics of the last stack call on this context (for bench.py / rocprof cross-checks). */
 typedef struct {

@@ -321,6 +321,16 @@ int or_stack_mean_with_rejection(const or_seq *seq, int rejection, int normalize
 		const double sig[2], const int *shiftx, const int *shifty,
 		const double *offset, const double *mul, const double *scale,
 		int max_thread, int max_number_of_rows, uint16_t *out, uint64_t rej[3][2]) {
+	return or_stack_mean_with_rejection_rows(seq, rejection, normalize, sig, shiftx, shifty, offset, mul, scale,
+			max_thread, max_number_of_rows, out, rej, NULL);
+}
+
+/* the same, also returning each memory row's low / high rejection counts (row_rej[(c H + r) 2 + k],
+ * test infrastructure: a row band's counters are the sum over its rows) */
+int or_stack_mean_with_rejection_rows(const or_seq *seq, int rejection, int normalize,
+		const double sig[2], const int *shiftx, const int *shifty,
+		const double *offset, const double *mul, const double *scale,
+		int max_thread, int max_number_of_rows, uint16_t *out, uint64_t rej[3][2], uint64_t *row_rej) {
 	const int nb_frames = seq->N;
 	const long W = seq->W, H = seq->H;
 	const int nb_channels = seq->C;
@@ -413,6 +423,11 @@ int or_stack_mean_with_rejection(const or_seq *seq, int rejection, int normalize
 				}
 				trej[t][my_block->channel][0] += crej[0];
 				trej[t][my_block->channel][1] += crej[1];
+				if (row_rej) {
+					uint64_t *rr = row_rej + ((size_t)my_block->channel * H + (H - (my_block->start_row + y) - 1)) * 2;
+					rr[0] = crej[0];
+					rr[1] = crej[1];
+				}
 			}
 		}
 		free(tmp);

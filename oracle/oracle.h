@@ -66,6 +66,10 @@ int or_stack_mean_with_rejection(const or_seq *seq, int rejection, int normalize
 		const double sig[2], const int *shiftx, const int *shifty,
 		const double *offset, const double *mul, const double *scale,
 		int max_thread, int max_number_of_rows, uint16_t *out, uint64_t rej[3][2]);
+int or_stack_mean_with_rejection_rows(const or_seq *seq, int rejection, int normalize,
+		const double sig[2], const int *shiftx, const int *shifty,
+		const double *offset, const double *mul, const double *scale,
+		int max_thread, int max_number_of_rows, uint16_t *out, uint64_t rej[3][2], uint64_t *row_rej);
 int or_stack_median(const or_seq *seq, int normalize, const double *offset,
 		const double *mul, const double *scale, int max_thread,
 		int max_number_of_rows, uint16_t *out);

@@ -12,7 +12,11 @@ requests, the case the guide calibrates.
 """
 import csv
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "siril-0.9_amd", "python"))
+import sg_srcid  # noqa: E402
 
 
 def per_dispatch(path, kernel, counter):
@@ -69,6 +73,9 @@ def main():
             "correction": "FETCH_SIZE x 2 (gfx950, 128-B requests tallied at 64 B), KiB -> B",
         }
         res["traffic_bytes"] = res["read_bytes"] + res["write_bytes"]
+    # the kernel sources these bytes describe (bench.py attaches them only while they match)
+    res["src_files"] = sg_srcid.sources_of(kernel)
+    res["src_id"] = sg_srcid.source_id(kernel)
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))

@@ -136,6 +136,8 @@ extern "C" void sg_shutdown(sg_ctx *ctx) {
 			(void)hipStreamDestroy(d.tail);
 		if (d.tail_ev)
 			(void)hipEventDestroy(d.tail_ev);
+		if (d.tail_done_ev)
+			(void)hipEventDestroy(d.tail_done_ev);
 		for (int k = 0; k < 2; k++)
 			if (d.pinned[k])
 				(void)hipHostFree(d.pinned[k]);
@@ -726,6 +728,7 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		if (!dv.tail) {
 			HIPCHK(hipStreamCreateWithFlags(&dv.tail, hipStreamNonBlocking));
 			HIPCHK(hipEventCreateWithFlags(&dv.tail_ev, hipEventDisableTiming));
+			HIPCHK(hipEventCreateWithFlags(&dv.tail_done_ev, hipEventDisableTiming));
 		}
 		HIPCHK(hipEventRecord(dv.tail_ev, s));
 		HIPCHK(hipStreamWaitEvent(dv.tail, dv.tail_ev, 0));
@@ -764,8 +767,6 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			}
 			p.flag_epoch = (unsigned int)++sb.flag_epoch;
 		}
-		/* flag_map (the band's rows) is cleared right after the main kernel is queued (only the
-		 * kernels after it read it), so the clear is not ahead of the histogram kernel's launch */
 		p.flag_list = (unsigned int *)sb.flag_list.p;
 		p.flag_cap = (unsigned int)npix_launch;
 		p.flag_map = (uint8_t *)sb.flag_map.p;
@@ -861,10 +862,10 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 				const void *kf = km == 8 ? (nw == 4 ? (const void *)k_stack_linfit<8, 4> :
 						nw == 8 ? (const void *)k_stack_linfit<8, 8> : (const void *)k_stack_linfit<8, 16>) :
 					(nw == 4 ? (const void *)k_stack_linfit<16, 4> : (const void *)k_stack_linfit<16, 8>);
-				(void)hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lfx_lds);
+				HIPCHK(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lfx_lds));
 				const dim3 lg((unsigned)((size_t)((W + 63) / 64) * nrows * C));
 				void *lfx_args[] = {&p, &redo_count, &redo_list};
-				(void)hipLaunchKernel(kf, lg, dim3(64 * nw), lfx_args, lfx_lds, s);
+				HIPCHK(hipLaunchKernel(kf, lg, dim3(64 * nw), lfx_args, lfx_lds, s));
 			} else
 			switch ((rj == 4 ? 10 : rj == 1 ? 20 : rj == 8 ? 30 : rj == 3 ? 40 : 0) + norm +
 					100 * (rj == 1 || rj == 8 || rj == 3 ? 1 : ni)) {
@@ -986,7 +987,8 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		/* XCD-aware SGPR-offset loads (k_stack_reduce3) when the shifted row offsets fit 32 bits,
 		 * the per-lane pair kernel (SG_REDUCE1=2, A/B) otherwise */
 		const bool r3 = pairs && hist_addr_ok && ctx->knobs.reduce1 == 0;
-		/* 256-byte segments per wave: SEG = 2 by default (SG_REDUCE_SEG: 1 / 2 / 4, A/B) */
+		/* 256-byte segments per wave: SEG = 1 by default (SG_REDUCE_SEG: 1 / 2 / 4, A/B; 2 and 4
+		 * measured slower, profiles/r05g_reduce_seg_*) */
 		const int seg = ctx->knobs.reduce_seg;
 		const unsigned nb3 = (unsigned)(((W + 512 * seg - 1) / (512 * seg)) * (size_t)nrows * C);
 		HIPCHK(hipEventRecord(cev[0], s));
@@ -1067,6 +1069,22 @@ extern "C" int sg_stack_u16_device_async(sg_ctx *ctx, int dev_index, const sg_st
 	const int rc = stack_device_core(ctx, dev_index, d, d_frames, frame_stride, plane_stride, d_out, row_begin,
 			row_end, nullptr, nullptr, stream, SUM_WHOLE, true);
 	return rc == SG_ERR_WALK ? SG_ERR_GENERIC : rc;
+}
+
+/* `stream` waits (on the device, the host does not block) for every tail kernel queued so far by
+ * SG_STACK_RESULT_AT_COLLECT calls of this device slot: they read d_frames and write d_out after
+ * the call's own stream has moved on, so a caller that refills d_frames or reuses d_out on its
+ * stream before sg_stack_collect orders the refill behind this */
+extern "C" int sg_stack_wait_tail(sg_ctx *ctx, int dev_index, void *stream) {
+	if (!ctx || dev_index < 0 || dev_index >= (int)ctx->dev.size())
+		return SG_ERR_GENERIC;
+	SgDevice &dv = ctx->dev[(size_t)dev_index];
+	if (!dv.tail)
+		return SG_OK;
+	HIPCHK(hipSetDevice(dv.id));
+	HIPCHK(hipEventRecord(dv.tail_done_ev, dv.tail));
+	HIPCHK(hipStreamWaitEvent(stream ? (hipStream_t)stream : dv.stream, dv.tail_done_ev, 0));
+	return SG_OK;
 }
 
 extern "C" int sg_stack_collect(sg_ctx *ctx, int dev_index, uint64_t rej[3][2], uint64_t *maxim) {
@@ -1309,6 +1327,10 @@ static int pull_device(sg_ctx *ctx, int g, PullCall &pc, int B, int E, int nread
 		const int rc = stack_fold(ctx, dv, pend.slot, brej, nullptr, true);
 		const Pending pd = pend;
 		pend.slot = -1;
+		if (!pc.multi) {	/* one device: its folded band is the call's statistics (sg_get_last_stats) */
+			std::lock_guard<std::mutex> lk(ctx->mu);
+			ctx->stats = dv.stats;
+		}
 		if (rc == SG_ERR_WALK && pd.hi < H - 1 && pd.e - pd.b > 1) {
 			extra = std::min(pd.e - pd.b - 1 + extra, extra ? 2 * extra : 4);
 			b = pd.b;

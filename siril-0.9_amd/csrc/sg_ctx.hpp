@@ -57,6 +57,7 @@ struct SgDevice {
 	SgSlot sl[2];
 	hipStream_t tail = nullptr;	/* SG_STACK_RESULT_AT_COLLECT calls: their post-processing */
 	hipEvent_t tail_ev = nullptr;	/* the main kernel of such a call has finished */
+	hipEvent_t tail_done_ev = nullptr;	/* sg_stack_wait_tail: the tail work queued so far has finished */
 	/* registration workspaces (sg_register.hip) */
 	SgBuf reg_sel, reg_spec, reg_work, reg_tw, reg_tw32, reg_best, reg_qbuf, reg_qacc;
 	/* registration: the quality estimate runs on its own stream beside the FFT passes; its

@@ -81,7 +81,7 @@ class SeqInfo(ctypes.Structure):
 
 # every symbol include/sirilgpu.h and include/sirilgpu_io.h declare
 EXPORTS = ["sg_init", "sg_shutdown", "sg_last_error", "sg_stack_u16", "sg_stack_u16_device",
-           "sg_stack_u16_device_async", "sg_stack_collect", "sg_device_count",
+           "sg_stack_u16_device_async", "sg_stack_collect", "sg_stack_wait_tail", "sg_device_count",
            "sg_get_last_stats", "sg_register_dft_u16", "sg_register_dft_u16_device",
            "sg_register_dft_u16_device_raw", "sg_synth_fill_device",
            "sg_seq_open_ser", "sg_seq_open_fits", "sg_seq_close", "sg_seq_get_info", "sg_seq_read_region",
@@ -123,6 +123,8 @@ def load():
     lib.sg_stack_u16_device_async.restype = ctypes.c_int
     lib.sg_stack_collect.argtypes = [P, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     lib.sg_stack_collect.restype = ctypes.c_int
+    lib.sg_stack_wait_tail.argtypes = [P, ctypes.c_int, ctypes.c_void_p]
+    lib.sg_stack_wait_tail.restype = ctypes.c_int
     lib.sg_device_count.argtypes = [P, ctypes.POINTER(ctypes.c_int)]
     lib.sg_device_count.restype = ctypes.c_int
     lib.sg_get_last_stats.argtypes = [P, ctypes.POINTER(StackStats)]
@@ -453,6 +455,11 @@ class Context:
                                                 frame_stride, plane_stride, ctypes.c_void_p(d_out), row_begin,
                                                 row_end, ctypes.c_void_p(stream) if stream else None)
         self.check(rc, "sg_stack_u16_device_async")
+
+    def wait_tail(self, stream=None, dev_index=0):
+        """sg_stack_wait_tail: work queued on `stream` from now on waits for the async calls' tail kernels"""
+        self.check(self.lib.sg_stack_wait_tail(self.ctx, dev_index, ctypes.c_void_p(stream) if stream else None),
+                   "sg_stack_wait_tail")
 
     def collect(self, dev_index=0):
         """sg_stack_collect: (rc, summed rejection counters [3][2], max SUM maximum) of the pending calls"""

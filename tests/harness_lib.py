@@ -35,6 +35,7 @@ def load():
     lib.harness_set_registration_layer.argtypes = [ctypes.c_int]
     lib.harness_set_max_thread.argtypes = [ctypes.c_int]
     lib.harness_set_cancel_after.argtypes = [ctypes.c_int]
+    lib.harness_set_fail_read.argtypes = [ctypes.c_int]
     lib.harness_set_reference_image.argtypes = [P, ctypes.c_int]
     lib.harness_set_included.argtypes = [P, ctypes.c_int, ctypes.c_int]
     lib.harness_gfit_shape.argtypes = [ctypes.POINTER(ctypes.c_int)] * 3

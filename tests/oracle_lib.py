@@ -36,6 +36,8 @@ def load():
     lib.Seq = Seq
     lib.or_stack_mean_with_rejection.argtypes = [ctypes.POINTER(Seq), ctypes.c_int, ctypes.c_int, P, P, P,
                                                  P, P, P, ctypes.c_int, ctypes.c_int, P, P]
+    lib.or_stack_mean_with_rejection_rows.argtypes = [ctypes.POINTER(Seq), ctypes.c_int, ctypes.c_int, P, P, P,
+                                                      P, P, P, ctypes.c_int, ctypes.c_int, P, P, P]
     lib.or_stack_median.argtypes = [ctypes.POINTER(Seq), ctypes.c_int, P, P, P, ctypes.c_int, ctypes.c_int, P]
     lib.or_stack_summing.argtypes = [ctypes.POINTER(Seq), P, P, P, P]
     lib.or_stack_addmax.argtypes = [ctypes.POINTER(Seq), P, P, P]
@@ -79,7 +81,9 @@ def _seq(frames):
 
 
 def stack_rejection(frames, rejection, sig=(4.0, 3.0), shiftx=None, shifty=None, normalize=0,
-                    offset=None, mul=None, scale=None, max_thread=8, max_number_of_rows=0):
+                    offset=None, mul=None, scale=None, max_thread=8, max_number_of_rows=0, row_counters=False):
+    """(rc, image [C][H][W], rejection counters [3][2]); row_counters=True adds each memory row's
+    low / high counts [C][H][2] (a row band's counters are their sum)"""
     lib = load()
     frames = np.ascontiguousarray(frames, dtype=np.uint16)
     N, C, H, W = frames.shape
@@ -91,6 +95,12 @@ def stack_rejection(frames, rejection, sig=(4.0, 3.0), shiftx=None, shifty=None,
     out = np.zeros((C, H, W), dtype=np.uint16)
     rej = np.zeros((3, 2), dtype=np.uint64)
     seq = _seq(frames)
+    if row_counters:
+        rows = np.zeros((C, H, 2), dtype=np.uint64)
+        rc = lib.or_stack_mean_with_rejection_rows(ctypes.byref(seq), rejection, normalize, _p(sg), _p(sx), _p(sy),
+                                                   _p(of), _p(mu), _p(sc), max_thread, max_number_of_rows,
+                                                   _p(out), _p(rej), _p(rows))
+        return rc, out, rej, rows
     rc = lib.or_stack_mean_with_rejection(ctypes.byref(seq), rejection, normalize, _p(sg), _p(sx), _p(sy),
                                           _p(of), _p(mu), _p(sc), max_thread, max_number_of_rows,
                                           _p(out), _p(rej))

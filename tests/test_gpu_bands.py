@@ -346,6 +346,42 @@ def test_async_bands_collect(gpu_ctx, method, rejection, flags):
     assert rc == 0 and not rej2.any()
 
 
+@pytest.mark.parametrize("rejection,sig", [(sg.SIGMA, (0.2, 0.2)), (sg.WINSORIZED, (0.3, 0.3)),
+                                           (sg.SIGMA, (4.0, 3.0))])
+def test_async_tail_frames_refilled(gpu_ctx, rejection, sig):
+    """a band loop that REFILLS its frame buffer between two SG_STACK_RESULT_AT_COLLECT calls on
+    one stream: the first call's tail kernels (redo list, replay, literal early breaks,
+    which strong rejection at N = 16 produces on most pixels) still read the buffer after the
+    stream has moved on, so the refill is queued behind sg_stack_wait_tail; each call's image
+    equals the oracle of ITS frames and the collected counters are their sum"""
+    import torch
+    N, C, H, W = 16, 1, 40, 160
+    fa = orc.synth(N, C, H, W, seed=71, maxshift=4)
+    fb = orc.synth(N, C, H, W, seed=72, maxshift=4)
+    sx, sy = orc.synth_shifts(N, seed=71, maxshift=4)
+    refa, rja = _oracle(fa, sg.MEAN, rejection, sig, sx, sy, 4)
+    refb, rjb = _oracle(fb, sg.MEAN, rejection, sig, sx, sy, 4)
+    buf, src_b = _dev(fa), _dev(fb)
+    outa = torch.zeros(C * H * W, dtype=torch.int16, device="cuda")
+    outb = torch.zeros(C * H * W, dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream().cuda_stream
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, C, rejection=rejection, sig=sig, shiftx=sx, shifty=sy,
+                              max_thread=4, max_number_of_rows=H, flags=sg.RESULT_AT_COLLECT)
+    gpu_ctx.stack_device_async(desc, buf.data_ptr(), C * H * W, H * W, outa.data_ptr(), 0, H, stream=stream)
+    gpu_ctx.wait_tail(stream)
+    buf.copy_(src_b)                # torch's current stream = the calls' stream
+    gpu_ctx.stack_device_async(desc, buf.data_ptr(), C * H * W, H * W, outb.data_ptr(), 0, H, stream=stream)
+    rc, rej, _ = gpu_ctx.collect()
+    assert rc == 0, gpu_ctx.error()
+    st = gpu_ctx.stats()
+    assert_same(outa.cpu().numpy().view(np.uint16).reshape(C, H, W), refa, "first call (frames A)")
+    assert_same(outb.cpu().numpy().view(np.uint16).reshape(C, H, W), refb, "second call (frames B, refilled)")
+    assert np.array_equal(rej, rja + rjb), (rej, rja, rjb)
+    if sig[0] < 1:
+        assert st.chain_pixels + st.slow_pixels > 0, "no tail work: the test would not exercise the ordering"
+
+
 def test_async_fault_reported_by_collect(gpu_ctx):
     """a refused regime met by a queued call (here SIGMEDIAN's never-ending loop) surfaces at
     sg_stack_collect, and the next collect starts clean"""

@@ -312,3 +312,128 @@ def test_cfg4_winsorized_more_oracle_bands(gpu_ctx):
             assert bad.size == 0, f"channel {c} rows {b}..{b + 64}: {len(bad)} pixels differ, first {bad[:3].tolist()}"
     del frames, out, fv
     _free()
+
+
+def _oracle_band_jobs(fv, starts, rows, M, C=None):
+    """host copies of the frame rows each 64-row band reads (band + M-row shift halo)"""
+    jobs = []
+    H = fv.shape[-2]
+    for b in starts:
+        lo, hi = max(0, b - M), min(H, b + rows + M)
+        src = fv[:, lo:hi, :] if C is None else fv[:, C, lo:hi, :]
+        jobs.append((b, lo, src.cpu().numpy().view(np.uint16)[:, None]))
+    return jobs
+
+
+@pytest.mark.parametrize("rejection", ["linearfit", "sigmedian"])
+def test_cfg2_fast_kernels_oracle_bands(gpu_ctx, rejection):
+    """configs[2]'s 512 x 4096^2 frames through the round-5 fast kernels, LINEARFIT (4, 3) on
+    k_stack_linfit (stacking.c:1750-1784) and SIGMEDIAN (4, 3) on k_stack_hist<3> (:1696-1709), at
+    full size.  The whole image is stacked in one call; 64 band calls of 64 rows repeat it (same
+    image) and report each band's redo pixels (decisions inside the recurrence-error bound /
+    rounding band, re-done by the sorted kernel's exact replay).  8 bands go to the oracle, run on
+    host threads while the GPU works: the top and bottom bands (rows shifted out of the frames,
+    zero fill) and the 6 bands with the MOST redo pixels, so the bound's edge is where the oracle
+    looks; each band's image rows and its rejection counters (the oracle's per-row counts) must be
+    equal, and for LINEARFIT the checked bands must hold redo pixels"""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    rj = {"linearfit": sg.LINEARFIT, "sigmedian": sg.SIGMEDIAN}[rejection]
+    frames, sx, sy, (N, H, W, M) = _sigma_cfg2(gpu_ctx)
+    fv = frames.view(N, H, W)
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=rj, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                              max_thread=16, max_number_of_rows=H)
+    out = torch.zeros(H * W, dtype=torch.int16, device="cuda")
+    outb = torch.zeros(H * W, dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
+    rej_all, _ = gpu_ctx.stack_device(desc, frames.data_ptr(), H * W, H * W, out.data_ptr(), 0, H)
+    st = gpu_ctx.stats()
+    assert st.path == 1, "not on the fast kernel"
+    redo_all = int(st.chain_pixels)
+    R = 64
+    band_rej, band_redo = {}, {}
+    for b in range(0, H, R):
+        r, _ = gpu_ctx.stack_device(desc, frames.data_ptr(), H * W, H * W, outb.data_ptr(), b, b + R)
+        band_rej[b] = r.copy()
+        band_redo[b] = int(gpu_ctx.stats().chain_pixels)
+    assert torch.equal(outb, out), "64 band calls differ from the one-call image"
+    assert np.array_equal(sum(band_rej.values()), rej_all)
+    assert sum(band_redo.values()) == redo_all, (sum(band_redo.values()), redo_all)
+    inner = sorted((b for b in band_redo if 0 < b < H - R), key=lambda b: (-band_redo[b], b))
+    starts = [0, H - R] + inner[:6]
+    jobs = _oracle_band_jobs(fv, starts, R, M)
+
+    def oracle_bands():
+        res = []
+        for b, lo, band in jobs:
+            rc, ref, _, rows = orc.stack_rejection(band, rj, sig=(4.0, 3.0), shiftx=sx, shifty=sy, max_thread=16,
+                                                   max_number_of_rows=16 * 24, row_counters=True)
+            res.append((b, rc, ref[0, b - lo:b + R - lo].copy(), rows[0, b - lo:b + R - lo].sum(axis=0)))
+        return res
+
+    pool = ThreadPoolExecutor(1)
+    fut = pool.submit(oracle_bands)
+    img = out.cpu().numpy().view(np.uint16).reshape(H, W)
+    checked_redo = sum(band_redo[b] for b in starts)
+    for b, rc, want, rows in fut.result():
+        assert rc == 0
+        bad = np.argwhere(img[b:b + R] != want)
+        assert bad.size == 0, f"{rejection} rows {b}..{b + R}: {len(bad)} pixels differ, first {bad[:3].tolist()}"
+        assert np.array_equal(band_rej[b][0], rows), (b, band_rej[b][0], rows)
+    pool.shutdown()
+    print(f"{rejection}: redo pixels {redo_all} in the image, {checked_redo} in the 8 oracle bands "
+          f"{[(b, band_redo[b]) for b in starts]}")
+    if rj == sg.LINEARFIT:
+        assert checked_redo > 0, "no redo pixel in the oracle bands: the bound's edge is not exercised"
+    del frames, out, outb, fv
+    _free()
+
+
+@pytest.mark.parametrize("part", [0, 1])
+def test_cfg4_winsorized_oracle_bands_spread(gpu_ctx, part):
+    """configs[4]'s WINSORIZED image at 3 more 64-row bands per channel and part (6 over both
+    parts, spread between the 5 of the two tests above), against the oracle run on a host thread
+    while the GPU stacks: with them 11 bands per channel, 18 % of the image"""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    g = np.load(os.path.join(GOLDEN, "register_cfg4.npz"))
+    N, C, H, W, layer, S, y0, x0, seed, M = (int(v) for v in g["geometry"])
+    sx, sy = g["shiftx"].astype(np.int32), g["shifty"].astype(np.int32)
+    frames = torch.empty(N * C * H * W, dtype=torch.int16, device="cuda")
+    gpu_ctx.synth_fill(frames.data_ptr(), N, C, H, W, 0, H, seed, M)
+    fv = frames.view(N, C, H, W)
+    starts = [H // 8 - 32, 3 * H // 8 - 32, 5 * H // 8 - 32] if part == 0 else \
+        [H // 8 + 96, 5 * H // 8 + 96, 7 * H // 8 + 96]
+    jobs = [(c, j) for c in range(C) for j in _oracle_band_jobs(fv, starts, 64, M, C=c)]
+
+    def oracle_bands():
+        res = []
+        for c, (b, lo, band) in jobs:
+            rc, ref, _, rows = orc.stack_rejection(band, sg.WINSORIZED, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                                                   max_thread=16, max_number_of_rows=16 * 24, row_counters=True)
+            res.append((c, b, rc, ref[0, b - lo:b + 64 - lo].copy(), rows[0, b - lo:b + 64 - lo].sum(axis=0)))
+        return res
+
+    pool = ThreadPoolExecutor(1)
+    fut = pool.submit(oracle_bands)
+    out = torch.zeros(C * H * W, dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, C, rejection=sg.WINSORIZED, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                              max_thread=16, max_number_of_rows=H)
+    gpu_ctx.stack_device(desc, frames.data_ptr(), C * H * W, H * W, out.data_ptr(), 0, H)
+    assert gpu_ctx.stats().path == 1
+    band_rej = {}
+    ob = torch.zeros(C * H * W, dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
+    for b in starts:        # each band's counters from a band call of its own
+        r, _ = gpu_ctx.stack_device(desc, frames.data_ptr(), C * H * W, H * W, ob.data_ptr(), b, b + 64)
+        band_rej[b] = r.copy()
+    img = out.cpu().numpy().view(np.uint16).reshape(C, H, W)
+    for c, b, rc, want, rows in fut.result():
+        assert rc == 0
+        bad = np.argwhere(img[c, b:b + 64] != want)
+        assert bad.size == 0, f"channel {c} rows {b}..{b + 64}: {len(bad)} pixels differ, first {bad[:3].tolist()}"
+        assert np.array_equal(band_rej[b][c], rows), (c, b, band_rej[b][c], rows)
+    pool.shutdown()
+    del frames, out, ob, fv
+    _free()

@@ -145,7 +145,6 @@ def test_register_fits_selection_touching_bottom_fails(tmp_path):
         assert lib.harness_register(seq.h, 0, 0, H - S, S, 1) == 0
 
 
-@pytest.mark.gpu
 def _star_field(N, H, W, seed, maxshift):
     """frames of one star field translated by up to maxshift pixels, plus noise: registrable by
     the DFT on a 64-pixel selection (the plain synthetic noise is not, and its arg-max shifts
@@ -301,6 +300,50 @@ def test_register_cancel_from_c(tmp_path, devs):
         lib.harness_set_run_in_thread(0)
         if devs:
             hl.set_devices(None)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("existing", [False, True])
+@pytest.mark.parametrize("bad", [7, 70, 0])
+def test_register_read_failure(tmp_path, capfd, existing, bad):
+    """one unreadable frame (seq_read_frame_part fails): register_shift_dft returns the failure,
+    the layer's registration array is freed and seq->regparam[layer] is NULL afterwards, whether
+    it was new or the existing one being recomputed (:375-381; the reference frame's failure
+    :238-244 frees it too), no 'Registration finished' is logged; an existing array's reuse is
+    logged as 'Recomputing already existing registration' (:213-216).  bad = 70 fails in the
+    second batch handed to the library, bad = 0 is the reference frame"""
+    lib = hl.load()
+    N, H, W, S = 80, 64, 64, 32
+    frames = orc.synth(N, 1, H, W, seed=19, maxshift=3)
+    p = str(tmp_path / "f.ser")
+    write_ser(p, frames, depth=16)
+    with hl.Sequence.ser(p) as seq:
+        if existing:
+            seq.set_regdata(0, np.arange(N, dtype=np.int32) % 5, -(np.arange(N, dtype=np.int32) % 3))
+        lib.harness_set_fail_read(bad)
+        try:
+            capfd.readouterr()
+            rc = lib.harness_register(seq.h, 0, 16, 16, S, 1)
+            out = capfd.readouterr().out
+        finally:
+            lib.harness_set_fail_read(-1)
+        assert rc == 1
+        assert seq.regdata(0, N) is None            # seq->regparam[0] == NULL
+        assert ("Recomputing already existing registration for this layer" in out) == existing, out
+        assert "Registration finished" not in out
+        if bad == 0:
+            assert "could not load first image to register, aborting" in out, out
+        else:
+            assert f"Could not load partial image {bad}" in out, out
+        # the sequence registers again once the frame reads (a new array, no 'Recomputing')
+        capfd.readouterr()
+        assert lib.harness_register(seq.h, 0, 16, 16, S, 1) == 0
+        out = capfd.readouterr().out
+        assert "Recomputing" not in out and "Registration finished" in out
+        sel = frames[:, 0, H - 16 - S:H - 16, 16:16 + S]
+        rx, ry, _ = orc.register_dft(sel)
+        gx, gy, _ = seq.regdata(0, N)
+        assert np.array_equal(gx, rx) and np.array_equal(gy, ry)
 
 
 @pytest.mark.gpu
