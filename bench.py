@@ -61,6 +61,10 @@ def parse():
     ap.add_argument("--band-of", type=int, default=0,
                     help="A/B at 1 GPU: stack only band 0 of the configs[3] job split into this many row bands "
                          "(one rank's call of the strong form), only that band's rows resident")
+    ap.add_argument("--strong-gather", choices=["overlap", "serial", "none"], default="overlap",
+                    help="strong form (and --band-of): overlap = band calls with their tails on the library's "
+                         "tail stream, output bands gathered on a comm stream from two alternating buffers; "
+                         "serial = tail and gather on the call's stream; none = no gather")
     ap.add_argument("--maxshift", type=int, default=16, help="synthetic registration shift range")
     ap.add_argument("--even-shifts", action="store_true",
                     help="A/B only: round x shifts down to even (4-byte aligned pixel-pair loads)")
@@ -365,27 +369,29 @@ def timed(steps, warmup, step, D, after_warmup=None):
     return D.max_time(time.perf_counter() - t0)
 
 
-def main_sigma(args):
+def sigma_form(args, ctx, D, strong, gather_mode):
+    """set up and time one form of the sigma / median workload on this rank; returns its numbers.
+    strong: one sequence of N frames of H x W in `world` row bands; weak: one sequence of N frames
+    of (H*world) x W, a full H-row band per rank.  Each rank holds only the frame rows its band
+    reads (band + shift halo), addressed through a biased base pointer.  --band-of K at 1 GPU:
+    rank 0's band of the strong form at K ranks, alone.  gather_mode (strong form): "overlap" = the
+    band calls queued with SG_STACK_RESULT_AT_COLLECT and their output bands gathered to rank 0 on
+    a comm stream from two alternating buffers (sirilgpu_dist.BandGatherPipeline), "serial" = the
+    call's tail and the gather on the call's stream, "none" = no gather (at 1 GPU with --band-of the
+    gather is a same-size device copy standing in for it)"""
     import numpy as np
     import torch
     import sirilgpu as sg
     import sirilgpu_dist as sd
-    D = Dist()
     world, rank = D.world, D.rank
-    dev = torch.cuda.current_device()
     N, W, H = args.frames, args.width, args.height
     rej_mode = {"sigma": sg.SIGMA, "winsorized": sg.WINSORIZED, "none": sg.NO_REJEC,
                 "percentile": sg.PERCENTILE, "sigmedian": sg.SIGMEDIAN, "linearfit": sg.LINEARFIT}[args.rejection]
     median = args.workload == "median"
     method = sg.MEDIAN if median else sg.MEAN
     sig = (0.2, 0.1) if rej_mode == sg.PERCENTILE else (4.0, 3.0)
-    ctx = sg.Context([dev])
-    strong = args.scaling == "strong" or world == 1
-    # strong: one sequence of N frames of H x W in `world` row bands; weak: one sequence of
-    # N frames of (H*world) x W, a full H-row band per rank.  Each rank holds only the frame
-    # rows its band reads (band + shift halo), addressed through a biased base pointer.
-    # --band-of K at 1 GPU: rank 0's band of the strong form at K ranks, alone
     nb = world if world > 1 else max(1, args.band_of)
+    strong = strong or world == 1
     Htot = H if strong else H * world
     shx, shy = synth_shifts_np(N, 0x5151, args.maxshift)
     if args.even_shifts:
@@ -403,11 +409,7 @@ def main_sigma(args):
     base = frames.data_ptr() - lo * W * 2
     ctx.synth_fill(base, N, 1, Htot, W, lo, hi + 1, 0x5151, args.maxshift, frame_stride=fstride)
     hband = -(-H // nb) if strong else H
-    band_out = torch.zeros(hband * W, dtype=torch.int16, device="cuda")
-    out_base = band_out.data_ptr() - b * W * 2          # the library writes rows [b, e) of the image
-    gathered = None
-    if strong and world > 1 and rank == 0:
-        gathered = [torch.empty(hband * W, dtype=torch.int16, device="cuda") for _ in range(world)]
+    gathering = strong and nb > 1 and gather_mode != "none"
     norm_mode, off, mul, scale = sg.NO_NORM, None, None, None
     if args.normalize != "none":
         # synthetic per-frame location / scale (the cached IKSS statistics), coefficients as
@@ -422,25 +424,43 @@ def main_sigma(args):
         else:
             norm_mode = sg.MULTIPLICATIVE_SCALING
             mul = loc[0] / loc
+    flags = 0 if gathering and gather_mode == "serial" else sg.RESULT_AT_COLLECT
     desc, keep = sg.make_desc(method, N, W, Htot, 1, rejection=rej_mode if not median else sg.NO_REJEC, sig=sig,
                               shiftx=shx, shifty=shy, normalize=norm_mode, offset=off, mul=mul, scale=scale,
-                              max_thread=8, max_number_of_rows=Htot, resident_rows=(lo, hi + 1),
-                              flags=0 if strong and world > 1 else sg.RESULT_AT_COLLECT)
-    torch.cuda.synchronize()
+                              max_thread=8, max_number_of_rows=Htot, resident_rows=(lo, hi + 1), flags=flags)
     kms = []
-    stream = torch.cuda.current_stream().cuda_stream
+    stream_obj = torch.cuda.current_stream()
+    stream = stream_obj.cuda_stream
+    mk = lambda: torch.zeros(hband * W, dtype=torch.int16, device="cuda")
+
+    if world > 1:
+        gather_fn = lambda band, lst: D.gather_to_root(band, lst)
+    else:       # --band-of K at 1 GPU: a device copy of the band standing in for the RCCL gather
+        gather_fn = lambda band, lst: lst[0].copy_(band)
+    if gathering and gather_mode == "overlap":
+        comm = torch.cuda.Stream()
+        pipe = sd.BandGatherPipeline(mk, rank, world, gather_fn,
+                                     ops=sd.TorchStreamOps(stream_obj, comm, lambda h: ctx.wait_tail(h)))
+    else:
+        band_out = mk()
+        gathered = ([mk() for _ in range(world)] if rank == 0 else None) if world > 1 else [mk()]
+    torch.cuda.synchronize()
 
     # one step = one whole stack of the band, queued with sg_stack_u16_device_async on torch's
     # stream (every launch decided on the device, the counters read back into a pinned slot):
-    # the host prepares the next step while the device runs this one.  The strong form gathers the
-    # output bands to rank 0 behind it on the same stream (RCCL over xGMI); otherwise the output is
-    # read after the timed region, so each step's work after its main kernel (redo list, replay,
-    # counters) runs on the library's tail stream beside the next step (SG_STACK_RESULT_AT_COLLECT)
+    # the host prepares the next step while the device runs this one.  Without a gather the
+    # output is read after the timed region, so each step's work after its main kernel (redo list,
+    # replay, counters) runs on the library's tail stream beside the next step
+    # (SG_STACK_RESULT_AT_COLLECT)
     def step():
-        ctx.stack_device_async(desc, base, fstride, nres * W, out_base, b, e, stream=stream)
+        if gathering and gather_mode == "overlap":
+            pipe.step(lambda buf: ctx.stack_device_async(desc, base, fstride, nres * W, buf.data_ptr() - b * W * 2,
+                                                         b, e, stream=stream))
+        else:
+            ctx.stack_device_async(desc, base, fstride, nres * W, band_out.data_ptr() - b * W * 2, b, e, stream=stream)
+            if gathering:
+                gather_fn(band_out, gathered)
         kms.append(ctx.stats().kernel_ms)       # the last folded call's (at most two calls behind)
-        if strong and world > 1:
-            D.gather_to_root(band_out, gathered)
 
     def reset_counters():
         rc, _, _ = ctx.collect()
@@ -458,16 +478,42 @@ def main_sigma(args):
     rej_tot = rej_steps // args.steps           # one step's (every step stacks the same band)
     if world > 1:
         rej_tot = sd.sum_counters(rej_tot, D.dist, device=D.cdev)   # rejection counters, :1796-1817
+    del frames
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return {"elapsed": elapsed, "kavg": kavg, "per_rank_kms": per_rank_kms, "rej_tot": rej_tot, "st": st,
+            "b": b, "e": e, "N": N, "H": H, "W": W, "Htot": Htot, "hband": hband, "nb": nb, "strong": strong,
+            "median": median, "sig": sig, "gather": gather_mode if gathering else "none"}
+
+
+def main_sigma(args):
+    import numpy as np
+    import torch
+    import sirilgpu as sg
+    D = Dist()
+    world, rank = D.world, D.rank
+    dev = torch.cuda.current_device()
+    ctx = sg.Context([dev])
+    strong = args.scaling == "strong" or world == 1
+    gmode = args.strong_gather if (world > 1 or args.band_of > 1) else "none"
+    f = sigma_form(args, ctx, D, strong, gmode)
+    # at N > 1 in the (default) weak form, configs[3]'s strong form is timed after it and reported
+    # beside it: the one 512-frame 4096-row sequence in N row bands, gathered to rank 0
+    f_strong = sigma_form(args, ctx, D, True, args.strong_gather) if world > 1 and not strong else None
+    N, H, W, b, e = f["N"], f["H"], f["W"], f["b"], f["e"]
+    elapsed, kavg, st, median = f["elapsed"], f["kavg"], f["st"], f["median"]
     ms_step = elapsed / args.steps * 1e3
     frames_per_s = N * (1 if strong else world) / (elapsed / args.steps)
     algo_bytes = N * (e - b) * W * 2 + (e - b) * W * 2     # this rank's launch: its band's samples + output
     achieved = algo_bytes / (kavg * 1e-3) / 1e9
     if rank == 0:
+        nb, hband, Htot, sig = f["nb"], f["hband"], f["Htot"], f["sig"]
         kind = "median stack" if median else f"{args.rejection} rejection stack"
         if world == 1 and nb > 1:
             workload = (f"A/B: band 0 ({e - b} rows) of the {kind} {N}x{H}x{W} u16 mono split into {nb} row bands "
                         f"(one rank's call of BASELINE configs[3] at {nb} GPUs), only its rows resident; "
-                        f"value = frames/s of this band's work")
+                        f"value = frames/s of this band's work; gather stand-in: {f['gather']} "
+                        f"(a {hband * W * 2}-byte device copy per step)")
             par = f"1 GPU, one of {nb} row bands"
         elif world == 1:
             workload = (f"{kind} {N}x{H}x{W} u16 mono (BASELINE configs[2] frames)" if median or args.rejection != "sigma"
@@ -475,8 +521,8 @@ def main_sigma(args):
             par = "1 GPU"
         elif strong:
             workload = (f"{kind} {N}x{H}x{W} u16 mono in {world} row bands of {hband} rows, output "
-                        f"gathered to rank 0 (BASELINE configs[3])")
-            par = f"row-band x{world}, RCCL gather"
+                        f"gathered to rank 0 (BASELINE configs[3], gather {f['gather']})")
+            par = f"row-band x{world}, RCCL gather ({f['gather']})"
         else:
             workload = f"{kind} {N}x{H}x{W} u16 mono per GPU, one {N}x{Htot}x{W} sequence in {world} bands"
             par = f"row-band x{world} (weak)"
@@ -489,7 +535,7 @@ def main_sigma(args):
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
-            "scaling": args.scaling,          # at N = 1 both forms are the same workload
+            "scaling": "strong" if strong and world > 1 else args.scaling,   # at N = 1 both forms are one workload
             "vs_baseline": None,
             "dtype": "u16",
             "data": "synthetic (include/sg_synth.h, generated in HBM)",
@@ -503,11 +549,20 @@ def main_sigma(args):
             "slow_pixels": int(st.slow_pixels),
             "redo_pixels": int(st.chain_pixels),
             "compact_pixels": int(st.compact_pixels),
-            "rejected": [int(x) for x in np.asarray(rej_tot).reshape(-1)[:2]],
+            "rejected": [int(x) for x in np.asarray(f["rej_tot"]).reshape(-1)[:2]],
         }
         if world > 1:
-            res["per_rank_kernel_ms"] = [round(x, 3) for x in per_rank_kms]
+            res["per_rank_kernel_ms"] = [round(x, 3) for x in f["per_rank_kms"]]
             res["rows_per_rank"] = e - b
+        if f_strong is not None:
+            fs = f_strong
+            res["configs3_strong"] = {
+                "workload": f"{kind} {N}x{H}x{W} u16 mono (BASELINE configs[3]) in {world} row bands of "
+                            f"{fs['hband']} rows, output bands gathered to rank 0 over RCCL ({fs['gather']})",
+                "value": round(N / (fs["elapsed"] / args.steps), 2), "unit": "frames/s",
+                "ms_per_step": round(fs["elapsed"] / args.steps * 1e3, 3), "scaling": "strong",
+                "per_rank_kernel_ms": [round(x, 3) for x in fs["per_rank_kms"]],
+                "rejected": [int(x) for x in np.asarray(fs["rej_tot"]).reshape(-1)[:2]]}
         if not args.no_cpu_baseline and world == 1 and nb == 1:
             res["cpu_baseline"] = cpu_baseline(args, N, W, median)
         print(json.dumps(res), flush=True)

@@ -134,3 +134,86 @@ def register_sharded(register_part, nframes, ref_image, included, dist, rank, wo
     gq[ref] = outs[0].cpu().numpy()[2, ref]         # every rank measured the reference
     gx[ref] = gy[ref] = 0
     return gx, gy, normalize_quality(gq, nframes, ref, included)
+
+
+class BandGatherPipeline:
+    """Output bands of successive stack calls gathered to rank 0 without serialising the calls
+    behind the gathers (configs[3]'s strong form): two band buffers, so the band
+    call of step k + 1 writes one buffer while the gather of step k still reads the other.
+
+    Per step k (slot = k mod 2):
+      1. ops.wait_free(slot):  the compute stream waits until the gather of step k - 2 has read
+                               buffer `slot` (nothing to wait for the first time);
+      2. stack_into(buf):      the caller queues its band call writing buf (async, its redo / replay
+                               tail allowed to run on the library's tail stream);
+      3. ops.to_comm():        the comm stream waits for this band's result (main kernel and tail:
+                               sg_stack_wait_tail), not for anything queued later;
+      4. gather_fn on comm:    rank 0 receives every rank's band into gathered[slot];
+      5. ops.release(slot):    buffer `slot` may be written again once the gather is done.
+    The reference's team likewise reads, stacks and writes block after block with no global
+    barrier between them (stacking.c:1513-1591).  `ops` supplies the stream / event plumbing
+    (TorchStreamOps on a GPU; the default no-op ops for synchronous CPU collectives, gloo)."""
+
+    class NoOps:
+        def __init__(self):
+            self.log = []
+
+        def wait_free(self, slot):
+            self.log.append(("wait_free", slot))
+
+        def to_comm(self):
+            self.log.append(("to_comm",))
+
+        def on_comm(self):
+            import contextlib
+            return contextlib.nullcontext()
+
+        def release(self, slot):
+            self.log.append(("release", slot))
+
+    def __init__(self, make_buf, rank, world, gather_fn, ops=None, nslots=2):
+        self.bufs = [make_buf() for _ in range(nslots)]
+        self.gathered = [[make_buf() for _ in range(world)] if rank == 0 else None for _ in range(nslots)]
+        self.gather_fn = gather_fn
+        self.ops = ops if ops is not None else BandGatherPipeline.NoOps()
+        self.nslots = nslots
+        self.k = 0
+
+    def step(self, stack_into):
+        slot = self.k % self.nslots
+        self.k += 1
+        self.ops.wait_free(slot)
+        stack_into(self.bufs[slot])
+        self.ops.to_comm()
+        with self.ops.on_comm():
+            self.gather_fn(self.bufs[slot], self.gathered[slot])
+            self.ops.release(slot)
+        return slot
+
+
+class TorchStreamOps:
+    """BandGatherPipeline plumbing on one GPU: `stream` is the stream the band calls are queued
+    on, `comm` a second stream the gathers run on; `wait_tail(stream_handle)` is the library's
+    sg_stack_wait_tail (a device-side wait for the async calls' tail kernels)."""
+
+    def __init__(self, stream, comm, wait_tail, nslots=2):
+        import torch
+        self.stream, self.comm, self.wait_tail = stream, comm, wait_tail
+        self.ev = [torch.cuda.Event() for _ in range(nslots)]
+        self.used = [False] * nslots
+
+    def wait_free(self, slot):
+        if self.used[slot]:
+            self.stream.wait_event(self.ev[slot])
+
+    def to_comm(self):
+        self.comm.wait_stream(self.stream)          # the band's main kernel
+        self.wait_tail(self.comm.cuda_stream)       # and its tail (redo list, replay, literal)
+
+    def on_comm(self):
+        import torch
+        return torch.cuda.stream(self.comm)
+
+    def release(self, slot):
+        self.ev[slot].record(self.comm)
+        self.used[slot] = True

@@ -127,3 +127,67 @@ def test_register_sharding_gloo(world, ref, excl, tmp_path):
         assert np.array_equal(d["sx"][keep], rx[keep]) and np.array_equal(d["sy"][keep], ry[keep]), r
         q, rq_k = d["q"][keep], rq[keep]
         assert np.array_equal(np.isnan(q), np.isnan(rq_k)) and np.array_equal(q[~np.isnan(q)], rq_k[~np.isnan(rq_k)])
+
+
+def _pipeline_worker(rank, world, port, q):
+    """BandGatherPipeline over gloo: each step's band (rank- and step-dependent) reaches rank 0
+    in the step's gathered slot; the ops log shows every buffer released (its gather done)
+    before the step two later waits to write it again"""
+    import os
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sirilgpu_dist as sd
+    try:
+        H, W = 10, 6
+        hb = -(-H // world)
+
+        def gather(band, lst):
+            dist.gather(band, gather_list=lst, dst=0)
+
+        pipe = sd.BandGatherPipeline(lambda: torch.zeros(hb * W, dtype=torch.int32), rank, world, gather)
+        seen = []
+        for k in range(5):
+            slot = pipe.step(lambda buf: buf.fill_(1000 * k + rank))
+            if rank == 0:
+                seen.append((k, slot, [int(t[0]) for t in pipe.gathered[slot]]))
+        q.put((rank, seen, pipe.ops.log))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_band_gather_pipeline_gloo():
+    import multiprocessing as mp
+    import socket
+    world = 3
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_pipeline_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, seen, log = q.get(timeout=120)
+        res[r] = (seen, log)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    seen, log = res[0]
+    assert [s[1] for s in seen] == [0, 1, 0, 1, 0]
+    for k, slot, vals in seen:
+        assert vals == [1000 * k + r for r in range(world)], (k, vals)
+    # order per step: wait_free(slot), to_comm, release(slot); a slot is written again only after
+    # its previous gather released it
+    steps = [log[i:i + 3] for i in range(0, len(log), 3)]
+    assert all(s[0][0] == "wait_free" and s[1] == ("to_comm",) and s[2][0] == "release" for s in steps)
+    released = set()
+    for k, s in enumerate(steps):
+        slot = s[0][1]
+        if k >= 2:
+            assert slot in released
+        released.add(s[2][1])

@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 #define NF 512
 #define W 4096
@@ -113,6 +114,136 @@ __global__ void __launch_bounds__(1024) k_probe(const char *__restrict__ base, c
 		out[0] = acc + lds[0];
 }
 
+/* mode 6 (round 6): the same 256-B shifted row segments staged by LDS-DMA
+ * (buffer_load_dword ... lds: per-lane source address, the wave's 64 dwords land lane-linear in
+ * LDS) into a per-wave ring of NSLOT slots of 8 frames; the consumer reads each frame's dword back
+ * with ds_read_b32 (what the binning would read instead of the load's VGPR).  The wait before a
+ * slot's reads is a counted vmcnt leaving the younger slots' DMAs in flight.  LDSX = LDS bytes per
+ * workgroup besides the ring (the histogram's 34.5 KB, or less to probe occupancy). */
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int NSLOT>
+__global__ void __launch_bounds__(256) k_probe_lds(const char *__restrict__ base, const int *__restrict__ c1,
+		unsigned *__restrict__ out, int ntiles_total, int check_tile) {
+	extern __shared__ unsigned lds[];
+	constexpr int M = 8, TW = 256;
+	const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const int nw = 4;
+	const int ntx = (W * 2) / TW;
+	const int xcd = (int)blockIdx.x & 7;
+	const int per_xcd = ntiles_total / 8;
+	const int t = xcd * per_xcd + ((int)blockIdx.x >> 3);
+	const int xt = t % ntx, R = t / ntx;
+	unsigned *ring = lds + wave * (NSLOT * M * 64);	/* this wave's slots: [slot][frame][lane] dwords */
+	const int nblk = NF / M / nw;			/* blocks of 8 frames per wave */
+	unsigned acc = 0;
+	auto issue = [&](int k) {
+		const int s = k % NSLOT;
+#pragma unroll
+		for (int m = 0; m < M; m++) {
+			const int f = (wave + k * nw) * M + m;
+			auto rs = __builtin_amdgcn_make_buffer_rsrc((void *)(base + (size_t)f * FRAMEB), (short)0, (int)FRAMEB,
+					0x00020000);
+			const int so = R * W * 2 + xt * TW + c1[f];
+			__builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void *)(ring + (s * M + m) * 64), 4, lane * 4, so, 0, 0);
+		}
+	};
+#pragma unroll
+	for (int k = 0; k < NSLOT - 1; k++)
+		issue(k);
+	for (int k = 0; k < nblk; k++) {
+		if (k + NSLOT - 1 < nblk)
+			issue(k + NSLOT - 1);
+		/* slot k's 8 DMAs retired: the (NSLOT - 1) younger slots' 8 DMAs each may stay in flight */
+		const unsigned sl = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned *)(ring + (k % NSLOT) * M * 64 + lane);
+		unsigned v[M];
+		if (k + NSLOT - 1 < nblk) {
+			if (NSLOT == 2)
+				asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+			else if (NSLOT == 3)
+				asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+			else
+				asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+		} else {
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		}
+#pragma unroll
+		for (int m = 0; m < M; m++)
+			asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v[m]) : "v"(sl), "i"(m * 256) : "memory");
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+		for (int m = 0; m < M; m++)
+			acc ^= v[m];
+		if (t == check_tile && k == 0) {	/* correctness: frames 0..7 of wave 0's first block */
+#pragma unroll
+			for (int m = 0; m < M; m++)
+				out[64 + ((wave * M + m) * 64 + lane)] = v[m];
+		}
+		/* the slot is rewritten NSLOT - 1 blocks later: the reads above have completed (lgkmcnt 0) */
+	}
+	if (acc == 0x12345678u)
+		out[0] = acc;
+}
+
+template <int NSLOT>
+static void run_lds(const char *d, const int *c1, unsigned *o, size_t lds_extra, const char *what) {
+	hipEvent_t a, b;
+	(void)hipEventCreate(&a);
+	(void)hipEventCreate(&b);
+	const int ntiles = H * (W * 2 / 256);
+	const size_t lds = (size_t)4 * NSLOT * 8 * 256 + lds_extra;
+	auto kf = k_probe_lds<NSLOT>;
+	(void)hipFuncSetAttribute((const void *)kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+	hipLaunchKernelGGL(kf, dim3(ntiles), dim3(256), lds, 0, d, c1, o, ntiles, 12345);
+	(void)hipDeviceSynchronize();
+	(void)hipEventRecord(a);
+	for (int i = 0; i < 5; i++)
+		hipLaunchKernelGGL(kf, dim3(ntiles), dim3(256), lds, 0, d, c1, o, ntiles, -1);
+	(void)hipEventRecord(b);
+	(void)hipEventSynchronize(b);
+	float ms;
+	(void)hipEventElapsedTime(&ms, a, b);
+	ms /= 5;
+	int per_cu = 0;
+	(void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)kf, 256, lds);
+	printf("LDS-DMA NSLOT=%d lds=%6zu (%s) wg/cu=%d: %7.3f ms %7.1f GB/s (%s)\n", NSLOT, lds, what, per_cu, ms,
+			(double)NF * FRAMEB / ms / 1e6, hipGetErrorString(hipGetLastError()));
+	fflush(stdout);
+}
+
+/* the LDS-DMA data of the check tile (12345, frames 0..31 of its waves' first blocks) against the
+ * bytes the frames hold at the shifted (2-byte aligned) addresses */
+static int check_lds(const char *d, const int *h_c1, unsigned *o) {
+	const int ntx = (W * 2) / 256, per_xcd = H * ntx / 8;
+	/* invert the XCD-major deal: blockIdx b -> tile xcd * per_xcd + (b >> 3) */
+	const int t = 12345, xt = t % ntx, R = t / ntx;
+	static unsigned got[4 * 8 * 64];
+	(void)hipMemcpy(got, o + 64, sizeof got, hipMemcpyDeviceToHost);
+	(void)per_xcd;
+	int bad = 0, odd = 0;
+	for (int wave = 0; wave < 4; wave++)
+		for (int m = 0; m < 8; m++) {
+			const int f = wave * 8 + m;
+			const long so = (long)R * W * 2 + xt * 256 + h_c1[f];
+			odd += (so & 3) != 0;
+			unsigned char bytes[260];
+			const long lo = so < 0 ? 0 : so;
+			(void)hipMemcpy(bytes, d + (size_t)f * FRAMEB + lo, 260, hipMemcpyDeviceToHost);
+			for (int lane = 0; lane < 64; lane++) {
+				const long a = so + lane * 4;
+				unsigned want = 0;
+				if (a >= 0 && a + 4 <= (long)FRAMEB)
+					memcpy(&want, bytes + (a - lo), 4);
+				if (got[(wave * 8 + m) * 64 + lane] != want && bad++ < 5)
+					printf("  mismatch frame %d lane %d (src offset %ld): got %08x want %08x\n", f, lane, a,
+							got[(wave * 8 + m) * 64 + lane], want);
+			}
+		}
+	printf("LDS-DMA data check: %d of %d dwords differ (%d of 32 frames at a 2-byte-misaligned source)\n", bad,
+			4 * 8 * 64, odd);
+	return bad;
+}
+
 __global__ void k_fill(unsigned *p, size_t n) {
 	for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
 		p[i] = (unsigned)(i * 2654435761u);
@@ -168,6 +299,22 @@ int main(int argc, char **argv) {
 	hipLaunchKernelGGL(k_fill, dim3(8192), dim3(256), 0, 0, (unsigned *)d, (size_t)NF * FRAMEB / 4);
 	(void)hipDeviceSynchronize();
 	const int mode = argc > 2 ? atoi(argv[2]) : 0;
+	if (mode == 6) {
+		run_lds<2>(d, c1, o, 0, "ring only");
+		if (check_lds(d, h, o))
+			return 1;
+		for (int rep = 0; rep < 2; rep++) {
+			run<256, 4, 2, false>(d, c1, o, 4, 4, 34560);	/* today's register-staged geometry */
+			run<256, 4, 2, false, 8>(d, c1, o, 4, 4, 34560);
+			run_lds<2>(d, c1, o, 0, "ring only");
+			run_lds<2>(d, c1, o, 24000, "ring + 24 KB");
+			run_lds<2>(d, c1, o, 34560, "ring + histogram");
+			run_lds<3>(d, c1, o, 0, "ring only");
+			run_lds<3>(d, c1, o, 14000, "ring + 14 KB");
+			run_lds<4>(d, c1, o, 0, "ring only");
+		}
+		return 0;
+	}
 	if (mode == 5) {	/* round 5: 512-B segments at 3 or 4 workgroups per CU */
 		for (int rep = 0; rep < 2; rep++) {
 			run<256, 4, 2, false>(d, c1, o, 4, 4, 34560);		/* today's geometry */
