@@ -429,7 +429,11 @@ def sigma_form(args, ctx, D, strong, gather_mode):
                               shiftx=shx, shifty=shy, normalize=norm_mode, offset=off, mul=mul, scale=scale,
                               max_thread=8, max_number_of_rows=Htot, resident_rows=(lo, hi + 1), flags=flags)
     kms = []
-    stream_obj = torch.cuda.current_stream()
+    # the band calls, the serial gather and the pipeline's waits on one explicit stream (handle 0,
+    # torch's default stream, would mean the library's own stream to sg_stack_u16_device_async)
+    stream_obj = torch.cuda.Stream()
+    prev_stream = torch.cuda.current_stream()
+    torch.cuda.set_stream(stream_obj)
     stream = stream_obj.cuda_stream
     mk = lambda: torch.zeros(hband * W, dtype=torch.int16, device="cuda")
 
@@ -480,6 +484,7 @@ def sigma_form(args, ctx, D, strong, gather_mode):
         rej_tot = sd.sum_counters(rej_tot, D.dist, device=D.cdev)   # rejection counters, :1796-1817
     del frames
     torch.cuda.synchronize()
+    torch.cuda.set_stream(prev_stream)
     torch.cuda.empty_cache()
     return {"elapsed": elapsed, "kavg": kavg, "per_rank_kms": per_rank_kms, "rej_tot": rej_tot, "st": st,
             "b": b, "e": e, "N": N, "H": H, "W": W, "Htot": Htot, "hband": hband, "nb": nb, "strong": strong,

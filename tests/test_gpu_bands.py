@@ -365,13 +365,16 @@ def test_async_tail_frames_refilled(gpu_ctx, rejection, sig):
     outa = torch.zeros(C * H * W, dtype=torch.int16, device="cuda")
     outb = torch.zeros(C * H * W, dtype=torch.int16, device="cuda")
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream().cuda_stream
+    # an explicit stream: handle 0 (torch's default stream) would mean the library's own stream
+    s = torch.cuda.Stream()
+    stream = s.cuda_stream
     desc, keep = sg.make_desc(sg.MEAN, N, W, H, C, rejection=rejection, sig=sig, shiftx=sx, shifty=sy,
                               max_thread=4, max_number_of_rows=H, flags=sg.RESULT_AT_COLLECT)
-    gpu_ctx.stack_device_async(desc, buf.data_ptr(), C * H * W, H * W, outa.data_ptr(), 0, H, stream=stream)
-    gpu_ctx.wait_tail(stream)
-    buf.copy_(src_b)                # torch's current stream = the calls' stream
-    gpu_ctx.stack_device_async(desc, buf.data_ptr(), C * H * W, H * W, outb.data_ptr(), 0, H, stream=stream)
+    with torch.cuda.stream(s):
+        gpu_ctx.stack_device_async(desc, buf.data_ptr(), C * H * W, H * W, outa.data_ptr(), 0, H, stream=stream)
+        gpu_ctx.wait_tail(stream)
+        buf.copy_(src_b)            # queued on s, behind the first call's tail kernels
+        gpu_ctx.stack_device_async(desc, buf.data_ptr(), C * H * W, H * W, outb.data_ptr(), 0, H, stream=stream)
     rc, rej, _ = gpu_ctx.collect()
     assert rc == 0, gpu_ctx.error()
     st = gpu_ctx.stats()
