@@ -731,6 +731,13 @@ def main_config(args):
               "frac": round(reg_ach / HBM_PEAK_GBS, 4), "algorithmic_bytes": int(reg_algo),
               "algorithmic_model": "22 S^2 per frame (DESIGN.md: 20 S^2 FFT passes + 2 S^2 quality)",
               "traffic": None}
+        # SURVEY 8(d)'s algorithmic MINIMUM: each u16 selection read once (2 S^2 per frame); the
+        # passes' planes cannot stay on chip at S = 2048 (32 MiB per c64 plane), so this is a floor
+        # no pass structure reaches, reported beside the pass model
+        reg_min = nsel * S * S * 2
+        rr["min_model"] = {"algorithmic_bytes": int(reg_min), "model": "2 S^2 per frame (SURVEY 8(d) minimum)",
+                           "achieved": round(reg_min / (reg_ms * 1e-3) / 1e9, 1),
+                           "frac": round(reg_min / (reg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
         if reg_traffic is not None:
             # PMC FETCH/WRITE bytes of the registration kernels per step (scripts/pmc_traffic.py)
             tb = reg_traffic["traffic_bytes_per_step"]
