@@ -42,7 +42,7 @@ for step in "$@"; do
     test|testall)
       k=(); [ -n "$spec" ] && k=(-k "${spec//,/ }")   # commas between the words of a -k expression
       x=-x; [ "$kind" = testall ] && x=--maxfail=8
-      lim=900; [ -n "$spec" ] && lim=300     # a selection runs under a shorter limit
+      lim=900; [ -n "$spec" ] && lim=600     # a selection runs under a shorter limit
       timeout -k 10 $lim python -u -m pytest tests -m gpu $x -v --durations=15 --timeout 200 --timeout-method thread "${k[@]}" \
         > "$O/pytest_gpu.log" 2>&1; rc=$?
       # testall goes on after plain test failures (pytest exit 1), never after a crash or a timeout
