@@ -282,7 +282,7 @@ int main(int argc, char **argv) {
 		printf("alloc failed\n");
 		return 1;
 	}
-	(void)hipMalloc(&o, 64);
+	(void)hipMalloc(&o, 65536);	/* out[0] + the LDS-DMA check block (out[64 .. 64 + 2048)) */
 	(void)hipMalloc(&c1, NF * sizeof(int));
 	int h[NF];
 	const int zero = argc > 1 && atoi(argv[1]) == 0;
