@@ -625,7 +625,6 @@ def main_config(args):
     if mine:
         ctx.synth_fill(sbase + Cs * S * W * 2, len(mine), Cs, H, W, y0, y0 + S, seed, M, frame_stride=Cs * S * W,
                        plane_stride=S * W, first_frame=mine[0])
-    selv = selsrc.view(nsel, Cs, S, W)
     # stack shard: row band of every frame (band + shift halo), all channels
     b, e = sd.row_band(rank, world, H)
     lo, hi = max(0, b - int(ey.max())), min(H - 1, e - 1 - int(ey.min()))
@@ -648,12 +647,16 @@ def main_config(args):
     reg_spans = []
     out = {}
 
+    # seq_read_frame_part of layer `layer`: the S x S windows read in place by the registration's
+    # first pass (sg_register_dft_u16_device_pitched; round 5 extracted them with a 2 x 2 GB copy
+    # first, the "selection" stage, 1.47 ms of configs[4]'s step)
+    sel_base = selsrc.data_ptr() + 2 * (layer * S * W + x0)
+
     def step():
         t0 = time.perf_counter()
-        sel = selv[:, layer, :, x0:x0 + S].contiguous()     # seq_read_frame_part of layer `layer`
-        torch.cuda.synchronize()
         t1 = time.perf_counter()
-        lx, ly, lq = ctx.register_dft_device(sel.data_ptr(), nsel, S, raw_quality=world > 1)
+        lx, ly, lq = ctx.register_dft_device(sel_base, nsel, S, raw_quality=world > 1, frame_pitch=Cs * S * W,
+                                             row_pitch=W)
         reg_spans.append(ctx.stats().reg_ms)
         if world > 1:
             rows = np.zeros((3, N))

@@ -251,6 +251,18 @@ int sg_register_dft_u16_device_raw(sg_ctx *ctx, int dev_index, const uint16_t *d
 		double *quality_raw, void *stream);
 
 /*
+ * The same on selections read IN PLACE from resident frames (no extraction copy): selection f,
+ * bottom-up row r, column x at d_sel[f * frame_pitch + r * row_pitch + x] (elements; row_pitch >=
+ * S), e.g. a window of layer `layer` of [C][H][W] frames: d_sel = frames + layer H W + y0 W + x0,
+ * frame_pitch = C H W, row_pitch = W.  What seq_read_frame_part (src/io/sequence.c:567-609)
+ * extracts per frame is thus read by the first pass itself.  raw_quality != 0: the quality is
+ * left raw as in sg_register_dft_u16_device_raw.
+ */
+int sg_register_dft_u16_device_pitched(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int64_t frame_pitch,
+		int64_t row_pitch, int nframes, int S, int ref_image, const int *included, int *shiftx, int *shifty,
+		double *quality, int raw_quality, void *stream);
+
+/*
  * Perspective warp: replaces cvTransformImage (src/opencv/opencv.cpp:242-309) as the
  * star-alignment registration uses it (src/registration/registration.c:719-723, flip /
  * warp / flip): memory-order (bottom-up) planes in, memory-order planes out of size

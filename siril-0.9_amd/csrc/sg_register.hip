@@ -91,21 +91,30 @@ __device__ __forceinline__ sg_c64 sg_xpower_at(sg_c64 zk, sg_c64 zm, sg_c64 rk) 
  * Same unnormalised FFTW_BACKWARD result as the full complex transforms; plane traffic per
  * pair 84 B per pixel instead of 116.
  * ------------------------------------------------------------------------------------- */
+/* the frames' selections as the registration kernels read them: selection f, row r at
+ * p[f fp + r rp] (elements).  Contiguous S x S selections: fp = S S, rp = S; in place in resident
+ * frames (sg_register_dft_u16_device_pitched): the frames' plane / row pitches */
+struct SgSel {
+	const uint16_t *p;
+	long long fp, rp;
+	__device__ __forceinline__ const uint16_t *frame(int f) const { return p + (size_t)f * (size_t)fp; }
+};
+
 #ifndef SG_REG_FWD_WPE
 #define SG_REG_FWD_WPE 4	/* forward row pass: waves per SIMD its register budget is sized for (4: 127 VGPRs, 28 B of scratch, registration 5.93 -> 5.82 ms on configs[1]; 1: 134 VGPRs; 6: 208 B of scratch, 6.97 ms) */
 #endif
 template <class C>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(SG_REG_FWD_WPE)))
-k_reg_rows_fwd_half(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const int *__restrict__ fb,
+k_reg_rows_fwd_half(SgSel sel, const int *__restrict__ fa, const int *__restrict__ fb,
 		int S, const C *__restrict__ tw, C *__restrict__ work, unsigned long long *__restrict__ energy, int rpb) {
 	typedef typename SgReal<C>::T T;
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 	C *buf = (C *)smem;
 	const int pair = blockIdx.y, H = S >> 1, per = S >> 3;
 	const size_t plane = (size_t)S * S;
-	const uint16_t *pa = sel + (size_t)fa[pair] * plane;
+	const uint16_t *pa = sel.frame(fa[pair]);
 	const int b = fb[pair];
-	const uint16_t *pb = b >= 0 ? sel + (size_t)b * plane : nullptr;
+	const uint16_t *pb = b >= 0 ? sel.frame(b) : nullptr;
 	/* rpb rows per workgroup; the next row's samples are loaded into registers before this
 	 * row's transform (the first pass's inputs: thread t takes elements t + r S / 8), so its
 	 * load latency hides behind the LDS passes instead of opening every row (round 2: one row
@@ -116,7 +125,7 @@ k_reg_rows_fwd_half(const uint16_t *__restrict__ sel, const int *__restrict__ fa
 	auto fetch = [&](int row) {
 #pragma unroll
 		for (int r = 0; r < 8; r++) {
-			const size_t i = (size_t)row * S + (size_t)(t + r * per);
+			const size_t i = (size_t)row * sel.rp + (size_t)(t + r * per);
 			ra[r] = act ? (uint32_t)pa[i] : 0u;
 			rb[r] = (act && pb) ? (uint32_t)pb[i] : 0u;
 		}
@@ -593,7 +602,7 @@ k_reg_cols_xpower_w(float2 *__restrict__ work, const float2 *__restrict__ spec, 
  * natural order in the wave's LDS for the separation into the half spectra A, B
  * (k_reg_rows_fwd_half's arithmetic); the frames' energies summed per wave */
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SG_WCOL_WPE)))
-k_reg_rows_fwd_half_w(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const int *__restrict__ fb,
+k_reg_rows_fwd_half_w(SgSel sel, const int *__restrict__ fa, const int *__restrict__ fb,
 		const float2 *__restrict__ tw, float2 *__restrict__ work, unsigned long long *__restrict__ energy, int rpw) {
 	constexpr int S = 2048, H = 1024, P = 32;
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -601,18 +610,19 @@ k_reg_rows_fwd_half_w(const uint16_t *__restrict__ sel, const int *__restrict__ 
 	const int row0 = blockIdx.x * 4 * rpw + wave, pair = blockIdx.y;
 	float2 *col = (float2 *)smem + wave * SG_WCOL_CS;
 	const size_t plane = (size_t)S * S;
-	const uint16_t *pa = sel + (size_t)fa[pair] * plane;
+	const uint16_t *pa = sel.frame(fa[pair]);
 	const int b = fb[pair];
-	const uint16_t *pb = b >= 0 ? sel + (size_t)b * plane : nullptr;
+	const uint16_t *pb = b >= 0 ? sel.frame(b) : nullptr;
+	const size_t rp = (size_t)sel.rp;
 	uint16_t ua[P], ub[P];
 	auto fetch = [&](int row) {
 #pragma unroll
 		for (int j = 0; j < P; j++)
-			ua[j] = pa[(size_t)row * S + 64 * j + lane];
+			ua[j] = pa[(size_t)row * rp + 64 * j + lane];
 		if (pb) {
 #pragma unroll
 			for (int j = 0; j < P; j++)
-				ub[j] = pb[(size_t)row * S + 64 * j + lane];
+				ub[j] = pb[(size_t)row * rp + 64 * j + lane];
 		}
 	};
 	fetch(row0);
@@ -861,12 +871,12 @@ k_reg_rows_inv_half_argmax(const C *__restrict__ work, int S, const C *__restric
 /* SubSample (:223-234) of one 3x3 sample row, plus the running max of the middle rows
  * (the maxp[] loop :119-133 reduces to max over 0 < v < 65530) */
 __global__ void __launch_bounds__(1024)
-k_quality_sub(const uint16_t *__restrict__ sel, const int *__restrict__ qframes, int S, int xs, int ys,
+k_quality_sub(SgSel sel, int al, const int *__restrict__ qframes, int S, int xs, int ys,
 		uint16_t *__restrict__ qbuf, unsigned int *__restrict__ qmax) {
 	/* SG_QROWS output rows per workgroup; a thread forms two adjacent outputs from three
 	 * 12-byte (6-pixel, dword-aligned) loads, one per input row */
 	const int q = blockIdx.y;
-	const uint16_t *frame = sel + (size_t)qframes[q] * S * S;
+	const uint16_t *frame = sel.frame(qframes[q]);
 	unsigned int m = 0;
 	const int j0 = blockIdx.x * SG_QROWS;
 	for (int k = threadIdx.x; 2 * k < xs; k += blockDim.x) {
@@ -877,8 +887,8 @@ k_quality_sub(const uint16_t *__restrict__ sel, const int *__restrict__ qframes,
 			const int j = j0 + jj < ys ? j0 + jj : ys - 1;
 #pragma unroll
 			for (int y = 0; y < 3; y++) {
-				const uint16_t *q16 = frame + (size_t)(3 * j + y) * S + 6 * k;
-				if (!(S & 1)) {	/* even side: the 12 bytes are dword aligned */
+				const uint16_t *q16 = frame + (size_t)(3 * j + y) * sel.rp + 6 * k;
+				if (al) {	/* even side, pitches and base: the 12 bytes are dword aligned */
 					const uint32_t *p = (const uint32_t *)q16;
 					d[jj][y][0] = p[0];
 					d[jj][y][1] = p[1];
@@ -1354,7 +1364,7 @@ enum { SG_GEN_FWD_U16 = 0, SG_GEN_C2C = 1, SG_GEN_INV_ARGMAX = 2, SG_GEN_INV_CAN
  * row), INV_CAND (inverse, candidates of a near tie) */
 template <bool BLUE>
 __global__ void __launch_bounds__(BLUE ? 1024 : 640) __attribute__((amdgpu_waves_per_eu(BLUE ? 1 : 4)))
-k_gen_rows(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const int *__restrict__ fb,
+k_gen_rows(SgSel sel, const int *__restrict__ fa, const int *__restrict__ fb,
 		sg_c64 *__restrict__ data, int S, SgGenPlan pl, SgGenTables tb, int mode, int inverse,
 		unsigned long long *__restrict__ energy, SgBest *__restrict__ best, const SgRegOut *__restrict__ res,
 		SgCand *__restrict__ cand) {
@@ -1375,9 +1385,8 @@ k_gen_rows(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const i
 	const uint16_t *pa = nullptr, *pb = nullptr;
 	const int b = mode == SG_GEN_FWD_U16 ? fb[pair] : -1;
 	if (mode == SG_GEN_FWD_U16) {
-		const size_t plane = (size_t)S * S;
-		pa = sel + (size_t)fa[pair] * plane + (size_t)row * S;
-		pb = b >= 0 ? sel + (size_t)b * plane + (size_t)row * S : nullptr;
+		pa = sel.frame(fa[pair]) + (size_t)row * sel.rp;
+		pb = b >= 0 ? sel.frame(b) + (size_t)row * sel.rp : nullptr;
 	}
 	if (mode == SG_GEN_FWD_U16) {	/* the frames' energies (the rows are read again by the transform, from cache) */
 		unsigned long long ea = 0, eb = 0;
@@ -1513,7 +1522,7 @@ k_gen_cols_xpower(sg_c64 *__restrict__ data, const sg_c64 *__restrict__ spec, in
 
 /* exact sum_n ref(n + k) img(n) (circular) at every candidate k of a near tie (below 2^56) */
 __global__ void __launch_bounds__(256)
-k_reg_exact(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const int *__restrict__ fb, int ref, int S,
+k_reg_exact(SgSel sel, const int *__restrict__ fa, const int *__restrict__ fb, int ref, int S,
 		SgCand *__restrict__ cand) {
 	__shared__ unsigned long long part[4];
 	const int c = blockIdx.x, slot = blockIdx.y;
@@ -1525,11 +1534,11 @@ k_reg_exact(const uint16_t *__restrict__ sel, const int *__restrict__ fa, const 
 	if (frame < 0)
 		return;
 	const int k = cd->idx[c], ky = k / S, kx = k - ky * S;
-	const uint16_t *R = sel + (size_t)ref * S * S, *I = sel + (size_t)frame * S * S;
+	const uint16_t *R = sel.frame(ref), *I = sel.frame(frame);
 	unsigned long long acc = 0;
 	for (int y = 0; y < S; y++) {
 		const int yr = y + ky < S ? y + ky : y + ky - S;
-		const uint16_t *rr = R + (size_t)yr * S, *ir = I + (size_t)y * S;
+		const uint16_t *rr = R + (size_t)yr * sel.rp, *ir = I + (size_t)y * sel.rp;
 		for (int x = threadIdx.x; x < S; x += blockDim.x) {
 			const int xr = x + kx < S ? x + kx : x + kx - S;
 			acc += (unsigned long long)((unsigned int)rr[xr] * (unsigned int)ir[x]);
@@ -1585,7 +1594,7 @@ k_reg_resolve(const SgCand *__restrict__ cand, int S, int np, SgRegOut *__restri
  * already on `s`, which produced d_sel) so that it runs beside the FFT passes: its kernels are
  * short and the passes leave the chip latency-bound.  reg_quality_finish waits for the sums and
  * forms the values; *launched = false when the subsample loop never runs (dval = 0, :95-98). */
-static int reg_quality_launch(sg_ctx *ctx, SgDevice &dv, hipStream_t s, const uint16_t *d_sel, int S,
+static int reg_quality_launch(sg_ctx *ctx, SgDevice &dv, hipStream_t s, SgSel d_sel, int S,
 		const std::vector<int> &frames, bool *launched) {
 	*launched = false;
 	const int nq = (int)frames.size();
@@ -1620,8 +1629,10 @@ static int reg_quality_launch(sg_ctx *ctx, SgDevice &dv, hipStream_t s, const ui
 	/* one wave per workgroup, walking the row pairs: 283 us per 129 frames of 2048^2 against
 	 * 332 / 348 / 403 / 618 us with 128 / 192 / 256 / 384 threads (scripts/gpu_qsub.sh) */
 	const int qthr = ctx->knobs.qsub_threads;	/* A/B knob SG_QSUB_THREADS */
-	hipLaunchKernelGGL(k_quality_sub, dim3((ys + SG_QROWS - 1) / SG_QROWS, nq), dim3(qthr), 0, dv.aux, d_sel, d_frames, S,
-			xs, ys, qbuf, qmax);
+	/* the dword loads of k_quality_sub need an even side, even pitches and a dword-aligned base */
+	const int al = !(S & 1) && !(d_sel.rp & 1) && !(d_sel.fp & 1) && !((uintptr_t)d_sel.p & 3);
+	hipLaunchKernelGGL(k_quality_sub, dim3((ys + SG_QROWS - 1) / SG_QROWS, nq), dim3(qthr), 0, dv.aux, d_sel, al, d_frames,
+			S, xs, ys, qbuf, qmax);
 	HIPCHK(hipGetLastError());
 	/* 2 waves per 64x16 tile: 214 us per 129 frames against 238 (4 waves) and 333 (1 wave),
 	 * scripts/gpu_qgrad.sh */
@@ -1735,27 +1746,40 @@ static void host_fft_pow2(std::vector<double> &re, std::vector<double> &im, int 
 	}
 }
 
-static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int nframes, int S, int ref_image,
-		const int *included, int *shiftx, int *shifty, double *quality, void *stream, bool normalize_q);
+static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel_p, int64_t fpitch, int64_t rpitch,
+		int nframes, int S, int ref_image, const int *included, int *shiftx, int *shifty, double *quality, void *stream,
+		bool normalize_q);
 
 extern "C" int sg_register_dft_u16_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int nframes,
 		int S, int ref_image, const int *included, int *shiftx, int *shifty, double *quality,
 		void *stream) {
-	return reg_dft_device(ctx, dev_index, d_sel, nframes, S, ref_image, included, shiftx, shifty, quality, stream,
-			true);
+	return reg_dft_device(ctx, dev_index, d_sel, (int64_t)S * S, S, nframes, S, ref_image, included, shiftx, shifty,
+			quality, stream, true);
 }
 
 extern "C" int sg_register_dft_u16_device_raw(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int nframes,
 		int S, int ref_image, const int *included, int *shiftx, int *shifty, double *quality_raw,
 		void *stream) {
-	return reg_dft_device(ctx, dev_index, d_sel, nframes, S, ref_image, included, shiftx, shifty, quality_raw,
-			stream, false);
+	return reg_dft_device(ctx, dev_index, d_sel, (int64_t)S * S, S, nframes, S, ref_image, included, shiftx, shifty,
+			quality_raw, stream, false);
 }
 
-static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int nframes, int S, int ref_image,
-		const int *included, int *shiftx, int *shifty, double *quality, void *stream, bool normalize_q) {
-	if (!ctx || dev_index < 0 || dev_index >= (int)ctx->dev.size() || !d_sel || !shiftx || !shifty || !quality)
+/* selections read in place from resident frames: selection f row r at d_sel[f frame_pitch + r row_pitch] */
+extern "C" int sg_register_dft_u16_device_pitched(sg_ctx *ctx, int dev_index, const uint16_t *d_sel, int64_t frame_pitch,
+		int64_t row_pitch, int nframes, int S, int ref_image, const int *included, int *shiftx, int *shifty,
+		double *quality, int raw_quality, void *stream) {
+	if (ctx && (row_pitch < S || frame_pitch < 0))
+		return set_err(ctx, SG_ERR_SIZE, "selection pitches: a row pitch below the side S%s (%ld)", "", (long)row_pitch);
+	return reg_dft_device(ctx, dev_index, d_sel, frame_pitch, row_pitch, nframes, S, ref_image, included, shiftx, shifty,
+			quality, stream, !raw_quality);
+}
+
+static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel_p, int64_t fpitch, int64_t rpitch,
+		int nframes, int S, int ref_image, const int *included, int *shiftx, int *shifty, double *quality, void *stream,
+		bool normalize_q) {
+	if (!ctx || dev_index < 0 || dev_index >= (int)ctx->dev.size() || !d_sel_p || !shiftx || !shifty || !quality)
 		return SG_ERR_GENERIC;
+	const SgSel d_sel{d_sel_p, (long long)fpitch, (long long)rpitch};
 	if (nframes < 1)
 		return set_err(ctx, SG_ERR_GENERIC, "no frame to register%s%ld", "", nframes);
 	if (S < 4 || S > 4096)
@@ -2442,7 +2466,8 @@ static int reg_host(sg_ctx *ctx, const uint16_t *sel, int nframes, int S, int re
 		const size_t bytes = (size_t)nframes * plane * sizeof(uint16_t);
 		HIPCHK(ensure(dv.reg_sel, bytes));
 		HIPCHK(hipMemcpyAsync(dv.reg_sel.p, sel, bytes, hipMemcpyHostToDevice, dv.stream));
-		return reg_dft_device(ctx, 0, (const uint16_t *)dv.reg_sel.p, nframes, S, ref_image, included, shiftx, shifty,
+		return reg_dft_device(ctx, 0, (const uint16_t *)dv.reg_sel.p, (int64_t)S * S, S, nframes, S, ref_image, included,
+				shiftx, shifty,
 				quality, nullptr, normalize_q);
 	}
 	/* shard g: local frame 0 = the reference, 1..k = todo[t0 .. t1) */
@@ -2475,7 +2500,8 @@ static int reg_host(sg_ctx *ctx, const uint16_t *sel, int nframes, int S, int re
 		}
 		std::vector<int> lx((size_t)k + 1), ly((size_t)k + 1);
 		std::vector<double> lq((size_t)k + 1);
-		rc = reg_dft_device(ctx, g, d, k + 1, S, 0, nullptr, lx.data(), ly.data(), lq.data(), nullptr, false);
+		rc = reg_dft_device(ctx, g, d, (int64_t)S * S, S, k + 1, S, 0, nullptr, lx.data(), ly.data(), lq.data(), nullptr,
+				false);
 		if (rc)
 			return;
 		qref[(size_t)g] = lq[0];

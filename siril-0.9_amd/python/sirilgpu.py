@@ -83,7 +83,7 @@ class SeqInfo(ctypes.Structure):
 EXPORTS = ["sg_init", "sg_shutdown", "sg_last_error", "sg_stack_u16", "sg_stack_u16_device",
            "sg_stack_u16_device_async", "sg_stack_collect", "sg_stack_wait_tail", "sg_device_count",
            "sg_get_last_stats", "sg_register_dft_u16", "sg_register_dft_u16_device",
-           "sg_register_dft_u16_device_raw", "sg_synth_fill_device",
+           "sg_register_dft_u16_device_raw", "sg_register_dft_u16_device_pitched", "sg_synth_fill_device",
            "sg_seq_open_ser", "sg_seq_open_fits", "sg_seq_close", "sg_seq_get_info", "sg_seq_read_region",
            "sg_seq_read_frame", "sg_seq_load_device", "sg_seq_set_debayer", "sg_warp_u16", "sg_warp_u16_device",
            "sg_frame_stats_ikss_device", "sg_compute_normalization", "sg_seqfile_read", "sg_seqfile_create",
@@ -144,6 +144,9 @@ def load():
     lib.sg_register_dft_u16_device.restype = ctypes.c_int
     lib.sg_register_dft_u16_device_raw.argtypes = lib.sg_register_dft_u16_device.argtypes
     lib.sg_register_dft_u16_device_raw.restype = ctypes.c_int
+    lib.sg_register_dft_u16_device_pitched.argtypes = [P, ctypes.c_int, P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                                       ctypes.c_int, ctypes.c_int, P, P, P, P, ctypes.c_int, P]
+    lib.sg_register_dft_u16_device_pitched.restype = ctypes.c_int
     lib.sg_seq_open_ser.argtypes = [ctypes.c_char_p, ctypes.POINTER(P)]
     lib.sg_seq_open_ser.restype = ctypes.c_int
     lib.sg_seq_open_fits.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.POINTER(P)]
@@ -562,19 +565,26 @@ class Context:
         return sx, sy, q
 
     def register_dft_device(self, d_sel, nframes, S, ref_image=0, included=None, stream=None, dev_index=0,
-                            raw_quality=False):
+                            raw_quality=False, frame_pitch=0, row_pitch=0):
         """register_shift_dft on device selections; raw_quality: the shard entry point
-        (sg_register_dft_u16_device_raw: QualityEstimate values, not normalised)"""
+        (sg_register_dft_u16_device_raw: QualityEstimate values, not normalised); frame_pitch /
+        row_pitch (elements): selections read in place from resident frames
+        (sg_register_dft_u16_device_pitched)"""
         inc = None if included is None else np.ascontiguousarray(included, dtype=np.int32)
         sx = np.zeros(nframes, dtype=np.int32)
         sy = np.zeros(nframes, dtype=np.int32)
         q = np.zeros(nframes, dtype=np.float64)
         P = ctypes.c_void_p
+        args = (inc.ctypes.data_as(P) if inc is not None else None, sx.ctypes.data_as(P), sy.ctypes.data_as(P),
+                q.ctypes.data_as(P))
+        if frame_pitch or row_pitch:
+            rc = self.lib.sg_register_dft_u16_device_pitched(
+                self.ctx, dev_index, P(d_sel), frame_pitch or S * S, row_pitch or S, nframes, S, ref_image, *args,
+                1 if raw_quality else 0, P(stream) if stream else None)
+            self.check(rc, "sg_register_dft_u16_device_pitched")
+            return sx, sy, q
         fn = self.lib.sg_register_dft_u16_device_raw if raw_quality else self.lib.sg_register_dft_u16_device
-        rc = fn(self.ctx, dev_index, P(d_sel), nframes, S, ref_image,
-                inc.ctypes.data_as(P) if inc is not None else None,
-                sx.ctypes.data_as(P), sy.ctypes.data_as(P),
-                q.ctypes.data_as(P), P(stream) if stream else None)
+        rc = fn(self.ctx, dev_index, P(d_sel), nframes, S, ref_image, *args, P(stream) if stream else None)
         self.check(rc, "sg_register_dft_u16_device" + ("_raw" if raw_quality else ""))
         return sx, sy, q
 

@@ -307,3 +307,54 @@ def test_register_raw_shards_reassemble(gpu_ctx, world, ref):
     assert _same_q(q, gq), (q, gq)
     # the raw values are QualityEstimate's (the oracle's, exactly)
     assert _same_q(qraw, np.array([orc.quality(sel[f]) for f in range(n)]))
+
+
+@pytest.mark.parametrize("S,x0,y0", [(2048, 1976, 976), (64, 7, 3), (60, 12, 5), (64, 8, 2)])
+def test_register_pitched_window_matches_extracted(gpu_ctx, S, x0, y0):
+    """selections read in place from resident [C][H][W] frames (sg_register_dft_u16_device_pitched:
+    layer 1's S x S window at (x0, y0), frame pitch C H W, row pitch W) register exactly as the
+    extracted contiguous selections do: shifts and raw / normalised qualities (the wave-level
+    S = 2048 rows, the block rows at 64, the generic passes at 60; an odd x0 takes k_quality_sub's
+    unaligned loads)"""
+    import torch
+    N, C = (6, 2) if S == 2048 else (9, 3)
+    H, W = S + 2 * y0 + 3, S + x0 + 17
+    frames = orc.synth(N, C, H, W, seed=S + x0, maxshift=5)
+    if S != 2048:
+        frames[:, 1, y0 + 10:y0 + 14, x0 + 20:x0 + 24] = 40000      # structure for QualityEstimate
+    d = torch.from_numpy(frames.view(np.int16).reshape(-1)).cuda()
+    sel = np.ascontiguousarray(frames[:, 1, y0:y0 + S, x0:x0 + S])
+    ds = torch.from_numpy(sel.view(np.int16).reshape(-1)).cuda()
+    torch.cuda.synchronize()
+    inc = np.ones(N, np.int32)
+    inc[2] = 0
+    want = gpu_ctx.register_dft_device(ds.data_ptr(), N, S, ref_image=1, included=inc)
+    base = d.data_ptr() + 2 * (H * W + y0 * W + x0)
+    got = gpu_ctx.register_dft_device(base, N, S, ref_image=1, included=inc, frame_pitch=C * H * W, row_pitch=W)
+    for a, b in zip(got, want):
+        assert np.array_equal(a, b, equal_nan=True), (a, b)
+    raw_w = gpu_ctx.register_dft_device(ds.data_ptr(), N, S, ref_image=1, included=inc, raw_quality=True)[2]
+    raw_g = gpu_ctx.register_dft_device(base, N, S, ref_image=1, included=inc, raw_quality=True, frame_pitch=C * H * W,
+                                        row_pitch=W)[2]
+    assert np.array_equal(raw_g, raw_w, equal_nan=True)
+    if S <= 64:
+        rx, ry, _ = orc.register_dft(sel, ref_image=1, included=inc)
+        m = inc.astype(bool)
+        assert np.array_equal(got[0][m], rx[m]) and np.array_equal(got[1][m], ry[m])
+
+
+def test_register_pitched_tie_exact(gpu_ctx):
+    """the exact integer correlations of a near tie (k_reg_exact) read the pitched selections"""
+    import torch
+    S, pad = 64, 9
+    ref, img = _periodic_pair(S, 3, 5, seed=S)
+    big = np.zeros((2, S + pad, S + 2 * pad), np.uint16)
+    big[:, pad:, pad:pad + S] = np.stack([ref, img]).astype(np.uint16)
+    d = torch.from_numpy(big.view(np.int16).reshape(-1)).cuda()
+    torch.cuda.synchronize()
+    W = S + 2 * pad
+    gx, gy, _ = gpu_ctx.register_dft_device(d.data_ptr() + 2 * (pad * W + pad), 2, S, frame_pitch=(S + pad) * W,
+                                            row_pitch=W)
+    cx, cy, _ = gpu_ctx.register_dft(np.stack([ref, img]).astype(np.uint16))
+    assert (gx[1], gy[1]) == (cx[1], cy[1])
+    assert gpu_ctx.stats().reg_ties_resolved >= 1
