@@ -134,6 +134,22 @@ static int sigma_clipping(uint16_t pixel, const double sig[], double sigma, doub
 		return 0;
 }
 
+static int or_is_sorted_u16(const uint16_t *a, int n) {
+	for (int i = 1; i < n; i++)
+		if (a[i] < a[i - 1])
+			return 0;
+	return 1;
+}
+
+/* quicksort_s (src/core/utils.c:512-533) where the reference calls it inside a rejection loop:
+ * from the second pass on the stack is already sorted (removal keeps the order, clamping keeps it
+ * sorted), and sorting a sorted array is the identity, so the sort runs only when an element is
+ * out of order: the same array either way, a test-time saving only */
+static void or_sort_stack(uint16_t *a, int n) {
+	if (!or_is_sorted_u16(a, n))
+		or_quicksort_s(a, n);
+}
+
 static void winsorize(uint16_t *pixel, double m0, double m1) {
 	if (*pixel < m0)
 		*pixel = or_round_to_WORD(m0);
@@ -167,7 +183,7 @@ static uint16_t reject_and_mean(uint16_t *stack, int *rejected, int nb_frames, i
 	int n, j, r = 0, frame;
 	switch (type) {
 	case OR_PERCENTILE:
-		or_quicksort_s(stack, N);
+		or_sort_stack(stack, N);
 		median = or_gsl_median_from_sorted_u16(stack, N);
 		for (frame = 0; frame < N; frame++)
 			rejected[frame] = percentile_clipping(stack[frame], sig, median, crej);
@@ -182,7 +198,7 @@ static uint16_t reject_and_mean(uint16_t *stack, int *rejected, int nb_frames, i
 	case OR_SIGMA:
 		do {
 			sigma = or_gsl_sd_u16(stack, N);
-			or_quicksort_s(stack, N);
+			or_sort_stack(stack, N);
 			median = or_gsl_median_from_sorted_u16(stack, N);
 			n = 0;
 			for (frame = 0; frame < N; frame++) {
@@ -205,7 +221,7 @@ static uint16_t reject_and_mean(uint16_t *stack, int *rejected, int nb_frames, i
 	case OR_SIGMEDIAN:
 		do {
 			sigma = or_gsl_sd_u16(stack, N);
-			or_quicksort_s(stack, N);
+			or_sort_stack(stack, N);
 			median = or_gsl_median_from_sorted_u16(stack, N);
 			n = 0;
 			for (frame = 0; frame < N; frame++) {
@@ -220,7 +236,7 @@ static uint16_t reject_and_mean(uint16_t *stack, int *rejected, int nb_frames, i
 		do {
 			double sigma0;
 			sigma = or_gsl_sd_u16(stack, N);
-			or_quicksort_s(stack, N);
+			or_sort_stack(stack, N);
 			median = or_gsl_median_from_sorted_u16(stack, N);
 			uint16_t *w_stack = malloc(N * sizeof(uint16_t));
 			memcpy(w_stack, stack, N * sizeof(uint16_t));
@@ -230,7 +246,7 @@ static uint16_t reject_and_mean(uint16_t *stack, int *rejected, int nb_frames, i
 				double m1 = median + 1.5 * sigma;
 				for (jj = 0; jj < N; jj++)
 					winsorize(&w_stack[jj], m0, m1);
-				or_quicksort_s(w_stack, N);
+				or_sort_stack(w_stack, N);	/* :1722 */
 				median = or_gsl_median_from_sorted_u16(w_stack, N);
 				sigma0 = sigma;
 				sigma = 1.134 * or_gsl_sd_u16(w_stack, N);
@@ -259,7 +275,7 @@ static uint16_t reject_and_mean(uint16_t *stack, int *rejected, int nb_frames, i
 			double *xf = malloc(N * sizeof(double));
 			double *yf = malloc(N * sizeof(double));
 			double a, b;
-			or_quicksort_s(stack, N);
+			or_sort_stack(stack, N);
 			for (frame = 0; frame < N; frame++) {
 				xf[frame] = (double)frame;
 				yf[frame] = (double)stack[frame];
