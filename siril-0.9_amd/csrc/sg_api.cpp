@@ -33,7 +33,7 @@ __global__ void k_stack_sorted(SgStackParams p, const unsigned int *list, const 
 template <int REJ, int NORM, int NI>
 __global__ void k_stack_hist(SgStackParams p, const int *tab, const int4 *norm, unsigned int *redo_count,
 		unsigned int *redo_list);
-template <int KM, int NW>
+template <int KM, int NW, bool PAIR>
 __global__ void k_stack_linfit(SgStackParams p, unsigned int *redo_count, unsigned int *redo_list);
 void sg_dbg_why_dump(hipStream_t s);
 int sgh_block_threads(int ni, int rej);
@@ -859,9 +859,15 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 				/* waves per tile: 4, 8 or (KM = 8 only: 187 VGPRs at KM = 16) 16 */
 				const int lw = ctx->knobs.linfit_waves;
 				const int nw = lw == 4 ? 4 : (lw == 16 && km == 8) ? 16 : 8;
-				const void *kf = km == 8 ? (nw == 4 ? (const void *)k_stack_linfit<8, 4> :
-						nw == 8 ? (const void *)k_stack_linfit<8, 8> : (const void *)k_stack_linfit<8, 16>) :
-					(nw == 4 ? (const void *)k_stack_linfit<16, 4> : (const void *)k_stack_linfit<16, 8>);
+				/* SG_LINFIT_PAIR: both pixels of a sorted pair in lockstep (lfx_pixel2_m), 4 or 8 waves */
+				const bool pr = ctx->knobs.linfit_pair && nw != 16;
+				const void *kf = pr ? (km == 8 ? (nw == 4 ? (const void *)k_stack_linfit<8, 4, true> :
+								(const void *)k_stack_linfit<8, 8, true>) :
+							(nw == 4 ? (const void *)k_stack_linfit<16, 4, true> :
+								(const void *)k_stack_linfit<16, 8, true>)) :
+					km == 8 ? (nw == 4 ? (const void *)k_stack_linfit<8, 4, false> :
+						nw == 8 ? (const void *)k_stack_linfit<8, 8, false> : (const void *)k_stack_linfit<8, 16, false>) :
+					(nw == 4 ? (const void *)k_stack_linfit<16, 4, false> : (const void *)k_stack_linfit<16, 8, false>);
 				HIPCHK(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lfx_lds));
 				const dim3 lg((unsigned)((size_t)((W + 63) / 64) * nrows * C));
 				void *lfx_args[] = {&p, &redo_count, &redo_list};

@@ -147,6 +147,7 @@ struct SgKnobs {
 	int reg_rpw = 8;		/* SG_REG_RPW: rows per wave of the wave-level forward row pass (the next row fetched during this one's transform) */
 	int reg_qafter = 0;		/* SG_REG_QAFTER: 1 = the quality estimate queued after the first batch's forward rows (beside the column pass) */
 	int linfit_waves = 8;		/* SG_LINFIT_WAVES: waves per 64-pixel k_stack_linfit tile (4, 8 or 16 (KM = 8)) */
+	int linfit_pair = 0;		/* SG_LINFIT_PAIR: 1 = both pixels of a sorted pair through one lockstep pass loop (lfx_pixel2_m) */
 	int linfit_fast = 1;		/* SG_LINFIT_FAST: 1 = LINEARFIT through the decision-exact k_stack_linfit (16 <= N <= 1024), redo pixels to the sorted kernel; 0 = every pixel through the sorted kernel */
 	int qgrad_stream = 1;		/* SG_QGRAD_STREAM: 1 = the quality gradient streamed down 60-column bands (k_quality_grad_s), 0 = tiled */
 	int reg_wcolw = 8;		/* SG_REG_WCOLW: columns per strip of the wave-level column pass (8: 64-B row segments, one workgroup per CU: configs[1] registration 3.33 -> 3.20 ms and the pass's HBM writes 1.57x -> 1.0x the plane, profiles/r05w_*; 4: 32-B segments, two workgroups per CU) */
@@ -194,6 +195,7 @@ struct SgKnobs {
 		qgrad_stream = sg_env_int("SG_QGRAD_STREAM", 0, 1, 1);
 		linfit_fast = sg_env_int("SG_LINFIT_FAST", 0, 1, 1);
 		linfit_waves = sg_env_int("SG_LINFIT_WAVES", 4, 16, 8);
+		linfit_pair = sg_env_int("SG_LINFIT_PAIR", 0, 1, 0);
 		reg_qafter = sg_env_int("SG_REG_QAFTER", 0, 1, 0);
 		reg_rpw = sg_env_int("SG_REG_RPW", 1, 64, 8);
 	}

@@ -2557,8 +2557,152 @@ __device__ int lfx_pixel_m(const uint32_t (&x)[KM], int N0, double sl, double sh
 	return 0;
 }
 
-template <int KM, int NW>
-__global__ void __launch_bounds__(64 * NW)
+/* the passes of BOTH pixels of a packed sorted pair (pixel 0 in the low u16 of x2[k], pixel 1 in
+ * the high one) in lockstep (round 6): per pixel the arithmetic and decisions of
+ * lfx_pixel_m, step for step; the two pixels' wave reductions and fp64 chains are independent work
+ * in one basic block, so each hides the other's latency (lfx_pixel_m is a serial chain of wave
+ * reductions per pass).  Per-element doubles (rank, sample, residual) are recomputed where used
+ * instead of held in arrays, which keeps two pixels in about one pixel's registers.  A pixel that
+ * has finished rides along (its results are not committed) until the other one finishes.
+ * ok[h]: 1 value and counters, 0 redo list. */
+template <int KM>
+__device__ void lfx_pixel2_m(const uint32_t (&x2)[KM], int N0, double sl, double sh, int lane, uint16_t (&value)[2],
+		uint32_t (&rlo)[2], uint32_t (&rhi)[2], int (&ok)[2]) {
+	constexpr double u = 1.1102230246251565e-16;
+	unsigned long long km[2][KM];
+#pragma unroll
+	for (int k = 0; k < KM; k++)
+		km[0][k] = km[1][k] = __ballot(64 * k + lane < N0);
+	int N[2] = {N0, N0}, r[2] = {0, 0}, st[2] = {0, 0};	/* st: 0 running, 1 value, 2 redo */
+	uint32_t clo[2] = {0, 0}, chi[2] = {0, 0};
+	const double asl = fabs(sl), ash = fabs(sh), amx = asl > ash ? asl : ash;
+	auto xv = [&](int h, int k) -> uint32_t { return h ? (x2[k] >> 16) : (x2[k] & 0xFFFFu); };
+	for (int pass = 0; pass < 4096 && (st[0] == 0 || st[1] == 0); pass++) {
+		uint32_t sy[2], siy[2], ymax[2];
+#pragma unroll
+		for (int h = 0; h < 2; h++) {
+			int base = 0;
+			sy[h] = siy[h] = ymax[h] = 0;
+#pragma unroll
+			for (int k = 0; k < KM; k++) {
+				const bool kp = (km[h][k] >> lane) & 1ull;
+				const int rk = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(km[h][k] >> 32),
+						__builtin_amdgcn_mbcnt_lo((unsigned)km[h][k], 0u));
+				base += __popcll(km[h][k]);
+				const uint32_t xk = kp ? xv(h, k) : 0u;
+				sy[h] += xk;
+				siy[h] += (uint32_t)rk * xk;
+				ymax[h] = xk > ymax[h] ? xk : ymax[h];
+			}
+		}
+		double Sy[2], Siy[2], Y[2];
+#pragma unroll
+		for (int h = 0; h < 2; h++) {
+			Sy[h] = (double)lfx_sum_u32(sy[h]);
+			Siy[h] = (double)lfx_sum_u32(siy[h] & 0xFFFFu) + 65536.0 * (double)lfx_sum_u32(siy[h] >> 16);
+			Y[h] = (double)lfx_max_u32(ymax[h]);
+		}
+		double slope[2], b0[2], sres[2], inv_n[2];
+#pragma unroll
+		for (int h = 0; h < 2; h++) {
+			const double n = (double)N[h];
+			inv_n[h] = 1.0 / n;
+			const double Pn = 12.0 * Siy[h] - 6.0 * (n - 1.0) * Sy[h];
+			slope[h] = Pn / (n * (n * n - 1.0));
+			b0[h] = Sy[h] * inv_n[h] - 0.5 * (n - 1.0) * slope[h];
+			int base = 0;
+			double sr = 0.0;
+#pragma unroll
+			for (int k = 0; k < KM; k++) {
+				const int rk = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(km[h][k] >> 32),
+						__builtin_amdgcn_mbcnt_lo((unsigned)km[h][k], 0u));
+				base += __popcll(km[h][k]);
+				const double dv = fma(slope[h], (double)rk, b0[h]) - (double)xv(h, k);
+				sr += ((km[h][k] >> lane) & 1ull) ? fabs(dv) : 0.0;
+			}
+			sres[h] = sr;
+		}
+		double sigma[2];
+#pragma unroll
+		for (int h = 0; h < 2; h++)
+			sigma[h] = lfx_sum_f64(sres[h]) * inv_n[h];
+#pragma unroll
+		for (int h = 0; h < 2; h++) {
+			if (st[h] != 0)
+				continue;
+			if (N[h] < 8) {
+				st[h] = 2;
+				continue;
+			}
+			const double n = (double)N[h];
+			/* lfx_pixel_m's closed-form bounds and 4x margins */
+			const double as = fabs(slope[h]), nas = n * as;
+			const double dS = 98.0 * u * (Y[h] + nas + as);
+			const double Rm = Y[h] + nas + fabs(b0[h]) + 1.0;
+			const double dB = 2.0 * u * n * (Y[h] + nas) + 0.5 * n * dS + 8.0 * u * Rm;
+			const double dline = n * dS + dB + 32.0 * u * Rm;
+			const double dsig = dline + 2.0 * (n + 2.0) * u * Rm;
+			if (!(sigma[h] > 4.0 * dsig) || !(sl == sl) || !(sh == sh) || !(sl > 0.0) || !(sh > 0.0)) {
+				st[h] = 2;
+				continue;
+			}
+			const double tL = sl * sigma[h], tH = sh * sigma[h];
+			const double e1 = 4.0 * dS;
+			const double eM = 4.0 * (dB + 32.0 * u * Rm + amx * dsig + 4.0 * u * (Rm + amx * sigma[h]));
+			unsigned long long amb = 0, rm[KM];
+			int nl = 0, nh = 0, base = 0;
+#pragma unroll
+			for (int k = 0; k < KM; k++) {
+				const int rk = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(km[h][k] >> 32),
+						__builtin_amdgcn_mbcnt_lo((unsigned)km[h][k], 0u));
+				base += __popcll(km[h][k]);
+				const double dv = fma(slope[h], (double)rk, b0[h]) - (double)xv(h, k);
+				const double e = fma(e1, (double)rk, eM);
+				const double a = dv - tL, b = dv + tH;
+				const unsigned long long lo = __ballot(a > e) & km[h][k], hi = __ballot(b < -e) & km[h][k];
+				amb |= __ballot(fabs(a) <= e || fabs(b) <= e) & km[h][k];
+				nl += __popcll(lo);
+				nh += __popcll(hi);
+				rm[k] = lo | hi;
+			}
+			if (amb) {
+				st[h] = 2;
+				continue;
+			}
+			const int nrej = nl + nh;
+			if (r[h] + nrej >= N[h] - 4) {
+				st[h] = 2;
+				continue;
+			}
+#pragma unroll
+			for (int k = 0; k < KM; k++)
+				km[h][k] &= ~rm[k];
+			clo[h] += nl;
+			chi[h] += nh;
+			r[h] += nrej;
+			N[h] -= nrej;
+			if (!(nrej > 0 && N[h] > 3)) {
+				double S = Sy[h];
+				if (nrej > 0) {
+					uint32_t s2 = 0;
+#pragma unroll
+					for (int k = 0; k < KM; k++)
+						s2 += ((km[h][k] >> lane) & 1ull) ? xv(h, k) : 0u;
+					S = (double)lfx_sum_u32(s2);
+				}
+				value[h] = sg_round_to_WORD(S / (double)N[h]);
+				rlo[h] = clo[h];
+				rhi[h] = chi[h];
+				st[h] = 1;
+			}
+		}
+	}
+	ok[0] = st[0] == 1;
+	ok[1] = st[1] == 1;
+}
+
+template <int KM, int NW, bool PAIR = false>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu((PAIR && KM == 8) ? 4 : 1)))	/* pair: 4 waves per SIMD */
 k_stack_linfit(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
 	extern __shared__ uint16_t lfx_cols[];
 	constexpr int LS = 64 * KM + 2;	/* column stride: an odd dword count (conflict-free stores) */
@@ -2604,6 +2748,31 @@ k_stack_linfit(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned 
 			v2[k] = (uint32_t)lfx_cols[q0 * LS + 64 * k + lane] |
 				((uint32_t)lfx_cols[(q0 + NW < 64 ? q0 + NW : q0) * LS + 64 * k + lane] << 16);
 		lfx_sort<KM>(v2, lane);
+		if (PAIR) {	/* both pixels' passes in lockstep (lfx_pixel2_m) */
+			uint16_t value[2] = {0, 0};
+			uint32_t rl[2] = {0, 0}, rh[2] = {0, 0};
+			int ok[2] = {0, 0};
+			lfx_pixel2_m<KM>(v2, N, p.sig0, p.sig1, lane, value, rl, rh, ok);
+			for (int h = 0; h < 2; h++) {
+				const int q = q0 + NW * h;
+				if (q >= np)
+					break;
+				const int64_t pix = ((int64_t)c * p.H + R) * p.W + x0 + q;
+				if (lane == 0) {
+					if (ok[h]) {
+						p.out[pix] = value[h];
+						unsigned long long *sh = p.rej + ((size_t)(blockIdx.x % SG_REJ_SHARDS) * 6 + c * 2);
+						if (rl[h])
+							atomicAdd(sh, (unsigned long long)rl[h]);
+						if (rh[h])
+							atomicAdd(sh + 1, (unsigned long long)rh[h]);
+					} else {
+						redo_list[atomicAdd(redo_count, 1u)] = (unsigned int)pix;
+					}
+				}
+			}
+			continue;
+		}
 #pragma unroll 1
 		for (int h = 0; h < 2; h++) {
 			const int q = q0 + NW * h;
@@ -2632,6 +2801,10 @@ k_stack_linfit(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned 
 		}
 	}
 }
+template __global__ void k_stack_linfit<8, 8, true>(SgStackParams, unsigned int *, unsigned int *);
+template __global__ void k_stack_linfit<8, 4, true>(SgStackParams, unsigned int *, unsigned int *);
+template __global__ void k_stack_linfit<16, 8, true>(SgStackParams, unsigned int *, unsigned int *);
+template __global__ void k_stack_linfit<16, 4, true>(SgStackParams, unsigned int *, unsigned int *);
 template __global__ void k_stack_linfit<8, 4>(SgStackParams, unsigned int *, unsigned int *);
 template __global__ void k_stack_linfit<8, 8>(SgStackParams, unsigned int *, unsigned int *);
 template __global__ void k_stack_linfit<8, 16>(SgStackParams, unsigned int *, unsigned int *);
