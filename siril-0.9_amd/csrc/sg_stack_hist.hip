@@ -1324,8 +1324,15 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 				SGH_WPEV(0);
 				const int side = (pend & 1) ? 0 : 1;
 				const SghX x = sgh_qx(P, side ? b1 : a1, side);
+#ifdef SGH_QX_TWICE	/* A/B probe build: every query body runs twice (its price in the kernel time) */
+				uint32_t z0;
+				asm volatile("v_mov_b32 %0, 0" : "=v"(z0));
+				const int qx_extra = sgh_qx(P, (side ? b1 : a1) + (int)z0, side).c & (int)z0;
+#else
+				const int qx_extra = 0;
+#endif
 				if (side) {
-					cH = x.c;
+					cH = x.c + qx_extra;
 					sB = x.s;
 					ssB = x.ss;
 					uhi = x.nb;
