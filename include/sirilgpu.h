@@ -193,6 +193,7 @@ typedef struct {
 					 * histogram kernel wrote out (no gather in the sorted kernel) */
 	double reg_ms;			/* last registration on a device: HIP-event span of its device work
 					 * (first pass to the quality estimate's end, host waits included) */
+	uint64_t exported_pixels;	/* histogram WINSORIZED: columns finished by k_hist_slow (SG_WINS_EXPORT) */
 } sg_stack_stats;
 int sg_get_last_stats(const sg_ctx *ctx, sg_stack_stats *st);
 /* device slots of the context (sg_init's ndev): callers size their batches by it, as the

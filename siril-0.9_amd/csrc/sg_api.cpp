@@ -35,6 +35,7 @@ __global__ void k_stack_hist(SgStackParams p, const int *tab, const int4 *norm, 
 		unsigned int *redo_list);
 template <int KM, int NW, bool PAIR>
 __global__ void k_stack_linfit(SgStackParams p, unsigned int *redo_count, unsigned int *redo_list);
+__global__ void k_hist_slow(SgStackParams p, unsigned int *redo_count, unsigned int *redo_list);
 void sg_dbg_why_dump(hipStream_t s);
 int sgh_block_threads(int ni, int rej);
 template <int NM>
@@ -123,7 +124,8 @@ extern "C" void sg_shutdown(sg_ctx *ctx) {
 			if (b->p)
 				(void)hipFree(b->p);
 		for (SgSlot &q : d.sl) {
-			SgBuf *sb[] = {&q.inb, &q.flag_list, &q.flag_map, &q.redo, &q.cmp_cols, &q.cmp_list, &q.scratch, &q.lin_tab};
+			SgBuf *sb[] = {&q.inb, &q.flag_list, &q.flag_map, &q.redo, &q.cmp_cols, &q.cmp_list, &q.scratch, &q.lin_tab,
+				&q.wx};
 			for (SgBuf *b : sb)
 				if (b->p)
 					(void)hipFree(b->p);
@@ -358,6 +360,7 @@ static int stack_fold(sg_ctx *ctx, SgDevice &dv, int slot, uint64_t rej[3][2], u
 	if (st.path == 1)
 		st.chain_pixels = fl[2];
 	st.compact_pixels = std::min<uint64_t>(fl[3], st.compact_pixels);	/* pstats holds the capacity */
+	st.exported_pixels = st.exported_pixels ? std::min<uint64_t>(fl[6], st.exported_pixels) : 0;	/* capacity, as compact */
 	if (sync) {	/* the calling stack_device_core publishes dv.stats when it returns */
 		dv.stats = st;
 	} else {
@@ -851,6 +854,17 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 				p.cmp_count = p.flag_count + 3;	/* cleared with the counters */
 				p.cmp_cap = (unsigned int)cap;
 			}
+			/* WINSORIZED without normalisation: the slow columns (a zero or a 65535 sample) leave their
+			 * tiles for k_hist_slow (SG_WINS_EXPORT), up to a quarter of the launch's pixels */
+			const bool wexp = rj == 4 && norm == 0 && ni == 1 && !linfit_fast && ctx->knobs.wins_export;
+			if (wexp) {
+				const size_t cap = ((npix_launch / 4 + 63) / 64) * 64;
+				HIPCHK(ensure(sb.wx, cap * (SG_HIST_HROWS + 3) * sizeof(uint32_t)));
+				p.wx = (uint32_t *)sb.wx.p;
+				p.wx_cap = (unsigned int)cap;
+				p.wx_count = p.flag_count + 6;	/* cleared with the counters */
+				st.exported_pixels = cap;	/* the capacity; clamped to the count when folded */
+			}
 			const dim3 hg((unsigned)nblk_h), hb((unsigned)sgh_block_threads(ni, rj));
 			if (linfit_fast) {
 				/* one workgroup per 64 pixels of a row, the tile's columns in LDS */
@@ -900,6 +914,10 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 			default: return set_err(ctx, SG_ERR_GENERIC, "no histogram kernel for this case%s%.0ld", "", 0);
 			}
 			HIPCHK(hipGetLastError());
+			if (wexp) {	/* the exported columns, before anything reads the redo list */
+				hipLaunchKernelGGL(k_hist_slow, dim3(3072), dim3(64), 0, s, p, redo_count, redo_list);	/* 12 waves per CU (153 VGPRs) */
+				HIPCHK(hipGetLastError());
+			}
 			HIPCHK(hipEventRecord(cev[1], s));
 			if (int rc = to_tail())
 				return rc;
@@ -1576,6 +1594,7 @@ extern "C" int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *d, sg_read_region_
 			agg.slow_pixels += s.slow_pixels;
 			agg.chain_pixels += s.chain_pixels;
 			agg.compact_pixels += s.compact_pixels;
+			agg.exported_pixels += s.exported_pixels;
 			agg.launches += s.launches;
 			agg.main_kernel_blocks += s.main_kernel_blocks;
 			agg.path = s.path;

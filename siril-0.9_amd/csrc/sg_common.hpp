@@ -25,6 +25,10 @@ enum { SG_CLS_OK = 0, SG_CLS_LITERAL = 1, SG_CLS_CHAIN = 2, SG_CLS_DONE = 3,
 #define SG_REPLAY_MAXN 2048
 #define SG_REDO_REPLAY_MAX 32768	/* histogram redo pixels sent straight to k_stack_replay (measured: 22 k faster there, 113 k slower) */
 
+/* dwords per pixel column of the histogram kernels' LDS histogram: 64 band dwords (256 u8 bins)
+ * and the out-of-band count (sg_stack_hist.hip SGH_HROWS) */
+#define SG_HIST_HROWS 65
+
 /* everything the stacking kernels need, passed by value */
 struct SgStackParams {
 	const uint16_t *frames;
@@ -79,6 +83,14 @@ struct SgStackParams {
 	const unsigned int *rp_list, *rp_count;
 	unsigned int rp_maxn;
 	const double *linfit_tab;		/* LINEARFIT: gsl_fit_linear's m_x, m_dx2 per N (k_linfit_tables) */
+	/* histogram WINSORIZED without normalisation (SG_WINS_EXPORT): the tile exports the columns that
+	 * hold a zero or a 65535 sample (the slow Winsorize pixels) instead of finishing them, and
+	 * k_hist_slow finishes them in waves of their own: wx[j * wx_cap + slot], rows j < SGH_HROWS the
+	 * column's histogram dwords, then lo, nz | ns << 16, the pixel index; wx_count (device) the slots
+	 * taken (null wx: every column finished in its tile) */
+	uint32_t *wx;				/* [SG_HIST_HROWS + 3][wx_cap] */
+	unsigned int wx_cap;
+	unsigned int *wx_count;
 	uint32_t *sum_buf;			/* SUM: raw sums [C][H][W] */
 	unsigned int *maxim;			/* SUM: global max of sums */
 };

@@ -36,7 +36,7 @@ struct SgReader {
  * once the call two back has been folded).  Synchronous calls use slot 0. */
 struct SgSlot {
 	SgBuf inb;		/* the call's inputs (shift table, normalisation pairs, chain tables) */
-	SgBuf flag_list, flag_map, redo, cmp_cols, cmp_list, scratch, lin_tab;
+	SgBuf flag_list, flag_map, redo, cmp_cols, cmp_list, scratch, lin_tab, wx;
 	/* pinned, host-mapped staging of the inputs (k_stage_copy reads it); stage_ev marks the copy
 	 * done before the host block is rewritten */
 	void *stage_h = nullptr, *stage_d = nullptr;
@@ -147,6 +147,7 @@ struct SgKnobs {
 	int reg_rpw = 8;		/* SG_REG_RPW: rows per wave of the wave-level forward row pass (the next row fetched during this one's transform) */
 	int reg_qafter = 0;		/* SG_REG_QAFTER: 1 = the quality estimate queued after the first batch's forward rows (beside the column pass) */
 	int linfit_waves = 8;		/* SG_LINFIT_WAVES: waves per 64-pixel k_stack_linfit tile (4, 8 or 16 (KM = 8)) */
+	int wins_export = 0;		/* SG_WINS_EXPORT: histogram WINSORIZED (no normalisation) exports its slow columns to k_hist_slow */
 	int linfit_pair = 0;		/* SG_LINFIT_PAIR: 1 = both pixels of a sorted pair through one lockstep pass loop (lfx_pixel2_m) */
 	int linfit_fast = 1;		/* SG_LINFIT_FAST: 1 = LINEARFIT through the decision-exact k_stack_linfit (16 <= N <= 1024), redo pixels to the sorted kernel; 0 = every pixel through the sorted kernel */
 	int qgrad_stream = 1;		/* SG_QGRAD_STREAM: 1 = the quality gradient streamed down 60-column bands (k_quality_grad_s), 0 = tiled */
@@ -196,6 +197,7 @@ struct SgKnobs {
 		linfit_fast = sg_env_int("SG_LINFIT_FAST", 0, 1, 1);
 		linfit_waves = sg_env_int("SG_LINFIT_WAVES", 4, 16, 8);
 		linfit_pair = sg_env_int("SG_LINFIT_PAIR", 0, 1, 0);
+		wins_export = sg_env_int("SG_WINS_EXPORT", 0, 1, 0);
 		reg_qafter = sg_env_int("SG_REG_QAFTER", 0, 1, 0);
 		reg_rpw = sg_env_int("SG_REG_RPW", 1, 64, 8);
 	}

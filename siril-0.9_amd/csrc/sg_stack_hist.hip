@@ -91,6 +91,7 @@ typedef unsigned short sgh_u16x2 __attribute__((ext_vector_type(2)));
  *   h[half][64][l]               : samples outside the band (u32: zeros, 65535s; anything
  *                                  else sends the pixel to the redo list) */
 #define SGH_HROWS (SGH_DW + 1)
+static_assert(SGH_HROWS == SG_HIST_HROWS, "sg_common.hpp's column size");
 #define SGH_OVK 4	/* out-of-band sample values captured per column (normalised stacks) */
 template <int NI>
 struct alignas(16) SghLds {
@@ -1690,8 +1691,8 @@ __device__ __forceinline__ void sgh_compact(const SgStackParams &p, const SghLds
 /* pixel column `col` of the tile (x its image column); PAIR: lane pair half `half`, else one
  * lane per column (half = 0); CAP: normalised SIGMA / WINSORIZED kernel (captured out-of-band
  * values, sgh_compact) */
-template <int REJ, bool PAIR, int NI, bool ZT = false, bool CAP = false>
-__device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int half, int lo, int R, int c, int x,
+template <int REJ, bool PAIR, int NI, bool ZT = false, bool CAP = false, class LT = SghLds<NI>>
+__device__ void sgh_finish2(const SgStackParams &p, LT &L, int col, int half, int lo, int R, int c, int x,
 		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list, bool zrow = false) {
 	const int lane = threadIdx.x & 63;
 	const int N = p.N;
@@ -1814,9 +1815,11 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 		} else if (P.nb + oob != N || (zc && zmax >= lo) || (REJ != 1 && REJ != 8 && oob != P.nz + P.ns + zc)) {
 			cls = 1;	/* out-of-band sample other than 0 / 65535 (or than this row's normalised
 				 * zeros), or a wrapped u8 counter */
-			if (CAP && p.cmp_cols) {	/* every sample known: no wrap, no row zeros, all captured */
-				const int k = oob - P.nz - P.ns;
-				cmp = P.nb + oob == N && zc == 0 && k > 0 && k <= SGH_OVK && (int)L.ovn[col] == k;
+			if constexpr (CAP) {
+				if (p.cmp_cols) {	/* every sample known: no wrap, no row zeros, all captured */
+					const int k = oob - P.nz - P.ns;
+					cmp = P.nb + oob == N && zc == 0 && k > 0 && k <= SGH_OVK && (int)L.ovn[col] == k;
+				}
 			}
 		} else {
 			const long long dz = -(long long)lo, ds = 65535 - (long long)lo;
@@ -1910,7 +1913,7 @@ __device__ void sgh_finish2(const SgStackParams &p, SghLds<NI> &L, int col, int 
 		}
 	}
 #endif
-	if (CAP)
+	if constexpr (CAP)
 		sgh_compact<NI>(p, L, cmp && !half && x < p.W, col, lo, (unsigned int)(((int64_t)c * p.H + R) * p.W + x),
 				P.nz, P.ns, oob - P.nz - P.ns, redo_count, redo_list);
 	const unsigned long long a = sgh_wave_sum(rlo), b = sgh_wave_sum(rhi);
@@ -2379,6 +2382,39 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 		 * ~3 (scripts/wins_predict.py, profiles/r02z_wins_predict.log), so those columns are
 		 * finished by wave 0 first and the rest after them (the sum of the two waves' maxima
 		 * 26.4 -> 21.5 iterations per tile on configs[4]'s data) */
+		if (NORM == 0 && NI == 1 && p.wx) {
+			/* SG_WINS_EXPORT: a column holding a zero or a 65535 sample needs ~10 inner iterations
+			 * against ~3 and holds its wave for them; it leaves the tile as its histogram (a slot per
+			 * column, one atomic per wave) and k_hist_slow finishes it among columns of its own kind.
+			 * The tile's waves finish the rest (a column without a slot is finished here) */
+			if (wave >= 2)
+				return;
+			const int col = 64 * wave + lane;
+			const int x = col_x(col);
+			const bool slow = x < p.W && (L.nz[col] | L.ns[col]) != 0u;
+			const uint64_t m = __ballot(slow);
+			unsigned int base = 0;
+			if (m) {
+				if (lane == 0)
+					base = atomicAdd(p.wx_count, (unsigned int)__popcll(m));
+				base = (unsigned int)__builtin_amdgcn_readfirstlane((int)base);
+			}
+			const unsigned int slot = base + (unsigned int)__popcll(m & ((1ull << lane) - 1ull));
+			const bool out = slow && slot < p.wx_cap;
+			if (out) {
+				const uint32_t *hc = &L.h[col >> 6][0][col & 63];
+				const size_t cap = p.wx_cap;
+#pragma unroll 5
+				for (int j = 0; j < SGH_HROWS; j++)
+					p.wx[(size_t)j * cap + slot] = hc[64 * j];
+				p.wx[(size_t)SGH_HROWS * cap + slot] = (uint32_t)col_lo(col);
+				p.wx[(size_t)(SGH_HROWS + 1) * cap + slot] = L.nz[col] | (L.ns[col] << 16);
+				p.wx[(size_t)(SGH_HROWS + 2) * cap + slot] = (uint32_t)(((int64_t)c * p.H + R) * p.W + x);
+			}
+			sgh_finish2<REJ, false, NI, false, false>(p, L, col, 0, col_lo(col), R, c, out ? p.W : x, redo_count,
+					redo_list);
+			return;
+		}
 		if (SGH_WINS_ORDER && NI == 1) {
 			if (wave == 0) {
 				const int ca = lane, cb = 64 + lane;
@@ -2450,6 +2486,44 @@ k_stack_hist(SgStackParams p, const int *__restrict__ tab, const int4 *__restric
 	 * (scripts/gpu_r3p.sh; the tile loop also costs registers: 128 VGPRs + scratch) */
 	if (vb < ntiles)
 		sgh_tile<REJ, NORM, NI>(p, ro, L, vb, false, redo_count, redo_list);
+}
+
+/* k_hist_slow: the exported WINSORIZED columns (SgStackParams::wx), 64 per wave, each lane's
+ * histogram column back in LDS in the tile's layout, finished by the tile's own code (sgh_finish2:
+ * the same queries, decisions, redo list and counters).  Waves of exported columns only: their
+ * inner-iteration counts are alike, and no build shares the CU's LDS with them. */
+struct SghSlowLds {
+	uint32_t h[1][SGH_HROWS][64];
+	uint32_t nz[64], ns[64], na[64];
+};
+#ifndef SGH_SLOW_WPE
+#define SGH_SLOW_WPE 2
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SGH_SLOW_WPE)))
+k_hist_slow(SgStackParams p, unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
+	__shared__ SghSlowLds L;
+	const int lane = threadIdx.x & 63;
+	const unsigned int cnt = *(volatile const unsigned int *)p.wx_count;
+	const unsigned int n = cnt < p.wx_cap ? cnt : p.wx_cap;
+	const size_t cap = p.wx_cap;
+	for (unsigned int s0 = blockIdx.x * 64u; s0 < n; s0 += gridDim.x * 64u) {
+		const unsigned int slot = s0 + (unsigned int)lane;
+		const bool v = slot < n;
+#pragma unroll 5
+		for (int j = 0; j < SGH_HROWS; j++)
+			L.h[0][j][lane] = v ? p.wx[(size_t)j * cap + slot] : 0u;
+		const uint32_t lo = v ? p.wx[(size_t)SGH_HROWS * cap + slot] : 1u;
+		const uint32_t zs = v ? p.wx[(size_t)(SGH_HROWS + 1) * cap + slot] : 0u;
+		const uint32_t pix = v ? p.wx[(size_t)(SGH_HROWS + 2) * cap + slot] : 0u;
+		L.nz[lane] = zs & 0xFFFFu;
+		L.ns[lane] = zs >> 16;
+		L.na[lane] = 0u;
+		const uint32_t W = (uint32_t)p.W, t = pix / W;
+		const int x = v ? (int)(pix - t * W) : p.W;
+		const int R = (int)(t % (uint32_t)p.H), c = (int)(t / (uint32_t)p.H);
+		/* each lane reads only its own column: no barrier */
+		sgh_finish2<4, false, 1, false, false, SghSlowLds>(p, L, lane, 0, (int)lo, R, c, x, redo_count, redo_list);
+	}
 }
 
 template __global__ void k_stack_hist<2, 0, 1>(SgStackParams, const int *, const int4 *, unsigned int *,

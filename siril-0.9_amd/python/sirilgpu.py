@@ -62,6 +62,7 @@ class StackStats(ctypes.Structure):
         ("reg_fp64_reruns", ctypes.c_uint64),
         ("compact_pixels", ctypes.c_uint64),
         ("reg_ms", ctypes.c_double),
+        ("exported_pixels", ctypes.c_uint64),
     ]
 
 

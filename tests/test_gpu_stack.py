@@ -3,6 +3,8 @@
 Bit-exact for every output pixel and the rejection counters (integer/median paths and the
 mean/sigma-clip paths alike: the kernels replay the reference's decisions exactly).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -667,3 +669,35 @@ def test_block_overflow_shift_refused(gpu_ctx):
     assert rc == 0
     out, rej, _ = gpu_stack(gpu_ctx, frames, sg.MEAN, sg.SIGMA, shiftx=sx, shifty=sy, max_thread=4)
     assert_same(out, ref, "shift below the block height")
+
+
+def _export_ctx():
+    """a context with SG_WINS_EXPORT=1 (the knob is read when the context opens)"""
+    old = os.environ.get("SG_WINS_EXPORT")
+    os.environ["SG_WINS_EXPORT"] = "1"
+    try:
+        return sg.Context([0])
+    finally:
+        if old is None:
+            del os.environ["SG_WINS_EXPORT"]
+        else:
+            os.environ["SG_WINS_EXPORT"] = old
+
+
+@pytest.mark.parametrize("N,H,W,M", [(16, 48, 200, 3), (40, 64, 300, 10), (256, 40, 384, 6), (96, 72, 260, 12)])
+def test_wins_export_matches_oracle(N, H, W, M):
+    """WINSORIZED with the slow columns exported from their tiles and finished by k_hist_slow
+    (SG_WINS_EXPORT): image and counters == the oracle and == the in-tile finish.  The synthetic
+    frames hold cosmics (65535) and dead pixels (0), and the shifted border rows zeros, so many
+    columns are exported; at M = 10 / 12 more than a quarter of the columns are slow and the slot
+    pool (a quarter of the pixels) overflows, so the columns beyond it finish in their tiles"""
+    frames = orc.synth(N, 1, H, W, seed=900 + N, maxshift=M)
+    sx, sy = orc.synth_shifts(N, seed=900 + N, maxshift=M)
+    rc, ref, rej_ref = orc.stack_rejection(frames, sg.WINSORIZED, sig=(4.0, 3.0), shiftx=sx, shifty=sy, max_thread=2)
+    assert rc == 0
+    with _export_ctx() as ctx:
+        out_x, rej_x, st = _stack_path(ctx, frames, sg.WINSORIZED, (4.0, 3.0), sx, sy, max_thread=2)
+    assert st.exported_pixels > 0, "no column was exported"
+    assert st.exported_pixels <= (H * W // 4 + 63) // 64 * 64
+    assert_same(out_x, ref, f"exported N={N}")
+    assert np.array_equal(rej_x, rej_ref), (rej_x, rej_ref)
