@@ -1179,12 +1179,13 @@ k_stack_reduce3(SgStackParams p, const int *__restrict__ tab, const int *__restr
 	for (int k = 0; k < SEG; k++)
 		acc_a[k] = acc_b[k] = M == 4 ? 65535u : 0u;
 	const bool interior = x0 > p.hist_maxsx && x0 + PXW + p.hist_maxsx <= p.W;
-	/* image-edge segments of SUM, MEAN (no normalisation) and MAX also stream: a lane sample whose
-	 * shifted column leaves the image is masked to 0 per frame (the reference skips it: for these
-	 * reductions a skipped sample and a 0 are the same), and so is source pixel 0 for SUM / MAX
-	 * (round 6: the general loop serialised its 16-frame batches, and 2 of every 16 waves of a
-	 * 2048-wide image took it) */
-	const bool edge_fast = !interior && p.use_shift && x0 + PXW <= p.W && (M == 0 || M == 1 || M == 3);
+	/* image-edge segments of MEAN (no normalisation), MAX and (right edge) SUM also stream: a lane
+	 * sample whose shifted column leaves the image is masked to 0 per frame (the reference skips it:
+	 * for these reductions a skipped sample and a 0 are the same), the load itself stays inside the
+	 * plane's bounds check (round 6: the general loop serialised its 16-frame batches, and 2 of
+	 * every 16 waves of a 2048-wide image took it) */
+	const bool edge_fast = !interior && p.use_shift && x0 + PXW <= p.W &&
+		(M == 1 || M == 3 || (M == 0 && x0 > p.hist_maxsx));
 	if (!interior && !edge_fast) {
 #pragma unroll
 		for (int k = 0; k < SEG; k++) {
@@ -1220,24 +1221,10 @@ k_stack_reduce3(SgStackParams p, const int *__restrict__ tab, const int *__restr
 		for (int m = 0; m < MB; m++) {
 			const uint32_t n = f0 + m < N ? nrec : 0u;
 #pragma unroll
-			for (int k = 0; k < SEG; k++) {
-				if (edge_fast) {
-					/* per-lane offsets: a negative SGPR offset would put the whole wave's load out of
-					 * range (gfx950 adds voffset + soffset without wrapping), and a pair straddling the
-					 * row's first or last column is read as the dword inside the row (sg_reduce_pairs'
-					 * rule), moved back into place in accb; rows outside the frame read nothing */
-					const int f = f0 + m;
-					const int ny = R - shifty[f], nx = x0 + 128 * k + 2 * lane - sxt[f];
-					const int lx = nx < 0 ? nx + 1 : (nx + 1 >= p.W ? nx - 1 : nx);
-					const int off = (unsigned)ny < (unsigned)p.H && lx >= 0 ? (ny * p.W + lx) * 2 : (int)0x80000000;
-					v[m][k] = __builtin_amdgcn_raw_buffer_load_b32(
-							sg_plane_rsrc((const uint16_t *)(fb + (int64_t)m * fstride2), n), off, 0, 0);
-				} else {
-					v[m][k] = __builtin_amdgcn_raw_buffer_load_b32(
-							sg_plane_rsrc((const uint16_t *)(fb + (int64_t)m * fstride2), n), vofs + 256 * k,
-							rowb - c1[m], 0);
-				}
-			}
+			for (int k = 0; k < SEG; k++)
+				v[m][k] = __builtin_amdgcn_raw_buffer_load_b32(
+						sg_plane_rsrc((const uint16_t *)(fb + (int64_t)m * fstride2), n), vofs + 256 * k,
+						rowb - c1[m], 0);
 		}
 	};
 	auto accb = [&](int f0, const uint32_t (&v)[MB][SEG], bool full) {
@@ -1256,14 +1243,8 @@ k_stack_reduce3(SgStackParams p, const int *__restrict__ tab, const int *__restr
 				uint32_t vv = v[m][k];
 				if (edge_fast) {	/* the lane's two source columns x - sx, x + 1 - sx inside the image */
 					const int xs = x0 + 128 * k + 2 * lane - sxt[f];
-					vv = xs < 0 ? vv << 16 : (xs + 1 >= p.W ? vv >> 16 : vv);	/* loadb's moved dword */
 					vv &= ((unsigned)xs < (unsigned)p.W ? 0x0000FFFFu : 0u) |
 						((unsigned)(xs + 1) < (unsigned)p.W ? 0xFFFF0000u : 0u);
-					/* SUM / MAX: source pixel 0 is never used (the `ii > 0` of :307, :880) */
-					if (M == 0 || M == 3) {
-						const bool p0 = R - shifty[f] == 0;
-						vv &= (p0 && xs == 0 ? 0xFFFF0000u : 0xFFFFFFFFu) & (p0 && xs + 1 == 0 ? 0x0000FFFFu : 0xFFFFFFFFu);
-					}
 				}
 				const uint32_t a = vv & 0xFFFFu, b = vv >> 16;
 				if (M == 0 || M == 1) {	/* SUM; MEAN without normalisation: the sum (the divisor is N) */
