@@ -1179,14 +1179,7 @@ k_stack_reduce3(SgStackParams p, const int *__restrict__ tab, const int *__restr
 	for (int k = 0; k < SEG; k++)
 		acc_a[k] = acc_b[k] = M == 4 ? 65535u : 0u;
 	const bool interior = x0 > p.hist_maxsx && x0 + PXW + p.hist_maxsx <= p.W;
-	/* image-edge segments of MEAN (no normalisation), MAX and (right edge) SUM also stream: a lane
-	 * sample whose shifted column leaves the image is masked to 0 per frame (the reference skips it:
-	 * for these reductions a skipped sample and a 0 are the same), the load itself stays inside the
-	 * plane's bounds check (round 6: the general loop serialised its 16-frame batches, and 2 of
-	 * every 16 waves of a 2048-wide image took it) */
-	const bool edge_fast = !interior && p.use_shift && x0 + PXW <= p.W &&
-		(M == 1 || M == 3 || (M == 0 && x0 > p.hist_maxsx));
-	if (!interior && !edge_fast) {
+	if (!interior) {
 #pragma unroll
 		for (int k = 0; k < SEG; k++) {
 			const int x = x0 + 128 * k + 2 * lane;
@@ -1200,8 +1193,6 @@ k_stack_reduce3(SgStackParams p, const int *__restrict__ tab, const int *__restr
 	const uint32_t nrec = (uint32_t)p.H * (uint32_t)p.W * 2u;
 	const int rowb = (R * p.W + x0) * 2;
 	const int vofs = lane * 4;
-	/* the call's shiftx, behind c1 and the int16 table in the same input block (scalar loads) */
-	const int *sxt = tab + p.hist_npad + p.hist_npad / 2;
 	uint32_t mm[SEG];	/* MAX / MIN: both pixels packed */
 #pragma unroll
 	for (int k = 0; k < SEG; k++)
@@ -1240,13 +1231,7 @@ k_stack_reduce3(SgStackParams p, const int *__restrict__ tab, const int *__restr
 				sy = p.use_shift ? __builtin_amdgcn_readlane(vsy, (f0 & 63) + m) : 0;
 #pragma unroll
 			for (int k = 0; k < SEG; k++) {
-				uint32_t vv = v[m][k];
-				if (edge_fast) {	/* the lane's two source columns x - sx, x + 1 - sx inside the image */
-					const int xs = x0 + 128 * k + 2 * lane - sxt[f];
-					vv &= ((unsigned)xs < (unsigned)p.W ? 0x0000FFFFu : 0u) |
-						((unsigned)(xs + 1) < (unsigned)p.W ? 0xFFFF0000u : 0u);
-				}
-				const uint32_t a = vv & 0xFFFFu, b = vv >> 16;
+				const uint32_t a = v[m][k] & 0xFFFFu, b = v[m][k] >> 16;
 				if (M == 0 || M == 1) {	/* SUM; MEAN without normalisation: the sum (the divisor is N) */
 					acc_a[k] += a;
 					acc_b[k] += b;
@@ -1255,7 +1240,7 @@ k_stack_reduce3(SgStackParams p, const int *__restrict__ tab, const int *__restr
 					acc_b[k] += sg_normalize(p, f, (uint16_t)b);
 				} else if (M == 3) {
 					mm[k] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(sg_u16x2, mm[k]),
-							__builtin_bit_cast(sg_u16x2, vv)));
+							__builtin_bit_cast(sg_u16x2, v[m][k])));
 				} else if ((unsigned)(R - sy) < (unsigned)p.H) {
 					mm[k] = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(sg_u16x2, mm[k]),
 							__builtin_bit_cast(sg_u16x2, v[m][k])));
