@@ -863,6 +863,7 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 				p.wx = (uint32_t *)sb.wx.p;
 				p.wx_cap = (unsigned int)cap;
 				p.wx_count = p.flag_count + 6;	/* cleared with the counters */
+				p.wx_kmax = ctx->knobs.wins_export;
 				st.exported_pixels = cap;	/* the capacity; clamped to the count when folded */
 			}
 			const dim3 hg((unsigned)nblk_h), hb((unsigned)sgh_block_threads(ni, rj));

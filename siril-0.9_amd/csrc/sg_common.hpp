@@ -91,6 +91,8 @@ struct SgStackParams {
 	uint32_t *wx;				/* [SG_HIST_HROWS + 3][wx_cap] */
 	unsigned int wx_cap;
 	unsigned int *wx_count;
+	int wx_kmax;				/* export a column with 1 .. wx_kmax zero / 65535 samples (more: the rows a
+						 * registration shift empties, whose tiles are slow throughout: finished there) */
 	uint32_t *sum_buf;			/* SUM: raw sums [C][H][W] */
 	unsigned int *maxim;			/* SUM: global max of sums */
 };

@@ -147,7 +147,7 @@ struct SgKnobs {
 	int reg_rpw = 8;		/* SG_REG_RPW: rows per wave of the wave-level forward row pass (the next row fetched during this one's transform) */
 	int reg_qafter = 0;		/* SG_REG_QAFTER: 1 = the quality estimate queued after the first batch's forward rows (beside the column pass) */
 	int linfit_waves = 8;		/* SG_LINFIT_WAVES: waves per 64-pixel k_stack_linfit tile (4, 8 or 16 (KM = 8)) */
-	int wins_export = 0;		/* SG_WINS_EXPORT: histogram WINSORIZED (no normalisation) exports its slow columns to k_hist_slow */
+	int wins_export = 0;		/* SG_WINS_EXPORT = k > 0: histogram WINSORIZED (no normalisation) exports its columns holding 1 .. k zero / 65535 samples to k_hist_slow */
 	int linfit_pair = 0;		/* SG_LINFIT_PAIR: 1 = both pixels of a sorted pair through one lockstep pass loop (lfx_pixel2_m) */
 	int linfit_fast = 1;		/* SG_LINFIT_FAST: 1 = LINEARFIT through the decision-exact k_stack_linfit (16 <= N <= 1024), redo pixels to the sorted kernel; 0 = every pixel through the sorted kernel */
 	int qgrad_stream = 1;		/* SG_QGRAD_STREAM: 1 = the quality gradient streamed down 60-column bands (k_quality_grad_s), 0 = tiled */
@@ -197,7 +197,7 @@ struct SgKnobs {
 		linfit_fast = sg_env_int("SG_LINFIT_FAST", 0, 1, 1);
 		linfit_waves = sg_env_int("SG_LINFIT_WAVES", 4, 16, 8);
 		linfit_pair = sg_env_int("SG_LINFIT_PAIR", 0, 1, 0);
-		wins_export = sg_env_int("SG_WINS_EXPORT", 0, 1, 0);
+		wins_export = sg_env_int("SG_WINS_EXPORT", 0, 65535, 0);
 		reg_qafter = sg_env_int("SG_REG_QAFTER", 0, 1, 0);
 		reg_rpw = sg_env_int("SG_REG_RPW", 1, 64, 8);
 	}

@@ -2391,7 +2391,8 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 				return;
 			const int col = 64 * wave + lane;
 			const int x = col_x(col);
-			const bool slow = x < p.W && (L.nz[col] | L.ns[col]) != 0u;
+			const uint32_t nout = L.nz[col] + L.ns[col];
+			const bool slow = x < p.W && nout != 0u && nout <= (uint32_t)p.wx_kmax;
 			const uint64_t m = __ballot(slow);
 			unsigned int base = 0;
 			if (m) {
