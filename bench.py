@@ -728,9 +728,12 @@ def main_config(args):
     # section 2, Registration): per pair of frames the two u16 selections (4 S^2), the pair plane
     # written and read back by the column pass (8 + 8 S^2), the reference's half spectrum (4 S^2),
     # the column pass's output read by the inverse rows (8 + 8 S^2): 40 S^2 per pair = 20 S^2 per
-    # frame, plus the quality estimate's read of the selection (2 S^2); the measured PMC bytes are
-    # the traffic
-    reg_algo = nsel * S * S * 22
+    # frame, plus the quality estimate's read of the selection (2 S^2; at S = 2048 the forward rows
+    # subsample the selections they read (SG_REG_QFOLD, default on), so the estimate adds only its
+    # subsampled frames written and read back, 2 x 2 (S / 3)^2 = 4/9 S^2); the measured PMC bytes
+    # are the traffic
+    qfold = S == 2048 and int(os.environ.get("SG_REG_QFOLD", "12")) >= 3
+    reg_algo = int(nsel * S * S * (20 + 4 / 9 if qfold else 22))
     reg_ms = sum(reg_spans) / len(reg_spans) if reg_spans else stage[1] * 1e3
     tpath = os.path.join(ROOT, "profiles", f"traffic_register_{N}x{S}.json")
     reg_tinfo = {}
@@ -762,7 +765,9 @@ def main_config(args):
                                         "rows + arg-max, quality estimate)",
               "achieved": round(reg_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
               "frac": round(reg_ach / HBM_PEAK_GBS, 4), "algorithmic_bytes": int(reg_algo),
-              "algorithmic_model": "22 S^2 per frame (DESIGN.md: 20 S^2 FFT passes + 2 S^2 quality)",
+              "algorithmic_model": "20 4/9 S^2 per frame (DESIGN.md: 20 S^2 FFT passes + 4/9 S^2 quality, subsample "
+                                   "folded into the forward rows)" if qfold else
+                                   "22 S^2 per frame (DESIGN.md: 20 S^2 FFT passes + 2 S^2 quality)",
               "traffic": None}
         # SURVEY 8(d)'s algorithmic MINIMUM: each u16 selection read once (2 S^2 per frame); the
         # passes' planes cannot stay on chip at S = 2048 (32 MiB per c64 plane), so this is a floor

@@ -146,6 +146,7 @@ struct SgKnobs {
 	int reg_genfuse = 1;		/* SG_REG_GENFUSE: 1 = generic sides' fused column pass (k_gen_cols_xpower), 0 = rows + k_gen_xpower + rows */
 	int reg_rpw = 8;		/* SG_REG_RPW: rows per wave of the wave-level forward row pass (the next row fetched during this one's transform) */
 	int reg_qafter = 0;		/* SG_REG_QAFTER: 1 = the quality estimate queued after the first batch's forward rows (beside the column pass) */
+	int reg_qfold = 12;		/* SG_REG_QFOLD = r (3, 6, 9 ...): QualityEstimate's 3x3 subsample folded into the wave-level forward row pass, r consecutive rows per wave (S = 2048, fp32; configs[1] registration 3.10 -> 2.95 ms, r = 6-12 equal, 24 / 48 slower, profiles/r06s_*, r06t_*); 0 = k_quality_sub */
 	int linfit_waves = 8;		/* SG_LINFIT_WAVES: waves per 64-pixel k_stack_linfit tile (4, 8 or 16 (KM = 8)) */
 	int wins_export = 0;		/* SG_WINS_EXPORT = k > 0: histogram WINSORIZED (no normalisation) exports its columns holding 1 .. k zero / 65535 samples to k_hist_slow */
 	int linfit_pair = 0;		/* SG_LINFIT_PAIR: 1 = both pixels of a sorted pair through one lockstep pass loop (lfx_pixel2_m) */
@@ -200,6 +201,7 @@ struct SgKnobs {
 		wins_export = sg_env_int("SG_WINS_EXPORT", 0, 65535, 0);
 		reg_qafter = sg_env_int("SG_REG_QAFTER", 0, 1, 0);
 		reg_rpw = sg_env_int("SG_REG_RPW", 1, 64, 8);
+		reg_qfold = sg_env_int("SG_REG_QFOLD", 0, 63, 12) / 3 * 3;
 	}
 };
 

@@ -601,13 +601,24 @@ k_reg_cols_xpower_w(float2 *__restrict__ work, const float2 *__restrict__ spec, 
  * SIMD being all the LDS allows), the row of a + i b through sg_fft2048_wave, then staged in
  * natural order in the wave's LDS for the separation into the half spectra A, B
  * (k_reg_rows_fwd_half's arithmetic); the frames' energies summed per wave */
+/* QF (SG_REG_QFOLD, A/B): QualityEstimate's SubSample (quality.c:223-234) folded in.  A wave then
+ * takes rpw consecutive rows from a multiple of 3 (rpw a multiple of 3), so each 3 x 3 block's three
+ * rows pass through one wave: before a row's transform its samples (a | b << 16) go through the
+ * wave's LDS, each lane adds the row's three-sample sums of outputs lane + 64 m (m < 11, xs = 682)
+ * to registers, and the third row of a block writes the 9-sample means to qbuf (frame q = qbase +
+ * 2 pair (+1 for b)) and keeps the middle rows' maximum for qmax (k_quality_sub's arithmetic). */
+template <bool QF>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SG_WCOL_WPE)))
 k_reg_rows_fwd_half_w(SgSel sel, const int *__restrict__ fa, const int *__restrict__ fb,
-		const float2 *__restrict__ tw, float2 *__restrict__ work, unsigned long long *__restrict__ energy, int rpw) {
+		const float2 *__restrict__ tw, float2 *__restrict__ work, unsigned long long *__restrict__ energy, int rpw,
+		uint16_t *__restrict__ qbuf, unsigned int *__restrict__ qmax, int qbase) {
 	constexpr int S = 2048, H = 1024, P = 32;
+	constexpr int XS = (S - 1) / 3, YS = (S - 1) / 3, QM = (XS + 63) / 64;
 	extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 	const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-	const int row0 = blockIdx.x * 4 * rpw + wave, pair = blockIdx.y;
+	const int row0 = QF ? (blockIdx.x * 4 + wave) * rpw : blockIdx.x * 4 * rpw + wave, pair = blockIdx.y;
+	if (QF && row0 >= S)
+		return;
 	float2 *col = (float2 *)smem + wave * SG_WCOL_CS;
 	const size_t plane = (size_t)S * S;
 	const uint16_t *pa = sel.frame(fa[pair]);
@@ -628,8 +639,35 @@ k_reg_rows_fwd_half_w(SgSel sel, const int *__restrict__ fa, const int *__restri
 	fetch(row0);
 	unsigned long long ea = 0, eb = 0;
 	const int km = lane >> 1, hm = lane & 1;
+	uint32_t qa[QM], qb[QM], mxa = 0, mxb = 0;
+	if constexpr (QF) {
+#pragma unroll
+		for (int m = 0; m < QM; m++)
+			qa[m] = qb[m] = 0;
+	}
 	for (int rr = 0; rr < rpw; rr++) {
-		const int row = row0 + 4 * rr;
+		const int row = QF ? row0 + rr : row0 + 4 * rr;
+		if (QF && row >= S)
+			break;
+		if constexpr (QF) {	/* the row's samples through LDS, its three-sample sums added */
+			uint32_t *cu = (uint32_t *)col;
+			if (row < 3 * YS) {
+#pragma unroll
+				for (int j = 0; j < P; j++)
+					cu[64 * j + lane] = (uint32_t)ua[j] | ((uint32_t)(pb ? ub[j] : 0) << 16);
+				__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+				for (int m = 0; m < QM; m++) {
+					const int i = 64 * m + lane;
+					if (i < XS) {
+						const uint32_t d0 = cu[3 * i], d1 = cu[3 * i + 1], d2 = cu[3 * i + 2];
+						qa[m] += (d0 & 0xFFFFu) + (d1 & 0xFFFFu) + (d2 & 0xFFFFu);
+						qb[m] += (d0 >> 16) + (d1 >> 16) + (d2 >> 16);
+					}
+				}
+				__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");	/* the transform reuses col */
+			}
+		}
 		float2 v[P];
 #pragma unroll
 		for (int j = 0; j < P; j++) {
@@ -645,8 +683,31 @@ k_reg_rows_fwd_half_w(SgSel sel, const int *__restrict__ fa, const int *__restri
 				v[j].y = (float)u;
 			}
 		}
-		if (rr + 1 < rpw)
-			fetch(row + 4);
+		if (QF ? (rr + 1 < rpw && row + 1 < S) : rr + 1 < rpw)
+			fetch(QF ? row + 1 : row + 4);
+		if constexpr (QF) {	/* a block's third row: the 9-sample means (SubSample, :223-234) */
+			if (row % 3 == 2 && row < 3 * YS) {
+				const int t = row / 3;
+				const bool middle = t >= 1 && t <= YS - 2;
+				uint16_t *da = qbuf + (size_t)(qbase + 2 * pair) * XS * YS + (size_t)t * XS;
+#pragma unroll
+				for (int m = 0; m < QM; m++) {
+					const int i = 64 * m + lane;
+					const uint32_t va = qa[m] / 9u, vb = qb[m] / 9u;
+					if (i < XS) {
+						da[i] = (uint16_t)va;
+						if (middle && va > 0 && va < 65530 && va > mxa)
+							mxa = va;
+						if (pb) {
+							da[(size_t)XS * YS + i] = (uint16_t)vb;
+							if (middle && vb > 0 && vb < 65530 && vb > mxb)
+								mxb = vb;
+						}
+					}
+					qa[m] = qb[m] = 0;
+				}
+			}
+		}
 		sg_fft2048_wave<false>(v, col, tw, lane);
 		__builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 		/* natural order, the upper half 8 entries up: lanes km and km + 8 (hm = 0 / 1) of a
@@ -681,6 +742,17 @@ k_reg_rows_fwd_half_w(SgSel sel, const int *__restrict__ fa, const int *__restri
 		atomicAdd(energy + fa[pair], ea);
 		if (b >= 0)
 			atomicAdd(energy + b, eb);
+	}
+	if constexpr (QF) {
+		for (int o = 32; o > 0; o >>= 1) {
+			const uint32_t ta = (uint32_t)__shfl_xor((int)mxa, o, 64), tb = (uint32_t)__shfl_xor((int)mxb, o, 64);
+			mxa = ta > mxa ? ta : mxa;
+			mxb = tb > mxb ? tb : mxb;
+		}
+		if (lane == 0 && mxa)
+			atomicMax(qmax + qbase + 2 * pair, mxa);
+		if (lane == 0 && mxb)
+			atomicMax(qmax + qbase + 2 * pair + 1, mxb);
 	}
 }
 
@@ -1594,13 +1666,15 @@ k_reg_resolve(const SgCand *__restrict__ cand, int S, int np, SgRegOut *__restri
  * already on `s`, which produced d_sel) so that it runs beside the FFT passes: its kernels are
  * short and the passes leave the chip latency-bound.  reg_quality_finish waits for the sums and
  * forms the values; *launched = false when the subsample loop never runs (dval = 0, :95-98). */
-static int reg_quality_launch(sg_ctx *ctx, SgDevice &dv, hipStream_t s, SgSel d_sel, int S,
-		const std::vector<int> &frames, bool *launched) {
-	*launched = false;
-	const int nq = (int)frames.size();
-	const int xs = (S - 1) / 3, ys = (S - 1) / 3;
-	if (!nq || xs < 2 || ys < 2)
-		return SG_OK;
+/* the estimate's buffers: qbuf (nq subsampled frames, then the frame list), acc [nq][3] + qmax [nq] */
+struct SgQBufs {
+	uint16_t *qbuf;
+	int *frames;
+	unsigned long long *acc;
+	unsigned int *qmax;
+};
+
+static int reg_quality_buffers(sg_ctx *ctx, SgDevice &dv, int nq, int xs, int ys, SgQBufs &qb) {
 	if (!dv.aux) {
 		HIPCHK(hipStreamCreateWithFlags(&dv.aux, hipStreamNonBlocking));
 		for (int k = 0; k < 2; k++)
@@ -1618,22 +1692,16 @@ static int reg_quality_launch(sg_ctx *ctx, SgDevice &dv, hipStream_t s, SgSel d_
 	HIPCHK(hipStreamSynchronize(dv.aux));	/* the previous call's buffers are free */
 	HIPCHK(ensure(dv.reg_qbuf, (size_t)nq * xs * ys * sizeof(uint16_t) + sizeof(int) * nq + 64));
 	HIPCHK(ensure(dv.reg_qacc, (size_t)nq * (3 * sizeof(unsigned long long) + sizeof(unsigned int))));
-	uint16_t *qbuf = (uint16_t *)dv.reg_qbuf.p;
-	int *d_frames = (int *)((char *)dv.reg_qbuf.p + (((size_t)nq * xs * ys * sizeof(uint16_t) + 15) & ~(size_t)15));
-	unsigned long long *acc = (unsigned long long *)dv.reg_qacc.p;
-	unsigned int *qmax = (unsigned int *)(acc + 3 * nq);
-	HIPCHK(hipEventRecord(dv.aux_ev[1], s));
-	HIPCHK(hipStreamWaitEvent(dv.aux, dv.aux_ev[1], 0));
-	HIPCHK(hipMemcpyAsync(d_frames, frames.data(), sizeof(int) * nq, hipMemcpyHostToDevice, dv.aux));
-	HIPCHK(hipMemsetAsync(dv.reg_qacc.p, 0, (size_t)nq * (3 * sizeof(unsigned long long) + sizeof(unsigned int)), dv.aux));
-	/* one wave per workgroup, walking the row pairs: 283 us per 129 frames of 2048^2 against
-	 * 332 / 348 / 403 / 618 us with 128 / 192 / 256 / 384 threads (scripts/gpu_qsub.sh) */
-	const int qthr = ctx->knobs.qsub_threads;	/* A/B knob SG_QSUB_THREADS */
-	/* the dword loads of k_quality_sub need an even side, even pitches and a dword-aligned base */
-	const int al = !(S & 1) && !(d_sel.rp & 1) && !(d_sel.fp & 1) && !((uintptr_t)d_sel.p & 3);
-	hipLaunchKernelGGL(k_quality_sub, dim3((ys + SG_QROWS - 1) / SG_QROWS, nq), dim3(qthr), 0, dv.aux, d_sel, al, d_frames,
-			S, xs, ys, qbuf, qmax);
-	HIPCHK(hipGetLastError());
+	qb.qbuf = (uint16_t *)dv.reg_qbuf.p;
+	qb.frames = (int *)((char *)dv.reg_qbuf.p + (((size_t)nq * xs * ys * sizeof(uint16_t) + 15) & ~(size_t)15));
+	qb.acc = (unsigned long long *)dv.reg_qacc.p;
+	qb.qmax = (unsigned int *)(qb.acc + 3 * nq);
+	return SG_OK;
+}
+
+/* gradient sums of the subsampled frames on the aux stream (after the work queued on it), read
+ * back into the pinned block; aux_ev[0] marks them */
+static int reg_quality_grad(sg_ctx *ctx, SgDevice &dv, int nq, int xs, int ys, const SgQBufs &qb) {
 	/* 2 waves per 64x16 tile: 214 us per 129 frames against 238 (4 waves) and 333 (1 wave),
 	 * scripts/gpu_qgrad.sh */
 	const int gthr = ctx->knobs.qgrad_threads;	/* A/B knob SG_QGRAD_THREADS */
@@ -1642,16 +1710,47 @@ static int reg_quality_launch(sg_ctx *ctx, SgDevice &dv, hipStream_t s, SgSel d_
 		const int wi = xs - 2 * xb, hi = ys - 2 * yb;
 		if (wi > 0 && hi > 0) {
 			hipLaunchKernelGGL(k_quality_grad_s, dim3((wi + 59) / 60, (hi + SG_QGS_ROWS - 1) / SG_QGS_ROWS, nq), dim3(64),
-					0, dv.aux, qbuf, xs, ys, qmax, acc);
+					0, dv.aux, qb.qbuf, xs, ys, qb.qmax, qb.acc);
 			HIPCHK(hipGetLastError());
 		}
 	} else {
-		hipLaunchKernelGGL(k_quality_grad, dim3((xs + 63) / 64, (ys + SG_QGT - 1) / SG_QGT, nq), dim3(gthr), 0, dv.aux, qbuf,
-				xs, ys, qmax, acc);
+		hipLaunchKernelGGL(k_quality_grad, dim3((xs + 63) / 64, (ys + SG_QGT - 1) / SG_QGT, nq), dim3(gthr), 0, dv.aux, qb.qbuf,
+				xs, ys, qb.qmax, qb.acc);
 		HIPCHK(hipGetLastError());
 	}
-	HIPCHK(hipMemcpyAsync(dv.qacc_h, acc, sizeof(unsigned long long) * 3 * nq, hipMemcpyDeviceToHost, dv.aux));
+	HIPCHK(hipMemcpyAsync(dv.qacc_h, qb.acc, sizeof(unsigned long long) * 3 * nq, hipMemcpyDeviceToHost, dv.aux));
 	HIPCHK(hipEventRecord(dv.aux_ev[0], dv.aux));
+	return SG_OK;
+}
+
+/* The quality estimate of `frames`, enqueued on the device's auxiliary stream (after the work
+ * already on `s`, which produced d_sel) so that it runs beside the FFT passes: its kernels are
+ * short and the passes leave the chip latency-bound.  reg_quality_finish waits for the sums and
+ * forms the values; *launched = false when the subsample loop never runs (dval = 0, :95-98). */
+static int reg_quality_launch(sg_ctx *ctx, SgDevice &dv, hipStream_t s, SgSel d_sel, int S,
+		const std::vector<int> &frames, bool *launched) {
+	*launched = false;
+	const int nq = (int)frames.size();
+	const int xs = (S - 1) / 3, ys = (S - 1) / 3;
+	if (!nq || xs < 2 || ys < 2)
+		return SG_OK;
+	SgQBufs qb;
+	if (int r = reg_quality_buffers(ctx, dv, nq, xs, ys, qb))
+		return r;
+	HIPCHK(hipEventRecord(dv.aux_ev[1], s));
+	HIPCHK(hipStreamWaitEvent(dv.aux, dv.aux_ev[1], 0));
+	HIPCHK(hipMemcpyAsync(qb.frames, frames.data(), sizeof(int) * nq, hipMemcpyHostToDevice, dv.aux));
+	HIPCHK(hipMemsetAsync(qb.acc, 0, (size_t)nq * (3 * sizeof(unsigned long long) + sizeof(unsigned int)), dv.aux));
+	/* one wave per workgroup, walking the row pairs: 283 us per 129 frames of 2048^2 against
+	 * 332 / 348 / 403 / 618 us with 128 / 192 / 256 / 384 threads (scripts/gpu_qsub.sh) */
+	const int qthr = ctx->knobs.qsub_threads;	/* A/B knob SG_QSUB_THREADS */
+	/* the dword loads of k_quality_sub need an even side, even pitches and a dword-aligned base */
+	const int al = !(S & 1) && !(d_sel.rp & 1) && !(d_sel.fp & 1) && !((uintptr_t)d_sel.p & 3);
+	hipLaunchKernelGGL(k_quality_sub, dim3((ys + SG_QROWS - 1) / SG_QROWS, nq), dim3(qthr), 0, dv.aux, d_sel, al, qb.frames,
+			S, xs, ys, qb.qbuf, qb.qmax);
+	HIPCHK(hipGetLastError());
+	if (int r = reg_quality_grad(ctx, dv, nq, xs, ys, qb))
+		return r;
 	*launched = true;
 	return SG_OK;
 }
@@ -2014,7 +2113,9 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel_p, i
 				(int)wcol_lds);
 		(void)hipFuncSetAttribute((const void *)k_reg_cols_fwd_perm_w, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)wcol_lds);
-		(void)hipFuncSetAttribute((const void *)k_reg_rows_fwd_half_w, hipFuncAttributeMaxDynamicSharedMemorySize,
+		(void)hipFuncSetAttribute((const void *)k_reg_rows_fwd_half_w<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+				(int)wcol_lds);
+		(void)hipFuncSetAttribute((const void *)k_reg_rows_fwd_half_w<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)wcol_lds);
 		(void)hipFuncSetAttribute((const void *)k_reg_rows_inv_half_w, hipFuncAttributeMaxDynamicSharedMemorySize,
 				(int)wcol_lds);
@@ -2072,6 +2173,24 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel_p, i
 	}
 
 	const bool ref_conc = fp32 && ctx->knobs.reg_refconc;	/* A/B knob SG_REG_REFCONC */
+	/* SG_REG_QFOLD (A/B): the quality estimate's subsample from the wave-level forward rows (every
+	 * frame of qframes passes through them: the reference and each pair), then only the gradient
+	 * kernel on the aux stream behind the last batch's forward rows */
+	const int qfold = (specp32 && npairs_total > 0 && S == 2048) ? ctx->knobs.reg_qfold : 0;
+	SgQBufs qfb{};
+	int q_qbase = 0;
+	bool q_fold_last = false;
+	auto fwd_w_launch = [&](hipStream_t st, const int *fa, const int *fb, int np, float2 *out, unsigned long long *en,
+			int rows, int qbase) {
+		if (qfold) {
+			const int waves = (S + qfold - 1) / qfold;
+			hipLaunchKernelGGL(k_reg_rows_fwd_half_w<true>, dim3((waves + 3) / 4, np), dim3(256), wcol_lds, st, d_sel, fa,
+					fb, tw32, out, en, qfold, qfb.qbuf, qfb.qmax, qbase);
+		} else {
+			hipLaunchKernelGGL(k_reg_rows_fwd_half_w<false>, dim3(S / 4 / rows, np), dim3(256), wcol_lds, st, d_sel, fa,
+					fb, tw32, out, en, rows, (uint16_t *)nullptr, (unsigned int *)nullptr, 0);
+		}
+	};
 	bool ref_pending = false, q_deferred = false;
 	if (ref_conc && !dv.aux2) {
 		HIPCHK(hipStreamCreateWithFlags(&dv.aux2, hipStreamNonBlocking));
@@ -2164,8 +2283,7 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel_p, i
 	};
 	auto half32 = [&](const int *fa, const int *fb, int np, unsigned long long *en) -> int {
 		if (wcol)
-			hipLaunchKernelGGL(k_reg_rows_fwd_half_w, dim3(S / 4 / rpw, np), dim3(256), wcol_lds, s, d_sel, fa, fb, tw32,
-					work32, en, rpw);
+			fwd_w_launch(s, fa, fb, np, work32, en, rpw, q_qbase);
 		else
 			hipLaunchKernelGGL(k_reg_rows_fwd_half<float2>, dim3(S / rpb, np), dim3(row_thr), row_lds32, s, d_sel, fa,
 					fb, S, tw32, work32, en, rpb);
@@ -2178,6 +2296,14 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel_p, i
 		if (ref_pending) {	/* the reference spectrum, from its stream */
 			HIPCHK(hipStreamWaitEvent(s, dv.aux2_ev[1], 0));
 			ref_pending = false;
+		}
+		if (qfold && q_fold_last) {	/* every frame subsampled (the reference's rows waited for above) */
+			const int nq = (int)qframes.size(), xs = (S - 1) / 3;
+			HIPCHK(hipEventRecord(dv.aux_ev[1], s));
+			HIPCHK(hipStreamWaitEvent(dv.aux, dv.aux_ev[1], 0));
+			if (int r = reg_quality_grad(ctx, dv, nq, xs, xs, qfb))
+				return r;
+			q_launched = true;
 		}
 		if (wcol && specp32 && ctx->knobs.reg_wcolw == 8)	/* 8-column strips: 64-B row segments, one workgroup per CU */
 			hipLaunchKernelGGL((k_reg_cols_xpower_w<true, 8>), dim3(S / 8, np), dim3(512), 2 * wcol_lds, s, work32,
@@ -2211,7 +2337,12 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel_p, i
 	/* the quality estimate on the aux stream, queued behind the main stream's table uploads and
 	 * fills (queued ahead of them, its long-running workgroups held the fills' single workgroup
 	 * back 0.2 ms, profiles/r05m_*) */
-	if (fp32 && npairs_total > 0 && ctx->knobs.reg_qafter) {
+	if (qfold) {	/* the sums zeroed on the call's stream, ahead of every forward row launch */
+		const int nq = (int)qframes.size(), xs = (S - 1) / 3;
+		if (int r = reg_quality_buffers(ctx, dv, nq, xs, xs, qfb))
+			return r;
+		HIPCHK(hipMemsetAsync(qfb.acc, 0, (size_t)nq * (3 * sizeof(unsigned long long) + sizeof(unsigned int)), s));
+	} else if (fp32 && npairs_total > 0 && ctx->knobs.reg_qafter) {
 		q_deferred = true;
 	} else {
 		rc = reg_quality_launch(ctx, dv, s, d_sel, S, qframes, &q_launched);
@@ -2239,8 +2370,7 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel_p, i
 			rs = dv.aux2;
 		}
 		if (specp32) {	/* wave-level passes: one row per wave, the columns straight into lane order */
-			hipLaunchKernelGGL(k_reg_rows_fwd_half_w, dim3(S / 4, 1), dim3(256), wcol_lds, rs, d_sel, d_fa + NP,
-					d_fb + NP, tw32, spec32, energy, 1);
+			fwd_w_launch(rs, d_fa + NP, d_fb + NP, 1, spec32, energy, 1, 0);
 			HIPCHK(hipGetLastError());
 			hipLaunchKernelGGL(k_reg_cols_fwd_perm_w, dim3(S / 2 / 4), dim3(256), wcol_lds, rs, spec32, specp32, tw32);
 		} else {
@@ -2280,6 +2410,8 @@ static int reg_dft_device(sg_ctx *ctx, int dev_index, const uint16_t *d_sel_p, i
 					pl, tbl, (int)SG_GEN_INV_ARGMAX, 1, energy, best, (const SgRegOut *)nullptr,
 					(SgCand *)nullptr);
 		} else if (fp32) {
+			q_qbase = 1 + 2 * p0;	/* qframes = ref, todo...: pair k's frames are entries 1 + 2k, 2 + 2k */
+			q_fold_last = p0 + np >= npairs_total;
 			if (int r = half32(d_fa + p0, d_fb + p0, np, energy))
 				return r;
 		} else {

@@ -358,3 +358,40 @@ def test_register_pitched_tie_exact(gpu_ctx):
     cx, cy, _ = gpu_ctx.register_dft(np.stack([ref, img]).astype(np.uint16))
     assert (gx[1], gy[1]) == (cx[1], cy[1])
     assert gpu_ctx.stats().reg_ties_resolved >= 1
+
+
+@pytest.mark.parametrize("rpw", [3, 6, 12])
+def test_register_quality_fold_matches(gpu_ctx, rpw):
+    """SG_REG_QFOLD (default 12): QualityEstimate's 3 x 3 subsample taken inside the wave-level forward
+    rows (r consecutive rows per wave) gives k_quality_sub's raw qualities, the oracle's
+    QualityEstimate and the same shifts; an odd frame count (a pair with no second frame), an
+    excluded frame, a reference that is not frame 0 and a pitched selection window"""
+    import torch
+    S, N, x0, y0 = 2048, 6, 5, 3
+    H, W = S + y0 + 2, S + x0 + 9
+    frames = orc.synth(N, 1, H, W, seed=300 + rpw, maxshift=6)[:, 0].copy()
+    frames[:, y0 + 700:y0 + 706, x0 + 900:x0 + 906] = 52000      # structure above the threshold
+    frames[3, y0 + 1500:y0 + 1503, x0 + 100:x0 + 103] = 65535
+    d = torch.from_numpy(frames.view(np.int16).reshape(-1)).cuda()
+    torch.cuda.synchronize()
+    inc = np.ones(N, np.int32)
+    inc[4] = 0
+    base = d.data_ptr() + 2 * (y0 * W + x0)
+    res = {}
+    for r in (0, rpw):
+        os.environ["SG_REG_QFOLD"] = str(r)
+        try:
+            with sg.Context() as c:
+                res[r] = (c.register_dft_device(base, N, S, ref_image=2, included=inc, raw_quality=True,
+                                                frame_pitch=H * W, row_pitch=W),
+                          c.register_dft_device(base, N, S, ref_image=2, included=inc, frame_pitch=H * W, row_pitch=W))
+        finally:
+            del os.environ["SG_REG_QFOLD"]
+    (want, norm_w), (got, norm) = res[0], res[rpw]
+    m = inc.astype(bool)
+    for a, b in zip(got, want):
+        assert np.array_equal(a[m], b[m], equal_nan=True), (a, b)
+    assert np.array_equal(norm[2][m], norm_w[2][m], equal_nan=True)
+    for f in (2, 3, 5):
+        sel = np.ascontiguousarray(frames[f, y0:y0 + S, x0:x0 + S])
+        assert _same_q(np.array([got[2][f]]), np.array([orc.quality(sel)])), (f, got[2][f])
