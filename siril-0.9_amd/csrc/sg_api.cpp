@@ -33,6 +33,7 @@ __global__ void k_stack_sorted(SgStackParams p, const unsigned int *list, const 
 template <int REJ, int NORM, int NI>
 __global__ void k_stack_hist(SgStackParams p, const int *tab, const int4 *norm, unsigned int *redo_count,
 		unsigned int *redo_list);
+__global__ void k_norm_fma_check(double *pairs, int N, int npad, int mode, unsigned int *verdict);
 template <int KM, int NW, bool PAIR>
 __global__ void k_stack_linfit(SgStackParams p, unsigned int *redo_count, unsigned int *redo_list);
 __global__ void k_hist_slow(SgStackParams p, unsigned int *redo_count, unsigned int *redo_list);
@@ -361,6 +362,8 @@ static int stack_fold(sg_ctx *ctx, SgDevice &dv, int slot, uint64_t rej[3][2], u
 		st.chain_pixels = fl[2];
 	st.compact_pixels = std::min<uint64_t>(fl[3], st.compact_pixels);	/* pstats holds the capacity */
 	st.exported_pixels = st.exported_pixels ? std::min<uint64_t>(fl[6], st.exported_pixels) : 0;	/* capacity, as compact */
+	if (st.norm_fma == 1)	/* k_norm_fma_check's verdict, read back beside the counters */
+		st.norm_fma = fl[7] ? 0 : 1;
 	if (sync) {	/* the calling stack_device_core publishes dv.stats when it returns */
 		dv.stats = st;
 	} else {
@@ -524,7 +527,13 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		/* the histogram path's per-frame pair {scale, offset} (additive) or {scale, mul}
 		 * (multiplicative), read with one scalar load per frame */
 		const bool additive = p.normalize == SG_ADDITIVE || p.normalize == SG_ADDITIVE_SCALING;
-		nm.resize(3 * N + 2 * Npad, 0.0);
+		/* + Npad single-rounding candidate pairs and the flag word of k_norm_fma_check (staged 1 = the
+		 * reference's operations; the call stages 0 when it runs the check) */
+		nm.resize(3 * N + 4 * Npad + 2, 0.0);
+		{
+			const unsigned int staged = ctx->knobs.norm_fma ? 0u : 1u;
+			memcpy(&nm[3 * N + 4 * Npad], &staged, sizeof staged);
+		}
 		/* additive: when every offset - 0.5 is exact (TwoSum error 0), the pair carries
 		 * offset - 0.5 and the kernel folds round_to_WORD's + 0.5 into the subtraction
 		 * (NORM 3: trunc(v scale - (offset - 0.5)), one fp64 add per sample less; equal to
@@ -867,6 +876,16 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 				st.exported_pixels = cap;	/* the capacity; clamped to the count when folded */
 			}
 			const dim3 hg((unsigned)nblk_h), hb((unsigned)sgh_block_threads(ni, rj));
+			/* normalised: check the single-rounding load against the reference's operations over every
+			 * u16 value of every frame (k_norm_fma_check, ~10 us); the kernel reads the verdict */
+			if (norm != 0 && !linfit_fast) {
+				if (ctx->knobs.norm_fma) {
+					hipLaunchKernelGGL(k_norm_fma_check, dim3(16, (unsigned)N), dim3(256), 0, s, (double *)p.hist_norm, N, Npad,
+							norm, p.flag_count + 7);
+					HIPCHK(hipGetLastError());
+					st.norm_fma = 1;	/* the verdict replaces it when the call is folded */
+				}
+			}
 			if (linfit_fast) {
 				/* one workgroup per 64 pixels of a row, the tile's columns in LDS */
 				const int km = N <= 512 ? 8 : 16;
@@ -1596,6 +1615,7 @@ extern "C" int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *d, sg_read_region_
 			agg.chain_pixels += s.chain_pixels;
 			agg.compact_pixels += s.compact_pixels;
 			agg.exported_pixels += s.exported_pixels;
+			agg.norm_fma |= s.norm_fma;
 			agg.launches += s.launches;
 			agg.main_kernel_blocks += s.main_kernel_blocks;
 			agg.path = s.path;

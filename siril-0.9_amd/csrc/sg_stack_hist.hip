@@ -522,7 +522,9 @@ __device__ __forceinline__ uint32_t sgh_fixup(uint32_t v, uint32_t fix, int m) {
 
 /* normalisation of a loaded pixel pair (:1635-1652): NORM 1 = round_to_WORD(v scale - offset),
  * 2 = round_to_WORD(v scale mul), 3 = NORM 1 with the + 0.5 folded into the offset, in the
- * reference's double operations; rows outside the
+ * reference's double operations; 4 (additive) / 5 (multiplicative) = trunc(fma(v, a, b)), one
+ * rounding, with {a, b} from k_norm_fma_check, which ran only because that equals the reference's
+ * operations for every u16 v of every frame; rows outside the
  * frame (read as 0) are normalised like read samples, but columns outside the image (EDGE
  * fix codes 1..3) stay 0, as the x shift writes 0 straight into the stack (:1628-1632) */
 template <int NORM, bool EDGE>
@@ -535,7 +537,8 @@ __device__ __forceinline__ uint32_t sgh_norm_pair(uint32_t v, double a, double b
 		const double t = (double)x * a;
 		/* NORM 3: b = offset - 0.5 (exact, checked on the host), so trunc(t - b) is
 		 * trunc(round(t - offset) + 0.5) of the reference with one add less */
-		const double y = NORM == 3 ? t - b : (NORM == 1 ? t - b : t * b) + 0.5;
+		const double y = NORM >= 4 ? __builtin_fma((double)x, a, b) :
+			NORM == 3 ? t - b : (NORM == 1 ? t - b : t * b) + 0.5;
 		uint32_t r;
 		asm("v_cvt_u32_f64 %0, %1" : "=v"(r) : "v"(y));
 		return r;
@@ -1692,7 +1695,7 @@ __device__ __forceinline__ void sgh_compact(const SgStackParams &p, const SghLds
  * lane per column (half = 0); CAP: normalised SIGMA / WINSORIZED kernel (captured out-of-band
  * values, sgh_compact) */
 template <int REJ, bool PAIR, int NI, bool ZT = false, bool CAP = false, class LT = SghLds<NI>>
-__device__ void sgh_finish2(const SgStackParams &p, LT &L, int col, int half, int lo, int R, int c, int x,
+__device__ __forceinline__ void sgh_finish2(const SgStackParams &p, LT &L, int col, int half, int lo, int R, int c, int x,
 		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list, bool zrow = false) {
 	const int lane = threadIdx.x & 63;
 	const int N = p.N;
@@ -2285,7 +2288,7 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
  * the workgroup still finish the previous tile (the clear waits for them) */
 template <int REJ, int NORM, int NI>
 __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro, SghLds<NI> &L, int bid, bool wait_prev,
-		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list) {
+		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list, bool fma = false) {
 	constexpr int WAVES = SghW<REJ, NI>::WAVES, COLS = 128 * NI;
 	const int tid = threadIdx.x, lane = tid & 63;
 	const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2337,7 +2340,24 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 		__builtin_amdgcn_s_setprio(1);
 	else if (p.prio == 2)
 		__builtin_amdgcn_s_setprio(3);
-	if (NI == 1 && !SGH_HALF1 && !AB) {
+	/* NORM 1..3 with fma: the build loads through the single-rounding pairs (NORM 4 / 5); the finish
+	 * is the same (so are the normalised samples) */
+	constexpr int NF = NORM == 2 ? 5 : 4;
+	SghRo rf = ro;
+	rf.norm = ro.norm + ro.npad;
+	if (NORM >= 1 && NORM <= 3 && fma && NI == 1 && !SGH_HALF1 && !AB) {
+		if (interior)
+			sgh_build<false, SGH_NBUF, NF, NI>(p, rf, L, F, wave, lane, lo2, nonzero, nsat, counted, wait_prev);
+		else
+			sgh_build<true, SGH_NBUF, NF, NI>(p, rf, L, F, wave, lane, lo2, nonzero, nsat, counted, wait_prev);
+	} else if (NORM >= 1 && NORM <= 3 && fma) {
+		if (interior)
+			sgh_build_half<false, NF, NI, NI == 1 ? SGH_NB : SGH_NB2, WAVES, SghWgBarrier, AB>(p, rf, L, F, wave, lane,
+					lo2, nonzero, nsat, counted, wait_prev, SghWgBarrier(), nab);
+		else
+			sgh_build_half<true, NF, NI, NI == 1 ? SGH_NB : SGH_NB2, WAVES, SghWgBarrier, AB>(p, rf, L, F, wave, lane,
+					lo2, nonzero, nsat, counted, wait_prev, SghWgBarrier(), nab);
+	} else if (NI == 1 && !SGH_HALF1 && !AB) {
 		if (interior)
 			sgh_build<false, SGH_NBUF, NORM, NI>(p, ro, L, F, wave, lane, lo2, nonzero, nsat, counted, wait_prev);
 		else
@@ -2449,7 +2469,7 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 	const int half = lane & 1;
 	int col = 32 * wave + (lane >> 1);
 	for (; col < COLS; col += 32 * WAVES)
-		sgh_finish2<REJ, true, NI, NORM == 1 || NORM == 3, NORM != 0 && REJ == 2>(p, L, col, half, col_lo(col), R, c,
+		sgh_finish2<REJ, true, NI, NORM == 1 || NORM == 3 || NORM == 4, NORM != 0 && REJ == 2>(p, L, col, half, col_lo(col), R, c,
 				col_x(col), redo_count, redo_list, interior);
 	if (timeline && lane == 0) {
 		const uint64_t t = __builtin_amdgcn_s_memrealtime();
@@ -2485,8 +2505,54 @@ k_stack_hist(SgStackParams p, const int *__restrict__ tab, const int4 *__restric
 	/* one tile per workgroup: stacking 2 or 4 consecutive tiles per workgroup (the next
 	 * tile's first loads overlapping the previous finish) measured 5.0 / 4.9 ms against 3.58
 	 * (scripts/gpu_r3p.sh; the tile loop also costs registers: 128 VGPRs + scratch) */
-	if (vb < ntiles)
-		sgh_tile<REJ, NORM, NI>(p, ro, L, vb, false, redo_count, redo_list);
+	if (vb >= ntiles)
+		return;
+	/* normalised: the single-rounding load when k_norm_fma_check found it exact for every frame (its
+	 * flag word behind the pairs stays 0; the host stages 1 when the check is not run) */
+	const bool fma = NORM >= 1 && NORM <= 3 && ((const unsigned int *)(norm + 2 * ro.npad))[0] == 0u;
+	sgh_tile<REJ, NORM, NI>(p, ro, L, vb, false, redo_count, redo_list, fma);
+}
+
+/* k_norm_fma_check: may the normalising load use one fma per sample?  The reference normalises
+ * a sample x in two or three roundings (:1642-1651, round_to_WORD utils.c:68-74): additive
+ * fl(fl(x scale) - offset) (+ 0.5), multiplicative fl(fl(x scale) mul) + 0.5.  The candidate is
+ * fma(x, a, b) with {a, b} = {scale, -(offset - 0.5)} (mode 3: the folded offset), {scale,
+ * fl(0.5 - offset)} (mode 1) or {fl(scale mul), 0.5} (mode 2).  Both go through the kernels'
+ * conversion (v_cvt_u32_f64, then the pack's clamp to 65535) for every u16 x of every frame; one
+ * difference anywhere sets the flag word and the call keeps the reference's operations.
+ * pairs: the {scale, offset - 0.5 | offset | mul} pairs of the histogram kernels; the candidates go
+ * npad pairs further, the flag word (staged 0 when the check runs) 2 npad pairs further.  Grid (16, N) x 256 threads,
+ * 16 values per thread. */
+__global__ void __launch_bounds__(256)
+k_norm_fma_check(double *__restrict__ pairs, int N, int npad, int mode, unsigned int *__restrict__ verdict) {
+	const int f = blockIdx.y;
+	if (f >= N)
+		return;
+	const double a = pairs[2 * f], b = pairs[2 * f + 1];
+	const double A = mode == 2 ? a * b : a;
+	const double B = mode == 2 ? 0.5 : (mode == 3 ? -b : 0.5 - b);
+	auto cvt = [](double y) -> uint32_t {
+		uint32_t r;
+		asm volatile("v_cvt_u32_f64 %0, %1" : "=v"(r) : "v"(y));
+		return r < 65535u ? r : 65535u;
+	};
+	bool bad = false;
+	const int x0 = blockIdx.x * 4096 + threadIdx.x;
+#pragma unroll 4
+	for (int k = 0; k < 16; k++) {
+		const double x = (double)(x0 + 256 * k);
+		const double t = x * a;
+		const double yr = mode == 3 ? t - b : (mode == 1 ? t - b : t * b) + 0.5;
+		bad |= cvt(yr) != cvt(__builtin_fma(x, A, B));
+	}
+	if (__ballot(bad) && (threadIdx.x & 63) == 0) {
+		atomicOr((unsigned int *)(pairs + 4 * (size_t)npad), 1u);
+		atomicOr(verdict, 1u);	/* counter block: read back with the counters (sg_stack_stats::norm_fma) */
+	}
+	if (blockIdx.x == 0 && threadIdx.x == 0) {
+		pairs[2 * ((size_t)npad + f)] = A;
+		pairs[2 * ((size_t)npad + f) + 1] = B;
+	}
 }
 
 /* k_hist_slow: the exported WINSORIZED columns (SgStackParams::wx), 64 per wave, each lane's

@@ -63,6 +63,7 @@ class StackStats(ctypes.Structure):
         ("compact_pixels", ctypes.c_uint64),
         ("reg_ms", ctypes.c_double),
         ("exported_pixels", ctypes.c_uint64),
+        ("norm_fma", ctypes.c_int64),
     ]
 
 
