@@ -437,3 +437,75 @@ def test_cfg4_winsorized_oracle_bands_spread(gpu_ctx, part):
     pool.shutdown()
     del frames, out, ob, fv
     _free()
+
+
+@pytest.mark.parametrize("normalize", ["additive-scaling", "multiplicative-scaling"])
+def test_cfg2_normalised_fma_load_whole_image(gpu_ctx, normalize):
+    """configs[2]'s 512 x 4096^2 SIGMA (4, 3) stack normalised as bench.py's --normalize (the GUI
+    defaults; coefficients as compute_normalization forms them, stacking.c:79-190): the histogram
+    kernel's single-rounding load (admitted by k_norm_fma_check, norm_fma = 1) gives the same whole
+    image and counters as a context held to the reference's roundings (SG_NORM_FMA=0, norm_fma = 0),
+    and 3 row bands (top, middle, bottom) equal the oracle (stacking.c:1642-1651)"""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    frames, sx, sy, (N, H, W, M) = _sigma_cfg2(gpu_ctx)
+    fv = frames.view(N, H, W)
+    i = np.arange(N, dtype=np.float64)
+    loc = 1000.0 + 0.6 * np.sin(0.37 * i)
+    scl = 30.0 + 0.3 * np.cos(0.23 * i)
+    scale = scl[0] / scl
+    if normalize == "additive-scaling":
+        mode, off, mul = sg.ADDITIVE_SCALING, scale * loc - loc[0], np.ones(N)
+    else:
+        mode, off, mul = sg.MULTIPLICATIVE_SCALING, np.zeros(N), loc[0] / loc
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=sg.SIGMA, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                              normalize=mode, offset=off, mul=mul, scale=scale, max_thread=16, max_number_of_rows=H)
+    out = torch.zeros(H * W, dtype=torch.int16, device="cuda")
+    outr = torch.zeros(H * W, dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
+    rej, _ = gpu_ctx.stack_device(desc, frames.data_ptr(), H * W, H * W, out.data_ptr(), 0, H)
+    assert gpu_ctx.stats().norm_fma == 1, "the single-rounding load was not admitted"
+    old = os.environ.get("SG_NORM_FMA")
+    os.environ["SG_NORM_FMA"] = "0"
+    try:
+        ref_ctx = sg.Context()
+    finally:
+        if old is None:
+            del os.environ["SG_NORM_FMA"]
+        else:
+            os.environ["SG_NORM_FMA"] = old
+    try:
+        rej_r, _ = ref_ctx.stack_device(desc, frames.data_ptr(), H * W, H * W, outr.data_ptr(), 0, H)
+        assert ref_ctx.stats().norm_fma == 0
+    finally:
+        ref_ctx.close()
+    assert torch.equal(out, outr), f"{normalize}: the fma load's image differs from the reference roundings'"
+    assert np.array_equal(rej, rej_r), (rej, rej_r)
+    R = 64
+    starts = [0, H // 2, H - R]
+    jobs = _oracle_band_jobs(fv, starts, R, M)
+
+    def oracle_bands():
+        res = []
+        for b, lo, band in jobs:
+            rc, ref, _, rows = orc.stack_rejection(band, sg.SIGMA, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                                                   normalize=mode, offset=off, mul=mul, scale=scale, max_thread=16,
+                                                   max_number_of_rows=16 * 24, row_counters=True)
+            res.append((b, rc, ref[0, b - lo:b + R - lo].copy(), rows[0, b - lo:b + R - lo].sum(axis=0)))
+        return res
+
+    pool = ThreadPoolExecutor(1)
+    fut = pool.submit(oracle_bands)
+    img = out.cpu().numpy().view(np.uint16).reshape(H, W)
+    band_rej = {}
+    for b in starts:
+        r, _ = gpu_ctx.stack_device(desc, frames.data_ptr(), H * W, H * W, outr.data_ptr(), b, b + R)
+        band_rej[b] = r.copy()
+    for b, rc, want, rows in fut.result():
+        assert rc == 0
+        bad = np.argwhere(img[b:b + R] != want)
+        assert bad.size == 0, f"{normalize} rows {b}..{b + R}: {len(bad)} pixels differ, first {bad[:3].tolist()}"
+        assert np.array_equal(band_rej[b][0], rows), (b, band_rej[b][0], rows)
+    pool.shutdown()
+    del frames, out, outr, fv
+    _free()
