@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--height", type=int, default=4096)
     ap.add_argument("--rejection", default="sigma")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--normalize", choices=["none", "additive-scaling", "multiplicative-scaling"], default="none",
+    ap.add_argument("--normalize", choices=["none", "additive", "additive-scaling", "multiplicative-scaling"], default="none",
                     help="sigma workload: per-frame normalisation (synthetic location / scale, as "
                          "compute_normalization derives them)")
     ap.add_argument("--band-of", type=int, default=0,
@@ -423,7 +423,11 @@ def sigma_form(args, ctx, D, strong, gather_mode):
         loc = 1000.0 + 0.6 * np.sin(0.37 * i)
         scl = 30.0 + 0.3 * np.cos(0.23 * i)
         scale = scl[0] / scl
-        if args.normalize == "additive-scaling":
+        if args.normalize == "additive":
+            norm_mode = sg.ADDITIVE
+            scale = np.ones(N)
+            off = loc - loc[0]
+        elif args.normalize == "additive-scaling":
             norm_mode = sg.ADDITIVE_SCALING
             off = scale * loc - loc[0]
         else:
@@ -560,6 +564,8 @@ def main_sigma(args):
             "redo_pixels": int(st.chain_pixels),
             "compact_pixels": int(st.compact_pixels),
             "rejected": [int(x) for x in np.asarray(f["rej_tot"]).reshape(-1)[:2]],
+            **({"norm_load": ["reference", "fma", "integer"][max(0, min(2, int(st.norm_fma)))]}
+               if args.normalize != "none" else {}),
         }
         if world > 1:
             res["per_rank_kernel_ms"] = [round(x, 3) for x in f["per_rank_kms"]]

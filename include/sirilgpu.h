@@ -194,8 +194,9 @@ typedef struct {
 	double reg_ms;			/* last registration on a device: HIP-event span of its device work
 					 * (first pass to the quality estimate's end, host waits included) */
 	uint64_t exported_pixels;	/* histogram WINSORIZED: columns finished by k_hist_slow (SG_WINS_EXPORT) */
-	int64_t norm_fma;		/* normalised histogram stack: 1 = samples normalised by one fma each (found equal to
-					 * the reference's roundings for every u16 value of every frame), 0 = the reference's operations */
+	int64_t norm_fma;		/* normalised histogram stack: the sample load found equal to the reference's roundings
+					 * for every u16 value of every frame: 2 = an integer offset (additive, scale 1), 1 = one
+					 * fma per sample; 0 = the reference's operations */
 } sg_stack_stats;
 int sg_get_last_stats(const sg_ctx *ctx, sg_stack_stats *st);
 /* device slots of the context (sg_init's ndev): callers size their batches by it, as the

@@ -362,8 +362,8 @@ static int stack_fold(sg_ctx *ctx, SgDevice &dv, int slot, uint64_t rej[3][2], u
 		st.chain_pixels = fl[2];
 	st.compact_pixels = std::min<uint64_t>(fl[3], st.compact_pixels);	/* pstats holds the capacity */
 	st.exported_pixels = st.exported_pixels ? std::min<uint64_t>(fl[6], st.exported_pixels) : 0;	/* capacity, as compact */
-	if (st.norm_fma == 1)	/* k_norm_fma_check's verdict, read back beside the counters */
-		st.norm_fma = fl[7] ? 0 : 1;
+	if (st.norm_fma > 0)	/* k_norm_fma_check's verdict, read back beside the counters (the launch set the best allowed) */
+		st.norm_fma = st.norm_fma == 2 && !(fl[7] & 2u) ? 2 : (fl[7] & 1u) ? 0 : 1;
 	if (sync) {	/* the calling stack_device_core publishes dv.stats when it returns */
 		dv.stats = st;
 	} else {
@@ -527,11 +527,12 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 		/* the histogram path's per-frame pair {scale, offset} (additive) or {scale, mul}
 		 * (multiplicative), read with one scalar load per frame */
 		const bool additive = p.normalize == SG_ADDITIVE || p.normalize == SG_ADDITIVE_SCALING;
-		/* + Npad single-rounding candidate pairs and the flag word of k_norm_fma_check (staged 1 = the
-		 * reference's operations; the call stages 0 when it runs the check) */
-		nm.resize(3 * N + 4 * Npad + 2, 0.0);
+		/* + Npad single-rounding candidate pairs and the flag word of k_norm_fma_check (bit 0: no fma
+		 * load, bit 1: no integer load; the check ORs in what it finds) */
+		nm.resize(3 * N + 6 * Npad + 2, 0.0);	/* + the integer offsets of k_norm_fma_check's scale-1 form */
 		{
-			const unsigned int staged = ctx->knobs.norm_fma ? 0u : 1u;
+			/* SG_NORM_FMA 0: neither form, 1: the fma only, 2 (default): the integer form first */
+			const unsigned int staged = ctx->knobs.norm_fma == 0 ? 3u : (ctx->knobs.norm_fma == 1 ? 2u : 0u);
 			memcpy(&nm[3 * N + 4 * Npad], &staged, sizeof staged);
 		}
 		/* additive: when every offset - 0.5 is exact (TwoSum error 0), the pair carries
@@ -883,7 +884,8 @@ static int stack_device_core(sg_ctx *ctx, int dev_index, const sg_stack_desc *d,
 					hipLaunchKernelGGL(k_norm_fma_check, dim3(16, (unsigned)N), dim3(256), 0, s, (double *)p.hist_norm, N, Npad,
 							norm, p.flag_count + 7);
 					HIPCHK(hipGetLastError());
-					st.norm_fma = 1;	/* the verdict replaces it when the call is folded */
+					/* the best load allowed; the verdict replaces it when the call is folded */
+					st.norm_fma = norm != 2 && ctx->knobs.norm_fma == 2 ? 2 : 1;
 				}
 			}
 			if (linfit_fast) {
@@ -1615,7 +1617,7 @@ extern "C" int sg_stack_u16(sg_ctx *ctx, const sg_stack_desc *d, sg_read_region_
 			agg.chain_pixels += s.chain_pixels;
 			agg.compact_pixels += s.compact_pixels;
 			agg.exported_pixels += s.exported_pixels;
-			agg.norm_fma |= s.norm_fma;
+			agg.norm_fma = std::max(agg.norm_fma, s.norm_fma);
 			agg.launches += s.launches;
 			agg.main_kernel_blocks += s.main_kernel_blocks;
 			agg.path = s.path;

@@ -155,8 +155,9 @@ struct SgKnobs {
 	int reg_wcolw = 8;		/* SG_REG_WCOLW: columns per strip of the wave-level column pass (8: 64-B row segments, one workgroup per CU: configs[1] registration 3.33 -> 3.20 ms and the pass's HBM writes 1.57x -> 1.0x the plane, profiles/r05w_*; 4: 32-B segments, two workgroups per CU) */
 	int reg_specp = 1;		/* SG_REG_SPECP: 1 = the wave-level column pass reads the reference spectrum in lane order (k_spec_perm), 0 = through LDS */
 	int reg_refconc = 1;		/* SG_REG_REFCONC: 1 = fp32 reference spectrum on its own stream beside the first batch's forward rows */
-	int norm_fma = 1;		/* SG_NORM_FMA: 1 = normalised histogram stacks load with one fma per sample when a device check
-					 * (k_norm_fma_check) finds it equal to the reference's two roundings for every u16 value of every frame */
+	int norm_fma = 2;		/* SG_NORM_FMA: normalised histogram stacks load with one fma per sample (1, 2) or, additive with
+					 * scale 1, an integer offset (2) when a device check (k_norm_fma_check) finds that equal to the
+					 * reference's roundings for every u16 value of every frame; 0 = the reference's operations */
 	int reg_rpb = 4;		/* SG_REG_RPB: rows per forward-row workgroup of the half-spectrum path (1 -> 4: 6.46 -> 5.92 ms registration on configs[1], profiles/r03u_ab_reg_rows.log) */
 	void read() {
 		hist_dbg = sg_env_int("SG_HIST_DBG", 0, 1000, 0);
@@ -204,7 +205,7 @@ struct SgKnobs {
 		reg_qafter = sg_env_int("SG_REG_QAFTER", 0, 1, 0);
 		reg_rpw = sg_env_int("SG_REG_RPW", 1, 64, 8);
 		reg_qfold = sg_env_int("SG_REG_QFOLD", 0, 63, 12) / 3 * 3;
-		norm_fma = sg_env_int("SG_NORM_FMA", 0, 1, 1);
+		norm_fma = sg_env_int("SG_NORM_FMA", 0, 2, 2);
 	}
 };
 

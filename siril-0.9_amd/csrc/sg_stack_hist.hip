@@ -138,8 +138,10 @@ struct SghPix {
 	uint64_t *wp;		/* probe build: this wave's region accumulators in LDS */
 #endif
 	SghM Z;			/* moments of the zeros (and of the border row's normalised zeros, ztab) */
-	int zmax;		/* > 0: the below-band samples include normalised zeros up to this value;
-				 * a count query at v in [0, zmax) or a rank among them is not decided here */
+	int zmax;		/* > 0: the below-band samples include normalised zeros (or captured samples) up to this
+				 * value; a count query at v in [0, zmax) or a rank among them is not decided here */
+	int omin;		/* < 65535: captured samples above the band from this value on (CAP SIGMA); a count
+				 * query at v in [omin, 65535) or a rank among the above-band samples is not decided here */
 	SghM T;			/* moments of all samples */
 	double zs, zss;		/* Z.s, Z.ss as doubles (exact: below 2^53) for the Winsorized queries */
 };
@@ -524,13 +526,28 @@ __device__ __forceinline__ uint32_t sgh_fixup(uint32_t v, uint32_t fix, int m) {
  * 2 = round_to_WORD(v scale mul), 3 = NORM 1 with the + 0.5 folded into the offset, in the
  * reference's double operations; 4 (additive) / 5 (multiplicative) = trunc(fma(v, a, b)), one
  * rounding, with {a, b} from k_norm_fma_check, which ran only because that equals the reference's
- * operations for every u16 v of every frame; rows outside the
+ * operations for every u16 v of every frame; 6 (additive, scale 1) = clamp(v - K, 0, 65535) with an
+ * integer K per frame, admitted the same way; rows outside the
  * frame (read as 0) are normalised like read samples, but columns outside the image (EDGE
  * fix codes 1..3) stay 0, as the x shift writes 0 straight into the stack (:1628-1632) */
 template <int NORM, bool EDGE>
 __device__ __forceinline__ uint32_t sgh_norm_pair(uint32_t v, double a, double b, uint32_t fix, int m) {
 	if (NORM == 0)
 		return v;
+	if (NORM == 6) {
+		/* additive with scale 1: sat(sat(v + kneg) - kpos) per half, K = kpos - kneg the frame's
+		 * integer offset (the pair's bits: a = {kpos, kneg} replicated in both halves) */
+		const sgh_u16x2 kp = __builtin_bit_cast(sgh_u16x2, (uint32_t)__double2loint(a));
+		const sgh_u16x2 kn = __builtin_bit_cast(sgh_u16x2, (uint32_t)__double2hiint(a));
+		uint32_t r = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_elementwise_add_sat(
+				__builtin_bit_cast(sgh_u16x2, v), kn), kp));
+		(void)b;
+		if (EDGE) {
+			const uint32_t f = (fix >> (2 * m)) & 3u;
+			r &= f == 0u ? 0xFFFFFFFFu : (f == 1u ? 0xFFFF0000u : (f == 2u ? 0x0000FFFFu : 0u));
+		}
+		return r;
+	}
 	/* round_to_WORD(y) = min(trunc(y + 0.5), 65535) with the conversion's clamp of
 	 * negative values to 0 (y <= 0 gives y + 0.5 <= 0.5, truncated to 0 either way) */
 	auto g = [&](uint32_t x) -> uint32_t {
@@ -794,11 +811,12 @@ __device__ __forceinline__ int sgh_med_value(const SghPix &P, const SghMed &m) {
  * pass, sigma comes from sgh_sigma_fast, and the clamps and selects are straight-line code, so
  * a pass is one basic block (round 2: the loop's VALU count, not its dependency chain, is what
  * the kernel pays for; scripts/gpu_r2t.sh, gpu_r2w.sh). */
-template <bool ZT>
+template <bool ZT, bool CAP = false>
 __device__ __forceinline__ int sgh_sigma3(const SghPix &P, int N, double sl, double sh, int half, uint16_t *value,
 		uint32_t *rlo_out, uint32_t *rhi_out, int &passes) {
-	/* a query the below-band normalised zeros make undecidable here (ZT: additive normalisation) */
-	auto zbad = [&](int v) { return ZT && v >= 0 && v < P.zmax; };
+	/* a query the below-band normalised zeros (ZT: additive normalisation) or the captured out-of-band
+	 * samples (CAP) make undecidable here */
+	auto zbad = [&](int v) { return ((ZT || CAP) && v >= 0 && v < P.zmax) || (CAP && v >= P.omin && v < 65535); };
 	int A = 0, B = 65535, n = N, r = 0, nrem;
 	SghM MA = {0, 0, 0}, MB = P.T;
 	uint32_t rlo = 0, rhi = 0;
@@ -813,7 +831,9 @@ __device__ __forceinline__ int sgh_sigma3(const SghPix &P, int N, double sl, dou
 		/* n >= 4: the halvings as unsigned shifts; the median as (m1 + m2) * 0.5 (exact), with
 		 * m2 = m1 for odd n, so no branch */
 		const int mv = sgh_med_value(P, md);
-		uint32_t zb = (ZT && P.zmax && md.r < 0) ? 1u : 0u;	/* a median rank among the below-band samples */
+		/* a median rank among below-band samples that are not all zeros, or among above-band ones that are
+		 * not all 65535 */
+		uint32_t zb = (((ZT || CAP) && P.zmax && md.r < 0) || (CAP && P.omin < 65535 && md.r >= P.nb)) ? 1u : 0u;
 		const int mo = (int)sgh_x((uint32_t)mv);
 		const int m1 = half ? mo : mv, m2 = (n & 1) ? m1 : (half ? mv : mo);
 		const double median = (double)(m1 + m2) * 0.5;
@@ -1797,6 +1817,7 @@ __device__ __forceinline__ void sgh_finish2(const SgStackParams &p, LT &L, int c
 		}
 	}
 	P.zmax = 0;
+	P.omin = 65535;
 	P.lo = lo;
 	P.nz = (int)L.nz[col];
 	P.ns = (int)L.ns[col];
@@ -1813,9 +1834,19 @@ __device__ __forceinline__ void sgh_finish2(const SgStackParams &p, LT &L, int c
 	bool cmp = false;	/* CAP: the pixel's sorted column goes out through sgh_compact */
 	const uint64_t c1 = SG_DBG(p) == 11 ? __builtin_readcyclecounter() : 0;
 	if (x < p.W) {
+		/* CAP SIGMA (round 6): up to SGH_OVK out-of-band samples other than 0 / 65535, every one captured
+		 * (their values in L.ov: a scaled cosmic ray, a dead pixel moved off 0), join the pixel as known
+		 * samples (counts and moments below or above the band) instead of sending it to the compact list;
+		 * a query or median rank among them is undecidable here (zbad) and redoes the pixel */
+		int kx = 0;
+		if constexpr (CAP && REJ == 2) {
+			const int k = oob - P.nz - P.ns;
+			if (P.nb + oob == N && zc == 0 && k > 0 && k <= SGH_OVK && (int)L.ovn[col] == k)
+				kx = k;
+		}
 		if (SG_DBG(p) == 1) {
 			value = (uint16_t)(s32 + ss32);
-		} else if (P.nb + oob != N || (zc && zmax >= lo) || (REJ != 1 && REJ != 8 && oob != P.nz + P.ns + zc)) {
+		} else if (P.nb + oob != N || (zc && zmax >= lo) || (REJ != 1 && REJ != 8 && oob != P.nz + P.ns + zc + kx)) {
 			cls = 1;	/* out-of-band sample other than 0 / 65535 (or than this row's normalised
 				 * zeros), or a wrapped u8 counter */
 			if constexpr (CAP) {
@@ -1840,6 +1871,29 @@ __device__ __forceinline__ void sgh_finish2(const SgStackParams &p, LT &L, int c
 			P.T.c = N;
 			P.T.s = (long long)s32 + P.Z.s + ds * P.ns;
 			P.T.ss = (unsigned long long)ss32 + P.Z.ss + (unsigned long long)(ds * ds) * (unsigned long long)P.ns;
+			if constexpr (CAP && REJ == 2) {
+				if (kx) {
+#pragma unroll
+					for (int k = 0; k < SGH_OVK; k++) {
+						if (k < kx) {
+							const int v = (int)L.ov[k][col];
+							const long long d = (long long)v - lo;
+							const unsigned long long d2 = (unsigned long long)(d * d);
+							P.T.s += d;
+							P.T.ss += d2;
+							if (v < lo) {	/* below the band: with the zeros (counts, moments, ranks) */
+								P.Z.c++;
+								P.Z.s += d;
+								P.Z.ss += d2;
+								P.nz++;
+								P.zmax = v > P.zmax ? v : P.zmax;
+							} else {
+								P.omin = v < P.omin ? v : P.omin;
+							}
+						}
+					}
+				}
+			}
 			if (REJ == 1 || REJ == 8) {
 				/* out-of-band samples of any value: below the band nbl of them, above na */
 				const int na = (int)L.na[col], nbl = oob - na;
@@ -1862,7 +1916,9 @@ __device__ __forceinline__ void sgh_finish2(const SgStackParams &p, LT &L, int c
 				rlo = rhi = 0;
 #endif
 			} else {
-				cls = sgh_sigma3<ZT>(P, N, p.sig0, p.sig1, half, &value, &rlo, &rhi, passes);
+				cls = sgh_sigma3<ZT, CAP>(P, N, p.sig0, p.sig1, half, &value, &rlo, &rhi, passes);
+				if constexpr (CAP && REJ == 2)
+					cmp = cls != SG_CLS_OK && kx && p.cmp_cols;	/* every sample known: the sorted column */
 #ifdef SGH_SIGMA_PASSES	/* A/B probe build: the image holds the pass counts */
 				value = (uint16_t)passes;
 				cls = SG_CLS_OK;
@@ -1918,7 +1974,7 @@ __device__ __forceinline__ void sgh_finish2(const SgStackParams &p, LT &L, int c
 #endif
 	if constexpr (CAP)
 		sgh_compact<NI>(p, L, cmp && !half && x < p.W, col, lo, (unsigned int)(((int64_t)c * p.H + R) * p.W + x),
-				P.nz, P.ns, oob - P.nz - P.ns, redo_count, redo_list);
+				(int)L.nz[col], (int)L.ns[col], oob - (int)L.nz[col] - (int)L.ns[col], redo_count, redo_list);
 	const unsigned long long a = sgh_wave_sum(rlo), b = sgh_wave_sum(rhi);
 	if (lane == 0 && (a | b)) {
 		unsigned long long *sh = p.rej + ((size_t)((blockIdx.x * 8 + (col >> 5)) % SG_REJ_SHARDS) * 6 + c * 2);
@@ -2288,7 +2344,7 @@ __device__ __forceinline__ void sgh_build_half(const SgStackParams &p, const Sgh
  * the workgroup still finish the previous tile (the clear waits for them) */
 template <int REJ, int NORM, int NI>
 __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro, SghLds<NI> &L, int bid, bool wait_prev,
-		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list, bool fma = false) {
+		unsigned int *__restrict__ redo_count, unsigned int *__restrict__ redo_list, int load = 0) {
 	constexpr int WAVES = SghW<REJ, NI>::WAVES, COLS = 128 * NI;
 	const int tid = threadIdx.x, lane = tid & 63;
 	const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2340,12 +2396,29 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 		__builtin_amdgcn_s_setprio(1);
 	else if (p.prio == 2)
 		__builtin_amdgcn_s_setprio(3);
-	/* NORM 1..3 with fma: the build loads through the single-rounding pairs (NORM 4 / 5); the finish
-	 * is the same (so are the normalised samples) */
+	/* NORM 1..3, load 1: the build loads through the single-rounding pairs (NORM 4 / 5), load 2
+	 * (additive, scale 1) through the integer offsets (NORM 6); the finish is the same (so are the
+	 * normalised samples) */
 	constexpr int NF = NORM == 2 ? 5 : 4;
+	constexpr bool NORMI = NORM == 1 || NORM == 3;
+	const bool fma = NORM >= 1 && NORM <= 3 && load == 1;
 	SghRo rf = ro;
 	rf.norm = ro.norm + ro.npad;
-	if (NORM >= 1 && NORM <= 3 && fma && NI == 1 && !SGH_HALF1 && !AB) {
+	SghRo ri = ro;
+	ri.norm = ro.norm + 2 * ro.npad + 1;
+	if (NORMI && load == 2 && NI == 1 && !SGH_HALF1 && !AB) {
+		if (interior)
+			sgh_build<false, SGH_NBUF, 6, NI>(p, ri, L, F, wave, lane, lo2, nonzero, nsat, counted, wait_prev);
+		else
+			sgh_build<true, SGH_NBUF, 6, NI>(p, ri, L, F, wave, lane, lo2, nonzero, nsat, counted, wait_prev);
+	} else if (NORMI && load == 2) {
+		if (interior)
+			sgh_build_half<false, 6, NI, NI == 1 ? SGH_NB : SGH_NB2, WAVES, SghWgBarrier, AB>(p, ri, L, F, wave, lane,
+					lo2, nonzero, nsat, counted, wait_prev, SghWgBarrier(), nab);
+		else
+			sgh_build_half<true, 6, NI, NI == 1 ? SGH_NB : SGH_NB2, WAVES, SghWgBarrier, AB>(p, ri, L, F, wave, lane,
+					lo2, nonzero, nsat, counted, wait_prev, SghWgBarrier(), nab);
+	} else if (NORM >= 1 && NORM <= 3 && fma && NI == 1 && !SGH_HALF1 && !AB) {
 		if (interior)
 			sgh_build<false, SGH_NBUF, NF, NI>(p, rf, L, F, wave, lane, lo2, nonzero, nsat, counted, wait_prev);
 		else
@@ -2509,8 +2582,10 @@ k_stack_hist(SgStackParams p, const int *__restrict__ tab, const int4 *__restric
 		return;
 	/* normalised: the single-rounding load when k_norm_fma_check found it exact for every frame (its
 	 * flag word behind the pairs stays 0; the host stages 1 when the check is not run) */
-	const bool fma = NORM >= 1 && NORM <= 3 && ((const unsigned int *)(norm + 2 * ro.npad))[0] == 0u;
-	sgh_tile<REJ, NORM, NI>(p, ro, L, vb, false, redo_count, redo_list, fma);
+	const unsigned int verdict = NORM >= 1 && NORM <= 3 ? ((const unsigned int *)(norm + 2 * ro.npad))[0] : 3u;
+	/* 1: single rounding (fma), 2: integer offset (additive, scale 1), 0: the reference's operations */
+	const int load = (NORM == 1 || NORM == 3) && !(verdict & 2u) ? 2 : (!(verdict & 1u) ? 1 : 0);
+	sgh_tile<REJ, NORM, NI>(p, ro, L, vb, false, redo_count, redo_list, load);
 }
 
 /* k_norm_fma_check: may the normalising load use one fma per sample?  The reference normalises
@@ -2521,7 +2596,9 @@ k_stack_hist(SgStackParams p, const int *__restrict__ tab, const int4 *__restric
  * conversion (v_cvt_u32_f64, then the pack's clamp to 65535) for every u16 x of every frame; one
  * difference anywhere sets the flag word and the call keeps the reference's operations.
  * pairs: the {scale, offset - 0.5 | offset | mul} pairs of the histogram kernels; the candidates go
- * npad pairs further, the flag word (staged 0 when the check runs) 2 npad pairs further.  Grid (16, N) x 256 threads,
+ * npad pairs further, the flag word (staged 0 when the check runs; bit 0: the fma differs, bit 1: the
+ * integer form differs) 2 npad pairs further.  Additive with scale 1 also tries clamp(x - K, 0, 65535)
+ * (two packed saturating u16 ops per pixel pair, NORM 6), written 2 npad + 1 pairs further.  Grid (16, N) x 256 threads,
  * 16 values per thread. */
 __global__ void __launch_bounds__(256)
 k_norm_fma_check(double *__restrict__ pairs, int N, int npad, int mode, unsigned int *__restrict__ verdict) {
@@ -2531,27 +2608,41 @@ k_norm_fma_check(double *__restrict__ pairs, int N, int npad, int mode, unsigned
 	const double a = pairs[2 * f], b = pairs[2 * f + 1];
 	const double A = mode == 2 ? a * b : a;
 	const double B = mode == 2 ? 0.5 : (mode == 3 ? -b : 0.5 - b);
+	/* additive with scale 1: clamp(x - K, 0, 65535), K = ceil(offset - 0.5) clamped to +-65535 */
+	const bool icand = mode != 2 && a == 1.0;
+	const double kc = ceil(mode == 3 ? b : b - 0.5);
+	const int K = icand ? (kc > 65535.0 ? 65535 : (kc < -65535.0 ? -65535 : (int)kc)) : 0;
 	auto cvt = [](double y) -> uint32_t {
 		uint32_t r;
 		asm volatile("v_cvt_u32_f64 %0, %1" : "=v"(r) : "v"(y));
 		return r < 65535u ? r : 65535u;
 	};
-	bool bad = false;
+	bool bad = false, ibad = !icand;
 	const int x0 = blockIdx.x * 4096 + threadIdx.x;
 #pragma unroll 4
 	for (int k = 0; k < 16; k++) {
-		const double x = (double)(x0 + 256 * k);
+		const int xi = x0 + 256 * k;
+		const double x = (double)xi;
 		const double t = x * a;
 		const double yr = mode == 3 ? t - b : (mode == 1 ? t - b : t * b) + 0.5;
-		bad |= cvt(yr) != cvt(__builtin_fma(x, A, B));
+		const uint32_t r = cvt(yr);
+		bad |= r != cvt(__builtin_fma(x, A, B));
+		const int yi = xi - K;
+		ibad |= r != (uint32_t)(yi < 0 ? 0 : (yi > 65535 ? 65535 : yi));
 	}
-	if (__ballot(bad) && (threadIdx.x & 63) == 0) {
-		atomicOr((unsigned int *)(pairs + 4 * (size_t)npad), 1u);
-		atomicOr(verdict, 1u);	/* counter block: read back with the counters (sg_stack_stats::norm_fma) */
+	const unsigned int flags = (__ballot(bad) ? 1u : 0u) | (__ballot(ibad) ? 2u : 0u);
+	if (flags && (threadIdx.x & 63) == 0) {
+		atomicOr((unsigned int *)(pairs + 4 * (size_t)npad), flags);
+		atomicOr(verdict, flags);	/* counter block: read back with the counters (sg_stack_stats::norm_fma) */
 	}
 	if (blockIdx.x == 0 && threadIdx.x == 0) {
 		pairs[2 * ((size_t)npad + f)] = A;
 		pairs[2 * ((size_t)npad + f) + 1] = B;
+		/* the integer pair (int4 2 npad + 1 + f): {kpos, kneg} in both u16 halves */
+		const uint32_t kp = (uint32_t)(K > 0 ? K : 0), kn = (uint32_t)(K < 0 ? -K : 0);
+		int *ip = (int *)(pairs + 4 * (size_t)npad + 2 + 2 * (size_t)f);
+		ip[0] = (int)(kp | kp << 16);
+		ip[1] = (int)(kn | kn << 16);
 	}
 }
 

@@ -1,4 +1,4 @@
-"""Single-rounding normalising load of the histogram kernels (round 6).
+"""Single-rounding / integer normalising loads of the histogram kernels (round 6).
 
 The reference normalises a sample x of frame f in two or three double roundings
 (src/stacking/stacking.c:1642-1651, round_to_WORD src/core/utils.c:68-74):
@@ -6,8 +6,10 @@ The reference normalises a sample x of frame f in two or three double roundings
     multiplicative  round_to_WORD(fl(x scale) mul)
 k_norm_fma_check (csrc/sg_stack_hist.hip) compares those, for every u16 x of every frame, with
 one fma(x, a, b) per sample and lets the histogram kernels load through the fma only when no x of
-any frame differs (sg_stack_stats.norm_fma = 1); otherwise the call keeps the reference's
-operations (norm_fma = 0).  Either way the image and the counters equal the oracle.
+any frame differs (sg_stack_stats.norm_fma = 1); additive normalisation with scale 1 (Siril's
+ADDITIVE) also tries clamp(x - K, 0, 65535) with an integer K per frame (two packed saturating u16
+ops per pixel pair, norm_fma = 2).  Otherwise the call keeps the reference's operations
+(norm_fma = 0).  Either way the image and the counters equal the oracle.
 
 The CPU test pins the premise of the fallback case: for the constructed coefficients the fma
 really differs from the reference's roundings at one sample value (exact rational arithmetic,
@@ -88,7 +90,8 @@ def test_fma_load_matches_oracle(gpu_ctx, method, rejection, normalize):
     assert rc == 0, gpu_ctx.error()
     st = gpu_ctx.stats()
     assert st.path == 1
-    assert st.norm_fma == 1, "the single-rounding load was not admitted"
+    want = 2 if normalize == sg.ADDITIVE else 1     # additive with scale 1: the integer offsets
+    assert st.norm_fma == want, (st.norm_fma, want)
     if method == sg.MEDIAN:
         rc, ref = orc.stack_median(frames, normalize=normalize, offset=off, mul=mul, scale=scale, max_thread=2)
         rej_ref = rej
@@ -136,3 +139,45 @@ def test_fma_load_refused_keeps_reference(gpu_ctx, rejection):
     diff = np.argwhere(out != ref)
     assert len(diff) == 0, f"{len(diff)} pixels differ, first {diff[:5].tolist()}"
     assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rejection", [sg.SIGMA, sg.WINSORIZED])
+def test_integer_load_refused_keeps_fma(gpu_ctx, rejection):
+    """ADDITIVE (scale 1) with one frame's offset 0.5 + 2^-40: fl(x - 2^-40) rounds back to x for the
+    large u16 values, which the integer form (K = 1) cannot reproduce, while the fma rounds the same
+    way; the check refuses the integer load, admits the fma (norm_fma = 1), and the stack equals the
+    oracle"""
+    N, H, W = 40, 24, 300
+    frames = orc.synth(N, 1, H, W, seed=621, maxshift=6)
+    sx, sy = orc.synth_shifts(N, seed=621, maxshift=6)
+    rng = np.random.default_rng(622)
+    off = rng.uniform(-60, 60, N)
+    off[0] = 0.0
+    off[5] = 0.5 + 2.0 ** -40
+    frames[5, 0, H // 2, 20:220] = 50000
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=rejection, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                              normalize=sg.ADDITIVE, offset=off, mul=np.ones(N), scale=np.ones(N),
+                              max_thread=2, max_number_of_rows=H)
+    rc, out, rej, _ = gpu_ctx.stack_host(desc, np.ascontiguousarray(frames))
+    assert rc == 0, gpu_ctx.error()
+    st = gpu_ctx.stats()
+    assert st.path == 1
+    assert st.norm_fma == 1, st.norm_fma
+    rc, ref, rej_ref = orc.stack_rejection(frames, rejection, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+                                           normalize=sg.ADDITIVE, offset=off, mul=np.ones(N), scale=np.ones(N),
+                                           max_thread=2)
+    assert rc == 0
+    diff = np.argwhere(out != ref)
+    assert len(diff) == 0, f"{len(diff)} pixels differ, first {diff[:5].tolist()}"
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+
+
+def test_integer_refusal_premise():
+    """the refusal case above: at x = 50000 the reference's fl(x - c) (c = offset - 0.5 = 2^-40) is
+    x, an integer, so round_to_WORD gives x, while x - ceil(c) = x - 1"""
+    c = 2.0 ** -40
+    x = 50000.0
+    assert (x - c) == x
+    y = x - (c + 0.5)
+    assert int(y + 0.5) == 50000
