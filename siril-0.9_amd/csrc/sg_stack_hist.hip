@@ -1257,8 +1257,14 @@ __device__ __forceinline__ void sgh_wpev(uint64_t *w, int k) {
 #define SGH_WPEV(k)
 #endif
 
+template <bool CAP = false>
 __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int cap, uint16_t *value, uint32_t *rlo_out,
 		uint32_t *rhi_out) {
+	/* CAP: the pixel's captured out-of-band samples (sgh_finish2, round 6) make a query at v in
+	 * [0, zmax) or [omin, 65535), or a median rank among the out-of-band samples, undecidable here;
+	 * the neighbour bounds of sgh_qx and the kept ends klo / khi stay bounds elsewhere */
+	auto zbad = [&](int v) { return CAP && ((v >= 0 && v < P.zmax) || (v >= P.omin && v < 65535)); };
+	auto rbad = [&](int g) { const int r = g - P.nz; return CAP && ((r < 0 && P.zmax > 0) || (r >= P.nb && P.omin < 65535)); };
 	int A = 0, B = 65535, n = N, r = 0, nrem;
 	SghM MA = {0, 0, 0}, MB = P.T;
 	uint32_t rlo = 0, rhi = 0;
@@ -1276,6 +1282,8 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 		double sigma = sgh_sd_rel(n, S, SS, &e0);
 		const int g1 = MA.c + (n - 1) / 2, g2 = MA.c + n / 2;
 		int km1, km2;	/* kept values at the median ranks: fixed for the whole pass */
+		if (rbad(g1) || rbad(g2))
+			return 1;
 		sgh_value_at2(P, g1, g2, km1, km2);
 		double median = (g1 == g2) ? (double)km1 : (double)(km1 + km2) / 2.0;
 		SGH_WP(1, 2);
@@ -1347,6 +1355,8 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 			while (pend != 0) {
 				SGH_WPEV(0);
 				const int side = (pend & 1) ? 0 : 1;
+				if (zbad(side ? b1 : a1))
+					return 1;
 				const SghX x = sgh_qx(P, side ? b1 : a1, side);
 #ifdef SGH_QX_TWICE	/* A/B probe build: every query body runs twice (its price in the kernel time) */
 				uint32_t z0;
@@ -1380,6 +1390,8 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 					} else {
 						if (!have)
 							SGH_WPEV(1);
+						if (!have && zbad(v))
+							return -1;
 						int k = have ? cq : sgh_cnt_le(P, v);
 						k = k < ciA0 ? ciA0 : (k > ciB0 ? ciB0 : k);
 						c += k - ciA0;
@@ -1390,11 +1402,17 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 				return c;
 			};
 			const int clo = w_le(a1, true, cL);
-			if (!sig_e0 && a2 != a1 && clo != w_le(a2, false, 0))
-				return 1;
+			if (!sig_e0 && a2 != a1) {
+				const int c2 = w_le(a2, false, 0);
+				if (c2 < 0 || clo != c2)
+					return 1;
+			}
 			const int chi = n - w_le(b1, true, cH);
-			if (!sig_e0 && b2 != b1 && chi != n - w_le(b2, false, 0))
-				return 1;
+			if (!sig_e0 && b2 != b1) {
+				const int c2 = w_le(b2, false, 0);
+				if (c2 < 0 || chi != n - c2)
+					return 1;
+			}
 			if (clo + chi > n)
 				return 1;
 			if (clo > 0) {
@@ -1485,18 +1503,20 @@ __device__ int sgh_winsorized(const SghPix &P, int N, double sl, double sh, int 
 			bt = B;
 		/* the clip counts, moments and the next pass's kept ends (exact doubles: relative to lo,
 		 * SS <= 65535^3 < 2^53) */
+		if (zbad(a - 1) || zbad(bt))
+			return 1;
 		const SghX xa = sgh_qx(P, a - 1, 0), xb = sgh_qx(P, bt, 1);
 		const int cnt_a = xa.c, cnt_bt = xb.c;
 		if (!sig_e0) {
 			int amb1 = sgh_floor_clamp(blo + tol);
 			if (amb1 > B)
 				amb1 = B;
-			if (a <= amb1 && sgh_cnt_le(P, amb1) - cnt_a > 0)
+			if (a <= amb1 && (zbad(amb1) || sgh_cnt_le(P, amb1) - cnt_a > 0))
 				return 1;
 			int amb0 = sgh_ceil_clamp(bhi - tol);
 			if (amb0 < A)
 				amb0 = A;
-			if (amb0 <= bt && cnt_bt - sgh_cnt_le(P, amb0 - 1) > 0)
+			if (amb0 <= bt && (zbad(amb0 - 1) || cnt_bt - sgh_cnt_le(P, amb0 - 1) > 0))
 				return 1;
 		}
 		const int L = cnt_a - MA.c, H = MB.c - cnt_bt;
@@ -1839,7 +1859,7 @@ __device__ __forceinline__ void sgh_finish2(const SgStackParams &p, LT &L, int c
 		 * samples (counts and moments below or above the band) instead of sending it to the compact list;
 		 * a query or median rank among them is undecidable here (zbad) and redoes the pixel */
 		int kx = 0;
-		if constexpr (CAP && REJ == 2) {
+		if constexpr (CAP && (REJ == 2 || REJ == 4)) {
 			const int k = oob - P.nz - P.ns;
 			if (P.nb + oob == N && zc == 0 && k > 0 && k <= SGH_OVK && (int)L.ovn[col] == k)
 				kx = k;
@@ -1871,7 +1891,7 @@ __device__ __forceinline__ void sgh_finish2(const SgStackParams &p, LT &L, int c
 			P.T.c = N;
 			P.T.s = (long long)s32 + P.Z.s + ds * P.ns;
 			P.T.ss = (unsigned long long)ss32 + P.Z.ss + (unsigned long long)(ds * ds) * (unsigned long long)P.ns;
-			if constexpr (CAP && REJ == 2) {
+			if constexpr (CAP && (REJ == 2 || REJ == 4)) {
 				if (kx) {
 #pragma unroll
 					for (int k = 0; k < SGH_OVK; k++) {
@@ -1901,10 +1921,13 @@ __device__ __forceinline__ void sgh_finish2(const SgStackParams &p, LT &L, int c
 			} else if (REJ == 3) {
 				cls = sgh_sigmedian(P, N, p.sig0, p.sig1, &value, &rlo, &rhi);
 			} else if (REJ == 4 || !PAIR) {
-				/* zeros: nz copies of -lo, exact as doubles (dz = -lo, dz^2 nz < 2^53) */
-				P.zs = -(double)lo * (double)P.nz;
-				P.zss = (double)lo * (double)lo * (double)P.nz;
-				cls = sgh_winsorized(P, N, p.sig0, p.sig1, p.wins_cap, &value, &rlo, &rhi);
+				/* zeros (and captured samples below the band): their moments, exact as doubles
+				 * (dz = -lo, dz^2 nz < 2^53) */
+				P.zs = (double)P.Z.s;
+				P.zss = (double)P.Z.ss;
+				cls = sgh_winsorized<CAP>(P, N, p.sig0, p.sig1, p.wins_cap, &value, &rlo, &rhi);
+				if constexpr (CAP && REJ == 4)
+					cmp = cls != SG_CLS_OK && kx && p.cmp_cols;	/* every sample known: the sorted column */
 #ifdef SGH_WINS_ITERS
 				value = (uint16_t)rlo;	/* A/B probe build: the image holds the inner iteration counts */
 				cls = SG_CLS_OK;

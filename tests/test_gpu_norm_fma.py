@@ -181,3 +181,44 @@ def test_integer_refusal_premise():
     assert (x - c) == x
     y = x - (c + 0.5)
     assert int(y + 0.5) == 50000
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rejection", [sg.SIGMA, sg.WINSORIZED])
+@pytest.mark.parametrize("normalize", [sg.ADDITIVE_SCALING, sg.MULTIPLICATIVE_SCALING])
+def test_captured_samples_near_the_band(gpu_ctx, rejection, normalize):
+    """normalised stacks whose columns hold 1..4 out-of-band samples just outside the 256-bin band
+    (60..260 ADU beyond it on either side, where the clipping thresholds of the first passes land)
+    and some 0 / 65535: the SIGMA / WINSORIZED finishes take the captured values as known samples,
+    or find a query among them undecidable and compact the column; every pixel and the counters
+    equal the oracle"""
+    N, H, W = 96, 40, 256
+    rng = np.random.default_rng(700 + 10 * rejection + normalize)
+    frames = np.clip(np.rint(2000 + rng.normal(0, 30, (N, 1, H, W))), 0, 65535).astype(np.uint16)
+    for y in range(H):
+        for x in range(W):
+            k = (x + 3 * y) % 5          # 0..4 outliers in this column
+            fr = rng.choice(N, size=k, replace=False)
+            side = rng.choice([-1, 1], size=k)
+            frames[fr, 0, y, x] = np.clip(2000 + side * rng.integers(190, 390, size=k), 1, 65534)
+    frames[rng.integers(0, N, 200), 0, rng.integers(0, H, 200), rng.integers(0, W, 200)] = 65535
+    frames[rng.integers(0, N, 60), 0, rng.integers(0, H, 60), rng.integers(0, W, 60)] = 0
+    loc = 2000 + rng.random(N) * 20
+    loc[0] = 2000.0
+    scl = 30 + rng.random(N) * 0.6
+    off, mul, scale = orc.compute_normalization(normalize, loc, scl, ref_image=0)
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=rejection, sig=(4.0, 3.0), normalize=normalize,
+                              offset=off, mul=mul, scale=scale, max_thread=2, max_number_of_rows=H)
+    rc, out, rej, _ = gpu_ctx.stack_host(desc, np.ascontiguousarray(frames))
+    assert rc == 0, gpu_ctx.error()
+    st = gpu_ctx.stats()
+    assert st.path == 1
+    rc, ref, rej_ref = orc.stack_rejection(frames, rejection, sig=(4.0, 3.0), normalize=normalize, offset=off,
+                                           mul=mul, scale=scale, max_thread=2)
+    assert rc == 0
+    diff = np.argwhere(out != ref)
+    assert len(diff) == 0, f"{len(diff)} pixels differ, first {diff[:5].tolist()}"
+    assert np.array_equal(rej, rej_ref), (rej, rej_ref)
+    # most columns hold captured samples; the finish decided most of them
+    assert st.compact_pixels < 0.5 * H * W, st.compact_pixels
+    print(f"compact {st.compact_pixels} redo {st.chain_pixels} of {H * W}")
