@@ -1826,7 +1826,7 @@ __device__ __forceinline__ void sgh_finish2(const SgStackParams &p, LT &L, int c
 	 * such frame from an unrelated out-of-band sample */
 	int zc = 0, zmax = 0;
 	long long zs = 0, zss = 0;
-	if (ZT && REJ == 2 && zrow && p.ztab) {
+	if (ZT && (REJ == 2 || REJ == 4) && zrow && p.ztab) {
 		const int t = R < p.ztab_k1 ? R : (R >= p.H - p.ztab_k2 ? p.ztab_k1 + (R - (p.H - p.ztab_k2)) : -1);
 		if (t >= 0) {
 			const int *e = p.ztab + 8 * t;
@@ -2547,13 +2547,13 @@ __device__ __forceinline__ void sgh_tile(const SgStackParams &p, const SghRo &ro
 			if (wave >= 2)
 				return;
 			const int col = L.perm[64 * wave + lane];
-			sgh_finish2<REJ, false, NI, false, NORM != 0>(p, L, col, 0, col_lo(col), R, c, col_x(col), redo_count,
-					redo_list);
+			sgh_finish2<REJ, false, NI, NORM == 1 || NORM == 3, NORM != 0>(p, L, col, 0, col_lo(col), R, c, col_x(col),
+					redo_count, redo_list, interior);
 			return;
 		}
 		for (int col = 64 * wave + lane; col < COLS; col += 64 * WAVES)
-			sgh_finish2<REJ, false, NI, false, NORM != 0>(p, L, col, 0, col_lo(col), R, c, col_x(col), redo_count,
-					redo_list);
+			sgh_finish2<REJ, false, NI, NORM == 1 || NORM == 3, NORM != 0>(p, L, col, 0, col_lo(col), R, c, col_x(col),
+					redo_count, redo_list, interior);
 		return;
 	}
 	if (REJ == 3) {	/* SIGMEDIAN: one lane per column (waves 0 and 1) */

@@ -546,14 +546,15 @@ def test_early_break_replay(gpu_ctx, rejection, sig):
     assert np.array_equal(rej, rej_ref), (rej, rej_ref)
 
 
+@pytest.mark.parametrize("rejection", [sg.SIGMA, sg.WINSORIZED])
 @pytest.mark.parametrize("dark", [False, True])
 @pytest.mark.parametrize("normalize", [sg.ADDITIVE, sg.ADDITIVE_SCALING])
-def test_hist_path_border_normalised_zeros(gpu_ctx, normalize, dark):
-    """SIGMA with additive normalisation: rows whose shifted source row leaves a frame hold
-    that frame's normalised zero round_to_WORD(-offset) (zero fill :1550-1577, then
-    :1635-1652); the histogram path takes them from the host's border-row table instead of
-    the redo list.  dark: background near the normalised zeros, so they fall inside the band
-    (the table must step aside and the rows go to the redo list)"""
+def test_hist_path_border_normalised_zeros(gpu_ctx, normalize, dark, rejection):
+    """SIGMA / WINSORIZED (round 6) with additive normalisation: rows whose shifted source row
+    leaves a frame hold that frame's normalised zero round_to_WORD(-offset) (zero fill
+    :1550-1577, then :1635-1652); the histogram path takes them from the host's border-row table
+    instead of the redo list.  dark: background near the normalised zeros, so they fall inside
+    the band (the table must step aside and the rows go to the redo list)"""
     N, H, W = 64, 48, 1024
     rng = np.random.default_rng(5 + normalize + 7 * dark)
     loc = (120.0 if dark else 1000.0) + rng.random(N) * 90
@@ -565,17 +566,17 @@ def test_hist_path_border_normalised_zeros(gpu_ctx, normalize, dark):
     frames[rng.random(frames.shape) < 5e-4] = 65535
     sx, sy = orc.synth_shifts(N, seed=77 + normalize, maxshift=10)
     off, mul, scale = orc.compute_normalization(normalize, loc, scl, ref_image=0)
-    desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=sg.SIGMA, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+    desc, keep = sg.make_desc(sg.MEAN, N, W, H, 1, rejection=rejection, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
                               normalize=normalize, offset=off, mul=mul, scale=scale, max_thread=3,
                               max_number_of_rows=H)
     rc, out, rej, _ = gpu_ctx.stack_host(desc, np.ascontiguousarray(frames))
     assert rc == 0, gpu_ctx.error()
     st = gpu_ctx.stats()
     assert st.path == 1
-    rc, ref, rej_ref = orc.stack_rejection(frames, sg.SIGMA, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
+    rc, ref, rej_ref = orc.stack_rejection(frames, rejection, sig=(4.0, 3.0), shiftx=sx, shifty=sy,
                                            normalize=normalize, offset=off, mul=mul, scale=scale, max_thread=3)
     assert rc == 0
-    assert_same(out, ref, f"border zeros norm={normalize} dark={dark}")
+    assert_same(out, ref, f"border zeros norm={normalize} dark={dark} rej={rejection}")
     assert np.array_equal(rej, rej_ref), (rej, rej_ref)
     if not dark:
         border = int(np.max(np.abs(sy)))
